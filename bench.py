@@ -1,0 +1,182 @@
+"""Benchmark: Gibbs sweeps/sec of the Neal-8 sweep (BASELINE.json metric) on MI355X.
+
+Workload: N = 1e6 items, D = 8, 64 components (sd 0.8, means 6 + U[-20,20]^8),
+M = 3, fp64, reference hyper-parameters (alpha 1, mu0 = 6, kappa 1/500, nu 4, Lambda 0.01 I),
+warm state (labels = ground truth, cluster parameters = the generating ones), frozen cluster
+parameters (the reference's effective behaviour).  One step = one full sweep:
+N point updates (np8_assign) + cluster bookkeeping (np8_finalize) + the max-likelihood check every
+5th sweep, exactly as np8_sweep runs it.  Inputs are resident in HBM before the timed region.
+
+Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): the N items are
+sharded contiguously over ranks (strong scaling, total N fixed as in config C4); one RCCL
+all-gather of the exchange record per sweep.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector (= FP64 matrix) peak, vendor spec
+HBM_PEAK_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--n", type=int, default=1_000_000)
+    ap.add_argument("--d", type=int, default=8)
+    ap.add_argument("--k", type=int, default=64)
+    ap.add_argument("--seed", type=int, default=20261015)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget (0 = skip)")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        world = max(world, 1)
+
+    import torch
+
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("gloo")  # host barrier + timing max; the sweep itself uses RCCL
+    torch.cuda.set_device(local_rank)
+
+    from noparama_amd import NealAlgorithm8, comm_unique_id, datasets
+
+    N, D, K = args.n, args.d, args.k
+    s, r = (0.3, 15.0) if D == 2 else (0.8, 20.0)
+    X, z, mu, sig = datasets.mixture(N, D, K, s, r, seed=args.seed)
+    lo = (N * rank) // world
+    hi = (N * (rank + 1)) // world
+
+    smp = NealAlgorithm8(D, seed=args.seed, device=local_rank)
+    if world > 1:
+        uid = [comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        smp.comm_init(uid[0], rank, world)
+    smp.set_data(X[lo:hi], offset=lo, n_global=N)
+    smp.set_state(z[lo:hi], mu, sig)
+
+    smp.sweep(args.warmup)  # includes np8_sync
+    torch.cuda.synchronize()
+    smp.set_timing(True)
+    st0 = smp.stats()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    smp.sweep(args.steps, sync=False)
+    smp.sync()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    t1 = time.perf_counter()
+    dt = t1 - t0
+    if dist:
+        tt = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    st1 = smp.stats()
+    Kfinal = st1["K"]
+
+    # roofline of the dominant kernel (np8_assign): algorithmic flops per launch / avg launch time
+    n_launch = args.steps
+    ms_assign = (st1["ms_assign"] - st0["ms_assign"]) / max(n_launch, 1)
+    Kc = Kfinal + smp.M
+    n_items = hi - lo
+    flops = float(n_items) * Kc * (D * D + 2 * D + 4)
+    achieved = flops / (ms_assign * 1e-3) / 1e12 if ms_assign > 0 else 0.0
+    traffic = None
+    if os.path.exists(args.traffic_json):
+        try:
+            traffic = json.load(open(args.traffic_json)).get("assign_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    if rank == 0:
+        cpu = None
+        if world == 1 and args.cpu_seconds > 0:
+            cpu = cpu_baseline(X, z, mu, sig, D, args.seed, args.cpu_seconds)
+        out = {
+            "metric": "Gibbs sweeps/sec (Neal-8, N=1e6 D=8)",
+            "value": args.steps / dt,
+            "unit": "sweeps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": dt / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic",
+            "config": {
+                "workload": f"C3: N={N} D={D} K~{K} M=3 mixture, warm state, frozen cluster parameters",
+                "N": N, "D": D, "K_final": Kfinal, "parallelism": f"data-sharded x{world}",
+            },
+            "roofline": {
+                "bound": "mfma",
+                "note": "fp64 compute roof (MI355X fp64 vector = fp64 matrix peak); kernel np8_assign",
+                "achieved": achieved,
+                "peak": FP64_PEAK_TFLOPS,
+                "unit": "TFLOP/s",
+                "frac": achieved / FP64_PEAK_TFLOPS,
+                "traffic": traffic,
+                "assign_ms_per_launch": ms_assign,
+                "algorithmic_flops_per_launch": flops,
+                "hbm_frac_algorithmic": (n_items * (8 * D + 8)) / (ms_assign * 1e-3) / 1e9 / HBM_PEAK_GBS
+                if ms_assign > 0 else None,
+            },
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out))
+    if dist:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(X, z, mu, sig, D, seed, budget_s):
+    """The oracle's sequential sweep (chunk = 1: the reference's algorithm, single thread) on the same
+    workload and state, timed on a bounded prefix of one sweep, extrapolated to sweeps/s."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O  # test infrastructure: timed as the CPU baseline only
+
+    c = O.Chain(D, seed=seed, chunk=1, kcap=2048)
+    c.set_data(X)
+    c.set_state(z, mu, sig)
+    done, t0 = 0, time.perf_counter()
+    batch = 10000
+    while time.perf_counter() - t0 < budget_s and done < X.shape[0]:
+        c.update_points(np.arange(done, min(done + batch, X.shape[0]), dtype=np.int64))
+        done = min(done + batch, X.shape[0])
+    el = time.perf_counter() - t0
+    rate = done / el
+    return {
+        "value": rate / X.shape[0],
+        "unit": "sweeps/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": f"{done} sequential point-updates (chunk=1) of one N={X.shape[0]} sweep in {el:.1f}s "
+                  f"on 1 core, extrapolated: {rate:.0f} point-updates/s",
+    }
+
+
+if __name__ == "__main__":
+    main()

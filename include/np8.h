@@ -1,0 +1,136 @@
+/*
+ * np8.h -- C ABI of the MI355X (gfx950) Neal Algorithm 8 Gibbs sweep.
+ *
+ * This is the drop-in boundary for mrquincle/noparama's sampler plug-in
+ *   class UpdateClusterPopulation { virtual void update(membertrix&, const data_ids_t&) = 0;
+ *                                   virtual void printStatistics() = 0; }
+ *   (reference include/np_update_cluster_population.h:13-44; Neal-8 implementation
+ *    src/np_neal_algorithm8.cpp:17-176, constructed in src/np_main.cpp:433-438).
+ * A C++ caller wraps it as `NealAlgorithm8Hip : UpdateClusterPopulation` (host/np_neal_algorithm8_hip.h);
+ * a ctypes caller binds it directly (noparama_amd/np8.py).  Plain pointers and sizes only: the
+ * library owns its device memory and copies host buffers in and out.
+ *
+ * Every entry point returns 0 on success or a negative np8_status; np8_last_error() has the text.
+ * One host thread per context; contexts are independent (the reference is single-threaded and
+ * non-reentrant: static RNGs in include/statistics/normal.h:61, multivariatenormal.cpp:41).
+ */
+#ifndef NP8_H
+#define NP8_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct np8_ctx np8_ctx;
+
+typedef enum {
+    NP8_OK = 0,
+    NP8_ERR_ARG = -1,      /* bad argument / unsupported configuration */
+    NP8_ERR_SIGMA = -2,    /* a covariance with det <= 0 (reference would produce NaN weights) */
+    NP8_ERR_RANGE = -3,    /* label or point index out of range */
+    NP8_ERR_CAPACITY = -4, /* new-cluster requests exceeded free slots or NP8_REQ_MAX in a chunk */
+    NP8_ERR_STATE = -5,    /* call order (no data / no state / no max-likelihood snapshot yet) */
+    NP8_ERR_HIP = -6,      /* HIP runtime error (message has the HIP error string) */
+    NP8_ERR_COMM = -7      /* RCCL error */
+} np8_status;
+
+#define NP8_REQ_MAX 4096 /* new-cluster requests one synchronous step can accept */
+
+typedef struct {
+    int32_t D;            /* dimension of the data items (data_t, include/np_data.h:9) */
+    int32_t M;            /* auxiliary clusters per point; reference _M = 3 (np_neal_algorithm8.cpp:33) */
+    double alpha;         /* DP concentration; reference alpha = 1 (np_main.cpp:164) */
+    const double *mu0;    /* [D] G0 mean; reference (6,6) (np_main.cpp:368) */
+    double kappa;         /* reference 1/500 (np_main.cpp:369) */
+    double nu;            /* reference 4 (np_main.cpp:370); sd of the scale draw (invwishart.h:30-31) */
+    const double *Lambda; /* [D*D] row-major, SPD; reference 0.01 I (np_main.cpp:371) */
+    uint64_t seed;        /* Philox key: every draw is a pure function of (seed, point, epoch) */
+    int32_t kcap;         /* cluster slot capacity (0 -> 2048) */
+    int64_t chunk;        /* points per synchronous step: 0 = the whole sweep (data-parallel);
+                             1 = the reference's exact sequential sweep (np_mcmc.cpp:146-164) */
+    int32_t device;       /* HIP device ordinal, -1 = current */
+} np8_config;
+
+typedef struct {
+    int32_t K;                  /* live clusters */
+    uint32_t epoch;             /* sweeps completed */
+    int64_t new_clusters;       /* cumulative "new cluster" events (np_statistics.h step[0].accept) */
+    int64_t existing_picks;     /* cumulative "existing cluster" events (step[0].reject) */
+    int64_t rejected_requests;  /* requests dropped by NP8_ERR_CAPACITY */
+    double best_loglik;         /* max over checks of sum_i log p(x_i | theta_z_i) (np_mcmc.cpp:187-203) */
+    double last_loglik;
+    double ms_assign, ms_finalize, ms_loglik; /* accumulated device time (when timing is enabled) */
+} np8_stats_t;
+
+/* Create / destroy.  Replaces NealAlgorithm8::NealAlgorithm8 (np_neal_algorithm8.cpp:17-34). */
+int np8_create(np8_ctx **out, const np8_config *cfg);
+int np8_destroy(np8_ctx *ctx);
+const char *np8_last_error(const np8_ctx *ctx);
+
+/* Data items, row-major [n][D] (membertrix::addData, membertrix.cpp:120-138).  For a data-parallel
+ * run over several ranks, pass this rank's contiguous shard [offset, offset+n) of n_global items. */
+int np8_set_data(np8_ctx *ctx, const double *X, int64_t n, int32_t D, int64_t offset, int64_t n_global);
+
+/* Explicit state: labels z[n] in [0,K) and per-cluster mu [K*D], Sigma [K*D*D] (row-major).
+ * Sigma is used as the reference uses it: inverse and determinant of the matrix as given
+ * (multivariatenormal.cpp:87,90), so a non-symmetric Sigma is accepted (test_mvn_likelihood.cpp:20). */
+int np8_set_state(np8_ctx *ctx, const int32_t *z, int32_t K, const double *mu, const double *Sigma);
+
+/* Reference initialisation: K_init G0 draws, uniform random assignment, cleanup of empty clusters
+ * (np_mcmc.cpp:49-92, np_init_clusters.cpp:24-40). */
+int np8_init_random(np8_ctx *ctx, int32_t K_init);
+
+/* n full sweeps (np_mcmc.cpp:109-175 with the population update of np_neal_algorithm8.cpp:49-167),
+ * including the max-likelihood check every 5th sweep (np_mcmc.cpp:172-174).  Asynchronous on the
+ * context's stream; errors raised on the device are reported by the next np8_sync(). */
+int np8_sweep(np8_ctx *ctx, int32_t n_sweeps);
+
+/* The reference's per-call granularity: sequential single-point updates of the listed items, in
+ * order, at the current epoch (NealAlgorithm8::update with data_ids.size()==1).  Call
+ * np8_end_sweep() after the last point of a sweep. */
+int np8_update_points(np8_ctx *ctx, const int64_t *ids, int64_t n);
+int np8_end_sweep(np8_ctx *ctx);
+
+/* Waits for queued work; returns the first device-side error since the last sync. */
+int np8_sync(np8_ctx *ctx);
+
+/* State out: which = 0 current, 1 max-likelihood snapshot (MCMC::getMaxLikelihoodMatrix,
+ * np_mcmc.cpp:183-185).  Labels are dense 0..K-1 in ascending slot order.  Any pointer may be NULL;
+ * mu/Sigma/counts need room for kcap clusters. */
+int np8_get_state(np8_ctx *ctx, int32_t which, int32_t *z, int32_t *K, double *mu, double *Sigma, int64_t *counts);
+
+/* Parity/debug: log-likelihood of the listed items (local indices) against every live cluster
+ * (ascending slot order) and then against the M auxiliary draws of the current epoch;
+ * out is n x (K+M) with K = current live count.  Same arithmetic as the sweep kernel. */
+int np8_loglik_matrix(np8_ctx *ctx, const int64_t *idx, int64_t n, double *out);
+
+/* Sum over items of log p(x_i | theta_{z_i}) for the current state (MCMC::considerMaxLikelihood). */
+int np8_total_loglik(np8_ctx *ctx, double *out);
+
+int np8_stats(np8_ctx *ctx, np8_stats_t *out);
+/* Device-event timing of the kernels (adds events around each launch). */
+int np8_set_timing(np8_ctx *ctx, int32_t enable);
+/* Launch on this stream instead of the context's own (hipStream_t as void*). */
+int np8_set_stream(np8_ctx *ctx, void *stream);
+
+/* Multi-GPU: one context per rank.  Rank 0 makes an id, the caller broadcasts the 128 bytes, every
+ * rank calls np8_comm_init.  Each sweep then exchanges one fixed-size record per rank (count deltas
+ * and new-cluster requests) with one ncclAllGather over xGMI; cluster tables stay replicated. */
+int np8_comm_unique_id(uint8_t out[128]);
+int np8_comm_init(np8_ctx *ctx, const uint8_t id[128], int32_t rank, int32_t world);
+
+/* Host-exchange variant of the same protocol (for callers that move the record themselves, e.g.
+ * over MPI or gloo): np8_comm_init(ctx, NULL, rank, world), then per sweep np8_step_local (writes
+ * this rank's record), the caller all-gathers np8_record_bytes() bytes from every rank in rank
+ * order, np8_step_merge(gathered, world), np8_end_sweep.  The max-likelihood check then uses this
+ * rank's partial sum only. */
+int64_t np8_record_bytes(np8_ctx *ctx);
+int np8_step_local(np8_ctx *ctx, void *record_out);
+int np8_step_merge(np8_ctx *ctx, const void *records, int32_t world);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

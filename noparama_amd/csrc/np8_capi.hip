@@ -1,0 +1,917 @@
+// np8_capi.hip -- the C ABI (include/np8.h): context, device memory, sweep orchestration, RCCL.
+//
+// Replaces, for the Neal-8 path, the reference's per-point call chain
+//   MCMC::run (src/np_mcmc.cpp:109-175) -> NealAlgorithm8::update (src/np_neal_algorithm8.cpp:49-167)
+//   -> membertrix retract/assign/addCluster (src/membertrix.cpp:87-244)
+// with sweep-granular launches: per synchronous step one np8_assign grid and one np8_finalize
+// workgroup (plus one ncclAllGather of the exchange record when sharded over ranks).
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/np8.h"
+#include "np8_device.h"
+#include "np8_kernels.h"
+
+using namespace np8;
+
+namespace {
+
+constexpr double kLog2PiC = 1.8378770664093454835606594728112;
+
+struct Timer {
+    hipEvent_t a, b;
+    int phase;
+};
+
+}  // namespace
+
+struct np8_ctx {
+    // configuration
+    int D = 0, M = 0, DP = 0, CS = 0, kcap = 0, rec_cap = 0;
+    double alpha = 1.0, kappa = 1.0, nu = 1.0;
+    uint64_t seed = 0;
+    int64_t chunk = 0;
+    int device = 0;
+    std::vector<double> mu0, Lambda;
+    // base-measure precomputes (DESIGN.md "G0")
+    std::vector<double> Lc, LT, UinvT, Gp, LTL;  // D*D row-major
+    double caux = 0, rsk = 0, logam = 0;
+    // data / state
+    int64_t n_loc = 0, offset = 0, n_glob = 0;
+    bool have_data = false, have_state = false;
+    uint32_t epoch = 0;
+    int32_t checks = 0;
+    // device buffers
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    double *X = nullptr;
+    int32_t *z = nullptr, *z_best = nullptr;
+    double *slot_mu = nullptr, *slot_P = nullptr, *slot_c = nullptr, *slot_sigma = nullptr;
+    int32_t *cnt = nullptr, *cnt_best = nullptr;
+    double *mu_best = nullptr, *sigma_best = nullptr;
+    double *cand = nullptr;
+    Ctl *ctl = nullptr;
+    double *hyp = nullptr, *d_mu0 = nullptr, *d_LT = nullptr, *d_Gp = nullptr, *d_LTL = nullptr;
+    unsigned char *rec = nullptr, *gath = nullptr;
+    int64_t rec_bytes = 0;
+    int64_t *order = nullptr;
+    int64_t order_cap = 0;
+    double *partial = nullptr;
+    int64_t partial_cap = 0;
+    // multi-GPU
+    ncclComm_t comm = nullptr;
+    int rank = 0, world = 1;
+    // timing
+    bool timing = false;
+    std::vector<Timer> timers;
+    double ms[3] = {0, 0, 0};
+    std::string err;
+};
+
+namespace {
+
+int fail(np8_ctx *c, int code, const std::string &msg) {
+    if (c) c->err = msg;
+    return code;
+}
+
+#define HIPC(ctx, expr)                                                                                   \
+    do {                                                                                                 \
+        hipError_t e_ = (expr);                                                                          \
+        if (e_ != hipSuccess)                                                                            \
+            return fail(ctx, NP8_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));           \
+    } while (0)
+
+#define NCCLC(ctx, expr)                                                                                  \
+    do {                                                                                                 \
+        ncclResult_t r_ = (expr);                                                                        \
+        if (r_ != ncclSuccess) return fail(ctx, NP8_ERR_COMM, std::string(#expr) + ": " + ncclGetErrorString(r_)); \
+    } while (0)
+
+int packed_index(int D, int a, int b) { return a * D - (a * (a - 1)) / 2 + (b - a); }
+
+// LU with partial pivoting (what Eigen's MatrixXd::inverse()/determinant() use,
+// multivariatenormal.cpp:87,90).  Row-major.  Returns false when singular.
+bool lu_inverse_det(const double *A, int D, double *inv, double *det) {
+    std::vector<double> LU(A, A + (size_t)D * D);
+    std::vector<int> perm(D);
+    int sign = 1;
+    for (int i = 0; i < D; ++i) perm[i] = i;
+    for (int k = 0; k < D; ++k) {
+        int p = k;
+        double best = std::fabs(LU[k * D + k]);
+        for (int i = k + 1; i < D; ++i)
+            if (std::fabs(LU[i * D + k]) > best) {
+                best = std::fabs(LU[i * D + k]);
+                p = i;
+            }
+        if (best == 0.0) return false;
+        if (p != k) {
+            for (int j = 0; j < D; ++j) std::swap(LU[k * D + j], LU[p * D + j]);
+            std::swap(perm[k], perm[p]);
+            sign = -sign;
+        }
+        for (int i = k + 1; i < D; ++i) {
+            const double f = LU[i * D + k] / LU[k * D + k];
+            LU[i * D + k] = f;
+            for (int j = k + 1; j < D; ++j) LU[i * D + j] = LU[i * D + j] - f * LU[k * D + j];
+        }
+    }
+    double d = (double)sign;
+    for (int k = 0; k < D; ++k) d *= LU[k * D + k];
+    *det = d;
+    std::vector<double> y(D);
+    for (int col = 0; col < D; ++col) {
+        for (int i = 0; i < D; ++i) {
+            double s = (perm[i] == col) ? 1.0 : 0.0;
+            for (int j = 0; j < i; ++j) s -= LU[i * D + j] * y[j];
+            y[i] = s;
+        }
+        for (int i = D - 1; i >= 0; --i) {
+            double s = y[i];
+            for (int j = i + 1; j < D; ++j) s -= LU[i * D + j] * y[j];
+            y[i] = s / LU[i * D + i];
+        }
+        for (int i = 0; i < D; ++i) inv[i * D + col] = y[i];
+    }
+    return true;
+}
+
+// Base-measure precomputes: L = chol(Lambda) (invwishart.h:40), (L^T)^{-1}, (L^T L)^{-1}, L^T L.
+bool prepare_base(np8_ctx *c) {
+    const int D = c->D;
+    c->Lc.assign((size_t)D * D, 0.0);
+    std::vector<double> &L = c->Lc;
+    for (int j = 0; j < D; ++j) {
+        double s = c->Lambda[j * D + j];
+        for (int k = 0; k < j; ++k) s -= L[j * D + k] * L[j * D + k];
+        if (!(s > 0.0)) return false;
+        L[j * D + j] = std::sqrt(s);
+        for (int i = j + 1; i < D; ++i) {
+            double v = c->Lambda[i * D + j];
+            for (int k = 0; k < j; ++k) v -= L[i * D + k] * L[j * D + k];
+            L[i * D + j] = v / L[j * D + j];
+        }
+    }
+    c->LT.assign((size_t)D * D, 0.0);
+    for (int a = 0; a < D; ++a)
+        for (int b = 0; b < D; ++b) c->LT[a * D + b] = L[b * D + a];
+    c->UinvT.assign((size_t)D * D, 0.0);
+    for (int col = 0; col < D; ++col)
+        for (int i = col; i >= 0; --i) {
+            double s = (i == col) ? 1.0 : 0.0;
+            for (int j = i + 1; j <= col; ++j) s -= c->LT[i * D + j] * c->UinvT[j * D + col];
+            c->UinvT[i * D + col] = s / c->LT[i * D + i];
+        }
+    c->Gp.assign((size_t)D * D, 0.0);
+    c->LTL.assign((size_t)D * D, 0.0);
+    for (int a = 0; a < D; ++a)
+        for (int b = 0; b < D; ++b) {
+            double s = 0.0, g = 0.0;
+            for (int k = 0; k < D; ++k) {
+                s += L[k * D + a] * L[k * D + b];
+                g += c->UinvT[a * D + k] * c->UinvT[b * D + k];
+            }
+            c->LTL[a * D + b] = s;
+            c->Gp[a * D + b] = (a == b) ? g : 2.0 * g;
+        }
+    double sumlog = 0.0;
+    for (int a = 0; a < D; ++a) sumlog += std::log(L[a * D + a]);
+    c->caux = -0.5 * (double)D * kLog2PiC - sumlog;
+    c->rsk = 1.0 / std::sqrt(c->kappa);
+    c->logam = std::log(c->alpha / (double)c->M);
+    return true;
+}
+
+// Host copy of a slot's parameters.
+struct SlotHost {
+    std::vector<double> mu, P, sigma;
+    double c = 0.0;
+};
+
+// G0 draw from (scale normal g0, xi): v = D + nu g0, mu = mu0 + (|v|/sqrt(kappa)) L^T xi.
+void slot_from_normals(const np8_ctx *c, double g0, const double *xi, SlotHost &o) {
+    const int D = c->D;
+    const double v = std::fma(c->nu, g0, (double)D);
+    const double s = std::fabs(v) * c->rsk;
+    o.mu.resize(D);
+    for (int a = 0; a < D; ++a) {
+        double t = c->LT[a * D + a] * xi[a];
+        for (int b = a + 1; b < D; ++b) t = std::fma(c->LT[a * D + b], xi[b], t);
+        o.mu[a] = std::fma(s, t, c->mu0[a]);
+    }
+    const double v2 = v * v;
+    o.P.resize(c->DP);
+    for (int a = 0; a < D; ++a)
+        for (int b = a; b < D; ++b) o.P[packed_index(D, a, b)] = c->Gp[a * D + b] / v2;
+    o.c = std::fma(-(double)D, std::log(std::fabs(v)), c->caux);
+    o.sigma.resize((size_t)D * D);
+    for (int k = 0; k < D * D; ++k) o.sigma[k] = v2 * c->LTL[k];
+}
+
+bool slot_from_sigma(const np8_ctx *c, const double *mu, const double *Sigma, SlotHost &o) {
+    const int D = c->D;
+    std::vector<double> inv((size_t)D * D);
+    double det = 0.0;
+    if (!lu_inverse_det(Sigma, D, inv.data(), &det) || !(det > 0.0)) return false;
+    o.mu.assign(mu, mu + D);
+    o.sigma.assign(Sigma, Sigma + (size_t)D * D);
+    o.P.resize(c->DP);
+    for (int a = 0; a < D; ++a)
+        for (int b = a; b < D; ++b)
+            o.P[packed_index(D, a, b)] = (a == b) ? inv[a * D + a] : inv[a * D + b] + inv[b * D + a];
+    o.c = -0.5 * ((double)D * kLog2PiC + std::log(det));
+    return true;
+}
+
+void free_device(np8_ctx *c) {
+    void *ptrs[] = {c->X,      c->z,       c->z_best, c->slot_mu, c->slot_P,  c->slot_c,  c->slot_sigma,
+                    c->cnt,    c->cnt_best, c->mu_best, c->sigma_best, c->cand, c->ctl,    c->hyp,
+                    c->d_mu0,  c->d_LT,    c->d_Gp,   c->d_LTL,   c->rec,     c->gath,    c->order,
+                    c->partial};
+    for (void *p : ptrs)
+        if (p) (void)hipFree(p);
+    c->X = nullptr;
+    c->z = c->z_best = nullptr;
+    c->slot_mu = c->slot_P = c->slot_c = c->slot_sigma = nullptr;
+    c->cnt = c->cnt_best = nullptr;
+    c->mu_best = c->sigma_best = c->cand = nullptr;
+    c->ctl = nullptr;
+    c->hyp = c->d_mu0 = c->d_LT = c->d_Gp = c->d_LTL = nullptr;
+    c->rec = c->gath = nullptr;
+    c->order = nullptr;
+    c->partial = nullptr;
+}
+
+template <typename T>
+int dalloc(np8_ctx *c, T **p, size_t n) {
+    if (*p) {
+        (void)hipFree(*p);
+        *p = nullptr;
+    }
+    HIPC(c, hipMalloc((void **)p, sizeof(T) * (n ? n : 1)));
+    HIPC(c, hipMemsetAsync(*p, 0, sizeof(T) * (n ? n : 1), c->stream));
+    return NP8_OK;
+}
+
+int upload_slots(np8_ctx *c, const std::vector<SlotHost> &slots, const std::vector<int32_t> &cnt) {
+    const int D = c->D, DP = c->DP, K = (int)slots.size();
+    std::vector<double> mu((size_t)c->kcap * D, 0.0), P((size_t)c->kcap * DP, 0.0), cc(c->kcap, 0.0),
+        sg((size_t)c->kcap * D * D, 0.0);
+    for (int s = 0; s < K; ++s) {
+        std::memcpy(&mu[(size_t)s * D], slots[s].mu.data(), sizeof(double) * D);
+        std::memcpy(&P[(size_t)s * DP], slots[s].P.data(), sizeof(double) * DP);
+        std::memcpy(&sg[(size_t)s * D * D], slots[s].sigma.data(), sizeof(double) * D * D);
+        cc[s] = slots[s].c;
+    }
+    std::vector<int32_t> cn(c->kcap, 0);
+    for (int s = 0; s < K; ++s) cn[s] = cnt[s];
+    HIPC(c, hipMemcpyAsync(c->slot_mu, mu.data(), sizeof(double) * mu.size(), hipMemcpyHostToDevice, c->stream));
+    HIPC(c, hipMemcpyAsync(c->slot_P, P.data(), sizeof(double) * P.size(), hipMemcpyHostToDevice, c->stream));
+    HIPC(c, hipMemcpyAsync(c->slot_c, cc.data(), sizeof(double) * cc.size(), hipMemcpyHostToDevice, c->stream));
+    HIPC(c, hipMemcpyAsync(c->slot_sigma, sg.data(), sizeof(double) * sg.size(), hipMemcpyHostToDevice, c->stream));
+    HIPC(c, hipMemcpyAsync(c->cnt, cn.data(), sizeof(int32_t) * cn.size(), hipMemcpyHostToDevice, c->stream));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    return NP8_OK;
+}
+
+void timer_begin(np8_ctx *c, int phase, Timer &t) {
+    if (!c->timing) return;
+    (void)hipEventCreate(&t.a);
+    (void)hipEventCreate(&t.b);
+    t.phase = phase;
+    (void)hipEventRecord(t.a, c->stream);
+}
+
+void timer_end(np8_ctx *c, Timer &t) {
+    if (!c->timing) return;
+    (void)hipEventRecord(t.b, c->stream);
+    c->timers.push_back(t);
+}
+
+void collect_timers(np8_ctx *c) {
+    for (Timer &t : c->timers) {
+        float ms = 0.0f;
+        if (hipEventElapsedTime(&ms, t.a, t.b) == hipSuccess) c->ms[t.phase] += ms;
+        (void)hipEventDestroy(t.a);
+        (void)hipEventDestroy(t.b);
+    }
+    c->timers.clear();
+}
+
+FinArgs fin_args(np8_ctx *c, const unsigned char *recs, int world) {
+    FinArgs F;
+    F.recs = recs;
+    F.local_rec = c->rec;
+    F.rec_bytes = c->rec_bytes;
+    F.world = world;
+    F.rec_cap = c->rec_cap;
+    F.kcap = c->kcap;
+    F.D = c->D;
+    F.M = c->M;
+    F.cnt = c->cnt;
+    F.z = c->z;
+    F.n_loc = c->n_loc;
+    F.offset = c->offset;
+    F.slot_mu = c->slot_mu;
+    F.slot_P = c->slot_P;
+    F.slot_c = c->slot_c;
+    F.slot_sigma = c->slot_sigma;
+    F.cand = c->cand;
+    F.ctl = c->ctl;
+    F.mu0 = c->d_mu0;
+    F.LT = c->d_LT;
+    F.Gp = c->d_Gp;
+    F.LTL = c->d_LTL;
+    F.caux = c->caux;
+    F.rsk = c->rsk;
+    F.nu = c->nu;
+    F.seed = c->seed;
+    F.t = c->epoch;
+    return F;
+}
+
+AssignArgs assign_args(np8_ctx *c, int64_t p0, int64_t p1, const int64_t *order, bool use_perm) {
+    AssignArgs A;
+    A.X = c->X;
+    A.z = c->z;
+    A.cand = c->cand;
+    A.ctl = c->ctl;
+    A.hyp = c->hyp;
+    A.order = order;
+    A.rec = c->rec;
+    A.n_loc = c->n_loc;
+    A.offset = c->offset;
+    A.p0 = p0;
+    A.p1 = p1;
+    A.use_perm = use_perm ? 1 : 0;
+    A.perm = make_perm(c->seed, c->epoch, (uint32_t)c->n_glob);
+    A.seed = c->seed;
+    A.t = c->epoch;
+    A.kcap = c->kcap;
+    A.rec_cap = c->rec_cap;
+    return A;
+}
+
+int launch_finalize(np8_ctx *c, const unsigned char *recs, int world) {
+    Timer t;
+    timer_begin(c, 1, t);
+    HIPC(c, np8_launch_finalize(fin_args(c, recs, world), c->stream));
+    timer_end(c, t);
+    return NP8_OK;
+}
+
+// Empty record: rebuild the candidate table from the slot arrays (after host uploads).
+int rebuild(np8_ctx *c) {
+    HIPC(c, hipMemsetAsync(c->rec, 0, c->rec_bytes, c->stream));
+    return launch_finalize(c, c->rec, 1);
+}
+
+int launch_assign(np8_ctx *c, int64_t p0, int64_t p1, const int64_t *order, bool use_perm) {
+    Timer t;
+    timer_begin(c, 0, t);
+    HIPC(c, np8_launch_assign(assign_args(c, p0, p1, order, use_perm), c->D, c->M, c->stream));
+    timer_end(c, t);
+    return NP8_OK;
+}
+
+// One synchronous step over local positions [p0,p1): assign, exchange, finalize.
+int step(np8_ctx *c, int64_t p0, int64_t p1, const int64_t *order, bool use_perm) {
+    int r = launch_assign(c, p0, p1, order, use_perm);
+    if (r) return r;
+    if (c->world > 1) {
+        if (!c->comm) return fail(c, NP8_ERR_STATE, "host-exchange mode: use np8_step_local/np8_step_merge");
+        NCCLC(c, ncclAllGather(c->rec, c->gath, (size_t)c->rec_bytes, ncclUint8, c->comm, c->stream));
+        return launch_finalize(c, c->gath, c->world);
+    }
+    return launch_finalize(c, c->rec, 1);
+}
+
+int ensure_partial(np8_ctx *c) {
+    const int64_t nb = (c->n_loc + 255) / 256;
+    if (nb > c->partial_cap) {
+        int r = dalloc(c, &c->partial, (size_t)nb);
+        if (r) return r;
+        c->partial_cap = nb;
+    }
+    return NP8_OK;
+}
+
+// sum_i log p(x_i | theta_{z_i}) into ctl->L (global when sharded over RCCL).
+int launch_total_loglik(np8_ctx *c) {
+    int r = ensure_partial(c);
+    if (r) return r;
+    Timer t;
+    timer_begin(c, 2, t);
+    LoglikArgs A;
+    A.X = c->X;
+    A.z = c->z;
+    A.slot_mu = c->slot_mu;
+    A.slot_P = c->slot_P;
+    A.slot_c = c->slot_c;
+    A.partial = c->partial;
+    A.n_loc = c->n_loc;
+    HIPC(c, np8_launch_loglik(A, c->D, c->stream));
+    HIPC(c, np8_launch_loglik_reduce(c->partial, (c->n_loc + 255) / 256, &c->ctl->L_local, c->stream));
+    if (c->world > 1 && c->comm) {
+        NCCLC(c, ncclAllReduce(&c->ctl->L_local, &c->ctl->L, 1, ncclFloat64, ncclSum, c->comm, c->stream));
+    } else {
+        HIPC(c, hipMemcpyAsync(&c->ctl->L, &c->ctl->L_local, sizeof(double), hipMemcpyDeviceToDevice, c->stream));
+    }
+    timer_end(c, t);
+    return NP8_OK;
+}
+
+int end_sweep(np8_ctx *c) {
+    if (c->epoch % 5u == 0u) {  // np_mcmc.cpp:172-174
+        int r = launch_total_loglik(c);
+        if (r) return r;
+        SnapArgs S;
+        S.L = &c->ctl->L;
+        S.best = c->ctl->best;
+        S.have_best = &c->ctl->have_best;
+        S.par = c->checks & 1;
+        S.z = c->z;
+        S.cnt = c->cnt;
+        S.z_best = c->z_best;
+        S.cnt_best = c->cnt_best;
+        S.slot_mu = c->slot_mu;
+        S.slot_sigma = c->slot_sigma;
+        S.mu_best = c->mu_best;
+        S.sigma_best = c->sigma_best;
+        S.n_loc = c->n_loc;
+        S.kcap = c->kcap;
+        S.D = c->D;
+        HIPC(c, np8_launch_snapshot(S, c->stream));
+        c->checks += 1;
+    }
+    c->epoch += 1;
+    return NP8_OK;
+}
+
+int reset_ctl(np8_ctx *c) {
+    Ctl h;
+    std::memset(&h, 0, sizeof(h));
+    h.best[0] = h.best[1] = -INFINITY;
+    HIPC(c, hipMemcpyAsync(c->ctl, &h, sizeof(h), hipMemcpyHostToDevice, c->stream));
+    c->epoch = 0;
+    c->checks = 0;
+    return NP8_OK;
+}
+
+int read_ctl(np8_ctx *c, Ctl *h) {
+    HIPC(c, hipStreamSynchronize(c->stream));
+    HIPC(c, hipMemcpy(h, c->ctl, sizeof(Ctl), hipMemcpyDeviceToHost));
+    return NP8_OK;
+}
+
+}  // namespace
+
+// =====================================================================================================
+extern "C" {
+
+int np8_create(np8_ctx **out, const np8_config *cfg) {
+    if (!out || !cfg) return NP8_ERR_ARG;
+    *out = nullptr;
+    np8_ctx *c = new np8_ctx();
+    c->D = cfg->D;
+    c->M = cfg->M;
+    if (c->D < 1 || c->D > kMaxD || c->M < 1 || c->M > kMaxM || !cfg->mu0 || !cfg->Lambda || !(cfg->kappa > 0.0) ||
+        !(cfg->alpha > 0.0)) {
+        delete c;
+        return NP8_ERR_ARG;
+    }
+    if (!np8_supported(c->D, c->M)) {
+        delete c;
+        return NP8_ERR_ARG;
+    }
+    c->DP = packed_size(c->D);
+    c->CS = cand_stride(c->D);
+    c->kcap = cfg->kcap > 0 ? cfg->kcap : 2048;
+    c->alpha = cfg->alpha;
+    c->kappa = cfg->kappa;
+    c->nu = cfg->nu;
+    c->seed = cfg->seed;
+    c->chunk = cfg->chunk;
+    c->mu0.assign(cfg->mu0, cfg->mu0 + c->D);
+    c->Lambda.assign(cfg->Lambda, cfg->Lambda + (size_t)c->D * c->D);
+    if (!prepare_base(c)) {
+        delete c;
+        return NP8_ERR_ARG;
+    }
+    if (cfg->device >= 0) {
+        c->device = cfg->device;
+        if (hipSetDevice(c->device) != hipSuccess) {
+            delete c;
+            return NP8_ERR_HIP;
+        }
+    } else {
+        (void)hipGetDevice(&c->device);
+    }
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return NP8_ERR_HIP;
+    }
+    c->own_stream = true;
+    c->rec_cap = kReqMax;
+    c->rec_bytes = record_bytes(c->kcap, c->rec_cap);
+    int r = 0;
+    const int D = c->D, DP = c->DP, kc = c->kcap;
+    if ((r = dalloc(c, &c->slot_mu, (size_t)kc * D)) || (r = dalloc(c, &c->slot_P, (size_t)kc * DP)) ||
+        (r = dalloc(c, &c->slot_c, (size_t)kc)) || (r = dalloc(c, &c->slot_sigma, (size_t)kc * D * D)) ||
+        (r = dalloc(c, &c->cnt, (size_t)kc)) || (r = dalloc(c, &c->cnt_best, (size_t)kc)) ||
+        (r = dalloc(c, &c->mu_best, (size_t)kc * D)) || (r = dalloc(c, &c->sigma_best, (size_t)kc * D * D)) ||
+        (r = dalloc(c, &c->cand, (size_t)kc * c->CS)) || (r = dalloc(c, &c->ctl, 1)) ||
+        (r = dalloc(c, &c->rec, (size_t)c->rec_bytes))) {
+        free_device(c);
+        delete c;
+        return r;
+    }
+    // hyp: mu0 | UinvT packed | caux | rsk | logam | nu
+    std::vector<double> hyp;
+    hyp.insert(hyp.end(), c->mu0.begin(), c->mu0.end());
+    for (int a = 0; a < D; ++a)
+        for (int b = a; b < D; ++b) hyp.push_back(c->UinvT[a * D + b]);
+    hyp.push_back(c->caux);
+    hyp.push_back(c->rsk);
+    hyp.push_back(c->logam);
+    hyp.push_back(c->nu);
+    std::vector<double> gp;
+    for (int a = 0; a < D; ++a)
+        for (int b = a; b < D; ++b) gp.push_back(c->Gp[a * D + b]);
+    if ((r = dalloc(c, &c->hyp, hyp.size())) || (r = dalloc(c, &c->d_mu0, (size_t)D)) ||
+        (r = dalloc(c, &c->d_LT, (size_t)D * D)) || (r = dalloc(c, &c->d_Gp, gp.size())) ||
+        (r = dalloc(c, &c->d_LTL, (size_t)D * D))) {
+        free_device(c);
+        delete c;
+        return r;
+    }
+    (void)hipMemcpy(c->hyp, hyp.data(), sizeof(double) * hyp.size(), hipMemcpyHostToDevice);
+    (void)hipMemcpy(c->d_mu0, c->mu0.data(), sizeof(double) * D, hipMemcpyHostToDevice);
+    (void)hipMemcpy(c->d_LT, c->LT.data(), sizeof(double) * D * D, hipMemcpyHostToDevice);
+    (void)hipMemcpy(c->d_Gp, gp.data(), sizeof(double) * gp.size(), hipMemcpyHostToDevice);
+    (void)hipMemcpy(c->d_LTL, c->LTL.data(), sizeof(double) * D * D, hipMemcpyHostToDevice);
+    if (reset_ctl(c) || hipStreamSynchronize(c->stream) != hipSuccess) {
+        free_device(c);
+        delete c;
+        return NP8_ERR_HIP;
+    }
+    *out = c;
+    return NP8_OK;
+}
+
+int np8_destroy(np8_ctx *c) {
+    if (!c) return NP8_OK;
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    collect_timers(c);
+    if (c->comm) (void)ncclCommDestroy(c->comm);
+    free_device(c);
+    if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+    return NP8_OK;
+}
+
+const char *np8_last_error(const np8_ctx *c) { return c ? c->err.c_str() : "null context"; }
+
+int np8_set_data(np8_ctx *c, const double *X, int64_t n, int32_t D, int64_t offset, int64_t n_global) {
+    if (!c) return NP8_ERR_ARG;
+    if (D != c->D) return fail(c, NP8_ERR_ARG, "np8_set_data: D does not match the configuration");
+    if (n < 0 || (n > 0 && !X)) return fail(c, NP8_ERR_ARG, "np8_set_data: bad buffer");
+    if (n_global <= 0) n_global = n;
+    if (offset < 0 || offset + n > n_global || n_global > 0x7FFFFFFFll)
+        return fail(c, NP8_ERR_ARG, "np8_set_data: shard outside [0, n_global) or n_global >= 2^31");
+    c->n_loc = n;
+    c->offset = offset;
+    c->n_glob = n_global;
+    int r = 0;
+    if ((r = dalloc(c, &c->X, (size_t)n * D)) || (r = dalloc(c, &c->z, (size_t)n)) ||
+        (r = dalloc(c, &c->z_best, (size_t)n)))
+        return r;
+    std::vector<double> soa((size_t)n * D);
+    for (int64_t i = 0; i < n; ++i)
+        for (int a = 0; a < D; ++a) soa[(size_t)a * n + i] = X[(size_t)i * D + a];
+    HIPC(c, hipMemcpyAsync(c->X, soa.data(), sizeof(double) * soa.size(), hipMemcpyHostToDevice, c->stream));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    c->have_data = true;
+    c->have_state = false;
+    return NP8_OK;
+}
+
+static int set_state_common(np8_ctx *c, const std::vector<SlotHost> &slots, const std::vector<int32_t> &cnt,
+                            const std::vector<int32_t> &zloc) {
+    int r = upload_slots(c, slots, cnt);
+    if (r) return r;
+    HIPC(c, hipMemcpyAsync(c->z, zloc.data(), sizeof(int32_t) * zloc.size(), hipMemcpyHostToDevice, c->stream));
+    r = reset_ctl(c);
+    if (r) return r;
+    r = rebuild(c);
+    if (r) return r;
+    HIPC(c, hipStreamSynchronize(c->stream));
+    c->have_state = true;
+    return NP8_OK;
+}
+
+int np8_set_state(np8_ctx *c, const int32_t *z, int32_t K, const double *mu, const double *Sigma) {
+    if (!c) return NP8_ERR_ARG;
+    if (!c->have_data) return fail(c, NP8_ERR_STATE, "np8_set_state: no data");
+    if (K < 1 || K > c->kcap || !mu || !Sigma || (c->n_loc > 0 && !z))
+        return fail(c, NP8_ERR_ARG, "np8_set_state: K outside [1,kcap] or null buffer");
+    std::vector<SlotHost> slots(K);
+    for (int k = 0; k < K; ++k)
+        if (!slot_from_sigma(c, mu + (size_t)k * c->D, Sigma + (size_t)k * c->D * c->D, slots[k]))
+            return fail(c, NP8_ERR_SIGMA, "np8_set_state: covariance " + std::to_string(k) + " has det <= 0");
+    std::vector<int32_t> cnt(K, 0), zl(c->n_loc);
+    for (int64_t i = 0; i < c->n_loc; ++i) {
+        if (z[i] < 0 || z[i] >= K) return fail(c, NP8_ERR_RANGE, "np8_set_state: label out of range");
+        zl[i] = z[i];
+        cnt[z[i]]++;
+    }
+    if (c->world > 1 && !c->comm)
+        return fail(c, NP8_ERR_STATE, "np8_set_state: host-exchange mode has no count reduction; use np8_init_random");
+    if (c->world > 1) {  // counts are global
+        int32_t *d = nullptr;
+        HIPC(c, hipMalloc(&d, sizeof(int32_t) * K));
+        HIPC(c, hipMemcpy(d, cnt.data(), sizeof(int32_t) * K, hipMemcpyHostToDevice));
+        NCCLC(c, ncclAllReduce(d, d, K, ncclInt32, ncclSum, c->comm, c->stream));
+        HIPC(c, hipStreamSynchronize(c->stream));
+        HIPC(c, hipMemcpy(cnt.data(), d, sizeof(int32_t) * K, hipMemcpyDeviceToHost));
+        (void)hipFree(d);
+    }
+    return set_state_common(c, slots, cnt, zl);
+}
+
+int np8_init_random(np8_ctx *c, int32_t K_init) {
+    if (!c) return NP8_ERR_ARG;
+    if (!c->have_data) return fail(c, NP8_ERR_STATE, "np8_init_random: no data");
+    if (K_init < 1 || K_init > c->kcap) return fail(c, NP8_ERR_ARG, "np8_init_random: K_init outside [1,kcap]");
+    const int D = c->D, P = (D + 2) / 2;
+    std::vector<SlotHost> draws(K_init);
+    for (int k = 0; k < K_init; ++k) {  // InitClusters::init: K G0 draws (np_init_clusters.cpp:24-40)
+        std::vector<double> g(2 * P);
+        for (int q = 0; q < P; ++q)
+            normal_pair(c->seed, (uint64_t)k, 0xFFFFFFFFu, kStreamInitTheta, (uint32_t)q, g[2 * q], g[2 * q + 1]);
+        slot_from_normals(c, g[0], g.data() + 1, draws[k]);
+    }
+    // uniform assignment of every item (np_mcmc.cpp:69-85); counts over ALL items, so every rank
+    // gets the same global counts without communication.
+    std::vector<int32_t> cntk(K_init, 0), zl(c->n_loc);
+    for (int64_t i = 0; i < c->n_glob; ++i) {
+        const double u = uniform(c->seed, (uint64_t)i, 0xFFFFFFFFu, kStreamInitZ, 0);
+        int k = (int)(u * (double)K_init);
+        if (k >= K_init) k = K_init - 1;
+        cntk[k]++;
+        if (i >= c->offset && i < c->offset + c->n_loc) zl[i - c->offset] = k;
+    }
+    // cleanup: drop empty clusters, keep order (membertrix.cpp:343-364)
+    std::vector<int32_t> remap(K_init, -1), cnt;
+    std::vector<SlotHost> slots;
+    for (int k = 0; k < K_init; ++k)
+        if (cntk[k] > 0) {
+            remap[k] = (int32_t)slots.size();
+            slots.push_back(draws[k]);
+            cnt.push_back(cntk[k]);
+        }
+    for (auto &v : zl) v = remap[v];
+    return set_state_common(c, slots, cnt, zl);
+}
+
+int np8_sweep(np8_ctx *c, int32_t n_sweeps) {
+    if (!c) return NP8_ERR_ARG;
+    if (!c->have_state) return fail(c, NP8_ERR_STATE, "np8_sweep: no state (np8_set_state/np8_init_random)");
+    const int64_t N = c->n_loc;
+    int64_t chunk = (c->chunk <= 0 || c->chunk >= c->n_glob) ? N : c->chunk;
+    const bool sync = chunk >= N;
+    if (!sync && c->world > 1) return fail(c, NP8_ERR_ARG, "np8_sweep: chunk < N is single-rank only");
+    for (int s = 0; s < n_sweeps; ++s) {
+        if (N > 0) {
+            for (int64_t p0 = 0; p0 < N; p0 += chunk) {
+                const int64_t p1 = (p0 + chunk < N) ? p0 + chunk : N;
+                int r = step(c, p0, p1, nullptr, !sync);
+                if (r) return r;
+            }
+        } else if (c->world > 1) {
+            int r = step(c, 0, 0, nullptr, false);  // still take part in the exchange
+            if (r) return r;
+        }
+        int r = end_sweep(c);
+        if (r) return r;
+    }
+    return NP8_OK;
+}
+
+int np8_update_points(np8_ctx *c, const int64_t *ids, int64_t n) {
+    if (!c) return NP8_ERR_ARG;
+    if (!c->have_state) return fail(c, NP8_ERR_STATE, "np8_update_points: no state");
+    if (c->world > 1) return fail(c, NP8_ERR_ARG, "np8_update_points: single-rank only");
+    if (n <= 0) return NP8_OK;
+    for (int64_t k = 0; k < n; ++k)
+        if (ids[k] < 0 || ids[k] >= c->n_loc) return fail(c, NP8_ERR_RANGE, "np8_update_points: id out of range");
+    if (n > c->order_cap) {
+        int r = dalloc(c, &c->order, (size_t)n);
+        if (r) return r;
+        c->order_cap = n;
+    }
+    HIPC(c, hipMemcpyAsync(c->order, ids, sizeof(int64_t) * n, hipMemcpyHostToDevice, c->stream));
+    for (int64_t k = 0; k < n; ++k) {
+        int r = step(c, k, k + 1, c->order, false);
+        if (r) return r;
+    }
+    HIPC(c, hipStreamSynchronize(c->stream));  // ids buffer may be reused by the caller
+    return NP8_OK;
+}
+
+int np8_end_sweep(np8_ctx *c) {
+    if (!c) return NP8_ERR_ARG;
+    if (!c->have_state) return fail(c, NP8_ERR_STATE, "np8_end_sweep: no state");
+    return end_sweep(c);
+}
+
+int np8_sync(np8_ctx *c) {
+    if (!c) return NP8_ERR_ARG;
+    Ctl h;
+    int r = read_ctl(c, &h);
+    if (r) return r;
+    if (h.err) {
+        int32_t zero = 0;
+        HIPC(c, hipMemcpy(&c->ctl->err, &zero, sizeof(zero), hipMemcpyHostToDevice));
+        if (h.err & kErrCapacity)
+            return fail(c, NP8_ERR_CAPACITY,
+                        "new-cluster requests exceeded the free slots or NP8_REQ_MAX in a step; those items kept "
+                        "their cluster (raise kcap or lower chunk)");
+    }
+    return NP8_OK;
+}
+
+int np8_get_state(np8_ctx *c, int32_t which, int32_t *z, int32_t *K, double *mu, double *Sigma, int64_t *counts) {
+    if (!c) return NP8_ERR_ARG;
+    if (!c->have_state) return fail(c, NP8_ERR_STATE, "np8_get_state: no state");
+    Ctl h;
+    int r = read_ctl(c, &h);
+    if (r) return r;
+    if (which == 1 && !h.have_best) return fail(c, NP8_ERR_STATE, "np8_get_state: no max-likelihood snapshot yet");
+    const int D = c->D, kc = c->kcap;
+    std::vector<int32_t> cn(kc), zz(c->n_loc);
+    HIPC(c, hipMemcpy(cn.data(), which ? c->cnt_best : c->cnt, sizeof(int32_t) * kc, hipMemcpyDeviceToHost));
+    std::vector<int32_t> lab(kc, -1);
+    int k = 0;
+    for (int s = 0; s < kc; ++s)
+        if (cn[s] > 0) lab[s] = k++;
+    if (K) *K = k;
+    if (z) {
+        HIPC(c, hipMemcpy(zz.data(), which ? c->z_best : c->z, sizeof(int32_t) * c->n_loc, hipMemcpyDeviceToHost));
+        for (int64_t i = 0; i < c->n_loc; ++i) z[i] = lab[zz[i]];
+    }
+    if (mu || Sigma || counts) {
+        std::vector<double> m((size_t)kc * D), sg((size_t)kc * D * D);
+        HIPC(c, hipMemcpy(m.data(), which ? c->mu_best : c->slot_mu, sizeof(double) * m.size(), hipMemcpyDeviceToHost));
+        HIPC(c, hipMemcpy(sg.data(), which ? c->sigma_best : c->slot_sigma, sizeof(double) * sg.size(),
+                          hipMemcpyDeviceToHost));
+        for (int s = 0; s < kc; ++s) {
+            if (lab[s] < 0) continue;
+            if (mu) std::memcpy(mu + (size_t)lab[s] * D, &m[(size_t)s * D], sizeof(double) * D);
+            if (Sigma) std::memcpy(Sigma + (size_t)lab[s] * D * D, &sg[(size_t)s * D * D], sizeof(double) * D * D);
+            if (counts) counts[lab[s]] = cn[s];
+        }
+    }
+    return NP8_OK;
+}
+
+int np8_loglik_matrix(np8_ctx *c, const int64_t *idx, int64_t n, double *out) {
+    if (!c) return NP8_ERR_ARG;
+    if (!c->have_state) return fail(c, NP8_ERR_STATE, "np8_loglik_matrix: no state");
+    if (n <= 0) return NP8_OK;
+    for (int64_t k = 0; k < n; ++k)
+        if (idx[k] < 0 || idx[k] >= c->n_loc) return fail(c, NP8_ERR_RANGE, "np8_loglik_matrix: index out of range");
+    Ctl h;
+    int r = read_ctl(c, &h);
+    if (r) return r;
+    const int64_t w = (int64_t)h.K + c->M;
+    int64_t *d_idx = nullptr;
+    double *d_out = nullptr;
+    HIPC(c, hipMalloc(&d_idx, sizeof(int64_t) * n));
+    HIPC(c, hipMalloc(&d_out, sizeof(double) * n * w));
+    HIPC(c, hipMemcpy(d_idx, idx, sizeof(int64_t) * n, hipMemcpyHostToDevice));
+    HIPC(c, np8_launch_loglik_matrix(assign_args(c, 0, 0, nullptr, false), c->D, c->M, d_idx, n, d_out, c->stream));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    HIPC(c, hipMemcpy(out, d_out, sizeof(double) * n * w, hipMemcpyDeviceToHost));
+    (void)hipFree(d_idx);
+    (void)hipFree(d_out);
+    return NP8_OK;
+}
+
+int np8_total_loglik(np8_ctx *c, double *out) {
+    if (!c || !out) return NP8_ERR_ARG;
+    if (!c->have_state) return fail(c, NP8_ERR_STATE, "np8_total_loglik: no state");
+    int r = launch_total_loglik(c);
+    if (r) return r;
+    Ctl h;
+    r = read_ctl(c, &h);
+    if (r) return r;
+    *out = h.L;
+    return NP8_OK;
+}
+
+int np8_stats(np8_ctx *c, np8_stats_t *out) {
+    if (!c || !out) return NP8_ERR_ARG;
+    Ctl h;
+    int r = read_ctl(c, &h);
+    if (r) return r;
+    collect_timers(c);
+    std::memset(out, 0, sizeof(*out));
+    out->K = h.K;
+    out->epoch = c->epoch;
+    out->new_clusters = h.n_new;
+    out->rejected_requests = h.n_rejected;
+    out->existing_picks = -1;
+    out->best_loglik = h.best[c->checks & 1];
+    out->last_loglik = h.L;
+    out->ms_assign = c->ms[0];
+    out->ms_finalize = c->ms[1];
+    out->ms_loglik = c->ms[2];
+    return NP8_OK;
+}
+
+int np8_set_timing(np8_ctx *c, int32_t enable) {
+    if (!c) return NP8_ERR_ARG;
+    c->timing = enable != 0;
+    return NP8_OK;
+}
+
+int np8_set_stream(np8_ctx *c, void *stream) {
+    if (!c) return NP8_ERR_ARG;
+    (void)hipStreamSynchronize(c->stream);
+    if (c->own_stream) (void)hipStreamDestroy(c->stream);
+    c->stream = (hipStream_t)stream;
+    c->own_stream = false;
+    return NP8_OK;
+}
+
+int np8_comm_unique_id(uint8_t out[128]) {
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess) return NP8_ERR_COMM;
+    static_assert(sizeof(id) == 128, "ncclUniqueId is 128 bytes");
+    std::memcpy(out, &id, sizeof(id));
+    return NP8_OK;
+}
+
+static int resize_records(np8_ctx *c, int world) {
+    c->world = world;
+    c->rec_cap = world > 1 ? (kReqMax / world > 64 ? kReqMax / world : 64) : kReqMax;
+    c->rec_bytes = record_bytes(c->kcap, c->rec_cap);
+    int r = dalloc(c, &c->rec, (size_t)c->rec_bytes);
+    if (r) return r;
+    if (world > 1) {
+        r = dalloc(c, &c->gath, (size_t)c->rec_bytes * world);
+        if (r) return r;
+    }
+    HIPC(c, hipStreamSynchronize(c->stream));
+    return NP8_OK;
+}
+
+int np8_comm_init(np8_ctx *c, const uint8_t id[128], int32_t rank, int32_t world) {
+    if (!c || world < 1 || rank < 0 || rank >= world) return NP8_ERR_ARG;
+    if (!id) {  // host-exchange mode: the caller moves records (np8_step_local / np8_step_merge)
+        c->rank = rank;
+        return resize_records(c, world);
+    }
+    HIPC(c, hipSetDevice(c->device));
+    ncclUniqueId uid;
+    std::memcpy(&uid, id, sizeof(uid));
+    NCCLC(c, ncclCommInitRank(&c->comm, world, uid, rank));
+    c->rank = rank;
+    return resize_records(c, world);
+}
+
+int64_t np8_record_bytes(np8_ctx *c) { return c ? c->rec_bytes : 0; }
+
+int np8_step_local(np8_ctx *c, void *record_out) {
+    if (!c || !record_out) return NP8_ERR_ARG;
+    if (!c->have_state) return fail(c, NP8_ERR_STATE, "np8_step_local: no state");
+    int r = launch_assign(c, 0, c->n_loc, nullptr, false);
+    if (r) return r;
+    HIPC(c, hipMemcpyAsync(record_out, c->rec, (size_t)c->rec_bytes, hipMemcpyDeviceToHost, c->stream));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    return NP8_OK;
+}
+
+int np8_step_merge(np8_ctx *c, const void *records, int32_t world) {
+    if (!c || !records || world < 1) return NP8_ERR_ARG;
+    if (world != c->world) return fail(c, NP8_ERR_ARG, "np8_step_merge: world differs from np8_comm_init");
+    if (world == 1) {
+        HIPC(c, hipMemcpyAsync(c->rec, records, (size_t)c->rec_bytes, hipMemcpyHostToDevice, c->stream));
+        return launch_finalize(c, c->rec, 1);
+    }
+    HIPC(c, hipMemcpyAsync(c->gath, records, (size_t)c->rec_bytes * world, hipMemcpyHostToDevice, c->stream));
+    int r = launch_finalize(c, c->gath, world);
+    if (r) return r;
+    HIPC(c, hipStreamSynchronize(c->stream));
+    return NP8_OK;
+}
+
+}  // extern "C"

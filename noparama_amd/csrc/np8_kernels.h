@@ -1,0 +1,111 @@
+// np8_kernels.h -- launch interface between the C-ABI host code (np8_capi.hip) and the kernels.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "np8_device.h"
+
+namespace np8 {
+
+// Device-resident control block (one per context).
+struct Ctl {
+    int32_t K;          // live clusters (rows of the dense candidate table)
+    int32_t err;        // sticky error bits
+    int32_t have_best;  // a max-likelihood snapshot exists
+    int32_t pad;
+    int64_t n_new;      // accepted new-cluster requests (cumulative)
+    int64_t n_rejected; // rejected requests (cumulative)
+    double L;           // last total log-likelihood (global after the exchange)
+    double L_local;     // this rank's part
+    double best[2];     // best L, double-buffered by check parity
+};
+
+enum : int32_t { kErrCapacity = 1 };
+
+// Exchange record of one rank for one synchronous step:
+//   RecHeader | int32 delta[kcap] | Request req[rec_cap]
+struct RecHeader {
+    int32_t nreq;
+    int32_t pad[3];
+};
+constexpr int kRecHeaderBytes = 16;
+
+struct Request {
+    int64_t pos;   // global scan position (orders requests across ranks)
+    int64_t i;     // global item index (Philox key of the auxiliary draw)
+    int32_t m;     // which auxiliary
+    int32_t zold;  // slot the item leaves
+};
+
+inline int64_t record_bytes(int kcap, int rec_cap) {
+    int64_t b = kRecHeaderBytes + 4ll * kcap + (int64_t)sizeof(Request) * rec_cap;
+    return (b + 15) & ~15ll;
+}
+
+struct AssignArgs {
+    const double *X;   // [D][n_loc] (structure of arrays)
+    int32_t *z;        // [n_loc] slot ids
+    const double *cand;
+    const Ctl *ctl;
+    const double *hyp; // mu0 | UinvT packed | caux | rsk | logam | nu
+    const int64_t *order;
+    unsigned char *rec;
+    int64_t n_loc, offset;
+    int64_t p0, p1;
+    int32_t use_perm;
+    Perm perm;
+    uint64_t seed;
+    uint32_t t;
+    int32_t kcap, rec_cap;
+};
+
+struct FinArgs {
+    const unsigned char *recs;  // world records, rec_bytes apart
+    unsigned char *local_rec;   // cleared after use
+    int64_t rec_bytes;
+    int32_t world, rec_cap, kcap, D, M;
+    int32_t *cnt;
+    int32_t *z;
+    int64_t n_loc, offset;
+    double *slot_mu, *slot_P, *slot_c, *slot_sigma;
+    double *cand;
+    Ctl *ctl;
+    const double *mu0, *LT, *Gp, *LTL;  // LT, LTL: D*D row-major; Gp packed
+    double caux, rsk, nu;
+    uint64_t seed;
+    uint32_t t;
+};
+
+struct LoglikArgs {
+    const double *X;
+    const int32_t *z;
+    const double *slot_mu, *slot_P, *slot_c;
+    double *partial;
+    int64_t n_loc;
+};
+
+struct SnapArgs {
+    const double *L;
+    double *best;
+    int32_t *have_best;
+    int32_t par;
+    const int32_t *z, *cnt;
+    int32_t *z_best, *cnt_best;
+    const double *slot_mu, *slot_sigma;
+    double *mu_best, *sigma_best;
+    int64_t n_loc;
+    int32_t kcap, D;
+};
+
+}  // namespace np8
+
+bool np8_supported(int D, int M);
+hipError_t np8_launch_assign(const np8::AssignArgs &A, int D, int M, hipStream_t s);
+hipError_t np8_launch_loglik_matrix(const np8::AssignArgs &A, int D, int M, const int64_t *idx, int64_t n,
+                                    double *out, hipStream_t s);
+size_t np8_finalize_lds_bytes(int kcap);
+hipError_t np8_launch_finalize(const np8::FinArgs &F, hipStream_t s);
+hipError_t np8_launch_loglik(const np8::LoglikArgs &A, int D, hipStream_t s);
+hipError_t np8_launch_loglik_reduce(const double *partial, int64_t nb, double *out, hipStream_t s);
+hipError_t np8_launch_snapshot(const np8::SnapArgs &A, hipStream_t s);

@@ -1,0 +1,566 @@
+// np8_kernels.hip -- gfx950 kernels of the Neal Algorithm 8 sweep.
+//
+//   np8_assign<D,M>   one lane per data item: fp64 log-likelihood against every live cluster (cluster
+//                     table read through the scalar cache: wave-uniform addresses, SGPR operands) and
+//                     against M auxiliary G0 draws generated in-register from Philox; block-reservoir
+//                     categorical draw; writes the new label or a new-cluster request.
+//                     Reference: src/np_neal_algorithm8.cpp:49-167 (one point), np_mcmc.cpp:146-164.
+//   np8_finalize      one workgroup: applies count deltas of all ranks, turns new-cluster requests into
+//                     clusters (membertrix::addCluster/assign, membertrix.cpp:87-164), frees empty ones
+//                     (retract auto-remove, membertrix.cpp:200-203) and rebuilds the dense candidate table.
+//   np8_loglik / np8_loglik_reduce / np8_snapshot
+//                     MCMC::considerMaxLikelihood (np_mcmc.cpp:187-203): sum_i log p(x_i|theta_z_i),
+//                     keep the labelling when it improves.
+//   np8_loglik_matrix debug/parity: the assign kernel's log-likelihoods for chosen items.
+#include "np8_kernels.h"
+
+#include <hip/hip_runtime.h>
+
+using namespace np8;
+
+namespace {
+
+template <int D>
+struct HypView {
+    // hyp layout: mu0[D] | UinvT packed[DP] | caux | rsk | logam | nu
+    static constexpr int DP = D * (D + 1) / 2;
+    static constexpr int kMu0 = 0;
+    static constexpr int kUinvT = D;
+    static constexpr int kCaux = D + DP;
+    static constexpr int kRsk = kCaux + 1;
+    static constexpr int kLogam = kCaux + 2;
+    static constexpr int kNu = kCaux + 3;
+};
+
+// ll = c - q/2 with q = d' P d over the packed upper triangle (off-diagonals pre-doubled).
+template <int D>
+__device__ __forceinline__ double cand_ll(const double *__restrict__ e, const double (&x)[D]) {
+    constexpr int DP = D * (D + 1) / 2;
+    double d[D];
+#pragma unroll
+    for (int a = 0; a < D; ++a) d[a] = x[a] - e[a];
+    const double *P = e + D;
+    double q = 0.0;
+    int k = 0;
+#pragma unroll
+    for (int a = 0; a < D; ++a) {
+        double t = P[k++] * d[a];
+#pragma unroll
+        for (int b = a + 1; b < D; ++b) t = fma(P[k++], d[b], t);
+        q = fma(t, d[a], q);
+    }
+    return fma(-0.5, q, e[D + DP]);
+}
+
+// y0 = (L^T)^{-1} (x - mu0): the item in the whitened frame of the base measure.
+template <int D>
+__device__ __forceinline__ void whiten(const double *__restrict__ hyp, const double (&x)[D], double (&y0)[D]) {
+    using H = HypView<D>;
+    double dx[D];
+#pragma unroll
+    for (int a = 0; a < D; ++a) dx[a] = x[a] - hyp[H::kMu0 + a];
+    const double *U = hyp + H::kUinvT;
+    int k = 0;
+#pragma unroll
+    for (int a = 0; a < D; ++a) {
+        double t0 = U[k++] * dx[a];
+#pragma unroll
+        for (int b = a + 1; b < D; ++b) t0 = fma(U[k++], dx[b], t0);
+        y0[a] = t0;
+    }
+}
+
+// Log-likelihood of x under auxiliary G0 draw m of (item ig, epoch t).  The draw uses Philox calls
+// m*P .. m*P+P-1 (P = ceil((D+1)/2)); normal 0 scales, normals 1..D are xi:
+// v = D + nu g, s = |v|/sqrt(kappa), q = |y0 - s xi|^2 / v^2, ll = caux - D log|v| - q/2
+// (normalinvwishart.h:44-64, invwishart.h:34-46, multivariatenormal.cpp:124-135; DESIGN.md "G0").
+template <int D>
+__device__ __forceinline__ double aux_ll(const double *__restrict__ hyp, const double (&y0)[D], uint64_t seed,
+                                         uint64_t ig, uint32_t t, int m) {
+    using H = HypView<D>;
+    constexpr int P = (D + 2) / 2;
+    const double caux = hyp[H::kCaux], rsk = hyp[H::kRsk], nu = hyp[H::kNu];
+    double g0 = 0.0, g1 = 0.0, v = 0.0, s = 0.0, r2 = 0.0;
+#pragma unroll
+    for (int k = 0; k <= D; ++k) {
+        if ((k & 1) == 0) normal_pair(seed, ig, t, kStreamAux, (uint32_t)(m * P + (k >> 1)), g0, g1);
+        const double g = (k & 1) ? g1 : g0;
+        if (k == 0) {
+            v = fma(nu, g, (double)D);
+            s = fabs(v) * rsk;
+        } else {
+            const double e = fma(-s, g, y0[k - 1]);
+            r2 = fma(e, e, r2);
+        }
+    }
+    const double q = r2 / (v * v);
+    const double cm = fma(-(double)D, log(fabs(v)), caux);
+    return fma(-0.5, q, cm);
+}
+
+// One step of the single-uniform weighted reservoir (DESIGN.md "Pick"): candidate j with log-weight l.
+__device__ __forceinline__ void pick_step(PickState &st, double l, int32_t j) {
+    if (l == -INFINITY) return;  // zero weight: can never be drawn, state unchanged
+    const bool gt = l > st.Tm;
+    const double e = exp(gt ? (st.Tm - l) : (l - st.Tm));
+    const double a = gt ? 1.0 : e;
+    const double S = gt ? fma(st.S, e, 1.0) : st.S + e;
+    const double uS = st.u * S;
+    const bool take = uS < a;
+    const double num = take ? uS : uS - a;
+    const double den = take ? a : S - a;
+    st.u = clamp_u(num / den);
+    st.pick = take ? j : st.pick;
+    st.Tm = gt ? l : st.Tm;
+    st.S = S;
+}
+
+__device__ __forceinline__ int64_t position_to_local(const AssignArgs &A, int64_t p) {
+    if (A.order) return A.order[p];
+    if (A.use_perm) return (int64_t)perm_apply(A.perm, (uint32_t)p);
+    return p;
+}
+
+template <int D, int M>
+__global__ __launch_bounds__(256) void np8_assign(AssignArgs A) {
+    constexpr int DP = D * (D + 1) / 2;
+    constexpr int CS = (D + DP + 4 + 1) & ~1;
+    const int64_t p = A.p0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= A.p1) return;
+    const int64_t il = position_to_local(A, p);
+    const uint64_t ig = (uint64_t)(A.offset + il);
+    const double *__restrict__ X = A.X;
+    const double *__restrict__ cand = A.cand;
+    const double *__restrict__ hyp = A.hyp;
+
+    double x[D];
+#pragma unroll
+    for (int a = 0; a < D; ++a) x[a] = X[(int64_t)a * A.n_loc + il];
+    const int32_t zi = A.z[il];
+
+    PickState st;
+    st.Tm = -INFINITY;
+    st.S = 0.0;
+    st.u = uniform(A.seed, ig, A.t, kStreamPick, 0);
+    st.pick = 0;
+
+    const int K = A.ctl->K;
+    for (int j = 0; j < K; ++j) {
+        const double *e = cand + (int64_t)j * CS;
+        const double ll = cand_ll<D>(e, x);
+        const int32_t slot = (int32_t)e[D + DP + 3];
+        pick_step(st, ll + ((slot == zi) ? e[D + DP + 2] : e[D + DP + 1]), j);
+    }
+    {
+        double y0[D];
+        whiten<D>(hyp, x, y0);
+        const double logam = hyp[HypView<D>::kLogam];
+#pragma unroll 1
+        for (int m = 0; m < M; ++m) pick_step(st, aux_ll<D>(hyp, y0, A.seed, ig, A.t, m) + logam, K + m);
+    }
+
+    RecHeader *hdr = reinterpret_cast<RecHeader *>(A.rec);
+    int32_t *delta = reinterpret_cast<int32_t *>(A.rec + kRecHeaderBytes);
+    if (st.pick < K) {
+        const int32_t s = (int32_t)cand[(int64_t)st.pick * CS + D + DP + 3];
+        if (s != zi) {
+            atomicSub(delta + zi, 1);
+            atomicAdd(delta + s, 1);
+            A.z[il] = s;
+        }
+    } else {
+        const int q = atomicAdd(&hdr->nreq, 1);
+        if (q < A.rec_cap) {
+            Request *req = reinterpret_cast<Request *>(A.rec + kRecHeaderBytes + (int64_t)A.kcap * 4);
+            Request r;
+            r.pos = A.offset + p;
+            r.i = (int64_t)ig;
+            r.m = st.pick - K;
+            r.zold = zi;
+            req[q] = r;
+        }
+    }
+}
+
+// ---- block-wide helpers (1024 threads) ------------------------------------------------------------
+constexpr int kFinThreads = 1024;
+
+__device__ __forceinline__ int wave_incl_scan(int v) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int n = __shfl_up(v, o, 64);
+        if (lane >= o) v += n;
+    }
+    return v;
+}
+
+// Exclusive scan over the block; returns this thread's prefix, *total the block sum.
+__device__ int block_excl_scan(int v, int *sh /* >= 16 ints */, int *total) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const int inc = wave_incl_scan(v);
+    __syncthreads();
+    if (lane == 63) sh[wid] = inc;
+    __syncthreads();
+    if (wid == 0) {
+        const int x = (lane < nw) ? sh[lane] : 0;
+        const int y = wave_incl_scan(x);
+        if (lane < nw) sh[lane] = y - x;
+        if (lane == nw - 1) sh[16] = y;
+    }
+    __syncthreads();
+    const int r = sh[wid] + inc - v;
+    *total = sh[16];
+    __syncthreads();
+    return r;
+}
+
+}  // namespace
+
+// ---- finalize --------------------------------------------------------------------------------------
+namespace {
+
+__device__ __forceinline__ const RecHeader *rec_header(const FinArgs &F, int r) {
+    return reinterpret_cast<const RecHeader *>(F.recs + (int64_t)r * F.rec_bytes);
+}
+
+__device__ __forceinline__ const int32_t *rec_delta(const FinArgs &F, int r) {
+    return reinterpret_cast<const int32_t *>(F.recs + (int64_t)r * F.rec_bytes + kRecHeaderBytes);
+}
+
+__device__ __forceinline__ const Request *rec_reqs(const FinArgs &F, int r) {
+    return reinterpret_cast<const Request *>(F.recs + (int64_t)r * F.rec_bytes + kRecHeaderBytes +
+                                             (int64_t)F.kcap * 4);
+}
+
+// Global request q (ranks concatenated in rank order) -> its record entry.
+__device__ const Request *request_at(const FinArgs &F, const int *base, int q) {
+    int r = 0;
+    while (r + 1 < F.world && q >= base[r + 1]) ++r;
+    return rec_reqs(F, r) + (q - base[r]);
+}
+
+// Auxiliary draw m of (item i, epoch t) -> a slot: the G0 draw of normalinvwishart.h:44-64 in the
+// factored form (DESIGN.md "G0").
+__device__ void write_new_slot(const FinArgs &F, const Request &r, int s) {
+    const int D = F.D, DP = D * (D + 1) / 2, P = (D + 2) / 2;
+    double g0 = 0.0, g1 = 0.0, v = 0.0;
+    double xi[kMaxD];  // only D used
+    for (int k = 0; k <= D; ++k) {
+        if ((k & 1) == 0) normal_pair(F.seed, (uint64_t)r.i, F.t, kStreamAux, (uint32_t)(r.m * P + (k >> 1)), g0, g1);
+        const double g = (k & 1) ? g1 : g0;
+        if (k == 0)
+            v = fma(F.nu, g, (double)D);
+        else
+            xi[k - 1] = g;
+    }
+    const double sc = fabs(v) * F.rsk;
+    for (int a = 0; a < D; ++a) {
+        const double *LTa = F.LT + a * D;
+        double t0 = LTa[a] * xi[a];
+        for (int b = a + 1; b < D; ++b) t0 = fma(LTa[b], xi[b], t0);
+        F.slot_mu[(int64_t)s * D + a] = fma(sc, t0, F.mu0[a]);
+    }
+    const double v2 = v * v;
+    for (int k = 0; k < DP; ++k) F.slot_P[(int64_t)s * DP + k] = F.Gp[k] / v2;
+    F.slot_c[s] = fma(-(double)D, log(fabs(v)), F.caux);
+    for (int k = 0; k < D * D; ++k) F.slot_sigma[(int64_t)s * D * D + k] = v2 * F.LTL[k];
+}
+
+}  // namespace
+
+// One workgroup of 1024 threads.  Dynamic LDS: sort keys int64[kReqMax] | sort idx int[kReqMax] |
+// free slots int[kReqMax] | cnt int[kcap].
+__global__ __launch_bounds__(kFinThreads) void np8_finalize(FinArgs F) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    int64_t *keys = reinterpret_cast<int64_t *>(smem);
+    int *kidx = reinterpret_cast<int *>(smem + sizeof(int64_t) * kReqMax);
+    int *freeslot = kidx + kReqMax;
+    int *cnt_s = freeslot + kReqMax;
+    __shared__ int sh[32];
+    __shared__ int base[65];
+    __shared__ int s_flags[4];  // nreq, overflow, accept, free
+    const int tid = threadIdx.x;
+    const int kcap = F.kcap;
+    const int D = F.D, DP = D * (D + 1) / 2, CS = cand_stride(D);
+    const int per = (kcap + kFinThreads - 1) / kFinThreads;
+    const int s0 = min(kcap, tid * per), s1 = min(kcap, s0 + per);
+
+    if (tid == 0) {
+        int n = 0, of = 0;
+        for (int r = 0; r < F.world; ++r) {
+            const int nr = rec_header(F, r)->nreq;
+            of |= (nr > F.rec_cap);
+            base[r] = n;
+            n += min(nr, F.rec_cap);
+        }
+        base[F.world] = n;
+        s_flags[0] = n;
+        s_flags[1] = of;
+    }
+    for (int s = s0; s < s1; ++s) {
+        int c = F.cnt[s];
+        for (int r = 0; r < F.world; ++r) c += rec_delta(F, r)[s];
+        cnt_s[s] = c;
+    }
+    __syncthreads();
+    const int nreq = s_flags[0];
+    const bool try_accept = (nreq > 0) && (s_flags[1] == 0) && (nreq <= kReqMax);
+    if (try_accept) {  // block-uniform
+        for (int q = tid; q < nreq; q += kFinThreads) atomicSub(&cnt_s[request_at(F, base, q)->zold], 1);
+    }
+    __syncthreads();
+    int nf = 0;
+    for (int s = s0; s < s1; ++s) nf += (cnt_s[s] == 0);
+    int nfree;
+    int frank = block_excl_scan(nf, sh, &nfree);
+    const bool accept = try_accept && (nreq <= nfree);
+    if (try_accept && !accept) {
+        for (int q = tid; q < nreq; q += kFinThreads) atomicAdd(&cnt_s[request_at(F, base, q)->zold], 1);
+    }
+    if (tid == 0) {
+        if (nreq > 0 && !accept) {
+            F.ctl->err |= kErrCapacity;
+            F.ctl->n_rejected += (s_flags[1] ? (int64_t)nreq + 1 : (int64_t)nreq);
+        }
+        if (accept) F.ctl->n_new += nreq;
+    }
+    if (accept) {  // block-uniform
+        for (int s = s0; s < s1; ++s)
+            if (cnt_s[s] == 0) {
+                if (frank < nreq) freeslot[frank] = s;
+                ++frank;
+            }
+        int n2 = 1;
+        while (n2 < nreq) n2 <<= 1;
+        for (int q = tid; q < n2; q += kFinThreads) {
+            keys[q] = (q < nreq) ? request_at(F, base, q)->pos : INT64_MAX;
+            kidx[q] = q;
+        }
+        __syncthreads();
+        for (int k = 2; k <= n2; k <<= 1) {
+            for (int j = k >> 1; j > 0; j >>= 1) {
+                for (int q = tid; q < n2; q += kFinThreads) {
+                    const int l = q ^ j;
+                    if (l > q) {
+                        const bool up = ((q & k) == 0);
+                        const int64_t a = keys[q], b = keys[l];
+                        if ((a > b) == up) {
+                            keys[q] = b;
+                            keys[l] = a;
+                            const int t = kidx[q];
+                            kidx[q] = kidx[l];
+                            kidx[l] = t;
+                        }
+                    }
+                }
+                __syncthreads();
+            }
+        }
+        for (int q = tid; q < nreq; q += kFinThreads) {
+            const Request r = *request_at(F, base, kidx[q]);
+            const int s = freeslot[q];
+            write_new_slot(F, r, s);
+            cnt_s[s] = 1;
+            if (r.i >= F.offset && r.i < F.offset + F.n_loc) F.z[r.i - F.offset] = s;
+        }
+    }
+    __syncthreads();
+    // write counts back and rebuild the dense candidate table in ascending slot order
+    int nl = 0;
+    for (int s = s0; s < s1; ++s) nl += (cnt_s[s] > 0);
+    int nlive;
+    int k = block_excl_scan(nl, sh, &nlive);
+    for (int s = s0; s < s1; ++s) {
+        const int c = cnt_s[s];
+        F.cnt[s] = c;
+        if (c > 0) {
+            double *e = F.cand + (int64_t)k * CS;
+            for (int a = 0; a < D; ++a) e[a] = F.slot_mu[(int64_t)s * D + a];
+            for (int a = 0; a < DP; ++a) e[D + a] = F.slot_P[(int64_t)s * DP + a];
+            e[D + DP] = F.slot_c[s];
+            e[D + DP + 1] = log((double)c);
+            e[D + DP + 2] = (c > 1) ? log((double)(c - 1)) : -INFINITY;
+            e[D + DP + 3] = (double)s;
+            ++k;
+        }
+    }
+    if (tid == 0) F.ctl->K = nlive;
+    // clear the local record for the next step (all reads of it are behind the barriers above)
+    if (F.local_rec) {
+        int32_t *delta = reinterpret_cast<int32_t *>(F.local_rec + kRecHeaderBytes);
+        for (int s = tid; s < kcap; s += kFinThreads) delta[s] = 0;
+        if (tid == 0) reinterpret_cast<RecHeader *>(F.local_rec)->nreq = 0;
+    }
+}
+
+// ---- max likelihood --------------------------------------------------------------------------------
+template <int D>
+__global__ __launch_bounds__(256) void np8_loglik(LoglikArgs A) {
+    constexpr int DP = D * (D + 1) / 2;
+    __shared__ double red[256];
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    double ll = 0.0;
+    if (i < A.n_loc) {
+        const int s = A.z[i];
+        double x[D];
+#pragma unroll
+        for (int a = 0; a < D; ++a) x[a] = A.X[(int64_t)a * A.n_loc + i];
+        const double *mu = A.slot_mu + (int64_t)s * D;
+        const double *P = A.slot_P + (int64_t)s * DP;
+        double d[D];
+#pragma unroll
+        for (int a = 0; a < D; ++a) d[a] = x[a] - mu[a];
+        double q = 0.0;
+        int k = 0;
+#pragma unroll
+        for (int a = 0; a < D; ++a) {
+            double t = P[k++] * d[a];
+#pragma unroll
+            for (int b = a + 1; b < D; ++b) t = fma(P[k++], d[b], t);
+            q = fma(t, d[a], q);
+        }
+        ll = fma(-0.5, q, A.slot_c[s]);
+    }
+    red[threadIdx.x] = ll;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (threadIdx.x < o) red[threadIdx.x] = red[threadIdx.x] + red[threadIdx.x + o];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) A.partial[blockIdx.x] = red[0];
+}
+
+__global__ __launch_bounds__(1024) void np8_loglik_reduce(const double *__restrict__ partial, int64_t nb,
+                                                          double *__restrict__ out) {
+    __shared__ double red[1024];
+    double s = 0.0;
+    for (int64_t b = threadIdx.x; b < nb; b += blockDim.x) s = s + partial[b];
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int o = 512; o > 0; o >>= 1) {
+        if (threadIdx.x < o) red[threadIdx.x] = red[threadIdx.x] + red[threadIdx.x + o];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *out = red[0];
+}
+
+// Every block decides from (L, best[par]); block 0 publishes best[par^1].
+__global__ __launch_bounds__(256) void np8_snapshot(SnapArgs A) {
+    const double L = *A.L;
+    const double best = A.best[A.par];
+    const bool better = L > best;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        A.best[A.par ^ 1] = better ? L : best;
+        if (better) *A.have_best = 1;
+    }
+    if (!better) return;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < A.n_loc; i += stride)
+        A.z_best[i] = A.z[i];
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < A.kcap; k += stride) A.cnt_best[k] = A.cnt[k];
+    const int64_t nm = (int64_t)A.kcap * A.D, ns = (int64_t)A.kcap * A.D * A.D;
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < nm; k += stride) A.mu_best[k] = A.slot_mu[k];
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < ns; k += stride)
+        A.sigma_best[k] = A.slot_sigma[k];
+}
+
+// ---- parity/debug: log-likelihood matrix --------------------------------------------------------------
+template <int D, int M>
+__global__ __launch_bounds__(256) void np8_loglik_matrix_kernel(AssignArgs A, const int64_t *__restrict__ idx,
+                                                                int64_t n, double *__restrict__ out) {
+    constexpr int DP = D * (D + 1) / 2;
+    constexpr int CS = (D + DP + 4 + 1) & ~1;
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    const int64_t il = idx[r];
+    const uint64_t ig = (uint64_t)(A.offset + il);
+    double x[D];
+#pragma unroll
+    for (int a = 0; a < D; ++a) x[a] = A.X[(int64_t)a * A.n_loc + il];
+    const int K = A.ctl->K;
+    for (int j = 0; j < K; ++j) out[r * (K + M) + j] = cand_ll<D>(A.cand + (int64_t)j * CS, x);
+    double y0[D];
+    whiten<D>(A.hyp, x, y0);
+    for (int m = 0; m < M; ++m) out[r * (K + M) + K + m] = aux_ll<D>(A.hyp, y0, A.seed, ig, A.t, m);
+}
+
+// ---- dispatch ----------------------------------------------------------------------------------------
+#define NP8_FOR_EACH_DM(X) \
+    X(1, 1) X(1, 2) X(1, 3) X(1, 4) X(2, 1) X(2, 2) X(2, 3) X(2, 4) X(3, 1) X(3, 2) X(3, 3) X(3, 4) X(4, 1) \
+    X(4, 2) X(4, 3) X(4, 4) X(8, 1) X(8, 2) X(8, 3) X(8, 4) X(16, 1) X(16, 2) X(16, 3) X(16, 4)
+
+bool np8_supported(int D, int M) {
+#define X(d, m) \
+    if (D == d && M == m) return true;
+    NP8_FOR_EACH_DM(X)
+#undef X
+    return false;
+}
+
+hipError_t np8_launch_assign(const AssignArgs &A, int D, int M, hipStream_t s) {
+    const int64_t n = A.p1 - A.p0;
+    if (n <= 0) return hipSuccess;
+    const dim3 grid((unsigned)((n + 255) / 256)), block(256);
+#define X(d, m)                                                               \
+    if (D == d && M == m) {                                                   \
+        hipLaunchKernelGGL((np8_assign<d, m>), grid, block, 0, s, A);         \
+        return hipGetLastError();                                             \
+    }
+    NP8_FOR_EACH_DM(X)
+#undef X
+    return hipErrorInvalidValue;
+}
+
+hipError_t np8_launch_loglik_matrix(const AssignArgs &A, int D, int M, const int64_t *idx, int64_t n, double *out,
+                                    hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    const dim3 grid((unsigned)((n + 255) / 256)), block(256);
+#define X(d, m)                                                                              \
+    if (D == d && M == m) {                                                                  \
+        hipLaunchKernelGGL((np8_loglik_matrix_kernel<d, m>), grid, block, 0, s, A, idx, n, out); \
+        return hipGetLastError();                                                            \
+    }
+    NP8_FOR_EACH_DM(X)
+#undef X
+    return hipErrorInvalidValue;
+}
+
+size_t np8_finalize_lds_bytes(int kcap) {
+    return sizeof(int64_t) * kReqMax + sizeof(int) * kReqMax * 2 + sizeof(int) * (size_t)kcap;
+}
+
+hipError_t np8_launch_finalize(const FinArgs &F, hipStream_t s) {
+    hipLaunchKernelGGL(np8_finalize, dim3(1), dim3(kFinThreads), np8_finalize_lds_bytes(F.kcap), s, F);
+    return hipGetLastError();
+}
+
+hipError_t np8_launch_loglik(const LoglikArgs &A, int D, hipStream_t s) {
+    const int64_t nb = (A.n_loc + 255) / 256;
+    if (nb <= 0) return hipSuccess;
+    switch (D) {
+#define Y(d)                                                                       \
+    case d:                                                                        \
+        hipLaunchKernelGGL((np8_loglik<d>), dim3((unsigned)nb), dim3(256), 0, s, A); \
+        break;
+        Y(1) Y(2) Y(3) Y(4) Y(8) Y(16)
+#undef Y
+        default:
+            return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t np8_launch_loglik_reduce(const double *partial, int64_t nb, double *out, hipStream_t s) {
+    hipLaunchKernelGGL(np8_loglik_reduce, dim3(1), dim3(1024), 0, s, partial, nb, out);
+    return hipGetLastError();
+}
+
+hipError_t np8_launch_snapshot(const SnapArgs &A, hipStream_t s) {
+    int64_t n = A.n_loc > (int64_t)A.kcap * A.D * A.D ? A.n_loc : (int64_t)A.kcap * A.D * A.D;
+    int64_t nb = (n + 255) / 256;
+    if (nb > 2048) nb = 2048;
+    if (nb < 1) nb = 1;
+    hipLaunchKernelGGL(np8_snapshot, dim3((unsigned)nb), dim3(256), 0, s, A);
+    return hipGetLastError();
+}

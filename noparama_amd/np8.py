@@ -1,0 +1,314 @@
+"""ctypes binding of libnp8.so (include/np8.h) and the host-side mirror of noparama's sampler API.
+
+`NealAlgorithm8` mirrors the reference plug-in (include/np_neal_algorithm8.h:52-73 on
+include/np_update_cluster_population.h:13-44): the same constructor parameters (likelihood =
+multivariate normal of dimension D, nonparametrics = DP(alpha) with the NIW-like base measure of
+src/np_main.cpp:365-372) and `update(membertrix, data_ids)`/`printStatistics()`.  Sweep-granular
+entry points (`sweep`) are the MI355X path; `update` with a single id is the reference's exact
+per-point granularity.  There is no CPU fallback: if the HIP library is missing this module raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import re
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libnp8.so")
+HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "np8.h")
+
+NP8_OK = 0
+NP8_ERR_ARG = -1
+NP8_ERR_SIGMA = -2
+NP8_ERR_RANGE = -3
+NP8_ERR_CAPACITY = -4
+NP8_ERR_STATE = -5
+NP8_ERR_HIP = -6
+NP8_ERR_COMM = -7
+NP8_REQ_MAX = 4096
+
+_ERRNAMES = {
+    NP8_ERR_ARG: "NP8_ERR_ARG",
+    NP8_ERR_SIGMA: "NP8_ERR_SIGMA",
+    NP8_ERR_RANGE: "NP8_ERR_RANGE",
+    NP8_ERR_CAPACITY: "NP8_ERR_CAPACITY",
+    NP8_ERR_STATE: "NP8_ERR_STATE",
+    NP8_ERR_HIP: "NP8_ERR_HIP",
+    NP8_ERR_COMM: "NP8_ERR_COMM",
+}
+
+
+class NP8Error(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"{_ERRNAMES.get(code, code)}: {msg}")
+        self.code = code
+
+
+class _Config(C.Structure):
+    _fields_ = [
+        ("D", C.c_int32),
+        ("M", C.c_int32),
+        ("alpha", C.c_double),
+        ("mu0", C.POINTER(C.c_double)),
+        ("kappa", C.c_double),
+        ("nu", C.c_double),
+        ("Lambda", C.POINTER(C.c_double)),
+        ("seed", C.c_uint64),
+        ("kcap", C.c_int32),
+        ("chunk", C.c_int64),
+        ("device", C.c_int32),
+    ]
+
+
+class Stats(C.Structure):
+    _fields_ = [
+        ("K", C.c_int32),
+        ("epoch", C.c_uint32),
+        ("new_clusters", C.c_int64),
+        ("existing_picks", C.c_int64),
+        ("rejected_requests", C.c_int64),
+        ("best_loglik", C.c_double),
+        ("last_loglik", C.c_double),
+        ("ms_assign", C.c_double),
+        ("ms_finalize", C.c_double),
+        ("ms_loglik", C.c_double),
+    ]
+
+
+_lib = None
+
+
+def header_symbols():
+    """Entry points declared in include/np8.h."""
+    txt = open(HEADER_PATH).read()
+    return sorted(set(re.findall(r"^\s*(?:int|int64_t|const char \*)\s*(np8_\w+)\s*\(", txt, re.M)))
+
+
+def lib():
+    """Load the in-tree HIP library.  Raises (no fallback) when it has not been built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"libnp8.so not built ({LIB_PATH}); run __graft_entry__.build()")
+    L = C.CDLL(LIB_PATH)
+    vp, i32, i64, d = C.c_void_p, C.c_int32, C.c_int64, C.c_double
+    P = C.POINTER
+    sig = {
+        "np8_create": ([P(vp), P(_Config)], i32),
+        "np8_destroy": ([vp], i32),
+        "np8_last_error": ([vp], C.c_char_p),
+        "np8_set_data": ([vp, vp, i64, i32, i64, i64], i32),
+        "np8_set_state": ([vp, vp, i32, vp, vp], i32),
+        "np8_init_random": ([vp, i32], i32),
+        "np8_sweep": ([vp, i32], i32),
+        "np8_update_points": ([vp, vp, i64], i32),
+        "np8_end_sweep": ([vp], i32),
+        "np8_sync": ([vp], i32),
+        "np8_get_state": ([vp, i32, vp, vp, vp, vp, vp], i32),
+        "np8_loglik_matrix": ([vp, vp, i64, vp], i32),
+        "np8_total_loglik": ([vp, P(d)], i32),
+        "np8_stats": ([vp, P(Stats)], i32),
+        "np8_set_timing": ([vp, i32], i32),
+        "np8_set_stream": ([vp, vp], i32),
+        "np8_comm_unique_id": ([vp], i32),
+        "np8_comm_init": ([vp, vp, i32, i32], i32),
+        "np8_record_bytes": ([vp], i64),
+        "np8_step_local": ([vp, vp], i32),
+        "np8_step_merge": ([vp, vp, i32], i32),
+    }
+    for name, (args, res) in sig.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = res
+    _lib = L
+    return L
+
+
+def _p(a):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def comm_unique_id() -> bytes:
+    buf = (C.c_uint8 * 128)()
+    r = lib().np8_comm_unique_id(buf)
+    if r:
+        raise NP8Error(r, "ncclGetUniqueId failed")
+    return bytes(buf)
+
+
+class NealAlgorithm8:
+    """Neal Algorithm 8 on one MI355X (or one shard of a multi-GPU run).
+
+    Parameters follow the reference wiring (src/np_main.cpp:164,365-372,433-438): D (likelihood
+    dimension), M auxiliaries (np_neal_algorithm8.cpp:33), alpha (Suffies_Dirichlet), and the base
+    measure mu0, kappa, nu, Lambda.  `chunk` = points per synchronous step (0: whole sweep).
+    """
+
+    def __init__(self, D, M=3, alpha=1.0, mu0=None, kappa=1.0 / 500, nu=4.0, Lambda=None, seed=0, kcap=2048,
+                 chunk=0, device=-1):
+        self.D, self.M, self.kcap = int(D), int(M), int(kcap)
+        self._mu0 = np.ascontiguousarray(np.full(D, 6.0) if mu0 is None else mu0, dtype=np.float64)
+        self._Lam = np.ascontiguousarray(0.01 * np.eye(D) if Lambda is None else Lambda, dtype=np.float64)
+        cfg = _Config()
+        cfg.D, cfg.M, cfg.alpha = self.D, self.M, float(alpha)
+        cfg.mu0 = self._mu0.ctypes.data_as(C.POINTER(C.c_double))
+        cfg.kappa, cfg.nu = float(kappa), float(nu)
+        cfg.Lambda = self._Lam.ctypes.data_as(C.POINTER(C.c_double))
+        cfg.seed, cfg.kcap, cfg.chunk, cfg.device = int(seed), int(kcap), int(chunk), int(device)
+        h = C.c_void_p()
+        r = lib().np8_create(C.byref(h), C.byref(cfg))
+        if r:
+            raise NP8Error(r, "np8_create failed (unsupported D/M, bad base measure or no HIP device)")
+        self._h = h
+        self.N = 0
+        self._statistics_new = 0
+
+    # -- plumbing ------------------------------------------------------------------------------
+    def _check(self, r):
+        if r:
+            raise NP8Error(r, lib().np8_last_error(self._h).decode())
+
+    def close(self):
+        h = getattr(self, "_h", None)
+        if h:
+            lib().np8_destroy(h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- state ---------------------------------------------------------------------------------
+    def set_data(self, X, offset=0, n_global=None):
+        X = np.ascontiguousarray(X, dtype=np.float64)
+        if X.ndim != 2 or X.shape[1] != self.D:
+            raise ValueError("X must be [n, D]")
+        self.N = X.shape[0]
+        self._check(lib().np8_set_data(self._h, _p(X), self.N, self.D, int(offset),
+                                       int(self.N if n_global is None else n_global)))
+
+    def set_state(self, z, mu, sigma):
+        z = np.ascontiguousarray(z, dtype=np.int32)
+        mu = np.ascontiguousarray(mu, dtype=np.float64)
+        sigma = np.ascontiguousarray(sigma, dtype=np.float64)
+        self._check(lib().np8_set_state(self._h, _p(z), mu.shape[0], _p(mu), _p(sigma)))
+
+    def init_random(self, K=20):
+        self._check(lib().np8_init_random(self._h, int(K)))
+
+    def sweep(self, n=1, sync=True):
+        self._check(lib().np8_sweep(self._h, int(n)))
+        if sync:
+            self.sync()
+
+    def sync(self):
+        self._check(lib().np8_sync(self._h))
+
+    def update_points(self, ids):
+        ids = np.ascontiguousarray(ids, dtype=np.int64)
+        self._check(lib().np8_update_points(self._h, _p(ids), ids.size))
+
+    def end_sweep(self):
+        self._check(lib().np8_end_sweep(self._h))
+
+    def state(self, which=0, params=True):
+        z = np.zeros(max(self.N, 1), dtype=np.int32)
+        K = C.c_int32(0)
+        mu = np.zeros((self.kcap, self.D))
+        sg = np.zeros((self.kcap, self.D, self.D))
+        cnt = np.zeros(self.kcap, dtype=np.int64)
+        if params:
+            self._check(lib().np8_get_state(self._h, int(which), _p(z), C.byref(K), _p(mu), _p(sg), _p(cnt)))
+        else:
+            self._check(lib().np8_get_state(self._h, int(which), _p(z), C.byref(K), None, None, _p(cnt)))
+        k = K.value
+        return {"z": z[: self.N], "K": k, "mu": mu[:k], "sigma": sg[:k], "counts": cnt[:k]}
+
+    def stats(self):
+        s = Stats()
+        self._check(lib().np8_stats(self._h, C.byref(s)))
+        return {f: getattr(s, f) for f, _ in Stats._fields_}
+
+    @property
+    def K(self):
+        return self.stats()["K"]
+
+    def loglik_matrix(self, idx):
+        idx = np.ascontiguousarray(idx, dtype=np.int64)
+        K = self.K
+        out = np.zeros((idx.size, K + self.M))
+        self._check(lib().np8_loglik_matrix(self._h, _p(idx), idx.size, _p(out)))
+        return out
+
+    def total_loglik(self):
+        v = C.c_double(0.0)
+        self._check(lib().np8_total_loglik(self._h, C.byref(v)))
+        return v.value
+
+    def set_timing(self, on=True):
+        self._check(lib().np8_set_timing(self._h, 1 if on else 0))
+
+    # -- multi-rank ----------------------------------------------------------------------------
+    def comm_init(self, uid, rank, world):
+        if uid is None:
+            self._check(lib().np8_comm_init(self._h, None, int(rank), int(world)))
+        else:
+            buf = (C.c_uint8 * 128).from_buffer_copy(uid)
+            self._check(lib().np8_comm_init(self._h, buf, int(rank), int(world)))
+
+    def record_bytes(self):
+        return int(lib().np8_record_bytes(self._h))
+
+    def step_local(self):
+        rec = np.zeros(self.record_bytes(), dtype=np.uint8)
+        self._check(lib().np8_step_local(self._h, _p(rec)))
+        return rec
+
+    def step_merge(self, records, world):
+        records = np.ascontiguousarray(records, dtype=np.uint8)
+        self._check(lib().np8_step_merge(self._h, _p(records), int(world)))
+
+    # -- reference plug-in interface (np_update_cluster_population.h:35-43) --------------------
+    def update(self, cluster_matrix, data_ids):
+        """UpdateClusterPopulation::update.  A full permutation of the items runs one data-parallel
+        sweep; a single id runs the exact sequential step of NealAlgorithm8::update."""
+        ids = np.asarray(data_ids, dtype=np.int64).reshape(-1)
+        if ids.size == self.N and self.N > 0 and np.array_equal(np.sort(ids), np.arange(self.N)):
+            self.sweep(1)
+        else:
+            self.update_points(ids)
+        if cluster_matrix is not None:
+            cluster_matrix.load(self.state(params=False))
+
+    def printStatistics(self):
+        s = self.stats()
+        print("Statistics:")
+        print(f" # of new cluster events accepted: {s['new_clusters']}")
+        print(f" # of rejected new-cluster requests: {s['rejected_requests']}")
+
+
+class membertrix:
+    """Host view of the membership state (reference include/membertrix.h:52-313), kept as labels and
+    counts instead of the dense N x C bool matrix (membertrix.h:30)."""
+
+    def __init__(self):
+        self.z = np.zeros(0, dtype=np.int32)
+        self.counts = np.zeros(0, dtype=np.int64)
+
+    def load(self, st):
+        self.z = np.asarray(st["z"], dtype=np.int32).copy()
+        self.counts = np.asarray(st["counts"], dtype=np.int64).copy()
+
+    def count(self, cluster_id=None):
+        return int(self.z.size if cluster_id is None else self.counts[cluster_id])
+
+    def getClusterId(self, data_id):
+        return int(self.z[data_id])
+
+    def getClusterCount(self):
+        return int((self.counts > 0).sum())

@@ -1,0 +1,892 @@
+/*
+ * np8_oracle.c -- TEST INFRASTRUCTURE ONLY (see np8_oracle.h).  CPU restatement of noparama's
+ * Neal-8 sweep.  Compiled with -O2 -ffp-contract=off so that every fused multiply-add is the
+ * explicit fma() written here, exactly as in the HIP kernels (DESIGN.md "Chain specification").
+ */
+#include "np8_oracle.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define LOG2PI 1.8378770664093454835606594728112
+#define TWO_PI 6.283185307179586476925286766559
+
+/* ================================================================================================
+ * Primitives
+ * ============================================================================================== */
+
+static inline uint32_t mulhi32(uint32_t a, uint32_t b) { return (uint32_t)(((uint64_t)a * b) >> 32); }
+
+/* Philox4x32-10 (Salmon et al., SC'11; Random123 philox4x32round / philox4x32bumpkey). */
+void np8o_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
+    uint32_t c0 = ctr[0], c1 = ctr[1], c2 = ctr[2], c3 = ctr[3];
+    uint32_t k0 = key[0], k1 = key[1];
+    for (int r = 0; r < 10; ++r) {
+        if (r) {
+            k0 += 0x9E3779B9u;
+            k1 += 0xBB67AE85u;
+        }
+        uint32_t hi0 = mulhi32(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
+        uint32_t hi1 = mulhi32(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+        c0 = hi1 ^ c1 ^ k0;
+        c1 = lo1;
+        c2 = hi0 ^ c3 ^ k1;
+        c3 = lo0;
+    }
+    out[0] = c0;
+    out[1] = c1;
+    out[2] = c2;
+    out[3] = c3;
+}
+
+/* Open-interval uniform from 64 random bits: an odd 53-bit integer times 2^-53, never 0 or 1. */
+double np8o_u01(uint32_t hi, uint32_t lo) {
+    uint64_t v = (((uint64_t)hi << 32) | lo) >> 11;
+    v |= 1u;
+    return (double)v * 0x1.0p-53;
+}
+
+static void philox_call(uint64_t seed, uint64_t i, uint32_t t, uint32_t stream, uint32_t call, uint32_t out[4]) {
+    uint32_t ctr[4] = {(uint32_t)i, (uint32_t)(i >> 32), t, (stream << 24) | (call & 0xFFFFFFu)};
+    uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+    np8o_philox4x32_10(ctr, key, out);
+}
+
+/* Box-Muller pair from one Philox call: (r cos th, r sin th). */
+static void normal_pair(uint64_t seed, uint64_t i, uint32_t t, uint32_t stream, uint32_t call, double g[2]) {
+    uint32_t o[4];
+    philox_call(seed, i, t, stream, call, o);
+    double u1 = np8o_u01(o[0], o[1]);
+    double u2 = np8o_u01(o[2], o[3]);
+    double r = sqrt(-2.0 * log(u1));
+    double th = TWO_PI * u2;
+    g[0] = r * cos(th);
+    g[1] = r * sin(th);
+}
+
+double np8o_normal(uint64_t seed, uint64_t i, uint32_t t, uint32_t stream, uint32_t n) {
+    double g[2];
+    normal_pair(seed, i, t, stream, n >> 1, g);
+    return g[n & 1];
+}
+
+double np8o_uniform(uint64_t seed, uint64_t i, uint32_t t, uint32_t stream, uint32_t n) {
+    uint32_t o[4];
+    philox_call(seed, i, t, stream, n, o);
+    return np8o_u01(o[0], o[1]);
+}
+
+static inline uint32_t fmix32(uint32_t h) {
+    h ^= h >> 16;
+    h *= 0x85EBCA6Bu;
+    h ^= h >> 13;
+    h *= 0xC2B2AE35u;
+    h ^= h >> 16;
+    return h;
+}
+
+/* Scan order of a chunked sweep (replaces dim1algebra.hpp:2066-2073 random_order): a keyed 4-round
+ * Feistel bijection on [0,2^b), cycle-walked into [0,N). */
+uint32_t np8o_perm(uint64_t seed, uint32_t t, uint32_t N, uint32_t p) {
+    if (N <= 1) return 0;
+    int b = 0;
+    while ((1ull << b) < (uint64_t)N) ++b;
+    if (b < 2) b = 2;
+    if (b & 1) ++b;
+    const int h = b / 2;
+    const uint32_t mask = (h >= 32) ? 0xFFFFFFFFu : ((1u << h) - 1u);
+    uint32_t k[4];
+    for (int r = 0; r < 4; ++r)
+        k[r] = fmix32((uint32_t)seed ^ fmix32(t * 4u + (uint32_t)r + 0x9E3779B9u)) ^ (uint32_t)(seed >> 32);
+    uint32_t x = p;
+    do {
+        uint32_t L = x >> h, R = x & mask;
+        for (int r = 0; r < 4; ++r) {
+            uint32_t nl = R;
+            R = L ^ (fmix32(R ^ k[r]) & mask);
+            L = nl;
+        }
+        x = (L << h) | R;
+    } while (x >= N);
+    return x;
+}
+
+/* ================================================================================================
+ * Faithful reference restatements
+ * ============================================================================================== */
+
+/* LU with partial pivoting, row-major; Eigen's PartialPivLU is what MatrixXd::inverse() and
+ * ::determinant() use for dynamic sizes (multivariatenormal.cpp:87,90). */
+int np8o_lu_inverse_det(const double *A, int D, double *inv, double *det) {
+    double LU[NP8O_DMAX * NP8O_DMAX];
+    int perm[NP8O_DMAX];
+    int sign = 1;
+    memcpy(LU, A, sizeof(double) * D * D);
+    for (int i = 0; i < D; ++i) perm[i] = i;
+    for (int k = 0; k < D; ++k) {
+        int p = k;
+        double best = fabs(LU[k * D + k]);
+        for (int i = k + 1; i < D; ++i)
+            if (fabs(LU[i * D + k]) > best) {
+                best = fabs(LU[i * D + k]);
+                p = i;
+            }
+        if (best == 0.0) {
+            if (det) *det = 0.0;
+            return -1;
+        }
+        if (p != k) {
+            for (int j = 0; j < D; ++j) {
+                double tmp = LU[k * D + j];
+                LU[k * D + j] = LU[p * D + j];
+                LU[p * D + j] = tmp;
+            }
+            int tp = perm[k];
+            perm[k] = perm[p];
+            perm[p] = tp;
+            sign = -sign;
+        }
+        for (int i = k + 1; i < D; ++i) {
+            double f = LU[i * D + k] / LU[k * D + k];
+            LU[i * D + k] = f;
+            for (int j = k + 1; j < D; ++j) LU[i * D + j] = LU[i * D + j] - f * LU[k * D + j];
+        }
+    }
+    if (det) {
+        double d = (double)sign;
+        for (int k = 0; k < D; ++k) d *= LU[k * D + k];
+        *det = d;
+    }
+    if (inv) {
+        /* Solve LU X = P I column by column. */
+        for (int c = 0; c < D; ++c) {
+            double y[NP8O_DMAX];
+            for (int i = 0; i < D; ++i) {
+                double s = (perm[i] == c) ? 1.0 : 0.0;
+                for (int j = 0; j < i; ++j) s -= LU[i * D + j] * y[j];
+                y[i] = s;
+            }
+            for (int i = D - 1; i >= 0; --i) {
+                double s = y[i];
+                for (int j = i + 1; j < D; ++j) s -= LU[i * D + j] * y[j];
+                y[i] = s / LU[i * D + i];
+            }
+            for (int i = 0; i < D; ++i) inv[i * D + c] = y[i];
+        }
+    }
+    return 0;
+}
+
+/* exponent = -0.5 * diff' * inverse * diff, evaluated left to right like Eigen's product chain. */
+static double ref_exponent(const double *x, const double *mu, const double *inv, int D) {
+    double d[NP8O_DMAX], r[NP8O_DMAX];
+    for (int a = 0; a < D; ++a) d[a] = x[a] - mu[a];
+    for (int b = 0; b < D; ++b) {
+        double s = 0.0;
+        for (int a = 0; a < D; ++a) s += (-0.5 * d[a]) * inv[a * D + b];
+        r[b] = s;
+    }
+    double e = 0.0;
+    for (int b = 0; b < D; ++b) e += r[b] * d[b];
+    return e;
+}
+
+/* src/statistics/multivariatenormal.cpp:82-93 */
+double np8o_mvn_probability_ref(const double *x, const double *mu, const double *Sigma, int D) {
+    double inv[NP8O_DMAX * NP8O_DMAX], det;
+    np8o_lu_inverse_det(Sigma, D, inv, &det);
+    double exponent = ref_exponent(x, mu, inv, D);
+    double constant = sqrt(pow(TWO_PI, D) * det);
+    return exp(exponent) / constant;
+}
+
+/* src/statistics/multivariatenormal.cpp:124-135 */
+double np8o_mvn_logprobability_ref(const double *x, const double *mu, const double *Sigma, int D) {
+    double inv[NP8O_DMAX * NP8O_DMAX], det;
+    np8o_lu_inverse_det(Sigma, D, inv, &det);
+    double exponent = ref_exponent(x, mu, inv, D);
+    double constant = sqrt(pow(TWO_PI, D) * det);
+    return exponent - log(constant);
+}
+
+/* include/helper/dim1algebra.hpp:2078-2104: partial_sum, u*cumsum.back(), lower_bound. */
+int64_t np8o_weighted_pick_ref(const double *w, int64_t n, double u) {
+    if (n <= 0) return 0;
+    double *cs = (double *)malloc(sizeof(double) * n);
+    double acc = 0.0;
+    for (int64_t j = 0; j < n; ++j) {
+        acc += w[j];
+        cs[j] = acc;
+    }
+    double target = u * cs[n - 1];
+    int64_t lo = 0, len = n; /* std::lower_bound: first element not less than target */
+    while (len > 0) {
+        int64_t half = len / 2;
+        if (cs[lo + half] < target) {
+            lo += half + 1;
+            len -= half + 1;
+        } else {
+            len = half;
+        }
+    }
+    free(cs);
+    return lo;
+}
+
+/* src/clustering_performance.cpp:14-82, with a,b,c,N in int64 (the reference's int overflows past
+ * a few hundred points).  Degenerate ARI (reference returns early) -> NaN. */
+void np8o_similarity(const int32_t *truth, const int32_t *result, int64_t n, double out[3]) {
+    out[0] = out[1] = out[2] = NAN;
+    if (n <= 0) return;
+    int32_t ga = 0, gb = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        if (truth[i] > ga) ga = truth[i];
+        if (result[i] > gb) gb = result[i];
+    }
+    int64_t A = (int64_t)ga + 1, B = (int64_t)gb + 1;
+    int64_t *F = (int64_t *)calloc((size_t)(A * B), sizeof(int64_t));
+    for (int64_t i = 0; i < n; ++i) F[(int64_t)truth[i] * B + result[i]] += 1;
+    int64_t N = n;
+    int64_t purity_sum = 0;
+    for (int64_t c = 0; c < B; ++c) {
+        int64_t m = 0;
+        for (int64_t r = 0; r < A; ++r)
+            if (F[r * B + c] > m) m = F[r * B + c];
+        purity_sum += m;
+    }
+    out[0] = (double)purity_sum / (double)N;
+    int64_t a = 0, b = 0, c = 0;
+    for (int64_t r = 0; r < A; ++r) {
+        int64_t rs = 0;
+        for (int64_t cc = 0; cc < B; ++cc) {
+            int64_t f = F[r * B + cc];
+            a += (f * f - f) / 2;
+            rs += f;
+        }
+        b += (rs * rs - rs) / 2;
+    }
+    for (int64_t cc = 0; cc < B; ++cc) {
+        int64_t cs = 0;
+        for (int64_t r = 0; r < A; ++r) cs += F[r * B + cc];
+        c += (cs * cs - cs) / 2;
+    }
+    free(F);
+    double S = ((double)N * (double)N - (double)N) / 2.0;
+    if (S == 0.0) return;
+    out[1] = (double)(2 * a - b - c) / S + 1.0;
+    double bc_S = (double)b * (double)c / S;
+    double bpc_2 = (double)(b + c) / 2.0;
+    if (bc_S == bpc_2) return;
+    out[2] = ((double)a - bc_S) / (bpc_2 - bc_S);
+}
+
+/* ================================================================================================
+ * The chain
+ * ============================================================================================== */
+
+struct np8o_ctx {
+    np8o_config cfg;
+    int D, M, DP, kcap;
+    /* G0 precomputes (DESIGN.md "G0"): L = chol(Lambda) lower. */
+    double LT[NP8O_DMAX * NP8O_DMAX];    /* L^T (upper), row-major */
+    double UinvT[NP8O_DMAX * NP8O_DMAX]; /* (L^T)^{-1} (upper) */
+    double Gp[NP8O_DMAX * NP8O_DMAX];    /* (L^T L)^{-1}, off-diagonals doubled (upper used) */
+    double LTL[NP8O_DMAX * NP8O_DMAX];   /* L^T L */
+    double caux, rsk, logam;
+    /* data */
+    int64_t N;
+    double *X; /* N x D row-major */
+    int32_t *z;
+    /* slots */
+    double *slot_mu, *slot_P, *slot_c, *slot_sigma;
+    int32_t *cnt;
+    /* dense candidate table (ascending slot order) */
+    int32_t K;
+    int32_t *live;
+    double *logn, *logn1;
+    uint32_t t;
+    /* max likelihood (np_mcmc.cpp:187-203) */
+    double best_L;
+    int have_best;
+    int32_t *z_best, *cnt_best;
+    double *mu_best, *sigma_best;
+    /* scratch for the sequential driver */
+    int32_t *delta;
+    int64_t *rq_pos, *rq_i;
+    int32_t *rq_m, *rq_zold;
+};
+
+static int packed_index(int D, int a, int b) { /* upper triangle, row-major, a <= b */
+    return a * D - (a * (a - 1)) / 2 + (b - a);
+}
+
+np8o_ctx *np8o_create(const np8o_config *cfg) {
+    if (cfg->D < 1 || cfg->D > NP8O_DMAX || cfg->M < 1 || cfg->M > NP8O_MMAX || cfg->kcap < 1) return NULL;
+    np8o_ctx *c = (np8o_ctx *)calloc(1, sizeof(np8o_ctx));
+    c->cfg = *cfg;
+    const int D = cfg->D;
+    c->D = D;
+    c->M = cfg->M;
+    c->DP = D * (D + 1) / 2;
+    c->kcap = cfg->kcap;
+    /* Cholesky of Lambda (invwishart.h:40 uses Lambda.llt().matrixL()). */
+    double L[NP8O_DMAX * NP8O_DMAX];
+    memset(L, 0, sizeof(L));
+    for (int j = 0; j < D; ++j) {
+        double s = cfg->Lambda[j * D + j];
+        for (int k = 0; k < j; ++k) s -= L[j * D + k] * L[j * D + k];
+        if (!(s > 0.0)) {
+            free(c);
+            return NULL;
+        }
+        L[j * D + j] = sqrt(s);
+        for (int i = j + 1; i < D; ++i) {
+            double v = cfg->Lambda[i * D + j];
+            for (int k = 0; k < j; ++k) v -= L[i * D + k] * L[j * D + k];
+            L[i * D + j] = v / L[j * D + j];
+        }
+    }
+    for (int a = 0; a < D; ++a)
+        for (int b = 0; b < D; ++b) c->LT[a * D + b] = L[b * D + a];
+    /* (L^T)^{-1}: invert the upper-triangular L^T by back substitution. */
+    memset(c->UinvT, 0, sizeof(c->UinvT));
+    for (int col = 0; col < D; ++col)
+        for (int i = col; i >= 0; --i) {
+            double s = (i == col) ? 1.0 : 0.0;
+            for (int j = i + 1; j <= col; ++j) s -= c->LT[i * D + j] * c->UinvT[j * D + col];
+            c->UinvT[i * D + col] = s / c->LT[i * D + i];
+        }
+    /* L^T L and its inverse (L^T L)^{-1} = UinvT * UinvT^T. */
+    for (int a = 0; a < D; ++a)
+        for (int b = 0; b < D; ++b) {
+            double s = 0.0, g = 0.0;
+            for (int k = 0; k < D; ++k) {
+                s += L[k * D + a] * L[k * D + b];
+                g += c->UinvT[a * D + k] * c->UinvT[b * D + k];
+            }
+            c->LTL[a * D + b] = s;
+            c->Gp[a * D + b] = (a == b) ? g : 2.0 * g;
+        }
+    double sumlog = 0.0;
+    for (int a = 0; a < D; ++a) sumlog += log(L[a * D + a]);
+    c->caux = -0.5 * (double)D * LOG2PI - sumlog;
+    c->rsk = 1.0 / sqrt(cfg->kappa);
+    c->logam = log(cfg->alpha / (double)cfg->M);
+    const int K = c->kcap;
+    c->slot_mu = (double *)calloc((size_t)K * D, sizeof(double));
+    c->slot_P = (double *)calloc((size_t)K * c->DP, sizeof(double));
+    c->slot_c = (double *)calloc((size_t)K, sizeof(double));
+    c->slot_sigma = (double *)calloc((size_t)K * D * D, sizeof(double));
+    c->cnt = (int32_t *)calloc((size_t)K, sizeof(int32_t));
+    c->live = (int32_t *)calloc((size_t)K, sizeof(int32_t));
+    c->logn = (double *)calloc((size_t)K, sizeof(double));
+    c->logn1 = (double *)calloc((size_t)K, sizeof(double));
+    c->cnt_best = (int32_t *)calloc((size_t)K, sizeof(int32_t));
+    c->mu_best = (double *)calloc((size_t)K * D, sizeof(double));
+    c->sigma_best = (double *)calloc((size_t)K * D * D, sizeof(double));
+    c->delta = (int32_t *)calloc((size_t)K, sizeof(int32_t));
+    c->best_L = -INFINITY;
+    return c;
+}
+
+void np8o_destroy(np8o_ctx *c) {
+    if (!c) return;
+    free(c->X);
+    free(c->z);
+    free(c->z_best);
+    free(c->slot_mu);
+    free(c->slot_P);
+    free(c->slot_c);
+    free(c->slot_sigma);
+    free(c->cnt);
+    free(c->live);
+    free(c->logn);
+    free(c->logn1);
+    free(c->cnt_best);
+    free(c->mu_best);
+    free(c->sigma_best);
+    free(c->delta);
+    free(c->rq_pos);
+    free(c->rq_i);
+    free(c->rq_m);
+    free(c->rq_zold);
+    free(c);
+}
+
+int np8o_set_data(np8o_ctx *c, const double *X, int64_t N) {
+    free(c->X);
+    free(c->z);
+    free(c->z_best);
+    free(c->rq_pos);
+    free(c->rq_i);
+    free(c->rq_m);
+    free(c->rq_zold);
+    c->N = N;
+    c->X = (double *)malloc(sizeof(double) * (size_t)(N > 0 ? N : 1) * c->D);
+    if (N > 0) memcpy(c->X, X, sizeof(double) * (size_t)N * c->D);
+    c->z = (int32_t *)calloc((size_t)(N > 0 ? N : 1), sizeof(int32_t));
+    c->z_best = (int32_t *)calloc((size_t)(N > 0 ? N : 1), sizeof(int32_t));
+    c->rq_pos = (int64_t *)malloc(sizeof(int64_t) * (size_t)(N > 0 ? N : 1));
+    c->rq_i = (int64_t *)malloc(sizeof(int64_t) * (size_t)(N > 0 ? N : 1));
+    c->rq_m = (int32_t *)malloc(sizeof(int32_t) * (size_t)(N > 0 ? N : 1));
+    c->rq_zold = (int32_t *)malloc(sizeof(int32_t) * (size_t)(N > 0 ? N : 1));
+    return 0;
+}
+
+/* Table entry from an explicit covariance: P' = sym(LU-inverse) with doubled off-diagonals,
+ * c = -0.5 (D log 2pi + log det). */
+static int slot_from_sigma(np8o_ctx *c, int s, const double *mu, const double *Sigma) {
+    const int D = c->D;
+    double inv[NP8O_DMAX * NP8O_DMAX], det;
+    if (np8o_lu_inverse_det(Sigma, D, inv, &det) != 0 || !(det > 0.0)) return -2;
+    memcpy(c->slot_mu + (size_t)s * D, mu, sizeof(double) * D);
+    memcpy(c->slot_sigma + (size_t)s * D * D, Sigma, sizeof(double) * D * D);
+    double *P = c->slot_P + (size_t)s * c->DP;
+    for (int a = 0; a < D; ++a)
+        for (int b = a; b < D; ++b)
+            P[packed_index(D, a, b)] = (a == b) ? inv[a * D + a] : inv[a * D + b] + inv[b * D + a];
+    c->slot_c[s] = -0.5 * ((double)D * LOG2PI + log(det));
+    return 0;
+}
+
+/* G0 draw from scale normal g0 and xi (normalinvwishart.h:44-64, invwishart.h:34-46):
+ * v = D + nu g0, Sigma = v^2 L^T L, mu = mu0 + (|v|/sqrt(kappa)) L^T xi. */
+static void aux_from_normals(const np8o_ctx *c, double g0, const double *xi, double *v_out, double *mu) {
+    const int D = c->D;
+    double v = fma(c->cfg.nu, g0, (double)D);
+    double s = fabs(v) * c->rsk;
+    for (int a = 0; a < D; ++a) {
+        double t = c->LT[a * D + a] * xi[a];
+        for (int b = a + 1; b < D; ++b) t = fma(c->LT[a * D + b], xi[b], t);
+        mu[a] = fma(s, t, c->cfg.mu0[a]);
+    }
+    *v_out = v;
+}
+
+static void slot_from_aux(np8o_ctx *c, int s, double v, const double *mu) {
+    const int D = c->D;
+    memcpy(c->slot_mu + (size_t)s * D, mu, sizeof(double) * D);
+    double v2 = v * v;
+    double *P = c->slot_P + (size_t)s * c->DP;
+    for (int a = 0; a < D; ++a)
+        for (int b = a; b < D; ++b) P[packed_index(D, a, b)] = c->Gp[a * D + b] / v2;
+    c->slot_c[s] = fma(-(double)D, log(fabs(v)), c->caux);
+    double *S = c->slot_sigma + (size_t)s * D * D;
+    for (int k = 0; k < D * D; ++k) S[k] = v2 * c->LTL[k];
+}
+
+/* Normals of auxiliary draw m of (item i, epoch t): Philox calls m*P .. m*P+P-1 of stream AUX,
+ * P = ceil((D+1)/2); g[0] scales, g[1..D] is xi. */
+static void aux_normals(const np8o_ctx *c, uint64_t i, uint32_t t, int m, double *g /* >= D+2 */) {
+    const int D = c->D, P = (D + 2) / 2;
+    for (int k = 0; k < P; ++k) normal_pair(c->cfg.seed, i, t, NP8O_STREAM_AUX, (uint32_t)(m * P + k), g + 2 * k);
+}
+
+static void aux_draws(const np8o_ctx *c, uint64_t i, uint32_t t, double *v, double *mu /* M*D */) {
+    for (int m = 0; m < c->M; ++m) {
+        double g[NP8O_DMAX + 2];
+        aux_normals(c, i, t, m, g);
+        aux_from_normals(c, g[0], g + 1, v + m, mu + m * c->D);
+    }
+}
+
+static void rebuild_dense(np8o_ctx *c) {
+    int K = 0;
+    for (int s = 0; s < c->kcap; ++s)
+        if (c->cnt[s] > 0) {
+            c->live[K] = s;
+            c->logn[K] = log((double)c->cnt[s]);
+            c->logn1[K] = (c->cnt[s] > 1) ? log((double)(c->cnt[s] - 1)) : -INFINITY;
+            ++K;
+        }
+    c->K = K;
+}
+
+int np8o_set_state(np8o_ctx *c, const int32_t *z, int32_t K, const double *mu, const double *Sigma) {
+    if (K > c->kcap || K < 0) return -1;
+    memset(c->cnt, 0, sizeof(int32_t) * c->kcap);
+    for (int k = 0; k < K; ++k)
+        if (slot_from_sigma(c, k, mu + (size_t)k * c->D, Sigma + (size_t)k * c->D * c->D) != 0) return -2;
+    for (int64_t i = 0; i < c->N; ++i) {
+        if (z[i] < 0 || z[i] >= K) return -3;
+        c->z[i] = z[i];
+        c->cnt[z[i]]++;
+    }
+    rebuild_dense(c);
+    c->t = 0;
+    c->have_best = 0;
+    c->best_L = -INFINITY;
+    return 0;
+}
+
+/* np_mcmc.cpp:49-92 + np_init_clusters.cpp:24-40: K_init G0 clusters, uniform assignment, cleanup. */
+int np8o_init_random(np8o_ctx *c, int32_t K_init) {
+    if (K_init < 1) return -1;
+    const int D = c->D;
+    if (K_init > c->kcap) return -1;
+    double *mu = (double *)malloc(sizeof(double) * (size_t)K_init * D);
+    double *vv = (double *)malloc(sizeof(double) * (size_t)K_init);
+    int32_t *cntk = (int32_t *)calloc((size_t)K_init, sizeof(int32_t));
+    for (int k = 0; k < K_init; ++k) {
+        double g[NP8O_DMAX + 2];
+        for (int call = 0; call < (D + 2) / 2; ++call)
+            normal_pair(c->cfg.seed, (uint64_t)k, 0xFFFFFFFFu, NP8O_STREAM_INIT_THETA, (uint32_t)call, g + 2 * call);
+        aux_from_normals(c, g[0], g + 1, vv + k, mu + (size_t)k * D);
+    }
+    for (int64_t i = 0; i < c->N; ++i) {
+        double u = np8o_uniform(c->cfg.seed, (uint64_t)i, 0xFFFFFFFFu, NP8O_STREAM_INIT_Z, 0);
+        int k = (int)(u * (double)K_init);
+        if (k >= K_init) k = K_init - 1;
+        c->z[i] = k;
+        cntk[k]++;
+    }
+    /* cleanup (membertrix.cpp:343-364): drop empty clusters, keep ascending order */
+    int32_t *remap = (int32_t *)malloc(sizeof(int32_t) * (size_t)K_init);
+    int s = 0;
+    memset(c->cnt, 0, sizeof(int32_t) * c->kcap);
+    for (int k = 0; k < K_init; ++k) {
+        if (cntk[k] > 0) {
+            remap[k] = s;
+            slot_from_aux(c, s, vv[k], mu + (size_t)k * D);
+            c->cnt[s] = cntk[k];
+            ++s;
+        } else {
+            remap[k] = -1;
+        }
+    }
+    for (int64_t i = 0; i < c->N; ++i) c->z[i] = remap[c->z[i]];
+    free(remap);
+    free(mu);
+    free(vv);
+    free(cntk);
+    rebuild_dense(c);
+    c->t = 0;
+    c->have_best = 0;
+    c->best_L = -INFINITY;
+    return 0;
+}
+
+static inline double quad_form(const np8o_ctx *c, const double *x, const double *mu, const double *P) {
+    const int D = c->D;
+    double d[NP8O_DMAX];
+    for (int a = 0; a < D; ++a) d[a] = x[a] - mu[a];
+    double q = 0.0;
+    int k = 0;
+    for (int a = 0; a < D; ++a) {
+        double t = P[k++] * d[a];
+        for (int b = a + 1; b < D; ++b) t = fma(P[k++], d[b], t);
+        q = fma(t, d[a], q);
+    }
+    return q;
+}
+
+/* ll of point x under slot s, table form. */
+static inline double slot_ll(const np8o_ctx *c, const double *x, int s) {
+    double q = quad_form(c, x, c->slot_mu + (size_t)s * c->D, c->slot_P + (size_t)s * c->DP);
+    return fma(-0.5, q, c->slot_c[s]);
+}
+
+/* ll of point x under its M auxiliary draws, factored form (DESIGN.md "G0"). */
+static void aux_ll(const np8o_ctx *c, const double *x, uint64_t i, uint32_t t, double *ll /* M */) {
+    const int D = c->D, M = c->M;
+    double y0[NP8O_DMAX], dx[NP8O_DMAX];
+    for (int a = 0; a < D; ++a) dx[a] = x[a] - c->cfg.mu0[a];
+    for (int a = 0; a < D; ++a) {
+        double t0 = c->UinvT[a * D + a] * dx[a];
+        for (int b = a + 1; b < D; ++b) t0 = fma(c->UinvT[a * D + b], dx[b], t0);
+        y0[a] = t0;
+    }
+    for (int m = 0; m < M; ++m) {
+        double g[NP8O_DMAX + 2];
+        aux_normals(c, i, t, m, g);
+        const double *xi = g + 1;
+        double v = fma(c->cfg.nu, g[0], (double)D);
+        double s = fabs(v) * c->rsk;
+        double r2 = 0.0;
+        for (int a = 0; a < D; ++a) {
+            double e = fma(-s, xi[a], y0[a]);
+            r2 = fma(e, e, r2);
+        }
+        double q = r2 / (v * v);
+        double cm = fma(-(double)D, log(fabs(v)), c->caux);
+        ll[m] = fma(-0.5, q, cm);
+    }
+}
+
+/* ---- categorical draw: single-uniform weighted reservoir (DESIGN.md "Pick") ------------------
+ * Equal in distribution to dim1algebra.hpp:2078-2104 (inverse CDF over the linear weights) but one
+ * pass: state (Tm, S, u) with S = sum of exp(l_j - Tm) so far and u ~ U(0,1) independent of the
+ * current pick; candidate j replaces the pick with probability w_j / S_new and u is renormalised
+ * into the chosen sub-interval. */
+typedef struct {
+    double Tm, S, u;
+    int32_t pick;
+} pick_state;
+
+static inline double clamp_u(double u) {
+    if (u < 0x1.0p-60) u = 0x1.0p-60;
+    if (u > 0x1.fffffffffffffp-1) u = 0x1.fffffffffffffp-1;
+    return u;
+}
+
+static inline void pick_step(pick_state *st, double l, int32_t j) {
+    if (l == -INFINITY) return;
+    const int gt = l > st->Tm;
+    const double e = exp(gt ? (st->Tm - l) : (l - st->Tm));
+    const double a = gt ? 1.0 : e;
+    const double S = gt ? fma(st->S, e, 1.0) : st->S + e;
+    const double uS = st->u * S;
+    const int take = uS < a;
+    const double num = take ? uS : uS - a;
+    const double den = take ? a : S - a;
+    st->u = clamp_u(num / den);
+    if (take) st->pick = j;
+    if (gt) st->Tm = l;
+    st->S = S;
+}
+
+/* One Neal-8 step for point i against the frozen candidate table (np_neal_algorithm8.cpp:60-130):
+ * existing clusters in ascending slot order with weight n_{-i,k}, then the M auxiliaries with
+ * weight alpha/M.  Returns the candidate index (< K existing, >= K auxiliary). */
+static int32_t choose(const np8o_ctx *c, int64_t i, const double *x, int32_t zi) {
+    const int K = c->K, M = c->M;
+    pick_state st = {-INFINITY, 0.0, np8o_uniform(c->cfg.seed, (uint64_t)i, c->t, NP8O_STREAM_PICK, 0), 0};
+    for (int j = 0; j < K; ++j) {
+        int s = c->live[j];
+        double ll = slot_ll(c, x, s);
+        pick_step(&st, ll + ((s == zi) ? c->logn1[j] : c->logn[j]), j);
+    }
+    double lla[NP8O_MMAX];
+    aux_ll(c, x, (uint64_t)i, c->t, lla);
+    for (int m = 0; m < M; ++m) pick_step(&st, lla[m] + c->logam, K + m);
+    return st.pick;
+}
+
+static inline int64_t position_to_point(const np8o_ctx *c, int64_t p, int sync, const int64_t *order) {
+    if (order) return order[p];
+    if (sync) return p;
+    return (int64_t)np8o_perm(c->cfg.seed, c->t, (uint32_t)c->N, (uint32_t)p);
+}
+
+static int assign_range_impl(np8o_ctx *c, int64_t p0, int64_t p1, int sync, const int64_t *order, int32_t *delta,
+                             int64_t *req_pos, int64_t *req_i, int32_t *req_m, int32_t *req_zold, int32_t req_cap,
+                             int32_t *n_req) {
+    int32_t nr = 0;
+    int err = 0;
+    for (int64_t p = p0; p < p1; ++p) {
+        int64_t i = position_to_point(c, p, sync, order);
+        const double *x = c->X + (size_t)i * c->D;
+        int32_t zi = c->z[i];
+        int32_t j = choose(c, i, x, zi);
+        if (j < c->K) {
+            int32_t s = c->live[j];
+            if (s != zi) {
+                delta[zi] -= 1;
+                delta[s] += 1;
+                c->z[i] = s;
+            }
+        } else {
+            if (nr < req_cap) {
+                req_pos[nr] = p;
+                req_i[nr] = i;
+                req_m[nr] = j - c->K;
+                req_zold[nr] = zi;
+            }
+            ++nr; /* counted even past the capacity: finalize then rejects the whole list */
+        }
+    }
+    *n_req = nr;
+    return err;
+}
+
+int np8o_assign_range(np8o_ctx *c, int64_t p0, int64_t p1, int32_t *delta, int64_t *req_pos, int64_t *req_i,
+                      int32_t *req_m, int32_t *req_zold, int32_t req_cap, int32_t *n_req) {
+    int64_t chunk = c->cfg.chunk <= 0 ? c->N : c->cfg.chunk;
+    return assign_range_impl(c, p0, p1, chunk >= c->N, NULL, delta, req_pos, req_i, req_m, req_zold, req_cap, n_req);
+}
+
+/* Requests are accepted all-or-none: at most NP8O_REQMAX per finalize and no more than the free
+ * slots left once every requester has left its old slot (DESIGN.md "Finalize"). */
+static int cmp_req(const void *a, const void *b) {
+    const int64_t *x = (const int64_t *)a, *y = (const int64_t *)b;
+    return (x[0] > y[0]) - (x[0] < y[0]);
+}
+
+int np8o_finalize(np8o_ctx *c, const int32_t *delta, const int64_t *req_pos, const int64_t *req_i,
+                  const int32_t *req_m, const int32_t *req_zold, int32_t n_req, int64_t owner_lo, int64_t owner_hi) {
+    const int D = c->D;
+    int err = 0;
+    for (int s = 0; s < c->kcap; ++s) c->cnt[s] += delta[s];
+    int accept = (n_req <= NP8O_REQMAX);
+    if (n_req > 0 && accept) {
+        for (int32_t q = 0; q < n_req; ++q) c->cnt[req_zold[q]] -= 1;
+        int32_t nfree = 0;
+        for (int s = 0; s < c->kcap; ++s) nfree += (c->cnt[s] == 0);
+        if (n_req > nfree) {
+            accept = 0;
+            for (int32_t q = 0; q < n_req; ++q) c->cnt[req_zold[q]] += 1;
+        }
+    }
+    if (n_req > 0 && !accept) err = -4;
+    if (n_req > 0 && accept) {
+        int64_t *ord = (int64_t *)malloc(sizeof(int64_t) * 2 * (size_t)n_req);
+        for (int32_t q = 0; q < n_req; ++q) {
+            ord[2 * q] = req_pos[q];
+            ord[2 * q + 1] = q;
+        }
+        qsort(ord, (size_t)n_req, 2 * sizeof(int64_t), cmp_req);
+        int32_t q = 0;
+        for (int s = 0; s < c->kcap && q < n_req; ++s) {
+            if (c->cnt[s] != 0) continue;
+            int64_t r = ord[2 * q + 1];
+            int64_t i = req_i[r];
+            double vv[NP8O_MMAX], mm[NP8O_MMAX * NP8O_DMAX];
+            aux_draws(c, (uint64_t)i, c->t, vv, mm);
+            slot_from_aux(c, s, vv[req_m[r]], mm + (size_t)req_m[r] * D);
+            c->cnt[s] = 1;
+            if (owner_hi < 0 || (i >= owner_lo && i < owner_hi)) c->z[i] = s;
+            ++q;
+        }
+        free(ord);
+    }
+    rebuild_dense(c);
+    return err;
+}
+
+double np8o_total_loglik(np8o_ctx *c) {
+    double L = 0.0;
+    for (int64_t i = 0; i < c->N; ++i) L += slot_ll(c, c->X + (size_t)i * c->D, c->z[i]);
+    return L;
+}
+
+int np8o_end_sweep(np8o_ctx *c) {
+    if (c->t % 5u == 0u) { /* np_mcmc.cpp:172-174 */
+        double L = np8o_total_loglik(c);
+        if (L > c->best_L) {
+            c->best_L = L;
+            c->have_best = 1;
+            memcpy(c->z_best, c->z, sizeof(int32_t) * (size_t)c->N);
+            memcpy(c->cnt_best, c->cnt, sizeof(int32_t) * c->kcap);
+            memcpy(c->mu_best, c->slot_mu, sizeof(double) * (size_t)c->kcap * c->D);
+            memcpy(c->sigma_best, c->slot_sigma, sizeof(double) * (size_t)c->kcap * c->D * c->D);
+        }
+    }
+    c->t += 1u;
+    return 0;
+}
+
+static int run_chunks(np8o_ctx *c, const int64_t *order, int64_t npos, int64_t chunk) {
+    int err = 0;
+    const int sync = (order == NULL) && (chunk >= c->N);
+    for (int64_t p0 = 0; p0 < npos; p0 += chunk) {
+        int64_t p1 = (p0 + chunk < npos) ? p0 + chunk : npos;
+        memset(c->delta, 0, sizeof(int32_t) * c->kcap);
+        int32_t nr = 0;
+        int e1 = assign_range_impl(c, p0, p1, sync, order, c->delta, c->rq_pos, c->rq_i, c->rq_m, c->rq_zold,
+                                   (int32_t)(p1 - p0), &nr);
+        int e2 = np8o_finalize(c, c->delta, c->rq_pos, c->rq_i, c->rq_m, c->rq_zold, nr, 0, -1);
+        if (e1) err = e1;
+        if (e2) err = e2;
+    }
+    return err;
+}
+
+int np8o_sweep(np8o_ctx *c, int32_t n) {
+    int err = 0;
+    int64_t chunk = c->cfg.chunk <= 0 ? c->N : c->cfg.chunk;
+    if (chunk > c->N) chunk = c->N;
+    for (int s = 0; s < n; ++s) {
+        if (c->N > 0) {
+            int e = run_chunks(c, NULL, c->N, chunk);
+            if (e) err = e;
+        }
+        np8o_end_sweep(c);
+    }
+    return err;
+}
+
+int np8o_update_points(np8o_ctx *c, const int64_t *ids, int64_t n) {
+    for (int64_t k = 0; k < n; ++k)
+        if (ids[k] < 0 || ids[k] >= c->N) return -3;
+    return run_chunks(c, ids, n, 1);
+}
+
+int np8o_get_state(np8o_ctx *c, int32_t which, int32_t *z, int32_t *K, double *mu, double *Sigma,
+                   int64_t *counts) {
+    const int D = c->D;
+    const int32_t *zz = c->z, *cc = c->cnt;
+    const double *mm = c->slot_mu, *ss = c->slot_sigma;
+    if (which == 1) {
+        if (!c->have_best) return -5;
+        zz = c->z_best;
+        cc = c->cnt_best;
+        mm = c->mu_best;
+        ss = c->sigma_best;
+    }
+    int32_t *lab = (int32_t *)malloc(sizeof(int32_t) * c->kcap);
+    int k = 0;
+    for (int s = 0; s < c->kcap; ++s) {
+        if (cc[s] > 0) {
+            lab[s] = k;
+            if (mu) memcpy(mu + (size_t)k * D, mm + (size_t)s * D, sizeof(double) * D);
+            if (Sigma) memcpy(Sigma + (size_t)k * D * D, ss + (size_t)s * D * D, sizeof(double) * D * D);
+            if (counts) counts[k] = cc[s];
+            ++k;
+        } else {
+            lab[s] = -1;
+        }
+    }
+    if (K) *K = k;
+    if (z)
+        for (int64_t i = 0; i < c->N; ++i) z[i] = lab[zz[i]];
+    free(lab);
+    return 0;
+}
+
+int32_t np8o_num_clusters(np8o_ctx *c) { return c->K; }
+uint32_t np8o_epoch(np8o_ctx *c) { return c->t; }
+double np8o_best_loglik(np8o_ctx *c) { return c->best_L; }
+int32_t *np8o_z_ptr(np8o_ctx *c) { return c->z; }
+
+int np8o_loglik_matrix(np8o_ctx *c, const int64_t *idx, int64_t n, double *out) {
+    const int K = c->K, M = c->M;
+    for (int64_t r = 0; r < n; ++r) {
+        int64_t i = idx[r];
+        if (i < 0 || i >= c->N) return -3;
+        const double *x = c->X + (size_t)i * c->D;
+        for (int j = 0; j < K; ++j) out[r * (K + M) + j] = slot_ll(c, x, c->live[j]);
+        aux_ll(c, x, (uint64_t)i, c->t, out + r * (K + M) + K);
+    }
+    return 0;
+}
+
+int np8o_aux_params(np8o_ctx *c, int64_t i, double *mu, double *Sigma) {
+    const int D = c->D;
+    double vv[NP8O_MMAX];
+    aux_draws(c, (uint64_t)i, c->t, vv, mu);
+    if (Sigma)
+        for (int m = 0; m < c->M; ++m)
+            for (int k = 0; k < D * D; ++k) Sigma[(size_t)m * D * D + k] = vv[m] * vv[m] * c->LTL[k];
+    return 0;
+}
+
+int np8o_loglik_matrix_ref(np8o_ctx *c, const int64_t *idx, int64_t n, double *out) {
+    const int K = c->K, M = c->M, D = c->D;
+    double amu[NP8O_MMAX * NP8O_DMAX], asig[NP8O_MMAX * NP8O_DMAX * NP8O_DMAX];
+    for (int64_t r = 0; r < n; ++r) {
+        int64_t i = idx[r];
+        if (i < 0 || i >= c->N) return -3;
+        const double *x = c->X + (size_t)i * D;
+        for (int j = 0; j < K; ++j) {
+            int s = c->live[j];
+            out[r * (K + M) + j] =
+                np8o_mvn_logprobability_ref(x, c->slot_mu + (size_t)s * D, c->slot_sigma + (size_t)s * D * D, D);
+        }
+        np8o_aux_params(c, i, amu, asig);
+        for (int m = 0; m < M; ++m)
+            out[r * (K + M) + K + m] =
+                np8o_mvn_logprobability_ref(x, amu + (size_t)m * D, asig + (size_t)m * D * D, D);
+    }
+    return 0;
+}

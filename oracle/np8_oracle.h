@@ -1,0 +1,118 @@
+/*
+ * np8_oracle.h -- TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement (plain C, single thread) of mrquincle/noparama's Neal Algorithm 8 Gibbs sweep
+ * for a Dirichlet-process mixture of multivariate normals.  Only tests/, __graft_entry__.smoke()
+ * and bench.py's cpu_baseline leg may load this library, and only as the checker / the timed CPU
+ * baseline -- never as the product path.  The product is noparama_amd/csrc (HIP, gfx950).
+ *
+ * Two layers:
+ *   1. Faithful restatements of the reference functions, cited file:line, used to pin numbers:
+ *        np8o_mvn_probability_ref / np8o_mvn_logprobability_ref  (src/statistics/multivariatenormal.cpp)
+ *        np8o_weighted_pick_ref                                (include/helper/dim1algebra.hpp)
+ *        np8o_similarity                                       (src/clustering_performance.cpp)
+ *   2. The chain itself (np8o_ctx): the reference sampler's semantics (src/np_neal_algorithm8.cpp:49-167
+ *      driven by src/np_mcmc.cpp:48-175) generalised to a `chunk` of points evaluated against a frozen
+ *      state (chunk = 1 is exactly the reference's sequential sweep).  Randomness comes from keyed
+ *      Philox4x32-10 streams instead of std::default_random_engine so that the HIP path can be
+ *      checked against it assignment for assignment (see DESIGN.md "Chain specification").
+ *
+ * Parity pinning: the likelihood is pinned by the reference's only known-answer test
+ * (test/test_mvn_likelihood.cpp:30-44); the weighted pick is pinned by compiling the reference's own
+ * header (oracle/ref_pick_harness.cpp -> oracle/_ref/); Philox by Random123/rocRAND known answers;
+ * the metrics by sklearn.  G0 and the chain have no reference fixture (the reference is unseeded,
+ * src/np_main.cpp:180): they are pinned by moment tests and by the statistical comparison of
+ * chunk=1 chains, see DESIGN.md.
+ */
+#ifndef NP8_ORACLE_H
+#define NP8_ORACLE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NP8O_DMAX 64
+#define NP8O_MMAX 8
+#define NP8O_REQMAX 4096 /* new-cluster requests one finalize accepts (must match) */
+
+/* Philox stream ids (high byte of counter word 3). */
+enum { NP8O_STREAM_AUX = 1, NP8O_STREAM_PICK = 2, NP8O_STREAM_INIT_THETA = 3, NP8O_STREAM_INIT_Z = 4 };
+
+/* ---- primitives ---------------------------------------------------------------------------- */
+void np8o_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
+double np8o_u01(uint32_t hi, uint32_t lo);
+/* n-th standard normal of stream (i, t, stream) under key seed. */
+double np8o_normal(uint64_t seed, uint64_t i, uint32_t t, uint32_t stream, uint32_t n);
+double np8o_uniform(uint64_t seed, uint64_t i, uint32_t t, uint32_t stream, uint32_t n);
+uint32_t np8o_perm(uint64_t seed, uint32_t t, uint32_t N, uint32_t p);
+
+/* ---- faithful reference restatements ------------------------------------------------------- */
+/* multivariatenormal.cpp:64-94 (clustering branch :82-93): exp(-0.5 d'Inv d)/sqrt((2pi)^D det). */
+double np8o_mvn_probability_ref(const double *x, const double *mu, const double *Sigma, int D);
+/* multivariatenormal.cpp:106-136: exponent - log(sqrt((2pi)^D det)). */
+double np8o_mvn_logprobability_ref(const double *x, const double *mu, const double *Sigma, int D);
+/* dim1algebra.hpp:2078-2104 with the uniform u supplied by the caller. */
+int64_t np8o_weighted_pick_ref(const double *w, int64_t n, double u);
+/* LU with partial pivoting (Eigen PartialPivLU): inverse (row-major) and determinant. 0 = ok. */
+int np8o_lu_inverse_det(const double *A, int D, double *inv, double *det);
+/* clustering_performance.cpp:14-82 in int64/double: out = {purity, rand_index, adjusted_rand_index}. */
+void np8o_similarity(const int32_t *truth, const int32_t *result, int64_t n, double out[3]);
+
+/* ---- the chain ------------------------------------------------------------------------------- */
+typedef struct np8o_ctx np8o_ctx;
+
+typedef struct {
+    int32_t D, M;
+    double alpha;
+    double mu0[NP8O_DMAX];
+    double kappa, nu;
+    double Lambda[NP8O_DMAX * NP8O_DMAX];
+    uint64_t seed;
+    int32_t kcap;
+    int64_t chunk; /* 0 => N (synchronous sweep) */
+} np8o_config;
+
+np8o_ctx *np8o_create(const np8o_config *cfg);
+void np8o_destroy(np8o_ctx *c);
+int np8o_set_data(np8o_ctx *c, const double *X, int64_t N);
+/* z in [0,K), clusters given by mu [K*D] and Sigma [K*D*D] row-major. */
+int np8o_set_state(np8o_ctx *c, const int32_t *z, int32_t K, const double *mu, const double *Sigma);
+int np8o_init_random(np8o_ctx *c, int32_t K_init);
+/* Runs n sweeps. Returns 0 or a negative error (capacity). */
+int np8o_sweep(np8o_ctx *c, int32_t n);
+/* Exact sequential updates of the listed points (chunk = 1, in the given order) at the current epoch. */
+int np8o_update_points(np8o_ctx *c, const int64_t *ids, int64_t n);
+/* Dense labels (ascending slot order), K, mu/Sigma per label (may be NULL), counts per label. */
+int np8o_get_state(np8o_ctx *c, int32_t which, int32_t *z, int32_t *K, double *mu, double *Sigma, int64_t *counts);
+int32_t np8o_num_clusters(np8o_ctx *c);
+uint32_t np8o_epoch(np8o_ctx *c);
+double np8o_best_loglik(np8o_ctx *c);
+double np8o_total_loglik(np8o_ctx *c);
+/* ll of the given points vs. every live cluster (ascending slot) then the M auxiliaries of the
+ * current epoch: out is n x (K+M). Table form (what the chain uses). */
+int np8o_loglik_matrix(np8o_ctx *c, const int64_t *idx, int64_t n, double *out);
+/* Same matrix computed with the faithful reference formula (general LU inverse, per call). */
+int np8o_loglik_matrix_ref(np8o_ctx *c, const int64_t *idx, int64_t n, double *out);
+/* The aux draws (mu [M*D], Sigma [M*D*D]) point i would see at the current epoch. */
+int np8o_aux_params(np8o_ctx *c, int64_t i, double *mu, double *Sigma);
+
+/* ---- sharded (multi-rank) protocol: the same exchange record the HIP path uses ------------- */
+/* Evaluate positions [p0,p1) of the current chunk against the frozen state. Writes z for movers
+ * to existing clusters, delta[kcap] (+/- counts of those moves) and new-cluster requests
+ * (pos, i, m, old slot); *n_req counts every request, also those past req_cap. */
+int np8o_assign_range(np8o_ctx *c, int64_t p0, int64_t p1, int32_t *delta, int64_t *req_pos,
+                      int64_t *req_i, int32_t *req_m, int32_t *req_zold, int32_t req_cap, int32_t *n_req);
+/* Apply summed deltas and the concatenated (pos-sorted) request list; rebuild the candidate table.
+ * owner_lo/owner_hi: only points in [owner_lo, owner_hi) get z written (all if owner_hi<0). */
+int np8o_finalize(np8o_ctx *c, const int32_t *delta, const int64_t *req_pos, const int64_t *req_i,
+                  const int32_t *req_m, const int32_t *req_zold, int32_t n_req, int64_t owner_lo, int64_t owner_hi);
+/* Advance the epoch (end of sweep): max-likelihood bookkeeping (np_mcmc.cpp:172-174). */
+int np8o_end_sweep(np8o_ctx *c);
+int32_t *np8o_z_ptr(np8o_ctx *c);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,194 @@
+"""GPU parity: the HIP path (libnp8.so via the C ABI) against the CPU oracle on identical inputs.
+
+Integer outputs (labels, cluster counts, K) must be bit-exact; log-likelihoods within 1e-12
+relative (fp64, DESIGN.md "Tolerances").  Mirrors the reference's own checks where they exist:
+test/test_mvn_likelihood.cpp (KAT) and test/test_membertrix.cpp (auto-remove of emptied clusters).
+"""
+import numpy as np
+import pytest
+
+import oracle as O
+from noparama_amd import NP8Error, NealAlgorithm8, datasets
+
+pytestmark = pytest.mark.gpu
+
+LL_RTOL = 1e-12
+
+
+def pair(D, seed, chunk=0, kcap=2048, **kw):
+    return (NealAlgorithm8(D, seed=seed, chunk=chunk, kcap=kcap, device=0, **kw),
+            O.Chain(D, seed=seed, chunk=chunk, kcap=kcap, **kw))
+
+
+def assert_same_state(a, b, which=0):
+    sa, sb = a.state(which), b.state(which)
+    assert sa["K"] == sb["K"]
+    assert np.array_equal(sa["z"], sb["z"])
+    assert np.array_equal(sa["counts"], sb["counts"])
+    np.testing.assert_allclose(sa["mu"], sb["mu"], rtol=1e-13, atol=1e-13)
+    np.testing.assert_allclose(sa["sigma"], sb["sigma"], rtol=1e-13, atol=1e-15)
+
+
+def test_kat_likelihood_through_abi():
+    """test/test_mvn_likelihood.cpp:18-33: mu=(1,1), Sigma=[[2,0],[1,2]] (non-symmetric), x=(1,2)."""
+    g = NealAlgorithm8(2, seed=0, device=0)
+    g.set_data(np.array([[1.0, 2.0], [1.0, 2.0]]))
+    g.set_state(np.zeros(2, np.int32), np.array([[1.0, 1.0]]), np.array([[[2.0, 0.0], [1.0, 2.0]]]))
+    ll = g.loglik_matrix(np.array([0, 1]))[:, 0]
+    p = np.exp(ll)
+    assert abs(p[0] - 0.061974) < 1e-5
+    assert abs(p[0] * p[1] - 0.0038409) < 1e-6  # probability(dataset) = product (:41-44)
+    np.testing.assert_allclose(ll[0], np.log(O.mvn_probability_ref([1, 2], [1, 1], [[2, 0], [1, 2]])),
+                               rtol=1e-14)
+
+
+@pytest.mark.parametrize("sweeps", [1, 4])
+def test_twogaussians_sync_bit_exact(sweeps):
+    X, _ = datasets.twogaussians()
+    g, o = pair(2, 11)
+    for s in (g, o):
+        s.set_data(X)
+        s.init_random(20)
+    assert_same_state(g, o)
+    g.sweep(sweeps)
+    o.sweep(sweeps)
+    assert_same_state(g, o)
+
+
+@pytest.mark.parametrize("chunk", [1, 7, 64])
+def test_chunked_sweeps_bit_exact(chunk):
+    """chunk = 1 is the reference's sequential sweep (np_mcmc.cpp:146-164)."""
+    X, _ = datasets.twogaussians(3)
+    g, o = pair(2, 5, chunk=chunk)
+    for s in (g, o):
+        s.set_data(X)
+        s.init_random(20)
+    g.sweep(3)
+    o.sweep(3)
+    assert_same_state(g, o)
+
+
+def test_update_points_explicit_order():
+    X, _ = datasets.twogaussians(4)
+    g, o = pair(2, 9)
+    order = np.random.default_rng(1).permutation(200)
+    for s in (g, o):
+        s.set_data(X)
+        s.init_random(20)
+        s.update_points(order)
+        s.end_sweep()
+        s.update_points(order[::-1].copy())
+    assert_same_state(g, o)
+
+
+def test_loglik_matrix_vs_oracle_and_reference_formula():
+    X, _, mu, sig = datasets.mixture(3000, 8, 16, 0.8, 20.0, seed=3)
+    g, o = pair(8, 21)
+    z = np.random.default_rng(0).integers(0, 16, size=3000).astype(np.int32)
+    for s in (g, o):
+        s.set_data(X)
+        s.set_state(z, mu, sig)
+    idx = np.arange(0, 3000, 7)
+    a = g.loglik_matrix(idx)
+    b = o.loglik_matrix(idx)
+    ref = o.loglik_matrix(idx, ref=True)  # multivariatenormal.cpp:124-135 with LU inverse per call
+    np.testing.assert_allclose(a, b, rtol=LL_RTOL, atol=1e-12)
+    np.testing.assert_allclose(a, ref, rtol=1e-10, atol=1e-9)
+
+
+@pytest.mark.parametrize("D,K,s,r", [(2, 10, 0.3, 15.0), (8, 64, 0.8, 20.0), (3, 5, 0.5, 5.0), (16, 8, 1.0, 10.0)])
+def test_warm_state_sweeps_bit_exact(D, K, s, r):
+    X, z, mu, sig = datasets.mixture(20000, D, K, s, r, seed=D)
+    g, o = pair(D, 100 + D)
+    for c in (g, o):
+        c.set_data(X)
+        c.set_state(z, mu, sig)
+    g.sweep(3)
+    o.sweep(3)
+    assert_same_state(g, o)
+    np.testing.assert_allclose(g.total_loglik(), o.total_loglik(), rtol=1e-11)
+
+
+def test_max_likelihood_snapshot():
+    X, _ = datasets.twogaussians(8)
+    g, o = pair(2, 13)
+    for s in (g, o):
+        s.set_data(X)
+        s.init_random(20)
+    g.sweep(16)
+    o.sweep(16)
+    assert_same_state(g, o, which=1)
+    np.testing.assert_allclose(g.stats()["best_loglik"], o.best_loglik(), rtol=1e-12)
+
+
+def test_singleton_cluster_auto_removed():
+    """test/test_membertrix.cpp:16-93 analogue: emptied clusters disappear from the live table."""
+    X = np.array([[0.0, 0.0], [0.1, 0.0], [50.0, 50.0]])
+    g, o = pair(2, 1)
+    mu = np.array([[0.0, 0.0], [50.0, 50.0], [-30.0, 8.0]])
+    sig = np.stack([np.eye(2) * 0.5] * 3)
+    z = np.array([0, 2, 1], np.int32)  # item 1 alone in a far cluster
+    for s in (g, o):
+        s.set_data(X)
+        s.set_state(z, mu, sig)
+        s.sweep(1)
+    assert_same_state(g, o)
+    assert g.state()["K"] <= 3
+
+
+def test_errors_are_reported():
+    g = NealAlgorithm8(2, seed=0, device=0)
+    with pytest.raises(NP8Error):
+        g.sweep(1)  # no data / state
+    g.set_data(np.zeros((4, 2)))
+    with pytest.raises(NP8Error):
+        g.set_state(np.array([0, 0, 0, 5], np.int32), np.zeros((1, 2)), np.eye(2)[None])
+    with pytest.raises(NP8Error):
+        g.set_state(np.zeros(4, np.int32), np.zeros((1, 2)), np.zeros((1, 2, 2)))  # det = 0
+    with pytest.raises(NP8Error):
+        NealAlgorithm8(5, seed=0, device=0)  # no kernel instantiated for D = 5
+
+
+def test_capacity_rejection_matches_oracle():
+    """More new-cluster requests than free slots: the whole step's requests are rejected."""
+    X, _ = datasets.twogaussians(5)
+    g, o = pair(2, 17, kcap=24)
+    for s in (g, o):
+        s.set_data(X)
+        s.init_random(20)
+    with pytest.raises(NP8Error) as e:
+        g.sweep(2)
+    assert e.value.code == -4
+    assert o.sweep(2) == -4
+    assert_same_state(g, o)
+
+
+def test_host_exchange_two_ranks_equals_one():
+    """The multi-GPU protocol (exchange record, rank-ordered requests) with two contexts on one GPU
+    and a host all-gather: identical to the single-rank sweep."""
+    X, _, mu, sig = datasets.mixture(5000, 8, 12, 0.8, 6.0, seed=9)
+    z = np.random.default_rng(2).integers(0, 12, size=5000).astype(np.int32)
+    one = NealAlgorithm8(8, seed=77, device=0)
+    one.set_data(X)
+    one.init_random(12)
+    one.sweep(3)
+    half = 2600
+    ranks = [NealAlgorithm8(8, seed=77, device=0) for _ in range(2)]
+    for r, c in enumerate(ranks):
+        c.comm_init(None, r, 2)
+        lo, hi = (0, half) if r == 0 else (half, 5000)
+        c.set_data(X[lo:hi], offset=lo, n_global=5000)
+        c.init_random(12)
+    for _ in range(3):
+        recs = np.concatenate([c.step_local() for c in ranks])
+        for c in ranks:
+            c.step_merge(recs, 2)
+            c.end_sweep()
+    s1 = one.state()
+    z2 = np.concatenate([c.state()["z"] for c in ranks])
+    assert np.array_equal(s1["z"], z2)
+    for c in ranks:
+        st = c.state()
+        assert st["K"] == s1["K"]
+        assert np.array_equal(st["counts"], s1["counts"])
+    del z, mu, sig
