@@ -1,0 +1,120 @@
+// np_main.cpp -- command-line driver mirroring the reference's `noparama` executable for the Neal-8
+// clustering path (src/np_main.cpp:156-507):
+//   np8_noparama -d <data> -a algorithm8 -T <sweeps> -c clustering [-s seed] [-C chunk] [-D dims]
+// reads "x_1 .. x_D label" rows (np_main.cpp:57-148, generalised from 2 columns), runs MCMC on the
+// GPU, and writes <workspace>/<stamp>/{snapshot,results}.score.txt in the reference's format
+// (clustering_performance.cpp:84-93) for the last state and the max-likelihood state.  Refuses to
+// overwrite an existing workspace (exit 106, np_main.cpp:273-276).
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <chrono>
+#include <cstdlib>
+#include <fstream>
+#include <iostream>
+#include <sstream>
+#include <string>
+
+#include "np_host.h"
+
+static void usage(const char *p) {
+    std::cerr << "usage: " << p << " -d <datafile> -a algorithm8 [-T sweeps=2000] [-c clustering] [-s seed]"
+              << " [-C chunk (0 = data-parallel sweep, 1 = sequential)] [-D dims=2] [-w workspace]" << std::endl;
+}
+
+static bool read_data(const std::string &fn, int D, dataset_t &ds, std::vector<int> &gt) {
+    std::ifstream f(fn);
+    std::string line;
+    while (std::getline(f, line)) {
+        std::istringstream ss(line);
+        auto *d = new data_t(D);
+        bool ok = true;
+        for (int a = 0; a < D; ++a) ok = ok && static_cast<bool>(ss >> (*d)[a]);
+        double c = 0;
+        ok = ok && static_cast<bool>(ss >> c);
+        if (!ok) {
+            delete d;
+            continue;
+        }
+        ds.push_back(d);
+        gt.push_back((int)c);
+    }
+    return !ds.empty();
+}
+
+int main(int argc, char *argv[]) {
+    std::string data, algo, mode = "clustering", ws;
+    int T = 2000, D = 2;
+    long long chunk = 0;
+    unsigned long long seed = 0;
+    bool seeded = false;
+    int tok;
+    while ((tok = getopt(argc, argv, "d:a:T:c:s:C:D:w:h?")) != EOF) {
+        switch (tok) {
+            case 'd': data = optarg; break;
+            case 'a': algo = optarg; break;
+            case 'T': T = std::stoi(optarg); break;
+            case 'c': mode = optarg; break;
+            case 's': seed = std::stoull(optarg); seeded = true; break;
+            case 'C': chunk = std::stoll(optarg); break;
+            case 'D': D = std::stoi(optarg); break;
+            case 'w': ws = optarg; break;
+            default: usage(argv[0]); return 1;
+        }
+    }
+    if (data.empty() || algo.empty()) {
+        usage(argv[0]);
+        return 1;
+    }
+    if (algo != "algorithm8") {
+        std::cerr << "Unknown algorithm: " << algo << " (this build implements algorithm8)" << std::endl;
+        return 1;
+    }
+    if (mode != "clustering") {
+        std::cerr << "Unknown likelihood" << std::endl;
+        return 107;
+    }
+    if (!seeded) seed = (unsigned long long)std::chrono::high_resolution_clock::now().time_since_epoch().count();
+    if (ws.empty()) ws = "output/" + algo + "/" + data.substr(data.find_last_of('/') + 1) + "/";
+    struct stat sb;
+    if (stat(ws.c_str(), &sb) == 0) {
+        std::cerr << "Directory already exists. Drop out. We don't want to overwrite it or do double work." << std::endl;
+        return 106;
+    }
+    dataset_t dataset;
+    std::vector<int> gt;
+    if (!read_data(data, D, dataset, gt)) {
+        std::cerr << "No data found... Check the file or the contents of the file." << std::endl;
+        return 7;
+    }
+    np8_prior prior;
+    prior.D = D;
+    try {
+        NealAlgorithm8Hip sampler(seed, prior, chunk);
+        MCMC mcmc(sampler);
+        auto t0 = std::chrono::steady_clock::now();
+        mcmc.run(dataset, T);
+        double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        sampler.printStatistics();
+        std::string dir = ws + std::to_string(seed) + "/";
+        std::string cmd = "mkdir -p '" + dir + "'";
+        if (std::system(cmd.c_str()) != 0) return 1;
+        for (int which = 0; which < 2; ++which) {
+            const membertrix &m = which ? mcmc.getMaxLikelihoodMatrix() : mcmc.getMembershipMatrix();
+            std::vector<int> res(m.count());
+            for (size_t i = 0; i < m.count(); ++i) res[i] = m.getClusterId((data_id_t)i);
+            clustering_performance cp;
+            cp.calculate(gt, res);
+            cp.write(dir + (which ? "results" : "snapshot") + ".score.txt");
+            std::cout << (which ? "results" : "snapshot") << ": K=" << m.getClusterCount() << " Purity: " << cp.purity
+                      << " Rand Index: " << cp.rand_index << " Adjusted Rand Index: " << cp.adjusted_rand_index
+                      << std::endl;
+        }
+        std::cout << "sweeps: " << T << " seconds: " << sec << " sweeps/s: " << T / sec << std::endl;
+    } catch (const std::exception &e) {
+        std::cerr << e.what() << std::endl;
+        return 2;
+    }
+    for (auto *d : dataset) delete d;
+    return 0;
+}

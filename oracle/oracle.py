@@ -273,5 +273,6 @@ class Chain:
         rz = np.ascontiguousarray(rz, dtype=np.int32)
         n = rp.size if n_req is None else n_req
         r = lib().np8o_finalize(self._h, _p(delta), _p(rp), _p(ri), _p(rm), _p(rz), n, owner_lo, owner_hi)
-        if r:
+        if r not in (0, -4):
             raise ValueError(f"oracle finalize: {r}")
+        return r  # -4: the step's new-cluster requests were rejected (capacity), state consistent

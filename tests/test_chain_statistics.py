@@ -1,0 +1,50 @@
+"""Statistical parity of the chain (the reference is unseeded, src/np_main.cpp:180, so runs can only
+be compared in distribution).  On twogaussians (scripts/generate.m) with the reference settings
+(alpha 1, M 3, K_init 20, mu0 (6,6), kappa 1/500, nu 4, Lambda 0.01 I), the data-parallel sweep
+(chunk = N, what the GPU runs by default) must score like the reference's sequential sweep (chunk = 1)
+on the max-likelihood labelling that results.score.txt reports (np_main.cpp:492-497).  Tolerances
+(DESIGN.md): |d mean purity| <= 0.02, |d mean ARI| <= 0.05 over 20 seeds.  CPU only (the GPU runs
+the same chunked algorithm bit-exactly, tests/test_gpu_parity.py)."""
+import os
+
+import numpy as np
+import pytest
+
+import oracle as O
+from noparama_amd import datasets
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+T = 300
+SEEDS = 20
+
+
+def run(seed, chunk):
+    X, lab = datasets.read_data(os.path.join(GOLD, "twogaussians.data"))
+    c = O.Chain(2, seed=seed, chunk=chunk, kcap=1024)
+    c.set_data(X)
+    c.init_random(20)
+    assert c.sweep(T) == 0
+    st = c.state(which=1)
+    m = O.similarity(lab, st["z"])
+    return m["purity"], m["adjusted_rand_index"], st["K"]
+
+
+@pytest.mark.slow
+def test_sync_sweep_scores_like_sequential_sweep():
+    seq = np.array([run(s, 1) for s in range(SEEDS)])
+    par = np.array([run(1000 + s, 0) for s in range(SEEDS)])
+    assert seq[:, 0].mean() > 0.95  # README.rst:53-55: purity "should be almost 1"
+    assert abs(seq[:, 0].mean() - par[:, 0].mean()) <= 0.02, (seq[:, 0].mean(), par[:, 0].mean())
+    assert abs(np.nanmean(seq[:, 1]) - np.nanmean(par[:, 1])) <= 0.05, (np.nanmean(seq[:, 1]), np.nanmean(par[:, 1]))
+
+
+def test_sequential_chain_is_a_valid_partition():
+    X, lab = datasets.read_data(os.path.join(GOLD, "twogaussians.data"))
+    c = O.Chain(2, seed=3, chunk=1, kcap=1024)
+    c.set_data(X)
+    c.init_random(20)
+    c.sweep(20)
+    st = c.state()
+    assert st["counts"].sum() == 200 and (st["counts"] > 0).all()
+    assert st["z"].min() == 0 and st["z"].max() == st["K"] - 1
+    assert np.array_equal(np.bincount(st["z"], minlength=st["K"]), st["counts"])

@@ -1,0 +1,75 @@
+"""CPU checks of the product library without compute: libnp8.so loads, exports exactly the C ABI that
+include/np8.h declares, rejects bad configurations cleanly, and the host mirror behaves."""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import noparama_amd
+from noparama_amd import np8
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_library_exports_every_declared_symbol():
+    L = noparama_amd.lib()
+    declared = noparama_amd.header_symbols()
+    assert len(declared) == 21
+    for name in declared:
+        assert hasattr(L, name), name
+    out = subprocess.run(["nm", "-D", "--defined-only", np8.LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    exported = sorted({ln.split()[-1] for ln in out.splitlines() if " T np8_" in ln})
+    assert exported == declared
+
+
+def test_library_is_gfx950_code_object():
+    blob = open(np8.LIB_PATH, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in blob
+    assert b"np8_assign" in blob and b"np8_finalize" in blob
+
+
+def test_create_rejects_bad_configuration_without_crashing():
+    L = noparama_amd.lib()
+    mu0 = np.zeros(5)
+    lam = np.eye(5)
+    cfg = np8._Config()
+    cfg.D, cfg.M, cfg.alpha = 5, 3, 1.0  # D = 5 has no kernel instantiation
+    cfg.mu0 = mu0.ctypes.data_as(C.POINTER(C.c_double))
+    cfg.Lambda = lam.ctypes.data_as(C.POINTER(C.c_double))
+    cfg.kappa, cfg.nu, cfg.kcap, cfg.device = 0.002, 4.0, 16, -1
+    h = C.c_void_p()
+    assert L.np8_create(C.byref(h), C.byref(cfg)) == np8.NP8_ERR_ARG
+    cfg.D = 2
+    lam2 = -np.eye(2)  # not SPD
+    cfg.Lambda = lam2.ctypes.data_as(C.POINTER(C.c_double))
+    assert L.np8_create(C.byref(h), C.byref(cfg)) == np8.NP8_ERR_ARG
+    assert L.np8_create(None, C.byref(cfg)) == np8.NP8_ERR_ARG
+    assert L.np8_sweep(None, 1) == np8.NP8_ERR_ARG
+    assert L.np8_destroy(None) == 0
+
+
+def test_no_gpu_means_loud_failure():
+    """Without a device the product must fail (no silent CPU fallback)."""
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    with pytest.raises(np8.NP8Error):
+        noparama_amd.NealAlgorithm8(2, device=0)
+
+
+def test_header_matches_python_mirror_of_config():
+    txt = open(np8.HEADER_PATH).read()
+    for field, _ in np8._Config._fields_:
+        assert field in txt
+    for field, _ in np8.Stats._fields_:
+        assert field in txt
+
+
+def test_membertrix_host_view():
+    m = noparama_amd.membertrix()
+    m.load({"z": np.array([0, 1, 1, 2]), "counts": np.array([1, 2, 1])})
+    assert m.count() == 4 and m.count(1) == 2 and m.getClusterId(2) == 1 and m.getClusterCount() == 3
