@@ -52,7 +52,7 @@ class membertrix {
     np_error_t remove(cluster_id_t cluster_id);
     bool assigned(data_id_t data_id) const { return _z[data_id] >= 0; }
     cluster_id_t getClusterId(data_id_t data_id) const { return _z[data_id]; }
-    size_t count() const { return _data.size(); }
+    size_t count() const { return _z.size(); }
     size_t count(cluster_id_t cluster_id) const;
     size_t getClusterCount() const { return _clusters.size(); }
     const clusters_t &getClusters() const { return _clusters; }

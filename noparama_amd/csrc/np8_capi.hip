@@ -56,6 +56,7 @@ struct np8_ctx {
     int32_t *cnt = nullptr, *cnt_best = nullptr;
     double *mu_best = nullptr, *sigma_best = nullptr;
     double *cand = nullptr;
+    int32_t *dense_of = nullptr;
     Ctl *ctl = nullptr;
     double *hyp = nullptr, *d_mu0 = nullptr, *d_LT = nullptr, *d_Gp = nullptr, *d_LTL = nullptr;
     unsigned char *rec = nullptr, *gath = nullptr;
@@ -210,7 +211,7 @@ void slot_from_normals(const np8_ctx *c, double g0, const double *xi, SlotHost &
     o.P.resize(c->DP);
     for (int a = 0; a < D; ++a)
         for (int b = a; b < D; ++b) o.P[packed_index(D, a, b)] = c->Gp[a * D + b] / v2;
-    o.c = std::fma(-(double)D, std::log(std::fabs(v)), c->caux);
+    o.c = std::fma(-(double)D, log_pos(std::fabs(v)), c->caux);
     o.sigma.resize((size_t)D * D);
     for (int k = 0; k < D * D; ++k) o.sigma[k] = v2 * c->LTL[k];
 }
@@ -234,7 +235,7 @@ void free_device(np8_ctx *c) {
     void *ptrs[] = {c->X,      c->z,       c->z_best, c->slot_mu, c->slot_P,  c->slot_c,  c->slot_sigma,
                     c->cnt,    c->cnt_best, c->mu_best, c->sigma_best, c->cand, c->ctl,    c->hyp,
                     c->d_mu0,  c->d_LT,    c->d_Gp,   c->d_LTL,   c->rec,     c->gath,    c->order,
-                    c->partial};
+                    c->partial, c->dense_of};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     c->X = nullptr;
@@ -247,6 +248,7 @@ void free_device(np8_ctx *c) {
     c->rec = c->gath = nullptr;
     c->order = nullptr;
     c->partial = nullptr;
+    c->dense_of = nullptr;
 }
 
 template <typename T>
@@ -324,6 +326,7 @@ FinArgs fin_args(np8_ctx *c, const unsigned char *recs, int world) {
     F.slot_c = c->slot_c;
     F.slot_sigma = c->slot_sigma;
     F.cand = c->cand;
+    F.dense_of = c->dense_of;
     F.ctl = c->ctl;
     F.mu0 = c->d_mu0;
     F.LT = c->d_LT;
@@ -342,6 +345,7 @@ AssignArgs assign_args(np8_ctx *c, int64_t p0, int64_t p1, const int64_t *order,
     A.X = c->X;
     A.z = c->z;
     A.cand = c->cand;
+    A.dense_of = c->dense_of;
     A.ctl = c->ctl;
     A.hyp = c->hyp;
     A.order = order;
@@ -528,6 +532,7 @@ int np8_create(np8_ctx **out, const np8_config *cfg) {
         (r = dalloc(c, &c->cnt, (size_t)kc)) || (r = dalloc(c, &c->cnt_best, (size_t)kc)) ||
         (r = dalloc(c, &c->mu_best, (size_t)kc * D)) || (r = dalloc(c, &c->sigma_best, (size_t)kc * D * D)) ||
         (r = dalloc(c, &c->cand, (size_t)kc * c->CS)) || (r = dalloc(c, &c->ctl, 1)) ||
+        (r = dalloc(c, &c->dense_of, (size_t)kc)) ||
         (r = dalloc(c, &c->rec, (size_t)c->rec_bytes))) {
         free_device(c);
         delete c;

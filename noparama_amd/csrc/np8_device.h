@@ -12,16 +12,19 @@ namespace np8 {
 
 constexpr double kLog2Pi = 1.8378770664093454835606594728112;
 constexpr double kTwoPi = 6.283185307179586476925286766559;
-constexpr int kPickBlock = 32;    // candidates per pick block (DESIGN.md "Pick")
 constexpr int kReqMax = 4096;     // new-cluster requests one finalize can accept
 constexpr int kMaxD = 64;
 constexpr int kMaxM = 8;
 
 enum Stream : uint32_t { kStreamAux = 1, kStreamPick = 2, kStreamInitTheta = 3, kStreamInitZ = 4 };
 
-// Candidate-table entry layout (doubles): [mu(D) | P'(D(D+1)/2) | c | logn | logn1 | slot]
+// Candidate-table entry layout (doubles):
+//   [mu(D) | P'(D(D+1)/2) | c | logn | logn1 | slot | iso]
+// P' = packed upper triangle of sym(Sigma^-1), off-diagonals doubled; iso = the common diagonal when
+// P' is a multiple of I (every G0 draw under an isotropic Lambda), else 0.
 NP8_HD int packed_size(int D) { return D * (D + 1) / 2; }
-NP8_HD int cand_stride(int D) { return (D + packed_size(D) + 4 + 1) & ~1; }
+NP8_HD int cand_stride(int D) { return (D + packed_size(D) + 5 + 1) & ~1; }
+enum CandField : int { kFieldC = 0, kFieldLogn = 1, kFieldLogn1 = 2, kFieldSlot = 3, kFieldIso = 4 };
 
 NP8_HD uint32_t mulhi32(uint32_t a, uint32_t b) { return (uint32_t)(((uint64_t)a * b) >> 32); }
 
@@ -59,17 +62,109 @@ NP8_HD double u01(uint32_t hi, uint32_t lo) {
     return (double)v * 0x1.0p-53;
 }
 
+// ---- elementary functions with identical bits on host and device (DESIGN.md "Math") ------------
+// Weight for the draw: exp(x) for x <= 0 (x may be -inf).  Cody-Waite reduction by ln2, degree-13
+// Taylor polynomial on |r| <= ln2/2, ldexp.  Below -800 the result is 0 (as IEEE exp would be).
+NP8_HD double exp_le0(double x) {
+    x = fmax(x, -800.0);
+    const double k = rint(x * 1.4426950408889634);
+    double r = fma(-k, 0.6931471803691238, x);
+    r = fma(-k, 1.9082149292705877e-10, r);
+    double p = 1.6059043836821613e-10;
+    p = fma(p, r, 2.08767569878681e-09);
+    p = fma(p, r, 2.505210838544172e-08);
+    p = fma(p, r, 2.755731922398589e-07);
+    p = fma(p, r, 2.7557319223985893e-06);
+    p = fma(p, r, 2.48015873015873e-05);
+    p = fma(p, r, 0.0001984126984126984);
+    p = fma(p, r, 0.001388888888888889);
+    p = fma(p, r, 0.008333333333333333);
+    p = fma(p, r, 0.041666666666666664);
+    p = fma(p, r, 0.16666666666666666);
+    p = fma(p, r, 0.5);
+    p = fma(p, r, 1.0);
+    p = fma(p, r, 1.0);
+    return ldexp(p, (int)k);
+}
+
+// log(u) for a positive normal u: u = m 2^e with m in [1/sqrt2, sqrt2), log1p(m-1) = 2 atanh(s),
+// s = (m-1)/(m+1), series to s^21.
+NP8_HD double log_pos(double u) {
+    int e;
+    double m = frexp(u, &e);
+    const bool lo = m < 0.70710678118654757;
+    m = lo ? m + m : m;
+    e = lo ? e - 1 : e;
+    const double f = m - 1.0;
+    const double s = f / (2.0 + f);
+    const double s2 = s * s;
+    double p = 0.09523809523809523;
+    p = fma(p, s2, 0.10526315789473684);
+    p = fma(p, s2, 0.11764705882352941);
+    p = fma(p, s2, 0.13333333333333333);
+    p = fma(p, s2, 0.15384615384615385);
+    p = fma(p, s2, 0.18181818181818182);
+    p = fma(p, s2, 0.2222222222222222);
+    p = fma(p, s2, 0.2857142857142857);
+    p = fma(p, s2, 0.4);
+    p = fma(p, s2, 0.6666666666666666);
+    const double l1 = fma(s * s2, p, s + s);
+    const double de = (double)e;
+    return fma(de, 0.6931471803691238, fma(de, 1.9082149292705877e-10, l1));
+}
+
+// (sin 2 pi t, cos 2 pi t) for t in [0,1]: exact quadrant reduction f = t - q/4 in [-1/8, 1/8],
+// Taylor polynomials of sin(2 pi f) (to f^17) and cos(2 pi f) (to f^18).
+NP8_HD void sincos_2pi(double t, double &sn, double &cs) {
+    const double q = rint(4.0 * t);
+    const double f = t - 0.25 * q;
+    const double f2 = f * f;
+    double ps = 0.10422916220813984;
+    ps = fma(ps, f2, -0.7181223017785006);
+    ps = fma(ps, f2, 3.819952584848282);
+    ps = fma(ps, f2, -15.09464257682299);
+    ps = fma(ps, f2, 42.058693944897655);
+    ps = fma(ps, f2, -76.70585975306139);
+    ps = fma(ps, f2, 81.60524927607506);
+    ps = fma(ps, f2, -41.34170224039976);
+    ps = fma(ps, f2, 6.283185307179586);
+    const double s0 = ps * f;
+    double pc = -0.03638284114254567;
+    pc = fma(pc, f2, 0.28200596845579123);
+    pc = fma(pc, f2, -1.714390711088672);
+    pc = fma(pc, f2, 7.903536371318469);
+    pc = fma(pc, f2, -26.4262567833744);
+    pc = fma(pc, f2, 60.24464137187666);
+    pc = fma(pc, f2, -85.45681720669373);
+    pc = fma(pc, f2, 64.9393940226683);
+    pc = fma(pc, f2, -19.739208802178716);
+    const double c0 = fma(pc, f2, 1.0);
+    const int qi = ((int)q) & 3;
+    const double a = (qi & 1) ? c0 : s0;
+    const double b = (qi & 1) ? s0 : c0;
+    sn = (qi & 2) ? -a : a;
+    cs = ((qi + 1) & 2) ? -b : b;
+}
+
+// Box-Muller pair from one Philox call: (r cos 2 pi u2, r sin 2 pi u2), r = sqrt(-2 log u1).
 NP8_HD void normal_pair(uint64_t seed, uint64_t i, uint32_t t, uint32_t stream, uint32_t call, double &g0,
                         double &g1) {
     uint32_t o[4];
     philox_call(seed, i, t, stream, call, o);
     const double u1 = u01(o[0], o[1]);
     const double u2 = u01(o[2], o[3]);
-    const double r = sqrt(-2.0 * log(u1));
-    const double th = kTwoPi * u2;
-    g0 = r * cos(th);
-    g1 = r * sin(th);
+    const double r = sqrt(-2.0 * log_pos(u1));
+    double sn, cs;
+    sincos_2pi(u2, sn, cs);
+    g0 = r * cs;
+    g1 = r * sn;
 }
+
+// Log-weight standing for weight 0 (a singleton's own cluster): finite, so no -inf arithmetic.
+constexpr double kZeroLogWeight = -1.0e300;
+// Candidates with log-weight <= running max - kSkip have exp() == 0 exactly and leave the draw's
+// state unchanged (DESIGN.md "Pick").
+constexpr double kSkip = 800.0;
 
 NP8_HD double uniform(uint64_t seed, uint64_t i, uint32_t t, uint32_t stream, uint32_t n) {
     uint32_t o[4];
@@ -121,72 +216,32 @@ NP8_HD uint32_t perm_apply(const Perm &P, uint32_t p) {
     return x;
 }
 
-NP8_HD double clamp_u(double u) {
-    u = (u < 0x1.0p-60) ? 0x1.0p-60 : u;
-    u = (u > 0x1.fffffffffffffp-1) ? 0x1.fffffffffffffp-1 : u;
-    return u;
-}
+NP8_HD double clamp_u(double u) { return fmin(fmax(u, 0x1.0p-60), 0x1.fffffffffffffp-1); }
 
-// Running state of the block-reservoir categorical draw (DESIGN.md "Pick").
+// State of the single-uniform weighted reservoir draw (DESIGN.md "Pick"): T running max log-weight,
+// S = sum of exp(lw - T) over the candidates taken into account, u ~ U(0,1) independent of pick.
 struct PickState {
-    double Tm, S, u;
+    double T, S, u;
     int32_t pick;
 };
 
-// One block of N candidate log-weights (entries beyond the live count are -inf).
-template <int N>
-NP8_HD void pick_block(PickState &st, const double (&lw)[N], int32_t base) {
-    double mb = -INFINITY;
-#pragma unroll
-    for (int j = 0; j < N; ++j) mb = fmax(mb, lw[j]);
-    if (mb == -INFINITY) return;
-    double e[N];
-    double Sb = 0.0;
-#pragma unroll
-    for (int j = 0; j < N; ++j) {
-        e[j] = exp(lw[j] - mb);
-        Sb = Sb + e[j];
-    }
-    double Sbs;
-    if (mb > st.Tm) {
-        st.S = st.S * exp(st.Tm - mb);
-        st.Tm = mb;
-        Sbs = Sb;
-    } else {
-        Sbs = Sb * exp(mb - st.Tm);
-    }
-    st.S = st.S + Sbs;
-    const double r = Sbs / st.S;
-    if (st.u < r) {
-        const double ui = st.u / r;
-        const double tgt = ui * Sb;
-        double cum = 0.0, lo = 0.0, ej = 1.0;
-        int pk = -1;
-#pragma unroll
-        for (int j = 0; j < N; ++j) {
-            const double prev = cum;
-            cum = cum + e[j];
-            const bool hit = (pk < 0) && (cum >= tgt);
-            pk = hit ? j : pk;
-            lo = hit ? prev : lo;
-            ej = hit ? e[j] : ej;
-        }
-        if (pk < 0) {  // rounding guard: last positive weight
-            cum = 0.0;
-#pragma unroll
-            for (int j = 0; j < N; ++j) {
-                const bool pos = e[j] > 0.0;
-                pk = pos ? j : pk;
-                lo = pos ? cum : lo;
-                ej = pos ? e[j] : ej;
-                cum = cum + e[j];
-            }
-        }
-        st.pick = base + pk;
-        st.u = clamp_u((tgt - lo) / ej);
-    } else {
-        st.u = clamp_u((st.u - r) / (1.0 - r));
-    }
+// Candidate j with log-weight lw.  Equal in distribution to an inverse-CDF draw over exp(lw)
+// (dim1algebra.hpp:2078-2104); one exp and one division, no stored weights.
+NP8_HD void pick_step(PickState &st, double lw, int32_t j) {
+    const double d = lw - st.T;
+    if (d <= -kSkip) return;
+    const bool gt = d > 0.0;
+    const double e = exp_le0(-fabs(d));
+    const double a = gt ? 1.0 : e;
+    const double S = gt ? fma(st.S, e, 1.0) : st.S + e;
+    const double uS = st.u * S;
+    const bool take = uS < a;
+    const double num = take ? uS : uS - a;
+    const double den = take ? a : S - a;
+    st.u = clamp_u(num / den);
+    st.pick = take ? j : st.pick;
+    st.T = gt ? lw : st.T;
+    st.S = S;
 }
 
 }  // namespace np8

@@ -47,6 +47,7 @@ struct AssignArgs {
     const double *X;   // [D][n_loc] (structure of arrays)
     int32_t *z;        // [n_loc] slot ids
     const double *cand;
+    const int32_t *dense_of;  // slot -> row of the candidate table
     const Ctl *ctl;
     const double *hyp; // mu0 | UinvT packed | caux | rsk | logam | nu
     const int64_t *order;
@@ -70,6 +71,7 @@ struct FinArgs {
     int64_t n_loc, offset;
     double *slot_mu, *slot_P, *slot_c, *slot_sigma;
     double *cand;
+    int32_t *dense_of;
     Ctl *ctl;
     const double *mu0, *LT, *Gp, *LTL;  // LT, LTL: D*D row-major; Gp packed
     double caux, rsk, nu;

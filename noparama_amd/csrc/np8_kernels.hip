@@ -32,24 +32,34 @@ struct HypView {
     static constexpr int kNu = kCaux + 3;
 };
 
-// ll = c - q/2 with q = d' P d over the packed upper triangle (off-diagonals pre-doubled).
+// ll = c - q/2 with q = d' P d.  Isotropic entries (iso > 0, a wave-uniform branch): q = iso * |d|^2;
+// otherwise the packed upper triangle with pre-doubled off-diagonals.
 template <int D>
 __device__ __forceinline__ double cand_ll(const double *__restrict__ e, const double (&x)[D]) {
     constexpr int DP = D * (D + 1) / 2;
     double d[D];
 #pragma unroll
     for (int a = 0; a < D; ++a) d[a] = x[a] - e[a];
-    const double *P = e + D;
-    double q = 0.0;
-    int k = 0;
+    const double iso = e[D + DP + kFieldIso];
+    double q;
+    if (iso > 0.0) {
+        double s = d[0] * d[0];
 #pragma unroll
-    for (int a = 0; a < D; ++a) {
-        double t = P[k++] * d[a];
+        for (int a = 1; a < D; ++a) s = fma(d[a], d[a], s);
+        q = s * iso;
+    } else {
+        const double *P = e + D;
+        q = 0.0;
+        int k = 0;
 #pragma unroll
-        for (int b = a + 1; b < D; ++b) t = fma(P[k++], d[b], t);
-        q = fma(t, d[a], q);
+        for (int a = 0; a < D; ++a) {
+            double t = P[k++] * d[a];
+#pragma unroll
+            for (int b = a + 1; b < D; ++b) t = fma(P[k++], d[b], t);
+            q = fma(t, d[a], q);
+        }
     }
-    return fma(-0.5, q, e[D + DP]);
+    return fma(-0.5, q, e[D + DP + kFieldC]);
 }
 
 // y0 = (L^T)^{-1} (x - mu0): the item in the whitened frame of the base measure.
@@ -94,25 +104,8 @@ __device__ __forceinline__ double aux_ll(const double *__restrict__ hyp, const d
         }
     }
     const double q = r2 / (v * v);
-    const double cm = fma(-(double)D, log(fabs(v)), caux);
+    const double cm = fma(-(double)D, log_pos(fabs(v)), caux);
     return fma(-0.5, q, cm);
-}
-
-// One step of the single-uniform weighted reservoir (DESIGN.md "Pick"): candidate j with log-weight l.
-__device__ __forceinline__ void pick_step(PickState &st, double l, int32_t j) {
-    if (l == -INFINITY) return;  // zero weight: can never be drawn, state unchanged
-    const bool gt = l > st.Tm;
-    const double e = exp(gt ? (st.Tm - l) : (l - st.Tm));
-    const double a = gt ? 1.0 : e;
-    const double S = gt ? fma(st.S, e, 1.0) : st.S + e;
-    const double uS = st.u * S;
-    const bool take = uS < a;
-    const double num = take ? uS : uS - a;
-    const double den = take ? a : S - a;
-    st.u = clamp_u(num / den);
-    st.pick = take ? j : st.pick;
-    st.Tm = gt ? l : st.Tm;
-    st.S = S;
 }
 
 __device__ __forceinline__ int64_t position_to_local(const AssignArgs &A, int64_t p) {
@@ -124,7 +117,8 @@ __device__ __forceinline__ int64_t position_to_local(const AssignArgs &A, int64_
 template <int D, int M>
 __global__ __launch_bounds__(256) void np8_assign(AssignArgs A) {
     constexpr int DP = D * (D + 1) / 2;
-    constexpr int CS = (D + DP + 4 + 1) & ~1;
+    constexpr int CS = (D + DP + 5 + 1) & ~1;
+    constexpr int F = D + DP;
     const int64_t p = A.p0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= A.p1) return;
     const int64_t il = position_to_local(A, p);
@@ -138,18 +132,23 @@ __global__ __launch_bounds__(256) void np8_assign(AssignArgs A) {
     for (int a = 0; a < D; ++a) x[a] = X[(int64_t)a * A.n_loc + il];
     const int32_t zi = A.z[il];
 
+    // The item's own cluster enters the draw first (weight n_k - 1): its log-weight is a lower bound
+    // of the final maximum, so every later candidate more than kSkip below it is skipped exactly.
+    const int32_t jo = A.dense_of[zi];
     PickState st;
-    st.Tm = -INFINITY;
-    st.S = 0.0;
-    st.u = uniform(A.seed, ig, A.t, kStreamPick, 0);
-    st.pick = 0;
-
+    {
+        const double *eo = cand + (int64_t)jo * CS;
+        st.T = cand_ll<D>(eo, x) + eo[F + kFieldLogn1];
+        st.S = 1.0;
+        st.u = uniform(A.seed, ig, A.t, kStreamPick, 0);
+        st.pick = jo;
+    }
+    const double zslot = (double)zi;
     const int K = A.ctl->K;
     for (int j = 0; j < K; ++j) {
-        const double *e = cand + (int64_t)j * CS;
-        const double ll = cand_ll<D>(e, x);
-        const int32_t slot = (int32_t)e[D + DP + 3];
-        pick_step(st, ll + ((slot == zi) ? e[D + DP + 2] : e[D + DP + 1]), j);
+        const double *e = cand + (int64_t)j * CS;  // wave-uniform: scalar loads
+        const double lw = cand_ll<D>(e, x) + e[F + kFieldLogn];
+        if (e[F + kFieldSlot] != zslot) pick_step(st, lw, j);
     }
     {
         double y0[D];
@@ -162,7 +161,7 @@ __global__ __launch_bounds__(256) void np8_assign(AssignArgs A) {
     RecHeader *hdr = reinterpret_cast<RecHeader *>(A.rec);
     int32_t *delta = reinterpret_cast<int32_t *>(A.rec + kRecHeaderBytes);
     if (st.pick < K) {
-        const int32_t s = (int32_t)cand[(int64_t)st.pick * CS + D + DP + 3];
+        const int32_t s = (int32_t)cand[(int64_t)st.pick * CS + F + kFieldSlot];
         if (s != zi) {
             atomicSub(delta + zi, 1);
             atomicAdd(delta + s, 1);
@@ -263,7 +262,7 @@ __device__ void write_new_slot(const FinArgs &F, const Request &r, int s) {
     }
     const double v2 = v * v;
     for (int k = 0; k < DP; ++k) F.slot_P[(int64_t)s * DP + k] = F.Gp[k] / v2;
-    F.slot_c[s] = fma(-(double)D, log(fabs(v)), F.caux);
+    F.slot_c[s] = fma(-(double)D, log_pos(fabs(v)), F.caux);
     for (int k = 0; k < D * D; ++k) F.slot_sigma[(int64_t)s * D * D + k] = v2 * F.LTL[k];
 }
 
@@ -374,14 +373,21 @@ __global__ __launch_bounds__(kFinThreads) void np8_finalize(FinArgs F) {
     for (int s = s0; s < s1; ++s) {
         const int c = cnt_s[s];
         F.cnt[s] = c;
+        F.dense_of[s] = (c > 0) ? k : -1;
         if (c > 0) {
             double *e = F.cand + (int64_t)k * CS;
+            const double *P = F.slot_P + (int64_t)s * DP;
             for (int a = 0; a < D; ++a) e[a] = F.slot_mu[(int64_t)s * D + a];
-            for (int a = 0; a < DP; ++a) e[D + a] = F.slot_P[(int64_t)s * DP + a];
-            e[D + DP] = F.slot_c[s];
-            e[D + DP + 1] = log((double)c);
-            e[D + DP + 2] = (c > 1) ? log((double)(c - 1)) : -INFINITY;
-            e[D + DP + 3] = (double)s;
+            // isotropic precision: off-diagonals exactly 0 and one common diagonal value
+            bool iso = true;
+            for (int a = 0, q = 0; a < D; ++a)
+                for (int b = a; b < D; ++b, ++q) iso = iso && ((a == b) ? (P[q] == P[0]) : (P[q] == 0.0));
+            for (int a = 0; a < DP; ++a) e[D + a] = P[a];
+            e[D + DP + kFieldC] = F.slot_c[s];
+            e[D + DP + kFieldLogn] = log_pos((double)c);
+            e[D + DP + kFieldLogn1] = (c > 1) ? log_pos((double)(c - 1)) : kZeroLogWeight;
+            e[D + DP + kFieldSlot] = (double)s;
+            e[D + DP + kFieldIso] = iso ? P[0] : 0.0;
             ++k;
         }
     }
@@ -470,7 +476,7 @@ template <int D, int M>
 __global__ __launch_bounds__(256) void np8_loglik_matrix_kernel(AssignArgs A, const int64_t *__restrict__ idx,
                                                                 int64_t n, double *__restrict__ out) {
     constexpr int DP = D * (D + 1) / 2;
-    constexpr int CS = (D + DP + 4 + 1) & ~1;
+    constexpr int CS = (D + DP + 5 + 1) & ~1;
     const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= n) return;
     const int64_t il = idx[r];

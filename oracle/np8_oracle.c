@@ -53,16 +53,81 @@ static void philox_call(uint64_t seed, uint64_t i, uint32_t t, uint32_t stream, 
     np8o_philox4x32_10(ctr, key, out);
 }
 
-/* Box-Muller pair from one Philox call: (r cos th, r sin th). */
+/* ---- elementary functions of the specification (DESIGN.md "Math"): the same polynomials the HIP
+ * code evaluates, so host and device agree to the bit. ------------------------------------------- */
+
+/* exp(x) for x <= 0: Cody-Waite reduction by ln2, degree-13 Taylor on |r| <= ln2/2, ldexp. */
+double np8o_exp_le0(double x) {
+    x = fmax(x, -800.0);
+    const double k = rint(x * 1.4426950408889634);
+    double r = fma(-k, 0.6931471803691238, x);
+    r = fma(-k, 1.9082149292705877e-10, r);
+    static const double C[14] = {1.6059043836821613e-10, 2.08767569878681e-09, 2.505210838544172e-08,
+                                 2.755731922398589e-07,  2.7557319223985893e-06, 2.48015873015873e-05,
+                                 0.0001984126984126984,  0.001388888888888889,  0.008333333333333333,
+                                 0.041666666666666664,   0.16666666666666666,   0.5,
+                                 1.0,                    1.0};
+    double p = C[0];
+    for (int n = 1; n < 14; ++n) p = fma(p, r, C[n]);
+    return ldexp(p, (int)k);
+}
+
+/* log(u), u > 0 normal: log1p(m-1) = 2 atanh((m-1)/(m+1)) with m in [1/sqrt2, sqrt2). */
+double np8o_log_pos(double u) {
+    int e;
+    double m = frexp(u, &e);
+    const int lo = m < 0.70710678118654757;
+    m = lo ? m + m : m;
+    e = lo ? e - 1 : e;
+    const double f = m - 1.0;
+    const double s = f / (2.0 + f);
+    const double s2 = s * s;
+    static const double A[10] = {0.09523809523809523, 0.10526315789473684, 0.11764705882352941, 0.13333333333333333,
+                                 0.15384615384615385, 0.18181818181818182, 0.2222222222222222,  0.2857142857142857,
+                                 0.4,                 0.6666666666666666};
+    double p = A[0];
+    for (int n = 1; n < 10; ++n) p = fma(p, s2, A[n]);
+    const double l1 = fma(s * s2, p, s + s);
+    const double de = (double)e;
+    return fma(de, 0.6931471803691238, fma(de, 1.9082149292705877e-10, l1));
+}
+
+/* (sin 2 pi t, cos 2 pi t), t in [0,1]: exact reduction to f in [-1/8,1/8] and Taylor polynomials. */
+void np8o_sincos_2pi(double t, double *sn, double *cs) {
+    const double q = rint(4.0 * t);
+    const double f = t - 0.25 * q;
+    const double f2 = f * f;
+    static const double S[9] = {0.10422916220813984, -0.7181223017785006, 3.819952584848282,
+                                -15.09464257682299,  42.058693944897655,  -76.70585975306139,
+                                81.60524927607506,   -41.34170224039976,  6.283185307179586};
+    static const double Cc[10] = {-0.03638284114254567, 0.28200596845579123, -1.714390711088672,
+                                  7.903536371318469,    -26.4262567833744,   60.24464137187666,
+                                  -85.45681720669373,   64.9393940226683,    -19.739208802178716,
+                                  1.0};
+    double ps = S[0];
+    for (int n = 1; n < 9; ++n) ps = fma(ps, f2, S[n]);
+    const double s0 = ps * f;
+    double pc = Cc[0];
+    for (int n = 1; n < 10; ++n) pc = fma(pc, f2, Cc[n]);
+    const double c0 = pc;
+    const int qi = ((int)q) & 3;
+    const double a = (qi & 1) ? c0 : s0;
+    const double b = (qi & 1) ? s0 : c0;
+    *sn = (qi & 2) ? -a : a;
+    *cs = ((qi + 1) & 2) ? -b : b;
+}
+
+/* Box-Muller pair from one Philox call: (r cos 2 pi u2, r sin 2 pi u2), r = sqrt(-2 log u1). */
 static void normal_pair(uint64_t seed, uint64_t i, uint32_t t, uint32_t stream, uint32_t call, double g[2]) {
     uint32_t o[4];
     philox_call(seed, i, t, stream, call, o);
     double u1 = np8o_u01(o[0], o[1]);
     double u2 = np8o_u01(o[2], o[3]);
-    double r = sqrt(-2.0 * log(u1));
-    double th = TWO_PI * u2;
-    g[0] = r * cos(th);
-    g[1] = r * sin(th);
+    double r = sqrt(-2.0 * np8o_log_pos(u1));
+    double sn, cs;
+    np8o_sincos_2pi(u2, &sn, &cs);
+    g[0] = r * cs;
+    g[1] = r * sn;
 }
 
 double np8o_normal(uint64_t seed, uint64_t i, uint32_t t, uint32_t stream, uint32_t n) {
@@ -303,8 +368,8 @@ struct np8o_ctx {
     int32_t *cnt;
     /* dense candidate table (ascending slot order) */
     int32_t K;
-    int32_t *live;
-    double *logn, *logn1;
+    int32_t *live, *dense_of;
+    double *logn, *logn1, *iso;
     uint32_t t;
     /* max likelihood (np_mcmc.cpp:187-203) */
     double best_L;
@@ -382,6 +447,8 @@ np8o_ctx *np8o_create(const np8o_config *cfg) {
     c->live = (int32_t *)calloc((size_t)K, sizeof(int32_t));
     c->logn = (double *)calloc((size_t)K, sizeof(double));
     c->logn1 = (double *)calloc((size_t)K, sizeof(double));
+    c->iso = (double *)calloc((size_t)K, sizeof(double));
+    c->dense_of = (int32_t *)calloc((size_t)K, sizeof(int32_t));
     c->cnt_best = (int32_t *)calloc((size_t)K, sizeof(int32_t));
     c->mu_best = (double *)calloc((size_t)K * D, sizeof(double));
     c->sigma_best = (double *)calloc((size_t)K * D * D, sizeof(double));
@@ -403,6 +470,8 @@ void np8o_destroy(np8o_ctx *c) {
     free(c->live);
     free(c->logn);
     free(c->logn1);
+    free(c->iso);
+    free(c->dense_of);
     free(c->cnt_best);
     free(c->mu_best);
     free(c->sigma_best);
@@ -471,7 +540,7 @@ static void slot_from_aux(np8o_ctx *c, int s, double v, const double *mu) {
     double *P = c->slot_P + (size_t)s * c->DP;
     for (int a = 0; a < D; ++a)
         for (int b = a; b < D; ++b) P[packed_index(D, a, b)] = c->Gp[a * D + b] / v2;
-    c->slot_c[s] = fma(-(double)D, log(fabs(v)), c->caux);
+    c->slot_c[s] = fma(-(double)D, np8o_log_pos(fabs(v)), c->caux);
     double *S = c->slot_sigma + (size_t)s * D * D;
     for (int k = 0; k < D * D; ++k) S[k] = v2 * c->LTL[k];
 }
@@ -491,15 +560,29 @@ static void aux_draws(const np8o_ctx *c, uint64_t i, uint32_t t, double *v, doub
     }
 }
 
+/* Candidate table: live slots in ascending order, log n_k, log(n_k - 1) (weight 0 as the finite
+ * NP8O_ZERO_LW), and the isotropy flag (off-diagonals of P' exactly 0, one common diagonal). */
+#define NP8O_ZERO_LW (-1.0e300)
+#define NP8O_SKIP 800.0
+
 static void rebuild_dense(np8o_ctx *c) {
     int K = 0;
-    for (int s = 0; s < c->kcap; ++s)
+    const int D = c->D;
+    for (int s = 0; s < c->kcap; ++s) {
+        c->dense_of[s] = -1;
         if (c->cnt[s] > 0) {
+            const double *P = c->slot_P + (size_t)s * c->DP;
+            int iso = 1;
+            for (int a = 0, q = 0; a < D; ++a)
+                for (int b = a; b < D; ++b, ++q) iso = iso && ((a == b) ? (P[q] == P[0]) : (P[q] == 0.0));
+            c->dense_of[s] = K;
             c->live[K] = s;
-            c->logn[K] = log((double)c->cnt[s]);
-            c->logn1[K] = (c->cnt[s] > 1) ? log((double)(c->cnt[s] - 1)) : -INFINITY;
+            c->logn[K] = np8o_log_pos((double)c->cnt[s]);
+            c->logn1[K] = (c->cnt[s] > 1) ? np8o_log_pos((double)(c->cnt[s] - 1)) : NP8O_ZERO_LW;
+            c->iso[K] = iso ? P[0] : 0.0;
             ++K;
         }
+    }
     c->K = K;
 }
 
@@ -581,10 +664,27 @@ static inline double quad_form(const np8o_ctx *c, const double *x, const double 
     return q;
 }
 
-/* ll of point x under slot s, table form. */
+/* ll of point x under slot s, packed table form (the max-likelihood sum, np_mcmc.cpp:187-203). */
 static inline double slot_ll(const np8o_ctx *c, const double *x, int s) {
     double q = quad_form(c, x, c->slot_mu + (size_t)s * c->D, c->slot_P + (size_t)s * c->DP);
     return fma(-0.5, q, c->slot_c[s]);
+}
+
+/* ll of point x under candidate row j (what the sweep uses): isotropic rows q = iso |d|^2. */
+static inline double cand_ll(const np8o_ctx *c, const double *x, int j) {
+    const int s = c->live[j];
+    if (c->iso[j] > 0.0) {
+        const int D = c->D;
+        const double *mu = c->slot_mu + (size_t)s * D;
+        double d0 = x[0] - mu[0];
+        double acc = d0 * d0;
+        for (int a = 1; a < D; ++a) {
+            const double d = x[a] - mu[a];
+            acc = fma(d, d, acc);
+        }
+        return fma(-0.5, acc * c->iso[j], c->slot_c[s]);
+    }
+    return slot_ll(c, x, s);
 }
 
 /* ll of point x under its M auxiliary draws, factored form (DESIGN.md "G0"). */
@@ -609,31 +709,29 @@ static void aux_ll(const np8o_ctx *c, const double *x, uint64_t i, uint32_t t, d
             r2 = fma(e, e, r2);
         }
         double q = r2 / (v * v);
-        double cm = fma(-(double)D, log(fabs(v)), c->caux);
+        double cm = fma(-(double)D, np8o_log_pos(fabs(v)), c->caux);
         ll[m] = fma(-0.5, q, cm);
     }
 }
 
 /* ---- categorical draw: single-uniform weighted reservoir (DESIGN.md "Pick") ------------------
  * Equal in distribution to dim1algebra.hpp:2078-2104 (inverse CDF over the linear weights) but one
- * pass: state (Tm, S, u) with S = sum of exp(l_j - Tm) so far and u ~ U(0,1) independent of the
+ * pass: state (T, S, u) with S = sum of exp(lw_j - T) so far and u ~ U(0,1) independent of the
  * current pick; candidate j replaces the pick with probability w_j / S_new and u is renormalised
- * into the chosen sub-interval. */
+ * into the chosen sub-interval.  A candidate with lw <= T - 800 has exp(lw - T) == 0 in double and
+ * leaves the state unchanged. */
 typedef struct {
-    double Tm, S, u;
+    double T, S, u;
     int32_t pick;
 } pick_state;
 
-static inline double clamp_u(double u) {
-    if (u < 0x1.0p-60) u = 0x1.0p-60;
-    if (u > 0x1.fffffffffffffp-1) u = 0x1.fffffffffffffp-1;
-    return u;
-}
+static inline double clamp_u(double u) { return fmin(fmax(u, 0x1.0p-60), 0x1.fffffffffffffp-1); }
 
-static inline void pick_step(pick_state *st, double l, int32_t j) {
-    if (l == -INFINITY) return;
-    const int gt = l > st->Tm;
-    const double e = exp(gt ? (st->Tm - l) : (l - st->Tm));
+static inline void pick_step(pick_state *st, double lw, int32_t j) {
+    const double d = lw - st->T;
+    if (d <= -NP8O_SKIP) return;
+    const int gt = d > 0.0;
+    const double e = np8o_exp_le0(-fabs(d));
     const double a = gt ? 1.0 : e;
     const double S = gt ? fma(st->S, e, 1.0) : st->S + e;
     const double uS = st->u * S;
@@ -642,20 +740,26 @@ static inline void pick_step(pick_state *st, double l, int32_t j) {
     const double den = take ? a : S - a;
     st->u = clamp_u(num / den);
     if (take) st->pick = j;
-    if (gt) st->Tm = l;
+    if (gt) st->T = lw;
     st->S = S;
 }
 
-/* One Neal-8 step for point i against the frozen candidate table (np_neal_algorithm8.cpp:60-130):
- * existing clusters in ascending slot order with weight n_{-i,k}, then the M auxiliaries with
- * weight alpha/M.  Returns the candidate index (< K existing, >= K auxiliary). */
+/* One Neal-8 step for point i against the frozen candidate table (np_neal_algorithm8.cpp:60-130).
+ * Order of the draw: the item's own cluster first (weight n_k - 1; 0 for a singleton, whose cluster
+ * the reference deletes on retract, membertrix.cpp:200-203), then every other live cluster in
+ * ascending slot order (weight n_k), then the M auxiliaries (weight alpha/M).  Returns the candidate
+ * row (< K existing, >= K auxiliary). */
 static int32_t choose(const np8o_ctx *c, int64_t i, const double *x, int32_t zi) {
     const int K = c->K, M = c->M;
-    pick_state st = {-INFINITY, 0.0, np8o_uniform(c->cfg.seed, (uint64_t)i, c->t, NP8O_STREAM_PICK, 0), 0};
+    const int jo = c->dense_of[zi];
+    pick_state st;
+    st.T = cand_ll(c, x, jo) + c->logn1[jo];
+    st.S = 1.0;
+    st.u = np8o_uniform(c->cfg.seed, (uint64_t)i, c->t, NP8O_STREAM_PICK, 0);
+    st.pick = jo;
     for (int j = 0; j < K; ++j) {
-        int s = c->live[j];
-        double ll = slot_ll(c, x, s);
-        pick_step(&st, ll + ((s == zi) ? c->logn1[j] : c->logn[j]), j);
+        if (j == jo) continue;
+        pick_step(&st, cand_ll(c, x, j) + c->logn[j], j);
     }
     double lla[NP8O_MMAX];
     aux_ll(c, x, (uint64_t)i, c->t, lla);
@@ -855,7 +959,7 @@ int np8o_loglik_matrix(np8o_ctx *c, const int64_t *idx, int64_t n, double *out) 
         int64_t i = idx[r];
         if (i < 0 || i >= c->N) return -3;
         const double *x = c->X + (size_t)i * c->D;
-        for (int j = 0; j < K; ++j) out[r * (K + M) + j] = slot_ll(c, x, c->live[j]);
+        for (int j = 0; j < K; ++j) out[r * (K + M) + j] = cand_ll(c, x, j);
         aux_ll(c, x, (uint64_t)i, c->t, out + r * (K + M) + K);
     }
     return 0;

@@ -47,6 +47,10 @@ double np8o_u01(uint32_t hi, uint32_t lo);
 double np8o_normal(uint64_t seed, uint64_t i, uint32_t t, uint32_t stream, uint32_t n);
 double np8o_uniform(uint64_t seed, uint64_t i, uint32_t t, uint32_t stream, uint32_t n);
 uint32_t np8o_perm(uint64_t seed, uint32_t t, uint32_t N, uint32_t p);
+/* Elementary functions of the specification (identical polynomials in the HIP code). */
+double np8o_exp_le0(double x);
+double np8o_log_pos(double u);
+void np8o_sincos_2pi(double t, double *sn, double *cs);
 
 /* ---- faithful reference restatements ------------------------------------------------------- */
 /* multivariatenormal.cpp:64-94 (clustering branch :82-93): exp(-0.5 d'Inv d)/sqrt((2pi)^D det). */

@@ -103,6 +103,32 @@ def test_lu_inverse_vs_numpy():
         assert abs(det.value - np.linalg.det(A)) < 1e-9 * abs(np.linalg.det(A))
 
 
+def test_spec_math_accuracy():
+    """exp_le0 / log_pos / sincos_2pi (DESIGN.md "Math") against numpy over their domains."""
+    import ctypes as C
+
+    L = O.lib()
+    L.np8o_exp_le0.argtypes = [C.c_double]
+    L.np8o_exp_le0.restype = C.c_double
+    L.np8o_log_pos.argtypes = [C.c_double]
+    L.np8o_log_pos.restype = C.c_double
+    L.np8o_sincos_2pi.argtypes = [C.c_double, C.c_void_p, C.c_void_p]
+    rng = np.random.default_rng(11)
+    xs = -rng.random(20000) * 740.0
+    ex = np.array([L.np8o_exp_le0(float(x)) for x in xs])
+    np.testing.assert_allclose(ex, np.exp(xs), rtol=4e-16 * 4, atol=0)
+    assert L.np8o_exp_le0(float("-inf")) == 0.0 and L.np8o_exp_le0(0.0) == 1.0
+    us = (np.floor(rng.random(20000) * 2**53) + 1) * 2.0**-53
+    lg = np.array([L.np8o_log_pos(float(u)) for u in us])
+    np.testing.assert_allclose(lg, np.log(us), rtol=5e-16, atol=0)
+    sn, cs = C.c_double(), C.c_double()
+    err = 0.0
+    for t in us[:5000]:
+        L.np8o_sincos_2pi(float(t), C.byref(sn), C.byref(cs))
+        err = max(err, abs(sn.value - np.sin(2 * np.pi * t)), abs(cs.value - np.cos(2 * np.pi * t)))
+    assert err < 1e-15
+
+
 def test_uniforms_open_interval_and_normals_moments():
     us = np.array([O.uniform(1, i, 0, 2, 0) for i in range(20000)])
     assert us.min() > 0.0 and us.max() < 1.0
