@@ -52,7 +52,8 @@ struct np8_ctx {
     bool own_stream = false;
     double *X = nullptr;
     int32_t *z = nullptr, *z_best = nullptr;
-    double *slot_mu = nullptr, *slot_P = nullptr, *slot_c = nullptr, *slot_sigma = nullptr;
+    double *slot_mu = nullptr, *slot_P = nullptr, *slot_c = nullptr, *slot_sigma = nullptr, *slot_iso = nullptr;
+    double gp_iso = 0.0;
     int32_t *cnt = nullptr, *cnt_best = nullptr;
     double *mu_best = nullptr, *sigma_best = nullptr;
     double *cand = nullptr;
@@ -65,13 +66,23 @@ struct np8_ctx {
     int64_t order_cap = 0;
     double *partial = nullptr;
     int64_t partial_cap = 0;
+    // label-sorted layout (double-buffered) for the synchronous sweep
+    double *Xs[2] = {nullptr, nullptr};
+    int32_t *zs[2] = {nullptr, nullptr}, *ids[2] = {nullptr, nullptr};
+    int32_t *s_hist = nullptr, *s_cursor = nullptr, *s_off = nullptr;
+    bool use_sorted = false;
+    bool sorted_valid = false;
+    uint32_t sorted_epoch = 0;
+    uint32_t resort_every = 4;
     // multi-GPU
     ncclComm_t comm = nullptr;
     int rank = 0, world = 1;
     // timing
     bool timing = false;
     std::vector<Timer> timers;
+    std::vector<hipEvent_t> event_pool;
     double ms[3] = {0, 0, 0};
+    int64_t n_timed[3] = {0, 0, 0};
     std::string err;
 };
 
@@ -187,6 +198,10 @@ bool prepare_base(np8_ctx *c) {
     c->caux = -0.5 * (double)D * kLog2PiC - sumlog;
     c->rsk = 1.0 / std::sqrt(c->kappa);
     c->logam = std::log(c->alpha / (double)c->M);
+    bool iso = true;
+    for (int a = 0; a < D; ++a)
+        for (int b = 0; b < D; ++b) iso = iso && ((a == b) ? c->Gp[a * D + b] == c->Gp[0] : c->Gp[a * D + b] == 0.0);
+    c->gp_iso = iso ? c->Gp[0] : 0.0;
     return true;
 }
 
@@ -235,9 +250,16 @@ void free_device(np8_ctx *c) {
     void *ptrs[] = {c->X,      c->z,       c->z_best, c->slot_mu, c->slot_P,  c->slot_c,  c->slot_sigma,
                     c->cnt,    c->cnt_best, c->mu_best, c->sigma_best, c->cand, c->ctl,    c->hyp,
                     c->d_mu0,  c->d_LT,    c->d_Gp,   c->d_LTL,   c->rec,     c->gath,    c->order,
-                    c->partial, c->dense_of};
+                    c->partial, c->dense_of, c->Xs[0], c->Xs[1], c->zs[0], c->zs[1], c->ids[0], c->ids[1],
+                    c->s_hist, c->s_cursor, c->s_off, c->slot_iso};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
+    for (int b = 0; b < 2; ++b) {
+        c->Xs[b] = nullptr;
+        c->zs[b] = c->ids[b] = nullptr;
+    }
+    c->s_hist = c->s_cursor = c->s_off = nullptr;
+    c->slot_iso = nullptr;
     c->X = nullptr;
     c->z = c->z_best = nullptr;
     c->slot_mu = c->slot_P = c->slot_c = c->slot_sigma = nullptr;
@@ -265,13 +287,20 @@ int dalloc(np8_ctx *c, T **p, size_t n) {
 int upload_slots(np8_ctx *c, const std::vector<SlotHost> &slots, const std::vector<int32_t> &cnt) {
     const int D = c->D, DP = c->DP, K = (int)slots.size();
     std::vector<double> mu((size_t)c->kcap * D, 0.0), P((size_t)c->kcap * DP, 0.0), cc(c->kcap, 0.0),
-        sg((size_t)c->kcap * D * D, 0.0);
+        sg((size_t)c->kcap * D * D, 0.0), iso(c->kcap, 0.0);
     for (int s = 0; s < K; ++s) {
         std::memcpy(&mu[(size_t)s * D], slots[s].mu.data(), sizeof(double) * D);
         std::memcpy(&P[(size_t)s * DP], slots[s].P.data(), sizeof(double) * DP);
         std::memcpy(&sg[(size_t)s * D * D], slots[s].sigma.data(), sizeof(double) * D * D);
         cc[s] = slots[s].c;
+        // isotropic precision: off-diagonals exactly 0 and one common diagonal (DESIGN.md "Pick")
+        bool is = true;
+        for (int a = 0, q = 0; a < D; ++a)
+            for (int b = a; b < D; ++b, ++q)
+                is = is && ((a == b) ? slots[s].P[q] == slots[s].P[0] : slots[s].P[q] == 0.0);
+        iso[s] = is ? slots[s].P[0] : 0.0;
     }
+    HIPC(c, hipMemcpyAsync(c->slot_iso, iso.data(), sizeof(double) * iso.size(), hipMemcpyHostToDevice, c->stream));
     std::vector<int32_t> cn(c->kcap, 0);
     for (int s = 0; s < K; ++s) cn[s] = cnt[s];
     HIPC(c, hipMemcpyAsync(c->slot_mu, mu.data(), sizeof(double) * mu.size(), hipMemcpyHostToDevice, c->stream));
@@ -283,10 +312,22 @@ int upload_slots(np8_ctx *c, const std::vector<SlotHost> &slots, const std::vect
     return NP8_OK;
 }
 
+// Device timing: event pairs from a reusable pool (no event creation on the launch path).
+void collect_timers(np8_ctx *c);
+
 void timer_begin(np8_ctx *c, int phase, Timer &t) {
     if (!c->timing) return;
-    (void)hipEventCreate(&t.a);
-    (void)hipEventCreate(&t.b);
+    if (c->timers.size() + 1 >= 4096) collect_timers(c);  // bounded pool
+    const size_t k = c->timers.size();
+    if (c->event_pool.size() < 2 * (k + 1)) {
+        hipEvent_t a, b;
+        (void)hipEventCreate(&a);
+        (void)hipEventCreate(&b);
+        c->event_pool.push_back(a);
+        c->event_pool.push_back(b);
+    }
+    t.a = c->event_pool[2 * k];
+    t.b = c->event_pool[2 * k + 1];
     t.phase = phase;
     (void)hipEventRecord(t.a, c->stream);
 }
@@ -298,11 +339,13 @@ void timer_end(np8_ctx *c, Timer &t) {
 }
 
 void collect_timers(np8_ctx *c) {
+    if (!c->timers.empty()) (void)hipEventSynchronize(c->timers.back().b);
     for (Timer &t : c->timers) {
         float ms = 0.0f;
-        if (hipEventElapsedTime(&ms, t.a, t.b) == hipSuccess) c->ms[t.phase] += ms;
-        (void)hipEventDestroy(t.a);
-        (void)hipEventDestroy(t.b);
+        if (hipEventElapsedTime(&ms, t.a, t.b) == hipSuccess) {
+            c->ms[t.phase] += ms;
+            c->n_timed[t.phase] += 1;
+        }
     }
     c->timers.clear();
 }
@@ -319,12 +362,16 @@ FinArgs fin_args(np8_ctx *c, const unsigned char *recs, int world) {
     F.M = c->M;
     F.cnt = c->cnt;
     F.z = c->z;
+    F.zs[0] = c->use_sorted ? c->zs[0] : nullptr;
+    F.zs[1] = c->use_sorted ? c->zs[1] : nullptr;
     F.n_loc = c->n_loc;
     F.offset = c->offset;
     F.slot_mu = c->slot_mu;
     F.slot_P = c->slot_P;
     F.slot_c = c->slot_c;
     F.slot_sigma = c->slot_sigma;
+    F.slot_iso = c->slot_iso;
+    F.gp_iso = c->gp_iso;
     F.cand = c->cand;
     F.dense_of = c->dense_of;
     F.ctl = c->ctl;
@@ -344,6 +391,12 @@ AssignArgs assign_args(np8_ctx *c, int64_t p0, int64_t p1, const int64_t *order,
     AssignArgs A;
     A.X = c->X;
     A.z = c->z;
+    A.sorted = c->use_sorted ? 1 : 0;
+    for (int b = 0; b < 2; ++b) {
+        A.Xs[b] = c->Xs[b];
+        A.zs[b] = c->zs[b];
+        A.ids[b] = c->ids[b];
+    }
     A.cand = c->cand;
     A.dense_of = c->dense_of;
     A.ctl = c->ctl;
@@ -385,8 +438,44 @@ int launch_assign(np8_ctx *c, int64_t p0, int64_t p1, const int64_t *order, bool
     return NP8_OK;
 }
 
-// One synchronous step over local positions [p0,p1): assign, exchange, finalize.
+// Label-sorted layout for the synchronous sweep: rebuilt from the item-order arrays when stale
+// (after a state upload or a chunked / per-item step), refreshed from itself every resort_every
+// sweeps so that items that moved cluster rejoin their group.
+int prepare_sorted(np8_ctx *c) {
+    const bool stale = !c->sorted_valid;
+    if (!stale && c->epoch - c->sorted_epoch < c->resort_every) return NP8_OK;
+    SortArgs S;
+    S.X = c->X;
+    S.z = c->z;
+    for (int b = 0; b < 2; ++b) {
+        S.Xs[b] = c->Xs[b];
+        S.zs[b] = c->zs[b];
+        S.ids[b] = c->ids[b];
+    }
+    S.hist = c->s_hist;
+    S.cursor = c->s_cursor;
+    S.off = c->s_off;
+    S.ctl = c->ctl;
+    S.n = c->n_loc;
+    S.kcap = c->kcap;
+    S.D = c->D;
+    S.force = stale ? 1 : 0;  // otherwise the device re-sorts only if > n/32 items moved
+    HIPC(c, np8_launch_resort(S, c->stream));
+    c->sorted_valid = true;
+    c->sorted_epoch = c->epoch;
+    return NP8_OK;
+}
+
+// One synchronous step over local positions [p0,p1): assign, exchange, finalize.  A whole-sweep
+// step (no order, no permutation) runs on the label-sorted layout.
 int step(np8_ctx *c, int64_t p0, int64_t p1, const int64_t *order, bool use_perm) {
+    c->use_sorted = (order == nullptr) && !use_perm && p0 == 0 && p1 == c->n_loc && c->n_loc > 0;
+    if (c->use_sorted) {
+        int r = prepare_sorted(c);
+        if (r) return r;
+    } else {
+        c->sorted_valid = false;
+    }
     int r = launch_assign(c, p0, p1, order, use_perm);
     if (r) return r;
     if (c->world > 1) {
@@ -416,9 +505,8 @@ int launch_total_loglik(np8_ctx *c) {
     LoglikArgs A;
     A.X = c->X;
     A.z = c->z;
-    A.slot_mu = c->slot_mu;
-    A.slot_P = c->slot_P;
-    A.slot_c = c->slot_c;
+    A.cand = c->cand;
+    A.dense_of = c->dense_of;
     A.partial = c->partial;
     A.n_loc = c->n_loc;
     HIPC(c, np8_launch_loglik(A, c->D, c->stream));
@@ -498,6 +586,10 @@ int np8_create(np8_ctx **out, const np8_config *cfg) {
     c->DP = packed_size(c->D);
     c->CS = cand_stride(c->D);
     c->kcap = cfg->kcap > 0 ? cfg->kcap : 2048;
+    if (c->kcap > 12288) {  // np8_finalize keeps two int[kcap] arrays in LDS beside 64 KB of request space
+        delete c;
+        return NP8_ERR_ARG;
+    }
     c->alpha = cfg->alpha;
     c->kappa = cfg->kappa;
     c->nu = cfg->nu;
@@ -532,7 +624,7 @@ int np8_create(np8_ctx **out, const np8_config *cfg) {
         (r = dalloc(c, &c->cnt, (size_t)kc)) || (r = dalloc(c, &c->cnt_best, (size_t)kc)) ||
         (r = dalloc(c, &c->mu_best, (size_t)kc * D)) || (r = dalloc(c, &c->sigma_best, (size_t)kc * D * D)) ||
         (r = dalloc(c, &c->cand, (size_t)kc * c->CS)) || (r = dalloc(c, &c->ctl, 1)) ||
-        (r = dalloc(c, &c->dense_of, (size_t)kc)) ||
+        (r = dalloc(c, &c->dense_of, (size_t)kc)) || (r = dalloc(c, &c->slot_iso, (size_t)kc)) ||
         (r = dalloc(c, &c->rec, (size_t)c->rec_bytes))) {
         free_device(c);
         delete c;
@@ -575,6 +667,7 @@ int np8_destroy(np8_ctx *c) {
     if (!c) return NP8_OK;
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     collect_timers(c);
+    for (hipEvent_t e : c->event_pool) (void)hipEventDestroy(e);
     if (c->comm) (void)ncclCommDestroy(c->comm);
     free_device(c);
     if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
@@ -598,6 +691,14 @@ int np8_set_data(np8_ctx *c, const double *X, int64_t n, int32_t D, int64_t offs
     if ((r = dalloc(c, &c->X, (size_t)n * D)) || (r = dalloc(c, &c->z, (size_t)n)) ||
         (r = dalloc(c, &c->z_best, (size_t)n)))
         return r;
+    for (int b = 0; b < 2; ++b)
+        if ((r = dalloc(c, &c->Xs[b], (size_t)n * D)) || (r = dalloc(c, &c->zs[b], (size_t)n)) ||
+            (r = dalloc(c, &c->ids[b], (size_t)n)))
+            return r;
+    if ((r = dalloc(c, &c->s_hist, (size_t)c->kcap)) || (r = dalloc(c, &c->s_cursor, (size_t)c->kcap)) ||
+        (r = dalloc(c, &c->s_off, (size_t)c->kcap)))
+        return r;
+    c->sorted_valid = false;
     std::vector<double> soa((size_t)n * D);
     for (int64_t i = 0; i < n; ++i)
         for (int a = 0; a < D; ++a) soa[(size_t)a * n + i] = X[(size_t)i * D + a];
@@ -613,6 +714,8 @@ static int set_state_common(np8_ctx *c, const std::vector<SlotHost> &slots, cons
     int r = upload_slots(c, slots, cnt);
     if (r) return r;
     HIPC(c, hipMemcpyAsync(c->z, zloc.data(), sizeof(int32_t) * zloc.size(), hipMemcpyHostToDevice, c->stream));
+    c->sorted_valid = false;
+    c->use_sorted = false;
     r = reset_ctl(c);
     if (r) return r;
     r = rebuild(c);
@@ -898,6 +1001,11 @@ int64_t np8_record_bytes(np8_ctx *c) { return c ? c->rec_bytes : 0; }
 int np8_step_local(np8_ctx *c, void *record_out) {
     if (!c || !record_out) return NP8_ERR_ARG;
     if (!c->have_state) return fail(c, NP8_ERR_STATE, "np8_step_local: no state");
+    c->use_sorted = c->n_loc > 0;
+    if (c->use_sorted) {
+        int r0 = prepare_sorted(c);
+        if (r0) return r0;
+    }
     int r = launch_assign(c, 0, c->n_loc, nullptr, false);
     if (r) return r;
     HIPC(c, hipMemcpyAsync(record_out, c->rec, (size_t)c->rec_bytes, hipMemcpyDeviceToHost, c->stream));

@@ -19,6 +19,11 @@ struct Ctl {
     double L;           // last total log-likelihood (global after the exchange)
     double L_local;     // this rank's part
     double best[2];     // best L, double-buffered by check parity
+    int64_t moved;      // items that changed cluster since the last re-sort (local)
+    int32_t cur;        // which label-sorted buffer is current
+    int32_t do_sort;    // this re-sort pass runs (decided by np8_sort_scan)
+    uint32_t done_blocks;
+    int32_t pad2;
 };
 
 enum : int32_t { kErrCapacity = 1 };
@@ -36,6 +41,8 @@ struct Request {
     int64_t i;     // global item index (Philox key of the auxiliary draw)
     int32_t m;     // which auxiliary
     int32_t zold;  // slot the item leaves
+    int32_t lpos;  // position in the owner's label-sorted layout (-1: none)
+    int32_t pad;
 };
 
 inline int64_t record_bytes(int kcap, int rec_cap) {
@@ -44,11 +51,15 @@ inline int64_t record_bytes(int kcap, int rec_cap) {
 }
 
 struct AssignArgs {
-    const double *X;   // [D][n_loc] (structure of arrays)
-    int32_t *z;        // [n_loc] slot ids
+    const double *X;   // [D][n_loc] (structure of arrays), item order
+    int32_t *z;        // [n_loc] slot ids, item order
+    int32_t sorted;    // run on the label-sorted layout (buffer ctl->cur of Xs/zs/ids)
+    const double *Xs[2];
+    int32_t *zs[2];
+    const int32_t *ids[2];  // position -> local item index
     const double *cand;
     const int32_t *dense_of;  // slot -> row of the candidate table
-    const Ctl *ctl;
+    Ctl *ctl;
     const double *hyp; // mu0 | UinvT packed | caux | rsk | logam | nu
     const int64_t *order;
     unsigned char *rec;
@@ -68,13 +79,15 @@ struct FinArgs {
     int32_t world, rec_cap, kcap, D, M;
     int32_t *cnt;
     int32_t *z;
+    int32_t *zs[2];  // sorted-layout labels (buffer ctl->cur), null when not in use
     int64_t n_loc, offset;
-    double *slot_mu, *slot_P, *slot_c, *slot_sigma;
+    double *slot_mu, *slot_P, *slot_c, *slot_sigma, *slot_iso;
     double *cand;
     int32_t *dense_of;
     Ctl *ctl;
     const double *mu0, *LT, *Gp, *LTL;  // LT, LTL: D*D row-major; Gp packed
     double caux, rsk, nu;
+    double gp_iso;  // common diagonal of Gp when (L^T L)^{-1} is a multiple of I, else 0
     uint64_t seed;
     uint32_t t;
 };
@@ -82,7 +95,8 @@ struct FinArgs {
 struct LoglikArgs {
     const double *X;
     const int32_t *z;
-    const double *slot_mu, *slot_P, *slot_c;
+    const double *cand;
+    const int32_t *dense_of;
     double *partial;
     int64_t n_loc;
 };
@@ -102,7 +116,23 @@ struct SnapArgs {
 
 }  // namespace np8
 
+// Label-sorted layout (items grouped by cluster so that a wave shares its candidate set).
+// force: rebuild from the item-order arrays (X, z); otherwise re-sort buffer ctl->cur into
+// ctl->cur ^ 1 when more than n/32 items moved since the last sort.  The last scatter block flips
+// ctl->cur.
+struct SortArgs {
+    const double *X;  // item-order layout [D][n]
+    const int32_t *z;
+    double *Xs[2];
+    int32_t *zs[2], *ids[2];
+    int32_t *hist, *cursor, *off;  // [kcap] scratch; hist is kept zero between passes
+    np8::Ctl *ctl;
+    int64_t n;
+    int32_t kcap, D, force;
+};
+
 bool np8_supported(int D, int M);
+hipError_t np8_launch_resort(const SortArgs &S, hipStream_t s);
 hipError_t np8_launch_assign(const np8::AssignArgs &A, int D, int M, hipStream_t s);
 hipError_t np8_launch_loglik_matrix(const np8::AssignArgs &A, int D, int M, const int64_t *idx, int64_t n,
                                     double *out, hipStream_t s);

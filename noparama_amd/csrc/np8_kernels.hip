@@ -121,16 +121,22 @@ __global__ __launch_bounds__(256) void np8_assign(AssignArgs A) {
     constexpr int F = D + DP;
     const int64_t p = A.p0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= A.p1) return;
-    const int64_t il = position_to_local(A, p);
+    const bool sorted = A.sorted != 0;  // label-sorted layout: X and zs indexed by position
+    // (ternaries, not A.zs[cur]: a runtime index into the argument struct would move it to scratch)
+    const int cur = sorted ? A.ctl->cur : 0;
+    int32_t *__restrict__ zs = cur ? A.zs[1] : A.zs[0];
+    const int32_t *__restrict__ ids = cur ? A.ids[1] : A.ids[0];
+    const int64_t il = sorted ? (int64_t)ids[p] : position_to_local(A, p);
+    const int64_t xr = sorted ? p : il;
     const uint64_t ig = (uint64_t)(A.offset + il);
-    const double *__restrict__ X = A.X;
+    const double *__restrict__ X = sorted ? (cur ? A.Xs[1] : A.Xs[0]) : A.X;
     const double *__restrict__ cand = A.cand;
     const double *__restrict__ hyp = A.hyp;
 
     double x[D];
 #pragma unroll
-    for (int a = 0; a < D; ++a) x[a] = X[(int64_t)a * A.n_loc + il];
-    const int32_t zi = A.z[il];
+    for (int a = 0; a < D; ++a) x[a] = X[(int64_t)a * A.n_loc + xr];
+    const int32_t zi = sorted ? zs[p] : A.z[il];
 
     // The item's own cluster enters the draw first (weight n_k - 1): its log-weight is a lower bound
     // of the final maximum, so every later candidate more than kSkip below it is skipped exactly.
@@ -160,24 +166,146 @@ __global__ __launch_bounds__(256) void np8_assign(AssignArgs A) {
 
     RecHeader *hdr = reinterpret_cast<RecHeader *>(A.rec);
     int32_t *delta = reinterpret_cast<int32_t *>(A.rec + kRecHeaderBytes);
+    const int32_t snew = (st.pick < K) ? (int32_t)cand[(int64_t)st.pick * CS + F + kFieldSlot] : -1;
+    // items leaving their cluster, counted per wave (drives the re-sort of the layout)
+    const uint64_t mv = __ballot(snew != zi);
+    if (mv && (threadIdx.x & 63) == (__ffsll((unsigned long long)__ballot(1)) - 1))
+        atomicAdd(reinterpret_cast<unsigned long long *>(&A.ctl->moved), (unsigned long long)__popcll(mv));
     if (st.pick < K) {
-        const int32_t s = (int32_t)cand[(int64_t)st.pick * CS + F + kFieldSlot];
+        const int32_t s = snew;
         if (s != zi) {
             atomicSub(delta + zi, 1);
             atomicAdd(delta + s, 1);
             A.z[il] = s;
+            if (sorted) zs[p] = s;
         }
     } else {
         const int q = atomicAdd(&hdr->nreq, 1);
         if (q < A.rec_cap) {
             Request *req = reinterpret_cast<Request *>(A.rec + kRecHeaderBytes + (int64_t)A.kcap * 4);
             Request r;
-            r.pos = A.offset + p;
+            r.pos = sorted ? (int64_t)ig : A.offset + p;  // synchronous sweep: scan position = item index
             r.i = (int64_t)ig;
             r.m = st.pick - K;
             r.zold = zi;
+            r.lpos = sorted ? (int32_t)p : -1;
+            r.pad = 0;
             req[q] = r;
         }
+    }
+}
+
+// ---- label-sorted layout ------------------------------------------------------------------------------
+// Counting sort by slot.  The order inside a cluster depends on atomic arrival, which changes no
+// result: in the synchronous sweep every item's draw is a pure function of (state, item, epoch).
+constexpr int kSortThreads = 1024, kSortItems = 4;  // 4096 items per block
+
+__device__ __forceinline__ bool sort_needed(const SortArgs &S) { return S.force || S.ctl->moved * 32 > S.n; }
+
+__global__ __launch_bounds__(kSortThreads) void np8_sort_hist(SortArgs S) {
+    if (!sort_needed(S)) return;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    int *lh = reinterpret_cast<int *>(smem);
+    const int32_t *z = S.force ? S.z : (S.ctl->cur ? S.zs[1] : S.zs[0]);
+    for (int s = threadIdx.x; s < S.kcap; s += kSortThreads) lh[s] = 0;
+    __syncthreads();
+    for (int k = 0; k < kSortItems; ++k) {
+        const int64_t p = ((int64_t)blockIdx.x * kSortItems + k) * kSortThreads + threadIdx.x;
+        if (p < S.n) atomicAdd(&lh[z[p]], 1);
+    }
+    __syncthreads();
+    for (int s = threadIdx.x; s < S.kcap; s += kSortThreads)
+        if (lh[s]) atomicAdd(&S.hist[s], lh[s]);
+}
+
+__global__ __launch_bounds__(kSortThreads) void np8_sort_scatter(SortArgs S) {
+    if (!S.ctl->do_sort) return;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    int *lh = reinterpret_cast<int *>(smem);
+    int *lbase = lh + S.kcap;
+    const int src = S.ctl->cur, dst = src ^ 1;
+    const int32_t *z = S.force ? S.z : (src ? S.zs[1] : S.zs[0]);
+    const int32_t *ids = S.force ? nullptr : (src ? S.ids[1] : S.ids[0]);
+    const double *X = S.force ? S.X : (src ? S.Xs[1] : S.Xs[0]);
+    int32_t *zo = dst ? S.zs[1] : S.zs[0];
+    int32_t *ido = dst ? S.ids[1] : S.ids[0];
+    double *Xo = dst ? S.Xs[1] : S.Xs[0];
+    for (int s = threadIdx.x; s < S.kcap; s += kSortThreads) lh[s] = 0;
+    __syncthreads();
+    int zp[kSortItems], rk[kSortItems];
+    for (int k = 0; k < kSortItems; ++k) {
+        const int64_t p = ((int64_t)blockIdx.x * kSortItems + k) * kSortThreads + threadIdx.x;
+        zp[k] = (p < S.n) ? z[p] : -1;
+        rk[k] = (zp[k] >= 0) ? atomicAdd(&lh[zp[k]], 1) : 0;
+    }
+    __syncthreads();
+    for (int s = threadIdx.x; s < S.kcap; s += kSortThreads)
+        if (lh[s]) lbase[s] = atomicAdd(&S.cursor[s], lh[s]);
+    __syncthreads();
+    for (int k = 0; k < kSortItems; ++k) {
+        if (zp[k] < 0) continue;
+        const int64_t p = ((int64_t)blockIdx.x * kSortItems + k) * kSortThreads + threadIdx.x;
+        const int64_t q = (int64_t)S.off[zp[k]] + lbase[zp[k]] + rk[k];
+        zo[q] = zp[k];
+        ido[q] = ids ? ids[p] : (int32_t)p;
+        for (int a = 0; a < S.D; ++a) Xo[(int64_t)a * S.n + q] = X[(int64_t)a * S.n + p];
+    }
+    // the last block to finish makes the new layout current (read by the next kernels)
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();
+        if (atomicAdd(&S.ctl->done_blocks, 1u) == gridDim.x - 1) S.ctl->cur = dst;
+    }
+}
+
+__global__ __launch_bounds__(1024) void np8_sort_scan(SortArgs S) {
+    const bool need = sort_needed(S);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        S.ctl->do_sort = need ? 1 : 0;
+        if (need) {
+            S.ctl->moved = 0;
+            S.ctl->done_blocks = 0;
+        }
+    }
+    if (!need) return;
+    __shared__ int sh[32];
+    const int per = (S.kcap + 1023) / 1024;
+    const int s0 = min(S.kcap, (int)threadIdx.x * per), s1 = min(S.kcap, s0 + per);
+    int v = 0;
+    for (int s = s0; s < s1; ++s) v += S.hist[s];
+    int tot;
+    int base = 0;
+    {
+        // inclusive wave scan, then across waves
+        const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+        int inc = v;
+        for (int o = 1; o < 64; o <<= 1) {
+            const int n = __shfl_up(inc, o, 64);
+            if (lane >= o) inc += n;
+        }
+        if (lane == 63) sh[wid] = inc;
+        __syncthreads();
+        if (wid == 0) {
+            const int x = (lane < 16) ? sh[lane] : 0;
+            int y = x;
+            for (int o = 1; o < 64; o <<= 1) {
+                const int n = __shfl_up(y, o, 64);
+                if (lane >= o) y += n;
+            }
+            if (lane < 16) sh[lane] = y - x;
+            if (lane == 15) sh[16] = y;
+        }
+        __syncthreads();
+        base = sh[wid] + inc - v;
+        tot = sh[16];
+    }
+    (void)tot;
+    for (int s = s0; s < s1; ++s) {
+        S.off[s] = base;
+        base += S.hist[s];
+        S.cursor[s] = 0;
+        S.hist[s] = 0;  // ready for the next pass
     }
 }
 
@@ -264,6 +392,7 @@ __device__ void write_new_slot(const FinArgs &F, const Request &r, int s) {
     for (int k = 0; k < DP; ++k) F.slot_P[(int64_t)s * DP + k] = F.Gp[k] / v2;
     F.slot_c[s] = fma(-(double)D, log_pos(fabs(v)), F.caux);
     for (int k = 0; k < D * D; ++k) F.slot_sigma[(int64_t)s * D * D + k] = v2 * F.LTL[k];
+    F.slot_iso[s] = (F.gp_iso > 0.0) ? F.Gp[0] / v2 : 0.0;
 }
 
 }  // namespace
@@ -276,6 +405,7 @@ __global__ __launch_bounds__(kFinThreads) void np8_finalize(FinArgs F) {
     int *kidx = reinterpret_cast<int *>(smem + sizeof(int64_t) * kReqMax);
     int *freeslot = kidx + kReqMax;
     int *cnt_s = freeslot + kReqMax;
+    int *live_s = cnt_s + F.kcap;
     __shared__ int sh[32];
     __shared__ int base[65];
     __shared__ int s_flags[4];  // nreq, overflow, accept, free
@@ -361,7 +491,10 @@ __global__ __launch_bounds__(kFinThreads) void np8_finalize(FinArgs F) {
             const int s = freeslot[q];
             write_new_slot(F, r, s);
             cnt_s[s] = 1;
-            if (r.i >= F.offset && r.i < F.offset + F.n_loc) F.z[r.i - F.offset] = s;
+            if (r.i >= F.offset && r.i < F.offset + F.n_loc) {
+                F.z[r.i - F.offset] = s;
+                if (F.zs[0] && r.lpos >= 0) (F.ctl->cur ? F.zs[1] : F.zs[0])[r.lpos] = s;
+            }
         }
     }
     __syncthreads();
@@ -375,21 +508,22 @@ __global__ __launch_bounds__(kFinThreads) void np8_finalize(FinArgs F) {
         F.cnt[s] = c;
         F.dense_of[s] = (c > 0) ? k : -1;
         if (c > 0) {
-            double *e = F.cand + (int64_t)k * CS;
-            const double *P = F.slot_P + (int64_t)s * DP;
-            for (int a = 0; a < D; ++a) e[a] = F.slot_mu[(int64_t)s * D + a];
-            // isotropic precision: off-diagonals exactly 0 and one common diagonal value
-            bool iso = true;
-            for (int a = 0, q = 0; a < D; ++a)
-                for (int b = a; b < D; ++b, ++q) iso = iso && ((a == b) ? (P[q] == P[0]) : (P[q] == 0.0));
-            for (int a = 0; a < DP; ++a) e[D + a] = P[a];
-            e[D + DP + kFieldC] = F.slot_c[s];
-            e[D + DP + kFieldLogn] = log_pos((double)c);
-            e[D + DP + kFieldLogn1] = (c > 1) ? log_pos((double)(c - 1)) : kZeroLogWeight;
-            e[D + DP + kFieldSlot] = (double)s;
-            e[D + DP + kFieldIso] = iso ? P[0] : 0.0;
+            double *e = F.cand + (int64_t)k * CS + D + DP;
+            e[kFieldC] = F.slot_c[s];
+            e[kFieldLogn] = log_pos((double)c);
+            e[kFieldLogn1] = (c > 1) ? log_pos((double)(c - 1)) : kZeroLogWeight;
+            e[kFieldSlot] = (double)s;
+            e[kFieldIso] = F.slot_iso[s];
+            live_s[k] = s;
             ++k;
         }
+    }
+    __syncthreads();
+    // mu and P' of every live row, all threads
+    const int W = D + DP;
+    for (int idx = tid; idx < nlive * W; idx += kFinThreads) {
+        const int r = idx / W, f = idx - r * W, s = live_s[r];
+        F.cand[(int64_t)r * CS + f] = (f < D) ? F.slot_mu[(int64_t)s * D + f] : F.slot_P[(int64_t)s * DP + (f - D)];
     }
     if (tid == 0) F.ctl->K = nlive;
     // clear the local record for the next step (all reads of it are behind the barriers above)
@@ -404,29 +538,15 @@ __global__ __launch_bounds__(kFinThreads) void np8_finalize(FinArgs F) {
 template <int D>
 __global__ __launch_bounds__(256) void np8_loglik(LoglikArgs A) {
     constexpr int DP = D * (D + 1) / 2;
+    constexpr int CS = (D + DP + 5 + 1) & ~1;
     __shared__ double red[256];
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     double ll = 0.0;
     if (i < A.n_loc) {
-        const int s = A.z[i];
         double x[D];
 #pragma unroll
         for (int a = 0; a < D; ++a) x[a] = A.X[(int64_t)a * A.n_loc + i];
-        const double *mu = A.slot_mu + (int64_t)s * D;
-        const double *P = A.slot_P + (int64_t)s * DP;
-        double d[D];
-#pragma unroll
-        for (int a = 0; a < D; ++a) d[a] = x[a] - mu[a];
-        double q = 0.0;
-        int k = 0;
-#pragma unroll
-        for (int a = 0; a < D; ++a) {
-            double t = P[k++] * d[a];
-#pragma unroll
-            for (int b = a + 1; b < D; ++b) t = fma(P[k++], d[b], t);
-            q = fma(t, d[a], q);
-        }
-        ll = fma(-0.5, q, A.slot_c[s]);
+        ll = cand_ll<D>(A.cand + (int64_t)A.dense_of[A.z[i]] * CS, x);
     }
     red[threadIdx.x] = ll;
     __syncthreads();
@@ -532,8 +652,18 @@ hipError_t np8_launch_loglik_matrix(const AssignArgs &A, int D, int M, const int
     return hipErrorInvalidValue;
 }
 
+hipError_t np8_launch_resort(const SortArgs &S, hipStream_t s) {
+    if (S.n <= 0) return hipSuccess;
+    const int64_t per = (int64_t)kSortThreads * kSortItems;
+    const unsigned nb = (unsigned)((S.n + per - 1) / per);
+    hipLaunchKernelGGL(np8_sort_hist, dim3(nb), dim3(kSortThreads), sizeof(int) * S.kcap, s, S);
+    hipLaunchKernelGGL(np8_sort_scan, dim3(1), dim3(1024), 0, s, S);
+    hipLaunchKernelGGL(np8_sort_scatter, dim3(nb), dim3(kSortThreads), 2 * sizeof(int) * S.kcap, s, S);
+    return hipGetLastError();
+}
+
 size_t np8_finalize_lds_bytes(int kcap) {
-    return sizeof(int64_t) * kReqMax + sizeof(int) * kReqMax * 2 + sizeof(int) * (size_t)kcap;
+    return sizeof(int64_t) * kReqMax + sizeof(int) * kReqMax * 2 + 2 * sizeof(int) * (size_t)kcap;
 }
 
 hipError_t np8_launch_finalize(const FinArgs &F, hipStream_t s) {

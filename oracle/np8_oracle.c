@@ -860,7 +860,7 @@ int np8o_finalize(np8o_ctx *c, const int32_t *delta, const int64_t *req_pos, con
 
 double np8o_total_loglik(np8o_ctx *c) {
     double L = 0.0;
-    for (int64_t i = 0; i < c->N; ++i) L += slot_ll(c, c->X + (size_t)i * c->D, c->z[i]);
+    for (int64_t i = 0; i < c->N; ++i) L += cand_ll(c, c->X + (size_t)i * c->D, c->dense_of[c->z[i]]);
     return L;
 }
 

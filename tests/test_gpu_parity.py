@@ -109,6 +109,26 @@ def test_warm_state_sweeps_bit_exact(D, K, s, r):
     np.testing.assert_allclose(g.total_loglik(), o.total_loglik(), rtol=1e-11)
 
 
+def test_sorted_layout_many_resorts_bit_exact():
+    """Synchronous sweeps run on a label-sorted copy of the data, re-sorted every few sweeps; from a
+    random start items move a lot, so the layout is stale most of the time.  Results must not care."""
+    X, _, _, _ = datasets.mixture(6000, 3, 12, 0.5, 5.0, seed=12)
+    g, o = pair(3, 41, kcap=4096)
+    for s in (g, o):
+        s.set_data(X)
+        s.init_random(20)
+    for _ in range(4):
+        g.sweep(3)
+        o.sweep(3)
+        assert_same_state(g, o)
+    # a per-item step in between invalidates the sorted copy
+    g.update_points(np.arange(0, 6000, 13))
+    o.update_points(np.arange(0, 6000, 13))
+    g.sweep(2)
+    o.sweep(2)
+    assert_same_state(g, o)
+
+
 def test_max_likelihood_snapshot():
     X, _ = datasets.twogaussians(8)
     g, o = pair(2, 13)
