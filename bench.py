@@ -57,6 +57,8 @@ def main():
         import torch.distributed as dist
 
         dist.init_process_group("gloo")  # host barrier + timing max; the sweep itself uses RCCL
+    # one GPU per rank on the scaling node; rehearsals with more ranks than GPUs share devices
+    local_rank = local_rank % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local_rank)
 
     from noparama_amd import NealAlgorithm8, comm_unique_id, datasets
@@ -68,14 +70,43 @@ def main():
     hi = (N * (rank + 1)) // world
 
     smp = NealAlgorithm8(D, seed=args.seed, device=local_rank)
+    transport = "local"
     if world > 1:
+        from noparama_amd import NP8Error
+
         uid = [comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
-        smp.comm_init(uid[0], rank, world)
+        try:
+            smp.comm_init(uid[0], rank, world)
+            ok = True
+        except NP8Error as e:
+            print(f"rank {rank}: RCCL unavailable ({e}); exchanging records over gloo", file=sys.stderr)
+            ok = False
+        flags = [None] * world
+        dist.all_gather_object(flags, ok)
+        transport = "rccl" if all(flags) else "gloo"
+        if transport == "gloo":
+            smp.close()
+            smp = NealAlgorithm8(D, seed=args.seed, device=local_rank)
+            smp.comm_init(None, rank, world)
     smp.set_data(X[lo:hi], offset=lo, n_global=N)
-    smp.set_state(z[lo:hi], mu, sig)
+    if transport == "gloo":
+        smp.set_state(z[lo:hi], mu, sig, counts=np.bincount(z, minlength=mu.shape[0]))
+    else:
+        smp.set_state(z[lo:hi], mu, sig)
 
-    smp.sweep(args.warmup)  # includes np8_sync
+    def sweeps(n, sync=True):
+        if transport != "gloo":
+            smp.sweep(n, sync=sync)
+            return
+        for _ in range(n):  # fallback transport: the exchange record through host memory
+            rec = torch.from_numpy(smp.step_local())
+            out = [torch.zeros_like(rec) for _ in range(world)]
+            dist.all_gather(out, rec)
+            smp.step_merge(np.concatenate([o.numpy() for o in out]), world)
+            smp.end_sweep()
+
+    sweeps(args.warmup)  # includes np8_sync
     torch.cuda.synchronize()
     smp.set_timing(True)
     st0 = smp.stats()
@@ -83,7 +114,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    smp.sweep(args.steps, sync=False)
+    sweeps(args.steps, sync=False)
     smp.sync()
     torch.cuda.synchronize()
     if dist:
@@ -131,6 +162,7 @@ def main():
             "config": {
                 "workload": f"C3: N={N} D={D} K~{K} M=3 mixture, warm state, frozen cluster parameters",
                 "N": N, "D": D, "K_final": Kfinal, "parallelism": f"data-sharded x{world}",
+                "exchange": transport,
             },
             "roofline": {
                 "bound": "mfma",

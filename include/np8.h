@@ -77,6 +77,11 @@ int np8_set_data(np8_ctx *ctx, const double *X, int64_t n, int32_t D, int64_t of
  * Sigma is used as the reference uses it: inverse and determinant of the matrix as given
  * (multivariatenormal.cpp:87,90), so a non-symmetric Sigma is accepted (test_mvn_likelihood.cpp:20). */
 int np8_set_state(np8_ctx *ctx, const int32_t *z, int32_t K, const double *mu, const double *Sigma);
+/* Same with the global cluster sizes given by the caller (counts[K]); for sharded runs whose
+ * records move over the caller's transport (np8_step_local / np8_step_merge), where no device
+ * reduction of the per-rank label counts is available. */
+int np8_set_state_counts(np8_ctx *ctx, const int32_t *z, int32_t K, const double *mu, const double *Sigma,
+                         const int64_t *counts);
 
 /* Reference initialisation: K_init G0 draws, uniform random assignment, cleanup of empty clusters
  * (np_mcmc.cpp:49-92, np_init_clusters.cpp:24-40). */

@@ -726,6 +726,11 @@ static int set_state_common(np8_ctx *c, const std::vector<SlotHost> &slots, cons
 }
 
 int np8_set_state(np8_ctx *c, const int32_t *z, int32_t K, const double *mu, const double *Sigma) {
+    return np8_set_state_counts(c, z, K, mu, Sigma, nullptr);
+}
+
+int np8_set_state_counts(np8_ctx *c, const int32_t *z, int32_t K, const double *mu, const double *Sigma,
+                         const int64_t *counts) {
     if (!c) return NP8_ERR_ARG;
     if (!c->have_data) return fail(c, NP8_ERR_STATE, "np8_set_state: no data");
     if (K < 1 || K > c->kcap || !mu || !Sigma || (c->n_loc > 0 && !z))
@@ -740,8 +745,17 @@ int np8_set_state(np8_ctx *c, const int32_t *z, int32_t K, const double *mu, con
         zl[i] = z[i];
         cnt[z[i]]++;
     }
+    if (counts) {  // caller-supplied global counts (host-exchange runs); local labels must fit in them
+        std::vector<int32_t> g(K);
+        for (int k = 0; k < K; ++k) {
+            if (counts[k] < cnt[k] || counts[k] > 0x7FFFFFFFll)
+                return fail(c, NP8_ERR_RANGE, "np8_set_state_counts: counts smaller than this rank's labels");
+            g[k] = (int32_t)counts[k];
+        }
+        return set_state_common(c, slots, g, zl);
+    }
     if (c->world > 1 && !c->comm)
-        return fail(c, NP8_ERR_STATE, "np8_set_state: host-exchange mode has no count reduction; use np8_init_random");
+        return fail(c, NP8_ERR_STATE, "np8_set_state: host-exchange mode needs np8_set_state_counts");
     if (c->world > 1) {  // counts are global
         int32_t *d = nullptr;
         HIPC(c, hipMalloc(&d, sizeof(int32_t) * K));

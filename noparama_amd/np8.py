@@ -102,6 +102,7 @@ def lib():
         "np8_last_error": ([vp], C.c_char_p),
         "np8_set_data": ([vp, vp, i64, i32, i64, i64], i32),
         "np8_set_state": ([vp, vp, i32, vp, vp], i32),
+        "np8_set_state_counts": ([vp, vp, i32, vp, vp, vp], i32),
         "np8_init_random": ([vp, i32], i32),
         "np8_sweep": ([vp, i32], i32),
         "np8_update_points": ([vp, vp, i64], i32),
@@ -192,11 +193,16 @@ class NealAlgorithm8:
         self._check(lib().np8_set_data(self._h, _p(X), self.N, self.D, int(offset),
                                        int(self.N if n_global is None else n_global)))
 
-    def set_state(self, z, mu, sigma):
+    def set_state(self, z, mu, sigma, counts=None):
+        """Labels of this shard; counts = global cluster sizes (host-exchange runs), else derived."""
         z = np.ascontiguousarray(z, dtype=np.int32)
         mu = np.ascontiguousarray(mu, dtype=np.float64)
         sigma = np.ascontiguousarray(sigma, dtype=np.float64)
-        self._check(lib().np8_set_state(self._h, _p(z), mu.shape[0], _p(mu), _p(sigma)))
+        if counts is None:
+            self._check(lib().np8_set_state(self._h, _p(z), mu.shape[0], _p(mu), _p(sigma)))
+        else:
+            cnt = np.ascontiguousarray(counts, dtype=np.int64)
+            self._check(lib().np8_set_state_counts(self._h, _p(z), mu.shape[0], _p(mu), _p(sigma), _p(cnt)))
 
     def init_random(self, K=20):
         self._check(lib().np8_init_random(self._h, int(K)))
