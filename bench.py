@@ -39,6 +39,8 @@ def parse():
     ap.add_argument("--seed", type=int, default=20261015)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget (0 = skip)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
+    ap.add_argument("--param-update", default="frozen", choices=["frozen", "mh_g0"],
+                    help="cluster-parameter update after every sweep (frozen = the reference's effective one)")
     return ap.parse_args()
 
 
@@ -69,7 +71,7 @@ def main():
     lo = (N * rank) // world
     hi = (N * (rank + 1)) // world
 
-    smp = NealAlgorithm8(D, seed=args.seed, device=local_rank)
+    smp = NealAlgorithm8(D, seed=args.seed, device=local_rank, param_update=args.param_update)
     transport = "local"
     if world > 1:
         from noparama_amd import NP8Error
@@ -87,7 +89,7 @@ def main():
         transport = "rccl" if all(flags) else "gloo"
         if transport == "gloo":
             smp.close()
-            smp = NealAlgorithm8(D, seed=args.seed, device=local_rank)
+            smp = NealAlgorithm8(D, seed=args.seed, device=local_rank, param_update=args.param_update)
             smp.comm_init(None, rank, world)
     smp.set_data(X[lo:hi], offset=lo, n_global=N)
     if transport == "gloo":
@@ -160,9 +162,13 @@ def main():
             "dtype": "f64",
             "data": "synthetic",
             "config": {
-                "workload": f"C3: N={N} D={D} K~{K} M=3 mixture, warm state, frozen cluster parameters",
+                "workload": f"C3: N={N} D={D} K~{K} M=3 mixture, warm state, "
+                            + ("frozen cluster parameters" if args.param_update == "frozen"
+                               else "mh_g0 cluster-parameter update (20 MH steps/cluster/sweep)"),
                 "N": N, "D": D, "K_final": Kfinal, "parallelism": f"data-sharded x{world}",
                 "exchange": transport,
+                "param_update": args.param_update,
+                "ms_params_per_sweep": (st1["ms_params"] - st0["ms_params"]) / max(args.steps, 1),
             },
             "roofline": {
                 "bound": "mfma",

@@ -135,6 +135,8 @@ NealAlgorithm8Hip::NealAlgorithm8Hip(uint64_t seed, const np8_prior &prior, int6
     if (kcap > 0) _kcap = kcap;
     cfg.chunk = chunk;
     cfg.device = device;
+    cfg.param_update = prior.param_update;
+    cfg.mh_steps = prior.mh_steps;
     check(np8_create(&_ctx, &cfg), "np8_create");
 }
 

@@ -90,6 +90,8 @@ struct np8_prior {
     double nu = 4.0;
     std::vector<double> Lambda;    // default 0.01 I
     int M = 3;                     // np_neal_algorithm8.cpp:33
+    int param_update = NP8_PARAM_FROZEN;  // UpdateClusters mode (np_mcmc.cpp:170), include/np8.h
+    int mh_steps = 20;                    // np_mcmc.cpp:54
 };
 
 class NealAlgorithm8Hip : public UpdateClusterPopulation {

@@ -19,7 +19,8 @@
 
 static void usage(const char *p) {
     std::cerr << "usage: " << p << " -d <datafile> -a algorithm8 [-T sweeps=2000] [-c clustering] [-s seed]"
-              << " [-C chunk (0 = data-parallel sweep, 1 = sequential)] [-D dims=2] [-w workspace]" << std::endl;
+              << " [-C chunk (0 = data-parallel sweep, 1 = sequential)] [-D dims=2] [-w workspace]"
+              << " [-u frozen|mh_g0 (cluster-parameter update)]" << std::endl;
 }
 
 static bool read_data(const std::string &fn, int D, dataset_t &ds, std::vector<int> &gt) {
@@ -43,13 +44,13 @@ static bool read_data(const std::string &fn, int D, dataset_t &ds, std::vector<i
 }
 
 int main(int argc, char *argv[]) {
-    std::string data, algo, mode = "clustering", ws;
+    std::string data, algo, mode = "clustering", ws, upd = "frozen";
     int T = 2000, D = 2;
     long long chunk = 0;
     unsigned long long seed = 0;
     bool seeded = false;
     int tok;
-    while ((tok = getopt(argc, argv, "d:a:T:c:s:C:D:w:h?")) != EOF) {
+    while ((tok = getopt(argc, argv, "d:a:T:c:s:C:D:w:u:h?")) != EOF) {
         switch (tok) {
             case 'd': data = optarg; break;
             case 'a': algo = optarg; break;
@@ -59,6 +60,7 @@ int main(int argc, char *argv[]) {
             case 'C': chunk = std::stoll(optarg); break;
             case 'D': D = std::stoi(optarg); break;
             case 'w': ws = optarg; break;
+            case 'u': upd = optarg; break;
             default: usage(argv[0]); return 1;
         }
     }
@@ -89,6 +91,12 @@ int main(int argc, char *argv[]) {
     }
     np8_prior prior;
     prior.D = D;
+    if (upd == "mh_g0") {
+        prior.param_update = NP8_PARAM_MH_G0;
+    } else if (upd != "frozen") {
+        usage(argv[0]);
+        return 1;
+    }
     try {
         NealAlgorithm8Hip sampler(seed, prior, chunk);
         MCMC mcmc(sampler);

@@ -51,7 +51,17 @@ typedef struct {
     int64_t chunk;        /* points per synchronous step: 0 = the whole sweep (data-parallel);
                              1 = the reference's exact sequential sweep (np_mcmc.cpp:146-164) */
     int32_t device;       /* HIP device ordinal, -1 = current */
+    int32_t param_update; /* NP8_PARAM_*: cluster-parameter update after every sweep (np_mcmc.cpp:170) */
+    int32_t mh_steps;     /* MH steps per cluster and sweep for NP8_PARAM_MH_G0; 0 -> 20 (np_mcmc.cpp:54) */
 } np8_config;
+
+/* Cluster-parameter update (UpdateClusters::update, src/np_update_clusters.cpp:71-142).
+ * FROZEN: parameters never change -- the reference's effective behaviour, because its accepted
+ *         proposal is sliced away in cluster_t::setSuffies.
+ * MH_G0:  what the reference intends: mh_steps independence-MH steps per live cluster with G0
+ *         proposals, evaluated from per-cluster sufficient statistics on the device. */
+#define NP8_PARAM_FROZEN 0
+#define NP8_PARAM_MH_G0 1
 
 typedef struct {
     int32_t K;                  /* live clusters */
@@ -62,6 +72,8 @@ typedef struct {
     double best_loglik;         /* max over checks of sum_i log p(x_i | theta_z_i) (np_mcmc.cpp:187-203) */
     double last_loglik;
     double ms_assign, ms_finalize, ms_loglik; /* accumulated device time (when timing is enabled) */
+    int64_t mh_accepted;        /* cumulative accepted parameter proposals (NP8_PARAM_MH_G0) */
+    double ms_params;           /* accumulated device time of the parameter update */
 } np8_stats_t;
 
 /* Create / destroy.  Replaces NealAlgorithm8::NealAlgorithm8 (np_neal_algorithm8.cpp:17-34). */

@@ -38,6 +38,8 @@ struct np8_ctx {
     uint64_t seed = 0;
     int64_t chunk = 0;
     int device = 0;
+    int param_update = NP8_PARAM_FROZEN, mh_steps = 20;
+    double *acc = nullptr;  // [kcap][D + DP] parameter-update statistics
     std::vector<double> mu0, Lambda;
     // base-measure precomputes (DESIGN.md "G0")
     std::vector<double> Lc, LT, UinvT, Gp, LTL;  // D*D row-major
@@ -81,8 +83,8 @@ struct np8_ctx {
     bool timing = false;
     std::vector<Timer> timers;
     std::vector<hipEvent_t> event_pool;
-    double ms[3] = {0, 0, 0};
-    int64_t n_timed[3] = {0, 0, 0};
+    double ms[4] = {0, 0, 0, 0};  // assign, finalize, loglik, params
+    int64_t n_timed[4] = {0, 0, 0, 0};
     std::string err;
 };
 
@@ -251,7 +253,7 @@ void free_device(np8_ctx *c) {
                     c->cnt,    c->cnt_best, c->mu_best, c->sigma_best, c->cand, c->ctl,    c->hyp,
                     c->d_mu0,  c->d_LT,    c->d_Gp,   c->d_LTL,   c->rec,     c->gath,    c->order,
                     c->partial, c->dense_of, c->Xs[0], c->Xs[1], c->zs[0], c->zs[1], c->ids[0], c->ids[1],
-                    c->s_hist, c->s_cursor, c->s_off, c->slot_iso};
+                    c->s_hist, c->s_cursor, c->s_off, c->slot_iso, c->acc};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     for (int b = 0; b < 2; ++b) {
@@ -260,6 +262,7 @@ void free_device(np8_ctx *c) {
     }
     c->s_hist = c->s_cursor = c->s_off = nullptr;
     c->slot_iso = nullptr;
+    c->acc = nullptr;
     c->X = nullptr;
     c->z = c->z_best = nullptr;
     c->slot_mu = c->slot_P = c->slot_c = c->slot_sigma = nullptr;
@@ -520,7 +523,59 @@ int launch_total_loglik(np8_ctx *c) {
     return NP8_OK;
 }
 
+// UpdateClusters::update (np_mcmc.cpp:170) in mh_g0 mode: statistics of the current labelling
+// (summed over ranks), then one MH chain per live slot; candidate rows are patched in place.
+int param_update(np8_ctx *c) {
+    if (c->param_update != NP8_PARAM_MH_G0) return NP8_OK;
+    if (c->world > 1 && !c->comm)
+        return fail(c, NP8_ERR_STATE, "mh_g0 parameter update needs the RCCL transport when sharded");
+    Timer t;
+    timer_begin(c, 3, t);
+    ParamArgs A;
+    A.X = c->X;
+    A.z = c->z;
+    const bool sorted = c->use_sorted && c->sorted_valid;
+    for (int b = 0; b < 2; ++b) {
+        A.Xs[b] = c->Xs[b];
+        A.zs[b] = c->zs[b];
+    }
+    A.sorted = sorted ? 1 : 0;
+    A.n_loc = c->n_loc;
+    A.kcap = c->kcap;
+    A.D = c->D;
+    A.steps = c->mh_steps;
+    A.acc = c->acc;
+    A.cnt = c->cnt;
+    A.dense_of = c->dense_of;
+    A.slot_mu = c->slot_mu;
+    A.slot_P = c->slot_P;
+    A.slot_c = c->slot_c;
+    A.slot_sigma = c->slot_sigma;
+    A.slot_iso = c->slot_iso;
+    A.cand = c->cand;
+    A.ctl = c->ctl;
+    A.mu0 = c->d_mu0;
+    A.LT = c->d_LT;
+    A.Gp = c->d_Gp;
+    A.LTL = c->d_LTL;
+    A.caux = c->caux;
+    A.rsk = c->rsk;
+    A.nu = c->nu;
+    A.gp_iso = c->gp_iso;
+    A.seed = c->seed;
+    A.t = c->epoch;
+    const size_t nacc = (size_t)c->kcap * (c->D + c->DP);
+    HIPC(c, hipMemsetAsync(c->acc, 0, sizeof(double) * nacc, c->stream));
+    HIPC(c, np8_launch_suffstats(A, c->stream));
+    if (c->world > 1) NCCLC(c, ncclAllReduce(c->acc, c->acc, nacc, ncclFloat64, ncclSum, c->comm, c->stream));
+    HIPC(c, np8_launch_mh_g0(A, c->stream));
+    timer_end(c, t);
+    return NP8_OK;
+}
+
 int end_sweep(np8_ctx *c) {
+    int r0 = param_update(c);
+    if (r0) return r0;
     if (c->epoch % 5u == 0u) {  // np_mcmc.cpp:172-174
         int r = launch_total_loglik(c);
         if (r) return r;
@@ -595,6 +650,13 @@ int np8_create(np8_ctx **out, const np8_config *cfg) {
     c->nu = cfg->nu;
     c->seed = cfg->seed;
     c->chunk = cfg->chunk;
+    if (cfg->param_update < NP8_PARAM_FROZEN || cfg->param_update > NP8_PARAM_MH_G0 || cfg->mh_steps < 0 ||
+        cfg->mh_steps > 65536) {
+        delete c;
+        return NP8_ERR_ARG;
+    }
+    c->param_update = cfg->param_update;
+    c->mh_steps = cfg->mh_steps > 0 ? cfg->mh_steps : 20;
     c->mu0.assign(cfg->mu0, cfg->mu0 + c->D);
     c->Lambda.assign(cfg->Lambda, cfg->Lambda + (size_t)c->D * c->D);
     if (!prepare_base(c)) {
@@ -625,7 +687,8 @@ int np8_create(np8_ctx **out, const np8_config *cfg) {
         (r = dalloc(c, &c->mu_best, (size_t)kc * D)) || (r = dalloc(c, &c->sigma_best, (size_t)kc * D * D)) ||
         (r = dalloc(c, &c->cand, (size_t)kc * c->CS)) || (r = dalloc(c, &c->ctl, 1)) ||
         (r = dalloc(c, &c->dense_of, (size_t)kc)) || (r = dalloc(c, &c->slot_iso, (size_t)kc)) ||
-        (r = dalloc(c, &c->rec, (size_t)c->rec_bytes))) {
+        (r = dalloc(c, &c->rec, (size_t)c->rec_bytes)) ||
+        (c->param_update != NP8_PARAM_FROZEN && (r = dalloc(c, &c->acc, (size_t)kc * (D + DP))))) {
         free_device(c);
         delete c;
         return r;
@@ -956,6 +1019,8 @@ int np8_stats(np8_ctx *c, np8_stats_t *out) {
     out->ms_assign = c->ms[0];
     out->ms_finalize = c->ms[1];
     out->ms_loglik = c->ms[2];
+    out->ms_params = c->ms[3];
+    out->mh_accepted = h.mh_accepted;
     return NP8_OK;
 }
 
@@ -999,6 +1064,8 @@ static int resize_records(np8_ctx *c, int world) {
 int np8_comm_init(np8_ctx *c, const uint8_t id[128], int32_t rank, int32_t world) {
     if (!c || world < 1 || rank < 0 || rank >= world) return NP8_ERR_ARG;
     if (!id) {  // host-exchange mode: the caller moves records (np8_step_local / np8_step_merge)
+        if (world > 1 && c->param_update != NP8_PARAM_FROZEN)
+            return fail(c, NP8_ERR_ARG, "np8_comm_init: the mh_g0 parameter update needs the RCCL transport");
         c->rank = rank;
         return resize_records(c, world);
     }

@@ -16,7 +16,14 @@ constexpr int kReqMax = 4096;     // new-cluster requests one finalize can accep
 constexpr int kMaxD = 64;
 constexpr int kMaxM = 8;
 
-enum Stream : uint32_t { kStreamAux = 1, kStreamPick = 2, kStreamInitTheta = 3, kStreamInitZ = 4 };
+enum Stream : uint32_t {
+    kStreamAux = 1,
+    kStreamPick = 2,
+    kStreamInitTheta = 3,
+    kStreamInitZ = 4,
+    kStreamParam = 5,  // MH proposal normals (i = slot)
+    kStreamParamU = 6  // MH acceptance uniforms (i = slot)
+};
 
 // Candidate-table entry layout (doubles):
 //   [mu(D) | P'(D(D+1)/2) | c | logn | logn1 | slot | iso]

@@ -24,6 +24,7 @@ struct Ctl {
     int32_t do_sort;    // this re-sort pass runs (decided by np8_sort_scan)
     uint32_t done_blocks;
     int32_t pad2;
+    int64_t mh_accepted;  // accepted MH proposals (cumulative)
 };
 
 enum : int32_t { kErrCapacity = 1 };
@@ -101,6 +102,28 @@ struct LoglikArgs {
     int64_t n_loc;
 };
 
+// Cluster-parameter update (mh_g0): per-slot statistics of the current labelling about the slot's
+// mean, then the MH chain of every live slot (DESIGN.md "Parameter update").
+struct ParamArgs {
+    const double *X;  // item-order layout [D][n_loc]
+    const int32_t *z;
+    const double *Xs[2];  // label-sorted layout (buffer ctl->cur) when sorted != 0
+    const int32_t *zs[2];
+    int32_t sorted;
+    int64_t n_loc;
+    int32_t kcap, D, steps;
+    double *acc;  // [kcap][D + DP]: sum d | packed sum d d^T, d = x - mu_slot
+    const int32_t *cnt;
+    const int32_t *dense_of;
+    double *slot_mu, *slot_P, *slot_c, *slot_sigma, *slot_iso;
+    double *cand;
+    Ctl *ctl;
+    const double *mu0, *LT, *Gp, *LTL;  // as FinArgs
+    double caux, rsk, nu, gp_iso;
+    uint64_t seed;
+    uint32_t t;
+};
+
 struct SnapArgs {
     const double *L;
     double *best;
@@ -141,3 +164,5 @@ hipError_t np8_launch_finalize(const np8::FinArgs &F, hipStream_t s);
 hipError_t np8_launch_loglik(const np8::LoglikArgs &A, int D, hipStream_t s);
 hipError_t np8_launch_loglik_reduce(const double *partial, int64_t nb, double *out, hipStream_t s);
 hipError_t np8_launch_snapshot(const np8::SnapArgs &A, hipStream_t s);
+hipError_t np8_launch_suffstats(const np8::ParamArgs &A, hipStream_t s);
+hipError_t np8_launch_mh_g0(const np8::ParamArgs &A, hipStream_t s);

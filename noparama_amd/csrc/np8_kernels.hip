@@ -591,6 +591,195 @@ __global__ __launch_bounds__(256) void np8_snapshot(SnapArgs A) {
         A.sigma_best[k] = A.slot_sigma[k];
 }
 
+// ---- cluster-parameter update (mh_g0) ------------------------------------------------------------------
+// UpdateClusters::update (src/np_update_clusters.cpp:71-142) from sufficient statistics; formulas in
+// oracle/np8_oracle.c (np8o_param_update) and DESIGN.md "Parameter update".
+
+// Per-slot statistics about the slot mean: one lane per item; the lanes of a wave that share a slot
+// (all of them on the label-sorted layout) are reduced in registers, one atomic per value and group.
+template <int D>
+__global__ __launch_bounds__(256) void np8_suffstats(ParamArgs A) {
+    constexpr int DP = D * (D + 1) / 2, W = D + DP;
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool valid = p < A.n_loc;
+    const bool sorted = A.sorted != 0;
+    const int cur = sorted ? A.ctl->cur : 0;
+    const double *__restrict__ X = sorted ? (cur ? A.Xs[1] : A.Xs[0]) : A.X;
+    const int32_t *__restrict__ z = sorted ? (cur ? A.zs[1] : A.zs[0]) : A.z;
+    const int32_t s = valid ? z[p] : -1;
+    double v[W];
+    if (valid) {
+        double d[D];
+#pragma unroll
+        for (int a = 0; a < D; ++a) {
+            d[a] = X[(int64_t)a * A.n_loc + p] - A.slot_mu[(int64_t)s * D + a];
+            v[a] = d[a];
+        }
+        int k = D;
+#pragma unroll
+        for (int a = 0; a < D; ++a)
+#pragma unroll
+            for (int b = a; b < D; ++b) v[k++] = d[a] * d[b];
+    } else {
+#pragma unroll
+        for (int w = 0; w < W; ++w) v[w] = 0.0;
+    }
+    const int lane = threadIdx.x & 63;
+    uint64_t pending = __ballot(valid);
+    while (pending) {  // wave-uniform: one pass per distinct slot in the wave
+        const int leader = __ffsll((unsigned long long)pending) - 1;
+        const int32_t sl = __shfl(s, leader);
+        const bool mine = valid && s == sl;
+        const uint64_t grp = __ballot(mine);
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+            double r = mine ? v[w] : 0.0;
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) r += __shfl_xor(r, o);
+            if (lane == leader) unsafeAtomicAdd(&A.acc[(int64_t)sl * W + w], r);
+        }
+        pending &= ~grp;
+    }
+}
+
+// G0 independence proposal `step` of slot s: the auxiliary-draw layout on stream PARAM.
+template <int D>
+__device__ __forceinline__ void mh_proposal(const ParamArgs &A, int s, int step, double &v, double (&mup)[D]) {
+    constexpr int P = (D + 2) / 2;
+    double g0 = 0.0, g1 = 0.0, xi[D];
+#pragma unroll
+    for (int k = 0; k <= D; ++k) {
+        if ((k & 1) == 0) normal_pair(A.seed, (uint64_t)s, A.t, kStreamParam, (uint32_t)(step * P + (k >> 1)), g0, g1);
+        const double g = (k & 1) ? g1 : g0;
+        if (k == 0)
+            v = fma(A.nu, g, (double)D);
+        else
+            xi[k - 1] = g;
+    }
+    const double sc = fabs(v) * A.rsk;
+#pragma unroll
+    for (int a = 0; a < D; ++a) {
+        double t0 = A.LT[a * D + a] * xi[a];
+#pragma unroll
+        for (int b = a + 1; b < D; ++b) t0 = fma(A.LT[a * D + b], xi[b], t0);
+        mup[a] = fma(sc, t0, A.mu0[a]);
+    }
+}
+
+__device__ __forceinline__ int packed_ix(int D, int a, int b) { return a * D - (a * (a - 1)) / 2 + (b - a); }
+
+// One wave per slot: the proposals of up to 64 MH steps are evaluated in parallel (their
+// likelihoods do not depend on the chain), then lane 0 walks the accept/reject sequence.
+template <int D>
+__global__ __launch_bounds__(64) void np8_mh_g0(ParamArgs A) {
+    constexpr int DP = D * (D + 1) / 2, W = D + DP;
+    const int s = blockIdx.x;
+    const int n = A.cnt[s];
+    if (n <= 0) return;
+    const int lane = threadIdx.x;
+    __shared__ double st[W];
+    __shared__ double llp[64], up[64];
+    __shared__ double s_LL;
+    __shared__ int s_chosen, s_nacc;
+    for (int w = lane; w < W; w += 64) st[w] = A.acc[(int64_t)s * W + w];
+    __syncthreads();
+    const double *s1 = st, *S = st + D;
+    const double *Pp = A.slot_P + (int64_t)s * DP;
+    double anchor[D], g1[D];
+#pragma unroll
+    for (int a = 0; a < D; ++a) anchor[a] = A.slot_mu[(int64_t)s * D + a];
+    double trPS = 0.0, trGS = 0.0;
+#pragma unroll
+    for (int k = 0; k < DP; ++k) {
+        trPS = fma(Pp[k], S[k], trPS);
+        trGS = fma(A.Gp[k], S[k], trGS);
+    }
+#pragma unroll
+    for (int a = 0; a < D; ++a) {
+        double acc = 0.0;
+#pragma unroll
+        for (int b = 0; b < D; ++b) {
+            const double G = (a == b) ? A.Gp[packed_ix(D, a, a)] : 0.5 * A.Gp[packed_ix(D, min(a, b), max(a, b))];
+            acc = fma(G, s1[b], acc);
+        }
+        g1[a] = acc;
+    }
+    const double nd = (double)n;
+    if (lane == 0) {
+        s_LL = fma(-0.5, trPS, nd * A.slot_c[s]);
+        s_chosen = -1;
+        s_nacc = 0;
+    }
+    for (int b0 = 0; b0 < A.steps; b0 += 64) {
+        const int step = b0 + lane;
+        if (step < A.steps) {
+            double v, mup[D];
+            mh_proposal<D>(A, s, step, v, mup);
+            double e[D], eg = 0.0, eGe = 0.0;
+#pragma unroll
+            for (int a = 0; a < D; ++a) {
+                e[a] = mup[a] - anchor[a];
+                eg = fma(e[a], g1[a], eg);
+            }
+            int k = 0;
+#pragma unroll
+            for (int a = 0; a < D; ++a)
+#pragma unroll
+                for (int b = a; b < D; ++b) eGe = fma(A.Gp[k++], e[a] * e[b], eGe);
+            const double tr = fma(nd, eGe, fma(-2.0, eg, trGS));
+            const double cp = fma(-(double)D, log_pos(fabs(v)), A.caux);
+            llp[lane] = fma(-0.5, tr / (v * v), nd * cp);
+            up[lane] = uniform(A.seed, (uint64_t)s, A.t, kStreamParamU, (uint32_t)step);
+        }
+        __syncthreads();
+        if (lane == 0) {  // np_update_clusters.cpp:114-137
+            double L = s_LL;
+            int ch = s_chosen, na = s_nacc;
+            const int nb = min(64, A.steps - b0);
+            for (int q = 0; q < nb; ++q) {
+                const double dl = llp[q] - L;
+                if (L == 0.0 || dl >= 0.0 || up[q] < exp_le0(dl)) {
+                    L = llp[q];
+                    ch = b0 + q;
+                    ++na;
+                }
+            }
+            s_LL = L;
+            s_chosen = ch;
+            s_nacc = na;
+        }
+        __syncthreads();
+    }
+    const int ch = s_chosen;
+    if (ch < 0) return;  // block-uniform
+    double v, mup[D];
+    mh_proposal<D>(A, s, ch, v, mup);
+    const double v2 = v * v;
+    const int CS = cand_stride(D);
+    const int row = A.dense_of[s];
+    double *crow = A.cand + (int64_t)row * CS;
+    for (int k = lane; k < DP; k += 64) {
+        const double val = A.Gp[k] / v2;
+        A.slot_P[(int64_t)s * DP + k] = val;
+        crow[D + k] = val;
+    }
+    for (int k = lane; k < D * D; k += 64) A.slot_sigma[(int64_t)s * D * D + k] = v2 * A.LTL[k];
+    if (lane == 0) {
+#pragma unroll
+        for (int a = 0; a < D; ++a) {
+            A.slot_mu[(int64_t)s * D + a] = mup[a];
+            crow[a] = mup[a];
+        }
+        const double c = fma(-(double)D, log_pos(fabs(v)), A.caux);
+        const double iso = (A.gp_iso > 0.0) ? A.Gp[0] / v2 : 0.0;
+        A.slot_c[s] = c;
+        A.slot_iso[s] = iso;
+        crow[D + DP + kFieldC] = c;
+        crow[D + DP + kFieldIso] = iso;
+        atomicAdd(reinterpret_cast<unsigned long long *>(&A.ctl->mh_accepted), (unsigned long long)s_nacc);
+    }
+}
+
 // ---- parity/debug: log-likelihood matrix --------------------------------------------------------------
 template <int D, int M>
 __global__ __launch_bounds__(256) void np8_loglik_matrix_kernel(AssignArgs A, const int64_t *__restrict__ idx,
@@ -689,6 +878,36 @@ hipError_t np8_launch_loglik(const LoglikArgs &A, int D, hipStream_t s) {
 
 hipError_t np8_launch_loglik_reduce(const double *partial, int64_t nb, double *out, hipStream_t s) {
     hipLaunchKernelGGL(np8_loglik_reduce, dim3(1), dim3(1024), 0, s, partial, nb, out);
+    return hipGetLastError();
+}
+
+hipError_t np8_launch_suffstats(const ParamArgs &A, hipStream_t s) {
+    const int64_t nb = (A.n_loc + 255) / 256;
+    if (nb <= 0) return hipSuccess;
+    switch (A.D) {
+#define Y(d)                                                                          \
+    case d:                                                                           \
+        hipLaunchKernelGGL((np8_suffstats<d>), dim3((unsigned)nb), dim3(256), 0, s, A); \
+        break;
+        Y(1) Y(2) Y(3) Y(4) Y(8) Y(16)
+#undef Y
+        default:
+            return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t np8_launch_mh_g0(const ParamArgs &A, hipStream_t s) {
+    switch (A.D) {
+#define Y(d)                                                                       \
+    case d:                                                                        \
+        hipLaunchKernelGGL((np8_mh_g0<d>), dim3((unsigned)A.kcap), dim3(64), 0, s, A); \
+        break;
+        Y(1) Y(2) Y(3) Y(4) Y(8) Y(16)
+#undef Y
+        default:
+            return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 

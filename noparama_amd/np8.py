@@ -59,7 +59,12 @@ class _Config(C.Structure):
         ("kcap", C.c_int32),
         ("chunk", C.c_int64),
         ("device", C.c_int32),
+        ("param_update", C.c_int32),
+        ("mh_steps", C.c_int32),
     ]
+
+
+PARAM_UPDATE = {"frozen": 0, "mh_g0": 1}  # NP8_PARAM_* (include/np8.h)
 
 
 class Stats(C.Structure):
@@ -74,6 +79,8 @@ class Stats(C.Structure):
         ("ms_assign", C.c_double),
         ("ms_finalize", C.c_double),
         ("ms_loglik", C.c_double),
+        ("mh_accepted", C.c_int64),
+        ("ms_params", C.c_double),
     ]
 
 
@@ -146,10 +153,12 @@ class NealAlgorithm8:
     Parameters follow the reference wiring (src/np_main.cpp:164,365-372,433-438): D (likelihood
     dimension), M auxiliaries (np_neal_algorithm8.cpp:33), alpha (Suffies_Dirichlet), and the base
     measure mu0, kappa, nu, Lambda.  `chunk` = points per synchronous step (0: whole sweep).
+    `param_update`: "frozen" (the reference's effective behaviour) or "mh_g0" (UpdateClusters as
+    intended: `mh_steps` G0-proposal MH steps per cluster after every sweep, np_update_clusters.cpp).
     """
 
     def __init__(self, D, M=3, alpha=1.0, mu0=None, kappa=1.0 / 500, nu=4.0, Lambda=None, seed=0, kcap=2048,
-                 chunk=0, device=-1):
+                 chunk=0, device=-1, param_update="frozen", mh_steps=20):
         self.D, self.M, self.kcap = int(D), int(M), int(kcap)
         self._mu0 = np.ascontiguousarray(np.full(D, 6.0) if mu0 is None else mu0, dtype=np.float64)
         self._Lam = np.ascontiguousarray(0.01 * np.eye(D) if Lambda is None else Lambda, dtype=np.float64)
@@ -159,6 +168,9 @@ class NealAlgorithm8:
         cfg.kappa, cfg.nu = float(kappa), float(nu)
         cfg.Lambda = self._Lam.ctypes.data_as(C.POINTER(C.c_double))
         cfg.seed, cfg.kcap, cfg.chunk, cfg.device = int(seed), int(kcap), int(chunk), int(device)
+        if param_update not in PARAM_UPDATE:
+            raise ValueError(f"param_update must be one of {sorted(PARAM_UPDATE)}")
+        cfg.param_update, cfg.mh_steps = PARAM_UPDATE[param_update], int(mh_steps)
         h = C.c_void_p()
         r = lib().np8_create(C.byref(h), C.byref(cfg))
         if r:

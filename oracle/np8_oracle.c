@@ -380,6 +380,7 @@ struct np8o_ctx {
     int32_t *delta;
     int64_t *rq_pos, *rq_i;
     int32_t *rq_m, *rq_zold;
+    int64_t mh_accepted;
 };
 
 static int packed_index(int D, int a, int b) { /* upper triangle, row-major, a <= b */
@@ -388,6 +389,7 @@ static int packed_index(int D, int a, int b) { /* upper triangle, row-major, a <
 
 np8o_ctx *np8o_create(const np8o_config *cfg) {
     if (cfg->D < 1 || cfg->D > NP8O_DMAX || cfg->M < 1 || cfg->M > NP8O_MMAX || cfg->kcap < 1) return NULL;
+    if (cfg->param_update < NP8O_PARAM_FROZEN || cfg->param_update > NP8O_PARAM_MH_G0 || cfg->mh_steps < 0) return NULL;
     np8o_ctx *c = (np8o_ctx *)calloc(1, sizeof(np8o_ctx));
     c->cfg = *cfg;
     const int D = cfg->D;
@@ -864,7 +866,115 @@ double np8o_total_loglik(np8o_ctx *c) {
     return L;
 }
 
+/* ---- cluster-parameter update (mh_g0) ---------------------------------------------------------
+ * The reference's UpdateClusters::update (src/np_update_clusters.cpp:71-142, called once per sweep
+ * from np_mcmc.cpp:170 with number_mh_steps = 20, :54) as it is meant to work -- in the reference
+ * the accepted proposal is sliced away, so `frozen` is its effective behaviour.
+ * Per live cluster and MH step: theta' ~ G0 (independence proposal, :33-59), accept if
+ * u < exp(LL(theta') - LL(theta)) (:118-132; LL == 0 accepts, :114-117), LL = sum over the cluster's
+ * items of log N(x | theta) (multivariatenormal.cpp:138-146), evaluated from statistics about the
+ * anchor a = mu at the start of the update (d = x - a, s1 = sum d, S = sum d d^T):
+ *   current:  LL = n c - tr(P' S)/2                                (P' = packed, off-diagonals doubled)
+ *   proposal: LL' = n c' - (tr(G S) - 2 e^T G s1 + n e^T G e) / (2 v'^2),  e = mu' - a,
+ *             G = (L^T L)^{-1}, c' = caux - D log|v'|               (Sigma' = v'^2 L^T L)
+ * Randomness: proposal normals = Philox stream PARAM (i = slot, calls step*P .. step*P+P-1, laid out
+ * like an auxiliary draw), acceptance uniform = stream PARAM_U (i = slot, call = step). */
+int np8o_suffstats(np8o_ctx *c, double *out) {
+    const int D = c->D, W = D + c->DP;
+    memset(out, 0, sizeof(double) * (size_t)c->kcap * W);
+    for (int64_t i = 0; i < c->N; ++i) {
+        const int s = c->z[i];
+        const double *x = c->X + (size_t)i * D;
+        const double *mu = c->slot_mu + (size_t)s * D;
+        double *o = out + (size_t)s * W;
+        double d[NP8O_DMAX];
+        for (int a = 0; a < D; ++a) {
+            d[a] = x[a] - mu[a];
+            o[a] += d[a];
+        }
+        for (int a = 0, k = D; a < D; ++a)
+            for (int b = a; b < D; ++b, ++k) o[k] += d[a] * d[b];
+    }
+    return 0;
+}
+
+/* log-likelihood of n items with statistics (s1, S) about anchor a under the G0 draw (v, mu'). */
+static double mh_proposal_ll(const np8o_ctx *c, int64_t n, double trGS, const double *g1, const double *anchor,
+                             double v, const double *mup) {
+    const int D = c->D;
+    double e[NP8O_DMAX], eg = 0.0, eGe = 0.0;
+    for (int a = 0; a < D; ++a) {
+        e[a] = mup[a] - anchor[a];
+        eg = fma(e[a], g1[a], eg);
+    }
+    for (int a = 0; a < D; ++a)
+        for (int b = a; b < D; ++b) eGe = fma(c->Gp[a * D + b], e[a] * e[b], eGe);
+    const double tr = fma((double)n, eGe, fma(-2.0, eg, trGS));
+    const double cp = fma(-(double)D, np8o_log_pos(fabs(v)), c->caux);
+    return fma(-0.5, tr / (v * v), (double)n * cp);
+}
+
+static void mh_proposal(const np8o_ctx *c, int s, uint32_t t, int step, double *v, double *mup) {
+    const int D = c->D, P = (D + 2) / 2;
+    double g[NP8O_DMAX + 2];
+    for (int k = 0; k < P; ++k)
+        normal_pair(c->cfg.seed, (uint64_t)s, t, NP8O_STREAM_PARAM, (uint32_t)(step * P + k), g + 2 * k);
+    aux_from_normals(c, g[0], g + 1, v, mup);
+}
+
+int64_t np8o_param_update(np8o_ctx *c, const double *stats) {
+    const int D = c->D, DP = c->DP, W = D + DP;
+    const int steps = c->cfg.mh_steps > 0 ? c->cfg.mh_steps : 20;
+    int64_t accepted = 0;
+    for (int s = 0; s < c->kcap; ++s) {
+        const int64_t n = c->cnt[s];
+        if (n <= 0) continue;
+        const double *s1 = stats + (size_t)s * W, *S = s1 + D;
+        const double *P = c->slot_P + (size_t)s * DP;
+        double anchor[NP8O_DMAX];
+        memcpy(anchor, c->slot_mu + (size_t)s * D, sizeof(double) * D);
+        double trPS = 0.0, trGS = 0.0, g1[NP8O_DMAX];
+        for (int a = 0, k = 0; a < D; ++a)
+            for (int b = a; b < D; ++b, ++k) {
+                trPS = fma(P[k], S[k], trPS);
+                trGS = fma(c->Gp[a * D + b], S[k], trGS);
+            }
+        for (int a = 0; a < D; ++a) {
+            double acc = 0.0;
+            for (int b = 0; b < D; ++b) acc = fma((a == b) ? c->Gp[a * D + b] : 0.5 * c->Gp[a * D + b], s1[b], acc);
+            g1[a] = acc;
+        }
+        double LL = fma(-0.5, trPS, (double)n * c->slot_c[s]);
+        int chosen = -1;
+        for (int step = 0; step < steps; ++step) {
+            double v, mup[NP8O_DMAX];
+            mh_proposal(c, s, c->t, step, &v, mup);
+            const double LLp = mh_proposal_ll(c, n, trGS, g1, anchor, v, mup);
+            const double u = np8o_uniform(c->cfg.seed, (uint64_t)s, c->t, NP8O_STREAM_PARAM_U, (uint32_t)step);
+            const double dl = LLp - LL;
+            if (LL == 0.0 || dl >= 0.0 || u < np8o_exp_le0(dl)) {
+                LL = LLp;
+                chosen = step;
+                ++accepted;
+            }
+        }
+        if (chosen >= 0) {
+            double v, mup[NP8O_DMAX];
+            mh_proposal(c, s, c->t, chosen, &v, mup);
+            slot_from_aux(c, s, v, mup);
+        }
+    }
+    rebuild_dense(c);
+    return accepted;
+}
+
 int np8o_end_sweep(np8o_ctx *c) {
+    if (c->cfg.param_update == NP8O_PARAM_MH_G0 && c->N > 0) {
+        double *st = (double *)malloc(sizeof(double) * (size_t)c->kcap * (c->D + c->DP));
+        np8o_suffstats(c, st);
+        c->mh_accepted += np8o_param_update(c, st);
+        free(st);
+    }
     if (c->t % 5u == 0u) { /* np_mcmc.cpp:172-174 */
         double L = np8o_total_loglik(c);
         if (L > c->best_L) {
@@ -951,6 +1061,7 @@ int np8o_get_state(np8o_ctx *c, int32_t which, int32_t *z, int32_t *K, double *m
 int32_t np8o_num_clusters(np8o_ctx *c) { return c->K; }
 uint32_t np8o_epoch(np8o_ctx *c) { return c->t; }
 double np8o_best_loglik(np8o_ctx *c) { return c->best_L; }
+int64_t np8o_mh_accepted(np8o_ctx *c) { return c->mh_accepted; }
 int32_t *np8o_z_ptr(np8o_ctx *c) { return c->z; }
 
 int np8o_loglik_matrix(np8o_ctx *c, const int64_t *idx, int64_t n, double *out) {

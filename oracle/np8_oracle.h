@@ -38,7 +38,17 @@ extern "C" {
 #define NP8O_REQMAX 4096 /* new-cluster requests one finalize accepts (must match) */
 
 /* Philox stream ids (high byte of counter word 3). */
-enum { NP8O_STREAM_AUX = 1, NP8O_STREAM_PICK = 2, NP8O_STREAM_INIT_THETA = 3, NP8O_STREAM_INIT_Z = 4 };
+enum {
+    NP8O_STREAM_AUX = 1,
+    NP8O_STREAM_PICK = 2,
+    NP8O_STREAM_INIT_THETA = 3,
+    NP8O_STREAM_INIT_Z = 4,
+    NP8O_STREAM_PARAM = 5,  /* MH proposal normals: i = slot, calls step*P .. */
+    NP8O_STREAM_PARAM_U = 6 /* MH acceptance uniform: i = slot, call = step */
+};
+
+/* Cluster-parameter update after each sweep (np_mcmc.cpp:170). */
+enum { NP8O_PARAM_FROZEN = 0, NP8O_PARAM_MH_G0 = 1 };
 
 /* ---- primitives ---------------------------------------------------------------------------- */
 void np8o_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
@@ -76,6 +86,8 @@ typedef struct {
     uint64_t seed;
     int32_t kcap;
     int64_t chunk; /* 0 => N (synchronous sweep) */
+    int32_t param_update; /* NP8O_PARAM_*: frozen = the reference's effective behaviour */
+    int32_t mh_steps;     /* MH steps per cluster and sweep (np_mcmc.cpp:54: 20); 0 -> 20 */
 } np8o_config;
 
 np8o_ctx *np8o_create(const np8o_config *cfg);
@@ -93,6 +105,7 @@ int np8o_get_state(np8o_ctx *c, int32_t which, int32_t *z, int32_t *K, double *m
 int32_t np8o_num_clusters(np8o_ctx *c);
 uint32_t np8o_epoch(np8o_ctx *c);
 double np8o_best_loglik(np8o_ctx *c);
+int64_t np8o_mh_accepted(np8o_ctx *c);
 double np8o_total_loglik(np8o_ctx *c);
 /* ll of the given points vs. every live cluster (ascending slot) then the M auxiliaries of the
  * current epoch: out is n x (K+M). Table form (what the chain uses). */
@@ -112,8 +125,15 @@ int np8o_assign_range(np8o_ctx *c, int64_t p0, int64_t p1, int32_t *delta, int64
  * owner_lo/owner_hi: only points in [owner_lo, owner_hi) get z written (all if owner_hi<0). */
 int np8o_finalize(np8o_ctx *c, const int32_t *delta, const int64_t *req_pos, const int64_t *req_i,
                   const int32_t *req_m, const int32_t *req_zold, int32_t n_req, int64_t owner_lo, int64_t owner_hi);
-/* Advance the epoch (end of sweep): max-likelihood bookkeeping (np_mcmc.cpp:172-174). */
+/* Advance the epoch (end of sweep): cluster-parameter update (np_mcmc.cpp:170) when configured,
+ * then max-likelihood bookkeeping (np_mcmc.cpp:172-174). */
 int np8o_end_sweep(np8o_ctx *c);
+/* Per-slot sufficient statistics of the current labelling about the slot's mean (anchor):
+ * out[kcap][D + D(D+1)/2] = sum d | sum d_a d_b (packed upper), d = x - mu_slot, items in order. */
+int np8o_suffstats(np8o_ctx *c, double *out);
+/* mh_g0 update of every live slot from statistics laid out as np8o_suffstats writes them;
+ * returns the number of accepted proposals. */
+int64_t np8o_param_update(np8o_ctx *c, const double *stats);
 int32_t *np8o_z_ptr(np8o_ctx *c);
 
 #ifdef __cplusplus

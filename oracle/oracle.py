@@ -31,7 +31,12 @@ class _Config(C.Structure):
         ("seed", C.c_uint64),
         ("kcap", C.c_int32),
         ("chunk", C.c_int64),
+        ("param_update", C.c_int32),
+        ("mh_steps", C.c_int32),
     ]
+
+
+PARAM_UPDATE = {"frozen": 0, "mh_g0": 1}
 
 
 def build() -> None:
@@ -90,6 +95,11 @@ def lib():
         L.np8o_assign_range.argtypes = [vp, i64, i64, vp, vp, vp, vp, vp, i32, vp]
         L.np8o_finalize.argtypes = [vp, vp, vp, vp, vp, vp, i32, i64, i64]
         L.np8o_end_sweep.argtypes = [vp]
+        L.np8o_suffstats.argtypes = [vp, vp]
+        L.np8o_param_update.argtypes = [vp, vp]
+        L.np8o_param_update.restype = i64
+        L.np8o_mh_accepted.argtypes = [vp]
+        L.np8o_mh_accepted.restype = i64
         _lib = L
     return _lib
 
@@ -157,8 +167,10 @@ class Chain:
     """The oracle chain (np8o_ctx).  Same constructor parameters as noparama_amd.NealAlgorithm8."""
 
     def __init__(self, D, M=3, alpha=1.0, mu0=None, kappa=1.0 / 500, nu=4.0, Lambda=None, seed=0,
-                 kcap=4096, chunk=0):
+                 kcap=4096, chunk=0, param_update="frozen", mh_steps=20):
         cfg = _Config()
+        cfg.param_update = PARAM_UPDATE[param_update]
+        cfg.mh_steps = mh_steps
         cfg.D, cfg.M, cfg.alpha = D, M, alpha
         mu0 = np.full(D, 6.0) if mu0 is None else np.asarray(mu0, dtype=np.float64)
         Lam = 0.01 * np.eye(D) if Lambda is None else np.asarray(Lambda, dtype=np.float64)
@@ -212,6 +224,20 @@ class Chain:
     @property
     def K(self):
         return lib().np8o_num_clusters(self._h)
+
+    @property
+    def mh_accepted(self):
+        return lib().np8o_mh_accepted(self._h)
+
+    def suffstats(self):
+        """Per-slot [kcap, D + D(D+1)/2] statistics about each slot's mean (np8o_suffstats)."""
+        out = np.zeros((self.kcap, self.D + self.D * (self.D + 1) // 2))
+        lib().np8o_suffstats(self._h, _p(out))
+        return out
+
+    def param_update(self, stats):
+        stats = np.ascontiguousarray(stats, dtype=np.float64)
+        return lib().np8o_param_update(self._h, _p(stats))
 
     @property
     def epoch(self):

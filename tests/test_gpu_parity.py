@@ -212,3 +212,42 @@ def test_host_exchange_two_ranks_equals_one():
         assert st["K"] == s1["K"]
         assert np.array_equal(st["counts"], s1["counts"])
     del z, mu, sig
+
+
+# ---- cluster-parameter update (mh_g0, UpdateClusters as intended) ------------------------------------
+# The statistics are fp64 sums whose order differs between the device (wave reduction + atomics) and
+# the oracle (item order); decisions u < exp(LL' - LL) can only differ when the two sides fall within
+# ~1e-12 of each other, so the chains are compared bit-for-bit.
+def _mh_pair(D, seed, **kw):
+    return pair(D, seed, param_update="mh_g0", **kw)
+
+
+@pytest.mark.parametrize("chunk", [0, 16])
+def test_mh_g0_twogaussians_bit_exact(chunk):
+    X, _ = datasets.twogaussians(6)
+    g, o = _mh_pair(2, 21, chunk=chunk)
+    for s in (g, o):
+        s.set_data(X)
+        s.init_random(20)
+    for _ in range(3):
+        g.sweep(2)
+        o.sweep(2)
+        assert_same_state(g, o)
+    assert g.stats()["mh_accepted"] == o.mh_accepted > 0
+
+
+@pytest.mark.parametrize("D,K", [(2, 6), (8, 16), (16, 4)])
+def test_mh_g0_warm_bit_exact(D, K):
+    """Poor starting parameters (wide covariances) so that proposals are accepted."""
+    X, z, mu, sig = datasets.mixture(20000, D, K, 0.3, 4.0, seed=D)
+    sig = sig * 9.0
+    g, o = _mh_pair(D, 300 + D, mh_steps=40)
+    for c in (g, o):
+        c.set_data(X)
+        c.set_state(z, mu, sig)
+    for _ in range(2):
+        g.sweep(2)
+        o.sweep(2)
+        assert_same_state(g, o)
+    assert g.stats()["mh_accepted"] == o.mh_accepted
+    np.testing.assert_allclose(g.total_loglik(), o.total_loglik(), rtol=1e-11)
