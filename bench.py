@@ -38,7 +38,7 @@ def parse():
     ap.add_argument("--k", type=int, default=64)
     ap.add_argument("--seed", type=int, default=20261015)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget (0 = skip)")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01c.json"))
     ap.add_argument("--param-update", default="frozen", choices=["frozen", "mh_g0"],
                     help="cluster-parameter update after every sweep (frozen = the reference's effective one)")
     return ap.parse_args()

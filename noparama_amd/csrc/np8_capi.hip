@@ -565,7 +565,8 @@ int param_update(np8_ctx *c) {
     A.seed = c->seed;
     A.t = c->epoch;
     const size_t nacc = (size_t)c->kcap * (c->D + c->DP);
-    HIPC(c, hipMemsetAsync(c->acc, 0, sizeof(double) * nacc, c->stream));
+    // acc is all zero here: allocated zeroed, and np8_mh_g0 clears every row it reads (the only
+    // rows np8_suffstats adds to are those of live slots)
     HIPC(c, np8_launch_suffstats(A, c->stream));
     if (c->world > 1) NCCLC(c, ncclAllReduce(c->acc, c->acc, nacc, ncclFloat64, ncclSum, c->comm, c->stream));
     HIPC(c, np8_launch_mh_g0(A, c->stream));

@@ -595,50 +595,100 @@ __global__ __launch_bounds__(256) void np8_snapshot(SnapArgs A) {
 // UpdateClusters::update (src/np_update_clusters.cpp:71-142) from sufficient statistics; formulas in
 // oracle/np8_oracle.c (np8o_param_update) and DESIGN.md "Parameter update".
 
-// Per-slot statistics about the slot mean: one lane per item; the lanes of a wave that share a slot
-// (all of them on the label-sorted layout) are reduced in registers, one atomic per value and group.
+// Per-slot statistics about the slot mean.  One wave per block covers kSuffRows rows of 64
+// consecutive positions (all loads issued up front).  For each distinct slot among its items -- one
+// on the label-sorted layout, a few where items moved since the last re-sort -- every lane sums its
+// items of that slot, the per-lane sums are transposed through LDS, lane c adds up component c and
+// the wave issues ONE contiguous atomic wave-instruction.  (Float atomics run at the memory side at
+// a fixed instruction rate, MI355X_MICROARCH.md "Global float atomics", so one-lane atomics per
+// component were the first bottleneck; DPP/readlane reductions of 44 components the second.)
+constexpr int kSuffRows = 4;
+
+// Column sums of T[w][0..63] for w = lane (+64 q), then one atomic add per component into dst.
+template <int W>
+__device__ __forceinline__ void suff_commit(double (*T)[65], int lane, double *dst) {
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < (W + 63) / 64; ++q) {
+        const int c = lane + 64 * q;
+        if (c < W) {
+            double r0 = 0.0, r1 = 0.0, r2 = 0.0, r3 = 0.0;
+#pragma unroll 4
+            for (int k = 0; k < 64; k += 4) {
+                r0 += T[c][k];
+                r1 += T[c][k + 1];
+                r2 += T[c][k + 2];
+                r3 += T[c][k + 3];
+            }
+            unsafeAtomicAdd(dst + c, (r0 + r1) + (r2 + r3));
+        }
+    }
+    __syncthreads();
+}
+
 template <int D>
-__global__ __launch_bounds__(256) void np8_suffstats(ParamArgs A) {
-    constexpr int DP = D * (D + 1) / 2, W = D + DP;
-    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const bool valid = p < A.n_loc;
+__global__ __launch_bounds__(64) void np8_suffstats(ParamArgs A) {
+    constexpr int W = D + D * (D + 1) / 2;
+    __shared__ double T[W][65];
+    const int lane = threadIdx.x;
     const bool sorted = A.sorted != 0;
     const int cur = sorted ? A.ctl->cur : 0;
     const double *__restrict__ X = sorted ? (cur ? A.Xs[1] : A.Xs[0]) : A.X;
     const int32_t *__restrict__ z = sorted ? (cur ? A.zs[1] : A.zs[0]) : A.z;
-    const int32_t s = valid ? z[p] : -1;
-    double v[W];
-    if (valid) {
-        double d[D];
+    const int64_t n = A.n_loc;
+    const int64_t base = (int64_t)blockIdx.x * (64 * kSuffRows) + lane;
+    double x[kSuffRows][D];
+    int32_t s[kSuffRows];
+    uint64_t pend[kSuffRows];
 #pragma unroll
-        for (int a = 0; a < D; ++a) {
-            d[a] = X[(int64_t)a * A.n_loc + p] - A.slot_mu[(int64_t)s * D + a];
-            v[a] = d[a];
-        }
-        int k = D;
+    for (int j = 0; j < kSuffRows; ++j) {
+        const int64_t p = base + 64 * j;
+        const bool v = p < n;
+        s[j] = v ? z[p] : -1;
 #pragma unroll
-        for (int a = 0; a < D; ++a)
-#pragma unroll
-            for (int b = a; b < D; ++b) v[k++] = d[a] * d[b];
-    } else {
-#pragma unroll
-        for (int w = 0; w < W; ++w) v[w] = 0.0;
+        for (int a = 0; a < D; ++a) x[j][a] = v ? X[(int64_t)a * n + p] : 0.0;
+        pend[j] = __ballot(v);
     }
-    const int lane = threadIdx.x & 63;
-    uint64_t pending = __ballot(valid);
-    while (pending) {  // wave-uniform: one pass per distinct slot in the wave
-        const int leader = __ffsll((unsigned long long)pending) - 1;
-        const int32_t sl = __shfl(s, leader);
-        const bool mine = valid && s == sl;
-        const uint64_t grp = __ballot(mine);
+    // one pass per distinct slot of the wave's items (one pass on the label-sorted layout, a few
+    // where items moved since the last re-sort)
+    for (;;) {
+        int jr = -1;
 #pragma unroll
-        for (int w = 0; w < W; ++w) {
-            double r = mine ? v[w] : 0.0;
+        for (int j = kSuffRows - 1; j >= 0; --j)
+            if (pend[j]) jr = j;
+        if (jr < 0) break;
+        uint64_t pm = pend[0];
+        int32_t sr = s[0];
 #pragma unroll
-            for (int o = 32; o > 0; o >>= 1) r += __shfl_xor(r, o);
-            if (lane == leader) unsafeAtomicAdd(&A.acc[(int64_t)sl * W + w], r);
+        for (int j = 1; j < kSuffRows; ++j) {
+            pm = (jr == j) ? pend[j] : pm;
+            sr = (jr == j) ? s[j] : sr;
         }
-        pending &= ~grp;
+        const int32_t g = __shfl(sr, __ffsll((unsigned long long)pm) - 1);
+        double mu[D];
+#pragma unroll
+        for (int a = 0; a < D; ++a) mu[a] = A.slot_mu[(int64_t)g * D + a];
+        double acc[W];
+#pragma unroll
+        for (int w = 0; w < W; ++w) acc[w] = 0.0;
+#pragma unroll
+        for (int j = 0; j < kSuffRows; ++j) {
+            const bool mine = s[j] == g;
+            pend[j] &= ~__ballot(mine);
+            double d[D];
+#pragma unroll
+            for (int a = 0; a < D; ++a) d[a] = mine ? x[j][a] - mu[a] : 0.0;
+            int k = 0;
+#pragma unroll
+            for (int a = 0; a < D; ++a, ++k) acc[k] += d[a];
+#pragma unroll
+            for (int a = 0; a < D; ++a)
+#pragma unroll
+                for (int b = a; b < D; ++b, ++k) acc[k] = fma(d[a], d[b], acc[k]);
+        }
+#pragma unroll
+        for (int w = 0; w < W; ++w) T[w][lane] = acc[w];
+        suff_commit<W>(T, lane, A.acc + (int64_t)g * W);
     }
 }
 
@@ -681,7 +731,10 @@ __global__ __launch_bounds__(64) void np8_mh_g0(ParamArgs A) {
     __shared__ double llp[64], up[64];
     __shared__ double s_LL;
     __shared__ int s_chosen, s_nacc;
-    for (int w = lane; w < W; w += 64) st[w] = A.acc[(int64_t)s * W + w];
+    for (int w = lane; w < W; w += 64) {
+        st[w] = A.acc[(int64_t)s * W + w];
+        A.acc[(int64_t)s * W + w] = 0.0;  // leaves the buffer zeroed for the next sweep
+    }
     __syncthreads();
     const double *s1 = st, *S = st + D;
     const double *Pp = A.slot_P + (int64_t)s * DP;
@@ -882,12 +935,13 @@ hipError_t np8_launch_loglik_reduce(const double *partial, int64_t nb, double *o
 }
 
 hipError_t np8_launch_suffstats(const ParamArgs &A, hipStream_t s) {
-    const int64_t nb = (A.n_loc + 255) / 256;
+    const int64_t per_block = 64 * kSuffRows;  // one wave per block
+    const int64_t nb = (A.n_loc + per_block - 1) / per_block;
     if (nb <= 0) return hipSuccess;
     switch (A.D) {
 #define Y(d)                                                                          \
     case d:                                                                           \
-        hipLaunchKernelGGL((np8_suffstats<d>), dim3((unsigned)nb), dim3(256), 0, s, A); \
+        hipLaunchKernelGGL((np8_suffstats<d>), dim3((unsigned)nb), dim3(64), 0, s, A); \
         break;
         Y(1) Y(2) Y(3) Y(4) Y(8) Y(16)
 #undef Y
