@@ -31,8 +31,8 @@ HBM_PEAK_GBS = 8000.0
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--n", type=int, default=1_000_000)
     ap.add_argument("--d", type=int, default=8)
     ap.add_argument("--k", type=int, default=64)
@@ -131,7 +131,8 @@ def main():
     Kfinal = st1["K"]
 
     # roofline of the dominant kernel (np8_assign): algorithmic flops per launch / avg launch time
-    n_launch = args.steps
+    # every launch is timed when sweeps go one by one; one per 20-sweep graph replay otherwise
+    n_launch = st1["n_timed_assign"] - st0["n_timed_assign"]
     ms_assign = (st1["ms_assign"] - st0["ms_assign"]) / max(n_launch, 1)
     Kc = Kfinal + smp.M
     n_items = hi - lo
@@ -168,7 +169,10 @@ def main():
                 "N": N, "D": D, "K_final": Kfinal, "parallelism": f"data-sharded x{world}",
                 "exchange": transport,
                 "param_update": args.param_update,
-                "ms_params_per_sweep": (st1["ms_params"] - st0["ms_params"]) / max(args.steps, 1),
+                "params_ms_per_timed_sweep": ((st1["ms_params"] - st0["ms_params"])
+                                              / (st1["n_timed_params"] - st0["n_timed_params"]))
+                if st1["n_timed_params"] > st0["n_timed_params"] else None,
+                "sweep_graphs": os.environ.get("NP8_NO_GRAPH") is None,
             },
             "roofline": {
                 "bound": "mfma",
@@ -179,6 +183,7 @@ def main():
                 "frac": achieved / FP64_PEAK_TFLOPS,
                 "traffic": traffic,
                 "assign_ms_per_launch": ms_assign,
+                "assign_launches_timed": n_launch,
                 "algorithmic_flops_per_launch": flops,
                 "hbm_frac_algorithmic": (n_items * (8 * D + 8)) / (ms_assign * 1e-3) / 1e9 / HBM_PEAK_GBS
                 if ms_assign > 0 else None,

@@ -74,6 +74,9 @@ typedef struct {
     double ms_assign, ms_finalize, ms_loglik; /* accumulated device time (when timing is enabled) */
     int64_t mh_accepted;        /* cumulative accepted parameter proposals (NP8_PARAM_MH_G0) */
     double ms_params;           /* accumulated device time of the parameter update */
+    /* launches behind ms_assign, ms_finalize, ms_loglik, ms_params: every launch when sweeps run one
+     * by one; one np8_assign launch per replay when they run from a captured 20-sweep graph */
+    int64_t n_timed_assign, n_timed_finalize, n_timed_loglik, n_timed_params;
 } np8_stats_t;
 
 /* Create / destroy.  Replaces NealAlgorithm8::NealAlgorithm8 (np_neal_algorithm8.cpp:17-34). */

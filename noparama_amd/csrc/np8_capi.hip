@@ -10,6 +10,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -25,8 +26,9 @@ namespace {
 constexpr double kLog2PiC = 1.8378770664093454835606594728112;
 
 struct Timer {
-    hipEvent_t a, b;
-    int phase;
+    hipEvent_t a = nullptr, b = nullptr;
+    int phase = -1;  // -1: not timed
+    hipGraphNode_t na = nullptr, nb = nullptr;  // event-record nodes when captured into a sweep graph
 };
 
 }  // namespace
@@ -74,8 +76,17 @@ struct np8_ctx {
     int32_t *s_hist = nullptr, *s_cursor = nullptr, *s_off = nullptr;
     bool use_sorted = false;
     bool sorted_valid = false;
-    uint32_t sorted_epoch = 0;
     uint32_t resort_every = 4;
+    // sweep graphs: kGraphSweeps synchronous sweeps captured once and replayed (launch gaps)
+    uint32_t t_base = 0;  // host mirror of ctl->t_base
+    hipGraphExec_t graph = nullptr;
+    hipGraph_t graph_tmpl = nullptr;  // kept alive: its event-record nodes are re-pointed per replay
+    int capture_timed_left = 0;
+    int graph_par = -1;          // max-likelihood check parity the graph was captured at
+    int graph_phase = -1;        // epoch mod kGraphSweeps the graph was captured at
+    bool graph_mh = false, graph_timing = false;
+    bool capturing = false, graphs_off = false;
+    std::vector<Timer> graph_timers;
     // multi-GPU
     ncclComm_t comm = nullptr;
     int rank = 0, world = 1;
@@ -318,27 +329,59 @@ int upload_slots(np8_ctx *c, const std::vector<SlotHost> &slots, const std::vect
 // Device timing: event pairs from a reusable pool (no event creation on the launch path).
 void collect_timers(np8_ctx *c);
 
-void timer_begin(np8_ctx *c, int phase, Timer &t) {
-    if (!c->timing) return;
-    if (c->timers.size() + 1 >= 4096) collect_timers(c);  // bounded pool
-    const size_t k = c->timers.size();
-    if (c->event_pool.size() < 2 * (k + 1)) {
-        hipEvent_t a, b;
+// Inside a stream capture hipEventRecord is not turned into a graph node; an event-record node is
+// added to the capturing graph explicitly and becomes the stream's capture dependency.
+void record_event(np8_ctx *c, hipEvent_t e, hipGraphNode_t *out = nullptr) {
+    if (!c->capturing) {
+        (void)hipEventRecord(e, c->stream);
+        return;
+    }
+    hipStreamCaptureStatus st;
+    unsigned long long id = 0;
+    hipGraph_t g = nullptr;
+    const hipGraphNode_t *deps = nullptr;
+    size_t nd = 0;
+    hipGraphNode_t node;
+    if (hipStreamGetCaptureInfo_v2(c->stream, &st, &id, &g, &deps, &nd) == hipSuccess &&
+        hipGraphAddEventRecordNode(&node, g, deps, nd, e) == hipSuccess) {
+        (void)hipStreamUpdateCaptureDependencies(c->stream, &node, 1, hipStreamSetCaptureDependencies);
+        if (out) *out = node;
+    }
+}
+
+// Event pair number k of the reusable pool.
+void pool_pair(np8_ctx *c, size_t k, Timer &t) {
+    while (c->event_pool.size() < 2 * (k + 1)) {
+        hipEvent_t a;
         (void)hipEventCreate(&a);
-        (void)hipEventCreate(&b);
         c->event_pool.push_back(a);
-        c->event_pool.push_back(b);
     }
     t.a = c->event_pool[2 * k];
     t.b = c->event_pool[2 * k + 1];
+}
+
+void timer_begin(np8_ctx *c, int phase, Timer &t) {
+    if (!c->timing) return;
+    if (c->capturing) {
+        // a sweep graph times one assign launch per replay: event-record nodes whose events are
+        // re-pointed to fresh pool events before every launch (run_graph)
+        if (phase != 0 || c->capture_timed_left <= 0) return;
+        c->capture_timed_left -= 1;
+        pool_pair(c, 0, t);  // placeholder events, replaced per replay
+        t.phase = phase;
+        record_event(c, t.a, &t.na);
+        return;
+    }
+    if (c->timers.size() + 1 >= 4096) collect_timers(c);  // bounded pool
+    pool_pair(c, c->timers.size(), t);
     t.phase = phase;
     (void)hipEventRecord(t.a, c->stream);
 }
 
 void timer_end(np8_ctx *c, Timer &t) {
-    if (!c->timing) return;
-    (void)hipEventRecord(t.b, c->stream);
-    c->timers.push_back(t);
+    if (!c->timing || t.phase < 0) return;
+    record_event(c, t.b, &t.nb);
+    (c->capturing ? c->graph_timers : c->timers).push_back(t);
 }
 
 void collect_timers(np8_ctx *c) {
@@ -386,7 +429,7 @@ FinArgs fin_args(np8_ctx *c, const unsigned char *recs, int world) {
     F.rsk = c->rsk;
     F.nu = c->nu;
     F.seed = c->seed;
-    F.t = c->epoch;
+    F.t = c->epoch - c->t_base;
     return F;
 }
 
@@ -413,7 +456,7 @@ AssignArgs assign_args(np8_ctx *c, int64_t p0, int64_t p1, const int64_t *order,
     A.use_perm = use_perm ? 1 : 0;
     A.perm = make_perm(c->seed, c->epoch, (uint32_t)c->n_glob);
     A.seed = c->seed;
-    A.t = c->epoch;
+    A.t = c->epoch - c->t_base;
     A.kcap = c->kcap;
     A.rec_cap = c->rec_cap;
     return A;
@@ -446,7 +489,7 @@ int launch_assign(np8_ctx *c, int64_t p0, int64_t p1, const int64_t *order, bool
 // sweeps so that items that moved cluster rejoin their group.
 int prepare_sorted(np8_ctx *c) {
     const bool stale = !c->sorted_valid;
-    if (!stale && c->epoch - c->sorted_epoch < c->resort_every) return NP8_OK;
+    if (!stale && c->epoch % c->resort_every != 0) return NP8_OK;
     SortArgs S;
     S.X = c->X;
     S.z = c->z;
@@ -465,7 +508,6 @@ int prepare_sorted(np8_ctx *c) {
     S.force = stale ? 1 : 0;  // otherwise the device re-sorts only if > n/32 items moved
     HIPC(c, np8_launch_resort(S, c->stream));
     c->sorted_valid = true;
-    c->sorted_epoch = c->epoch;
     return NP8_OK;
 }
 
@@ -563,7 +605,7 @@ int param_update(np8_ctx *c) {
     A.nu = c->nu;
     A.gp_iso = c->gp_iso;
     A.seed = c->seed;
-    A.t = c->epoch;
+    A.t = c->epoch - c->t_base;
     const size_t nacc = (size_t)c->kcap * (c->D + c->DP);
     // acc is all zero here: allocated zeroed, and np8_mh_g0 clears every row it reads (the only
     // rows np8_suffstats adds to are those of live slots)
@@ -610,12 +652,101 @@ int reset_ctl(np8_ctx *c) {
     HIPC(c, hipMemcpyAsync(c->ctl, &h, sizeof(h), hipMemcpyHostToDevice, c->stream));
     c->epoch = 0;
     c->checks = 0;
+    c->t_base = 0;
     return NP8_OK;
 }
 
 int read_ctl(np8_ctx *c, Ctl *h) {
     HIPC(c, hipStreamSynchronize(c->stream));
     HIPC(c, hipMemcpy(h, c->ctl, sizeof(Ctl), hipMemcpyDeviceToHost));
+    return NP8_OK;
+}
+
+// ---- sweep graphs ---------------------------------------------------------------------------------
+// A synchronous single-rank sweep is a fixed sequence of launches whose only per-sweep inputs are
+// the epoch (read on the device as ctl->t_base + offset), the re-sort cadence (epoch % 4) and the
+// max-likelihood cadence and parity (epoch % 5, check count).  kGraphSweeps = 20 sweeps therefore
+// repeat exactly: they are captured once into a hipGraph and replayed, which removes the host
+// launch gaps between kernels (≈6 µs each).  The graph ends with np8_advance_epoch (t_base += 20).
+constexpr uint32_t kGraphSweeps = 20;
+
+void drop_graph(np8_ctx *c) {
+    if (c->graph) (void)hipGraphExecDestroy(c->graph);
+    if (c->graph_tmpl) (void)hipGraphDestroy(c->graph_tmpl);
+    c->graph = nullptr;
+    c->graph_tmpl = nullptr;
+    c->graph_timers.clear();
+    c->graph_par = c->graph_phase = -1;
+}
+
+bool graph_eligible(np8_ctx *c, bool sync) {
+    return sync && !c->graphs_off && c->world == 1 && c->n_loc > 0 && c->sorted_valid;
+}
+
+// Captures kGraphSweeps sweeps starting at the current epoch.  Nothing runs during capture; on any
+// failure the context falls back to launching sweeps one by one (graphs_off).
+int capture_graph(np8_ctx *c) {
+    drop_graph(c);
+    int r = ensure_partial(c);  // no allocation inside the capture
+    if (r) return r;
+    const uint32_t e0 = c->epoch;
+    const int32_t ch0 = c->checks;
+    if (c->t_base != e0) {
+        HIPC(c, hipMemsetD32Async(reinterpret_cast<int *>(&c->ctl->t_base), (int)e0, 1, c->stream));
+        c->t_base = e0;
+    }
+    if (hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal) != hipSuccess) {
+        c->graphs_off = true;
+        return NP8_OK;
+    }
+    c->capturing = true;
+    c->capture_timed_left = 1;
+    for (uint32_t i = 0; i < kGraphSweeps && !r; ++i) {
+        r = step(c, 0, c->n_loc, nullptr, false);
+        if (!r) r = end_sweep(c);
+    }
+    if (!r && np8_launch_advance_epoch(c->ctl, kGraphSweeps, c->stream) != hipSuccess) r = NP8_ERR_HIP;
+    hipGraph_t g = nullptr;
+    const hipError_t ee = hipStreamEndCapture(c->stream, &g);
+    c->capturing = false;
+    c->epoch = e0;  // nothing has run yet
+    c->checks = ch0;
+    hipGraphExec_t exec = nullptr;
+    if (!r && ee == hipSuccess && g && hipGraphInstantiate(&exec, g, nullptr, nullptr, 0) == hipSuccess) {
+        c->graph = exec;
+        c->graph_tmpl = g;
+        g = nullptr;
+        c->graph_par = ch0 & 1;
+        c->graph_phase = (int)(e0 % kGraphSweeps);
+        c->graph_timing = c->timing;
+    } else {
+        c->graph_timers.clear();
+        c->graphs_off = true;
+        (void)hipGetLastError();
+    }
+    if (g) (void)hipGraphDestroy(g);
+    return NP8_OK;
+}
+
+int run_graph(np8_ctx *c) {
+    if (c->t_base != c->epoch) {  // the graph's epoch offsets are 0 .. kGraphSweeps-1
+        HIPC(c, hipMemsetD32Async(reinterpret_cast<int *>(&c->ctl->t_base), (int)c->epoch, 1, c->stream));
+        c->t_base = c->epoch;
+    }
+    std::vector<Timer> sampled;
+    for (const Timer &g : c->graph_timers) {  // fresh events for this replay, collected lazily
+        if (c->timers.size() + sampled.size() + 1 >= 4096) collect_timers(c);
+        Timer t = g;
+        pool_pair(c, c->timers.size() + sampled.size(), t);
+        HIPC(c, hipGraphExecEventRecordNodeSetEvent(c->graph, g.na, t.a));
+        HIPC(c, hipGraphExecEventRecordNodeSetEvent(c->graph, g.nb, t.b));
+        sampled.push_back(t);
+    }
+    HIPC(c, hipGraphLaunch(c->graph, c->stream));
+    for (const Timer &t : sampled) c->timers.push_back(t);
+    c->epoch += kGraphSweeps;
+    c->checks += (int32_t)(kGraphSweeps / 5);
+    c->t_base += kGraphSweeps;
     return NP8_OK;
 }
 
@@ -678,6 +809,7 @@ int np8_create(np8_ctx **out, const np8_config *cfg) {
         return NP8_ERR_HIP;
     }
     c->own_stream = true;
+    c->graphs_off = std::getenv("NP8_NO_GRAPH") != nullptr;  // A/B switch for launch-by-launch sweeps
     c->rec_cap = kReqMax;
     c->rec_bytes = record_bytes(c->kcap, c->rec_cap);
     int r = 0;
@@ -731,6 +863,7 @@ int np8_destroy(np8_ctx *c) {
     if (!c) return NP8_OK;
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     collect_timers(c);
+    drop_graph(c);
     for (hipEvent_t e : c->event_pool) (void)hipEventDestroy(e);
     if (c->comm) (void)ncclCommDestroy(c->comm);
     free_device(c);
@@ -748,6 +881,7 @@ int np8_set_data(np8_ctx *c, const double *X, int64_t n, int32_t D, int64_t offs
     if (n_global <= 0) n_global = n;
     if (offset < 0 || offset + n > n_global || n_global > 0x7FFFFFFFll)
         return fail(c, NP8_ERR_ARG, "np8_set_data: shard outside [0, n_global) or n_global >= 2^31");
+    drop_graph(c);
     c->n_loc = n;
     c->offset = offset;
     c->n_glob = n_global;
@@ -875,6 +1009,19 @@ int np8_sweep(np8_ctx *c, int32_t n_sweeps) {
     const bool sync = chunk >= N;
     if (!sync && c->world > 1) return fail(c, NP8_ERR_ARG, "np8_sweep: chunk < N is single-rank only");
     for (int s = 0; s < n_sweeps; ++s) {
+        if (graph_eligible(c, sync) && (uint32_t)(n_sweeps - s) >= kGraphSweeps) {
+            if (!c->graph || c->graph_par != (c->checks & 1) || c->graph_phase != (int)(c->epoch % kGraphSweeps) ||
+                c->graph_timing != c->timing) {
+                int r = capture_graph(c);
+                if (r) return r;
+            }
+            if (c->graph) {
+                int r = run_graph(c);
+                if (r) return r;
+                s += (int)kGraphSweeps - 1;
+                continue;
+            }
+        }
         if (N > 0) {
             for (int64_t p0 = 0; p0 < N; p0 += chunk) {
                 const int64_t p1 = (p0 + chunk < N) ? p0 + chunk : N;
@@ -1021,6 +1168,10 @@ int np8_stats(np8_ctx *c, np8_stats_t *out) {
     out->ms_finalize = c->ms[1];
     out->ms_loglik = c->ms[2];
     out->ms_params = c->ms[3];
+    out->n_timed_assign = c->n_timed[0];
+    out->n_timed_finalize = c->n_timed[1];
+    out->n_timed_loglik = c->n_timed[2];
+    out->n_timed_params = c->n_timed[3];
     out->mh_accepted = h.mh_accepted;
     return NP8_OK;
 }
@@ -1034,6 +1185,7 @@ int np8_set_timing(np8_ctx *c, int32_t enable) {
 int np8_set_stream(np8_ctx *c, void *stream) {
     if (!c) return NP8_ERR_ARG;
     (void)hipStreamSynchronize(c->stream);
+    drop_graph(c);
     if (c->own_stream) (void)hipStreamDestroy(c->stream);
     c->stream = (hipStream_t)stream;
     c->own_stream = false;

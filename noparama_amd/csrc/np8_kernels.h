@@ -25,6 +25,8 @@ struct Ctl {
     uint32_t done_blocks;
     int32_t pad2;
     int64_t mh_accepted;  // accepted MH proposals (cumulative)
+    uint32_t t_base;      // epoch = t_base + the launch's epoch offset (advanced on the device by
+    int32_t pad3;         // replayed sweep graphs, np8_advance_epoch)
 };
 
 enum : int32_t { kErrCapacity = 1 };
@@ -69,7 +71,7 @@ struct AssignArgs {
     int32_t use_perm;
     Perm perm;
     uint64_t seed;
-    uint32_t t;
+    uint32_t t;  // epoch offset: epoch = ctl->t_base + t
     int32_t kcap, rec_cap;
 };
 
@@ -90,7 +92,7 @@ struct FinArgs {
     double caux, rsk, nu;
     double gp_iso;  // common diagonal of Gp when (L^T L)^{-1} is a multiple of I, else 0
     uint64_t seed;
-    uint32_t t;
+    uint32_t t;  // epoch offset: epoch = ctl->t_base + t
 };
 
 struct LoglikArgs {
@@ -121,7 +123,7 @@ struct ParamArgs {
     const double *mu0, *LT, *Gp, *LTL;  // as FinArgs
     double caux, rsk, nu, gp_iso;
     uint64_t seed;
-    uint32_t t;
+    uint32_t t;  // epoch offset: epoch = ctl->t_base + t
 };
 
 struct SnapArgs {
@@ -166,3 +168,4 @@ hipError_t np8_launch_loglik_reduce(const double *partial, int64_t nb, double *o
 hipError_t np8_launch_snapshot(const np8::SnapArgs &A, hipStream_t s);
 hipError_t np8_launch_suffstats(const np8::ParamArgs &A, hipStream_t s);
 hipError_t np8_launch_mh_g0(const np8::ParamArgs &A, hipStream_t s);
+hipError_t np8_launch_advance_epoch(np8::Ctl *ctl, uint32_t n, hipStream_t s);

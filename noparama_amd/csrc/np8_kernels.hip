@@ -133,6 +133,7 @@ __global__ __launch_bounds__(256) void np8_assign(AssignArgs A) {
     const double *__restrict__ cand = A.cand;
     const double *__restrict__ hyp = A.hyp;
 
+    const uint32_t t = A.ctl->t_base + A.t;
     double x[D];
 #pragma unroll
     for (int a = 0; a < D; ++a) x[a] = X[(int64_t)a * A.n_loc + xr];
@@ -146,7 +147,7 @@ __global__ __launch_bounds__(256) void np8_assign(AssignArgs A) {
         const double *eo = cand + (int64_t)jo * CS;
         st.T = cand_ll<D>(eo, x) + eo[F + kFieldLogn1];
         st.S = 1.0;
-        st.u = uniform(A.seed, ig, A.t, kStreamPick, 0);
+        st.u = uniform(A.seed, ig, t, kStreamPick, 0);
         st.pick = jo;
     }
     const double zslot = (double)zi;
@@ -161,7 +162,7 @@ __global__ __launch_bounds__(256) void np8_assign(AssignArgs A) {
         whiten<D>(hyp, x, y0);
         const double logam = hyp[HypView<D>::kLogam];
 #pragma unroll 1
-        for (int m = 0; m < M; ++m) pick_step(st, aux_ll<D>(hyp, y0, A.seed, ig, A.t, m) + logam, K + m);
+        for (int m = 0; m < M; ++m) pick_step(st, aux_ll<D>(hyp, y0, A.seed, ig, t, m) + logam, K + m);
     }
 
     RecHeader *hdr = reinterpret_cast<RecHeader *>(A.rec);
@@ -369,12 +370,12 @@ __device__ const Request *request_at(const FinArgs &F, const int *base, int q) {
 
 // Auxiliary draw m of (item i, epoch t) -> a slot: the G0 draw of normalinvwishart.h:44-64 in the
 // factored form (DESIGN.md "G0").
-__device__ void write_new_slot(const FinArgs &F, const Request &r, int s) {
+__device__ void write_new_slot(const FinArgs &F, const Request &r, int s, uint32_t t) {
     const int D = F.D, DP = D * (D + 1) / 2, P = (D + 2) / 2;
     double g0 = 0.0, g1 = 0.0, v = 0.0;
     double xi[kMaxD];  // only D used
     for (int k = 0; k <= D; ++k) {
-        if ((k & 1) == 0) normal_pair(F.seed, (uint64_t)r.i, F.t, kStreamAux, (uint32_t)(r.m * P + (k >> 1)), g0, g1);
+        if ((k & 1) == 0) normal_pair(F.seed, (uint64_t)r.i, t, kStreamAux, (uint32_t)(r.m * P + (k >> 1)), g0, g1);
         const double g = (k & 1) ? g1 : g0;
         if (k == 0)
             v = fma(F.nu, g, (double)D);
@@ -489,7 +490,7 @@ __global__ __launch_bounds__(kFinThreads) void np8_finalize(FinArgs F) {
         for (int q = tid; q < nreq; q += kFinThreads) {
             const Request r = *request_at(F, base, kidx[q]);
             const int s = freeslot[q];
-            write_new_slot(F, r, s);
+            write_new_slot(F, r, s, F.ctl->t_base + F.t);
             cnt_s[s] = 1;
             if (r.i >= F.offset && r.i < F.offset + F.n_loc) {
                 F.z[r.i - F.offset] = s;
@@ -694,12 +695,13 @@ __global__ __launch_bounds__(64) void np8_suffstats(ParamArgs A) {
 
 // G0 independence proposal `step` of slot s: the auxiliary-draw layout on stream PARAM.
 template <int D>
-__device__ __forceinline__ void mh_proposal(const ParamArgs &A, int s, int step, double &v, double (&mup)[D]) {
+__device__ __forceinline__ void mh_proposal(const ParamArgs &A, uint32_t t, int s, int step, double &v,
+                                            double (&mup)[D]) {
     constexpr int P = (D + 2) / 2;
     double g0 = 0.0, g1 = 0.0, xi[D];
 #pragma unroll
     for (int k = 0; k <= D; ++k) {
-        if ((k & 1) == 0) normal_pair(A.seed, (uint64_t)s, A.t, kStreamParam, (uint32_t)(step * P + (k >> 1)), g0, g1);
+        if ((k & 1) == 0) normal_pair(A.seed, (uint64_t)s, t, kStreamParam, (uint32_t)(step * P + (k >> 1)), g0, g1);
         const double g = (k & 1) ? g1 : g0;
         if (k == 0)
             v = fma(A.nu, g, (double)D);
@@ -727,6 +729,7 @@ __global__ __launch_bounds__(64) void np8_mh_g0(ParamArgs A) {
     const int n = A.cnt[s];
     if (n <= 0) return;
     const int lane = threadIdx.x;
+    const uint32_t t = A.ctl->t_base + A.t;
     __shared__ double st[W];
     __shared__ double llp[64], up[64];
     __shared__ double s_LL;
@@ -767,7 +770,7 @@ __global__ __launch_bounds__(64) void np8_mh_g0(ParamArgs A) {
         const int step = b0 + lane;
         if (step < A.steps) {
             double v, mup[D];
-            mh_proposal<D>(A, s, step, v, mup);
+            mh_proposal<D>(A, t, s, step, v, mup);
             double e[D], eg = 0.0, eGe = 0.0;
 #pragma unroll
             for (int a = 0; a < D; ++a) {
@@ -782,7 +785,7 @@ __global__ __launch_bounds__(64) void np8_mh_g0(ParamArgs A) {
             const double tr = fma(nd, eGe, fma(-2.0, eg, trGS));
             const double cp = fma(-(double)D, log_pos(fabs(v)), A.caux);
             llp[lane] = fma(-0.5, tr / (v * v), nd * cp);
-            up[lane] = uniform(A.seed, (uint64_t)s, A.t, kStreamParamU, (uint32_t)step);
+            up[lane] = uniform(A.seed, (uint64_t)s, t, kStreamParamU, (uint32_t)step);
         }
         __syncthreads();
         if (lane == 0) {  // np_update_clusters.cpp:114-137
@@ -806,7 +809,7 @@ __global__ __launch_bounds__(64) void np8_mh_g0(ParamArgs A) {
     const int ch = s_chosen;
     if (ch < 0) return;  // block-uniform
     double v, mup[D];
-    mh_proposal<D>(A, s, ch, v, mup);
+    mh_proposal<D>(A, t, s, ch, v, mup);
     const double v2 = v * v;
     const int CS = cand_stride(D);
     const int row = A.dense_of[s];
@@ -850,7 +853,8 @@ __global__ __launch_bounds__(256) void np8_loglik_matrix_kernel(AssignArgs A, co
     for (int j = 0; j < K; ++j) out[r * (K + M) + j] = cand_ll<D>(A.cand + (int64_t)j * CS, x);
     double y0[D];
     whiten<D>(A.hyp, x, y0);
-    for (int m = 0; m < M; ++m) out[r * (K + M) + K + m] = aux_ll<D>(A.hyp, y0, A.seed, ig, A.t, m);
+    const uint32_t t = A.ctl->t_base + A.t;
+    for (int m = 0; m < M; ++m) out[r * (K + M) + K + m] = aux_ll<D>(A.hyp, y0, A.seed, ig, t, m);
 }
 
 // ---- dispatch ----------------------------------------------------------------------------------------
@@ -962,6 +966,13 @@ hipError_t np8_launch_mh_g0(const ParamArgs &A, hipStream_t s) {
         default:
             return hipErrorInvalidValue;
     }
+    return hipGetLastError();
+}
+
+__global__ void np8_advance_epoch(Ctl *ctl, uint32_t n) { ctl->t_base += n; }
+
+hipError_t np8_launch_advance_epoch(Ctl *ctl, uint32_t n, hipStream_t s) {
+    hipLaunchKernelGGL(np8_advance_epoch, dim3(1), dim3(1), 0, s, ctl, n);
     return hipGetLastError();
 }
 

@@ -81,6 +81,10 @@ class Stats(C.Structure):
         ("ms_loglik", C.c_double),
         ("mh_accepted", C.c_int64),
         ("ms_params", C.c_double),
+        ("n_timed_assign", C.c_int64),
+        ("n_timed_finalize", C.c_int64),
+        ("n_timed_loglik", C.c_int64),
+        ("n_timed_params", C.c_int64),
     ]
 
 

@@ -251,3 +251,38 @@ def test_mh_g0_warm_bit_exact(D, K):
         assert_same_state(g, o)
     assert g.stats()["mh_accepted"] == o.mh_accepted
     np.testing.assert_allclose(g.total_loglik(), o.total_loglik(), rtol=1e-11)
+
+
+def test_sweep_graph_replay_bit_exact():
+    """Runs of >= 20 synchronous sweeps are replayed from a captured hipGraph (epoch, re-sort and
+    max-likelihood cadence read on the device); results must equal the oracle's sweep by sweep."""
+    X, z, mu, sig = datasets.mixture(30000, 3, 10, 0.5, 6.0, seed=4)
+    g, o = pair(3, 77)
+    for c in (g, o):
+        c.set_data(X)
+        c.init_random(20)
+    for n in (3, 20, 41, 7, 20):  # eager, graph at any phase, graph+eager, re-capture at a new phase
+        g.sweep(n)
+        o.sweep(n)
+        assert_same_state(g, o)
+        assert_same_state(g, o, which=1)
+    assert g.stats()["epoch"] == o.epoch
+    # a new state resets the device epoch; the cached graph must follow
+    for c in (g, o):
+        c.set_state(z, mu, sig)
+    g.sweep(25)
+    o.sweep(25)
+    assert_same_state(g, o)
+    np.testing.assert_allclose(g.stats()["best_loglik"], o.best_loglik(), rtol=1e-11)
+
+
+def test_sweep_graph_mh_g0_bit_exact():
+    X, z, mu, sig = datasets.mixture(20000, 2, 6, 0.3, 4.0, seed=9)
+    g, o = _mh_pair(2, 55)
+    for c in (g, o):
+        c.set_data(X)
+        c.set_state(z, mu, sig * 9.0)
+    g.sweep(45)
+    o.sweep(45)
+    assert_same_state(g, o)
+    assert g.stats()["mh_accepted"] == o.mh_accepted
