@@ -256,8 +256,8 @@ def test_mh_g0_warm_bit_exact(D, K):
 def test_sweep_graph_replay_bit_exact():
     """Runs of >= 20 synchronous sweeps are replayed from a captured hipGraph (epoch, re-sort and
     max-likelihood cadence read on the device); results must equal the oracle's sweep by sweep."""
-    X, z, mu, sig = datasets.mixture(30000, 3, 10, 0.5, 6.0, seed=4)
-    g, o = pair(3, 77)
+    X, z, mu, sig = datasets.mixture(6000, 3, 10, 0.5, 6.0, seed=4)
+    g, o = pair(3, 77, kcap=4096)
     for c in (g, o):
         c.set_data(X)
         c.init_random(20)
