@@ -24,6 +24,7 @@ using namespace np8;
 namespace {
 
 constexpr double kLog2PiC = 1.8378770664093454835606594728112;
+constexpr int kPruneMaxKcap = 4096;  // kcap x kcap int32 candidate lists (64 MB at the limit)
 
 struct Timer {
     hipEvent_t a = nullptr, b = nullptr;
@@ -42,6 +43,13 @@ struct np8_ctx {
     int device = 0;
     int param_update = NP8_PARAM_FROZEN, mh_steps = 20;
     double *acc = nullptr;  // [kcap][D + DP] parameter-update statistics
+    // candidate pruning (np8_prune): per-slot radii and per-row candidate lists
+    double *r2 = nullptr;
+    int32_t *plist = nullptr, *plen = nullptr;
+    bool prune_on = false;     // kcap small enough for kcap x kcap lists
+    bool lists_valid = false;  // plist/plen describe the current table and membership
+    bool r2_zero = false;      // r2 is 0 for every live slot (ready to collect)
+    bool collecting = false;   // the running sweep collects r2 (a whole synchronous sweep)
     std::vector<double> mu0, Lambda;
     // base-measure precomputes (DESIGN.md "G0")
     std::vector<double> Lc, LT, UinvT, Gp, LTL;  // D*D row-major
@@ -264,7 +272,7 @@ void free_device(np8_ctx *c) {
                     c->cnt,    c->cnt_best, c->mu_best, c->sigma_best, c->cand, c->ctl,    c->hyp,
                     c->d_mu0,  c->d_LT,    c->d_Gp,   c->d_LTL,   c->rec,     c->gath,    c->order,
                     c->partial, c->dense_of, c->Xs[0], c->Xs[1], c->zs[0], c->zs[1], c->ids[0], c->ids[1],
-                    c->s_hist, c->s_cursor, c->s_off, c->slot_iso, c->acc};
+                    c->s_hist, c->s_cursor, c->s_off, c->slot_iso, c->acc, c->r2, c->plist, c->plen};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     for (int b = 0; b < 2; ++b) {
@@ -274,6 +282,8 @@ void free_device(np8_ctx *c) {
     c->s_hist = c->s_cursor = c->s_off = nullptr;
     c->slot_iso = nullptr;
     c->acc = nullptr;
+    c->r2 = nullptr;
+    c->plist = c->plen = nullptr;
     c->X = nullptr;
     c->z = c->z_best = nullptr;
     c->slot_mu = c->slot_P = c->slot_c = c->slot_sigma = nullptr;
@@ -430,6 +440,7 @@ FinArgs fin_args(np8_ctx *c, const unsigned char *recs, int world) {
     F.nu = c->nu;
     F.seed = c->seed;
     F.t = c->epoch - c->t_base;
+    F.r2 = c->r2;
     return F;
 }
 
@@ -459,6 +470,13 @@ AssignArgs assign_args(np8_ctx *c, int64_t p0, int64_t p1, const int64_t *order,
     A.t = c->epoch - c->t_base;
     A.kcap = c->kcap;
     A.rec_cap = c->rec_cap;
+    A.plist = c->plist;
+    A.plen = c->plen;
+    A.ls = c->kcap;
+    A.use_lists = 0;
+    A.collect_r2 = 0;
+    A.pad = 0;
+    A.r2 = c->r2;
     return A;
 }
 
@@ -479,8 +497,29 @@ int rebuild(np8_ctx *c) {
 int launch_assign(np8_ctx *c, int64_t p0, int64_t p1, const int64_t *order, bool use_perm) {
     Timer t;
     timer_begin(c, 0, t);
-    HIPC(c, np8_launch_assign(assign_args(c, p0, p1, order, use_perm), c->D, c->M, c->stream));
+    AssignArgs A = assign_args(c, p0, p1, order, use_perm);
+    A.collect_r2 = c->collecting ? 1 : 0;
+    A.use_lists = (c->collecting && c->lists_valid) ? 1 : 0;
+    HIPC(c, np8_launch_assign(A, c->D, c->M, c->stream));
     timer_end(c, t);
+    if (c->collecting) c->r2_zero = false;
+    return NP8_OK;
+}
+
+// Candidate lists for the next sweep from the radii this sweep collected (after every change of
+// the table: finalize and the parameter update).
+int launch_prune(np8_ctx *c) {
+    PruneArgs P;
+    P.cand = c->cand;
+    P.ctl = c->ctl;
+    P.r2 = c->r2;
+    P.plist = c->plist;
+    P.plen = c->plen;
+    P.ls = c->kcap;
+    P.D = c->D;
+    HIPC(c, np8_launch_prune(P, c->kcap, c->stream));
+    c->lists_valid = true;
+    c->r2_zero = true;
     return NP8_OK;
 }
 
@@ -520,6 +559,14 @@ int step(np8_ctx *c, int64_t p0, int64_t p1, const int64_t *order, bool use_perm
         if (r) return r;
     } else {
         c->sorted_valid = false;
+    }
+    // candidate pruning runs on whole synchronous sweeps; any other step changes the membership
+    // behind the lists' back
+    c->collecting = c->prune_on && c->use_sorted;
+    if (!c->use_sorted) c->lists_valid = c->r2_zero = false;
+    if (c->collecting && !c->r2_zero) {
+        HIPC(c, hipMemsetAsync(c->r2, 0, sizeof(double) * c->kcap, c->stream));
+        c->r2_zero = true;
     }
     int r = launch_assign(c, p0, p1, order, use_perm);
     if (r) return r;
@@ -606,6 +653,7 @@ int param_update(np8_ctx *c) {
     A.gp_iso = c->gp_iso;
     A.seed = c->seed;
     A.t = c->epoch - c->t_base;
+    A.r2 = c->r2;
     const size_t nacc = (size_t)c->kcap * (c->D + c->DP);
     // acc is all zero here: allocated zeroed, and np8_mh_g0 clears every row it reads (the only
     // rows np8_suffstats adds to are those of live slots)
@@ -619,6 +667,11 @@ int param_update(np8_ctx *c) {
 int end_sweep(np8_ctx *c) {
     int r0 = param_update(c);
     if (r0) return r0;
+    if (c->collecting) {
+        r0 = launch_prune(c);
+        if (r0) return r0;
+        c->collecting = false;
+    }
     if (c->epoch % 5u == 0u) {  // np_mcmc.cpp:172-174
         int r = launch_total_loglik(c);
         if (r) return r;
@@ -680,7 +733,8 @@ void drop_graph(np8_ctx *c) {
 }
 
 bool graph_eligible(np8_ctx *c, bool sync) {
-    return sync && !c->graphs_off && c->world == 1 && c->n_loc > 0 && c->sorted_valid;
+    return sync && !c->graphs_off && c->world == 1 && c->n_loc > 0 && c->sorted_valid &&
+           (!c->prune_on || (c->lists_valid && c->r2_zero));
 }
 
 // Captures kGraphSweeps sweeps starting at the current epoch.  Nothing runs during capture; on any
@@ -810,6 +864,7 @@ int np8_create(np8_ctx **out, const np8_config *cfg) {
     }
     c->own_stream = true;
     c->graphs_off = std::getenv("NP8_NO_GRAPH") != nullptr;  // A/B switch for launch-by-launch sweeps
+    c->prune_on = c->kcap <= kPruneMaxKcap && std::getenv("NP8_NO_PRUNE") == nullptr;
     c->rec_cap = kReqMax;
     c->rec_bytes = record_bytes(c->kcap, c->rec_cap);
     int r = 0;
@@ -821,7 +876,9 @@ int np8_create(np8_ctx **out, const np8_config *cfg) {
         (r = dalloc(c, &c->cand, (size_t)kc * c->CS)) || (r = dalloc(c, &c->ctl, 1)) ||
         (r = dalloc(c, &c->dense_of, (size_t)kc)) || (r = dalloc(c, &c->slot_iso, (size_t)kc)) ||
         (r = dalloc(c, &c->rec, (size_t)c->rec_bytes)) ||
-        (c->param_update != NP8_PARAM_FROZEN && (r = dalloc(c, &c->acc, (size_t)kc * (D + DP))))) {
+        (c->param_update != NP8_PARAM_FROZEN && (r = dalloc(c, &c->acc, (size_t)kc * (D + DP)))) ||
+        (kc <= kPruneMaxKcap && ((r = dalloc(c, &c->r2, (size_t)kc)) || (r = dalloc(c, &c->plen, (size_t)kc)) ||
+                                 (r = dalloc(c, &c->plist, (size_t)kc * kc))))) {
         free_device(c);
         delete c;
         return r;
@@ -845,12 +902,15 @@ int np8_create(np8_ctx **out, const np8_config *cfg) {
         delete c;
         return r;
     }
-    (void)hipMemcpy(c->hyp, hyp.data(), sizeof(double) * hyp.size(), hipMemcpyHostToDevice);
-    (void)hipMemcpy(c->d_mu0, c->mu0.data(), sizeof(double) * D, hipMemcpyHostToDevice);
-    (void)hipMemcpy(c->d_LT, c->LT.data(), sizeof(double) * D * D, hipMemcpyHostToDevice);
-    (void)hipMemcpy(c->d_Gp, gp.data(), sizeof(double) * gp.size(), hipMemcpyHostToDevice);
-    (void)hipMemcpy(c->d_LTL, c->LTL.data(), sizeof(double) * D * D, hipMemcpyHostToDevice);
-    if (reset_ctl(c) || hipStreamSynchronize(c->stream) != hipSuccess) {
+    // on the context's stream, behind the zero-fills dalloc queued there (a null-stream hipMemcpy does
+    // not order against a non-blocking stream: the fill could land after the copy)
+    const bool up_ok =
+        hipMemcpyAsync(c->hyp, hyp.data(), sizeof(double) * hyp.size(), hipMemcpyHostToDevice, c->stream) == hipSuccess &&
+        hipMemcpyAsync(c->d_mu0, c->mu0.data(), sizeof(double) * D, hipMemcpyHostToDevice, c->stream) == hipSuccess &&
+        hipMemcpyAsync(c->d_LT, c->LT.data(), sizeof(double) * D * D, hipMemcpyHostToDevice, c->stream) == hipSuccess &&
+        hipMemcpyAsync(c->d_Gp, gp.data(), sizeof(double) * gp.size(), hipMemcpyHostToDevice, c->stream) == hipSuccess &&
+        hipMemcpyAsync(c->d_LTL, c->LTL.data(), sizeof(double) * D * D, hipMemcpyHostToDevice, c->stream) == hipSuccess;
+    if (!up_ok || reset_ctl(c) || hipStreamSynchronize(c->stream) != hipSuccess) {
         free_device(c);
         delete c;
         return NP8_ERR_HIP;
@@ -882,6 +942,7 @@ int np8_set_data(np8_ctx *c, const double *X, int64_t n, int32_t D, int64_t offs
     if (offset < 0 || offset + n > n_global || n_global > 0x7FFFFFFFll)
         return fail(c, NP8_ERR_ARG, "np8_set_data: shard outside [0, n_global) or n_global >= 2^31");
     drop_graph(c);
+    c->lists_valid = c->r2_zero = c->collecting = false;
     c->n_loc = n;
     c->offset = offset;
     c->n_glob = n_global;
@@ -914,6 +975,7 @@ static int set_state_common(np8_ctx *c, const std::vector<SlotHost> &slots, cons
     HIPC(c, hipMemcpyAsync(c->z, zloc.data(), sizeof(int32_t) * zloc.size(), hipMemcpyHostToDevice, c->stream));
     c->sorted_valid = false;
     c->use_sorted = false;
+    c->lists_valid = c->r2_zero = c->collecting = false;
     r = reset_ctl(c);
     if (r) return r;
     r = rebuild(c);
@@ -1240,6 +1302,8 @@ int np8_step_local(np8_ctx *c, void *record_out) {
         int r0 = prepare_sorted(c);
         if (r0) return r0;
     }
+    c->collecting = false;  // no pruning on the host-exchange path
+    c->lists_valid = c->r2_zero = false;
     int r = launch_assign(c, 0, c->n_loc, nullptr, false);
     if (r) return r;
     HIPC(c, hipMemcpyAsync(record_out, c->rec, (size_t)c->rec_bytes, hipMemcpyDeviceToHost, c->stream));

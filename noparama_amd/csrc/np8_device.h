@@ -33,7 +33,6 @@ NP8_HD int packed_size(int D) { return D * (D + 1) / 2; }
 NP8_HD int cand_stride(int D) { return (D + packed_size(D) + 5 + 1) & ~1; }
 enum CandField : int { kFieldC = 0, kFieldLogn = 1, kFieldLogn1 = 2, kFieldSlot = 3, kFieldIso = 4 };
 
-NP8_HD uint32_t mulhi32(uint32_t a, uint32_t b) { return (uint32_t)(((uint64_t)a * b) >> 32); }
 
 // Philox4x32-10 (Salmon et al. SC'11).
 NP8_HD void philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1,
@@ -44,12 +43,14 @@ NP8_HD void philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, ui
             k0 += 0x9E3779B9u;
             k1 += 0xBB67AE85u;
         }
-        const uint32_t hi0 = mulhi32(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
-        const uint32_t hi1 = mulhi32(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
-        c0 = hi1 ^ c1 ^ k0;
-        c1 = lo1;
-        c2 = hi0 ^ c3 ^ k1;
-        c3 = lo0;
+        // one 32x32->64 product per multiplier: a single v_mad_u64_u32 instead of a
+        // v_mul_hi_u32 + v_mul_lo_u32 pair
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+        const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+        c0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
+        c1 = (uint32_t)p1;
+        c2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+        c3 = (uint32_t)p0;
     }
     out[0] = c0;
     out[1] = c1;

@@ -73,6 +73,22 @@ struct AssignArgs {
     uint64_t seed;
     uint32_t t;  // epoch offset: epoch = ctl->t_base + t
     int32_t kcap, rec_cap;
+    // candidate pruning (DESIGN.md "Pruning"): a wave whose items all sit in dense row k0 walks
+    // plist[k0*ls .. +plen[k0]] instead of every row; r2 collects max |x - mu|^2 per slot for the
+    // lists of the next sweep
+    const int32_t *plist, *plen;
+    int32_t ls, use_lists, collect_r2, pad;
+    double *r2;
+};
+
+// Builds the candidate lists of every live dense row from the radii r2 collected by the sweep
+// (then clears r2 for the next one).  One block per row.
+struct PruneArgs {
+    const double *cand;
+    const Ctl *ctl;
+    double *r2;
+    int32_t *plist, *plen;
+    int32_t ls, D;
 };
 
 struct FinArgs {
@@ -93,6 +109,7 @@ struct FinArgs {
     double gp_iso;  // common diagonal of Gp when (L^T L)^{-1} is a multiple of I, else 0
     uint64_t seed;
     uint32_t t;  // epoch offset: epoch = ctl->t_base + t
+    double *r2;  // pruning radii: +inf for every slot created here (unknown radius)
 };
 
 struct LoglikArgs {
@@ -124,6 +141,7 @@ struct ParamArgs {
     double caux, rsk, nu, gp_iso;
     uint64_t seed;
     uint32_t t;  // epoch offset: epoch = ctl->t_base + t
+    double *r2;  // pruning radii: +inf for every slot whose parameters change
 };
 
 struct SnapArgs {
@@ -169,3 +187,4 @@ hipError_t np8_launch_snapshot(const np8::SnapArgs &A, hipStream_t s);
 hipError_t np8_launch_suffstats(const np8::ParamArgs &A, hipStream_t s);
 hipError_t np8_launch_mh_g0(const np8::ParamArgs &A, hipStream_t s);
 hipError_t np8_launch_advance_epoch(np8::Ctl *ctl, uint32_t n, hipStream_t s);
+hipError_t np8_launch_prune(const np8::PruneArgs &A, int kcap, hipStream_t s);

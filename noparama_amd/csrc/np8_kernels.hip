@@ -152,10 +152,24 @@ __global__ __launch_bounds__(256) void np8_assign(AssignArgs A) {
     }
     const double zslot = (double)zi;
     const int K = A.ctl->K;
-    for (int j = 0; j < K; ++j) {
-        const double *e = cand + (int64_t)j * CS;  // wave-uniform: scalar loads
-        const double lw = cand_ll<D>(e, x) + e[F + kFieldLogn];
-        if (e[F + kFieldSlot] != zslot) pick_step(st, lw, j);
+    // a wave whose items share their cluster (the label-sorted layout) walks that cluster's pruned
+    // candidate list: the rows left out are skipped by every lane's pick_step anyway (np8_prune)
+    const int32_t z0 = __builtin_amdgcn_readfirstlane(zi);
+    if (A.use_lists && __ballot(zi != z0) == 0) {
+        const int32_t j0 = __builtin_amdgcn_readfirstlane(jo);
+        const int32_t nl = A.plen[j0];
+        const int32_t *__restrict__ lst = A.plist + (int64_t)j0 * A.ls;
+        for (int q = 0; q < nl; ++q) {
+            const int j = lst[q];  // wave-uniform: scalar loads
+            const double *e = cand + (int64_t)j * CS;
+            pick_step(st, cand_ll<D>(e, x) + e[F + kFieldLogn], j);
+        }
+    } else {
+        for (int j = 0; j < K; ++j) {
+            const double *e = cand + (int64_t)j * CS;  // wave-uniform: scalar loads
+            const double lw = cand_ll<D>(e, x) + e[F + kFieldLogn];
+            if (e[F + kFieldSlot] != zslot) pick_step(st, lw, j);
+        }
     }
     {
         double y0[D];
@@ -168,6 +182,29 @@ __global__ __launch_bounds__(256) void np8_assign(AssignArgs A) {
     RecHeader *hdr = reinterpret_cast<RecHeader *>(A.rec);
     int32_t *delta = reinterpret_cast<int32_t *>(A.rec + kRecHeaderBytes);
     const int32_t snew = (st.pick < K) ? (int32_t)cand[(int64_t)st.pick * CS + F + kFieldSlot] : -1;
+    if (A.collect_r2) {
+        // radius of the item's cluster for the next sweep's lists: its distance to the mean of the row
+        // it joins (an item that asked for a new cluster counts for its old one, in case the request
+        // is rejected; the new slot's radius is set to +inf by np8_finalize)
+        const int32_t tr = (st.pick < K) ? st.pick : jo;
+        const int32_t ts = (st.pick < K) ? snew : zi;
+        const double *e = cand + (int64_t)tr * CS;
+        double d2 = 0.0;
+#pragma unroll
+        for (int a = 0; a < D; ++a) {
+            const double dd = x[a] - e[a];
+            d2 = fma(dd, dd, d2);
+        }
+        const int32_t t0 = __builtin_amdgcn_readfirstlane(ts);
+        if (__ballot(1) == ~0ull && __ballot(ts != t0) == 0) {  // full wave, one slot: one atomic
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) d2 = fmax(d2, __shfl_xor(d2, o));
+            if ((threadIdx.x & 63) == 0)
+                atomicMax(reinterpret_cast<unsigned long long *>(A.r2 + t0), (unsigned long long)__double_as_longlong(d2));
+        } else {
+            atomicMax(reinterpret_cast<unsigned long long *>(A.r2 + ts), (unsigned long long)__double_as_longlong(d2));
+        }
+    }
     // items leaving their cluster, counted per wave (drives the re-sort of the layout)
     const uint64_t mv = __ballot(snew != zi);
     if (mv && (threadIdx.x & 63) == (__ffsll((unsigned long long)__ballot(1)) - 1))
@@ -394,6 +431,7 @@ __device__ void write_new_slot(const FinArgs &F, const Request &r, int s, uint32
     F.slot_c[s] = fma(-(double)D, log_pos(fabs(v)), F.caux);
     for (int k = 0; k < D * D; ++k) F.slot_sigma[(int64_t)s * D * D + k] = v2 * F.LTL[k];
     F.slot_iso[s] = (F.gp_iso > 0.0) ? F.Gp[0] / v2 : 0.0;
+    if (F.r2) F.r2[s] = __longlong_as_double(0x7FF0000000000000ll);  // radius unknown until a sweep measures it
 }
 
 }  // namespace
@@ -830,6 +868,7 @@ __global__ __launch_bounds__(64) void np8_mh_g0(ParamArgs A) {
         const double iso = (A.gp_iso > 0.0) ? A.Gp[0] / v2 : 0.0;
         A.slot_c[s] = c;
         A.slot_iso[s] = iso;
+        if (A.r2) A.r2[s] = __longlong_as_double(0x7FF0000000000000ll);  // the mean moved
         crow[D + DP + kFieldC] = c;
         crow[D + DP + kFieldIso] = iso;
         atomicAdd(reinterpret_cast<unsigned long long *>(&A.ctl->mh_accepted), (unsigned long long)s_nacc);
@@ -969,7 +1008,77 @@ hipError_t np8_launch_mh_g0(const ParamArgs &A, hipStream_t s) {
     return hipGetLastError();
 }
 
+// ---- candidate pruning ------------------------------------------------------------------------------
+// For dense row k0 (mean mu0, radius R = max |x - mu0| over its items, collected by the sweep), row j
+// can be left out of k0's list when no item of k0 can bring it within kSkip of its own log-weight:
+//   lw_j(x) - lw_own(x) <= (c_j + log n_j) - (c_0 + log(n_0 - 1)) - iso_j (|mu_j - mu0| - R)^2 / 2
+//                           + iso_0 R^2 / 2  =: U,
+// using q_j(x) = iso_j |x - mu_j|^2 >= iso_j (|mu_j - mu0| - R)^2 (triangle inequality) and
+// q_0(x) <= iso_0 R^2; T >= lw_own at every step of the pick.  Rows are left out only for U below
+// -kSkip by a margin of 2 nats plus 1e-9 of the terms' magnitude (rounding of the kernel's own
+// arithmetic is ~1e-15 relative).  Non-isotropic rows and singletons (own weight 0) keep every row.
+__global__ __launch_bounds__(256) void np8_prune(PruneArgs A) {
+    __shared__ int wsum[4];
+    const int K = A.ctl->K;
+    const int k0 = blockIdx.x;
+    if (k0 >= K) return;
+    const int D = A.D, DP = D * (D + 1) / 2, CS = cand_stride(D), F = D + DP;
+    const double *e0 = A.cand + (int64_t)k0 * CS;
+    const int slot0 = (int)e0[F + kFieldSlot];
+    const double R2 = A.r2[slot0];
+    const double iso0 = e0[F + kFieldIso];
+    const double base0 = e0[F + kFieldC] + e0[F + kFieldLogn1];
+    const bool prunable = iso0 > 0.0 && R2 < 1e300 && base0 > -1e299;
+    const double R = sqrt(R2);
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    int count = 0;
+    for (int jb = 0; jb < K; jb += 256) {
+        const int j = jb + tid;
+        bool keep = j < K && j != k0;
+        if (keep && prunable) {
+            const double *ej = A.cand + (int64_t)j * CS;
+            const double isoj = ej[F + kFieldIso];
+            if (isoj > 0.0) {
+                double dist2 = 0.0;
+                for (int a = 0; a < D; ++a) {
+                    const double dd = ej[a] - e0[a];
+                    dist2 = fma(dd, dd, dist2);
+                }
+                const double delta = sqrt(dist2) - R;
+                if (delta > 0.0) {
+                    const double wj = ej[F + kFieldC] + ej[F + kFieldLogn];
+                    const double far = 0.5 * isoj * delta * delta, near = 0.5 * iso0 * R2;
+                    const double U = (wj - base0) - far + near;
+                    const double mag = fabs(wj) + fabs(base0) + far + near;
+                    keep = !(U <= -kSkip - 2.0 - 1e-9 * mag);
+                }
+            }
+        }
+        const uint64_t b = __ballot(keep);
+        const int rank = __popcll(b & ((1ull << lane) - 1ull));
+        if (lane == 0) wsum[wv] = __popcll(b);
+        __syncthreads();
+        int before = 0, total = 0;
+        for (int w = 0; w < 4; ++w) {
+            before += (w < wv) ? wsum[w] : 0;
+            total += wsum[w];
+        }
+        if (keep) A.plist[(int64_t)k0 * A.ls + count + before + rank] = j;
+        count += total;
+        __syncthreads();
+    }
+    if (tid == 0) {
+        A.plen[k0] = count;
+        A.r2[slot0] = 0.0;  // collected afresh by the next sweep
+    }
+}
+
 __global__ void np8_advance_epoch(Ctl *ctl, uint32_t n) { ctl->t_base += n; }
+
+hipError_t np8_launch_prune(const PruneArgs &A, int kcap, hipStream_t s) {
+    hipLaunchKernelGGL(np8_prune, dim3((unsigned)kcap), dim3(256), 0, s, A);
+    return hipGetLastError();
+}
 
 hipError_t np8_launch_advance_epoch(Ctl *ctl, uint32_t n, hipStream_t s) {
     hipLaunchKernelGGL(np8_advance_epoch, dim3(1), dim3(1), 0, s, ctl, n);
