@@ -222,7 +222,10 @@ void NealAlgorithm8Hip::printStatistics() {
 MCMC::MCMC(NealAlgorithm8Hip &sampler, int k_init) : _sampler(sampler), _k_init(k_init) {}
 
 void MCMC::run(dataset_t &dataset, int T) {
-    for (auto *d : dataset) _membertrix.addData(*d);
+    for (auto *d : dataset) {
+        _membertrix.addData(*d);
+        _max_likelihood_membertrix.addData(*d);
+    }
     _sampler.setData(dataset);
     _sampler.initRandom(_k_init);
     data_ids_t all(dataset.size());

@@ -2,9 +2,10 @@
 // clustering path (src/np_main.cpp:156-507):
 //   np8_noparama -d <data> -a algorithm8 -T <sweeps> -c clustering [-s seed] [-C chunk] [-D dims]
 // reads "x_1 .. x_D label" rows (np_main.cpp:57-148, generalised from 2 columns), runs MCMC on the
-// GPU, and writes <workspace>/<stamp>/{snapshot,results}.score.txt in the reference's format
-// (clustering_performance.cpp:84-93) for the last state and the max-likelihood state.  Refuses to
-// overwrite an existing workspace (exit 106, np_main.cpp:273-276).
+// GPU, and writes <workspace><YYYYmmdd_HH:MM>/{snapshot,results}{,<k>,.score}.txt and the LATEST
+// symlink in the reference's formats (np_results.cpp:39-196, host/np_results.h) for the last state
+// and the max-likelihood state.  Refuses to overwrite an existing workspace (exit 106,
+// np_main.cpp:273-276).
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -12,10 +13,13 @@
 #include <cstdlib>
 #include <fstream>
 #include <iostream>
+#include <ctime>
+#include <iomanip>
 #include <sstream>
 #include <string>
 
 #include "np_host.h"
+#include "np_results.h"
 
 static void usage(const char *p) {
     std::cerr << "usage: " << p << " -d <datafile> -a algorithm8 [-T sweeps=2000] [-c clustering] [-s seed]"
@@ -104,16 +108,17 @@ int main(int argc, char *argv[]) {
         mcmc.run(dataset, T);
         double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         sampler.printStatistics();
-        std::string dir = ws + std::to_string(seed) + "/";
-        std::string cmd = "mkdir -p '" + dir + "'";
-        if (std::system(cmd.c_str()) != 0) return 1;
+        // np_main.cpp:476-497: <workspace><YYYYmmdd_HH:MM>/{snapshot,results}*, LATEST symlink
+        const std::time_t now = std::time(nullptr);
+        std::tm tm = *std::localtime(&now);
+        std::stringstream tss;
+        tss << std::put_time(&tm, "%Y%m%d_%H:%M");
+        const std::string dirname = tss.str();
         for (int which = 0; which < 2; ++which) {
             const membertrix &m = which ? mcmc.getMaxLikelihoodMatrix() : mcmc.getMembershipMatrix();
-            std::vector<int> res(m.count());
-            for (size_t i = 0; i < m.count(); ++i) res[i] = m.getClusterId((data_id_t)i);
-            clustering_performance cp;
-            cp.calculate(gt, res);
-            cp.write(dir + (which ? "results" : "snapshot") + ".score.txt");
+            Results res(m, gt);
+            res.write(ws, dirname, which ? "results" : "snapshot");
+            const clustering_performance &cp = res.performance();
             std::cout << (which ? "results" : "snapshot") << ": K=" << m.getClusterCount() << " Purity: " << cp.purity
                       << " Rand Index: " << cp.rand_index << " Adjusted Rand Index: " << cp.adjusted_rand_index
                       << std::endl;

@@ -32,9 +32,31 @@ def test_twogaussians_t1000_end_to_end(tmp_path):
     ws = str(tmp_path / "ws") + "/"
     r = run(["-d", DATA, "-a", "algorithm8", "-T", "1000", "-c", "clustering", "-s", "5", "-w", ws])
     assert r.returncode == 0, r.stderr + r.stdout
-    score = open(os.path.join(ws, "5", "results.score.txt")).read()
+    run_dir = os.path.join(ws, "LATEST")  # np_results.cpp:53-63
+    score = open(os.path.join(run_dir, "results.score.txt")).read()
     vals = dict(ln.split(": ") for ln in score.strip().splitlines())
     assert set(vals) == {"Purity", "Rand Index", "Adjusted Rand Index"}
     assert float(vals["Purity"]) > 0.95  # README.rst:53-55 "should be almost 1"
     assert float(vals["Adjusted Rand Index"]) > 0.0
-    assert os.path.exists(os.path.join(ws, "5", "snapshot.score.txt"))
+    for base in ("snapshot", "results"):
+        assert os.path.exists(os.path.join(run_dir, base + ".score.txt"))
+        K = int(open(os.path.join(run_dir, base + ".txt")).read().split("# rows: ")[1].split()[0])
+        sizes = [len(open(os.path.join(run_dir, f"{base}{k}.txt")).read().splitlines()) for k in range(K)]
+        assert sum(sizes) == 200 and min(sizes) > 0  # every item in exactly one cluster file
+
+
+def test_results_files_in_reference_format(tmp_path):
+    """np_results.cpp:39-196: per-cluster item files, Octave mu/sigma, scores, LATEST symlink."""
+    exe = os.path.join(ROOT, "host", "build", "results_selftest")
+    ws = str(tmp_path) + "/"
+    r = subprocess.run([exe, ws], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    d = os.path.join(ws, "20261015_12:00")
+    assert os.path.realpath(os.path.join(ws, "LATEST")) == os.path.realpath(d)
+    assert open(os.path.join(d, "results0.txt")).read() == "1.5 2.25 \n1 2 \n1.25 2.5 \n"
+    assert open(os.path.join(d, "results1.txt")).read() == "-3 0.5 \n-2.5 0.75 \n"
+    assert open(os.path.join(d, "results.txt")).read() == (
+        "# name: mu\n# type: matrix\n# rows: 2\n# columns: 2\n 1.25 2.25\n -2.75 0.625\n\n\n"
+        "# name: sigma\n# type: matrix\n# ndims: 3\n 2 2 2\n 0.1 0 \n0 0.2\n 0.3 0.01 \n0.01 0.4\n")
+    assert open(os.path.join(d, "results.score.txt")).read() == (
+        "Purity: 1\nRand Index: 1\nAdjusted Rand Index: 1\n")
