@@ -9,12 +9,15 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstdlib>
 #include <fstream>
 #include <iostream>
 #include <ctime>
 #include <iomanip>
+#include <numeric>
+#include <random>
 #include <sstream>
 #include <string>
 
@@ -24,10 +27,23 @@
 static void usage(const char *p) {
     std::cerr << "usage: " << p << " -d <datafile> -a algorithm8 [-T sweeps=2000] [-c clustering] [-s seed]"
               << " [-C chunk (0 = data-parallel sweep, 1 = sequential)] [-D dims=2] [-w workspace]"
-              << " [-u frozen|mh_g0 (cluster-parameter update)]" << std::endl;
+              << " [-u frozen|mh_g0 (cluster-parameter update)]"
+              << " [-n subsample size=200, 0 = all items]; data: 'x_1 .. x_D label' text or [N][D+1] .f64"
+              << std::endl;
 }
 
+// Rows "x_1 .. x_D label" (np_main.cpp:57-148, generalised from 2 columns), or, for a file ending in
+// ".f64", the same rows as raw little-endian float64 ([N][D+1], written by noparama_amd.datasets).
 static bool read_data(const std::string &fn, int D, dataset_t &ds, std::vector<int> &gt) {
+    if (fn.size() > 4 && fn.compare(fn.size() - 4, 4, ".f64") == 0) {
+        std::ifstream f(fn, std::ios::binary);
+        std::vector<double> row((size_t)D + 1);
+        while (f.read(reinterpret_cast<char *>(row.data()), (std::streamsize)(sizeof(double) * row.size()))) {
+            ds.push_back(new data_t(row.begin(), row.begin() + D));
+            gt.push_back((int)row[D]);
+        }
+        return !ds.empty();
+    }
     std::ifstream f(fn);
     std::string line;
     while (std::getline(f, line)) {
@@ -47,14 +63,34 @@ static bool read_data(const std::string &fn, int D, dataset_t &ds, std::vector<i
     return !ds.empty();
 }
 
+// np_main.cpp:283-295: a random permutation of the items, of which the first `n` are kept (the
+// reference always subsamples, n = 200, :166-167); n <= 0 keeps all items in file order.
+static void subsample(dataset_t &ds, std::vector<int> &gt, int n, uint64_t seed) {
+    if (n <= 0) return;
+    if ((size_t)n > ds.size()) n = (int)ds.size();  // the reference asserts here (:291)
+    std::vector<size_t> idx(ds.size());
+    std::iota(idx.begin(), idx.end(), 0);
+    std::mt19937_64 gen(seed ^ 0x5DEECE66DULL);
+    std::shuffle(idx.begin(), idx.end(), gen);  // dim1algebra.hpp:2020-2025
+    dataset_t out;
+    std::vector<int> g;
+    for (int i = 0; i < n; ++i) {
+        out.push_back(ds[idx[i]]);
+        g.push_back(gt[idx[i]]);
+    }
+    for (size_t i = n; i < idx.size(); ++i) delete ds[idx[i]];
+    ds.swap(out);
+    gt.swap(g);
+}
+
 int main(int argc, char *argv[]) {
     std::string data, algo, mode = "clustering", ws, upd = "frozen";
-    int T = 2000, D = 2;
+    int T = 2000, D = 2, nsub = 200;
     long long chunk = 0;
     unsigned long long seed = 0;
     bool seeded = false;
     int tok;
-    while ((tok = getopt(argc, argv, "d:a:T:c:s:C:D:w:u:h?")) != EOF) {
+    while ((tok = getopt(argc, argv, "d:a:T:c:s:C:D:w:u:n:h?")) != EOF) {
         switch (tok) {
             case 'd': data = optarg; break;
             case 'a': algo = optarg; break;
@@ -65,6 +101,7 @@ int main(int argc, char *argv[]) {
             case 'D': D = std::stoi(optarg); break;
             case 'w': ws = optarg; break;
             case 'u': upd = optarg; break;
+            case 'n': nsub = std::stoi(optarg); break;
             default: usage(argv[0]); return 1;
         }
     }
@@ -93,6 +130,7 @@ int main(int argc, char *argv[]) {
         std::cerr << "No data found... Check the file or the contents of the file." << std::endl;
         return 7;
     }
+    subsample(dataset, gt, nsub, seed);
     np8_prior prior;
     prior.D = D;
     if (upd == "mh_g0") {

@@ -29,12 +29,24 @@ def write_data(path, X, labels):
 
 def read_data(path, D=None):
     """Reader of the reference format, generalised to D value columns + one label column
-    (src/np_main.cpp:57-148 hard-codes 2 columns in clustering mode)."""
+    (src/np_main.cpp:57-148 hard-codes 2 columns in clustering mode).  A path ending in ".f64" is
+    the binary form: raw float64 rows [N][D+1] (D required), memory-mapped."""
+    if str(path).endswith(".f64"):
+        if D is None:
+            raise ValueError("read_data: D is required for .f64 files")
+        A = np.memmap(path, dtype="<f8", mode="r").reshape(-1, D + 1)
+        return np.ascontiguousarray(A[:, :D]), A[:, D].astype(np.int32)
     rows = [list(map(float, ln.split())) for ln in open(path) if ln.strip()]
     A = np.asarray(rows, dtype=np.float64)
     if D is None:
         D = A.shape[1] - 1
     return np.ascontiguousarray(A[:, :D]), A[:, D].astype(np.int32)
+
+
+def write_data_f64(path, X, labels):
+    """Binary form of the data file: little-endian float64 rows (x_1 .. x_D, label)."""
+    A = np.concatenate([np.asarray(X, dtype="<f8"), np.asarray(labels, dtype="<f8")[:, None]], axis=1)
+    A.tofile(path)
 
 
 def mixture(N: int, D: int, K: int, s: float, r: float, seed: int = 20261015):

@@ -60,3 +60,30 @@ def test_results_files_in_reference_format(tmp_path):
         "# name: sigma\n# type: matrix\n# ndims: 3\n 2 2 2\n 0.1 0 \n0 0.2\n 0.3 0.01 \n0.01 0.4\n")
     assert open(os.path.join(d, "results.score.txt")).read() == (
         "Purity: 1\nRand Index: 1\nAdjusted Rand Index: 1\n")
+
+
+def test_f64_data_roundtrip(tmp_path):
+    from noparama_amd import datasets
+
+    X, z = datasets.twogaussians()
+    p = str(tmp_path / "tg.f64")
+    datasets.write_data_f64(p, X, z)
+    X2, z2 = datasets.read_data(p, D=2)
+    assert (X2 == X).all() and (z2 == z).all()
+
+
+@pytest.mark.gpu
+def test_binary_data_and_subsample(tmp_path):
+    """np_main.cpp:283-295: a random subset of -n items (the reference's default is 200 of the file)."""
+    from noparama_amd import datasets
+
+    X, z = datasets.twogaussians()
+    data = str(tmp_path / "tg.f64")
+    datasets.write_data_f64(data, X, z)
+    ws = str(tmp_path / "ws") + "/"
+    r = run(["-d", data, "-a", "algorithm8", "-T", "200", "-s", "3", "-n", "120", "-w", ws])
+    assert r.returncode == 0, r.stderr + r.stdout
+    run_dir = os.path.join(ws, "LATEST")
+    K = int(open(os.path.join(run_dir, "snapshot.txt")).read().split("# rows: ")[1].split()[0])
+    n = sum(len(open(os.path.join(run_dir, f"snapshot{k}.txt")).read().splitlines()) for k in range(K))
+    assert n == 120
