@@ -1032,12 +1032,15 @@ int np8_init_random(np8_ctx *c, int32_t K_init) {
     if (!c) return NP8_ERR_ARG;
     if (!c->have_data) return fail(c, NP8_ERR_STATE, "np8_init_random: no data");
     if (K_init < 1 || K_init > c->kcap) return fail(c, NP8_ERR_ARG, "np8_init_random: K_init outside [1,kcap]");
-    const int D = c->D, P = (D + 2) / 2;
+    const int D = c->D, Q = g0_calls(D);
     std::vector<SlotHost> draws(K_init);
     for (int k = 0; k < K_init; ++k) {  // InitClusters::init: K G0 draws (np_init_clusters.cpp:24-40)
-        std::vector<double> g(2 * P);
-        for (int q = 0; q < P; ++q)
-            normal_pair(c->seed, (uint64_t)k, 0xFFFFFFFFu, kStreamInitTheta, (uint32_t)q, g[2 * q], g[2 * q + 1]);
+        std::vector<double> g(4 * Q);
+        for (int q = 0; q < Q; ++q) {
+            double gq[4];
+            normal_quad(c->seed, (uint64_t)k, 0xFFFFFFFFu, kStreamInitTheta, (uint32_t)q, gq);
+            for (int h = 0; h < 4; ++h) g[4 * q + h] = gq[h];
+        }
         slot_from_normals(c, g[0], g.data() + 1, draws[k]);
     }
     // uniform assignment of every item (np_mcmc.cpp:69-85); counts over ALL items, so every rank

@@ -63,11 +63,23 @@ NP8_HD void philox_call(uint64_t seed, uint64_t i, uint32_t t, uint32_t stream, 
                   (uint32_t)(seed >> 32), out);
 }
 
-// Odd 53-bit integer times 2^-53: uniform on (0,1), never 0 or 1.
+// Odd 53-bit integer times 2^-53: uniform on (0,1), never 0 or 1 (the draws' uniforms).
 NP8_HD double u01(uint32_t hi, uint32_t lo) {
     uint64_t v = ((((uint64_t)hi) << 32) | lo) >> 11;
     v |= 1u;
     return (double)v * 0x1.0p-53;
+}
+
+// (k + 1/2) 2^-32: a 32-bit uniform on (0,1), exact in fp64 (the Box-Muller inputs).
+NP8_HD double u32_01(uint32_t k) { return fma((double)k, 0x1.0p-32, 0x1.0p-33); }
+
+// 1/y for y in [2 - (1 - 1/sqrt2), 2 + (sqrt2 - 1)] (the log's s = f/(2+f)): minimax quadratic
+// (relative error 1.3e-3) and three Newton steps, fma only -- no IEEE division sequence.
+NP8_HD double recip_logden(double y) {
+    double r = fma(fma(0.11686276, y, -0.72244362), y, 1.47775548);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) r = fma(r, fma(-y, r, 1.0), r);
+    return r;
 }
 
 // ---- elementary functions with identical bits on host and device (DESIGN.md "Math") ------------
@@ -104,7 +116,7 @@ NP8_HD double log_pos(double u) {
     m = lo ? m + m : m;
     e = lo ? e - 1 : e;
     const double f = m - 1.0;
-    const double s = f / (2.0 + f);
+    const double s = f * recip_logden(2.0 + f);
     const double s2 = s * s;
     double p = 0.09523809523809523;
     p = fma(p, s2, 0.10526315789473684);
@@ -154,19 +166,24 @@ NP8_HD void sincos_2pi(double t, double &sn, double &cs) {
     cs = ((qi + 1) & 2) ? -b : b;
 }
 
-// Box-Muller pair from one Philox call: (r cos 2 pi u2, r sin 2 pi u2), r = sqrt(-2 log u1).
-NP8_HD void normal_pair(uint64_t seed, uint64_t i, uint32_t t, uint32_t stream, uint32_t call, double &g0,
-                        double &g1) {
+// Four normals from one Philox call: two Box-Muller pairs over 32-bit uniforms,
+// (r cos 2 pi u2, r sin 2 pi u2), r = sqrt(-2 log u1), (u1, u2) = words (0, 1) and (2, 3).
+// A draw of n normals uses calls base .. base + ceil(n/4) - 1; normal k is g[k & 3] of call k >> 2.
+NP8_HD void normal_quad(uint64_t seed, uint64_t i, uint32_t t, uint32_t stream, uint32_t call, double (&g)[4]) {
     uint32_t o[4];
     philox_call(seed, i, t, stream, call, o);
-    const double u1 = u01(o[0], o[1]);
-    const double u2 = u01(o[2], o[3]);
-    const double r = sqrt(-2.0 * log_pos(u1));
-    double sn, cs;
-    sincos_2pi(u2, sn, cs);
-    g0 = r * cs;
-    g1 = r * sn;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const double r = sqrt(-2.0 * log_pos(u32_01(o[2 * h])));
+        double sn, cs;
+        sincos_2pi(u32_01(o[2 * h + 1]), sn, cs);
+        g[2 * h] = r * cs;
+        g[2 * h + 1] = r * sn;
+    }
 }
+
+// Philox calls per G0 draw (D+1 normals: the scale normal, then xi).
+NP8_HD int g0_calls(int D) { return (D + 4) / 4; }
 
 // Log-weight standing for weight 0 (a singleton's own cluster): finite, so no -inf arithmetic.
 constexpr double kZeroLogWeight = -1.0e300;

@@ -81,20 +81,20 @@ __device__ __forceinline__ void whiten(const double *__restrict__ hyp, const dou
 }
 
 // Log-likelihood of x under auxiliary G0 draw m of (item ig, epoch t).  The draw uses Philox calls
-// m*P .. m*P+P-1 (P = ceil((D+1)/2)); normal 0 scales, normals 1..D are xi:
+// m*Q .. m*Q+Q-1 (Q = ceil((D+1)/4), normal_quad); normal 0 scales, normals 1..D are xi:
 // v = D + nu g, s = |v|/sqrt(kappa), q = |y0 - s xi|^2 / v^2, ll = caux - D log|v| - q/2
 // (normalinvwishart.h:44-64, invwishart.h:34-46, multivariatenormal.cpp:124-135; DESIGN.md "G0").
 template <int D>
 __device__ __forceinline__ double aux_ll(const double *__restrict__ hyp, const double (&y0)[D], uint64_t seed,
                                          uint64_t ig, uint32_t t, int m) {
     using H = HypView<D>;
-    constexpr int P = (D + 2) / 2;
+    constexpr int Q = (D + 4) / 4;  // g0_calls(D)
     const double caux = hyp[H::kCaux], rsk = hyp[H::kRsk], nu = hyp[H::kNu];
-    double g0 = 0.0, g1 = 0.0, v = 0.0, s = 0.0, r2 = 0.0;
+    double gq[4] = {0.0, 0.0, 0.0, 0.0}, v = 0.0, s = 0.0, r2 = 0.0;
 #pragma unroll
     for (int k = 0; k <= D; ++k) {
-        if ((k & 1) == 0) normal_pair(seed, ig, t, kStreamAux, (uint32_t)(m * P + (k >> 1)), g0, g1);
-        const double g = (k & 1) ? g1 : g0;
+        if ((k & 3) == 0) normal_quad(seed, ig, t, kStreamAux, (uint32_t)(m * Q + (k >> 2)), gq);
+        const double g = gq[k & 3];
         if (k == 0) {
             v = fma(nu, g, (double)D);
             s = fabs(v) * rsk;
@@ -115,7 +115,7 @@ __device__ __forceinline__ int64_t position_to_local(const AssignArgs &A, int64_
 }
 
 template <int D, int M>
-__global__ __launch_bounds__(256) void np8_assign(AssignArgs A) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void np8_assign(AssignArgs A) {
     constexpr int DP = D * (D + 1) / 2;
     constexpr int CS = (D + DP + 5 + 1) & ~1;
     constexpr int F = D + DP;
@@ -408,12 +408,12 @@ __device__ const Request *request_at(const FinArgs &F, const int *base, int q) {
 // Auxiliary draw m of (item i, epoch t) -> a slot: the G0 draw of normalinvwishart.h:44-64 in the
 // factored form (DESIGN.md "G0").
 __device__ void write_new_slot(const FinArgs &F, const Request &r, int s, uint32_t t) {
-    const int D = F.D, DP = D * (D + 1) / 2, P = (D + 2) / 2;
-    double g0 = 0.0, g1 = 0.0, v = 0.0;
+    const int D = F.D, DP = D * (D + 1) / 2, Q = g0_calls(D);
+    double gq[4] = {0.0, 0.0, 0.0, 0.0}, v = 0.0;
     double xi[kMaxD];  // only D used
     for (int k = 0; k <= D; ++k) {
-        if ((k & 1) == 0) normal_pair(F.seed, (uint64_t)r.i, t, kStreamAux, (uint32_t)(r.m * P + (k >> 1)), g0, g1);
-        const double g = (k & 1) ? g1 : g0;
+        if ((k & 3) == 0) normal_quad(F.seed, (uint64_t)r.i, t, kStreamAux, (uint32_t)(r.m * Q + (k >> 2)), gq);
+        const double g = gq[k & 3];
         if (k == 0)
             v = fma(F.nu, g, (double)D);
         else
@@ -735,12 +735,12 @@ __global__ __launch_bounds__(64) void np8_suffstats(ParamArgs A) {
 template <int D>
 __device__ __forceinline__ void mh_proposal(const ParamArgs &A, uint32_t t, int s, int step, double &v,
                                             double (&mup)[D]) {
-    constexpr int P = (D + 2) / 2;
-    double g0 = 0.0, g1 = 0.0, xi[D];
+    constexpr int Q = (D + 4) / 4;  // g0_calls(D)
+    double gq[4] = {0.0, 0.0, 0.0, 0.0}, xi[D];
 #pragma unroll
     for (int k = 0; k <= D; ++k) {
-        if ((k & 1) == 0) normal_pair(A.seed, (uint64_t)s, t, kStreamParam, (uint32_t)(step * P + (k >> 1)), g0, g1);
-        const double g = (k & 1) ? g1 : g0;
+        if ((k & 3) == 0) normal_quad(A.seed, (uint64_t)s, t, kStreamParam, (uint32_t)(step * Q + (k >> 2)), gq);
+        const double g = gq[k & 3];
         if (k == 0)
             v = fma(A.nu, g, (double)D);
         else

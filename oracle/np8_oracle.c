@@ -47,6 +47,16 @@ double np8o_u01(uint32_t hi, uint32_t lo) {
     return (double)v * 0x1.0p-53;
 }
 
+/* (k + 1/2) 2^-32: 32-bit uniform on (0,1), exact (the Box-Muller inputs). */
+static inline double u32_01(uint32_t k) { return fma((double)k, 0x1.0p-32, 0x1.0p-33); }
+
+/* 1/y on the log's denominator range: minimax quadratic + three Newton steps (fma only). */
+static inline double recip_logden(double y) {
+    double r = fma(fma(0.11686276, y, -0.72244362), y, 1.47775548);
+    for (int k = 0; k < 3; ++k) r = fma(r, fma(-y, r, 1.0), r);
+    return r;
+}
+
 static void philox_call(uint64_t seed, uint64_t i, uint32_t t, uint32_t stream, uint32_t call, uint32_t out[4]) {
     uint32_t ctr[4] = {(uint32_t)i, (uint32_t)(i >> 32), t, (stream << 24) | (call & 0xFFFFFFu)};
     uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
@@ -80,7 +90,7 @@ double np8o_log_pos(double u) {
     m = lo ? m + m : m;
     e = lo ? e - 1 : e;
     const double f = m - 1.0;
-    const double s = f / (2.0 + f);
+    const double s = f * recip_logden(2.0 + f);
     const double s2 = s * s;
     static const double A[10] = {0.09523809523809523, 0.10526315789473684, 0.11764705882352941, 0.13333333333333333,
                                  0.15384615384615385, 0.18181818181818182, 0.2222222222222222,  0.2857142857142857,
@@ -117,23 +127,28 @@ void np8o_sincos_2pi(double t, double *sn, double *cs) {
     *cs = ((qi + 1) & 2) ? -b : b;
 }
 
-/* Box-Muller pair from one Philox call: (r cos 2 pi u2, r sin 2 pi u2), r = sqrt(-2 log u1). */
-static void normal_pair(uint64_t seed, uint64_t i, uint32_t t, uint32_t stream, uint32_t call, double g[2]) {
+/* Four normals from one Philox call: two Box-Muller pairs over 32-bit uniforms (words 0,1 and 2,3),
+ * (r cos 2 pi u2, r sin 2 pi u2), r = sqrt(-2 log u1).  A draw of n normals uses calls
+ * base .. base + ceil(n/4) - 1; normal k is g[k & 3] of call k >> 2. */
+static void normal_quad(uint64_t seed, uint64_t i, uint32_t t, uint32_t stream, uint32_t call, double g[4]) {
     uint32_t o[4];
     philox_call(seed, i, t, stream, call, o);
-    double u1 = np8o_u01(o[0], o[1]);
-    double u2 = np8o_u01(o[2], o[3]);
-    double r = sqrt(-2.0 * np8o_log_pos(u1));
-    double sn, cs;
-    np8o_sincos_2pi(u2, &sn, &cs);
-    g[0] = r * cs;
-    g[1] = r * sn;
+    for (int h = 0; h < 2; ++h) {
+        const double r = sqrt(-2.0 * np8o_log_pos(u32_01(o[2 * h])));
+        double sn, cs;
+        np8o_sincos_2pi(u32_01(o[2 * h + 1]), &sn, &cs);
+        g[2 * h] = r * cs;
+        g[2 * h + 1] = r * sn;
+    }
 }
 
+/* Philox calls per G0 draw (D+1 normals). */
+static inline int g0_calls(int D) { return (D + 4) / 4; }
+
 double np8o_normal(uint64_t seed, uint64_t i, uint32_t t, uint32_t stream, uint32_t n) {
-    double g[2];
-    normal_pair(seed, i, t, stream, n >> 1, g);
-    return g[n & 1];
+    double g[4];
+    normal_quad(seed, i, t, stream, n >> 2, g);
+    return g[n & 3];
 }
 
 double np8o_uniform(uint64_t seed, uint64_t i, uint32_t t, uint32_t stream, uint32_t n) {
@@ -547,16 +562,16 @@ static void slot_from_aux(np8o_ctx *c, int s, double v, const double *mu) {
     for (int k = 0; k < D * D; ++k) S[k] = v2 * c->LTL[k];
 }
 
-/* Normals of auxiliary draw m of (item i, epoch t): Philox calls m*P .. m*P+P-1 of stream AUX,
- * P = ceil((D+1)/2); g[0] scales, g[1..D] is xi. */
-static void aux_normals(const np8o_ctx *c, uint64_t i, uint32_t t, int m, double *g /* >= D+2 */) {
-    const int D = c->D, P = (D + 2) / 2;
-    for (int k = 0; k < P; ++k) normal_pair(c->cfg.seed, i, t, NP8O_STREAM_AUX, (uint32_t)(m * P + k), g + 2 * k);
+/* Normals of auxiliary draw m of (item i, epoch t): Philox calls m*Q .. m*Q+Q-1 of stream AUX,
+ * Q = ceil((D+1)/4); g[0] scales, g[1..D] is xi. */
+static void aux_normals(const np8o_ctx *c, uint64_t i, uint32_t t, int m, double *g /* >= D+4 */) {
+    const int Q = g0_calls(c->D);
+    for (int k = 0; k < Q; ++k) normal_quad(c->cfg.seed, i, t, NP8O_STREAM_AUX, (uint32_t)(m * Q + k), g + 4 * k);
 }
 
 static void aux_draws(const np8o_ctx *c, uint64_t i, uint32_t t, double *v, double *mu /* M*D */) {
     for (int m = 0; m < c->M; ++m) {
-        double g[NP8O_DMAX + 2];
+        double g[NP8O_DMAX + 4];
         aux_normals(c, i, t, m, g);
         aux_from_normals(c, g[0], g + 1, v + m, mu + m * c->D);
     }
@@ -614,9 +629,9 @@ int np8o_init_random(np8o_ctx *c, int32_t K_init) {
     double *vv = (double *)malloc(sizeof(double) * (size_t)K_init);
     int32_t *cntk = (int32_t *)calloc((size_t)K_init, sizeof(int32_t));
     for (int k = 0; k < K_init; ++k) {
-        double g[NP8O_DMAX + 2];
-        for (int call = 0; call < (D + 2) / 2; ++call)
-            normal_pair(c->cfg.seed, (uint64_t)k, 0xFFFFFFFFu, NP8O_STREAM_INIT_THETA, (uint32_t)call, g + 2 * call);
+        double g[NP8O_DMAX + 4];
+        for (int call = 0; call < g0_calls(D); ++call)
+            normal_quad(c->cfg.seed, (uint64_t)k, 0xFFFFFFFFu, NP8O_STREAM_INIT_THETA, (uint32_t)call, g + 4 * call);
         aux_from_normals(c, g[0], g + 1, vv + k, mu + (size_t)k * D);
     }
     for (int64_t i = 0; i < c->N; ++i) {
@@ -700,7 +715,7 @@ static void aux_ll(const np8o_ctx *c, const double *x, uint64_t i, uint32_t t, d
         y0[a] = t0;
     }
     for (int m = 0; m < M; ++m) {
-        double g[NP8O_DMAX + 2];
+        double g[NP8O_DMAX + 4];
         aux_normals(c, i, t, m, g);
         const double *xi = g + 1;
         double v = fma(c->cfg.nu, g[0], (double)D);
@@ -877,7 +892,7 @@ double np8o_total_loglik(np8o_ctx *c) {
  *   current:  LL = n c - tr(P' S)/2                                (P' = packed, off-diagonals doubled)
  *   proposal: LL' = n c' - (tr(G S) - 2 e^T G s1 + n e^T G e) / (2 v'^2),  e = mu' - a,
  *             G = (L^T L)^{-1}, c' = caux - D log|v'|               (Sigma' = v'^2 L^T L)
- * Randomness: proposal normals = Philox stream PARAM (i = slot, calls step*P .. step*P+P-1, laid out
+ * Randomness: proposal normals = Philox stream PARAM (i = slot, calls step*Q .. step*Q+Q-1, laid out
  * like an auxiliary draw), acceptance uniform = stream PARAM_U (i = slot, call = step). */
 int np8o_suffstats(np8o_ctx *c, double *out) {
     const int D = c->D, W = D + c->DP;
@@ -915,10 +930,10 @@ static double mh_proposal_ll(const np8o_ctx *c, int64_t n, double trGS, const do
 }
 
 static void mh_proposal(const np8o_ctx *c, int s, uint32_t t, int step, double *v, double *mup) {
-    const int D = c->D, P = (D + 2) / 2;
-    double g[NP8O_DMAX + 2];
-    for (int k = 0; k < P; ++k)
-        normal_pair(c->cfg.seed, (uint64_t)s, t, NP8O_STREAM_PARAM, (uint32_t)(step * P + k), g + 2 * k);
+    const int Q = g0_calls(c->D);
+    double g[NP8O_DMAX + 4];
+    for (int k = 0; k < Q; ++k)
+        normal_quad(c->cfg.seed, (uint64_t)s, t, NP8O_STREAM_PARAM, (uint32_t)(step * Q + k), g + 4 * k);
     aux_from_normals(c, g[0], g + 1, v, mup);
 }
 

@@ -43,7 +43,7 @@ enum {
     NP8O_STREAM_PICK = 2,
     NP8O_STREAM_INIT_THETA = 3,
     NP8O_STREAM_INIT_Z = 4,
-    NP8O_STREAM_PARAM = 5,  /* MH proposal normals: i = slot, calls step*P .. */
+    NP8O_STREAM_PARAM = 5,  /* MH proposal normals: i = slot, calls step*Q .. */
     NP8O_STREAM_PARAM_U = 6 /* MH acceptance uniform: i = slot, call = step */
 };
 

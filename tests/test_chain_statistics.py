@@ -3,8 +3,9 @@ be compared in distribution).  On twogaussians (scripts/generate.m) with the ref
 (alpha 1, M 3, K_init 20, mu0 (6,6), kappa 1/500, nu 4, Lambda 0.01 I), the data-parallel sweep
 (chunk = N, what the GPU runs by default) must score like the reference's sequential sweep (chunk = 1)
 on the max-likelihood labelling that results.score.txt reports (np_main.cpp:492-497).  Tolerances
-(DESIGN.md): |d mean purity| <= 0.02, |d mean ARI| <= 0.05 over 20 seeds.  CPU only (the GPU runs
-the same chunked algorithm bit-exactly, tests/test_gpu_parity.py)."""
+(DESIGN.md): over 40 seeds each, |d mean purity| <= 0.02 and the mean purity and ARI of the two
+samplers within 3 standard errors of each other (Welch).  CPU only (the GPU runs the same chunked
+algorithm bit-exactly, tests/test_gpu_parity.py)."""
 import os
 
 import numpy as np
@@ -15,7 +16,7 @@ from noparama_amd import datasets
 
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 T = 300
-SEEDS = 20
+SEEDS = 40
 
 
 def run(seed, chunk):
@@ -35,7 +36,10 @@ def test_sync_sweep_scores_like_sequential_sweep():
     par = np.array([run(1000 + s, 0) for s in range(SEEDS)])
     assert seq[:, 0].mean() > 0.95  # README.rst:53-55: purity "should be almost 1"
     assert abs(seq[:, 0].mean() - par[:, 0].mean()) <= 0.02, (seq[:, 0].mean(), par[:, 0].mean())
-    assert abs(np.nanmean(seq[:, 1]) - np.nanmean(par[:, 1])) <= 0.05, (np.nanmean(seq[:, 1]), np.nanmean(par[:, 1]))
+    for col in (0, 1):  # purity, ARI: Welch t statistic of the difference of means
+        a, b = seq[:, col][~np.isnan(seq[:, col])], par[:, col][~np.isnan(par[:, col])]
+        se = np.sqrt(a.var(ddof=1) / a.size + b.var(ddof=1) / b.size)
+        assert abs(a.mean() - b.mean()) <= 3.0 * se + 1e-12, (col, a.mean(), b.mean(), se)
 
 
 def test_sequential_chain_is_a_valid_partition():

@@ -170,9 +170,10 @@ def test_errors_are_reported():
 
 
 def test_capacity_rejection_matches_oracle():
-    """More new-cluster requests than free slots: the whole step's requests are rejected."""
+    """More new-cluster requests than free slots: the whole step's requests are rejected (a huge
+    alpha makes most items ask for a new cluster)."""
     X, _ = datasets.twogaussians(5)
-    g, o = pair(2, 17, kcap=24)
+    g, o = pair(2, 17, kcap=24, alpha=1e6)
     for s in (g, o):
         s.set_data(X)
         s.init_random(20)

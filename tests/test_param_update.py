@@ -20,8 +20,8 @@ def _logpdf_sum(X, mu, S):
 
 
 def _proposal(seed, slot, t, step, D, mu0, kappa, nu, Lam):
-    P = (D + 2) // 2
-    g = [O.normal(seed, slot, t, STREAM_PARAM, 2 * step * P + k) for k in range(D + 1)]
+    Q = (D + 4) // 4  # Philox calls per G0 draw (normal_quad)
+    g = [O.normal(seed, slot, t, STREAM_PARAM, 4 * step * Q + k) for k in range(D + 1)]
     v = D + nu * g[0]
     L = np.linalg.cholesky(Lam)
     mu = mu0 + abs(v) / np.sqrt(kappa) * (L.T @ np.array(g[1:]))
@@ -53,10 +53,10 @@ def test_suffstats_about_slot_means():
     assert np.all(st[4:] == 0)
 
 
-@pytest.mark.parametrize("D", [2, 3])
-def test_mh_g0_matches_direct_restatement(D):
-    seed, steps = 11, 300
-    X, z, mu, sig = _problem(seed=D, D=D)
+@pytest.mark.parametrize("D,steps,n", [(2, 300, 60), (3, 3000, 5)])
+def test_mh_g0_matches_direct_restatement(D, steps, n):
+    seed = 12
+    X, z, mu, sig = _problem(seed=D, D=D, n=n)
     mu0, kappa, nu, Lam = np.full(D, 6.0), 1.0 / 500, 4.0, 0.01 * np.eye(D)
     c = O.Chain(D, seed=seed, kcap=8, param_update="mh_g0", mh_steps=steps)
     c.set_data(X)

@@ -41,9 +41,10 @@ def _violations(chain, X, D):
     return pruned, bad
 
 
-@pytest.mark.parametrize("D,K,N,init", [(3, 10, 3000, True), (8, 24, 6000, False), (2, 12, 4000, False)])
-def test_pruned_rows_are_always_skipped(D, K, N, init):
-    X, z, mu, sig = datasets.mixture(N, D, K, 0.5, 8.0, seed=D)
+@pytest.mark.parametrize("D,K,N,s,r,init", [(3, 10, 3000, 0.5, 8.0, True), (8, 24, 6000, 0.5, 8.0, False),
+                                            (2, 12, 4000, 0.3, 15.0, False)])
+def test_pruned_rows_are_always_skipped(D, K, N, s, r, init):
+    X, z, mu, sig = datasets.mixture(N, D, K, s, r, seed=D)
     c = O.Chain(D, seed=5 + D, kcap=4096)
     c.set_data(X)
     if init:
