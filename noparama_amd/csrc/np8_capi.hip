@@ -866,7 +866,7 @@ int np8_create(np8_ctx **out, const np8_config *cfg) {
     c->graphs_off = std::getenv("NP8_NO_GRAPH") != nullptr;  // A/B switch for launch-by-launch sweeps
     c->prune_on = c->kcap <= kPruneMaxKcap && std::getenv("NP8_NO_PRUNE") == nullptr;
     c->rec_cap = kReqMax;
-    c->rec_bytes = record_bytes(c->kcap, c->rec_cap);
+    c->rec_bytes = record_bytes(c->kcap, c->rec_cap, c->D);
     int r = 0;
     const int D = c->D, DP = c->DP, kc = c->kcap;
     if ((r = dalloc(c, &c->slot_mu, (size_t)kc * D)) || (r = dalloc(c, &c->slot_P, (size_t)kc * DP)) ||
@@ -883,7 +883,7 @@ int np8_create(np8_ctx **out, const np8_config *cfg) {
         delete c;
         return r;
     }
-    // hyp: mu0 | UinvT packed | caux | rsk | logam | nu
+    // hyp: mu0 | UinvT packed | caux | rsk | logam | nu | LT packed
     std::vector<double> hyp;
     hyp.insert(hyp.end(), c->mu0.begin(), c->mu0.end());
     for (int a = 0; a < D; ++a)
@@ -892,6 +892,8 @@ int np8_create(np8_ctx **out, const np8_config *cfg) {
     hyp.push_back(c->rsk);
     hyp.push_back(c->logam);
     hyp.push_back(c->nu);
+    for (int a = 0; a < D; ++a)
+        for (int b = a; b < D; ++b) hyp.push_back(c->LT[a * D + b]);
     std::vector<double> gp;
     for (int a = 0; a < D; ++a)
         for (int b = a; b < D; ++b) gp.push_back(c->Gp[a * D + b]);
@@ -1268,7 +1270,7 @@ int np8_comm_unique_id(uint8_t out[128]) {
 static int resize_records(np8_ctx *c, int world) {
     c->world = world;
     c->rec_cap = world > 1 ? (kReqMax / world > 64 ? kReqMax / world : 64) : kReqMax;
-    c->rec_bytes = record_bytes(c->kcap, c->rec_cap);
+    c->rec_bytes = record_bytes(c->kcap, c->rec_cap, c->D);
     int r = dalloc(c, &c->rec, (size_t)c->rec_bytes);
     if (r) return r;
     if (world > 1) {

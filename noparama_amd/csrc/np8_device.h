@@ -22,7 +22,8 @@ enum Stream : uint32_t {
     kStreamInitTheta = 3,
     kStreamInitZ = 4,
     kStreamParam = 5,  // MH proposal normals (i = slot)
-    kStreamParamU = 6  // MH acceptance uniforms (i = slot)
+    kStreamParamU = 6,  // MH acceptance uniforms (i = slot)
+    kStreamAuxDir = 7   // direction of a picked auxiliary's xi orthogonal to the item (i = item)
 };
 
 // Candidate-table entry layout (doubles):
@@ -182,8 +183,78 @@ NP8_HD void normal_quad(uint64_t seed, uint64_t i, uint32_t t, uint32_t stream, 
     }
 }
 
-// Philox calls per G0 draw (D+1 normals: the scale normal, then xi).
+// Philox calls per full G0 draw (D+1 normals: the scale normal, then xi) -- init and MH proposals.
 NP8_HD int g0_calls(int D) { return (D + 4) / 4; }
+
+// ---- auxiliary draws in the item's frame (DESIGN.md "G0") -------------------------------------------
+// Auxiliary m of item i is theta = (v, mu0 + (|v|/sqrt kappa) L^T xi), xi ~ N(0, I_D).  With the item
+// whitened, y0 = (L^T)^{-1}(x - mu0), the likelihood depends on xi only through xi_par = xi . y0/|y0|
+// ~ N(0,1) and chi2 = |xi_perp|^2 ~ chi^2_{D-1}:  |y0 - s xi|^2 = (|y0| - s xi_par)^2 + s^2 chi2.  So
+// the draw is (v, xi_par, chi2): call m*aux_calls(D) gives normals (v-normal, xi_par, g_odd, -);
+// chi^2_{2k}, k = (D-1)/2, is -2 log of the product of k 32-bit uniforms (calls m*aux_calls(D)+1 ..,
+// products of at most 16 per log), plus g_odd^2 when D-1 is odd.  Only a picked auxiliary needs xi
+// itself: xi = xi_par yhat + sqrt(chi2) w_perp/|w_perp| with w ~ N(0, I_D) on stream AUX_DIR
+// (exactly N(0, I) in distribution: independent radial, parallel and direction parts).
+NP8_HD int aux_calls(int D) { return 1 + ((D - 1) / 2 + 3) / 4; }
+NP8_HD int dir_calls(int D) { return (D + 3) / 4; }
+
+NP8_HD void aux_core(uint64_t seed, uint64_t i, uint32_t t, int m, int D, double nu, double &v, double &xpar,
+                     double &chi2) {
+    const int Qa = aux_calls(D), k = (D - 1) / 2;
+    double g[4];
+    normal_quad(seed, i, t, kStreamAux, (uint32_t)(m * Qa), g);
+    v = fma(nu, g[0], (double)D);
+    xpar = g[1];
+    double c2 = 0.0, prod = 1.0;
+    uint32_t w[4] = {0u, 0u, 0u, 0u};
+    int in_chunk = 0;
+    for (int j = 0; j < k; ++j) {
+        if ((j & 3) == 0) philox_call(seed, i, t, kStreamAux, (uint32_t)(m * Qa + 1 + (j >> 2)), w);
+        prod *= u32_01(w[j & 3]);
+        if (++in_chunk == 16 || j == k - 1) {
+            c2 = fma(-2.0, log_pos(prod), c2);
+            prod = 1.0;
+            in_chunk = 0;
+        }
+    }
+    if ((D - 1) & 1) c2 = fma(g[2], g[2], c2);
+    chi2 = c2;
+}
+
+// Log-likelihood of the item under auxiliary (v, xi_par, chi2); ny = |y0|.
+NP8_HD double aux_loglik(double ny, double v, double xpar, double chi2, int D, double rsk, double caux) {
+    const double s = fabs(v) * rsk;
+    const double d = fma(-s, xpar, ny);
+    const double r2 = fma(d, d, (s * s) * chi2);
+    const double q = r2 / (v * v);
+    const double cm = fma(-(double)D, log_pos(fabs(v)), caux);
+    return fma(-0.5, q, cm);
+}
+
+// xi of a picked auxiliary (see above); y0 and ny of the item.  DM bounds D at compile time (the
+// kernels instantiate it with their D, host code and np8_finalize with kMaxD).
+template <int DM>
+NP8_HD void aux_xi(uint64_t seed, uint64_t i, uint32_t t, int m, int D, const double *y0, double ny, double xpar,
+                   double chi2, double *xi /* D */) {
+    double yh[DM], w[DM];
+    for (int a = 0; a < D; ++a) yh[a] = (ny > 0.0) ? y0[a] / ny : (a == 0 ? 1.0 : 0.0);
+    const int Qd = dir_calls(D);
+    double g[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int a = 0; a < D; ++a) {
+        if ((a & 3) == 0) normal_quad(seed, i, t, kStreamAuxDir, (uint32_t)(m * Qd + (a >> 2)), g);
+        w[a] = g[a & 3];
+    }
+    double dot = 0.0;
+    for (int a = 0; a < D; ++a) dot = fma(w[a], yh[a], dot);
+    double n2 = 0.0;
+    for (int a = 0; a < D; ++a) {
+        w[a] = fma(-dot, yh[a], w[a]);
+        n2 = fma(w[a], w[a], n2);
+    }
+    const double np = sqrt(n2);
+    const double sc = (np > 0.0) ? sqrt(chi2) / np : 0.0;
+    for (int a = 0; a < D; ++a) xi[a] = fma(xpar, yh[a], sc * w[a]);
+}
 
 // Log-weight standing for weight 0 (a singleton's own cluster): finite, so no -inf arithmetic.
 constexpr double kZeroLogWeight = -1.0e300;

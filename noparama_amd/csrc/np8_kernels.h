@@ -32,7 +32,9 @@ struct Ctl {
 enum : int32_t { kErrCapacity = 1 };
 
 // Exchange record of one rank for one synchronous step:
-//   RecHeader | int32 delta[kcap] | Request req[rec_cap]
+//   RecHeader | int32 delta[kcap] | Request req[rec_cap] | double vmu[rec_cap][D+1]
+// vmu[q] = (v, mu) of the auxiliary request q asks to become a cluster (computed by the rank that
+// owns the item: mu needs the item's data, DESIGN.md "G0").
 struct RecHeader {
     int32_t nreq;
     int32_t pad[3];
@@ -48,8 +50,12 @@ struct Request {
     int32_t pad;
 };
 
-inline int64_t record_bytes(int kcap, int rec_cap) {
-    int64_t b = kRecHeaderBytes + 4ll * kcap + (int64_t)sizeof(Request) * rec_cap;
+NP8_HD int64_t record_vmu_offset(int kcap, int rec_cap) {
+    return (kRecHeaderBytes + 4ll * kcap + (int64_t)sizeof(Request) * rec_cap + 15) & ~15ll;
+}
+
+NP8_HD int64_t record_bytes(int kcap, int rec_cap, int D) {
+    int64_t b = record_vmu_offset(kcap, rec_cap) + 8ll * (D + 1) * rec_cap;
     return (b + 15) & ~15ll;
 }
 

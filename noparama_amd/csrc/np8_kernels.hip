@@ -22,7 +22,7 @@ namespace {
 
 template <int D>
 struct HypView {
-    // hyp layout: mu0[D] | UinvT packed[DP] | caux | rsk | logam | nu
+    // hyp layout: mu0[D] | UinvT packed[DP] | caux | rsk | logam | nu | LT packed[DP]
     static constexpr int DP = D * (D + 1) / 2;
     static constexpr int kMu0 = 0;
     static constexpr int kUinvT = D;
@@ -30,6 +30,7 @@ struct HypView {
     static constexpr int kRsk = kCaux + 1;
     static constexpr int kLogam = kCaux + 2;
     static constexpr int kNu = kCaux + 3;
+    static constexpr int kLT = kCaux + 4;
 };
 
 // ll = c - q/2 with q = d' P d.  Isotropic entries (iso > 0, a wave-uniform branch): q = iso * |d|^2;
@@ -80,32 +81,45 @@ __device__ __forceinline__ void whiten(const double *__restrict__ hyp, const dou
     }
 }
 
-// Log-likelihood of x under auxiliary G0 draw m of (item ig, epoch t).  The draw uses Philox calls
-// m*Q .. m*Q+Q-1 (Q = ceil((D+1)/4), normal_quad); normal 0 scales, normals 1..D are xi:
-// v = D + nu g, s = |v|/sqrt(kappa), q = |y0 - s xi|^2 / v^2, ll = caux - D log|v| - q/2
-// (normalinvwishart.h:44-64, invwishart.h:34-46, multivariatenormal.cpp:124-135; DESIGN.md "G0").
+// Log-likelihood of the item (whitened: ny = |y0|) under auxiliary G0 draw m of (item ig, epoch t),
+// in the item's frame: (v, xi_par, chi2) from aux_core (normalinvwishart.h:44-64, invwishart.h:34-46,
+// multivariatenormal.cpp:124-135; DESIGN.md "G0").
 template <int D>
-__device__ __forceinline__ double aux_ll(const double *__restrict__ hyp, const double (&y0)[D], uint64_t seed,
-                                         uint64_t ig, uint32_t t, int m) {
+__device__ __forceinline__ double aux_ll(const double *__restrict__ hyp, double ny, uint64_t seed, uint64_t ig,
+                                         uint32_t t, int m) {
     using H = HypView<D>;
-    constexpr int Q = (D + 4) / 4;  // g0_calls(D)
-    const double caux = hyp[H::kCaux], rsk = hyp[H::kRsk], nu = hyp[H::kNu];
-    double gq[4] = {0.0, 0.0, 0.0, 0.0}, v = 0.0, s = 0.0, r2 = 0.0;
+    double v, xpar, chi2;
+    aux_core(seed, ig, t, m, D, hyp[H::kNu], v, xpar, chi2);
+    return aux_loglik(ny, v, xpar, chi2, D, hyp[H::kRsk], hyp[H::kCaux]);
+}
+
+// (v, mu) of a picked auxiliary: mu = mu0 + (|v|/sqrt kappa) L^T xi with xi from aux_xi.
+template <int D>
+__device__ __forceinline__ void aux_params(const double *__restrict__ hyp, const double (&y0)[D], double ny,
+                                           uint64_t seed, uint64_t ig, uint32_t t, int m, double *vmu) {
+    using H = HypView<D>;
+    double v, xpar, chi2, xi[D];
+    aux_core(seed, ig, t, m, D, hyp[H::kNu], v, xpar, chi2);
+    aux_xi<D>(seed, ig, t, m, D, y0, ny, xpar, chi2, xi);
+    const double sc = fabs(v) * hyp[H::kRsk];
+    const double *LT = hyp + H::kLT;
+    vmu[0] = v;
+    int k = 0;
 #pragma unroll
-    for (int k = 0; k <= D; ++k) {
-        if ((k & 3) == 0) normal_quad(seed, ig, t, kStreamAux, (uint32_t)(m * Q + (k >> 2)), gq);
-        const double g = gq[k & 3];
-        if (k == 0) {
-            v = fma(nu, g, (double)D);
-            s = fabs(v) * rsk;
-        } else {
-            const double e = fma(-s, g, y0[k - 1]);
-            r2 = fma(e, e, r2);
-        }
+    for (int a = 0; a < D; ++a) {
+        double t0 = LT[k++] * xi[a];
+#pragma unroll
+        for (int b = a + 1; b < D; ++b) t0 = fma(LT[k++], xi[b], t0);
+        vmu[1 + a] = fma(sc, t0, hyp[H::kMu0 + a]);
     }
-    const double q = r2 / (v * v);
-    const double cm = fma(-(double)D, log_pos(fabs(v)), caux);
-    return fma(-0.5, q, cm);
+}
+
+template <int D>
+__device__ __forceinline__ double norm_of(const double (&y0)[D]) {
+    double n2 = 0.0;
+#pragma unroll
+    for (int a = 0; a < D; ++a) n2 = fma(y0[a], y0[a], n2);
+    return sqrt(n2);
 }
 
 __device__ __forceinline__ int64_t position_to_local(const AssignArgs &A, int64_t p) {
@@ -171,12 +185,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void n
             if (e[F + kFieldSlot] != zslot) pick_step(st, lw, j);
         }
     }
+    double y0[D];
+    whiten<D>(hyp, x, y0);
+    const double ny = norm_of<D>(y0);
     {
-        double y0[D];
-        whiten<D>(hyp, x, y0);
         const double logam = hyp[HypView<D>::kLogam];
 #pragma unroll 1
-        for (int m = 0; m < M; ++m) pick_step(st, aux_ll<D>(hyp, y0, A.seed, ig, t, m) + logam, K + m);
+        for (int m = 0; m < M; ++m) pick_step(st, aux_ll<D>(hyp, ny, A.seed, ig, t, m) + logam, K + m);
     }
 
     RecHeader *hdr = reinterpret_cast<RecHeader *>(A.rec);
@@ -229,6 +244,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void n
             r.lpos = sorted ? (int32_t)p : -1;
             r.pad = 0;
             req[q] = r;
+            double *vmu = reinterpret_cast<double *>(A.rec + record_vmu_offset(A.kcap, A.rec_cap)) + (int64_t)q * (D + 1);
+            aux_params<D>(hyp, y0, ny, A.seed, ig, t, st.pick - K, vmu);
         }
     }
 }
@@ -405,27 +422,20 @@ __device__ const Request *request_at(const FinArgs &F, const int *base, int q) {
     return rec_reqs(F, r) + (q - base[r]);
 }
 
+// ... and the (v, mu) its rank computed for it.
+__device__ const double *request_vmu(const FinArgs &F, const int *base, int q) {
+    int r = 0;
+    while (r + 1 < F.world && q >= base[r + 1]) ++r;
+    return reinterpret_cast<const double *>(F.recs + (int64_t)r * F.rec_bytes + record_vmu_offset(F.kcap, F.rec_cap)) +
+           (int64_t)(q - base[r]) * (F.D + 1);
+}
+
 // Auxiliary draw m of (item i, epoch t) -> a slot: the G0 draw of normalinvwishart.h:44-64 in the
 // factored form (DESIGN.md "G0").
-__device__ void write_new_slot(const FinArgs &F, const Request &r, int s, uint32_t t) {
-    const int D = F.D, DP = D * (D + 1) / 2, Q = g0_calls(D);
-    double gq[4] = {0.0, 0.0, 0.0, 0.0}, v = 0.0;
-    double xi[kMaxD];  // only D used
-    for (int k = 0; k <= D; ++k) {
-        if ((k & 3) == 0) normal_quad(F.seed, (uint64_t)r.i, t, kStreamAux, (uint32_t)(r.m * Q + (k >> 2)), gq);
-        const double g = gq[k & 3];
-        if (k == 0)
-            v = fma(F.nu, g, (double)D);
-        else
-            xi[k - 1] = g;
-    }
-    const double sc = fabs(v) * F.rsk;
-    for (int a = 0; a < D; ++a) {
-        const double *LTa = F.LT + a * D;
-        double t0 = LTa[a] * xi[a];
-        for (int b = a + 1; b < D; ++b) t0 = fma(LTa[b], xi[b], t0);
-        F.slot_mu[(int64_t)s * D + a] = fma(sc, t0, F.mu0[a]);
-    }
+__device__ void write_new_slot(const FinArgs &F, const double *vmu, int s) {
+    const int D = F.D, DP = D * (D + 1) / 2;
+    const double v = vmu[0];
+    for (int a = 0; a < D; ++a) F.slot_mu[(int64_t)s * D + a] = vmu[1 + a];
     const double v2 = v * v;
     for (int k = 0; k < DP; ++k) F.slot_P[(int64_t)s * DP + k] = F.Gp[k] / v2;
     F.slot_c[s] = fma(-(double)D, log_pos(fabs(v)), F.caux);
@@ -528,7 +538,7 @@ __global__ __launch_bounds__(kFinThreads) void np8_finalize(FinArgs F) {
         for (int q = tid; q < nreq; q += kFinThreads) {
             const Request r = *request_at(F, base, kidx[q]);
             const int s = freeslot[q];
-            write_new_slot(F, r, s, F.ctl->t_base + F.t);
+            write_new_slot(F, request_vmu(F, base, kidx[q]), s);
             cnt_s[s] = 1;
             if (r.i >= F.offset && r.i < F.offset + F.n_loc) {
                 F.z[r.i - F.offset] = s;
@@ -892,8 +902,9 @@ __global__ __launch_bounds__(256) void np8_loglik_matrix_kernel(AssignArgs A, co
     for (int j = 0; j < K; ++j) out[r * (K + M) + j] = cand_ll<D>(A.cand + (int64_t)j * CS, x);
     double y0[D];
     whiten<D>(A.hyp, x, y0);
+    const double ny = norm_of<D>(y0);
     const uint32_t t = A.ctl->t_base + A.t;
-    for (int m = 0; m < M; ++m) out[r * (K + M) + K + m] = aux_ll<D>(A.hyp, y0, A.seed, ig, t, m);
+    for (int m = 0; m < M; ++m) out[r * (K + M) + K + m] = aux_ll<D>(A.hyp, ny, A.seed, ig, t, m);
 }
 
 // ---- dispatch ----------------------------------------------------------------------------------------

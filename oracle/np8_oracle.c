@@ -562,18 +562,98 @@ static void slot_from_aux(np8o_ctx *c, int s, double v, const double *mu) {
     for (int k = 0; k < D * D; ++k) S[k] = v2 * c->LTL[k];
 }
 
-/* Normals of auxiliary draw m of (item i, epoch t): Philox calls m*Q .. m*Q+Q-1 of stream AUX,
- * Q = ceil((D+1)/4); g[0] scales, g[1..D] is xi. */
-static void aux_normals(const np8o_ctx *c, uint64_t i, uint32_t t, int m, double *g /* >= D+4 */) {
-    const int Q = g0_calls(c->D);
-    for (int k = 0; k < Q; ++k) normal_quad(c->cfg.seed, i, t, NP8O_STREAM_AUX, (uint32_t)(m * Q + k), g + 4 * k);
+/* ---- auxiliary draws in the item's frame (DESIGN.md "G0") ----------------------------------------
+ * Auxiliary m of item i is theta = (v, mu0 + (|v|/sqrt kappa) L^T xi), xi ~ N(0, I_D).  With
+ * y0 = (L^T)^{-1}(x - mu0) the likelihood needs only xi_par = xi . y0/|y0| ~ N(0,1) and
+ * chi2 = |xi_perp|^2 ~ chi^2_{D-1}: |y0 - s xi|^2 = (|y0| - s xi_par)^2 + s^2 chi2.  Call m*Qa of
+ * stream AUX gives the normals (v-normal, xi_par, g_odd, -); chi^2_{2k}, k = (D-1)/2, is -2 log of the
+ * product of k 32-bit uniforms (calls m*Qa+1 .., at most 16 per log), plus g_odd^2 for odd D-1.  A
+ * picked auxiliary's xi = xi_par yhat + sqrt(chi2) w_perp/|w_perp|, w ~ N(0,I) on stream AUX_DIR. */
+static inline int aux_calls(int D) { return 1 + ((D - 1) / 2 + 3) / 4; }
+static inline int dir_calls(int D) { return (D + 3) / 4; }
+
+static void aux_core(const np8o_ctx *c, uint64_t i, uint32_t t, int m, double *v, double *xpar, double *chi2) {
+    const int D = c->D, Qa = aux_calls(D), k = (D - 1) / 2;
+    double g[4];
+    normal_quad(c->cfg.seed, i, t, NP8O_STREAM_AUX, (uint32_t)(m * Qa), g);
+    *v = fma(c->cfg.nu, g[0], (double)D);
+    *xpar = g[1];
+    double c2 = 0.0, prod = 1.0;
+    uint32_t w[4] = {0u, 0u, 0u, 0u};
+    int in_chunk = 0;
+    for (int j = 0; j < k; ++j) {
+        if ((j & 3) == 0) philox_call(c->cfg.seed, i, t, NP8O_STREAM_AUX, (uint32_t)(m * Qa + 1 + (j >> 2)), w);
+        prod *= u32_01(w[j & 3]);
+        if (++in_chunk == 16 || j == k - 1) {
+            c2 = fma(-2.0, np8o_log_pos(prod), c2);
+            prod = 1.0;
+            in_chunk = 0;
+        }
+    }
+    if ((D - 1) & 1) c2 = fma(g[2], g[2], c2);
+    *chi2 = c2;
 }
 
+static double aux_loglik(const np8o_ctx *c, double ny, double v, double xpar, double chi2) {
+    const double s = fabs(v) * c->rsk;
+    const double d = fma(-s, xpar, ny);
+    const double r2 = fma(d, d, (s * s) * chi2);
+    const double q = r2 / (v * v);
+    const double cm = fma(-(double)c->D, np8o_log_pos(fabs(v)), c->caux);
+    return fma(-0.5, q, cm);
+}
+
+/* y0 = (L^T)^{-1}(x - mu0) and |y0|. */
+static double whiten(const np8o_ctx *c, const double *x, double *y0) {
+    const int D = c->D;
+    double dx[NP8O_DMAX];
+    for (int a = 0; a < D; ++a) dx[a] = x[a] - c->cfg.mu0[a];
+    for (int a = 0; a < D; ++a) {
+        double t0 = c->UinvT[a * D + a] * dx[a];
+        for (int b = a + 1; b < D; ++b) t0 = fma(c->UinvT[a * D + b], dx[b], t0);
+        y0[a] = t0;
+    }
+    double n2 = 0.0;
+    for (int a = 0; a < D; ++a) n2 = fma(y0[a], y0[a], n2);
+    return sqrt(n2);
+}
+
+static void aux_xi(const np8o_ctx *c, uint64_t i, uint32_t t, int m, const double *y0, double ny, double xpar,
+                   double chi2, double *xi) {
+    const int D = c->D, Qd = dir_calls(D);
+    double yh[NP8O_DMAX], w[NP8O_DMAX], g[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int a = 0; a < D; ++a) yh[a] = (ny > 0.0) ? y0[a] / ny : (a == 0 ? 1.0 : 0.0);
+    for (int a = 0; a < D; ++a) {
+        if ((a & 3) == 0) normal_quad(c->cfg.seed, i, t, NP8O_STREAM_AUX_DIR, (uint32_t)(m * Qd + (a >> 2)), g);
+        w[a] = g[a & 3];
+    }
+    double dot = 0.0;
+    for (int a = 0; a < D; ++a) dot = fma(w[a], yh[a], dot);
+    double n2 = 0.0;
+    for (int a = 0; a < D; ++a) {
+        w[a] = fma(-dot, yh[a], w[a]);
+        n2 = fma(w[a], w[a], n2);
+    }
+    const double np = sqrt(n2);
+    const double sc = (np > 0.0) ? sqrt(chi2) / np : 0.0;
+    for (int a = 0; a < D; ++a) xi[a] = fma(xpar, yh[a], sc * w[a]);
+}
+
+/* The M auxiliary draws of item i (local data row) at epoch t: v[m], mu[m*D..]. */
 static void aux_draws(const np8o_ctx *c, uint64_t i, uint32_t t, double *v, double *mu /* M*D */) {
+    double y0[NP8O_DMAX];
+    const double ny = whiten(c, c->X + (size_t)i * c->D, y0);
     for (int m = 0; m < c->M; ++m) {
-        double g[NP8O_DMAX + 4];
-        aux_normals(c, i, t, m, g);
-        aux_from_normals(c, g[0], g + 1, v + m, mu + m * c->D);
+        double xpar, chi2, xi[NP8O_DMAX];
+        aux_core(c, i, t, m, v + m, &xpar, &chi2);
+        aux_xi(c, i, t, m, y0, ny, xpar, chi2, xi);
+        const int D = c->D;
+        const double s = fabs(v[m]) * c->rsk;
+        for (int a = 0; a < D; ++a) {
+            double t0 = c->LT[a * D + a] * xi[a];
+            for (int b = a + 1; b < D; ++b) t0 = fma(c->LT[a * D + b], xi[b], t0);
+            mu[(size_t)m * D + a] = fma(s, t0, c->cfg.mu0[a]);
+        }
     }
 }
 
@@ -704,30 +784,14 @@ static inline double cand_ll(const np8o_ctx *c, const double *x, int j) {
     return slot_ll(c, x, s);
 }
 
-/* ll of point x under its M auxiliary draws, factored form (DESIGN.md "G0"). */
+/* ll of point x under its M auxiliary draws, in the item's frame (DESIGN.md "G0"). */
 static void aux_ll(const np8o_ctx *c, const double *x, uint64_t i, uint32_t t, double *ll /* M */) {
-    const int D = c->D, M = c->M;
-    double y0[NP8O_DMAX], dx[NP8O_DMAX];
-    for (int a = 0; a < D; ++a) dx[a] = x[a] - c->cfg.mu0[a];
-    for (int a = 0; a < D; ++a) {
-        double t0 = c->UinvT[a * D + a] * dx[a];
-        for (int b = a + 1; b < D; ++b) t0 = fma(c->UinvT[a * D + b], dx[b], t0);
-        y0[a] = t0;
-    }
-    for (int m = 0; m < M; ++m) {
-        double g[NP8O_DMAX + 4];
-        aux_normals(c, i, t, m, g);
-        const double *xi = g + 1;
-        double v = fma(c->cfg.nu, g[0], (double)D);
-        double s = fabs(v) * c->rsk;
-        double r2 = 0.0;
-        for (int a = 0; a < D; ++a) {
-            double e = fma(-s, xi[a], y0[a]);
-            r2 = fma(e, e, r2);
-        }
-        double q = r2 / (v * v);
-        double cm = fma(-(double)D, np8o_log_pos(fabs(v)), c->caux);
-        ll[m] = fma(-0.5, q, cm);
+    double y0[NP8O_DMAX];
+    const double ny = whiten(c, x, y0);
+    for (int m = 0; m < c->M; ++m) {
+        double v, xpar, chi2;
+        aux_core(c, i, t, m, &v, &xpar, &chi2);
+        ll[m] = aux_loglik(c, ny, v, xpar, chi2);
     }
 }
 

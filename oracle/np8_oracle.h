@@ -44,7 +44,8 @@ enum {
     NP8O_STREAM_INIT_THETA = 3,
     NP8O_STREAM_INIT_Z = 4,
     NP8O_STREAM_PARAM = 5,  /* MH proposal normals: i = slot, calls step*Q .. */
-    NP8O_STREAM_PARAM_U = 6 /* MH acceptance uniform: i = slot, call = step */
+    NP8O_STREAM_PARAM_U = 6, /* MH acceptance uniform: i = slot, call = step */
+    NP8O_STREAM_AUX_DIR = 7  /* direction of a picked auxiliary's xi orthogonal to the item */
 };
 
 /* Cluster-parameter update after each sweep (np_mcmc.cpp:170). */
