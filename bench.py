@@ -37,8 +37,9 @@ def parse():
     ap.add_argument("--d", type=int, default=8)
     ap.add_argument("--k", type=int, default=64)
     ap.add_argument("--seed", type=int, default=20261015)
+    ap.add_argument("--config", default="C3", help="config tag for the JSON line (BASELINE.json configs)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget (0 = skip)")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01c.json"))
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01f.json"))
     ap.add_argument("--param-update", default="frozen", choices=["frozen", "mh_g0"],
                     help="cluster-parameter update after every sweep (frozen = the reference's effective one)")
     return ap.parse_args()
@@ -163,7 +164,7 @@ def main():
             "dtype": "f64",
             "data": "synthetic",
             "config": {
-                "workload": f"C3: N={N} D={D} K~{K} M=3 mixture, warm state, "
+                "workload": f"{args.config}: N={N} D={D} K~{K} M=3 mixture, warm state, "
                             + ("frozen cluster parameters" if args.param_update == "frozen"
                                else "mh_g0 cluster-parameter update (20 MH steps/cluster/sweep)"),
                 "N": N, "D": D, "K_final": Kfinal, "parallelism": f"data-sharded x{world}",
@@ -211,7 +212,7 @@ def cpu_baseline(X, z, mu, sig, D, seed, budget_s):
         done = min(done + batch, X.shape[0])
     el = time.perf_counter() - t0
     rate = done / el
-    return {
+    out = {
         "value": rate / X.shape[0],
         "unit": "sweeps/s",
         "cores": 1,
@@ -219,6 +220,23 @@ def cpu_baseline(X, z, mu, sig, D, seed, budget_s):
         "sample": f"{done} sequential point-updates (chunk=1) of one N={X.shape[0]} sweep in {el:.1f}s "
                   f"on 1 core, extrapolated: {rate:.0f} point-updates/s",
     }
+    # cpu_par: the same synchronous sweep the GPU runs, OpenMP over the items, on the
+    # host cores this process may use (the box's share, not the whole machine)
+    threads = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16")))
+    O.set_threads(threads)
+    cp = O.Chain(D, seed=seed, chunk=0, kcap=2048)
+    cp.set_data(X)
+    cp.set_state(z, mu, sig)
+    n, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < budget_s / 2 or n == 0:
+        cp.sweep(1)
+        n += 1
+    el2 = time.perf_counter() - t0
+    O.set_threads(1)
+    out["parallel"] = {"value": n / el2, "unit": "sweeps/s", "cores": threads, "kind": "port",
+                       "sample": f"{n} full synchronous sweeps (chunk=N, the GPU's algorithm) in {el2:.1f}s "
+                                 f"on {threads} threads"}
+    return out
 
 
 if __name__ == "__main__":

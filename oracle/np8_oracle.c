@@ -8,6 +8,9 @@
 #include <math.h>
 #include <stdlib.h>
 #include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
 
 #define LOG2PI 1.8378770664093454835606594728112
 #define TWO_PI 6.283185307179586476925286766559
@@ -859,6 +862,40 @@ static int assign_range_impl(np8o_ctx *c, int64_t p0, int64_t p1, int sync, cons
                              int32_t *n_req) {
     int32_t nr = 0;
     int err = 0;
+    if (sync && p1 - p0 > 1) {
+        /* synchronous step: items are independent given the frozen state, so the CPU-parallel
+         * baseline (SURVEY.md 8(d) "cpu_par") runs them on all threads with identical results
+         * (finalize orders requests by position) */
+#pragma omp parallel for schedule(static)
+        for (int64_t p = p0; p < p1; ++p) {
+            const int64_t i = position_to_point(c, p, sync, order);
+            const double *x = c->X + (size_t)i * c->D;
+            const int32_t zi = c->z[i];
+            const int32_t j = choose(c, i, x, zi);
+            if (j < c->K) {
+                const int32_t s = c->live[j];
+                if (s != zi) {
+#pragma omp atomic
+                    delta[zi] -= 1;
+#pragma omp atomic
+                    delta[s] += 1;
+                    c->z[i] = s;
+                }
+            } else {
+                int32_t q;
+#pragma omp atomic capture
+                q = nr++;
+                if (q < req_cap) {
+                    req_pos[q] = p;
+                    req_i[q] = i;
+                    req_m[q] = j - c->K;
+                    req_zold[q] = zi;
+                }
+            }
+        }
+        *n_req = nr;
+        return err;
+    }
     for (int64_t p = p0; p < p1; ++p) {
         int64_t i = position_to_point(c, p, sync, order);
         const double *x = c->X + (size_t)i * c->D;
@@ -1141,6 +1178,14 @@ int32_t np8o_num_clusters(np8o_ctx *c) { return c->K; }
 uint32_t np8o_epoch(np8o_ctx *c) { return c->t; }
 double np8o_best_loglik(np8o_ctx *c) { return c->best_L; }
 int64_t np8o_mh_accepted(np8o_ctx *c) { return c->mh_accepted; }
+
+void np8o_set_threads(int n) {
+#ifdef _OPENMP
+    if (n > 0) omp_set_num_threads(n);
+#else
+    (void)n;
+#endif
+}
 int32_t *np8o_z_ptr(np8o_ctx *c) { return c->z; }
 
 int np8o_loglik_matrix(np8o_ctx *c, const int64_t *idx, int64_t n, double *out) {

@@ -107,6 +107,8 @@ int32_t np8o_num_clusters(np8o_ctx *c);
 uint32_t np8o_epoch(np8o_ctx *c);
 double np8o_best_loglik(np8o_ctx *c);
 int64_t np8o_mh_accepted(np8o_ctx *c);
+/* Threads of the synchronous step (OpenMP; results do not depend on it). */
+void np8o_set_threads(int n);
 double np8o_total_loglik(np8o_ctx *c);
 /* ll of the given points vs. every live cluster (ascending slot) then the M auxiliaries of the
  * current epoch: out is n x (K+M). Table form (what the chain uses). */

@@ -100,6 +100,7 @@ def lib():
         L.np8o_param_update.restype = i64
         L.np8o_mh_accepted.argtypes = [vp]
         L.np8o_mh_accepted.restype = i64
+        L.np8o_set_threads.argtypes = [C.c_int]
         _lib = L
     return _lib
 
@@ -142,6 +143,11 @@ def mvn_logprobability_ref(x, mu, sigma):
 def weighted_pick_ref(w, u):
     w = np.ascontiguousarray(w, dtype=np.float64)
     return int(lib().np8o_weighted_pick_ref(_p(w), w.size, float(u)))
+
+
+def set_threads(n):
+    """OpenMP threads of the oracle's synchronous step (the cpu_par baseline); results unchanged."""
+    lib().np8o_set_threads(int(n))
 
 
 def similarity(truth, result):

@@ -177,3 +177,21 @@ def test_twogaussians_fixture_matches_recipe():
     assert np.allclose(X[:100].mean(0), 0.0, atol=0.35) and np.allclose(X[100:].mean(0), 5.0, atol=0.35)
     X2, lab2 = datasets.twogaussians()
     np.testing.assert_allclose(X, X2, rtol=0, atol=1e-15)
+
+
+def test_parallel_sync_step_is_deterministic():
+    """The cpu_par baseline (OpenMP over the items of a synchronous step) equals the 1-thread run."""
+    from noparama_amd import datasets
+
+    X, z, mu, sig = datasets.mixture(3000, 3, 8, 0.5, 6.0, seed=3)
+    out = []
+    for threads in (1, 4):
+        O.set_threads(threads)
+        c = O.Chain(3, seed=8, kcap=1024)
+        c.set_data(X)
+        c.init_random(20)
+        c.sweep(3)
+        out.append(c.state())
+    O.set_threads(1)
+    assert out[0]["K"] == out[1]["K"] and np.array_equal(out[0]["z"], out[1]["z"])
+    np.testing.assert_array_equal(out[0]["mu"], out[1]["mu"])
