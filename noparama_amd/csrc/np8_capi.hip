@@ -441,6 +441,10 @@ FinArgs fin_args(np8_ctx *c, const unsigned char *recs, int world) {
     F.seed = c->seed;
     F.t = c->epoch - c->t_base;
     F.r2 = c->r2;
+    F.prune = 0;
+    F.ls = c->kcap;
+    F.plist = c->plist;
+    F.plen = c->plen;
     return F;
 }
 
@@ -483,8 +487,16 @@ AssignArgs assign_args(np8_ctx *c, int64_t p0, int64_t p1, const int64_t *order,
 int launch_finalize(np8_ctx *c, const unsigned char *recs, int world) {
     Timer t;
     timer_begin(c, 1, t);
-    HIPC(c, np8_launch_finalize(fin_args(c, recs, world), c->stream));
+    FinArgs F = fin_args(c, recs, world);
+    // Fused list building (F.prune) is available but off: one workgroup walks the rows 16 at a time,
+    // slower (≈+10 µs at K = 64) than the standalone np8_prune launch with one wave per row.
+    F.prune = 0;
+    HIPC(c, np8_launch_finalize(F, c->stream));
     timer_end(c, t);
+    if (F.prune) {
+        c->lists_valid = true;
+        c->r2_zero = true;
+    }
     return NP8_OK;
 }
 
@@ -667,7 +679,7 @@ int param_update(np8_ctx *c) {
 int end_sweep(np8_ctx *c) {
     int r0 = param_update(c);
     if (r0) return r0;
-    if (c->collecting) {
+    if (c->collecting) {  // after finalize and the parameter update: the table is final
         r0 = launch_prune(c);
         if (r0) return r0;
         c->collecting = false;

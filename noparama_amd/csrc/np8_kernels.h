@@ -26,7 +26,8 @@ struct Ctl {
     int32_t pad2;
     int64_t mh_accepted;  // accepted MH proposals (cumulative)
     uint32_t t_base;      // epoch = t_base + the launch's epoch offset (advanced on the device by
-    int32_t pad3;         // replayed sweep graphs, np8_advance_epoch)
+                          // replayed sweep graphs, np8_advance_epoch)
+    int32_t lists_ok;     // the candidate lists describe the current table (set by the prune pass)
 };
 
 enum : int32_t { kErrCapacity = 1 };
@@ -91,7 +92,7 @@ struct AssignArgs {
 // (then clears r2 for the next one).  One block per row.
 struct PruneArgs {
     const double *cand;
-    const Ctl *ctl;
+    Ctl *ctl;
     double *r2;
     int32_t *plist, *plen;
     int32_t ls, D;
@@ -116,6 +117,10 @@ struct FinArgs {
     uint64_t seed;
     uint32_t t;  // epoch offset: epoch = ctl->t_base + t
     double *r2;  // pruning radii: +inf for every slot created here (unknown radius)
+    // fused candidate pruning after the table rebuild (whole synchronous sweep, no parameter update
+    // to follow); skipped -- lists marked stale -- above kPruneFusedMaxK rows
+    int32_t prune, ls;
+    int32_t *plist, *plen;
 };
 
 struct LoglikArgs {

@@ -169,7 +169,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void n
     // a wave whose items share their cluster (the label-sorted layout) walks that cluster's pruned
     // candidate list: the rows left out are skipped by every lane's pick_step anyway (np8_prune)
     const int32_t z0 = __builtin_amdgcn_readfirstlane(zi);
-    if (A.use_lists && __ballot(zi != z0) == 0) {
+    if (A.use_lists && A.ctl->lists_ok && __ballot(zi != z0) == 0) {
         const int32_t j0 = __builtin_amdgcn_readfirstlane(jo);
         const int32_t nl = A.plen[j0];
         const int32_t *__restrict__ lst = A.plist + (int64_t)j0 * A.ls;
@@ -399,6 +399,62 @@ __device__ int block_excl_scan(int v, int *sh /* >= 16 ints */, int *total) {
 
 }  // namespace
 
+// ---- candidate pruning ------------------------------------------------------------------------------
+// For dense row k0 (mean mu0, radius R = max |x - mu0| over its items, collected by the sweep), row j
+// can be left out of k0's list when no item of k0 can bring it within kSkip of its own log-weight:
+//   lw_j(x) - lw_own(x) <= (c_j + log n_j) - (c_0 + log(n_0 - 1)) - iso_j (|mu_j - mu0| - R)^2 / 2
+//                           + iso_0 R^2 / 2  =: U,
+// using q_j(x) = iso_j |x - mu_j|^2 >= iso_j (|mu_j - mu0| - R)^2 (triangle inequality) and
+// q_0(x) <= iso_0 R^2; T >= lw_own at every step of the pick.  Rows are left out only for U below
+// -kSkip by a margin of 2 nats plus 1e-9 of the terms' magnitude (rounding of the kernel's own
+// arithmetic is ~1e-15 relative).  Non-isotropic rows and singletons (own weight 0) keep every row.
+// One wave builds one row's list (ascending j) and clears the row's radius for the next sweep.
+constexpr int kPruneFusedMaxK = 512;
+
+__device__ void prune_row(const double *__restrict__ cand, double *__restrict__ r2, int32_t *__restrict__ plist,
+                          int32_t *__restrict__ plen, int ls, int D, int K, int k0) {
+    const int DP = D * (D + 1) / 2, CS = cand_stride(D), F = D + DP;
+    const int lane = threadIdx.x & 63;
+    const double *e0 = cand + (int64_t)k0 * CS;
+    const int slot0 = (int)e0[F + kFieldSlot];
+    const double R2 = r2[slot0];
+    const double iso0 = e0[F + kFieldIso];
+    const double base0 = e0[F + kFieldC] + e0[F + kFieldLogn1];
+    const bool prunable = iso0 > 0.0 && R2 < 1e300 && base0 > -1e299;
+    const double R = sqrt(R2);
+    int count = 0;
+    for (int jb = 0; jb < K; jb += 64) {
+        const int j = jb + lane;
+        bool keep = j < K && j != k0;
+        if (keep && prunable) {
+            const double *ej = cand + (int64_t)j * CS;
+            const double isoj = ej[F + kFieldIso];
+            if (isoj > 0.0) {
+                double dist2 = 0.0;
+                for (int a = 0; a < D; ++a) {
+                    const double dd = ej[a] - e0[a];
+                    dist2 = fma(dd, dd, dist2);
+                }
+                const double delta = sqrt(dist2) - R;
+                if (delta > 0.0) {
+                    const double wj = ej[F + kFieldC] + ej[F + kFieldLogn];
+                    const double far = 0.5 * isoj * delta * delta, near = 0.5 * iso0 * R2;
+                    const double U = (wj - base0) - far + near;
+                    const double mag = fabs(wj) + fabs(base0) + far + near;
+                    keep = !(U <= -kSkip - 2.0 - 1e-9 * mag);
+                }
+            }
+        }
+        const uint64_t b = __ballot(keep);
+        if (keep) plist[(int64_t)k0 * ls + count + __popcll(b & ((1ull << lane) - 1ull))] = j;
+        count += __popcll(b);
+    }
+    if (lane == 0) {
+        plen[k0] = count;
+        r2[slot0] = 0.0;  // collected afresh by the next sweep
+    }
+}
+
 // ---- finalize --------------------------------------------------------------------------------------
 namespace {
 
@@ -575,6 +631,14 @@ __global__ __launch_bounds__(kFinThreads) void np8_finalize(FinArgs F) {
         F.cand[(int64_t)r * CS + f] = (f < D) ? F.slot_mu[(int64_t)s * D + f] : F.slot_P[(int64_t)s * DP + (f - D)];
     }
     if (tid == 0) F.ctl->K = nlive;
+    if (F.prune) {  // candidate lists for the next sweep, one wave per row (block-uniform branch)
+        __syncthreads();
+        if (nlive <= kPruneFusedMaxK) {
+            for (int k0 = tid >> 6; k0 < nlive; k0 += kFinThreads / 64)
+                prune_row(F.cand, F.r2, F.plist, F.plen, F.ls, D, nlive, k0);
+        }
+        if (tid == 0) F.ctl->lists_ok = (nlive <= kPruneFusedMaxK) ? 1 : 0;
+    }
     // clear the local record for the next step (all reads of it are behind the barriers above)
     if (F.local_rec) {
         int32_t *delta = reinterpret_cast<int32_t *>(F.local_rec + kRecHeaderBytes);
@@ -1019,75 +1083,19 @@ hipError_t np8_launch_mh_g0(const ParamArgs &A, hipStream_t s) {
     return hipGetLastError();
 }
 
-// ---- candidate pruning ------------------------------------------------------------------------------
-// For dense row k0 (mean mu0, radius R = max |x - mu0| over its items, collected by the sweep), row j
-// can be left out of k0's list when no item of k0 can bring it within kSkip of its own log-weight:
-//   lw_j(x) - lw_own(x) <= (c_j + log n_j) - (c_0 + log(n_0 - 1)) - iso_j (|mu_j - mu0| - R)^2 / 2
-//                           + iso_0 R^2 / 2  =: U,
-// using q_j(x) = iso_j |x - mu_j|^2 >= iso_j (|mu_j - mu0| - R)^2 (triangle inequality) and
-// q_0(x) <= iso_0 R^2; T >= lw_own at every step of the pick.  Rows are left out only for U below
-// -kSkip by a margin of 2 nats plus 1e-9 of the terms' magnitude (rounding of the kernel's own
-// arithmetic is ~1e-15 relative).  Non-isotropic rows and singletons (own weight 0) keep every row.
+// Standalone pass (after the mh_g0 update has moved means): four rows per block.
 __global__ __launch_bounds__(256) void np8_prune(PruneArgs A) {
-    __shared__ int wsum[4];
     const int K = A.ctl->K;
-    const int k0 = blockIdx.x;
+    const int k0 = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (blockIdx.x == 0 && threadIdx.x == 0) A.ctl->lists_ok = 1;
     if (k0 >= K) return;
-    const int D = A.D, DP = D * (D + 1) / 2, CS = cand_stride(D), F = D + DP;
-    const double *e0 = A.cand + (int64_t)k0 * CS;
-    const int slot0 = (int)e0[F + kFieldSlot];
-    const double R2 = A.r2[slot0];
-    const double iso0 = e0[F + kFieldIso];
-    const double base0 = e0[F + kFieldC] + e0[F + kFieldLogn1];
-    const bool prunable = iso0 > 0.0 && R2 < 1e300 && base0 > -1e299;
-    const double R = sqrt(R2);
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    int count = 0;
-    for (int jb = 0; jb < K; jb += 256) {
-        const int j = jb + tid;
-        bool keep = j < K && j != k0;
-        if (keep && prunable) {
-            const double *ej = A.cand + (int64_t)j * CS;
-            const double isoj = ej[F + kFieldIso];
-            if (isoj > 0.0) {
-                double dist2 = 0.0;
-                for (int a = 0; a < D; ++a) {
-                    const double dd = ej[a] - e0[a];
-                    dist2 = fma(dd, dd, dist2);
-                }
-                const double delta = sqrt(dist2) - R;
-                if (delta > 0.0) {
-                    const double wj = ej[F + kFieldC] + ej[F + kFieldLogn];
-                    const double far = 0.5 * isoj * delta * delta, near = 0.5 * iso0 * R2;
-                    const double U = (wj - base0) - far + near;
-                    const double mag = fabs(wj) + fabs(base0) + far + near;
-                    keep = !(U <= -kSkip - 2.0 - 1e-9 * mag);
-                }
-            }
-        }
-        const uint64_t b = __ballot(keep);
-        const int rank = __popcll(b & ((1ull << lane) - 1ull));
-        if (lane == 0) wsum[wv] = __popcll(b);
-        __syncthreads();
-        int before = 0, total = 0;
-        for (int w = 0; w < 4; ++w) {
-            before += (w < wv) ? wsum[w] : 0;
-            total += wsum[w];
-        }
-        if (keep) A.plist[(int64_t)k0 * A.ls + count + before + rank] = j;
-        count += total;
-        __syncthreads();
-    }
-    if (tid == 0) {
-        A.plen[k0] = count;
-        A.r2[slot0] = 0.0;  // collected afresh by the next sweep
-    }
+    prune_row(A.cand, A.r2, A.plist, A.plen, A.ls, A.D, K, k0);
 }
 
 __global__ void np8_advance_epoch(Ctl *ctl, uint32_t n) { ctl->t_base += n; }
 
 hipError_t np8_launch_prune(const PruneArgs &A, int kcap, hipStream_t s) {
-    hipLaunchKernelGGL(np8_prune, dim3((unsigned)kcap), dim3(256), 0, s, A);
+    hipLaunchKernelGGL(np8_prune, dim3((unsigned)((kcap + 3) / 4)), dim3(256), 0, s, A);
     return hipGetLastError();
 }
 
