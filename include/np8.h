@@ -53,15 +53,30 @@ typedef struct {
     int32_t device;       /* HIP device ordinal, -1 = current */
     int32_t param_update; /* NP8_PARAM_*: cluster-parameter update after every sweep (np_mcmc.cpp:170) */
     int32_t mh_steps;     /* MH steps per cluster and sweep for NP8_PARAM_MH_G0; 0 -> 20 (np_mcmc.cpp:54) */
+    int32_t prior;        /* NP8_PRIOR_*: the base measure G0 */
 } np8_config;
+
+/* Base measure G0 (dirichlet_process::sample_base, include/statistics/dirichlet.h:91-93).
+ * REFERENCE: normal_inverse_wishart_distribution as the reference actually draws it
+ *            (normalinvwishart.h:44-64, invwishart.h:30-46): v ~ N(D, nu), Sigma = v^2 chol(Lambda)^T
+ *            chol(Lambda), mu ~ N(mu0, Sigma/kappa).
+ * NIW:       a proper Normal-Inverse-Wishart(mu0, kappa0 = kappa, nu0 = nu, Psi0 = Lambda):
+ *            Sigma ~ IW(Psi0, nu0), mu | Sigma ~ N(mu0, Sigma/kappa0); needs nu0 >= D + 1.  The
+ *            extension config C5 of BASELINE.json runs on. */
+#define NP8_PRIOR_REFERENCE 0
+#define NP8_PRIOR_NIW 1
 
 /* Cluster-parameter update (UpdateClusters::update, src/np_update_clusters.cpp:71-142).
  * FROZEN: parameters never change -- the reference's effective behaviour, because its accepted
  *         proposal is sliced away in cluster_t::setSuffies.
  * MH_G0:  what the reference intends: mh_steps independence-MH steps per live cluster with G0
  *         proposals, evaluated from per-cluster sufficient statistics on the device. */
+/* NIW_CONJUGATE (NIW prior): every live cluster's (mu, Sigma) drawn from its exact Normal-Inverse-
+ *         Wishart posterior given its items -- the Gibbs update the reference leaves as a stub
+ *         (normal_inverse_wishart_distribution::update, include/statistics/normalinvwishart.h:66-75). */
 #define NP8_PARAM_FROZEN 0
 #define NP8_PARAM_MH_G0 1
+#define NP8_PARAM_NIW_CONJUGATE 2
 
 typedef struct {
     int32_t K;                  /* live clusters */

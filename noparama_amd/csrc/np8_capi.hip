@@ -42,6 +42,11 @@ struct np8_ctx {
     int64_t chunk = 0;
     int device = 0;
     int param_update = NP8_PARAM_FROZEN, mh_steps = 20;
+    int prior = NP8_PRIOR_REFERENCE;
+    // NIW prior: U = chol(Psi0^{-1}) (lower), U^{-1}; device copies and the pending-request list
+    std::vector<double> U, Uinv;
+    double *d_U = nullptr, *d_Uinv = nullptr, *d_Psi0 = nullptr;
+    int64_t *pend = nullptr;
     double *acc = nullptr;  // [kcap][D + DP] parameter-update statistics
     // candidate pruning (np8_prune): per-slot radii and per-row candidate lists
     double *r2 = nullptr;
@@ -176,8 +181,69 @@ bool lu_inverse_det(const double *A, int D, double *inv, double *det) {
     return true;
 }
 
+// Cholesky (lower) and lower-triangular inverse in the loop order of oracle/np8_oracle.c (chol_lower,
+// inv_lower): the NIW precomputes must agree to the bit with the oracle's.
+bool chol_lower(const double *A, int D, std::vector<double> &L) {
+    L.assign((size_t)D * D, 0.0);
+    for (int j = 0; j < D; ++j) {
+        double s = A[j * D + j];
+        for (int k = 0; k < j; ++k) s -= L[j * D + k] * L[j * D + k];
+        if (!(s > 0.0)) return false;
+        L[j * D + j] = std::sqrt(s);
+        for (int i = j + 1; i < D; ++i) {
+            double v = A[i * D + j];
+            for (int k = 0; k < j; ++k) v -= L[i * D + k] * L[j * D + k];
+            L[i * D + j] = v / L[j * D + j];
+        }
+    }
+    return true;
+}
+
+void inv_lower(const std::vector<double> &L, int D, std::vector<double> &Li) {
+    Li.assign((size_t)D * D, 0.0);
+    for (int j = 0; j < D; ++j) {
+        Li[j * D + j] = 1.0 / L[j * D + j];
+        for (int r = j + 1; r < D; ++r) {
+            double s = 0.0;
+            for (int k = j; k < r; ++k) s -= L[r * D + k] * Li[k * D + j];
+            Li[r * D + j] = s / L[r * D + r];
+        }
+    }
+}
+
+// NIW prior (DESIGN.md "Priors"): U = chol(Psi0^{-1}) with Psi0^{-1} = Lp^{-T} Lp^{-1}, Lp = chol(Psi0);
+// UinvT holds U^T (the whitening of the item frame) and caux = -D/2 log 2pi + sum log U_aa.
+bool prepare_niw(np8_ctx *c) {
+    const int D = c->D;
+    std::vector<double> Lp, Li, Pi((size_t)D * D);
+    if (!chol_lower(c->Lambda.data(), D, Lp)) return false;
+    inv_lower(Lp, D, Li);
+    for (int a = 0; a < D; ++a)
+        for (int b = 0; b < D; ++b) {
+            double s = 0.0;
+            for (int k = (a > b ? a : b); k < D; ++k) s += Li[k * D + a] * Li[k * D + b];
+            Pi[a * D + b] = s;
+        }
+    if (!chol_lower(Pi.data(), D, c->U)) return false;
+    inv_lower(c->U, D, c->Uinv);
+    double sl = 0.0;
+    for (int a = 0; a < D; ++a) sl += std::log(c->U[a * D + a]);
+    c->caux = -0.5 * (double)D * kLog2PiC + sl;
+    c->UinvT.assign((size_t)D * D, 0.0);
+    for (int a = 0; a < D; ++a)
+        for (int b = 0; b < D; ++b) c->UinvT[a * D + b] = c->U[b * D + a];
+    c->LT.assign((size_t)D * D, 0.0);  // unused by the NIW prior
+    c->Gp.assign((size_t)D * D, 0.0);
+    c->LTL.assign((size_t)D * D, 0.0);
+    c->gp_iso = 0.0;
+    c->rsk = 1.0 / std::sqrt(c->kappa);
+    c->logam = std::log(c->alpha / (double)c->M);
+    return true;
+}
+
 // Base-measure precomputes: L = chol(Lambda) (invwishart.h:40), (L^T)^{-1}, (L^T L)^{-1}, L^T L.
 bool prepare_base(np8_ctx *c) {
+    if (c->prior == NP8_PRIOR_NIW) return prepare_niw(c);
     const int D = c->D;
     c->Lc.assign((size_t)D * D, 0.0);
     std::vector<double> &L = c->Lc;
@@ -268,6 +334,11 @@ bool slot_from_sigma(const np8_ctx *c, const double *mu, const double *Sigma, Sl
 }
 
 void free_device(np8_ctx *c) {
+    void *niw_ptrs[] = {c->d_U, c->d_Uinv, c->d_Psi0, c->pend};
+    for (void *p : niw_ptrs)
+        if (p) (void)hipFree(p);
+    c->d_U = c->d_Uinv = c->d_Psi0 = nullptr;
+    c->pend = nullptr;
     void *ptrs[] = {c->X,      c->z,       c->z_best, c->slot_mu, c->slot_P,  c->slot_c,  c->slot_sigma,
                     c->cnt,    c->cnt_best, c->mu_best, c->sigma_best, c->cand, c->ctl,    c->hyp,
                     c->d_mu0,  c->d_LT,    c->d_Gp,   c->d_LTL,   c->rec,     c->gath,    c->order,
@@ -445,7 +516,40 @@ FinArgs fin_args(np8_ctx *c, const unsigned char *recs, int world) {
     F.ls = c->kcap;
     F.plist = c->plist;
     F.plen = c->plen;
+    F.prior = c->prior;
+    F.pad2 = 0;
+    F.pend = c->pend;
     return F;
+}
+
+NiwArgs niw_args(np8_ctx *c) {
+    NiwArgs A;
+    std::memset(&A, 0, sizeof(A));
+    A.D = c->D;
+    A.kcap = c->kcap;
+    A.kappa0 = c->kappa;
+    A.nu0 = c->nu;
+    A.rsk = c->rsk;
+    A.caux = c->caux;
+    A.mu0 = c->d_mu0;
+    A.Psi0 = c->d_Psi0;
+    A.U = c->d_U;
+    A.Uinv = c->d_Uinv;
+    A.seed = c->seed;
+    A.t = c->epoch - c->t_base;
+    A.write_cand = 1;
+    A.ctl = c->ctl;
+    A.cnt = c->cnt;
+    A.dense_of = c->dense_of;
+    A.acc = c->acc;
+    A.slot_mu = c->slot_mu;
+    A.slot_P = c->slot_P;
+    A.slot_c = c->slot_c;
+    A.slot_sigma = c->slot_sigma;
+    A.slot_iso = c->slot_iso;
+    A.cand = c->cand;
+    A.r2 = c->r2;
+    return A;
 }
 
 AssignArgs assign_args(np8_ctx *c, int64_t p0, int64_t p1, const int64_t *order, bool use_perm) {
@@ -492,6 +596,12 @@ int launch_finalize(np8_ctx *c, const unsigned char *recs, int world) {
     // slower (≈+10 µs at K = 64) than the standalone np8_prune launch with one wave per row.
     F.prune = 0;
     HIPC(c, np8_launch_finalize(F, c->stream));
+    if (c->prior == NP8_PRIOR_NIW) {  // the accepted auxiliaries' full parameters
+        NiwArgs A = niw_args(c);
+        A.recs = recs;
+        A.pend = c->pend;
+        HIPC(c, np8_launch_niw_aux_slots(A, c->stream));
+    }
     timer_end(c, t);
     if (F.prune) {
         c->lists_valid = true;
@@ -512,7 +622,7 @@ int launch_assign(np8_ctx *c, int64_t p0, int64_t p1, const int64_t *order, bool
     AssignArgs A = assign_args(c, p0, p1, order, use_perm);
     A.collect_r2 = c->collecting ? 1 : 0;
     A.use_lists = (c->collecting && c->lists_valid) ? 1 : 0;
-    HIPC(c, np8_launch_assign(A, c->D, c->M, c->stream));
+    HIPC(c, np8_launch_assign(A, c->D, c->M, c->prior, c->stream));
     timer_end(c, t);
     if (c->collecting) c->r2_zero = false;
     return NP8_OK;
@@ -627,9 +737,9 @@ int launch_total_loglik(np8_ctx *c) {
 // UpdateClusters::update (np_mcmc.cpp:170) in mh_g0 mode: statistics of the current labelling
 // (summed over ranks), then one MH chain per live slot; candidate rows are patched in place.
 int param_update(np8_ctx *c) {
-    if (c->param_update != NP8_PARAM_MH_G0) return NP8_OK;
+    if (c->param_update == NP8_PARAM_FROZEN) return NP8_OK;
     if (c->world > 1 && !c->comm)
-        return fail(c, NP8_ERR_STATE, "mh_g0 parameter update needs the RCCL transport when sharded");
+        return fail(c, NP8_ERR_STATE, "the parameter update needs the RCCL transport when sharded");
     Timer t;
     timer_begin(c, 3, t);
     ParamArgs A;
@@ -671,7 +781,10 @@ int param_update(np8_ctx *c) {
     // rows np8_suffstats adds to are those of live slots)
     HIPC(c, np8_launch_suffstats(A, c->stream));
     if (c->world > 1) NCCLC(c, ncclAllReduce(c->acc, c->acc, nacc, ncclFloat64, ncclSum, c->comm, c->stream));
-    HIPC(c, np8_launch_mh_g0(A, c->stream));
+    if (c->param_update == NP8_PARAM_NIW_CONJUGATE)
+        HIPC(c, np8_launch_niw_post(niw_args(c), c->kcap, c->stream));
+    else
+        HIPC(c, np8_launch_mh_g0(A, c->stream));
     timer_end(c, t);
     return NP8_OK;
 }
@@ -848,11 +961,20 @@ int np8_create(np8_ctx **out, const np8_config *cfg) {
     c->nu = cfg->nu;
     c->seed = cfg->seed;
     c->chunk = cfg->chunk;
-    if (cfg->param_update < NP8_PARAM_FROZEN || cfg->param_update > NP8_PARAM_MH_G0 || cfg->mh_steps < 0 ||
-        cfg->mh_steps > 65536) {
+    if (cfg->param_update < NP8_PARAM_FROZEN || cfg->param_update > NP8_PARAM_NIW_CONJUGATE || cfg->mh_steps < 0 ||
+        cfg->mh_steps > 65536 || (cfg->prior != NP8_PRIOR_REFERENCE && cfg->prior != NP8_PRIOR_NIW)) {
         delete c;
         return NP8_ERR_ARG;
     }
+    // mh_g0 proposes from the reference's G0; the conjugate update needs the NIW prior; the Bartlett
+    // chi^2(nu0 - a), a < D, need nu0 >= D + 1 (Marsaglia-Tsang shape >= 1)
+    const bool niw = cfg->prior == NP8_PRIOR_NIW;
+    if ((niw && cfg->param_update == NP8_PARAM_MH_G0) || (!niw && cfg->param_update == NP8_PARAM_NIW_CONJUGATE) ||
+        (niw && !(cfg->nu >= cfg->D + 1.0 && cfg->nu < 1e12))) {
+        delete c;
+        return NP8_ERR_ARG;
+    }
+    c->prior = cfg->prior;
     c->param_update = cfg->param_update;
     c->mh_steps = cfg->mh_steps > 0 ? cfg->mh_steps : 20;
     c->mu0.assign(cfg->mu0, cfg->mu0 + c->D);
@@ -911,7 +1033,10 @@ int np8_create(np8_ctx **out, const np8_config *cfg) {
         for (int b = a; b < D; ++b) gp.push_back(c->Gp[a * D + b]);
     if ((r = dalloc(c, &c->hyp, hyp.size())) || (r = dalloc(c, &c->d_mu0, (size_t)D)) ||
         (r = dalloc(c, &c->d_LT, (size_t)D * D)) || (r = dalloc(c, &c->d_Gp, gp.size())) ||
-        (r = dalloc(c, &c->d_LTL, (size_t)D * D))) {
+        (r = dalloc(c, &c->d_LTL, (size_t)D * D)) ||
+        (c->prior == NP8_PRIOR_NIW &&
+         ((r = dalloc(c, &c->d_U, (size_t)D * D)) || (r = dalloc(c, &c->d_Uinv, (size_t)D * D)) ||
+          (r = dalloc(c, &c->d_Psi0, (size_t)D * D)) || (r = dalloc(c, &c->pend, (size_t)4 * kReqMax))))) {
         free_device(c);
         delete c;
         return r;
@@ -923,8 +1048,15 @@ int np8_create(np8_ctx **out, const np8_config *cfg) {
         hipMemcpyAsync(c->d_mu0, c->mu0.data(), sizeof(double) * D, hipMemcpyHostToDevice, c->stream) == hipSuccess &&
         hipMemcpyAsync(c->d_LT, c->LT.data(), sizeof(double) * D * D, hipMemcpyHostToDevice, c->stream) == hipSuccess &&
         hipMemcpyAsync(c->d_Gp, gp.data(), sizeof(double) * gp.size(), hipMemcpyHostToDevice, c->stream) == hipSuccess &&
-        hipMemcpyAsync(c->d_LTL, c->LTL.data(), sizeof(double) * D * D, hipMemcpyHostToDevice, c->stream) == hipSuccess;
-    if (!up_ok || reset_ctl(c) || hipStreamSynchronize(c->stream) != hipSuccess) {
+        hipMemcpyAsync(c->d_LTL, c->LTL.data(), sizeof(double) * D * D, hipMemcpyHostToDevice, c->stream) == hipSuccess &&
+        (c->prior != NP8_PRIOR_NIW ||
+         (hipMemcpyAsync(c->d_U, c->U.data(), sizeof(double) * D * D, hipMemcpyHostToDevice, c->stream) == hipSuccess &&
+          hipMemcpyAsync(c->d_Uinv, c->Uinv.data(), sizeof(double) * D * D, hipMemcpyHostToDevice, c->stream) ==
+              hipSuccess &&
+          hipMemcpyAsync(c->d_Psi0, c->Lambda.data(), sizeof(double) * D * D, hipMemcpyHostToDevice, c->stream) ==
+              hipSuccess));
+    if (!up_ok || reset_ctl(c) || hipStreamSynchronize(c->stream) != hipSuccess ||
+        (c->prior == NP8_PRIOR_NIW && np8_niw_prepare(D) != hipSuccess)) {
         free_device(c);
         delete c;
         return NP8_ERR_HIP;
@@ -982,10 +1114,26 @@ int np8_set_data(np8_ctx *c, const double *X, int64_t n, int32_t D, int64_t offs
     return NP8_OK;
 }
 
+// niw_init_map (NIW prior, np8_init_random): G0 draw k goes to slot (*niw_init_map)[k] (-1: dropped),
+// drawn on the device by np8_niw_post before the candidate table is built.
 static int set_state_common(np8_ctx *c, const std::vector<SlotHost> &slots, const std::vector<int32_t> &cnt,
-                            const std::vector<int32_t> &zloc) {
+                            const std::vector<int32_t> &zloc, const std::vector<int32_t> *niw_init_map = nullptr) {
     int r = upload_slots(c, slots, cnt);
     if (r) return r;
+    if (niw_init_map) {
+        int32_t *d_map = nullptr;
+        const int kinit = (int)niw_init_map->size();
+        HIPC(c, hipMalloc(&d_map, sizeof(int32_t) * kinit));
+        HIPC(c, hipMemcpyAsync(d_map, niw_init_map->data(), sizeof(int32_t) * kinit, hipMemcpyHostToDevice, c->stream));
+        NiwArgs A = niw_args(c);
+        A.write_cand = 0;
+        A.init_k = kinit;
+        A.init_map = d_map;
+        const hipError_t e = np8_launch_niw_post(A, kinit, c->stream);
+        HIPC(c, hipStreamSynchronize(c->stream));
+        (void)hipFree(d_map);
+        HIPC(c, e);
+    }
     HIPC(c, hipMemcpyAsync(c->z, zloc.data(), sizeof(int32_t) * zloc.size(), hipMemcpyHostToDevice, c->stream));
     c->sorted_valid = false;
     c->use_sorted = false;
@@ -1047,8 +1195,15 @@ int np8_init_random(np8_ctx *c, int32_t K_init) {
     if (!c->have_data) return fail(c, NP8_ERR_STATE, "np8_init_random: no data");
     if (K_init < 1 || K_init > c->kcap) return fail(c, NP8_ERR_ARG, "np8_init_random: K_init outside [1,kcap]");
     const int D = c->D, Q = g0_calls(D);
+    const bool niw = c->prior == NP8_PRIOR_NIW;  // NIW: the draws are made on the device (np8_niw_post)
     std::vector<SlotHost> draws(K_init);
     for (int k = 0; k < K_init; ++k) {  // InitClusters::init: K G0 draws (np_init_clusters.cpp:24-40)
+        if (niw) {
+            draws[k].mu.assign(D, 0.0);
+            draws[k].P.assign(c->DP, 0.0);
+            draws[k].sigma.assign((size_t)D * D, 0.0);
+            continue;
+        }
         std::vector<double> g(4 * Q);
         for (int q = 0; q < Q; ++q) {
             double gq[4];
@@ -1077,7 +1232,7 @@ int np8_init_random(np8_ctx *c, int32_t K_init) {
             cnt.push_back(cntk[k]);
         }
     for (auto &v : zl) v = remap[v];
-    return set_state_common(c, slots, cnt, zl);
+    return set_state_common(c, slots, cnt, zl, niw ? &remap : nullptr);
 }
 
 int np8_sweep(np8_ctx *c, int32_t n_sweeps) {
@@ -1209,7 +1364,8 @@ int np8_loglik_matrix(np8_ctx *c, const int64_t *idx, int64_t n, double *out) {
     HIPC(c, hipMalloc(&d_idx, sizeof(int64_t) * n));
     HIPC(c, hipMalloc(&d_out, sizeof(double) * n * w));
     HIPC(c, hipMemcpy(d_idx, idx, sizeof(int64_t) * n, hipMemcpyHostToDevice));
-    HIPC(c, np8_launch_loglik_matrix(assign_args(c, 0, 0, nullptr, false), c->D, c->M, d_idx, n, d_out, c->stream));
+    HIPC(c, np8_launch_loglik_matrix(assign_args(c, 0, 0, nullptr, false), c->D, c->M, c->prior, d_idx, n, d_out,
+                                     c->stream));
     HIPC(c, hipStreamSynchronize(c->stream));
     HIPC(c, hipMemcpy(out, d_out, sizeof(double) * n * w, hipMemcpyDeviceToHost));
     (void)hipFree(d_idx);
@@ -1297,7 +1453,7 @@ int np8_comm_init(np8_ctx *c, const uint8_t id[128], int32_t rank, int32_t world
     if (!c || world < 1 || rank < 0 || rank >= world) return NP8_ERR_ARG;
     if (!id) {  // host-exchange mode: the caller moves records (np8_step_local / np8_step_merge)
         if (world > 1 && c->param_update != NP8_PARAM_FROZEN)
-            return fail(c, NP8_ERR_ARG, "np8_comm_init: the mh_g0 parameter update needs the RCCL transport");
+            return fail(c, NP8_ERR_ARG, "np8_comm_init: the parameter update needs the RCCL transport");
         c->rank = rank;
         return resize_records(c, world);
     }

@@ -23,8 +23,13 @@ enum Stream : uint32_t {
     kStreamInitZ = 4,
     kStreamParam = 5,  // MH proposal normals (i = slot)
     kStreamParamU = 6,  // MH acceptance uniforms (i = slot)
-    kStreamAuxDir = 7   // direction of a picked auxiliary's xi orthogonal to the item (i = item)
+    kStreamAuxDir = 7,  // direction of a picked auxiliary's xi orthogonal to the item (i = item);
+                        // NIW: Bartlett off-diagonals and the z_perp direction of a picked auxiliary
+    kStreamAuxNiw = 8   // NIW prior: an auxiliary's Bartlett chi^2 draws, chi^2_{D-1} and z_1 (i = item)
 };
+
+// Base measures (include/np8.h NP8_PRIOR_*).
+enum Prior : int { kPriorReference = 0, kPriorNiw = 1 };
 
 // Candidate-table entry layout (doubles):
 //   [mu(D) | P'(D(D+1)/2) | c | logn | logn1 | slot | iso]
@@ -254,6 +259,98 @@ NP8_HD void aux_xi(uint64_t seed, uint64_t i, uint32_t t, int m, int D, const do
     const double np = sqrt(n2);
     const double sc = (np > 0.0) ? sqrt(chi2) / np : 0.0;
     for (int a = 0; a < D; ++a) xi[a] = fma(xpar, yh[a], sc * w[a]);
+}
+
+// ---- NIW prior (DESIGN.md "Priors"; oracle/np8_oracle.c has the derivation) ----------------------
+constexpr uint32_t kNiwAuxCalls = 8192u;   // Philox calls reserved per auxiliary m
+constexpr uint32_t kNiwGammaCalls = 64u;   // calls reserved per chi^2 draw
+constexpr uint32_t kNiwNormalCall0 = 8192u; // posterior draws: first call of the normals
+
+// Marsaglia-Tsang Gamma(alpha, 1), alpha >= 1: two attempts per Philox call (Box-Muller pair from
+// words 0, 1; 32-bit uniforms words 2, 3); at most 4096 calls, so every lane terminates.
+NP8_HD double gamma_mt(uint64_t seed, uint64_t i, uint32_t t, uint32_t stream, uint32_t call0, double alpha) {
+    const double d = alpha - 1.0 / 3.0;
+    const double cc = 1.0 / sqrt(9.0 * d);
+    for (uint32_t r = 0; r < 4096u; ++r) {
+        uint32_t o[4];
+        philox_call(seed, i, t, stream, call0 + r, o);
+        const double rad = sqrt(-2.0 * log_pos(u32_01(o[0])));
+        double sn, cs;
+        sincos_2pi(u32_01(o[1]), sn, cs);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const double x = rad * (h ? sn : cs);
+            const double v1 = fma(cc, x, 1.0);
+            if (v1 <= 0.0) continue;
+            const double v = v1 * v1 * v1;
+            const double u = u32_01(o[2 + h]);
+            const double x2 = x * x;
+            if (u < fma(-0.0331, x2 * x2, 1.0)) return d * v;
+            if (log_pos(u) < fma(0.5, x2, d * ((1.0 - v) + log_pos(v)))) return d * v;
+        }
+    }
+    return d;
+}
+
+NP8_HD double chi2_mt(uint64_t seed, uint64_t i, uint32_t t, uint32_t stream, uint32_t call0, double dof) {
+    return 2.0 * gamma_mt(seed, i, t, stream, call0, 0.5 * dof);
+}
+
+// Normal number n of stream (i, t) counted from call c0 (normal_quad layout).
+NP8_HD double normal_at(uint64_t seed, uint64_t i, uint32_t t, uint32_t stream, uint32_t c0, uint32_t n) {
+    double g[4];
+    normal_quad(seed, i, t, stream, c0 + (n >> 2), g);
+    return g[n & 3];
+}
+
+// chi^2_{D-1} = |z_perp|^2 of auxiliary draw `base`: D-1 squared normals for D <= 4, else Marsaglia-Tsang.
+NP8_HD double niw_chi_perp(uint64_t seed, uint64_t i, uint32_t t, uint32_t stream, uint32_t base, int D) {
+    const int k = D - 1;
+    if (k <= 0) return 0.0;
+    if (k <= 3) {
+        double g[4];
+        normal_quad(seed, i, t, stream, base + kNiwAuxCalls - 2u, g);
+        double s = g[0] * g[0];
+        for (int j = 1; j < k; ++j) s = fma(g[j], g[j], s);
+        return s;
+    }
+    return chi2_mt(seed, i, t, stream, base + kNiwGammaCalls * (uint32_t)D, (double)k);
+}
+
+// Sum of logs of chi^2 draws, taken over products of at most 16.
+struct LogAcc {
+    double prod = 1.0, sumlog = 0.0;
+    NP8_HD void add(double g, int idx, int last) {
+        prod *= g;
+        if ((idx & 15) == 15 || idx == last) {
+            sumlog += log_pos(prod);
+            prod = 1.0;
+        }
+    }
+};
+
+// Auxiliary m of item i under the NIW prior, in the item's frame: the D Bartlett chi^2 draws
+// (sumlog = sum log, b00 = sqrt of the first), chi^2_{D-1} and z_1.
+NP8_HD void niw_aux_core(uint64_t seed, uint64_t i, uint32_t t, int m, int D, double nu0, double &sumlog, double &b00,
+                         double &chi, double &z1) {
+    const uint32_t base = (uint32_t)m * kNiwAuxCalls;
+    LogAcc la;
+    b00 = 0.0;
+    for (int a = 0; a < D; ++a) {
+        const double g = chi2_mt(seed, i, t, kStreamAuxNiw, base + kNiwGammaCalls * (uint32_t)a, nu0 - a);
+        if (a == 0) b00 = sqrt(g);
+        la.add(g, a, D - 1);
+    }
+    sumlog = la.sumlog;
+    chi = niw_chi_perp(seed, i, t, kStreamAuxNiw, base, D);
+    z1 = normal_at(seed, i, t, kStreamAuxNiw, base + kNiwAuxCalls - 1u, 0);
+}
+
+// ll = caux + sumlog/2 - q/2, q = (|dt| b00 - z1/sqrt(kappa0))^2 + chi/kappa0 (nd = |dt|).
+NP8_HD double niw_aux_loglik(double nd, double sumlog, double b00, double chi, double z1, double rsk, double caux) {
+    const double e = fma(-z1, rsk, nd * b00);
+    const double q = fma(e, e, chi * (rsk * rsk));
+    return fma(-0.5, q, fma(0.5, sumlog, caux));
 }
 
 // Log-weight standing for weight 0 (a singleton's own cluster): finite, so no -inf arithmetic.

@@ -28,6 +28,8 @@ struct Ctl {
     uint32_t t_base;      // epoch = t_base + the launch's epoch offset (advanced on the device by
                           // replayed sweep graphs, np8_advance_epoch)
     int32_t lists_ok;     // the candidate lists describe the current table (set by the prune pass)
+    int32_t n_pend;       // NIW prior: accepted requests waiting for np8_niw_aux_slots (set by np8_finalize)
+    int32_t pad3;
 };
 
 enum : int32_t { kErrCapacity = 1 };
@@ -121,6 +123,31 @@ struct FinArgs {
     // to follow); skipped -- lists marked stale -- above kPruneFusedMaxK rows
     int32_t prune, ls;
     int32_t *plist, *plen;
+    // NIW prior: accepted requests are listed in pend[4 q] = (byte offset of the request's record
+    // payload in recs, item, m, slot) for np8_niw_aux_slots instead of being written here
+    int32_t prior, pad2;
+    int64_t *pend;
+};
+
+// NIW prior kernels (np8_niw.hip): posterior / prior draws per slot and picked auxiliaries -> slots.
+struct NiwArgs {
+    int32_t D, kcap;
+    double kappa0, nu0, rsk, caux;  // rsk = 1/sqrt(kappa0); caux = -D/2 log 2pi + sum log U_aa
+    const double *mu0, *Psi0;       // Psi0: D x D row-major
+    const double *U, *Uinv;         // U = chol(Psi0^{-1}) (lower) and its inverse, D x D row-major
+    uint64_t seed;
+    uint32_t t;  // epoch offset: epoch = ctl->t_base + t
+    int32_t write_cand;  // also patch the candidate rows (dense_of valid)
+    Ctl *ctl;
+    const int32_t *cnt, *dense_of;
+    double *acc;  // [kcap][D + DP] statistics (np8_suffstats), zeroed after use
+    double *slot_mu, *slot_P, *slot_c, *slot_sigma, *slot_iso;
+    double *cand;
+    double *r2;
+    int32_t init_k, pad;             // > 0: draw G0 sample b into slot init_map[b] (b < init_k)
+    const int32_t *init_map;
+    const unsigned char *recs;  // np8_niw_aux_slots: the records np8_finalize read
+    const int64_t *pend;
 };
 
 struct LoglikArgs {
@@ -186,9 +213,13 @@ struct SortArgs {
 };
 
 bool np8_supported(int D, int M);
+size_t np8_niw_lds_bytes(int D);
+hipError_t np8_niw_prepare(int D);
+hipError_t np8_launch_niw_post(const np8::NiwArgs &A, int nblocks, hipStream_t s);
+hipError_t np8_launch_niw_aux_slots(const np8::NiwArgs &A, hipStream_t s);
 hipError_t np8_launch_resort(const SortArgs &S, hipStream_t s);
-hipError_t np8_launch_assign(const np8::AssignArgs &A, int D, int M, hipStream_t s);
-hipError_t np8_launch_loglik_matrix(const np8::AssignArgs &A, int D, int M, const int64_t *idx, int64_t n,
+hipError_t np8_launch_assign(const np8::AssignArgs &A, int D, int M, int prior, hipStream_t s);
+hipError_t np8_launch_loglik_matrix(const np8::AssignArgs &A, int D, int M, int prior, const int64_t *idx, int64_t n,
                                     double *out, hipStream_t s);
 size_t np8_finalize_lds_bytes(int kcap);
 hipError_t np8_launch_finalize(const np8::FinArgs &F, hipStream_t s);

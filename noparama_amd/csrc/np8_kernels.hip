@@ -93,6 +93,25 @@ __device__ __forceinline__ double aux_ll(const double *__restrict__ hyp, double 
     return aux_loglik(ny, v, xpar, chi2, D, hyp[H::kRsk], hyp[H::kCaux]);
 }
 
+// Log-likelihood of the item (whitened by U^T: nd = |U^T (x - mu0)|) under auxiliary m of the NIW prior.
+template <int D>
+__device__ __forceinline__ double niw_aux_ll(const double *__restrict__ hyp, double nd, uint64_t seed, uint64_t ig,
+                                             uint32_t t, int m) {
+    using H = HypView<D>;
+    double sumlog, b00, chi, z1;
+    niw_aux_core(seed, ig, t, m, D, hyp[H::kNu], sumlog, b00, chi, z1);
+    return niw_aux_loglik(nd, sumlog, b00, chi, z1, hyp[H::kRsk], hyp[H::kCaux]);
+}
+
+template <int D, int PRIOR>
+__device__ __forceinline__ double prior_aux_ll(const double *__restrict__ hyp, double ny, uint64_t seed, uint64_t ig,
+                                               uint32_t t, int m) {
+    if constexpr (PRIOR == kPriorNiw)
+        return niw_aux_ll<D>(hyp, ny, seed, ig, t, m);
+    else
+        return aux_ll<D>(hyp, ny, seed, ig, t, m);
+}
+
 // (v, mu) of a picked auxiliary: mu = mu0 + (|v|/sqrt kappa) L^T xi with xi from aux_xi.
 template <int D>
 __device__ __forceinline__ void aux_params(const double *__restrict__ hyp, const double (&y0)[D], double ny,
@@ -128,7 +147,7 @@ __device__ __forceinline__ int64_t position_to_local(const AssignArgs &A, int64_
     return p;
 }
 
-template <int D, int M>
+template <int D, int M, int PRIOR>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void np8_assign(AssignArgs A) {
     constexpr int DP = D * (D + 1) / 2;
     constexpr int CS = (D + DP + 5 + 1) & ~1;
@@ -191,7 +210,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void n
     {
         const double logam = hyp[HypView<D>::kLogam];
 #pragma unroll 1
-        for (int m = 0; m < M; ++m) pick_step(st, aux_ll<D>(hyp, ny, A.seed, ig, t, m) + logam, K + m);
+        for (int m = 0; m < M; ++m) pick_step(st, prior_aux_ll<D, PRIOR>(hyp, ny, A.seed, ig, t, m) + logam, K + m);
     }
 
     RecHeader *hdr = reinterpret_cast<RecHeader *>(A.rec);
@@ -245,7 +264,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void n
             r.pad = 0;
             req[q] = r;
             double *vmu = reinterpret_cast<double *>(A.rec + record_vmu_offset(A.kcap, A.rec_cap)) + (int64_t)q * (D + 1);
-            aux_params<D>(hyp, y0, ny, A.seed, ig, t, st.pick - K, vmu);
+            if constexpr (PRIOR == kPriorNiw) {  // the item's frame; np8_niw_aux_slots builds the slot
+                vmu[0] = ny;
+#pragma unroll
+                for (int a = 0; a < D; ++a) vmu[1 + a] = y0[a];
+            } else {
+                aux_params<D>(hyp, y0, ny, A.seed, ig, t, st.pick - K, vmu);
+            }
         }
     }
 }
@@ -594,7 +619,15 @@ __global__ __launch_bounds__(kFinThreads) void np8_finalize(FinArgs F) {
         for (int q = tid; q < nreq; q += kFinThreads) {
             const Request r = *request_at(F, base, kidx[q]);
             const int s = freeslot[q];
-            write_new_slot(F, request_vmu(F, base, kidx[q]), s);
+            if (F.prior == kPriorNiw) {  // built by np8_niw_aux_slots (O(D^3) per slot)
+                int64_t *pe = F.pend + 4 * (int64_t)q;
+                pe[0] = reinterpret_cast<const unsigned char *>(request_vmu(F, base, kidx[q])) - F.recs;
+                pe[1] = r.i;
+                pe[2] = r.m;
+                pe[3] = s;
+            } else {
+                write_new_slot(F, request_vmu(F, base, kidx[q]), s);
+            }
             cnt_s[s] = 1;
             if (r.i >= F.offset && r.i < F.offset + F.n_loc) {
                 F.z[r.i - F.offset] = s;
@@ -630,7 +663,10 @@ __global__ __launch_bounds__(kFinThreads) void np8_finalize(FinArgs F) {
         const int r = idx / W, f = idx - r * W, s = live_s[r];
         F.cand[(int64_t)r * CS + f] = (f < D) ? F.slot_mu[(int64_t)s * D + f] : F.slot_P[(int64_t)s * DP + (f - D)];
     }
-    if (tid == 0) F.ctl->K = nlive;
+    if (tid == 0) {
+        F.ctl->K = nlive;
+        F.ctl->n_pend = (F.prior == kPriorNiw && accept) ? nreq : 0;
+    }
     if (F.prune) {  // candidate lists for the next sweep, one wave per row (block-uniform branch)
         __syncthreads();
         if (nlive <= kPruneFusedMaxK) {
@@ -950,7 +986,7 @@ __global__ __launch_bounds__(64) void np8_mh_g0(ParamArgs A) {
 }
 
 // ---- parity/debug: log-likelihood matrix --------------------------------------------------------------
-template <int D, int M>
+template <int D, int M, int PRIOR>
 __global__ __launch_bounds__(256) void np8_loglik_matrix_kernel(AssignArgs A, const int64_t *__restrict__ idx,
                                                                 int64_t n, double *__restrict__ out) {
     constexpr int DP = D * (D + 1) / 2;
@@ -968,7 +1004,7 @@ __global__ __launch_bounds__(256) void np8_loglik_matrix_kernel(AssignArgs A, co
     whiten<D>(A.hyp, x, y0);
     const double ny = norm_of<D>(y0);
     const uint32_t t = A.ctl->t_base + A.t;
-    for (int m = 0; m < M; ++m) out[r * (K + M) + K + m] = aux_ll<D>(A.hyp, ny, A.seed, ig, t, m);
+    for (int m = 0; m < M; ++m) out[r * (K + M) + K + m] = prior_aux_ll<D, PRIOR>(A.hyp, ny, A.seed, ig, t, m);
 }
 
 // ---- dispatch ----------------------------------------------------------------------------------------
@@ -984,28 +1020,35 @@ bool np8_supported(int D, int M) {
     return false;
 }
 
-hipError_t np8_launch_assign(const AssignArgs &A, int D, int M, hipStream_t s) {
+hipError_t np8_launch_assign(const AssignArgs &A, int D, int M, int prior, hipStream_t s) {
     const int64_t n = A.p1 - A.p0;
     if (n <= 0) return hipSuccess;
     const dim3 grid((unsigned)((n + 255) / 256)), block(256);
-#define X(d, m)                                                               \
-    if (D == d && M == m) {                                                   \
-        hipLaunchKernelGGL((np8_assign<d, m>), grid, block, 0, s, A);         \
-        return hipGetLastError();                                             \
+#define X(d, m)                                                                           \
+    if (D == d && M == m) {                                                               \
+        if (prior == kPriorNiw)                                                           \
+            hipLaunchKernelGGL((np8_assign<d, m, kPriorNiw>), grid, block, 0, s, A);       \
+        else                                                                              \
+            hipLaunchKernelGGL((np8_assign<d, m, kPriorReference>), grid, block, 0, s, A); \
+        return hipGetLastError();                                                         \
     }
     NP8_FOR_EACH_DM(X)
 #undef X
     return hipErrorInvalidValue;
 }
 
-hipError_t np8_launch_loglik_matrix(const AssignArgs &A, int D, int M, const int64_t *idx, int64_t n, double *out,
-                                    hipStream_t s) {
+hipError_t np8_launch_loglik_matrix(const AssignArgs &A, int D, int M, int prior, const int64_t *idx, int64_t n,
+                                    double *out, hipStream_t s) {
     if (n <= 0) return hipSuccess;
     const dim3 grid((unsigned)((n + 255) / 256)), block(256);
-#define X(d, m)                                                                              \
-    if (D == d && M == m) {                                                                  \
-        hipLaunchKernelGGL((np8_loglik_matrix_kernel<d, m>), grid, block, 0, s, A, idx, n, out); \
-        return hipGetLastError();                                                            \
+#define X(d, m)                                                                                                 \
+    if (D == d && M == m) {                                                                                     \
+        if (prior == kPriorNiw)                                                                                 \
+            hipLaunchKernelGGL((np8_loglik_matrix_kernel<d, m, kPriorNiw>), grid, block, 0, s, A, idx, n, out);   \
+        else                                                                                                    \
+            hipLaunchKernelGGL((np8_loglik_matrix_kernel<d, m, kPriorReference>), grid, block, 0, s, A, idx, n, \
+                               out);                                                                            \
+        return hipGetLastError();                                                                               \
     }
     NP8_FOR_EACH_DM(X)
 #undef X

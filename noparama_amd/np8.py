@@ -61,10 +61,12 @@ class _Config(C.Structure):
         ("device", C.c_int32),
         ("param_update", C.c_int32),
         ("mh_steps", C.c_int32),
+        ("prior", C.c_int32),
     ]
 
 
-PARAM_UPDATE = {"frozen": 0, "mh_g0": 1}  # NP8_PARAM_* (include/np8.h)
+PARAM_UPDATE = {"frozen": 0, "mh_g0": 1, "niw_conjugate": 2}  # NP8_PARAM_* (include/np8.h)
+PRIOR = {"reference": 0, "niw": 1}  # NP8_PRIOR_*
 
 
 class Stats(C.Structure):
@@ -157,12 +159,15 @@ class NealAlgorithm8:
     Parameters follow the reference wiring (src/np_main.cpp:164,365-372,433-438): D (likelihood
     dimension), M auxiliaries (np_neal_algorithm8.cpp:33), alpha (Suffies_Dirichlet), and the base
     measure mu0, kappa, nu, Lambda.  `chunk` = points per synchronous step (0: whole sweep).
-    `param_update`: "frozen" (the reference's effective behaviour) or "mh_g0" (UpdateClusters as
-    intended: `mh_steps` G0-proposal MH steps per cluster after every sweep, np_update_clusters.cpp).
+    `param_update`: "frozen" (the reference's effective behaviour), "mh_g0" (UpdateClusters as
+    intended: `mh_steps` G0-proposal MH steps per cluster after every sweep, np_update_clusters.cpp) or
+    "niw_conjugate" (prior="niw": exact posterior draw per cluster, normalinvwishart.h:66-75).
+    `prior`: "reference" (the reference's G0 as it draws) or "niw" (a proper Normal-Inverse-Wishart with
+    kappa0 = kappa, nu0 = nu >= D + 1, Psi0 = Lambda).
     """
 
     def __init__(self, D, M=3, alpha=1.0, mu0=None, kappa=1.0 / 500, nu=4.0, Lambda=None, seed=0, kcap=2048,
-                 chunk=0, device=-1, param_update="frozen", mh_steps=20):
+                 chunk=0, device=-1, param_update="frozen", mh_steps=20, prior="reference"):
         self.D, self.M, self.kcap = int(D), int(M), int(kcap)
         self._mu0 = np.ascontiguousarray(np.full(D, 6.0) if mu0 is None else mu0, dtype=np.float64)
         self._Lam = np.ascontiguousarray(0.01 * np.eye(D) if Lambda is None else Lambda, dtype=np.float64)
@@ -175,6 +180,9 @@ class NealAlgorithm8:
         if param_update not in PARAM_UPDATE:
             raise ValueError(f"param_update must be one of {sorted(PARAM_UPDATE)}")
         cfg.param_update, cfg.mh_steps = PARAM_UPDATE[param_update], int(mh_steps)
+        if prior not in PRIOR:
+            raise ValueError(f"prior must be one of {sorted(PRIOR)}")
+        cfg.prior = PRIOR[prior]
         h = C.c_void_p()
         r = lib().np8_create(C.byref(h), C.byref(cfg))
         if r:

@@ -377,6 +377,9 @@ struct np8o_ctx {
     double Gp[NP8O_DMAX * NP8O_DMAX];    /* (L^T L)^{-1}, off-diagonals doubled (upper used) */
     double LTL[NP8O_DMAX * NP8O_DMAX];   /* L^T L */
     double caux, rsk, logam;
+    /* NIW prior: U = chol(Psi0^{-1}) (lower) and its inverse; UinvT then holds U^T and caux the NIW
+     * constant -D/2 log 2pi + sum log U_aa (DESIGN.md "Priors") */
+    double U[NP8O_DMAX * NP8O_DMAX], Uinv[NP8O_DMAX * NP8O_DMAX];
     /* data */
     int64_t N;
     double *X; /* N x D row-major */
@@ -405,9 +408,69 @@ static int packed_index(int D, int a, int b) { /* upper triangle, row-major, a <
     return a * D - (a * (a - 1)) / 2 + (b - a);
 }
 
+/* Host-side precomputes (the library's host code runs the same loops): Cholesky (lower) and the
+ * inverse of a lower-triangular matrix. */
+static int chol_lower(const double *A, int D, double *L) {
+    memset(L, 0, sizeof(double) * D * D);
+    for (int j = 0; j < D; ++j) {
+        double s = A[j * D + j];
+        for (int k = 0; k < j; ++k) s -= L[j * D + k] * L[j * D + k];
+        if (!(s > 0.0)) return -1;
+        L[j * D + j] = sqrt(s);
+        for (int i = j + 1; i < D; ++i) {
+            double v = A[i * D + j];
+            for (int k = 0; k < j; ++k) v -= L[i * D + k] * L[j * D + k];
+            L[i * D + j] = v / L[j * D + j];
+        }
+    }
+    return 0;
+}
+
+static void inv_lower(const double *L, int D, double *Li) {
+    memset(Li, 0, sizeof(double) * D * D);
+    for (int j = 0; j < D; ++j) {
+        Li[j * D + j] = 1.0 / L[j * D + j];
+        for (int r = j + 1; r < D; ++r) {
+            double s = 0.0;
+            for (int k = j; k < r; ++k) s -= L[r * D + k] * Li[k * D + j];
+            Li[r * D + j] = s / L[r * D + r];
+        }
+    }
+}
+
+/* NIW prior: U = chol(Psi0^{-1}) with Psi0^{-1} = Lp^{-T} Lp^{-1}, Lp = chol(Psi0). */
+static int niw_prepare(np8o_ctx *c) {
+    const int D = c->D;
+    static double Lp[NP8O_DMAX * NP8O_DMAX], Li[NP8O_DMAX * NP8O_DMAX], Pi[NP8O_DMAX * NP8O_DMAX];
+    if (chol_lower(c->cfg.Lambda, D, Lp) != 0) return -1;
+    inv_lower(Lp, D, Li);
+    for (int a = 0; a < D; ++a)
+        for (int b = 0; b < D; ++b) {
+            double s = 0.0;
+            for (int k = (a > b ? a : b); k < D; ++k) s += Li[k * D + a] * Li[k * D + b];
+            Pi[a * D + b] = s;
+        }
+    if (chol_lower(Pi, D, c->U) != 0) return -1;
+    inv_lower(c->U, D, c->Uinv);
+    double sl = 0.0;
+    for (int a = 0; a < D; ++a) sl += log(c->U[a * D + a]);
+    c->caux = -0.5 * (double)D * LOG2PI + sl;
+    for (int a = 0; a < D; ++a)
+        for (int b = 0; b < D; ++b) c->UinvT[a * D + b] = c->U[b * D + a];
+    return 0;
+}
+
 np8o_ctx *np8o_create(const np8o_config *cfg) {
     if (cfg->D < 1 || cfg->D > NP8O_DMAX || cfg->M < 1 || cfg->M > NP8O_MMAX || cfg->kcap < 1) return NULL;
-    if (cfg->param_update < NP8O_PARAM_FROZEN || cfg->param_update > NP8O_PARAM_MH_G0 || cfg->mh_steps < 0) return NULL;
+    if (cfg->param_update < NP8O_PARAM_FROZEN || cfg->param_update > NP8O_PARAM_NIW_CONJUGATE || cfg->mh_steps < 0)
+        return NULL;
+    if (cfg->prior != NP8O_PRIOR_REFERENCE && cfg->prior != NP8O_PRIOR_NIW) return NULL;
+    /* mh_g0 proposes from the reference's G0; the conjugate update needs the NIW prior; Bartlett's
+     * chi^2(nu0 - a), a < D, need nu0 >= D + 1 for Marsaglia-Tsang's shape >= 1 */
+    if ((cfg->prior == NP8O_PRIOR_NIW) != (cfg->param_update == NP8O_PARAM_NIW_CONJUGATE) &&
+        !(cfg->prior == NP8O_PRIOR_NIW && cfg->param_update == NP8O_PARAM_FROZEN))
+        return NULL;
+    if (cfg->prior == NP8O_PRIOR_NIW && !(cfg->nu >= cfg->D + 1.0 && cfg->nu < 1e12)) return NULL;
     np8o_ctx *c = (np8o_ctx *)calloc(1, sizeof(np8o_ctx));
     c->cfg = *cfg;
     const int D = cfg->D;
@@ -458,6 +521,10 @@ np8o_ctx *np8o_create(const np8o_config *cfg) {
     c->caux = -0.5 * (double)D * LOG2PI - sumlog;
     c->rsk = 1.0 / sqrt(cfg->kappa);
     c->logam = log(cfg->alpha / (double)cfg->M);
+    if (cfg->prior == NP8O_PRIOR_NIW && niw_prepare(c) != 0) {
+        free(c);
+        return NULL;
+    }
     const int K = c->kcap;
     c->slot_mu = (double *)calloc((size_t)K * D, sizeof(double));
     c->slot_P = (double *)calloc((size_t)K * c->DP, sizeof(double));
@@ -660,10 +727,338 @@ static void aux_draws(const np8o_ctx *c, uint64_t i, uint32_t t, double *v, doub
     }
 }
 
+/* ================================================================================================
+ * NIW prior (DESIGN.md "Priors").  A proper Normal-Inverse-
+ * Wishart G0 -- Sigma ~ IW(Psi0, nu0), mu | Sigma ~ N(mu0, Sigma/kappa0) -- replacing the reference's
+ * scale-only draw, and its conjugate posterior (the update the reference stubs with assert(false),
+ * include/statistics/normalinvwishart.h:66-75).  Sampling follows the reference's two-stage
+ * operator() (normalinvwishart.h:44-64: Sigma from the inverse Wishart, then mu from N(mu, Sigma/kappa));
+ * the inverse Wishart is drawn through Bartlett's decomposition of the Wishart precision.
+ * ============================================================================================== */
+#define NIW_AUX_CALLS 8192u   /* Philox calls reserved per auxiliary m on streams AUX_NIW / AUX_DIR */
+#define NIW_GAMMA_CALLS 64u   /* calls reserved per chi^2 draw (two Marsaglia-Tsang attempts per call) */
+#define NIW_NORMAL_CALL0 8192u /* posterior draws: first call of the Bartlett off-diagonal and z normals */
+
+/* Marsaglia & Tsang (2000), Gamma(alpha, 1) for alpha >= 1: per Philox call one Box-Muller pair
+ * (words 0, 1) gives two attempts x, with 32-bit uniforms words 2, 3; accept d v, v = (1 + c x)^3, when
+ * u < 1 - 0.0331 x^4 or log u < x^2/2 + d (1 - v + log v).  4096 calls at most (never reached: each
+ * attempt is accepted with probability > 0.95), so every lane of a kernel terminates. */
+double np8o_gamma_mt(uint64_t seed, uint64_t i, uint32_t t, uint32_t stream, uint32_t call0, double alpha) {
+    const double d = alpha - 1.0 / 3.0;
+    const double cc = 1.0 / sqrt(9.0 * d);
+    for (uint32_t r = 0; r < 4096u; ++r) {
+        uint32_t o[4];
+        philox_call(seed, i, t, stream, call0 + r, o);
+        const double rad = sqrt(-2.0 * np8o_log_pos(u32_01(o[0])));
+        double sn, cs;
+        np8o_sincos_2pi(u32_01(o[1]), &sn, &cs);
+        for (int h = 0; h < 2; ++h) {
+            const double x = rad * (h ? sn : cs);
+            const double v1 = fma(cc, x, 1.0);
+            if (v1 <= 0.0) continue;
+            const double v = v1 * v1 * v1;
+            const double u = u32_01(o[2 + h]);
+            const double x2 = x * x;
+            if (u < fma(-0.0331, x2 * x2, 1.0)) return d * v;
+            if (np8o_log_pos(u) < fma(0.5, x2, d * ((1.0 - v) + np8o_log_pos(v)))) return d * v;
+        }
+    }
+    return d;
+}
+
+/* chi^2 with dof degrees of freedom (dof >= 2) = 2 Gamma(dof/2). */
+static inline double chi2_mt(uint64_t seed, uint64_t i, uint32_t t, uint32_t stream, uint32_t call0, double dof) {
+    return 2.0 * np8o_gamma_mt(seed, i, t, stream, call0, 0.5 * dof);
+}
+
+/* Normal number n of stream (i, t) counted from call c0 (normal_quad layout). */
+static inline double normal_at(uint64_t seed, uint64_t i, uint32_t t, uint32_t stream, uint32_t c0, uint32_t n) {
+    double g[4];
+    normal_quad(seed, i, t, stream, c0 + (n >> 2), g);
+    return g[n & 3];
+}
+
+/* chi^2_{D-1} of |z_perp|^2: a sum of D-1 squared normals (one call) for D <= 4, else Marsaglia-Tsang
+ * at call base + 64 D. */
+static double niw_chi_perp(uint64_t seed, uint64_t i, uint32_t t, uint32_t stream, uint32_t base, int D) {
+    const int k = D - 1;
+    if (k <= 0) return 0.0;
+    if (k <= 3) {
+        double g[4];
+        normal_quad(seed, i, t, stream, base + NIW_AUX_CALLS - 2u, g);
+        double s = g[0] * g[0];
+        for (int j = 1; j < k; ++j) s = fma(g[j], g[j], s);
+        return s;
+    }
+    return chi2_mt(seed, i, t, stream, base + NIW_GAMMA_CALLS * (uint32_t)D, (double)k);
+}
+
+/* Running sum of logs of products of at most 16 chi^2 draws (their product cannot overflow). */
+typedef struct {
+    double prod, sumlog;
+} logacc;
+
+static inline void logacc_add(logacc *a, double g, int idx, int last) {
+    a->prod *= g;
+    if ((idx & 15) == 15 || idx == last) {
+        a->sumlog += np8o_log_pos(a->prod);
+        a->prod = 1.0;
+    }
+}
+
+/* ---- auxiliary draws in the item's frame ------------------------------------------------------
+ * Sigma^{-1} = U Omega U^T with U U^T = Psi0^{-1} (U = chol(Psi0^{-1}), lower) and Omega ~ W(I, nu0);
+ * mu = mu0 + eps, U^T... Write Omega = R B B^T R with B Bartlett-lower (B_aa^2 ~ chi^2(nu0 - a),
+ * B_ab ~ N(0,1) below) and R the reflection taking e1 to -+ dt/|dt|, dt = U^T (x - mu0): rotation
+ * invariance of W(I, nu0) makes this a G0 draw whatever R is.  With F = U R B, Sigma^{-1} = F F^T and
+ * mu = mu0 + F^{-T} z'/sqrt(kappa0), z' ~ N(0, I):
+ *   F^T (x - mu) = (s |dt| B_00 - s z'_0/sqrt(kappa0), -z'_rest/sqrt(kappa0))          (s = +-1)
+ *   ll = -D/2 log 2pi + sum log U_aa + 1/2 sum_a log B_aa^2 - q/2,
+ *   q  = (|dt| B_00 - z_1/sqrt(kappa0))^2 + chi^2_{D-1}/kappa0.
+ * So the likelihood needs the D diagonal chi^2 draws, z_1 and chi^2_{D-1} = |z_rest|^2: auxiliary m
+ * draws them on stream AUX_NIW, calls base = m NIW_AUX_CALLS: chi^2(nu0 - a) from base + 64 a,
+ * chi^2_{D-1} from niw_chi_perp, z_1 = normal 0 of call base + NIW_AUX_CALLS - 1.  Only a picked
+ * auxiliary is built in full (niw_aux_slot): B's off-diagonals (normal a(a-1)/2 + b) and the direction
+ * w of z_rest (normals D(D-1)/2 + j) on stream AUX_DIR from call base. */
+static void niw_aux_core(const np8o_ctx *c, uint64_t i, uint32_t t, int m, double *sumlog, double *b00, double *chi,
+                         double *z1) {
+    const int D = c->D;
+    const uint64_t seed = c->cfg.seed;
+    const uint32_t base = (uint32_t)m * NIW_AUX_CALLS;
+    logacc la = {1.0, 0.0};
+    *b00 = 0.0;
+    for (int a = 0; a < D; ++a) {
+        const double g = chi2_mt(seed, i, t, NP8O_STREAM_AUX_NIW, base + NIW_GAMMA_CALLS * (uint32_t)a, c->cfg.nu - a);
+        if (a == 0) *b00 = sqrt(g);
+        logacc_add(&la, g, a, D - 1);
+    }
+    *sumlog = la.sumlog;
+    *chi = niw_chi_perp(seed, i, t, NP8O_STREAM_AUX_NIW, base, D);
+    *z1 = normal_at(seed, i, t, NP8O_STREAM_AUX_NIW, base + NIW_AUX_CALLS - 1u, 0);
+}
+
+static double niw_aux_loglik(const np8o_ctx *c, double nd, double sumlog, double b00, double chi, double z1) {
+    const double e = fma(-z1, c->rsk, nd * b00);
+    const double q = fma(e, e, chi * (c->rsk * c->rsk));
+    return fma(-0.5, q, fma(0.5, sumlog, c->caux));
+}
+
+static inline int packed_ix(int D, int a, int b) { return a * D - (a * (a - 1)) / 2 + (b - a); }
+
+/* Outputs shared by the NIW draws: mu, packed P' = sym(Sigma^{-1}) (off-diagonals doubled), Sigma, c. */
+static void niw_outputs_from_F(int D, const double *F, double *Ppk) {
+    for (int a = 0; a < D; ++a)
+        for (int b = a; b < D; ++b) {
+            double s = 0.0;
+            for (int k = 0; k < D; ++k) s = fma(F[a * D + k], F[b * D + k], s);
+            Ppk[packed_ix(D, a, b)] = (a == b) ? s : 2.0 * s;
+        }
+}
+
+/* Sigma = T^T T with T lower-solved from B T = Rhs (B lower triangular, Rhs full). */
+static void niw_sigma(int D, const double *B, const double *Rhs, double *T, double *Sigma) {
+    for (int j = 0; j < D; ++j)
+        for (int a = 0; a < D; ++a) {
+            double s = Rhs[a * D + j];
+            for (int k = 0; k < a; ++k) s = fma(-B[a * D + k], T[k * D + j], s);
+            T[a * D + j] = s / B[a * D + a];
+        }
+    for (int a = 0; a < D; ++a)
+        for (int b = 0; b < D; ++b) {
+            double s = 0.0;
+            for (int k = 0; k < D; ++k) s = fma(T[k * D + a], T[k * D + b], s);
+            Sigma[a * D + b] = s;
+        }
+}
+
+/* The full parameters of auxiliary m of item i (dt = U^T (x - mu0)), exactly the draw whose
+ * likelihood niw_aux_core/niw_aux_loglik evaluated. */
+static void niw_aux_slot(const np8o_ctx *c, uint64_t i, uint32_t t, int m, const double *dt, double *mu, double *Ppk,
+                         double *Sigma, double *cc) {
+    const int D = c->D;
+    const uint64_t seed = c->cfg.seed;
+    const uint32_t base = (uint32_t)m * NIW_AUX_CALLS;
+    static _Thread_local double B[NP8O_DMAX * NP8O_DMAX], RB[NP8O_DMAX * NP8O_DMAX], F[NP8O_DMAX * NP8O_DMAX],
+        T[NP8O_DMAX * NP8O_DMAX];
+    memset(B, 0, sizeof(double) * D * D);
+    logacc la = {1.0, 0.0};
+    for (int a = 0; a < D; ++a) {
+        const double g = chi2_mt(seed, i, t, NP8O_STREAM_AUX_NIW, base + NIW_GAMMA_CALLS * (uint32_t)a, c->cfg.nu - a);
+        B[a * D + a] = sqrt(g);
+        logacc_add(&la, g, a, D - 1);
+    }
+    const double chi = niw_chi_perp(seed, i, t, NP8O_STREAM_AUX_NIW, base, D);
+    const double z1 = normal_at(seed, i, t, NP8O_STREAM_AUX_NIW, base + NIW_AUX_CALLS - 1u, 0);
+    for (int a = 1; a < D; ++a)
+        for (int b = 0; b < a; ++b)
+            B[a * D + b] = normal_at(seed, i, t, NP8O_STREAM_AUX_DIR, base, (uint32_t)(a * (a - 1) / 2 + b));
+    double z[NP8O_DMAX], w2 = 0.0;
+    const uint32_t nw0 = (uint32_t)(D * (D - 1) / 2);
+    for (int j = 0; j + 1 < D; ++j) {
+        z[1 + j] = normal_at(seed, i, t, NP8O_STREAM_AUX_DIR, base, nw0 + (uint32_t)j);
+        w2 = fma(z[1 + j], z[1 + j], w2);
+    }
+    const double sc = (w2 > 0.0) ? sqrt(chi / w2) : 0.0;
+    for (int j = 1; j < D; ++j) z[j] *= sc;
+    /* Householder reflection R = I - beta h h^T, R dt = sig |dt| e1 */
+    double n2 = 0.0;
+    for (int a = 0; a < D; ++a) n2 = fma(dt[a], dt[a], n2);
+    const double nd = sqrt(n2);
+    double h[NP8O_DMAX] = {0.0}, beta = 0.0, sig = 1.0;
+    if (nd > 0.0) {
+        for (int a = 0; a < D; ++a) h[a] = dt[a] / nd;
+        const double sg = (h[0] >= 0.0) ? 1.0 : -1.0;
+        h[0] = h[0] + sg;
+        double hh = 0.0;
+        for (int a = 0; a < D; ++a) hh = fma(h[a], h[a], hh);
+        beta = 2.0 / hh;
+        sig = -sg;
+    }
+    z[0] = sig * z1;
+    /* RB = B - beta h (h^T B);  F = U RB */
+    for (int b = 0; b < D; ++b) {
+        double cs = 0.0;
+        for (int k = b; k < D; ++k) cs = fma(h[k], B[k * D + b], cs);
+        for (int a = 0; a < D; ++a) RB[a * D + b] = fma(-(beta * h[a]), cs, B[a * D + b]);
+    }
+    for (int a = 0; a < D; ++a)
+        for (int b = 0; b < D; ++b) {
+            double s = 0.0;
+            for (int k = 0; k <= a; ++k) s = fma(c->U[a * D + k], RB[k * D + b], s);
+            F[a * D + b] = s;
+        }
+    niw_outputs_from_F(D, F, Ppk);
+    /* mu = mu0 + U^{-T} R B^{-T} z rsk */
+    double y[NP8O_DMAX], ry[NP8O_DMAX], eps[NP8O_DMAX];
+    for (int a = D - 1; a >= 0; --a) {
+        double s = z[a] * c->rsk;
+        for (int k = a + 1; k < D; ++k) s = fma(-B[k * D + a], y[k], s);
+        y[a] = s / B[a * D + a];
+    }
+    double hy = 0.0;
+    for (int k = 0; k < D; ++k) hy = fma(h[k], y[k], hy);
+    for (int a = 0; a < D; ++a) ry[a] = fma(-(beta * h[a]), hy, y[a]);
+    for (int a = D - 1; a >= 0; --a) {
+        double s = ry[a];
+        for (int k = a + 1; k < D; ++k) s = fma(-c->U[k * D + a], eps[k], s);
+        eps[a] = s / c->U[a * D + a];
+    }
+    for (int a = 0; a < D; ++a) mu[a] = c->cfg.mu0[a] + eps[a];
+    /* Sigma = T^T T, T = F^{-1} = B^{-1} (R U^{-1}) */
+    for (int b = 0; b < D; ++b) {
+        double cs = 0.0;
+        for (int k = b; k < D; ++k) cs = fma(h[k], c->Uinv[k * D + b], cs);
+        for (int a = 0; a < D; ++a) RB[a * D + b] = fma(-(beta * h[a]), cs, c->Uinv[a * D + b]);
+    }
+    niw_sigma(D, B, RB, T, Sigma);
+    *cc = fma(0.5, la.sumlog, c->caux);
+}
+
+/* NIW(mu0, kappa0, nu0, Psi0) posterior of n items with statistics s1 = sum d, S = sum d d^T (packed
+ * upper) about the anchor a (d = x - a), then a draw (Sigma, mu) from it (n = 0: the prior):
+ *   kn = kappa0 + n, nun = nu0 + n, xb = a + s1/n, mun = (kappa0 mu0 + n xb)/kn,
+ *   Psin = Psi0 + (S - s1 s1^T/n) + (kappa0 n/kn)(xb - mu0)(xb - mu0)^T;
+ *   Ln = chol(Psin); Sigma^{-1} = F F^T with F = Ln^{-T} B (B Bartlett-lower with nun), so Sigma ~ IW(Psin, nun);
+ *   mu = mun + Ln B^{-T} z / sqrt(kn) ~ N(mun, Sigma/kn);  c = -D/2 log 2pi - sum log Ln_aa + 1/2 sum log B_aa^2.
+ * Draws of (i, t, stream): chi^2(nun - a) from call 64 a, then normals from call NIW_NORMAL_CALL0:
+ * B_ab (a > b) is normal a(a-1)/2 + b, z_j is normal D(D-1)/2 + j.  Returns -1 (nothing written) if
+ * Psin is not numerically positive definite. */
+static int niw_draw_impl(const np8o_ctx *c, uint64_t i, uint32_t t, uint32_t stream, int64_t n, const double *s1,
+                         const double *S, const double *anchor, double *mu, double *Ppk, double *Sigma, double *cc) {
+    const int D = c->D;
+    const uint64_t seed = c->cfg.seed;
+    static _Thread_local double L[NP8O_DMAX * NP8O_DMAX], Li[NP8O_DMAX * NP8O_DMAX], B[NP8O_DMAX * NP8O_DMAX],
+        F[NP8O_DMAX * NP8O_DMAX], T[NP8O_DMAX * NP8O_DMAX], Lt[NP8O_DMAX * NP8O_DMAX];
+    const double k0 = c->cfg.kappa, nd = (double)n;
+    const double kn = k0 + nd, nun = c->cfg.nu + nd;
+    const double kf = (k0 * nd) / kn;
+    double xb[NP8O_DMAX], dm[NP8O_DMAX], mun[NP8O_DMAX];
+    for (int a = 0; a < D; ++a) {
+        xb[a] = (n > 0) ? anchor[a] + s1[a] / nd : c->cfg.mu0[a];
+        dm[a] = xb[a] - c->cfg.mu0[a];
+        mun[a] = fma(k0, c->cfg.mu0[a], nd * xb[a]) / kn;
+    }
+    /* Cholesky of Psin (lower triangle of Psin formed on the fly) */
+    memset(L, 0, sizeof(double) * D * D);
+    for (int j = 0; j < D; ++j) {
+        for (int r = j; r < D; ++r) {
+            const double sc = (n > 0) ? S[packed_ix(D, j, r)] - (s1[r] * s1[j]) / nd : 0.0;
+            double v = fma(kf, dm[r] * dm[j], c->cfg.Lambda[r * D + j] + sc);
+            for (int k = 0; k < j; ++k) v = fma(-L[r * D + k], L[j * D + k], v);
+            if (r == j) {
+                if (!(v > 0.0)) return -1;
+                L[j * D + j] = sqrt(v);
+            } else {
+                L[r * D + j] = v / L[j * D + j];
+            }
+        }
+    }
+    /* Li = Ln^{-1} (lower), forward substitution per column */
+    memset(Li, 0, sizeof(double) * D * D);
+    for (int j = 0; j < D; ++j) {
+        Li[j * D + j] = 1.0 / L[j * D + j];
+        for (int r = j + 1; r < D; ++r) {
+            double s = 0.0;
+            for (int k = j; k < r; ++k) s = fma(-L[r * D + k], Li[k * D + j], s);
+            Li[r * D + j] = s / L[r * D + r];
+        }
+    }
+    memset(B, 0, sizeof(double) * D * D);
+    logacc la = {1.0, 0.0};
+    for (int a = 0; a < D; ++a) {
+        const double g = chi2_mt(seed, i, t, stream, NIW_GAMMA_CALLS * (uint32_t)a, nun - a);
+        B[a * D + a] = sqrt(g);
+        logacc_add(&la, g, a, D - 1);
+    }
+    for (int a = 1; a < D; ++a)
+        for (int b = 0; b < a; ++b)
+            B[a * D + b] = normal_at(seed, i, t, stream, NIW_NORMAL_CALL0, (uint32_t)(a * (a - 1) / 2 + b));
+    double z[NP8O_DMAX];
+    for (int j = 0; j < D; ++j) z[j] = normal_at(seed, i, t, stream, NIW_NORMAL_CALL0, (uint32_t)(D * (D - 1) / 2 + j));
+    /* F = Li^T B */
+    for (int a = 0; a < D; ++a)
+        for (int b = 0; b < D; ++b) {
+            double s = 0.0;
+            for (int k = (a > b ? a : b); k < D; ++k) s = fma(Li[k * D + a], B[k * D + b], s);
+            F[a * D + b] = s;
+        }
+    niw_outputs_from_F(D, F, Ppk);
+    /* mu = mun + Ln B^{-T} z rskn */
+    const double rskn = 1.0 / sqrt(kn);
+    double y[NP8O_DMAX];
+    for (int a = D - 1; a >= 0; --a) {
+        double s = z[a] * rskn;
+        for (int k = a + 1; k < D; ++k) s = fma(-B[k * D + a], y[k], s);
+        y[a] = s / B[a * D + a];
+    }
+    for (int a = 0; a < D; ++a) {
+        double s = 0.0;
+        for (int k = 0; k <= a; ++k) s = fma(L[a * D + k], y[k], s);
+        mu[a] = mun[a] + s;
+    }
+    /* Sigma = T^T T, T = B^{-1} Ln^T */
+    for (int a = 0; a < D; ++a)
+        for (int b = 0; b < D; ++b) Lt[a * D + b] = L[b * D + a];
+    niw_sigma(D, B, Lt, T, Sigma);
+    double sl = 0.0;
+    for (int a = 0; a < D; ++a) sl += np8o_log_pos(L[a * D + a]);
+    *cc = fma(0.5, la.sumlog, fma(-0.5 * (double)D, LOG2PI, -sl));
+    return 0;
+}
+
 /* Candidate table: live slots in ascending order, log n_k, log(n_k - 1) (weight 0 as the finite
  * NP8O_ZERO_LW), and the isotropy flag (off-diagonals of P' exactly 0, one common diagonal). */
 #define NP8O_ZERO_LW (-1.0e300)
 #define NP8O_SKIP 800.0
+
+/* Slot s from auxiliary m of item i (NIW prior). */
+static void niw_slot_from_aux(np8o_ctx *c, int s, uint64_t i, uint32_t t, int m) {
+    const int D = c->D;
+    double dt[NP8O_DMAX];
+    whiten(c, c->X + (size_t)i * D, dt);
+    niw_aux_slot(c, i, t, m, dt, c->slot_mu + (size_t)s * D, c->slot_P + (size_t)s * c->DP,
+                 c->slot_sigma + (size_t)s * D * D, c->slot_c + s);
+}
 
 static void rebuild_dense(np8o_ctx *c) {
     int K = 0;
@@ -711,7 +1106,8 @@ int np8o_init_random(np8o_ctx *c, int32_t K_init) {
     double *mu = (double *)malloc(sizeof(double) * (size_t)K_init * D);
     double *vv = (double *)malloc(sizeof(double) * (size_t)K_init);
     int32_t *cntk = (int32_t *)calloc((size_t)K_init, sizeof(int32_t));
-    for (int k = 0; k < K_init; ++k) {
+    const int niw = c->cfg.prior == NP8O_PRIOR_NIW;
+    for (int k = 0; k < K_init && !niw; ++k) {
         double g[NP8O_DMAX + 4];
         for (int call = 0; call < g0_calls(D); ++call)
             normal_quad(c->cfg.seed, (uint64_t)k, 0xFFFFFFFFu, NP8O_STREAM_INIT_THETA, (uint32_t)call, g + 4 * call);
@@ -731,7 +1127,12 @@ int np8o_init_random(np8o_ctx *c, int32_t K_init) {
     for (int k = 0; k < K_init; ++k) {
         if (cntk[k] > 0) {
             remap[k] = s;
-            slot_from_aux(c, s, vv[k], mu + (size_t)k * D);
+            if (niw) /* G0 draw k: the NIW posterior of no items, stream INIT_THETA (i = k) */
+                niw_draw_impl(c, (uint64_t)k, 0xFFFFFFFFu, NP8O_STREAM_INIT_THETA, 0, NULL, NULL, NULL,
+                              c->slot_mu + (size_t)s * D, c->slot_P + (size_t)s * c->DP,
+                              c->slot_sigma + (size_t)s * D * D, c->slot_c + s);
+            else
+                slot_from_aux(c, s, vv[k], mu + (size_t)k * D);
             c->cnt[s] = cntk[k];
             ++s;
         } else {
@@ -790,7 +1191,15 @@ static inline double cand_ll(const np8o_ctx *c, const double *x, int j) {
 /* ll of point x under its M auxiliary draws, in the item's frame (DESIGN.md "G0"). */
 static void aux_ll(const np8o_ctx *c, const double *x, uint64_t i, uint32_t t, double *ll /* M */) {
     double y0[NP8O_DMAX];
-    const double ny = whiten(c, x, y0);
+    const double ny = whiten(c, x, y0); /* NIW: dt = U^T (x - mu0) */
+    if (c->cfg.prior == NP8O_PRIOR_NIW) {
+        for (int m = 0; m < c->M; ++m) {
+            double sumlog, b00, chi, z1;
+            niw_aux_core(c, i, t, m, &sumlog, &b00, &chi, &z1);
+            ll[m] = niw_aux_loglik(c, ny, sumlog, b00, chi, z1);
+        }
+        return;
+    }
     for (int m = 0; m < c->M; ++m) {
         double v, xpar, chi2;
         aux_core(c, i, t, m, &v, &xpar, &chi2);
@@ -963,9 +1372,13 @@ int np8o_finalize(np8o_ctx *c, const int32_t *delta, const int64_t *req_pos, con
             if (c->cnt[s] != 0) continue;
             int64_t r = ord[2 * q + 1];
             int64_t i = req_i[r];
-            double vv[NP8O_MMAX], mm[NP8O_MMAX * NP8O_DMAX];
-            aux_draws(c, (uint64_t)i, c->t, vv, mm);
-            slot_from_aux(c, s, vv[req_m[r]], mm + (size_t)req_m[r] * D);
+            if (c->cfg.prior == NP8O_PRIOR_NIW) {
+                niw_slot_from_aux(c, s, (uint64_t)i, c->t, req_m[r]);
+            } else {
+                double vv[NP8O_MMAX], mm[NP8O_MMAX * NP8O_DMAX];
+                aux_draws(c, (uint64_t)i, c->t, vv, mm);
+                slot_from_aux(c, s, vv[req_m[r]], mm + (size_t)req_m[r] * D);
+            }
             c->cnt[s] = 1;
             if (owner_hi < 0 || (i >= owner_lo && i < owner_hi)) c->z[i] = s;
             ++q;
@@ -1038,7 +1451,36 @@ static void mh_proposal(const np8o_ctx *c, int s, uint32_t t, int step, double *
     aux_from_normals(c, g[0], g + 1, v, mup);
 }
 
+/* NIW_CONJUGATE: every live slot's (mu, Sigma) drawn from its posterior (niw_draw_impl) given the
+ * statistics about its current mean; draws on stream PARAM (i = slot) at the current epoch.  A slot
+ * whose posterior scale is not numerically positive definite keeps its parameters. */
+static int64_t niw_param_update(np8o_ctx *c, const double *stats) {
+    const int D = c->D, W = D + c->DP;
+    int64_t updated = 0;
+    double anchor[NP8O_DMAX];
+    for (int s = 0; s < c->kcap; ++s) {
+        const int64_t n = c->cnt[s];
+        if (n <= 0) continue;
+        memcpy(anchor, c->slot_mu + (size_t)s * D, sizeof(double) * D);
+        const double *s1 = stats + (size_t)s * W;
+        if (niw_draw_impl(c, (uint64_t)s, c->t, NP8O_STREAM_PARAM, n, s1, s1 + D, anchor, c->slot_mu + (size_t)s * D,
+                          c->slot_P + (size_t)s * c->DP, c->slot_sigma + (size_t)s * D * D, c->slot_c + s) == 0)
+            ++updated;
+    }
+    rebuild_dense(c);
+    return updated;
+}
+
+int np8o_niw_draw(np8o_ctx *c, uint64_t i, uint32_t t, uint32_t stream, int64_t n, const double *stats,
+                  const double *anchor, double *mu, double *Sigma) {
+    if (c->cfg.prior != NP8O_PRIOR_NIW) return -1;
+    static double P[NP8O_DMAX * (NP8O_DMAX + 1) / 2];
+    double cc;
+    return niw_draw_impl(c, i, t, stream, n, stats, stats ? stats + c->D : NULL, anchor, mu, P, Sigma, &cc);
+}
+
 int64_t np8o_param_update(np8o_ctx *c, const double *stats) {
+    if (c->cfg.param_update == NP8O_PARAM_NIW_CONJUGATE) return niw_param_update(c, stats);
     const int D = c->D, DP = c->DP, W = D + DP;
     const int steps = c->cfg.mh_steps > 0 ? c->cfg.mh_steps : 20;
     int64_t accepted = 0;
@@ -1085,7 +1527,7 @@ int64_t np8o_param_update(np8o_ctx *c, const double *stats) {
 }
 
 int np8o_end_sweep(np8o_ctx *c) {
-    if (c->cfg.param_update == NP8O_PARAM_MH_G0 && c->N > 0) {
+    if (c->cfg.param_update != NP8O_PARAM_FROZEN && c->N > 0) {
         double *st = (double *)malloc(sizeof(double) * (size_t)c->kcap * (c->D + c->DP));
         np8o_suffstats(c, st);
         c->mh_accepted += np8o_param_update(c, st);
@@ -1202,6 +1644,16 @@ int np8o_loglik_matrix(np8o_ctx *c, const int64_t *idx, int64_t n, double *out) 
 
 int np8o_aux_params(np8o_ctx *c, int64_t i, double *mu, double *Sigma) {
     const int D = c->D;
+    if (c->cfg.prior == NP8O_PRIOR_NIW) {
+        double dt[NP8O_DMAX], cc;
+        static double P[NP8O_DMAX * (NP8O_DMAX + 1) / 2], Sg[NP8O_DMAX * NP8O_DMAX];
+        whiten(c, c->X + (size_t)i * D, dt);
+        for (int m = 0; m < c->M; ++m) {
+            niw_aux_slot(c, (uint64_t)i, c->t, m, dt, mu + (size_t)m * D, P, Sg, &cc);
+            if (Sigma) memcpy(Sigma + (size_t)m * D * D, Sg, sizeof(double) * D * D);
+        }
+        return 0;
+    }
     double vv[NP8O_MMAX];
     aux_draws(c, (uint64_t)i, c->t, vv, mu);
     if (Sigma)

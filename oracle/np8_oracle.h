@@ -45,11 +45,24 @@ enum {
     NP8O_STREAM_INIT_Z = 4,
     NP8O_STREAM_PARAM = 5,  /* MH proposal normals: i = slot, calls step*Q .. */
     NP8O_STREAM_PARAM_U = 6, /* MH acceptance uniform: i = slot, call = step */
-    NP8O_STREAM_AUX_DIR = 7  /* direction of a picked auxiliary's xi orthogonal to the item */
+    NP8O_STREAM_AUX_DIR = 7, /* direction of a picked auxiliary's xi orthogonal to the item; NIW:
+                                the Bartlett off-diagonals and z_perp direction of a picked auxiliary */
+    NP8O_STREAM_AUX_NIW = 8  /* NIW prior: the auxiliary's Bartlett chi^2 draws, chi^2_{D-1}, z_1 */
 };
 
+/* Base measure G0 (DESIGN.md "Priors").
+ *   REFERENCE: the reference's normal_inverse_wishart_distribution as it actually draws
+ *              (v ~ N(D, nu), Sigma = v^2 L^T L, mu ~ N(mu0, Sigma/kappa)).
+ *   NIW:       a proper Normal-Inverse-Wishart(mu0, kappa0, nu0, Psi0) (build extension for config C5:
+ *              Sigma ~ IW(Psi0, nu0), mu | Sigma ~ N(mu0, Sigma/kappa0)); hyper-parameters come in the
+ *              same fields (mu0, kappa, nu, Lambda = Psi0), nu0 >= D + 1. */
+enum { NP8O_PRIOR_REFERENCE = 0, NP8O_PRIOR_NIW = 1 };
+
 /* Cluster-parameter update after each sweep (np_mcmc.cpp:170). */
-enum { NP8O_PARAM_FROZEN = 0, NP8O_PARAM_MH_G0 = 1 };
+/* NIW_CONJUGATE (NIW prior only): every live cluster's (mu, Sigma) drawn from its exact NIW posterior
+ * given the cluster's items (the Gibbs step the reference's stubbed NIW update would be,
+ * include/statistics/normalinvwishart.h:66-75). */
+enum { NP8O_PARAM_FROZEN = 0, NP8O_PARAM_MH_G0 = 1, NP8O_PARAM_NIW_CONJUGATE = 2 };
 
 /* ---- primitives ---------------------------------------------------------------------------- */
 void np8o_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
@@ -89,6 +102,7 @@ typedef struct {
     int64_t chunk; /* 0 => N (synchronous sweep) */
     int32_t param_update; /* NP8O_PARAM_*: frozen = the reference's effective behaviour */
     int32_t mh_steps;     /* MH steps per cluster and sweep (np_mcmc.cpp:54: 20); 0 -> 20 */
+    int32_t prior;        /* NP8O_PRIOR_* */
 } np8o_config;
 
 np8o_ctx *np8o_create(const np8o_config *cfg);
@@ -138,6 +152,14 @@ int np8o_suffstats(np8o_ctx *c, double *out);
  * returns the number of accepted proposals. */
 int64_t np8o_param_update(np8o_ctx *c, const double *stats);
 int32_t *np8o_z_ptr(np8o_ctx *c);
+
+/* ---- NIW prior primitives (for distribution tests) ------------------------------------------- */
+/* Marsaglia-Tsang Gamma(alpha, 1), alpha >= 1, from Philox calls call0, call0+1, .. of (i, t, stream). */
+double np8o_gamma_mt(uint64_t seed, uint64_t i, uint32_t t, uint32_t stream, uint32_t call0, double alpha);
+/* NIW posterior draw of slot s given the statistics np8o_suffstats writes (n = count); the prior
+ * draw for n = 0.  Outputs mu [D], Sigma [D*D].  Does not change the chain.  0 = ok. */
+int np8o_niw_draw(np8o_ctx *c, uint64_t i, uint32_t t, uint32_t stream, int64_t n, const double *stats,
+                  const double *anchor, double *mu, double *Sigma);
 
 #ifdef __cplusplus
 }

@@ -33,10 +33,12 @@ class _Config(C.Structure):
         ("chunk", C.c_int64),
         ("param_update", C.c_int32),
         ("mh_steps", C.c_int32),
+        ("prior", C.c_int32),
     ]
 
 
-PARAM_UPDATE = {"frozen": 0, "mh_g0": 1}
+PARAM_UPDATE = {"frozen": 0, "mh_g0": 1, "niw_conjugate": 2}
+PRIOR = {"reference": 0, "niw": 1}
 
 
 def build() -> None:
@@ -101,6 +103,9 @@ def lib():
         L.np8o_mh_accepted.argtypes = [vp]
         L.np8o_mh_accepted.restype = i64
         L.np8o_set_threads.argtypes = [C.c_int]
+        L.np8o_gamma_mt.argtypes = [u64, u64, u32, u32, u32, d]
+        L.np8o_gamma_mt.restype = d
+        L.np8o_niw_draw.argtypes = [vp, u64, u32, u32, i64, vp, vp, vp, vp]
         _lib = L
     return _lib
 
@@ -128,6 +133,11 @@ def uniform(seed, i, t, stream, n):
 
 def perm(seed, t, N, p):
     return lib().np8o_perm(seed, t, N, p)
+
+
+def gamma_mt(seed, i, t, stream, call0, alpha):
+    """The specification's Marsaglia-Tsang Gamma(alpha, 1) draw (NIW prior)."""
+    return lib().np8o_gamma_mt(seed, i, t, stream, call0, alpha)
 
 
 def mvn_probability_ref(x, mu, sigma):
@@ -173,9 +183,10 @@ class Chain:
     """The oracle chain (np8o_ctx).  Same constructor parameters as noparama_amd.NealAlgorithm8."""
 
     def __init__(self, D, M=3, alpha=1.0, mu0=None, kappa=1.0 / 500, nu=4.0, Lambda=None, seed=0,
-                 kcap=4096, chunk=0, param_update="frozen", mh_steps=20):
+                 kcap=4096, chunk=0, param_update="frozen", mh_steps=20, prior="reference"):
         cfg = _Config()
         cfg.param_update = PARAM_UPDATE[param_update]
+        cfg.prior = PRIOR[prior]
         cfg.mh_steps = mh_steps
         cfg.D, cfg.M, cfg.alpha = D, M, alpha
         mu0 = np.full(D, 6.0) if mu0 is None else np.asarray(mu0, dtype=np.float64)
@@ -275,6 +286,19 @@ class Chain:
         if r:
             raise ValueError(f"oracle loglik_matrix: {r}")
         return out
+
+    def niw_draw(self, i, t, stream, n=0, stats=None, anchor=None):
+        """NIW posterior draw of n items with statistics (np8o_suffstats layout) about anchor; the
+        prior draw for n = 0.  Returns (mu, Sigma); does not change the chain."""
+        mu = np.zeros(self.D)
+        sg = np.zeros((self.D, self.D))
+        st = None if stats is None else np.ascontiguousarray(stats, dtype=np.float64)
+        an = None if anchor is None else np.ascontiguousarray(anchor, dtype=np.float64)
+        r = lib().np8o_niw_draw(self._h, int(i), int(t), int(stream), int(n), None if st is None else _p(st),
+                                None if an is None else _p(an), _p(mu), _p(sg))
+        if r:
+            raise ValueError(f"oracle niw_draw: {r}")
+        return mu, sg
 
     def aux_params(self, i):
         mu = np.zeros((self.M, self.D))
