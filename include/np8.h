@@ -54,7 +54,17 @@ typedef struct {
     int32_t param_update; /* NP8_PARAM_*: cluster-parameter update after every sweep (np_mcmc.cpp:170) */
     int32_t mh_steps;     /* MH steps per cluster and sweep for NP8_PARAM_MH_G0; 0 -> 20 (np_mcmc.cpp:54) */
     int32_t prior;        /* NP8_PRIOR_*: the base measure G0 */
+    int32_t contraction;  /* NP8_CONTRACT_*: arithmetic of the cluster likelihoods */
 } np8_config;
+
+/* Cluster-likelihood arithmetic (DESIGN.md "Wide path").
+ * F64:      fp64 table form (packed sym(Sigma^{-1})), D in {1,2,3,4,8,16}.
+ * F32_MFMA: D in {32, 64} (config C5): items held in fp32, (x-mu)^T Sigma^{-1} (x-mu) = |A (x-mu)|^2 with
+ *           A = fp32(chol(sym Sigma^{-1})) contracted on the matrix cores (v_mfma_f32_32x32x2_f32),
+ *           |.|^2, the draws and the pick in fp64; bit-exact against oracle/ (NP8O_CONTRACT_F32) and
+ *           within 1e-6 relative of the fp64 formula.  param_update must be FROZEN (for now). */
+#define NP8_CONTRACT_F64 0
+#define NP8_CONTRACT_F32_MFMA 1
 
 /* Base measure G0 (dirichlet_process::sample_base, include/statistics/dirichlet.h:91-93).
  * REFERENCE: normal_inverse_wishart_distribution as the reference actually draws it

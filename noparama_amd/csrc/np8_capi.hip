@@ -47,6 +47,11 @@ struct np8_ctx {
     std::vector<double> U, Uinv;
     double *d_U = nullptr, *d_Uinv = nullptr, *d_Psi0 = nullptr;
     int64_t *pend = nullptr;
+    // wide path (NP8_CONTRACT_F32_MFMA, D in {32, 64}): fp32 items in X/Xs, fp32 MFMA contraction
+    int contraction = NP8_CONTRACT_F64;
+    bool wide = false;
+    float *wA = nullptr, *wfrag = nullptr, *wmu = nullptr, *gtab = nullptr;
+    int32_t *wdirty = nullptr;
     double *acc = nullptr;  // [kcap][D + DP] parameter-update statistics
     // candidate pruning (np8_prune): per-slot radii and per-row candidate lists
     double *r2 = nullptr;
@@ -334,11 +339,13 @@ bool slot_from_sigma(const np8_ctx *c, const double *mu, const double *Sigma, Sl
 }
 
 void free_device(np8_ctx *c) {
-    void *niw_ptrs[] = {c->d_U, c->d_Uinv, c->d_Psi0, c->pend};
+    void *niw_ptrs[] = {c->d_U, c->d_Uinv, c->d_Psi0, c->pend, c->wA, c->wfrag, c->wmu, c->gtab, c->wdirty};
     for (void *p : niw_ptrs)
         if (p) (void)hipFree(p);
     c->d_U = c->d_Uinv = c->d_Psi0 = nullptr;
     c->pend = nullptr;
+    c->wA = c->wfrag = c->wmu = c->gtab = nullptr;
+    c->wdirty = nullptr;
     void *ptrs[] = {c->X,      c->z,       c->z_best, c->slot_mu, c->slot_P,  c->slot_c,  c->slot_sigma,
                     c->cnt,    c->cnt_best, c->mu_best, c->sigma_best, c->cand, c->ctl,    c->hyp,
                     c->d_mu0,  c->d_LT,    c->d_Gp,   c->d_LTL,   c->rec,     c->gath,    c->order,
@@ -519,7 +526,35 @@ FinArgs fin_args(np8_ctx *c, const unsigned char *recs, int world) {
     F.prior = c->prior;
     F.pad2 = 0;
     F.pend = c->pend;
+    F.frame_payload = c->wide ? 1 : 0;
+    F.pad3 = 0;
+    F.hyp = c->hyp;
+    F.wdirty = c->wdirty;
     return F;
+}
+
+WideArgs wide_args(np8_ctx *c) {
+    WideArgs W;
+    W.D = c->D;
+    W.kcap = c->kcap;
+    W.dirty = c->wdirty;
+    W.cnt = c->cnt;
+    W.slot_P = c->slot_P;
+    W.slot_mu = c->slot_mu;
+    W.wA = c->wA;
+    W.wfrag = c->wfrag;
+    W.wmu = c->wmu;
+    W.gtab = c->gtab;
+    W.ctl = c->ctl;
+    return W;
+}
+
+// Wide path: factors, fp32 means and candidate offsets of the slots flagged in wdirty (all = 1).
+int refresh_wide(np8_ctx *c, bool all) {
+    if (!c->wide) return NP8_OK;
+    if (all) HIPC(c, hipMemsetD32Async(reinterpret_cast<int *>(c->wdirty), 1, c->kcap, c->stream));
+    HIPC(c, np8_launch_wide_refresh(wide_args(c), c->stream));
+    return NP8_OK;
 }
 
 NiwArgs niw_args(np8_ctx *c) {
@@ -585,6 +620,9 @@ AssignArgs assign_args(np8_ctx *c, int64_t p0, int64_t p1, const int64_t *order,
     A.collect_r2 = 0;
     A.pad = 0;
     A.r2 = c->r2;
+    A.wfrag = c->wfrag;
+    A.wmu = c->wmu;
+    A.gtab = c->gtab;
     return A;
 }
 
@@ -602,6 +640,8 @@ int launch_finalize(np8_ctx *c, const unsigned char *recs, int world) {
         A.pend = c->pend;
         HIPC(c, np8_launch_niw_aux_slots(A, c->stream));
     }
+    int r = refresh_wide(c, false);  // the slots created here
+    if (r) return r;
     timer_end(c, t);
     if (F.prune) {
         c->lists_valid = true;
@@ -622,7 +662,10 @@ int launch_assign(np8_ctx *c, int64_t p0, int64_t p1, const int64_t *order, bool
     AssignArgs A = assign_args(c, p0, p1, order, use_perm);
     A.collect_r2 = c->collecting ? 1 : 0;
     A.use_lists = (c->collecting && c->lists_valid) ? 1 : 0;
-    HIPC(c, np8_launch_assign(A, c->D, c->M, c->prior, c->stream));
+    if (c->wide)
+        HIPC(c, np8_launch_assign_wide(A, c->D, c->M, c->prior, c->stream));
+    else
+        HIPC(c, np8_launch_assign(A, c->D, c->M, c->prior, c->stream));
     timer_end(c, t);
     if (c->collecting) c->r2_zero = false;
     return NP8_OK;
@@ -666,6 +709,7 @@ int prepare_sorted(np8_ctx *c) {
     S.n = c->n_loc;
     S.kcap = c->kcap;
     S.D = c->D;
+    S.esz = c->wide ? 4 : 8;
     S.force = stale ? 1 : 0;  // otherwise the device re-sorts only if > n/32 items moved
     HIPC(c, np8_launch_resort(S, c->stream));
     c->sorted_valid = true;
@@ -723,7 +767,10 @@ int launch_total_loglik(np8_ctx *c) {
     A.dense_of = c->dense_of;
     A.partial = c->partial;
     A.n_loc = c->n_loc;
-    HIPC(c, np8_launch_loglik(A, c->D, c->stream));
+    if (c->wide)
+        HIPC(c, np8_launch_loglik_wide(A, wide_args(c), c->D, c->stream));
+    else
+        HIPC(c, np8_launch_loglik(A, c->D, c->stream));
     HIPC(c, np8_launch_loglik_reduce(c->partial, (c->n_loc + 255) / 256, &c->ctl->L_local, c->stream));
     if (c->world > 1 && c->comm) {
         NCCLC(c, ncclAllReduce(&c->ctl->L_local, &c->ctl->L, 1, ncclFloat64, ncclSum, c->comm, c->stream));
@@ -785,6 +832,8 @@ int param_update(np8_ctx *c) {
         HIPC(c, np8_launch_niw_post(niw_args(c), c->kcap, c->stream));
     else
         HIPC(c, np8_launch_mh_g0(A, c->stream));
+    int r = refresh_wide(c, true);  // every live slot's parameters changed
+    if (r) return r;
     timer_end(c, t);
     return NP8_OK;
 }
@@ -945,13 +994,17 @@ int np8_create(np8_ctx **out, const np8_config *cfg) {
         delete c;
         return NP8_ERR_ARG;
     }
-    if (!np8_supported(c->D, c->M)) {
+    if (!np8_supported(c->D, c->M) && !(cfg->contraction == NP8_CONTRACT_F32_MFMA && np8_wide_supported(c->D, c->M))) {
         delete c;
         return NP8_ERR_ARG;
     }
     c->DP = packed_size(c->D);
     c->CS = cand_stride(c->D);
-    c->kcap = cfg->kcap > 0 ? cfg->kcap : 2048;
+    c->kcap = cfg->kcap > 0 ? cfg->kcap : (cfg->contraction == NP8_CONTRACT_F32_MFMA ? 512 : 2048);
+    if (cfg->contraction == NP8_CONTRACT_F32_MFMA && c->kcap > 2048) {  // g table: kcap^2 x D fp32
+        delete c;
+        return NP8_ERR_ARG;
+    }
     if (c->kcap > 12288) {  // np8_finalize keeps two int[kcap] arrays in LDS beside 64 KB of request space
         delete c;
         return NP8_ERR_ARG;
@@ -975,6 +1028,13 @@ int np8_create(np8_ctx **out, const np8_config *cfg) {
         return NP8_ERR_ARG;
     }
     c->prior = cfg->prior;
+    c->contraction = cfg->contraction;
+    c->wide = cfg->contraction == NP8_CONTRACT_F32_MFMA;
+    if ((cfg->contraction != NP8_CONTRACT_F64 && !c->wide) ||
+        (c->wide && (!np8_wide_supported(cfg->D, cfg->M) || cfg->param_update != NP8_PARAM_FROZEN))) {
+        delete c;
+        return NP8_ERR_ARG;
+    }
     c->param_update = cfg->param_update;
     c->mh_steps = cfg->mh_steps > 0 ? cfg->mh_steps : 20;
     c->mu0.assign(cfg->mu0, cfg->mu0 + c->D);
@@ -998,7 +1058,7 @@ int np8_create(np8_ctx **out, const np8_config *cfg) {
     }
     c->own_stream = true;
     c->graphs_off = std::getenv("NP8_NO_GRAPH") != nullptr;  // A/B switch for launch-by-launch sweeps
-    c->prune_on = c->kcap <= kPruneMaxKcap && std::getenv("NP8_NO_PRUNE") == nullptr;
+    c->prune_on = !c->wide && c->kcap <= kPruneMaxKcap && std::getenv("NP8_NO_PRUNE") == nullptr;
     c->rec_cap = kReqMax;
     c->rec_bytes = record_bytes(c->kcap, c->rec_cap, c->D);
     int r = 0;
@@ -1036,7 +1096,10 @@ int np8_create(np8_ctx **out, const np8_config *cfg) {
         (r = dalloc(c, &c->d_LTL, (size_t)D * D)) ||
         (c->prior == NP8_PRIOR_NIW &&
          ((r = dalloc(c, &c->d_U, (size_t)D * D)) || (r = dalloc(c, &c->d_Uinv, (size_t)D * D)) ||
-          (r = dalloc(c, &c->d_Psi0, (size_t)D * D)) || (r = dalloc(c, &c->pend, (size_t)4 * kReqMax))))) {
+          (r = dalloc(c, &c->d_Psi0, (size_t)D * D)) || (r = dalloc(c, &c->pend, (size_t)4 * kReqMax)))) ||
+        (c->wide && ((r = dalloc(c, &c->wA, (size_t)kc * D * D)) || (r = dalloc(c, &c->wfrag, (size_t)kc * D * D)) ||
+                     (r = dalloc(c, &c->wmu, (size_t)kc * D)) || (r = dalloc(c, &c->gtab, (size_t)kc * kc * D)) ||
+                     (r = dalloc(c, &c->wdirty, (size_t)kc))))) {
         free_device(c);
         delete c;
         return r;
@@ -1093,21 +1156,30 @@ int np8_set_data(np8_ctx *c, const double *X, int64_t n, int32_t D, int64_t offs
     c->offset = offset;
     c->n_glob = n_global;
     int r = 0;
-    if ((r = dalloc(c, &c->X, (size_t)n * D)) || (r = dalloc(c, &c->z, (size_t)n)) ||
+    const size_t nx = c->wide ? ((size_t)n * D + 1) / 2 : (size_t)n * D;  // wide path: fp32 items
+    if ((r = dalloc(c, &c->X, nx)) || (r = dalloc(c, &c->z, (size_t)n)) ||
         (r = dalloc(c, &c->z_best, (size_t)n)))
         return r;
     for (int b = 0; b < 2; ++b)
-        if ((r = dalloc(c, &c->Xs[b], (size_t)n * D)) || (r = dalloc(c, &c->zs[b], (size_t)n)) ||
+        if ((r = dalloc(c, &c->Xs[b], nx)) || (r = dalloc(c, &c->zs[b], (size_t)n)) ||
             (r = dalloc(c, &c->ids[b], (size_t)n)))
             return r;
     if ((r = dalloc(c, &c->s_hist, (size_t)c->kcap)) || (r = dalloc(c, &c->s_cursor, (size_t)c->kcap)) ||
         (r = dalloc(c, &c->s_off, (size_t)c->kcap)))
         return r;
     c->sorted_valid = false;
-    std::vector<double> soa((size_t)n * D);
-    for (int64_t i = 0; i < n; ++i)
-        for (int a = 0; a < D; ++a) soa[(size_t)a * n + i] = X[(size_t)i * D + a];
-    HIPC(c, hipMemcpyAsync(c->X, soa.data(), sizeof(double) * soa.size(), hipMemcpyHostToDevice, c->stream));
+    if (c->wide) {  // rounded to fp32 (round to nearest even), as oracle/np8_oracle.c set_data does
+        std::vector<float> soa((size_t)n * D);
+        for (int64_t i = 0; i < n; ++i)
+            for (int a = 0; a < D; ++a) soa[(size_t)a * n + i] = (float)X[(size_t)i * D + a];
+        HIPC(c, hipMemcpyAsync(c->X, soa.data(), sizeof(float) * soa.size(), hipMemcpyHostToDevice, c->stream));
+        HIPC(c, hipStreamSynchronize(c->stream));
+    } else {
+        std::vector<double> soa((size_t)n * D);
+        for (int64_t i = 0; i < n; ++i)
+            for (int a = 0; a < D; ++a) soa[(size_t)a * n + i] = X[(size_t)i * D + a];
+        HIPC(c, hipMemcpyAsync(c->X, soa.data(), sizeof(double) * soa.size(), hipMemcpyHostToDevice, c->stream));
+    }
     HIPC(c, hipStreamSynchronize(c->stream));
     c->have_data = true;
     c->have_state = false;
@@ -1141,6 +1213,8 @@ static int set_state_common(np8_ctx *c, const std::vector<SlotHost> &slots, cons
     r = reset_ctl(c);
     if (r) return r;
     r = rebuild(c);
+    if (r) return r;
+    r = refresh_wide(c, true);
     if (r) return r;
     HIPC(c, hipStreamSynchronize(c->stream));
     c->have_state = true;
@@ -1307,6 +1381,8 @@ int np8_sync(np8_ctx *c) {
     if (h.err) {
         int32_t zero = 0;
         HIPC(c, hipMemcpy(&c->ctl->err, &zero, sizeof(zero), hipMemcpyHostToDevice));
+        if (h.err & kErrSigma)
+            return fail(c, NP8_ERR_SIGMA, "a cluster precision is not numerically positive definite (wide path factor)");
         if (h.err & kErrCapacity)
             return fail(c, NP8_ERR_CAPACITY,
                         "new-cluster requests exceeded the free slots or NP8_REQ_MAX in a step; those items kept "
@@ -1364,8 +1440,12 @@ int np8_loglik_matrix(np8_ctx *c, const int64_t *idx, int64_t n, double *out) {
     HIPC(c, hipMalloc(&d_idx, sizeof(int64_t) * n));
     HIPC(c, hipMalloc(&d_out, sizeof(double) * n * w));
     HIPC(c, hipMemcpy(d_idx, idx, sizeof(int64_t) * n, hipMemcpyHostToDevice));
-    HIPC(c, np8_launch_loglik_matrix(assign_args(c, 0, 0, nullptr, false), c->D, c->M, c->prior, d_idx, n, d_out,
-                                     c->stream));
+    if (c->wide)
+        HIPC(c, np8_launch_loglik_matrix_wide(assign_args(c, 0, 0, nullptr, false), wide_args(c), c->D, c->M, c->prior,
+                                              d_idx, n, d_out, c->stream));
+    else
+        HIPC(c, np8_launch_loglik_matrix(assign_args(c, 0, 0, nullptr, false), c->D, c->M, c->prior, d_idx, n, d_out,
+                                         c->stream));
     HIPC(c, hipStreamSynchronize(c->stream));
     HIPC(c, hipMemcpy(out, d_out, sizeof(double) * n * w, hipMemcpyDeviceToHost));
     (void)hipFree(d_idx);

@@ -32,7 +32,7 @@ struct Ctl {
     int32_t pad3;
 };
 
-enum : int32_t { kErrCapacity = 1 };
+enum : int32_t { kErrCapacity = 1, kErrSigma = 2 };
 
 // Exchange record of one rank for one synchronous step:
 //   RecHeader | int32 delta[kcap] | Request req[rec_cap] | double vmu[rec_cap][D+1]
@@ -88,6 +88,19 @@ struct AssignArgs {
     const int32_t *plist, *plen;
     int32_t ls, use_lists, collect_r2, pad;
     double *r2;
+    // wide path (np8_wide.hip): per-slot fp32 factors in MFMA fragment order, fp32 means, and the
+    // candidate offsets g[sj][sk] (stride kcap rows of D)
+    const float *wfrag, *wmu, *gtab;
+};
+
+// Wide-path tables (np8_wide.hip), maintained for the slots flagged in dirty.
+struct WideArgs {
+    int32_t D, kcap;
+    int32_t *dirty;
+    const int32_t *cnt;
+    const double *slot_P, *slot_mu;
+    float *wA, *wfrag, *wmu, *gtab;
+    Ctl *ctl;
 };
 
 // Builds the candidate lists of every live dense row from the radii r2 collected by the sweep
@@ -127,6 +140,11 @@ struct FinArgs {
     // payload in recs, item, m, slot) for np8_niw_aux_slots instead of being written here
     int32_t prior, pad2;
     int64_t *pend;
+    // wide path: request payloads are the item frame (|y0|, y0); slots created here are flagged for
+    // the table refresh
+    int32_t frame_payload, pad3;
+    const double *hyp;
+    int32_t *wdirty;
 };
 
 // NIW prior kernels (np8_niw.hip): posterior / prior draws per slot and picked auxiliaries -> slots.
@@ -210,9 +228,16 @@ struct SortArgs {
     np8::Ctl *ctl;
     int64_t n;
     int32_t kcap, D, force;
+    int32_t esz;  // bytes per element of X: 8 (fp64) or 4 (wide path, fp32)
 };
 
 bool np8_supported(int D, int M);
+bool np8_wide_supported(int D, int M);
+hipError_t np8_launch_assign_wide(const np8::AssignArgs &A, int D, int M, int prior, hipStream_t s);
+hipError_t np8_launch_loglik_matrix_wide(const np8::AssignArgs &A, const np8::WideArgs &W, int D, int M, int prior,
+                                         const int64_t *idx, int64_t n, double *out, hipStream_t s);
+hipError_t np8_launch_loglik_wide(const np8::LoglikArgs &L, const np8::WideArgs &W, int D, hipStream_t s);
+hipError_t np8_launch_wide_refresh(const np8::WideArgs &W, hipStream_t s);
 size_t np8_niw_lds_bytes(int D);
 hipError_t np8_niw_prepare(int D);
 hipError_t np8_launch_niw_post(const np8::NiwArgs &A, int nblocks, hipStream_t s);

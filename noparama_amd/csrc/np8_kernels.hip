@@ -328,7 +328,13 @@ __global__ __launch_bounds__(kSortThreads) void np8_sort_scatter(SortArgs S) {
         const int64_t q = (int64_t)S.off[zp[k]] + lbase[zp[k]] + rk[k];
         zo[q] = zp[k];
         ido[q] = ids ? ids[p] : (int32_t)p;
-        for (int a = 0; a < S.D; ++a) Xo[(int64_t)a * S.n + q] = X[(int64_t)a * S.n + p];
+        if (S.esz == 4) {  // wide path: fp32 items
+            const float *Xf = reinterpret_cast<const float *>(X);
+            float *Xfo = reinterpret_cast<float *>(Xo);
+            for (int a = 0; a < S.D; ++a) Xfo[(int64_t)a * S.n + q] = Xf[(int64_t)a * S.n + p];
+        } else {
+            for (int a = 0; a < S.D; ++a) Xo[(int64_t)a * S.n + q] = X[(int64_t)a * S.n + p];
+        }
     }
     // the last block to finish makes the new layout current (read by the next kernels)
     __syncthreads();
@@ -525,6 +531,22 @@ __device__ void write_new_slot(const FinArgs &F, const double *vmu, int s) {
     if (F.r2) F.r2[s] = __longlong_as_double(0x7FF0000000000000ll);  // radius unknown until a sweep measures it
 }
 
+// Wide path, reference prior: (v, mu) of auxiliary m of item i from the item frame (|y0|, y0) its
+// rank recorded (aux_params of the narrow path, with the frame read back instead of recomputed).
+template <int D>
+__device__ void frame_to_vmu_d(const FinArgs &F, const double *frame, int64_t i, int m, double *vmu) {
+    double y0[D];
+    for (int a = 0; a < D; ++a) y0[a] = frame[1 + a];
+    aux_params<D>(F.hyp, y0, frame[0], F.seed, (uint64_t)i, F.ctl->t_base + F.t, m, vmu);
+}
+
+__device__ void frame_to_vmu(const FinArgs &F, const double *frame, int64_t i, int m, double *vmu) {
+    if (F.D == 32)
+        frame_to_vmu_d<32>(F, frame, i, m, vmu);
+    else
+        frame_to_vmu_d<64>(F, frame, i, m, vmu);
+}
+
 }  // namespace
 
 // One workgroup of 1024 threads.  Dynamic LDS: sort keys int64[kReqMax] | sort idx int[kReqMax] |
@@ -625,9 +647,14 @@ __global__ __launch_bounds__(kFinThreads) void np8_finalize(FinArgs F) {
                 pe[1] = r.i;
                 pe[2] = r.m;
                 pe[3] = s;
+            } else if (F.frame_payload) {  // wide path: (v, mu) from the item frame
+                double vmu[kMaxD + 1];
+                frame_to_vmu(F, request_vmu(F, base, kidx[q]), r.i, r.m, vmu);
+                write_new_slot(F, vmu, s);
             } else {
                 write_new_slot(F, request_vmu(F, base, kidx[q]), s);
             }
+            if (F.wdirty) F.wdirty[s] = 1;
             cnt_s[s] = 1;
             if (r.i >= F.offset && r.i < F.offset + F.n_loc) {
                 F.z[r.i - F.offset] = s;

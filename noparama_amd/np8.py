@@ -62,11 +62,13 @@ class _Config(C.Structure):
         ("param_update", C.c_int32),
         ("mh_steps", C.c_int32),
         ("prior", C.c_int32),
+        ("contraction", C.c_int32),
     ]
 
 
 PARAM_UPDATE = {"frozen": 0, "mh_g0": 1, "niw_conjugate": 2}  # NP8_PARAM_* (include/np8.h)
 PRIOR = {"reference": 0, "niw": 1}  # NP8_PRIOR_*
+CONTRACTION = {"f64": 0, "f32": 1}  # NP8_CONTRACT_*: "f32" = the fp32 MFMA wide path (D in {32, 64})
 
 
 class Stats(C.Structure):
@@ -163,11 +165,14 @@ class NealAlgorithm8:
     intended: `mh_steps` G0-proposal MH steps per cluster after every sweep, np_update_clusters.cpp) or
     "niw_conjugate" (prior="niw": exact posterior draw per cluster, normalinvwishart.h:66-75).
     `prior`: "reference" (the reference's G0 as it draws) or "niw" (a proper Normal-Inverse-Wishart with
-    kappa0 = kappa, nu0 = nu >= D + 1, Psi0 = Lambda).
+    kappa0 = kappa, nu0 = nu >= D + 1, Psi0 = Lambda).  `contraction`: "f64" (D <= 16) or "f32" (D in
+    {32, 64}: items in fp32, cluster likelihoods on the fp32 matrix cores; config C5).
     """
 
-    def __init__(self, D, M=3, alpha=1.0, mu0=None, kappa=1.0 / 500, nu=4.0, Lambda=None, seed=0, kcap=2048,
-                 chunk=0, device=-1, param_update="frozen", mh_steps=20, prior="reference"):
+    def __init__(self, D, M=3, alpha=1.0, mu0=None, kappa=1.0 / 500, nu=4.0, Lambda=None, seed=0, kcap=None,
+                 chunk=0, device=-1, param_update="frozen", mh_steps=20, prior="reference", contraction="f64"):
+        if kcap is None:  # the library's default: 512 on the wide path (kcap^2 x D offset table), else 2048
+            kcap = 512 if contraction == "f32" else 2048
         self.D, self.M, self.kcap = int(D), int(M), int(kcap)
         self._mu0 = np.ascontiguousarray(np.full(D, 6.0) if mu0 is None else mu0, dtype=np.float64)
         self._Lam = np.ascontiguousarray(0.01 * np.eye(D) if Lambda is None else Lambda, dtype=np.float64)
@@ -183,6 +188,9 @@ class NealAlgorithm8:
         if prior not in PRIOR:
             raise ValueError(f"prior must be one of {sorted(PRIOR)}")
         cfg.prior = PRIOR[prior]
+        if contraction not in CONTRACTION:
+            raise ValueError(f"contraction must be one of {sorted(CONTRACTION)}")
+        cfg.contraction = CONTRACTION[contraction]
         h = C.c_void_p()
         r = lib().np8_create(C.byref(h), C.byref(cfg))
         if r:

@@ -380,6 +380,8 @@ struct np8o_ctx {
     /* NIW prior: U = chol(Psi0^{-1}) (lower) and its inverse; UinvT then holds U^T and caux the NIW
      * constant -D/2 log 2pi + sum log U_aa (DESIGN.md "Priors") */
     double U[NP8O_DMAX * NP8O_DMAX], Uinv[NP8O_DMAX * NP8O_DMAX];
+    /* F32 contraction: per slot A = fp32(chol_upper(sym P)) [kcap][D][D] and muf = fp32(mu) [kcap][D] */
+    float *wA, *wmu;
     /* data */
     int64_t N;
     double *X; /* N x D row-major */
@@ -471,6 +473,10 @@ np8o_ctx *np8o_create(const np8o_config *cfg) {
         !(cfg->prior == NP8O_PRIOR_NIW && cfg->param_update == NP8O_PARAM_FROZEN))
         return NULL;
     if (cfg->prior == NP8O_PRIOR_NIW && !(cfg->nu >= cfg->D + 1.0 && cfg->nu < 1e12)) return NULL;
+    if (cfg->contraction != NP8O_CONTRACT_F64 &&
+        !(cfg->contraction == NP8O_CONTRACT_F32 && (cfg->D == 32 || cfg->D == 64) &&
+          cfg->param_update != NP8O_PARAM_MH_G0))
+        return NULL;
     np8o_ctx *c = (np8o_ctx *)calloc(1, sizeof(np8o_ctx));
     c->cfg = *cfg;
     const int D = cfg->D;
@@ -540,6 +546,10 @@ np8o_ctx *np8o_create(const np8o_config *cfg) {
     c->mu_best = (double *)calloc((size_t)K * D, sizeof(double));
     c->sigma_best = (double *)calloc((size_t)K * D * D, sizeof(double));
     c->delta = (int32_t *)calloc((size_t)K, sizeof(int32_t));
+    if (cfg->contraction == NP8O_CONTRACT_F32) {
+        c->wA = (float *)calloc((size_t)K * D * D, sizeof(float));
+        c->wmu = (float *)calloc((size_t)K * D, sizeof(float));
+    }
     c->best_L = -INFINITY;
     return c;
 }
@@ -563,6 +573,8 @@ void np8o_destroy(np8o_ctx *c) {
     free(c->mu_best);
     free(c->sigma_best);
     free(c->delta);
+    free(c->wA);
+    free(c->wmu);
     free(c->rq_pos);
     free(c->rq_i);
     free(c->rq_m);
@@ -581,6 +593,8 @@ int np8o_set_data(np8o_ctx *c, const double *X, int64_t N) {
     c->N = N;
     c->X = (double *)malloc(sizeof(double) * (size_t)(N > 0 ? N : 1) * c->D);
     if (N > 0) memcpy(c->X, X, sizeof(double) * (size_t)N * c->D);
+    if (c->cfg.contraction == NP8O_CONTRACT_F32) /* the items as the device holds them */
+        for (int64_t k = 0; k < N * c->D; ++k) c->X[k] = (double)(float)c->X[k];
     c->z = (int32_t *)calloc((size_t)(N > 0 ? N : 1), sizeof(int32_t));
     c->z_best = (int32_t *)calloc((size_t)(N > 0 ? N : 1), sizeof(int32_t));
     c->rq_pos = (int64_t *)malloc(sizeof(int64_t) * (size_t)(N > 0 ? N : 1));
@@ -1060,9 +1074,62 @@ static void niw_slot_from_aux(np8o_ctx *c, int s, uint64_t i, uint32_t t, int m)
                  c->slot_sigma + (size_t)s * D * D, c->slot_c + s);
 }
 
+/* F32 contraction: A = fp32(R), R = chol_upper(sym Sigma^{-1}) (R^T R = P, fp64, R_jj first, then
+ * row j of R left to right), and muf = fp32(mu).  A pivot <= 0 (not numerically positive definite)
+ * leaves the rest of the row 0 and the pivot at 1e-300 (the device sets an error bit). */
+static void wide_factor(np8o_ctx *c, int s) {
+    const int D = c->D;
+    const double *Pp = c->slot_P + (size_t)s * c->DP;
+    double R[NP8O_DMAX * NP8O_DMAX];
+    memset(R, 0, sizeof(double) * D * D);
+    for (int j = 0; j < D; ++j) {
+        double v = Pp[packed_index(D, j, j)];
+        for (int k = 0; k < j; ++k) v = fma(-R[k * D + j], R[k * D + j], v);
+        const int ok = v > 0.0;
+        R[j * D + j] = ok ? sqrt(v) : 1e-300;
+        for (int i = j + 1; i < D && ok; ++i) {
+            double w = 0.5 * Pp[packed_index(D, j, i)];
+            for (int k = 0; k < j; ++k) w = fma(-R[k * D + j], R[k * D + i], w);
+            R[j * D + i] = w / R[j * D + j];
+        }
+    }
+    float *A = c->wA + (size_t)s * D * D;
+    for (int k = 0; k < D * D; ++k) A[k] = (float)R[k];
+    for (int a = 0; a < D; ++a) c->wmu[(size_t)s * D + a] = (float)c->slot_mu[(size_t)s * D + a];
+}
+
+/* q of item x (fp32 values) for candidate slot sj in the frame of its own slot sk (np8_oracle.h). */
+static double wide_q(const np8o_ctx *c, const double *x, int sk, int sj) {
+    const int D = c->D;
+    const float *A = c->wA + (size_t)sj * D * D, *mj = c->wmu + (size_t)sj * D, *mk = c->wmu + (size_t)sk * D;
+    float xt[NP8O_DMAX], dl[NP8O_DMAX], y[NP8O_DMAX];
+    for (int b = 0; b < D; ++b) {
+        xt[b] = (float)x[b] - mk[b];
+        dl[b] = mj[b] - mk[b];
+    }
+    for (int a = 0; a < D; ++a) {
+        float g = 0.0f;
+        for (int b = 0; b < D; ++b) g = fmaf(A[a * D + b], dl[b], g);
+        float v = -g;
+        for (int b = 0; b < D; ++b) v = fmaf(A[a * D + b], xt[b], v);
+        y[a] = v;
+    }
+    double s[2] = {0.0, 0.0};
+    for (int h = 0; h < 2; ++h)
+        for (int mt = 0; mt < D / 32; ++mt)
+            for (int r = 0; r < 16; ++r) {
+                const double v = (double)y[32 * mt + (r & 3) + 8 * (r >> 2) + 4 * h];
+                s[h] = fma(v, v, s[h]);
+            }
+    return s[0] + s[1];
+}
+
 static void rebuild_dense(np8o_ctx *c) {
     int K = 0;
     const int D = c->D;
+    if (c->cfg.contraction == NP8O_CONTRACT_F32)
+        for (int s = 0; s < c->kcap; ++s)
+            if (c->cnt[s] > 0) wide_factor(c, s);
     for (int s = 0; s < c->kcap; ++s) {
         c->dense_of[s] = -1;
         if (c->cnt[s] > 0) {
@@ -1171,9 +1238,11 @@ static inline double slot_ll(const np8o_ctx *c, const double *x, int s) {
     return fma(-0.5, q, c->slot_c[s]);
 }
 
-/* ll of point x under candidate row j (what the sweep uses): isotropic rows q = iso |d|^2. */
-static inline double cand_ll(const np8o_ctx *c, const double *x, int j) {
+/* ll of point x (own row jo) under candidate row j (what the sweep uses): isotropic rows q = iso |d|^2;
+ * F32 contraction: wide_q in the frame of the own cluster. */
+static inline double cand_ll(const np8o_ctx *c, const double *x, int jo, int j) {
     const int s = c->live[j];
+    if (c->cfg.contraction == NP8O_CONTRACT_F32) return fma(-0.5, wide_q(c, x, c->live[jo], s), c->slot_c[s]);
     if (c->iso[j] > 0.0) {
         const int D = c->D;
         const double *mu = c->slot_mu + (size_t)s * D;
@@ -1246,13 +1315,13 @@ static int32_t choose(const np8o_ctx *c, int64_t i, const double *x, int32_t zi)
     const int K = c->K, M = c->M;
     const int jo = c->dense_of[zi];
     pick_state st;
-    st.T = cand_ll(c, x, jo) + c->logn1[jo];
+    st.T = cand_ll(c, x, jo, jo) + c->logn1[jo];
     st.S = 1.0;
     st.u = np8o_uniform(c->cfg.seed, (uint64_t)i, c->t, NP8O_STREAM_PICK, 0);
     st.pick = jo;
     for (int j = 0; j < K; ++j) {
         if (j == jo) continue;
-        pick_step(&st, cand_ll(c, x, j) + c->logn[j], j);
+        pick_step(&st, cand_ll(c, x, jo, j) + c->logn[j], j);
     }
     double lla[NP8O_MMAX];
     aux_ll(c, x, (uint64_t)i, c->t, lla);
@@ -1391,7 +1460,10 @@ int np8o_finalize(np8o_ctx *c, const int32_t *delta, const int64_t *req_pos, con
 
 double np8o_total_loglik(np8o_ctx *c) {
     double L = 0.0;
-    for (int64_t i = 0; i < c->N; ++i) L += cand_ll(c, c->X + (size_t)i * c->D, c->dense_of[c->z[i]]);
+    for (int64_t i = 0; i < c->N; ++i) {
+        const int jo = c->dense_of[c->z[i]];
+        L += cand_ll(c, c->X + (size_t)i * c->D, jo, jo);
+    }
     return L;
 }
 
@@ -1636,7 +1708,7 @@ int np8o_loglik_matrix(np8o_ctx *c, const int64_t *idx, int64_t n, double *out) 
         int64_t i = idx[r];
         if (i < 0 || i >= c->N) return -3;
         const double *x = c->X + (size_t)i * c->D;
-        for (int j = 0; j < K; ++j) out[r * (K + M) + j] = cand_ll(c, x, j);
+        for (int j = 0; j < K; ++j) out[r * (K + M) + j] = cand_ll(c, x, c->dense_of[c->z[i]], j);
         aux_ll(c, x, (uint64_t)i, c->t, out + r * (K + M) + K);
     }
     return 0;

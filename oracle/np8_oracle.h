@@ -103,7 +103,18 @@ typedef struct {
     int32_t param_update; /* NP8O_PARAM_*: frozen = the reference's effective behaviour */
     int32_t mh_steps;     /* MH steps per cluster and sweep (np_mcmc.cpp:54: 20); 0 -> 20 */
     int32_t prior;        /* NP8O_PRIOR_* */
+    int32_t contraction;  /* NP8O_CONTRACT_*: arithmetic of the cluster likelihoods */
 } np8o_config;
+
+/* Cluster-likelihood arithmetic (DESIGN.md "Wide path").
+ *   F64: fp64 table form, packed sym(Sigma^{-1}) (D <= 16 on the device).
+ *   F32: D in {32, 64}: items rounded to fp32 at set_data; per cluster A = fp32(chol_upper(sym Sigma^{-1}))
+ *        and muf = fp32(mu); for item x with own cluster k and candidate j:
+ *          xt = x - muf_k (fp32), g_jk[a] = fmaf chain_b A_j[a][b] (muf_j[b] - muf_k[b]) from 0,
+ *          y_a = fmaf chain_b A_j[a][b] xt[b] from -g_jk[a]   (= the MFMA contraction, bit for bit),
+ *          q = s_0 + s_1, s_h = fp64 fma chain of y_a^2 over a = 32 mt + (r & 3) + 8 (r >> 2) + 4 h,
+ *              mt outer, r = 0..15 inner (the MFMA accumulator layout), ll = c_j - q/2 (fp64). */
+enum { NP8O_CONTRACT_F64 = 0, NP8O_CONTRACT_F32 = 1 };
 
 np8o_ctx *np8o_create(const np8o_config *cfg);
 void np8o_destroy(np8o_ctx *c);

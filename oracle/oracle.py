@@ -34,11 +34,13 @@ class _Config(C.Structure):
         ("param_update", C.c_int32),
         ("mh_steps", C.c_int32),
         ("prior", C.c_int32),
+        ("contraction", C.c_int32),
     ]
 
 
 PARAM_UPDATE = {"frozen": 0, "mh_g0": 1, "niw_conjugate": 2}
 PRIOR = {"reference": 0, "niw": 1}
+CONTRACTION = {"f64": 0, "f32": 1}
 
 
 def build() -> None:
@@ -183,8 +185,9 @@ class Chain:
     """The oracle chain (np8o_ctx).  Same constructor parameters as noparama_amd.NealAlgorithm8."""
 
     def __init__(self, D, M=3, alpha=1.0, mu0=None, kappa=1.0 / 500, nu=4.0, Lambda=None, seed=0,
-                 kcap=4096, chunk=0, param_update="frozen", mh_steps=20, prior="reference"):
+                 kcap=4096, chunk=0, param_update="frozen", mh_steps=20, prior="reference", contraction="f64"):
         cfg = _Config()
+        cfg.contraction = CONTRACTION[contraction]
         cfg.param_update = PARAM_UPDATE[param_update]
         cfg.prior = PRIOR[prior]
         cfg.mh_steps = mh_steps
