@@ -7,6 +7,11 @@ parameters (the reference's effective behaviour).  One step = one
 N point updates (np8_assign) + cluster bookkeeping (np8_finalize) + the max-likelihood check every
 5th sweep, exactly as np8_sweep runs it.  Inputs are resident in HBM before the timed region.
 
+--config C5 (BASELINE.json configs[4]): N = 1e6, D = 64, 256 components (sd 1,
+means 6 + U[-5,5]^64), a proper Normal-Inverse-Wishart prior (mu0 = 6, kappa0 = 0.01, nu0 = D + 2,
+Psi0 = I, so E[Sigma] = I), items in fp32 and the cluster likelihoods on the fp32 matrix cores
+(np8_assign_wide); roofline against the fp32 MFMA peak.
+
 Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): the N items are
 sharded contiguously over ranks (strong scaling, total N fixed as in config C4); one RCCL
 all-gather of the exchange record per sweep.
@@ -25,6 +30,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector (= FP64 matrix) peak, vendor spec
+FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X FP32 matrix peak (MI355X_MICROARCH.md: 155 measured)
 HBM_PEAK_GBS = 8000.0
 
 
@@ -34,15 +40,37 @@ def parse():
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--n", type=int, default=1_000_000)
-    ap.add_argument("--d", type=int, default=8)
-    ap.add_argument("--k", type=int, default=64)
+    ap.add_argument("--d", type=int, default=None, help="default: 8 (C3) / 64 (C5)")
+    ap.add_argument("--k", type=int, default=None, help="default: 64 (C3) / 256 (C5)")
     ap.add_argument("--seed", type=int, default=20261015)
     ap.add_argument("--config", default="C3", help="config tag for the JSON line (BASELINE.json configs)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget (0 = skip)")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01f.json"))
-    ap.add_argument("--param-update", default="frozen", choices=["frozen", "mh_g0"],
+    ap.add_argument("--traffic-json", default=None,
+                    help="HBM bytes per assign launch from the committed PMC profile of this config")
+    ap.add_argument("--param-update", default="frozen", choices=["frozen", "mh_g0", "niw_conjugate"],
                     help="cluster-parameter update after every sweep (frozen = the reference's effective one)")
-    return ap.parse_args()
+    a = ap.parse_args()
+    c5 = a.config.upper() == "C5"
+    a.d = a.d if a.d is not None else (64 if c5 else 8)
+    a.k = a.k if a.k is not None else (256 if c5 else 64)
+    if a.traffic_json is None:
+        a.traffic_json = os.path.join(ROOT, "profiles", "traffic_r01_c5.json" if c5 else "traffic_r01g.json")
+    return a
+
+
+def workload(args):
+    """Data, warm state and sampler options of the configuration."""
+    from noparama_amd import datasets
+
+    N, D, K = args.n, args.d, args.k
+    if args.config.upper() == "C5":
+        X, z, mu, sig = datasets.mixture(N, D, K, 1.0, 5.0, seed=args.seed)
+        opts = dict(prior="niw", contraction="f32", kcap=512, mu0=np.full(D, 6.0), kappa=0.01, nu=D + 2.0,
+                    Lambda=np.eye(D))
+        return X, z, mu, sig, opts
+    s, r = (0.3, 15.0) if D == 2 else (0.8, 20.0)
+    X, z, mu, sig = datasets.mixture(N, D, K, s, r, seed=args.seed)
+    return X, z, mu, sig, {}
 
 
 def main():
@@ -64,15 +92,15 @@ def main():
     local_rank = local_rank % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local_rank)
 
-    from noparama_amd import NealAlgorithm8, comm_unique_id, datasets
+    from noparama_amd import NealAlgorithm8, comm_unique_id
 
     N, D, K = args.n, args.d, args.k
-    s, r = (0.3, 15.0) if D == 2 else (0.8, 20.0)
-    X, z, mu, sig = datasets.mixture(N, D, K, s, r, seed=args.seed)
+    X, z, mu, sig, opts = workload(args)
+    wide = opts.get("contraction") == "f32"
     lo = (N * rank) // world
     hi = (N * (rank + 1)) // world
 
-    smp = NealAlgorithm8(D, seed=args.seed, device=local_rank, param_update=args.param_update)
+    smp = NealAlgorithm8(D, seed=args.seed, device=local_rank, param_update=args.param_update, **opts)
     transport = "local"
     if world > 1:
         from noparama_amd import NP8Error
@@ -90,7 +118,7 @@ def main():
         transport = "rccl" if all(flags) else "gloo"
         if transport == "gloo":
             smp.close()
-            smp = NealAlgorithm8(D, seed=args.seed, device=local_rank, param_update=args.param_update)
+            smp = NealAlgorithm8(D, seed=args.seed, device=local_rank, param_update=args.param_update, **opts)
             smp.comm_init(None, rank, world)
     smp.set_data(X[lo:hi], offset=lo, n_global=N)
     if transport == "gloo":
@@ -137,8 +165,11 @@ def main():
     ms_assign = (st1["ms_assign"] - st0["ms_assign"]) / max(n_launch, 1)
     Kc = Kfinal + smp.M
     n_items = hi - lo
-    flops = float(n_items) * Kc * (D * D + 2 * D + 4)
+    # N (K+M) (D^2 + 2D + 4) for the fp64 table form; the C5 MFMA form 2D^2 + 4D
+    flops = float(n_items) * Kc * ((2 * D * D + 4 * D) if wide else (D * D + 2 * D + 4))
     achieved = flops / (ms_assign * 1e-3) / 1e12 if ms_assign > 0 else 0.0
+    peak = FP32_MFMA_PEAK_TFLOPS if wide else FP64_PEAK_TFLOPS
+    xbytes = 4 * D if wide else 8 * D
     traffic = None
     if os.path.exists(args.traffic_json):
         try:
@@ -149,9 +180,9 @@ def main():
     if rank == 0:
         cpu = None
         if world == 1 and args.cpu_seconds > 0:
-            cpu = cpu_baseline(X, z, mu, sig, D, args.seed, args.cpu_seconds)
+            cpu = cpu_baseline(X, z, mu, sig, D, args.seed, args.cpu_seconds, opts)
         out = {
-            "metric": "Gibbs sweeps/sec (Neal-8, N=1e6 D=8)",
+            "metric": f"Gibbs sweeps/sec (Neal-8, N={N:.0e} D={D})".replace("+0", ""),
             "value": args.steps / dt,
             "unit": "sweeps/s",
             "n_gpus": world,
@@ -161,12 +192,14 @@ def main():
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
-            "dtype": "f64",
+            "dtype": "f32-mfma contraction, f64 draws" if wide else "f64",
             "data": "synthetic",
             "config": {
                 "workload": f"{args.config}: N={N} D={D} K~{K} M=3 mixture, warm state, "
-                            + ("frozen cluster parameters" if args.param_update == "frozen"
-                               else "mh_g0 cluster-parameter update (20 MH steps/cluster/sweep)"),
+                            + ("NIW prior, fp32 items + fp32 MFMA contraction, " if wide else "")
+                            + {"frozen": "frozen cluster parameters",
+                               "mh_g0": "mh_g0 cluster-parameter update (20 MH steps/cluster/sweep)",
+                               "niw_conjugate": "niw_conjugate cluster-parameter update"}[args.param_update],
                 "N": N, "D": D, "K_final": Kfinal, "parallelism": f"data-sharded x{world}",
                 "exchange": transport,
                 "param_update": args.param_update,
@@ -177,16 +210,17 @@ def main():
             },
             "roofline": {
                 "bound": "mfma",
-                "note": "fp64 compute roof (MI355X fp64 vector = fp64 matrix peak); kernel np8_assign",
+                "note": ("fp32 MFMA roof; kernel np8_assign_wide" if wide else
+                         "fp64 compute roof (MI355X fp64 vector = fp64 matrix peak); kernel np8_assign"),
                 "achieved": achieved,
-                "peak": FP64_PEAK_TFLOPS,
+                "peak": peak,
                 "unit": "TFLOP/s",
-                "frac": achieved / FP64_PEAK_TFLOPS,
+                "frac": achieved / peak,
                 "traffic": traffic,
                 "assign_ms_per_launch": ms_assign,
                 "assign_launches_timed": n_launch,
                 "algorithmic_flops_per_launch": flops,
-                "hbm_frac_algorithmic": (n_items * (8 * D + 8)) / (ms_assign * 1e-3) / 1e9 / HBM_PEAK_GBS
+                "hbm_frac_algorithmic": (n_items * (xbytes + 8)) / (ms_assign * 1e-3) / 1e9 / HBM_PEAK_GBS
                 if ms_assign > 0 else None,
             },
             "cpu_baseline": cpu,
@@ -196,17 +230,20 @@ def main():
         dist.destroy_process_group()
 
 
-def cpu_baseline(X, z, mu, sig, D, seed, budget_s):
+def cpu_baseline(X, z, mu, sig, D, seed, budget_s, opts):
     """The oracle's sequential sweep (chunk = 1: the reference's algorithm, single thread) on the same
     workload and state, timed on a bounded prefix of one sweep, extrapolated to sweeps/s."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O  # test infrastructure: timed as the CPU baseline only
 
-    c = O.Chain(D, seed=seed, chunk=1, kcap=2048)
+    kc = opts.get("kcap", 2048)
+    # the reference computes in fp64: the CPU legs use the fp64 table form (contraction f64)
+    okw = {k: v for k, v in opts.items() if k not in ("kcap", "contraction")}
+    c = O.Chain(D, seed=seed, chunk=1, kcap=kc, **okw)
     c.set_data(X)
     c.set_state(z, mu, sig)
     done, t0 = 0, time.perf_counter()
-    batch = 10000
+    batch = 10000 if D <= 16 else 64
     while time.perf_counter() - t0 < budget_s and done < X.shape[0]:
         c.update_points(np.arange(done, min(done + batch, X.shape[0]), dtype=np.int64))
         done = min(done + batch, X.shape[0])
@@ -224,18 +261,32 @@ def cpu_baseline(X, z, mu, sig, D, seed, budget_s):
     # host cores this process may use (the box's share, not the whole machine)
     threads = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16")))
     O.set_threads(threads)
-    cp = O.Chain(D, seed=seed, chunk=0, kcap=2048)
+    cp = O.Chain(D, seed=seed, chunk=0, kcap=kc, **okw)
     cp.set_data(X)
     cp.set_state(z, mu, sig)
-    n, t0 = 0, time.perf_counter()
-    while time.perf_counter() - t0 < budget_s / 2 or n == 0:
-        cp.sweep(1)
-        n += 1
-    el2 = time.perf_counter() - t0
+    N = X.shape[0]
+    t0 = time.perf_counter()
+    cp.assign_range(0, min(N, 2048), req_cap=4096)  # probe: how many items fit the budget
+    el = time.perf_counter() - t0
+    if el * N / min(N, 2048) < budget_s:  # whole synchronous sweeps
+        n, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < budget_s / 2 or n == 0:
+            cp.sweep(1)
+            n += 1
+        el2 = time.perf_counter() - t0
+        par = {"value": n / el2, "sample": f"{n} full synchronous sweeps (chunk=N, the GPU's algorithm) in "
+                                           f"{el2:.1f}s on {threads} threads"}
+    else:  # a prefix of one synchronous sweep's assignments, extrapolated
+        m = int(min(N, max(2048, 2048 * (budget_s / 2) / max(el, 1e-6))))
+        t0 = time.perf_counter()
+        cp.assign_range(0, m, req_cap=65536)
+        el2 = time.perf_counter() - t0
+        par = {"value": m / el2 / N, "sample": f"{m} of the {N} point updates of one synchronous sweep "
+                                                f"(chunk=N, the GPU's algorithm) in {el2:.1f}s on {threads} "
+                                                f"threads, extrapolated"}
     O.set_threads(1)
-    out["parallel"] = {"value": n / el2, "unit": "sweeps/s", "cores": threads, "kind": "port",
-                       "sample": f"{n} full synchronous sweeps (chunk=N, the GPU's algorithm) in {el2:.1f}s "
-                                 f"on {threads} threads"}
+    out["parallel"] = {"value": par["value"], "unit": "sweeps/s", "cores": threads, "kind": "port",
+                       "sample": par["sample"]}
     return out
 
 

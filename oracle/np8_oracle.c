@@ -382,6 +382,7 @@ struct np8o_ctx {
     double U[NP8O_DMAX * NP8O_DMAX], Uinv[NP8O_DMAX * NP8O_DMAX];
     /* F32 contraction: per slot A = fp32(chol_upper(sym P)) [kcap][D][D] and muf = fp32(mu) [kcap][D] */
     float *wA, *wmu;
+    unsigned char *wdirty; /* slot parameters changed since its factor was computed */
     /* data */
     int64_t N;
     double *X; /* N x D row-major */
@@ -549,6 +550,7 @@ np8o_ctx *np8o_create(const np8o_config *cfg) {
     if (cfg->contraction == NP8O_CONTRACT_F32) {
         c->wA = (float *)calloc((size_t)K * D * D, sizeof(float));
         c->wmu = (float *)calloc((size_t)K * D, sizeof(float));
+        c->wdirty = (unsigned char *)calloc((size_t)K, 1);
     }
     c->best_L = -INFINITY;
     return c;
@@ -575,6 +577,7 @@ void np8o_destroy(np8o_ctx *c) {
     free(c->delta);
     free(c->wA);
     free(c->wmu);
+    free(c->wdirty);
     free(c->rq_pos);
     free(c->rq_i);
     free(c->rq_m);
@@ -617,6 +620,7 @@ static int slot_from_sigma(np8o_ctx *c, int s, const double *mu, const double *S
         for (int b = a; b < D; ++b)
             P[packed_index(D, a, b)] = (a == b) ? inv[a * D + a] : inv[a * D + b] + inv[b * D + a];
     c->slot_c[s] = -0.5 * ((double)D * LOG2PI + log(det));
+    if (c->wdirty) c->wdirty[s] = 1;
     return 0;
 }
 
@@ -642,6 +646,7 @@ static void slot_from_aux(np8o_ctx *c, int s, double v, const double *mu) {
     for (int a = 0; a < D; ++a)
         for (int b = a; b < D; ++b) P[packed_index(D, a, b)] = c->Gp[a * D + b] / v2;
     c->slot_c[s] = fma(-(double)D, np8o_log_pos(fabs(v)), c->caux);
+    if (c->wdirty) c->wdirty[s] = 1;
     double *S = c->slot_sigma + (size_t)s * D * D;
     for (int k = 0; k < D * D; ++k) S[k] = v2 * c->LTL[k];
 }
@@ -1072,6 +1077,7 @@ static void niw_slot_from_aux(np8o_ctx *c, int s, uint64_t i, uint32_t t, int m)
     whiten(c, c->X + (size_t)i * D, dt);
     niw_aux_slot(c, i, t, m, dt, c->slot_mu + (size_t)s * D, c->slot_P + (size_t)s * c->DP,
                  c->slot_sigma + (size_t)s * D * D, c->slot_c + s);
+    if (c->wdirty) c->wdirty[s] = 1;
 }
 
 /* F32 contraction: A = fp32(R), R = chol_upper(sym Sigma^{-1}) (R^T R = P, fp64, R_jj first, then
@@ -1129,7 +1135,10 @@ static void rebuild_dense(np8o_ctx *c) {
     const int D = c->D;
     if (c->cfg.contraction == NP8O_CONTRACT_F32)
         for (int s = 0; s < c->kcap; ++s)
-            if (c->cnt[s] > 0) wide_factor(c, s);
+            if (c->cnt[s] > 0 && c->wdirty[s]) {
+                wide_factor(c, s);
+                c->wdirty[s] = 0;
+            }
     for (int s = 0; s < c->kcap; ++s) {
         c->dense_of[s] = -1;
         if (c->cnt[s] > 0) {
@@ -1194,6 +1203,7 @@ int np8o_init_random(np8o_ctx *c, int32_t K_init) {
     for (int k = 0; k < K_init; ++k) {
         if (cntk[k] > 0) {
             remap[k] = s;
+            if (c->wdirty) c->wdirty[s] = 1;
             if (niw) /* G0 draw k: the NIW posterior of no items, stream INIT_THETA (i = k) */
                 niw_draw_impl(c, (uint64_t)k, 0xFFFFFFFFu, NP8O_STREAM_INIT_THETA, 0, NULL, NULL, NULL,
                               c->slot_mu + (size_t)s * D, c->slot_P + (size_t)s * c->DP,
@@ -1536,8 +1546,10 @@ static int64_t niw_param_update(np8o_ctx *c, const double *stats) {
         memcpy(anchor, c->slot_mu + (size_t)s * D, sizeof(double) * D);
         const double *s1 = stats + (size_t)s * W;
         if (niw_draw_impl(c, (uint64_t)s, c->t, NP8O_STREAM_PARAM, n, s1, s1 + D, anchor, c->slot_mu + (size_t)s * D,
-                          c->slot_P + (size_t)s * c->DP, c->slot_sigma + (size_t)s * D * D, c->slot_c + s) == 0)
+                          c->slot_P + (size_t)s * c->DP, c->slot_sigma + (size_t)s * D * D, c->slot_c + s) == 0) {
             ++updated;
+            if (c->wdirty) c->wdirty[s] = 1;
+        }
     }
     rebuild_dense(c);
     return updated;
