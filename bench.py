@@ -165,8 +165,13 @@ def main():
     ms_assign = (st1["ms_assign"] - st0["ms_assign"]) / max(n_launch, 1)
     Kc = Kfinal + smp.M
     n_items = hi - lo
-    # N (K+M) (D^2 + 2D + 4) for the fp64 table form; the C5 MFMA form 2D^2 + 4D
-    flops = float(n_items) * Kc * ((2 * D * D + 4 * D) if wide else (D * D + 2 * D + 4))
+    # N (K+M) (D^2 + 2D + 4) for the fp64 table form (packed P: D(D+1)/2 multiply-adds
+    # plus d = x - mu and the weight).  Wide path: the triangular factor form y = A (x - mu), |y|^2:
+    # D subtractions + D(D+1)/2 multiply-adds + D squares-and-adds = D^2 + 4D per item and candidate
+    # (SURVEY.md's 2D^2 + 4D counts a full D x D contraction, which the kernel does not perform).
+    flops = float(n_items) * Kc * ((D * D + 4 * D) if wide else (D * D + 2 * D + 4))
+    # what the matrix cores execute on the wide path: 16-row tiles of the triangular A, 2 flops per MAC
+    mfma_flops = float(n_items) * Kc * 2 * sum(16 * (D - 16 * t) for t in range(D // 16)) if wide else None
     achieved = flops / (ms_assign * 1e-3) / 1e12 if ms_assign > 0 else 0.0
     peak = FP32_MFMA_PEAK_TFLOPS if wide else FP64_PEAK_TFLOPS
     xbytes = 4 * D if wide else 8 * D
@@ -218,6 +223,7 @@ def main():
                 "frac": achieved / peak,
                 "traffic": traffic,
                 "assign_ms_per_launch": ms_assign,
+                "mfma_executed_tflops": (mfma_flops / (ms_assign * 1e-3) / 1e12) if (wide and ms_assign > 0) else None,
                 "assign_launches_timed": n_launch,
                 "algorithmic_flops_per_launch": flops,
                 "hbm_frac_algorithmic": (n_items * (xbytes + 8)) / (ms_assign * 1e-3) / 1e9 / HBM_PEAK_GBS

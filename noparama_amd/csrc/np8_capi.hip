@@ -50,7 +50,7 @@ struct np8_ctx {
     // wide path (NP8_CONTRACT_F32_MFMA, D in {32, 64}): fp32 items in X/Xs, fp32 MFMA contraction
     int contraction = NP8_CONTRACT_F64;
     bool wide = false;
-    float *wA = nullptr, *wfrag = nullptr, *wmu = nullptr, *gtab = nullptr;
+    float *wA = nullptr, *wfrag = nullptr, *wmu = nullptr;
     int32_t *wdirty = nullptr;
     double *acc = nullptr;  // [kcap][D + DP] parameter-update statistics
     // candidate pruning (np8_prune): per-slot radii and per-row candidate lists
@@ -339,12 +339,12 @@ bool slot_from_sigma(const np8_ctx *c, const double *mu, const double *Sigma, Sl
 }
 
 void free_device(np8_ctx *c) {
-    void *niw_ptrs[] = {c->d_U, c->d_Uinv, c->d_Psi0, c->pend, c->wA, c->wfrag, c->wmu, c->gtab, c->wdirty};
+    void *niw_ptrs[] = {c->d_U, c->d_Uinv, c->d_Psi0, c->pend, c->wA, c->wfrag, c->wmu, c->wdirty};
     for (void *p : niw_ptrs)
         if (p) (void)hipFree(p);
     c->d_U = c->d_Uinv = c->d_Psi0 = nullptr;
     c->pend = nullptr;
-    c->wA = c->wfrag = c->wmu = c->gtab = nullptr;
+    c->wA = c->wfrag = c->wmu = nullptr;
     c->wdirty = nullptr;
     void *ptrs[] = {c->X,      c->z,       c->z_best, c->slot_mu, c->slot_P,  c->slot_c,  c->slot_sigma,
                     c->cnt,    c->cnt_best, c->mu_best, c->sigma_best, c->cand, c->ctl,    c->hyp,
@@ -544,7 +544,6 @@ WideArgs wide_args(np8_ctx *c) {
     W.wA = c->wA;
     W.wfrag = c->wfrag;
     W.wmu = c->wmu;
-    W.gtab = c->gtab;
     W.ctl = c->ctl;
     return W;
 }
@@ -621,8 +620,6 @@ AssignArgs assign_args(np8_ctx *c, int64_t p0, int64_t p1, const int64_t *order,
     A.pad = 0;
     A.r2 = c->r2;
     A.wfrag = c->wfrag;
-    A.wmu = c->wmu;
-    A.gtab = c->gtab;
     return A;
 }
 
@@ -1001,10 +998,7 @@ int np8_create(np8_ctx **out, const np8_config *cfg) {
     c->DP = packed_size(c->D);
     c->CS = cand_stride(c->D);
     c->kcap = cfg->kcap > 0 ? cfg->kcap : (cfg->contraction == NP8_CONTRACT_F32_MFMA ? 512 : 2048);
-    if (cfg->contraction == NP8_CONTRACT_F32_MFMA && c->kcap > 2048) {  // g table: kcap^2 x D fp32
-        delete c;
-        return NP8_ERR_ARG;
-    }
+
     if (c->kcap > 12288) {  // np8_finalize keeps two int[kcap] arrays in LDS beside 64 KB of request space
         delete c;
         return NP8_ERR_ARG;
@@ -1097,8 +1091,8 @@ int np8_create(np8_ctx **out, const np8_config *cfg) {
         (c->prior == NP8_PRIOR_NIW &&
          ((r = dalloc(c, &c->d_U, (size_t)D * D)) || (r = dalloc(c, &c->d_Uinv, (size_t)D * D)) ||
           (r = dalloc(c, &c->d_Psi0, (size_t)D * D)) || (r = dalloc(c, &c->pend, (size_t)4 * kReqMax)))) ||
-        (c->wide && ((r = dalloc(c, &c->wA, (size_t)kc * D * D)) || (r = dalloc(c, &c->wfrag, (size_t)kc * D * D)) ||
-                     (r = dalloc(c, &c->wmu, (size_t)kc * D)) || (r = dalloc(c, &c->gtab, (size_t)kc * kc * D)) ||
+        (c->wide && ((r = dalloc(c, &c->wA, (size_t)kc * D * D)) ||
+                     (r = dalloc(c, &c->wfrag, (size_t)kc * (D * D + D))) || (r = dalloc(c, &c->wmu, (size_t)kc * D)) ||
                      (r = dalloc(c, &c->wdirty, (size_t)kc))))) {
         free_device(c);
         delete c;

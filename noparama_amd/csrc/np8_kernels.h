@@ -88,9 +88,9 @@ struct AssignArgs {
     const int32_t *plist, *plen;
     int32_t ls, use_lists, collect_r2, pad;
     double *r2;
-    // wide path (np8_wide.hip): per-slot fp32 factors in MFMA fragment order, fp32 means, and the
-    // candidate offsets g[sj][sk] (stride kcap rows of D)
-    const float *wfrag, *wmu, *gtab;
+    // wide path (np8_wide.hip): per slot, D*D fp32 factor entries in MFMA fragment order followed by
+    // the fp32 mean in fragment order (D*D + D floats)
+    const float *wfrag;
 };
 
 // Wide-path tables (np8_wide.hip), maintained for the slots flagged in dirty.
@@ -99,7 +99,7 @@ struct WideArgs {
     int32_t *dirty;
     const int32_t *cnt;
     const double *slot_P, *slot_mu;
-    float *wA, *wfrag, *wmu, *gtab;
+    float *wA, *wfrag, *wmu;  // wA natural [D][D]; wfrag as AssignArgs::wfrag; wmu natural [D]
     Ctl *ctl;
 };
 

@@ -1,21 +1,22 @@
 // np8_wide.hip -- the wide path (DESIGN.md "Wide path"; BASELINE.json config C5): D in {32, 64}, items
-// held in fp32, cluster likelihoods through fp32 MFMA (v_mfma_f32_32x32x2_f32, exact k-ordered fmaf
+// held in fp32, cluster likelihoods through fp32 MFMA (v_mfma_f32_16x16x4_f32, exact k-ordered fmaf
 // chains), everything else (auxiliary draws, the categorical pick, counts) in fp64 as on the narrow path.
 //
 //   np8_wide_rows     per slot whose parameters changed: R = chol_upper(sym Sigma^{-1}) (fp64, in LDS),
-//                     A = fp32(R) in natural and MFMA-fragment order, muf = fp32(mu)
-//   np8_wide_gtab     g[sj][sk] = A_j (muf_j - muf_k) for every live pair touching a changed slot: the
-//                     offset of candidate j in the frame of an item's own cluster k
+//                     A = fp32(R) in natural and MFMA-fragment order, muf = fp32(mu) (natural and
+//                     fragment order)
 //   np8_wide_clean    clears the change flags
-//   np8_assign_wide   one wave per 64 items (one lane per item for the fp64 parts): per candidate row
-//                     the 64 x D x D contraction y = A_j (x - muf_k) - g_jk on the matrix cores,
-//                     q = |y|^2 in fp64, then the same single-uniform reservoir pick as np8_assign
-//                     (src/np_neal_algorithm8.cpp:49-167 for every item of the wave)
+//   np8_assign_wide   4 waves x 64 items per block (one lane per item for the fp64 parts): per candidate
+//                     row the 64 x D x D contraction y = A_j (x - muf_j) on the matrix cores, q = |y|^2 in
+//                     fp64, then the single-uniform reservoir pick of np8_assign (src/np_neal_algorithm8.cpp:
+//                     49-167 for every item); the candidate rows stream through a double-buffered LDS stage
+//                     shared by the block's waves
 //   np8_loglik_wide / np8_loglik_matrix_wide   the same arithmetic on the vector ALU (bit-identical:
 //                     an MFMA is an fmaf chain) for the max-likelihood sum and the parity debug entry
 //
 // The contraction is specified in oracle/np8_oracle.h (NP8O_CONTRACT_F32) so that the CPU oracle
-// reproduces it bit for bit.  A is upper triangular: rows 32..63 skip the k-steps of columns 0..31.
+// reproduces it bit for bit.  A is upper triangular: 16-row tile mt skips the k-steps of columns < 16 mt
+// (2560 instead of 4096 multiply-adds per item and candidate at D = 64).
 #include "np8_kernels.h"
 
 #include <hip/hip_runtime.h>
@@ -28,12 +29,13 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 template <int D>
 struct Wide {
-    static constexpr int MT = D / 32;  // 32-row tiles of A
-    static constexpr int S = D / 2;    // k-steps of the 32x32x2 MFMA
+    static constexpr int MT = D / 16;  // 16-row tiles of A (and 16-item column tiles: 4 per wave)
+    static constexpr int S = D / 4;    // k-steps of the 16x16x4 MFMA
     static constexpr int S4 = S / 4;   // float4 groups of k-steps per lane
     static constexpr int DP = D * (D + 1) / 2;
     static constexpr int CS = (D + DP + 5 + 1) & ~1;
     static constexpr int F = D + DP;
+    static constexpr int ROW = D * D + D;  // floats per staged candidate row: A fragments | muf transposed
 };
 
 __device__ __forceinline__ int64_t wpos_to_local(const AssignArgs &A, int64_t p) {
@@ -94,56 +96,82 @@ __device__ __forceinline__ double wide_aux_ll(const double *__restrict__ hyp, do
     }
 }
 
-// q for the lane's item (item index = lane) against slot sj: the 64 items' x~ fragments are in xb,
-// their own slots in zc (items col and 32 + col).
+// q for the lane's item (item index = lane) against a candidate row staged at `row` (A fragments,
+// then muf transposed: row[D*D + g*S + s] = muf[4 s + g]); xb holds the raw items of the wave's four
+// 16-item column tiles (lane l: item 16 nt + (l & 15), dims 4 s + (l >> 4)).
+// Column tile nt, row tile mt: lane group g = l >> 4 holds rows 16 mt + 4 g + r (r = 0..3) of item
+// 16 nt + (l & 15); s_g = fp32 fmaf chain of y^2 over (mt, r); q = (s_0 + s_1) + (s_2 + s_3) in fp32.
 template <int D>
-__device__ __forceinline__ double wide_pass(const AssignArgs &A, int sj, const float (&xb)[2][D / 2],
-                                            const int32_t (&zc)[2], int lane) {
+__device__ __forceinline__ double wide_pass(const float *row, const float (&xb)[4][D / 4], int lane) {
     using W = Wide<D>;
-    const int h = lane >> 5;
-    f32x16 acc[W::MT][2];
-#pragma unroll
-    for (int nt = 0; nt < 2; ++nt) {
-        const float *gp = A.gtab + ((int64_t)sj * A.kcap + zc[nt]) * D;
-#pragma unroll
-        for (int mt = 0; mt < W::MT; ++mt)
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const float4 v = *reinterpret_cast<const float4 *>(gp + mt * 32 + 8 * g + 4 * h);
-                acc[mt][nt][4 * g + 0] = -v.x;
-                acc[mt][nt][4 * g + 1] = -v.y;
-                acc[mt][nt][4 * g + 2] = -v.z;
-                acc[mt][nt][4 * g + 3] = -v.w;
-            }
-    }
-    const float *wf = A.wfrag + (int64_t)sj * (W::MT * W::S * 64);
+    const int g = lane >> 4;
+    typedef float f32x4 __attribute__((ext_vector_type(4)));
+    f32x4 acc[W::MT][4];
 #pragma unroll
     for (int mt = 0; mt < W::MT; ++mt)
 #pragma unroll
-        for (int s4 = mt * 4; s4 < W::S4; ++s4) {  // A upper triangular: tile mt starts at column 32 mt
-            const float4 a4 = *reinterpret_cast<const float4 *>(wf + ((mt * W::S4 + s4) * 64 + lane) * 4);
+        for (int nt = 0; nt < 4; ++nt) acc[mt][nt] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+    const float *mut = row + D * D + g * W::S;
+#pragma unroll
+    for (int s4 = 0; s4 < W::S4; ++s4) {
+        const float4 m4 = *reinterpret_cast<const float4 *>(mut + 4 * s4);
+        const float mv[4] = {m4.x, m4.y, m4.z, m4.w};
+        float xt[4][4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+            for (int nt = 0; nt < 4; ++nt) xt[e][nt] = xb[nt][4 * s4 + e] - mv[e];
+#pragma unroll
+        for (int mt = 0; mt < W::MT; ++mt) {
+            if (s4 < mt) continue;  // A upper triangular: columns < 16 mt of row tile mt are zero
+            const float4 a4 = *reinterpret_cast<const float4 *>(row + ((mt * W::S4 + s4) * 64 + lane) * 4);
             const float av[4] = {a4.x, a4.y, a4.z, a4.w};
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                acc[mt][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[e], xb[0][s4 * 4 + e], acc[mt][0], 0, 0, 0);
-                acc[mt][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[e], xb[1][s4 * 4 + e], acc[mt][1], 0, 0, 0);
-            }
-        }
-    double sh[2];
+            for (int e = 0; e < 4; ++e)
 #pragma unroll
-    for (int nt = 0; nt < 2; ++nt) {
-        double s = 0.0;
+                for (int nt = 0; nt < 4; ++nt)
+                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[e], xt[e][nt], acc[mt][nt], 0, 0, 0);
+        }
+    }
+    float sp[4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+        float sacc = 0.0f;
 #pragma unroll
         for (int mt = 0; mt < W::MT; ++mt)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const double v = (double)acc[mt][nt][r];
-                s = fma(v, v, s);
-            }
-        sh[nt] = s;
+            for (int r = 0; r < 4; ++r) sacc = fmaf(acc[mt][nt][r], acc[mt][nt][r], sacc);
+        sp[nt] = sacc;
     }
-    const double recv = __shfl_xor(h ? sh[0] : sh[1], 32);
-    return h ? recv + sh[1] : sh[0] + recv;  // s_0 + s_1 for item `lane`
+    // 4 x 4 transpose across the lane groups (lane group g, register k) -> (group k's partial of
+    // column tile g): the half exchanges of permlane32_swap then permlane16_swap
+    const auto r02 = __builtin_amdgcn_permlane32_swap(__float_as_uint(sp[0]), __float_as_uint(sp[2]), false, false);
+    const auto r13 = __builtin_amdgcn_permlane32_swap(__float_as_uint(sp[1]), __float_as_uint(sp[3]), false, false);
+    const auto r01 = __builtin_amdgcn_permlane16_swap(r02[0], r13[0], false, false);
+    const auto r23 = __builtin_amdgcn_permlane16_swap(r02[1], r13[1], false, false);
+    const float q = (__uint_as_float(r01[0]) + __uint_as_float(r01[1])) +
+                    (__uint_as_float(r23[0]) + __uint_as_float(r23[1]));
+    (void)g;
+    return (double)q;
+}
+
+// The block's 256 threads copy one candidate row (A fragments + transposed muf of slot sj) from HBM
+// straight into an LDS stage (global_load_lds_dwordx4, no registers): wave w moves the 1 KB chunks
+// w, w + 4, ... of the A fragments, wave 0's first D/4 lanes the muf part.  The LDS image equals the
+// HBM row (lane-linear 16-byte pieces).  Landed once the block passes a __syncthreads().
+template <int D>
+__device__ __forceinline__ void row_glds(const float *__restrict__ wfrag, int sj, float *dst) {
+    const float4 *src = reinterpret_cast<const float4 *>(wfrag + (int64_t)sj * Wide<D>::ROW);
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+    for (int k = 0; k < D * D / 1024; ++k) {
+        const int c = w + 4 * k;
+        __builtin_amdgcn_global_load_lds((const void *)(src + 64 * c + lane),
+                                         (__attribute__((address_space(3))) void *)(dst + 256 * c), 16, 0, 0);
+    }
+    if (w == 0 && lane < D / 4)
+        __builtin_amdgcn_global_load_lds((const void *)(src + D * D / 4 + lane),
+                                         (__attribute__((address_space(3))) void *)(dst + D * D), 16, 0, 0);
 }
 
 }  // namespace
@@ -178,31 +206,21 @@ __global__ __launch_bounds__(256) void np8_wide_rows(WideArgs W) {
     }
     float *An = W.wA + (int64_t)s * D * D;
     for (int k = threadIdx.x; k < D * D; k += blockDim.x) An[k] = (float)R[k];
-    // fragment order [mt][s4][lane][e]: lane l, k-step s = 4 s4 + e holds A[32 mt + (l & 31)][2 s + (l >> 5)]
-    const int MT = D / 32, S4 = D / 8;
-    float *Af = W.wfrag + (int64_t)s * D * D;
+    // fragment order [mt][s4][lane][e]: lane l, k-step s = 4 s4 + e holds A[16 mt + (l & 15)][4 s + (l >> 4)];
+    // then muf transposed: [g][s] = muf[4 s + g]
+    const int S = D / 4, S4 = D / 16;
+    float *Af = W.wfrag + (int64_t)s * (D * D + D);
     for (int k = threadIdx.x; k < D * D; k += blockDim.x) {
         const int e = k & 3, l = (k >> 2) & 63, rest = k >> 8;
         const int s4 = rest % S4, mt = rest / S4;
-        (void)MT;
         const int ks = 4 * s4 + e;
-        Af[k] = (float)R[(32 * mt + (l & 31)) * D + 2 * ks + (l >> 5)];
+        Af[k] = (float)R[(16 * mt + (l & 15)) * D + 4 * ks + (l >> 4)];
+    }
+    for (int k = threadIdx.x; k < D; k += blockDim.x) {
+        const int g = k / S, st = k - g * S;
+        Af[D * D + k] = (float)W.slot_mu[(int64_t)s * D + 4 * st + g];
     }
     for (int a = threadIdx.x; a < D; a += blockDim.x) W.wmu[(int64_t)s * D + a] = (float)W.slot_mu[(int64_t)s * D + a];
-}
-
-// g[sj][sk][a] = fmaf chain over b >= a of A_j[a][b] (muf_j[b] - muf_k[b]) (zero terms b < a skipped:
-// fmaf(0, x, v) == v).  Grid (kcap, kcap / 4): block (sj, 4 sk), one wave per sk, lane = row a.
-__global__ __launch_bounds__(256) void np8_wide_gtab(WideArgs W) {
-    const int sj = blockIdx.x, sk = blockIdx.y * 4 + (threadIdx.x >> 6);
-    if (sk >= W.kcap || W.cnt[sj] <= 0 || W.cnt[sk] <= 0 || !(W.dirty[sj] || W.dirty[sk])) return;
-    const int D = W.D, a = threadIdx.x & 63;
-    if (a >= D) return;
-    const float *Aj = W.wA + (int64_t)sj * D * D + (int64_t)a * D;
-    const float *mj = W.wmu + (int64_t)sj * D, *mk = W.wmu + (int64_t)sk * D;
-    float g = 0.0f;
-    for (int b = a; b < D; ++b) g = fmaf(Aj[b], mj[b] - mk[b], g);
-    W.gtab[((int64_t)sj * W.kcap + sk) * D + a] = g;
 }
 
 __global__ void np8_wide_clean(WideArgs W) {
@@ -210,13 +228,15 @@ __global__ void np8_wide_clean(WideArgs W) {
 }
 
 // ---- the sweep kernel -----------------------------------------------------------------------------
+// Dynamic LDS: two candidate-row stages of Wide<D>::ROW floats (33 KB at D = 64).
 template <int D, int M, int PRIOR>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void np8_assign_wide(AssignArgs A) {
     using W = Wide<D>;
     constexpr int CS = W::CS, F = W::F;
-    const int lane = threadIdx.x & 63, h = lane >> 5, col = lane & 31;
+    extern __shared__ __attribute__((aligned(16))) float stage[];
+    const int lane = threadIdx.x & 63, g = lane >> 4, col = lane & 15;
     const int64_t pw = A.p0 + (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63);
-    if (pw >= A.p1) return;  // wave-uniform
+    const bool wave_live = pw < A.p1;  // waves past the end still take part in the block's staging
     const int64_t p = pw + lane;
     const bool valid = p < A.p1;
     const bool sorted = A.sorted != 0;
@@ -228,9 +248,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void n
     const double *__restrict__ hyp = A.hyp;
     const uint32_t t = A.ctl->t_base + A.t;
     const int64_t n = A.n_loc;
+    const int K = A.ctl->K;
 
-    // the lane's own item
-    const int64_t pc = valid ? p : pw;
+    // the lane's own item (lanes past the end of the range mirror the wave's first item)
+    const int64_t pc = valid ? p : (wave_live ? pw : A.p0);
     const int64_t il = sorted ? (int64_t)ids[pc] : wpos_to_local(A, pc);
     const int64_t xr = sorted ? pc : il;
     const uint64_t ig = (uint64_t)(A.offset + il);
@@ -239,6 +260,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void n
 
     // auxiliaries first (fp64, per lane): only |U^T (x - mu0)| of the item is needed
     double lwa[M];
+#pragma unroll
+    for (int m = 0; m < M; ++m) lwa[m] = 0.0;
     {
         float xf[D];
 #pragma unroll
@@ -246,35 +269,36 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void n
         const double ny = wide_whiten_norm<D>(hyp, xf);
         const double logam = hyp[D + W::DP + 2];
 #pragma unroll 1
-        for (int m = 0; m < M; ++m) lwa[m] = wide_aux_ll<D, PRIOR>(hyp, ny, A.seed, ig, t, m) + logam;
+        for (int m = 0; m < M; ++m) {
+            const double v = wide_aux_ll<D, PRIOR>(hyp, ny, A.seed, ig, t, m) + logam;
+#pragma unroll
+            for (int k = 0; k < M; ++k) lwa[k] = (k == m) ? v : lwa[k];  // no dynamic register index
+        }
     }
 
-    // MFMA operand B: x~ = x - muf(own) of items col and 32 + col, dims 2 s + h
-    float xb[2][W::S];
-    int32_t zc[2];
+    // MFMA operand B: raw items 16 nt + col of the wave, dims 4 s + g
+    float xb[4][W::S];
 #pragma unroll
-    for (int nt = 0; nt < 2; ++nt) {
-        int64_t pq = pw + nt * 32 + col;
-        if (pq >= A.p1) pq = pw;  // padding column: any valid item, result unused
-        const int64_t iq = sorted ? (int64_t)ids[pq] : wpos_to_local(A, pq);
-        const int64_t xq = sorted ? pq : iq;
-        zc[nt] = sorted ? zs[pq] : A.z[iq];
-        const float *mk = A.wmu + (int64_t)zc[nt] * D;
+    for (int nt = 0; nt < 4; ++nt) {
+        int64_t pq = pw + nt * 16 + col;
+        if (pq >= A.p1) pq = pc;  // padding column: any valid item, result unused
+        const int64_t xq = sorted ? pq : wpos_to_local(A, pq);
 #pragma unroll
-        for (int s = 0; s < W::S; ++s) xb[nt][s] = X[(int64_t)(2 * s + h) * n + xq] - mk[2 * s + h];
+        for (int st = 0; st < W::S; ++st) xb[nt][st] = X[(int64_t)(4 * st + g) * n + xq];
     }
 
-    // own clusters first (weight n_k - 1), one pass per distinct own slot of the wave
+    // own clusters first (weight n_k - 1): one pass per distinct own slot of the wave, rows read
+    // straight from HBM (L2)
     PickState st;
     st.T = 0.0;
     st.S = 1.0;
     st.u = uniform(A.seed, ig, t, kStreamPick, 0);
     st.pick = jo;
-    uint64_t pend = __ballot(valid);
+    uint64_t pend = wave_live ? __ballot(valid) : 0ull;
     while (pend) {
         const int lead = __ffsll((unsigned long long)pend) - 1;
         const int32_t sj = __shfl(zi, lead);
-        const double q = wide_pass<D>(A, sj, xb, zc, lane);
+        const double q = wide_pass<D>(A.wfrag + (int64_t)sj * W::ROW, xb, lane);
         const bool mine = valid && zi == sj;
         if (mine) {
             const double *e = cand + (int64_t)jo * CS;
@@ -282,15 +306,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void n
         }
         pend &= ~__ballot(mine);
     }
-    const int K = A.ctl->K;
-    const int32_t z0 = __builtin_amdgcn_readfirstlane(zi);
-    const bool homog = __ballot(valid && zi != z0) == 0;
+
+    // every other candidate in ascending order, block-uniform: row j + 1 is copied into the other
+    // stage while the MFMAs of row j run; one barrier per row
+    row_glds<D>(A.wfrag, (int)cand[F + kFieldSlot], stage);
+    __syncthreads();
     for (int j = 0; j < K; ++j) {
-        const double *e = cand + (int64_t)j * CS;  // wave-uniform: scalar loads
+        const double *e = cand + (int64_t)j * CS;  // block-uniform: scalar loads
         const int32_t sj = (int32_t)e[F + kFieldSlot];
-        if (homog && sj == z0) continue;
-        const double q = wide_pass<D>(A, sj, xb, zc, lane);
-        if (sj != zi) pick_step(st, fma(-0.5, q, e[F + kFieldC]) + e[F + kFieldLogn], j);
+        if (j + 1 < K) row_glds<D>(A.wfrag, (int)cand[(int64_t)(j + 1) * CS + F + kFieldSlot], stage + ((j + 1) & 1) * W::ROW);
+        const float *row = stage + (j & 1) * W::ROW;
+        if (wave_live) {
+            const double q = wide_pass<D>(row, xb, lane);
+            if (sj != zi) pick_step(st, fma(-0.5, q, e[F + kFieldC]) + e[F + kFieldLogn], j);
+        }
+        __syncthreads();  // the next row has landed (vmcnt(0)); this row's stage may be overwritten
     }
 #pragma unroll
     for (int m = 0; m < M; ++m) pick_step(st, lwa[m], K + m);
@@ -328,30 +358,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void n
 }
 
 // ---- max likelihood and parity ---------------------------------------------------------------------
-// q of item x (fp32 values) against slot sj in the frame of its own slot sk, on the vector ALU:
-// the same fmaf chains (zero terms of the triangular A skipped) and the same fp64 summation order.
+// q of item x (fp32 values) against slot sj on the vector ALU: the same fmaf chains (zero terms of the
+// triangular A skipped) and the same fp64 summation order as wide_pass.
 template <int D>
-__device__ double wide_q_valu(const WideArgs &W, const float *__restrict__ X, int64_t n, int64_t xr, int sk, int sj) {
+__device__ double wide_q_valu(const WideArgs &W, const float *__restrict__ X, int64_t n, int64_t xr, int sj) {
     const float *Aj = W.wA + (int64_t)sj * D * D;
-    const float *mk = W.wmu + (int64_t)sk * D;
-    const float *g = W.gtab + ((int64_t)sj * W.kcap + sk) * D;
+    const float *mj = W.wmu + (int64_t)sj * D;
     float xt[D];
 #pragma unroll
-    for (int b = 0; b < D; ++b) xt[b] = X[(int64_t)b * n + xr] - mk[b];
-    double s[2] = {0.0, 0.0};
+    for (int b = 0; b < D; ++b) xt[b] = X[(int64_t)b * n + xr] - mj[b];
+    float sg[4] = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-    for (int mt = 0; mt < D / 32; ++mt)
+    for (int mt = 0; mt < D / 16; ++mt)
 #pragma unroll
-        for (int r = 0; r < 16; ++r)
+        for (int r = 0; r < 4; ++r)
 #pragma unroll
-            for (int hh = 0; hh < 2; ++hh) {
-                const int a = 32 * mt + (r & 3) + 8 * (r >> 2) + 4 * hh;
-                float v = -g[a];
+            for (int gg = 0; gg < 4; ++gg) {
+                const int a = 16 * mt + 4 * gg + r;
+                float v = 0.0f;
                 for (int b = a; b < D; ++b) v = fmaf(Aj[(int64_t)a * D + b], xt[b], v);
-                const double dv = (double)v;
-                s[hh] = fma(dv, dv, s[hh]);
+                sg[gg] = fmaf(v, v, sg[gg]);
             }
-    return s[0] + s[1];
+    return (double)((sg[0] + sg[1]) + (sg[2] + sg[3]));
 }
 
 template <int D>
@@ -363,7 +391,7 @@ __global__ __launch_bounds__(256) void np8_loglik_wide(LoglikArgs L, WideArgs W)
     if (i < L.n_loc) {
         const int32_t s = L.z[i];
         const double *e = L.cand + (int64_t)L.dense_of[s] * CS;
-        ll = fma(-0.5, wide_q_valu<D>(W, reinterpret_cast<const float *>(L.X), L.n_loc, i, s, s), e[F + kFieldC]);
+        ll = fma(-0.5, wide_q_valu<D>(W, reinterpret_cast<const float *>(L.X), L.n_loc, i, s), e[F + kFieldC]);
     }
     red[threadIdx.x] = ll;
     __syncthreads();
@@ -383,10 +411,9 @@ __global__ __launch_bounds__(64) void np8_loglik_matrix_wide(AssignArgs A, WideA
     const int64_t il = idx[r];
     const float *X = reinterpret_cast<const float *>(A.X);
     const int K = A.ctl->K;
-    const int32_t sk = A.z[il];
     for (int j = 0; j < K; ++j) {
         const double *e = A.cand + (int64_t)j * CS;
-        out[r * (K + M) + j] = fma(-0.5, wide_q_valu<D>(W, X, A.n_loc, il, sk, (int)e[F + kFieldSlot]), e[F + kFieldC]);
+        out[r * (K + M) + j] = fma(-0.5, wide_q_valu<D>(W, X, A.n_loc, il, (int)e[F + kFieldSlot]), e[F + kFieldC]);
     }
     float xf[D];
     for (int a = 0; a < D; ++a) xf[a] = X[(int64_t)a * A.n_loc + il];
@@ -410,13 +437,14 @@ hipError_t np8_launch_assign_wide(const AssignArgs &A, int D, int M, int prior, 
     const int64_t n = A.p1 - A.p0;
     if (n <= 0) return hipSuccess;
     const dim3 grid((unsigned)((n + 255) / 256)), block(256);
-#define X(d, m)                                                                                 \
-    if (D == d && M == m) {                                                                     \
-        if (prior == kPriorNiw)                                                                 \
-            hipLaunchKernelGGL((np8_assign_wide<d, m, kPriorNiw>), grid, block, 0, s, A);       \
-        else                                                                                    \
-            hipLaunchKernelGGL((np8_assign_wide<d, m, kPriorReference>), grid, block, 0, s, A); \
-        return hipGetLastError();                                                               \
+#define X(d, m)                                                                                       \
+    if (D == d && M == m) {                                                                           \
+        const size_t lds = 2 * sizeof(float) * Wide<d>::ROW;                                          \
+        if (prior == kPriorNiw)                                                                       \
+            hipLaunchKernelGGL((np8_assign_wide<d, m, kPriorNiw>), grid, block, lds, s, A);           \
+        else                                                                                          \
+            hipLaunchKernelGGL((np8_assign_wide<d, m, kPriorReference>), grid, block, lds, s, A);     \
+        return hipGetLastError();                                                                     \
     }
     NP8_WIDE_FOR_EACH(X)
 #undef X
@@ -455,7 +483,6 @@ hipError_t np8_launch_loglik_wide(const LoglikArgs &L, const WideArgs &W, int D,
 
 hipError_t np8_launch_wide_refresh(const WideArgs &W, hipStream_t s) {
     hipLaunchKernelGGL(np8_wide_rows, dim3((unsigned)W.kcap), dim3(256), sizeof(double) * W.D * W.D, s, W);
-    hipLaunchKernelGGL(np8_wide_gtab, dim3((unsigned)W.kcap, (unsigned)((W.kcap + 3) / 4)), dim3(256), 0, s, W);
     hipLaunchKernelGGL(np8_wide_clean, dim3((unsigned)((W.kcap + 255) / 256)), dim3(256), 0, s, W);
     return hipGetLastError();
 }

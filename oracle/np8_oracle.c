@@ -1104,30 +1104,28 @@ static void wide_factor(np8o_ctx *c, int s) {
     for (int a = 0; a < D; ++a) c->wmu[(size_t)s * D + a] = (float)c->slot_mu[(size_t)s * D + a];
 }
 
-/* q of item x (fp32 values) for candidate slot sj in the frame of its own slot sk (np8_oracle.h). */
-static double wide_q(const np8o_ctx *c, const double *x, int sk, int sj) {
+/* q of item x (fp32 values) for candidate slot sj (np8_oracle.h NP8O_CONTRACT_F32):
+ * y_a = fmaf chain over b of A[a][b] (x_b - muf_b) from 0 (= v_mfma_f32_16x16x4_f32 in k order),
+ * q = (s_0 + s_1) + (s_2 + s_3) in fp32, s_g = fp32 fmaf chain of y_a^2 over a = 16 mt + 4 g + r (mt outer,
+ * r inner): the lane groups of the 16x16 accumulator layout; ll = c - q/2 in fp64. */
+static double wide_q(const np8o_ctx *c, const double *x, int sj) {
     const int D = c->D;
-    const float *A = c->wA + (size_t)sj * D * D, *mj = c->wmu + (size_t)sj * D, *mk = c->wmu + (size_t)sk * D;
-    float xt[NP8O_DMAX], dl[NP8O_DMAX], y[NP8O_DMAX];
-    for (int b = 0; b < D; ++b) {
-        xt[b] = (float)x[b] - mk[b];
-        dl[b] = mj[b] - mk[b];
-    }
+    const float *A = c->wA + (size_t)sj * D * D, *mj = c->wmu + (size_t)sj * D;
+    float xt[NP8O_DMAX], y[NP8O_DMAX];
+    for (int b = 0; b < D; ++b) xt[b] = (float)x[b] - mj[b];
     for (int a = 0; a < D; ++a) {
-        float g = 0.0f;
-        for (int b = 0; b < D; ++b) g = fmaf(A[a * D + b], dl[b], g);
-        float v = -g;
+        float v = 0.0f;
         for (int b = 0; b < D; ++b) v = fmaf(A[a * D + b], xt[b], v);
         y[a] = v;
     }
-    double s[2] = {0.0, 0.0};
-    for (int h = 0; h < 2; ++h)
-        for (int mt = 0; mt < D / 32; ++mt)
-            for (int r = 0; r < 16; ++r) {
-                const double v = (double)y[32 * mt + (r & 3) + 8 * (r >> 2) + 4 * h];
-                s[h] = fma(v, v, s[h]);
+    float s[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    for (int g = 0; g < 4; ++g)
+        for (int mt = 0; mt < D / 16; ++mt)
+            for (int r = 0; r < 4; ++r) {
+                const float v = y[16 * mt + 4 * g + r];
+                s[g] = fmaf(v, v, s[g]);
             }
-    return s[0] + s[1];
+    return (double)((s[0] + s[1]) + (s[2] + s[3]));
 }
 
 static void rebuild_dense(np8o_ctx *c) {
@@ -1252,7 +1250,8 @@ static inline double slot_ll(const np8o_ctx *c, const double *x, int s) {
  * F32 contraction: wide_q in the frame of the own cluster. */
 static inline double cand_ll(const np8o_ctx *c, const double *x, int jo, int j) {
     const int s = c->live[j];
-    if (c->cfg.contraction == NP8O_CONTRACT_F32) return fma(-0.5, wide_q(c, x, c->live[jo], s), c->slot_c[s]);
+    (void)jo;
+    if (c->cfg.contraction == NP8O_CONTRACT_F32) return fma(-0.5, wide_q(c, x, s), c->slot_c[s]);
     if (c->iso[j] > 0.0) {
         const int D = c->D;
         const double *mu = c->slot_mu + (size_t)s * D;

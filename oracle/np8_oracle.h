@@ -109,11 +109,10 @@ typedef struct {
 /* Cluster-likelihood arithmetic (DESIGN.md "Wide path").
  *   F64: fp64 table form, packed sym(Sigma^{-1}) (D <= 16 on the device).
  *   F32: D in {32, 64}: items rounded to fp32 at set_data; per cluster A = fp32(chol_upper(sym Sigma^{-1}))
- *        and muf = fp32(mu); for item x with own cluster k and candidate j:
- *          xt = x - muf_k (fp32), g_jk[a] = fmaf chain_b A_j[a][b] (muf_j[b] - muf_k[b]) from 0,
- *          y_a = fmaf chain_b A_j[a][b] xt[b] from -g_jk[a]   (= the MFMA contraction, bit for bit),
- *          q = s_0 + s_1, s_h = fp64 fma chain of y_a^2 over a = 32 mt + (r & 3) + 8 (r >> 2) + 4 h,
- *              mt outer, r = 0..15 inner (the MFMA accumulator layout), ll = c_j - q/2 (fp64). */
+ *        and muf = fp32(mu); for item x and candidate j:
+ *          y_a = fmaf chain_b A_j[a][b] (x_b - muf_j[b]) from 0   (= the MFMA contraction, bit for bit),
+ *          q = (s_0 + s_1) + (s_2 + s_3) in fp32, s_g = fp32 fmaf chain of y_a^2 over a = 16 mt + 4 g + r,
+ *              mt outer, r = 0..3 inner (the 16x16 accumulator layout), ll = c_j - q/2 (fp64). */
 enum { NP8O_CONTRACT_F64 = 0, NP8O_CONTRACT_F32 = 1 };
 
 np8o_ctx *np8o_create(const np8o_config *cfg);

@@ -4,7 +4,7 @@ cluster likelihoods contracted on the fp32 matrix cores (v_mfma_f32_32x32x2_f32)
 The oracle restates the contraction (NP8O_CONTRACT_F32: fmaf chains in k order, the accumulator
 layout's fp64 summation order), so labels, counts, parameters and log-likelihoods are bit-exact.  The
 fp32 contraction itself is checked against the fp64 reference formula (multivariatenormal.cpp:106-136)
-within 1e-6 relative (BASELINE.json north star: "a stated tolerance"; SURVEY.md 8(d) proposes 1e-4).
+within 1e-5 relative (BASELINE.json north star: "a stated tolerance"; SURVEY.md 8(d) proposes 1e-4).
 """
 import numpy as np
 import pytest
@@ -14,7 +14,7 @@ from noparama_amd import NealAlgorithm8
 
 pytestmark = pytest.mark.gpu
 
-F32_LL_RTOL = 1e-6
+F32_LL_RTOL = 1e-5
 
 
 def kw_for(D, prior, seed):

@@ -19,7 +19,7 @@ os.makedirs(dst, exist_ok=True)
 shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(dst, f"{tag}_kernel_stats.csv"))
 
 agg = defaultdict(list)
-for sub in ("fetch", "write", "sq"):
+for sub in ("fetch", "write", "sq", "sq2"):
     p = os.path.join(src, sub, "run_counter_collection.csv")
     if not os.path.exists(p):
         continue
@@ -30,6 +30,7 @@ for (k, c), v in agg.items():
     per_kernel[k][c] = {"launches": len(v), "mean": sum(v) / len(v)}
 out = {"source": src, "counters": per_kernel}
 assign = [k for k in per_kernel if "np8_assign" in k]
+assign.sort(key=lambda k: -per_kernel[k].get("SQ_WAVES", {}).get("launches", 0))
 if assign:
     a = per_kernel[assign[0]]
     fetch = a.get("FETCH_SIZE", {}).get("mean")
