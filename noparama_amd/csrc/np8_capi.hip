@@ -823,7 +823,10 @@ int param_update(np8_ctx *c) {
     const size_t nacc = (size_t)c->kcap * (c->D + c->DP);
     // acc is all zero here: allocated zeroed, and np8_mh_g0 clears every row it reads (the only
     // rows np8_suffstats adds to are those of live slots)
-    HIPC(c, np8_launch_suffstats(A, c->stream));
+    if (c->wide)
+        HIPC(c, np8_launch_suffstats_wide(A, c->stream));
+    else
+        HIPC(c, np8_launch_suffstats(A, c->stream));
     if (c->world > 1) NCCLC(c, ncclAllReduce(c->acc, c->acc, nacc, ncclFloat64, ncclSum, c->comm, c->stream));
     if (c->param_update == NP8_PARAM_NIW_CONJUGATE)
         HIPC(c, np8_launch_niw_post(niw_args(c), c->kcap, c->stream));
@@ -1025,7 +1028,7 @@ int np8_create(np8_ctx **out, const np8_config *cfg) {
     c->contraction = cfg->contraction;
     c->wide = cfg->contraction == NP8_CONTRACT_F32_MFMA;
     if ((cfg->contraction != NP8_CONTRACT_F64 && !c->wide) ||
-        (c->wide && (!np8_wide_supported(cfg->D, cfg->M) || cfg->param_update != NP8_PARAM_FROZEN))) {
+        (c->wide && (!np8_wide_supported(cfg->D, cfg->M) || cfg->param_update == NP8_PARAM_MH_G0))) {
         delete c;
         return NP8_ERR_ARG;
     }

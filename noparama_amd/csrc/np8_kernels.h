@@ -252,6 +252,7 @@ hipError_t np8_launch_loglik(const np8::LoglikArgs &A, int D, hipStream_t s);
 hipError_t np8_launch_loglik_reduce(const double *partial, int64_t nb, double *out, hipStream_t s);
 hipError_t np8_launch_snapshot(const np8::SnapArgs &A, hipStream_t s);
 hipError_t np8_launch_suffstats(const np8::ParamArgs &A, hipStream_t s);
+hipError_t np8_launch_suffstats_wide(const np8::ParamArgs &P, hipStream_t s);
 hipError_t np8_launch_mh_g0(const np8::ParamArgs &A, hipStream_t s);
 hipError_t np8_launch_advance_epoch(np8::Ctl *ctl, uint32_t n, hipStream_t s);
 hipError_t np8_launch_prune(const np8::PruneArgs &A, int kcap, hipStream_t s);

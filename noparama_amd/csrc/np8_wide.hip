@@ -422,6 +422,115 @@ __global__ __launch_bounds__(64) void np8_loglik_matrix_wide(AssignArgs A, WideA
     for (int m = 0; m < M; ++m) out[r * (K + M) + K + m] = wide_aux_ll<D, PRIOR>(A.hyp, ny, A.seed, (uint64_t)(A.offset + il), t, m);
 }
 
+// ---- sufficient statistics on the fp64 matrix cores (niw_conjugate on the wide path) -------------------
+// Per slot: s1 = sum d, S = sum d d^T (packed upper) with d = x - mu_slot in fp64 (the layout of
+// np8_suffstats / np8o_suffstats).  One wave walks kSuffChunks chunks of 64 consecutive positions of
+// the (label-sorted) layout; each chunk is staged in LDS (coalesced row reads), then for the slot run
+// being accumulated S += D^T D on v_mfma_f64_16x16x4_f64 (items = the k dimension: 4 per MFMA, 16 steps
+// per chunk, the 16x16 tiles ti <= tj of S), items of other slots masked to 0.  Sums stay in registers
+// while the slot does not change and are committed with fp64 atomics when it does.
+constexpr int kSuffChunks = 8;
+
+template <int D>
+__global__ __launch_bounds__(256) void np8_suffstats_wide(ParamArgs P) {
+    constexpr int T = D / 16, NT = T * (T + 1) / 2, W = D + D * (D + 1) / 2;
+    typedef double f64x4 __attribute__((ext_vector_type(4)));
+    __shared__ float tile[4][D][65];  // per wave: [dim][item] (+1 pad: conflict-free column reads)
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, g = lane >> 4, col = lane & 15;
+    const bool sorted = P.sorted != 0;
+    const int cur = sorted ? P.ctl->cur : 0;
+    const float *__restrict__ X = reinterpret_cast<const float *>(sorted ? (cur ? P.Xs[1] : P.Xs[0]) : P.X);
+    const int32_t *__restrict__ z = sorted ? (cur ? P.zs[1] : P.zs[0]) : P.z;
+    const int64_t n = P.n_loc;
+    const int64_t base = ((int64_t)blockIdx.x * 4 + wv) * (64 * kSuffChunks);
+    if (base >= n) return;  // wave-uniform; no block barrier below
+    float(*tl)[65] = tile[wv];
+    f64x4 acc[NT];
+    double s1[T];
+    int32_t cs = -1;        // slot being accumulated
+    double anc[T];          // its mean, dims 16 t + col
+    auto reset = [&]() {
+#pragma unroll
+        for (int q = 0; q < NT; ++q) acc[q] = (f64x4){0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int t = 0; t < T; ++t) s1[t] = 0.0;
+    };
+    auto commit = [&]() {
+        double *dst = P.acc + (int64_t)cs * W;
+        int q = 0;
+#pragma unroll
+        for (int ti = 0; ti < T; ++ti)
+#pragma unroll
+            for (int tj = ti; tj < T; ++tj, ++q)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int a = 16 * ti + g + 4 * r, b = 16 * tj + col;  // f64 MFMA layout
+                    if (a <= b) unsafeAtomicAdd(dst + D + a * D - (a * (a - 1)) / 2 + (b - a), acc[q][r]);
+                }
+#pragma unroll
+        for (int t = 0; t < T; ++t) {
+            double v = s1[t];
+            v += __shfl_xor(v, 16);
+            v += __shfl_xor(v, 32);
+            if (g == 0) unsafeAtomicAdd(dst + 16 * t + col, v);
+        }
+    };
+    reset();
+    for (int c = 0; c < kSuffChunks; ++c) {
+        const int64_t p0 = base + 64 * c;
+        if (p0 >= n) break;
+        const int64_t p = p0 + lane;
+        const bool valid = p < n;
+        const int32_t zl = valid ? z[p] : -1;
+#pragma unroll 8
+        for (int a = 0; a < D; ++a) tl[a][lane] = valid ? X[(int64_t)a * n + p] : 0.0f;
+        __builtin_amdgcn_wave_barrier();
+        uint64_t pend = __ballot(valid);
+        while (pend) {
+            const int32_t sl = __shfl(zl, __ffsll((unsigned long long)pend) - 1);
+            if (sl != cs) {
+                if (cs >= 0) commit();
+                reset();
+                cs = sl;
+#pragma unroll
+                for (int t = 0; t < T; ++t) anc[t] = P.slot_mu[(int64_t)cs * D + 16 * t + col];
+            }
+            pend &= ~__ballot(zl == sl);
+#pragma unroll
+            for (int st = 0; st < 16; ++st) {
+                const int it = 4 * st + g;  // item of this k-step held by the lane
+                const bool in = __shfl(zl, it) == sl;
+                double dv[T];
+#pragma unroll
+                for (int t = 0; t < T; ++t) dv[t] = in ? (double)tl[16 * t + col][it] - anc[t] : 0.0;
+#pragma unroll
+                for (int t = 0; t < T; ++t) s1[t] += dv[t];
+                int q = 0;
+#pragma unroll
+                for (int ti = 0; ti < T; ++ti)
+#pragma unroll
+                    for (int tj = ti; tj < T; ++tj, ++q)
+                        acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(dv[ti], dv[tj], acc[q], 0, 0, 0);
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+    if (cs >= 0) commit();
+}
+
+hipError_t np8_launch_suffstats_wide(const ParamArgs &P, hipStream_t s) {
+    const int64_t per_block = 4 * 64 * kSuffChunks;
+    const int64_t nb = (P.n_loc + per_block - 1) / per_block;
+    if (nb <= 0) return hipSuccess;
+    if (P.D == 32)
+        hipLaunchKernelGGL((np8_suffstats_wide<32>), dim3((unsigned)nb), dim3(256), 0, s, P);
+    else if (P.D == 64)
+        hipLaunchKernelGGL((np8_suffstats_wide<64>), dim3((unsigned)nb), dim3(256), 0, s, P);
+    else
+        return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+
 // ---- dispatch ----------------------------------------------------------------------------------------
 #define NP8_WIDE_FOR_EACH(X) X(32, 3) X(64, 3)
 

@@ -136,3 +136,27 @@ def test_wide_graph_replay_bit_exact():
     g.sweep(25)
     o.sweep(25)
     assert_state(g, o)
+
+
+@pytest.mark.parametrize("D", [32, 64])
+def test_wide_niw_conjugate_chain(D):
+    """niw_conjugate on the wide path: statistics on the fp64 matrix cores (np8_suffstats_wide), summed
+    in another order than the oracle's item loop, so posterior parameters agree to ~1e-13 relative and
+    labels stay identical over the compared sweeps."""
+    X, z, cent = mixture(D, 4000, 6, 300 + D)
+    kw = kw_for(D, "niw", 17)
+    g = NealAlgorithm8(D, contraction="f32", kcap=256, device=0, param_update="niw_conjugate", **kw)
+    o = O.Chain(D, contraction="f32", kcap=256, param_update="niw_conjugate", **kw)
+    sig = np.repeat(np.eye(D)[None] * 2.0, 6, axis=0)
+    for c in (g, o):
+        c.set_data(X)
+        c.set_state(z.astype(np.int32), cent + 0.3, sig)
+    for _ in range(3):
+        g.sweep(1)
+        o.sweep(1)
+        sa, sb = g.state(), o.state()
+        assert sa["K"] == sb["K"]
+        assert np.array_equal(sa["z"], sb["z"])
+        np.testing.assert_allclose(sa["mu"], sb["mu"], rtol=1e-10, atol=1e-10)
+        np.testing.assert_allclose(sa["sigma"], sb["sigma"], rtol=1e-9, atol=1e-11)
+    np.testing.assert_allclose(g.total_loglik(), o.total_loglik(), rtol=1e-10)
