@@ -135,7 +135,12 @@ def main():
             out = [torch.zeros_like(rec) for _ in range(world)]
             dist.all_gather(out, rec)
             smp.step_merge(np.concatenate([o.numpy() for o in out]), world)
-            smp.end_sweep()
+            if args.param_update == "frozen":
+                smp.end_sweep()
+            else:  # the per-cluster statistics summed over ranks on the host transport
+                st = torch.from_numpy(smp.param_stats_local())
+                dist.all_reduce(st)
+                smp.end_sweep_stats(st.numpy())
 
     sweeps(args.warmup)  # includes np8_sync
     torch.cuda.synchronize()

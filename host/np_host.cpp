@@ -137,6 +137,8 @@ NealAlgorithm8Hip::NealAlgorithm8Hip(uint64_t seed, const np8_prior &prior, int6
     cfg.device = device;
     cfg.param_update = prior.param_update;
     cfg.mh_steps = prior.mh_steps;
+    cfg.prior = prior.prior;
+    cfg.contraction = prior.contraction;
     check(np8_create(&_ctx, &cfg), "np8_create");
 }
 

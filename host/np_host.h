@@ -92,6 +92,8 @@ struct np8_prior {
     int M = 3;                     // np_neal_algorithm8.cpp:33
     int param_update = NP8_PARAM_FROZEN;  // UpdateClusters mode (np_mcmc.cpp:170), include/np8.h
     int mh_steps = 20;                    // np_mcmc.cpp:54
+    int prior = NP8_PRIOR_REFERENCE;      // base measure (include/np8.h NP8_PRIOR_*)
+    int contraction = NP8_CONTRACT_F64;   // NP8_CONTRACT_F32_MFMA: the wide path (D in {32, 64})
 };
 
 class NealAlgorithm8Hip : public UpdateClusterPopulation {

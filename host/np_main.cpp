@@ -27,7 +27,8 @@
 static void usage(const char *p) {
     std::cerr << "usage: " << p << " -d <datafile> -a algorithm8 [-T sweeps=2000] [-c clustering] [-s seed]"
               << " [-C chunk (0 = data-parallel sweep, 1 = sequential)] [-D dims=2] [-w workspace]"
-              << " [-u frozen|mh_g0 (cluster-parameter update)]"
+              << " [-u frozen|mh_g0|niw_conjugate (cluster-parameter update)] [-p reference|niw (base measure)]"
+              << " [-x f64|f32 (cluster likelihoods; f32 = fp32 matrix cores, D in {32, 64})]"
               << " [-n subsample size=200, 0 = all items]; data: 'x_1 .. x_D label' text or [N][D+1] .f64"
               << std::endl;
 }
@@ -84,13 +85,13 @@ static void subsample(dataset_t &ds, std::vector<int> &gt, int n, uint64_t seed)
 }
 
 int main(int argc, char *argv[]) {
-    std::string data, algo, mode = "clustering", ws, upd = "frozen";
+    std::string data, algo, mode = "clustering", ws, upd = "frozen", base = "reference", contr = "f64";
     int T = 2000, D = 2, nsub = 200;
     long long chunk = 0;
     unsigned long long seed = 0;
     bool seeded = false;
     int tok;
-    while ((tok = getopt(argc, argv, "d:a:T:c:s:C:D:w:u:n:h?")) != EOF) {
+    while ((tok = getopt(argc, argv, "d:a:T:c:s:C:D:w:u:n:p:x:h?")) != EOF) {
         switch (tok) {
             case 'd': data = optarg; break;
             case 'a': algo = optarg; break;
@@ -102,6 +103,8 @@ int main(int argc, char *argv[]) {
             case 'w': ws = optarg; break;
             case 'u': upd = optarg; break;
             case 'n': nsub = std::stoi(optarg); break;
+            case 'p': base = optarg; break;
+            case 'x': contr = optarg; break;
             default: usage(argv[0]); return 1;
         }
     }
@@ -135,7 +138,26 @@ int main(int argc, char *argv[]) {
     prior.D = D;
     if (upd == "mh_g0") {
         prior.param_update = NP8_PARAM_MH_G0;
+    } else if (upd == "niw_conjugate") {
+        prior.param_update = NP8_PARAM_NIW_CONJUGATE;
+        base = "niw";
     } else if (upd != "frozen") {
+        usage(argv[0]);
+        return 1;
+    }
+    if (base == "niw") {  // a proper NIW(mu0 = 6, kappa0 = 0.01, nu0 = D + 2, Psi0 = I): E[Sigma] = I
+        prior.prior = NP8_PRIOR_NIW;
+        prior.kappa = 0.01;
+        prior.nu = D + 2.0;
+        prior.Lambda.assign((size_t)D * D, 0.0);
+        for (int a = 0; a < D; ++a) prior.Lambda[(size_t)a * D + a] = 1.0;
+    } else if (base != "reference") {
+        usage(argv[0]);
+        return 1;
+    }
+    if (contr == "f32") {
+        prior.contraction = NP8_CONTRACT_F32_MFMA;
+    } else if (contr != "f64") {
         usage(argv[0]);
         return 1;
     }

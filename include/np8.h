@@ -175,6 +175,15 @@ int64_t np8_record_bytes(np8_ctx *ctx);
 int np8_step_local(np8_ctx *ctx, void *record_out);
 int np8_step_merge(np8_ctx *ctx, const void *records, int32_t world);
 
+/* Host-exchange form of the cluster-parameter update (param_update != FROZEN): after the sweep's
+ * np8_step_merge, np8_param_stats_local writes this rank's per-cluster statistics (np8_param_stats_bytes()
+ * bytes: kcap rows of D + D(D+1)/2 doubles), the caller sums them over ranks (an all-reduce), and
+ * np8_end_sweep_stats(summed) ends the sweep: the parameter update from the global statistics, then
+ * the bookkeeping of np8_end_sweep. */
+int64_t np8_param_stats_bytes(np8_ctx *ctx);
+int np8_param_stats_local(np8_ctx *ctx, double *stats_out);
+int np8_end_sweep_stats(np8_ctx *ctx, const double *summed_stats);
+
 #ifdef __cplusplus
 }
 #endif

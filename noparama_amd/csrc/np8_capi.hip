@@ -780,10 +780,15 @@ int launch_total_loglik(np8_ctx *c) {
 
 // UpdateClusters::update (np_mcmc.cpp:170) in mh_g0 mode: statistics of the current labelling
 // (summed over ranks), then one MH chain per live slot; candidate rows are patched in place.
-int param_update(np8_ctx *c) {
+// stats_mode: 0 = compute the statistics (+ RCCL all-reduce when sharded) and update; 1 = compute the
+// local statistics only (np8_param_stats_local); 2 = update from the statistics already placed in acc
+// (np8_end_sweep_stats).
+int param_update(np8_ctx *c, int stats_mode = 0) {
     if (c->param_update == NP8_PARAM_FROZEN) return NP8_OK;
-    if (c->world > 1 && !c->comm)
-        return fail(c, NP8_ERR_STATE, "the parameter update needs the RCCL transport when sharded");
+    if (stats_mode == 0 && c->world > 1 && !c->comm)
+        return fail(c, NP8_ERR_STATE,
+                    "the parameter update needs the RCCL transport when sharded (or np8_param_stats_local / "
+                    "np8_end_sweep_stats)");
     Timer t;
     timer_begin(c, 3, t);
     ParamArgs A;
@@ -823,11 +828,18 @@ int param_update(np8_ctx *c) {
     const size_t nacc = (size_t)c->kcap * (c->D + c->DP);
     // acc is all zero here: allocated zeroed, and np8_mh_g0 clears every row it reads (the only
     // rows np8_suffstats adds to are those of live slots)
-    if (c->wide)
-        HIPC(c, np8_launch_suffstats_wide(A, c->stream));
-    else
-        HIPC(c, np8_launch_suffstats(A, c->stream));
-    if (c->world > 1) NCCLC(c, ncclAllReduce(c->acc, c->acc, nacc, ncclFloat64, ncclSum, c->comm, c->stream));
+    if (stats_mode != 2) {
+        if (c->wide)
+            HIPC(c, np8_launch_suffstats_wide(A, c->stream));
+        else
+            HIPC(c, np8_launch_suffstats(A, c->stream));
+    }
+    if (stats_mode == 1) {
+        timer_end(c, t);
+        return NP8_OK;
+    }
+    if (stats_mode == 0 && c->world > 1)
+        NCCLC(c, ncclAllReduce(c->acc, c->acc, nacc, ncclFloat64, ncclSum, c->comm, c->stream));
     if (c->param_update == NP8_PARAM_NIW_CONJUGATE)
         HIPC(c, np8_launch_niw_post(niw_args(c), c->kcap, c->stream));
     else
@@ -838,8 +850,8 @@ int param_update(np8_ctx *c) {
     return NP8_OK;
 }
 
-int end_sweep(np8_ctx *c) {
-    int r0 = param_update(c);
+int end_sweep(np8_ctx *c, bool stats_given = false) {
+    int r0 = param_update(c, stats_given ? 2 : 0);
     if (r0) return r0;
     if (c->collecting) {  // after finalize and the parameter update: the table is final
         r0 = launch_prune(c);
@@ -1529,8 +1541,6 @@ static int resize_records(np8_ctx *c, int world) {
 int np8_comm_init(np8_ctx *c, const uint8_t id[128], int32_t rank, int32_t world) {
     if (!c || world < 1 || rank < 0 || rank >= world) return NP8_ERR_ARG;
     if (!id) {  // host-exchange mode: the caller moves records (np8_step_local / np8_step_merge)
-        if (world > 1 && c->param_update != NP8_PARAM_FROZEN)
-            return fail(c, NP8_ERR_ARG, "np8_comm_init: the parameter update needs the RCCL transport");
         c->rank = rank;
         return resize_records(c, world);
     }
@@ -1558,6 +1568,35 @@ int np8_step_local(np8_ctx *c, void *record_out) {
     if (r) return r;
     HIPC(c, hipMemcpyAsync(record_out, c->rec, (size_t)c->rec_bytes, hipMemcpyDeviceToHost, c->stream));
     HIPC(c, hipStreamSynchronize(c->stream));
+    return NP8_OK;
+}
+
+int64_t np8_param_stats_bytes(np8_ctx *c) {
+    return c ? (int64_t)sizeof(double) * c->kcap * (c->D + c->DP) : 0;
+}
+
+int np8_param_stats_local(np8_ctx *c, double *out) {
+    if (!c || !out) return NP8_ERR_ARG;
+    if (!c->have_state) return fail(c, NP8_ERR_STATE, "np8_param_stats_local: no state");
+    if (c->param_update == NP8_PARAM_FROZEN) return fail(c, NP8_ERR_STATE, "np8_param_stats_local: frozen parameters");
+    const size_t nacc = (size_t)c->kcap * (c->D + c->DP);
+    int r = param_update(c, 1);
+    if (r) return r;
+    HIPC(c, hipMemcpyAsync(out, c->acc, sizeof(double) * nacc, hipMemcpyDeviceToHost, c->stream));
+    HIPC(c, hipMemsetAsync(c->acc, 0, sizeof(double) * nacc, c->stream));  // acc stays zero between sweeps
+    HIPC(c, hipStreamSynchronize(c->stream));
+    return NP8_OK;
+}
+
+int np8_end_sweep_stats(np8_ctx *c, const double *summed) {
+    if (!c || !summed) return NP8_ERR_ARG;
+    if (!c->have_state) return fail(c, NP8_ERR_STATE, "np8_end_sweep_stats: no state");
+    if (c->param_update == NP8_PARAM_FROZEN) return fail(c, NP8_ERR_STATE, "np8_end_sweep_stats: frozen parameters");
+    const size_t nacc = (size_t)c->kcap * (c->D + c->DP);
+    HIPC(c, hipMemcpyAsync(c->acc, summed, sizeof(double) * nacc, hipMemcpyHostToDevice, c->stream));
+    int r = end_sweep(c, true);
+    if (r) return r;
+    HIPC(c, hipStreamSynchronize(c->stream));  // the caller's buffer may be reused
     return NP8_OK;
 }
 

@@ -134,6 +134,9 @@ def lib():
         "np8_record_bytes": ([vp], i64),
         "np8_step_local": ([vp, vp], i32),
         "np8_step_merge": ([vp, vp, i32], i32),
+        "np8_param_stats_bytes": ([vp], i64),
+        "np8_param_stats_local": ([vp, vp], i32),
+        "np8_end_sweep_stats": ([vp, vp], i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -310,6 +313,17 @@ class NealAlgorithm8:
     def step_merge(self, records, world):
         records = np.ascontiguousarray(records, dtype=np.uint8)
         self._check(lib().np8_step_merge(self._h, _p(records), int(world)))
+
+    def param_stats_local(self):
+        """This rank's per-cluster statistics (host exchange of the parameter update)."""
+        out = np.zeros(int(lib().np8_param_stats_bytes(self._h)) // 8)
+        self._check(lib().np8_param_stats_local(self._h, _p(out)))
+        return out
+
+    def end_sweep_stats(self, summed):
+        """End the sweep with the statistics summed over ranks (parameter update, bookkeeping)."""
+        summed = np.ascontiguousarray(summed, dtype=np.float64)
+        self._check(lib().np8_end_sweep_stats(self._h, _p(summed)))
 
     # -- reference plug-in interface (np_update_cluster_population.h:35-43) --------------------
     def update(self, cluster_matrix, data_ids):

@@ -87,3 +87,19 @@ def test_binary_data_and_subsample(tmp_path):
     K = int(open(os.path.join(run_dir, "snapshot.txt")).read().split("# rows: ")[1].split()[0])
     n = sum(len(open(os.path.join(run_dir, f"snapshot{k}.txt")).read().splitlines()) for k in range(K))
     assert n == 120
+
+
+@pytest.mark.gpu
+def test_twogaussians_niw_conjugate_end_to_end(tmp_path):
+    """The C++ driver with the NIW prior and the conjugate cluster update (-u niw_conjugate)."""
+    ws = str(tmp_path / "ws") + "/"
+    r = run(["-d", DATA, "-a", "algorithm8", "-T", "300", "-s", "3", "-u", "niw_conjugate", "-w", ws])
+    assert r.returncode == 0, r.stderr + r.stdout
+    score = open(os.path.join(ws, "LATEST", "results.score.txt")).read()
+    vals = dict(ln.split(": ") for ln in score.strip().splitlines())
+    assert float(vals["Purity"]) > 0.95
+
+
+def test_cli_rejects_bad_prior_and_contraction(tmp_path):
+    assert run(["-d", DATA, "-a", "algorithm8", "-p", "dirichlet", "-w", str(tmp_path / "a")]).returncode == 1
+    assert run(["-d", DATA, "-a", "algorithm8", "-x", "bf16", "-w", str(tmp_path / "b")]).returncode == 1
