@@ -1107,7 +1107,8 @@ int np8_create(np8_ctx **out, const np8_config *cfg) {
          ((r = dalloc(c, &c->d_U, (size_t)D * D)) || (r = dalloc(c, &c->d_Uinv, (size_t)D * D)) ||
           (r = dalloc(c, &c->d_Psi0, (size_t)D * D)) || (r = dalloc(c, &c->pend, (size_t)4 * kReqMax)))) ||
         (c->wide && ((r = dalloc(c, &c->wA, (size_t)kc * D * D)) ||
-                     (r = dalloc(c, &c->wfrag, (size_t)kc * (D * D + D))) || (r = dalloc(c, &c->wmu, (size_t)kc * D)) ||
+                     (r = dalloc(c, &c->wfrag, (size_t)kc * (D * D + D))) ||  // >= the compact rows
+                     (r = dalloc(c, &c->wmu, (size_t)kc * D)) ||
                      (r = dalloc(c, &c->wdirty, (size_t)kc))))) {
         free_device(c);
         delete c;

@@ -88,8 +88,8 @@ struct AssignArgs {
     const int32_t *plist, *plen;
     int32_t ls, use_lists, collect_r2, pad;
     double *r2;
-    // wide path (np8_wide.hip): per slot, D*D fp32 factor entries in MFMA fragment order followed by
-    // the fp32 mean in fragment order (D*D + D floats)
+    // wide path (np8_wide.hip): per slot, the used MFMA fragment chunks of the fp32 factor followed by
+    // the fp32 mean in fragment order (Wide<D>::ROW floats)
     const float *wfrag;
 };
 

@@ -35,7 +35,10 @@ struct Wide {
     static constexpr int DP = D * (D + 1) / 2;
     static constexpr int CS = (D + DP + 5 + 1) & ~1;
     static constexpr int F = D + DP;
-    static constexpr int ROW = D * D + D;  // floats per staged candidate row: A fragments | muf transposed
+    // used fragment chunks (1 KB = one float4 per lane): (mt, s4) with s4 >= mt, compact order
+    static constexpr int NCH = MT * (MT + 1) / 2;
+    static constexpr int ROW = NCH * 256 + D;  // floats per candidate row: chunks | muf transposed
+    static __host__ __device__ constexpr int chunk(int mt, int s4) { return mt * S4 - (mt * (mt - 1)) / 2 + (s4 - mt); }
 };
 
 __device__ __forceinline__ int64_t wpos_to_local(const AssignArgs &A, int64_t p) {
@@ -111,7 +114,7 @@ __device__ __forceinline__ double wide_pass(const float *row, const float (&xb)[
     for (int mt = 0; mt < W::MT; ++mt)
 #pragma unroll
         for (int nt = 0; nt < 4; ++nt) acc[mt][nt] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
-    const float *mut = row + D * D + g * W::S;
+    const float *mut = row + W::NCH * 256 + g * W::S;
 #pragma unroll
     for (int s4 = 0; s4 < W::S4; ++s4) {
         const float4 m4 = *reinterpret_cast<const float4 *>(mut + 4 * s4);
@@ -124,7 +127,7 @@ __device__ __forceinline__ double wide_pass(const float *row, const float (&xb)[
 #pragma unroll
         for (int mt = 0; mt < W::MT; ++mt) {
             if (s4 < mt) continue;  // A upper triangular: columns < 16 mt of row tile mt are zero
-            const float4 a4 = *reinterpret_cast<const float4 *>(row + ((mt * W::S4 + s4) * 64 + lane) * 4);
+            const float4 a4 = *reinterpret_cast<const float4 *>(row + (W::chunk(mt, s4) * 64 + lane) * 4);
             const float av[4] = {a4.x, a4.y, a4.z, a4.w};
 #pragma unroll
             for (int e = 0; e < 4; ++e)
@@ -161,17 +164,19 @@ __device__ __forceinline__ double wide_pass(const float *row, const float (&xb)[
 // HBM row (lane-linear 16-byte pieces).  Landed once the block passes a __syncthreads().
 template <int D>
 __device__ __forceinline__ void row_glds(const float *__restrict__ wfrag, int sj, float *dst) {
+    constexpr int NCH = Wide<D>::NCH;
     const float4 *src = reinterpret_cast<const float4 *>(wfrag + (int64_t)sj * Wide<D>::ROW);
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
 #pragma unroll
-    for (int k = 0; k < D * D / 1024; ++k) {
-        const int c = w + 4 * k;
-        __builtin_amdgcn_global_load_lds((const void *)(src + 64 * c + lane),
-                                         (__attribute__((address_space(3))) void *)(dst + 256 * c), 16, 0, 0);
+    for (int k = 0; k < (NCH + 3) / 4; ++k) {
+        const int c = w + 4 * k;  // wave-uniform
+        if (c < NCH)
+            __builtin_amdgcn_global_load_lds((const void *)(src + 64 * c + lane),
+                                             (__attribute__((address_space(3))) void *)(dst + 256 * c), 16, 0, 0);
     }
-    if (w == 0 && lane < D / 4)
-        __builtin_amdgcn_global_load_lds((const void *)(src + D * D / 4 + lane),
-                                         (__attribute__((address_space(3))) void *)(dst + D * D), 16, 0, 0);
+    if (w == 3 && lane < D / 4)  // the wave with the fewest chunks
+        __builtin_amdgcn_global_load_lds((const void *)(src + 64 * NCH + lane),
+                                         (__attribute__((address_space(3))) void *)(dst + 256 * NCH), 16, 0, 0);
 }
 
 }  // namespace
@@ -206,19 +211,22 @@ __global__ __launch_bounds__(256) void np8_wide_rows(WideArgs W) {
     }
     float *An = W.wA + (int64_t)s * D * D;
     for (int k = threadIdx.x; k < D * D; k += blockDim.x) An[k] = (float)R[k];
-    // fragment order [mt][s4][lane][e]: lane l, k-step s = 4 s4 + e holds A[16 mt + (l & 15)][4 s + (l >> 4)];
-    // then muf transposed: [g][s] = muf[4 s + g]
-    const int S = D / 4, S4 = D / 16;
-    float *Af = W.wfrag + (int64_t)s * (D * D + D);
-    for (int k = threadIdx.x; k < D * D; k += blockDim.x) {
-        const int e = k & 3, l = (k >> 2) & 63, rest = k >> 8;
-        const int s4 = rest % S4, mt = rest / S4;
+    // fragment chunks (mt, s4), s4 >= mt, in compact order; in chunk c = chunk(mt, s4) lane l's float4
+    // element e (k-step ks = 4 s4 + e) holds A[16 mt + (l & 15)][4 ks + (l >> 4)]; then muf transposed:
+    // [g][s] = muf[4 s + g]
+    const int S = D / 4, S4 = D / 16, MT = D / 16, NCH = MT * (MT + 1) / 2;
+    float *Af = W.wfrag + (int64_t)s * (NCH * 256 + D);
+    for (int k = threadIdx.x; k < NCH * 256; k += blockDim.x) {
+        const int e = k & 3, l = (k >> 2) & 63, c = k >> 8;
+        int mt = 0;
+        while (c >= (mt + 1) * S4 - (mt * (mt + 1)) / 2) ++mt;  // chunk -> (mt, s4)
+        const int s4 = mt + (c - (mt * S4 - (mt * (mt - 1)) / 2));
         const int ks = 4 * s4 + e;
         Af[k] = (float)R[(16 * mt + (l & 15)) * D + 4 * ks + (l >> 4)];
     }
     for (int k = threadIdx.x; k < D; k += blockDim.x) {
         const int g = k / S, st = k - g * S;
-        Af[D * D + k] = (float)W.slot_mu[(int64_t)s * D + 4 * st + g];
+        Af[NCH * 256 + k] = (float)W.slot_mu[(int64_t)s * D + 4 * st + g];
     }
     for (int a = threadIdx.x; a < D; a += blockDim.x) W.wmu[(int64_t)s * D + a] = (float)W.slot_mu[(int64_t)s * D + a];
 }
