@@ -355,9 +355,10 @@ NP8_HD double niw_aux_loglik(double nd, double sumlog, double b00, double chi, d
 
 // Log-weight standing for weight 0 (a singleton's own cluster): finite, so no -inf arithmetic.
 constexpr double kZeroLogWeight = -1.0e300;
-// Candidates with log-weight <= running max - kSkip have exp() == 0 exactly and leave the draw's
-// state unchanged (DESIGN.md "Pick").
-constexpr double kSkip = 800.0;
+// Candidates with log-weight <= running max - kSkip are skipped (DESIGN.md "Pick"): a relative weight
+// below e^-80 (1.8e-35) that no 53-bit uniform can resolve -- the reference's random_weighted_pick
+// (dim1algebra.hpp:2078-2104) draws one double u; skipping saves the exp and the division.
+constexpr double kSkip = 80.0;
 
 NP8_HD double uniform(uint64_t seed, uint64_t i, uint32_t t, uint32_t stream, uint32_t n) {
     uint32_t o[4];

@@ -173,7 +173,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void n
     const int32_t zi = sorted ? zs[p] : A.z[il];
 
     // The item's own cluster enters the draw first (weight n_k - 1): its log-weight is a lower bound
-    // of the final maximum, so every later candidate more than kSkip below it is skipped exactly.
+    // of the final maximum, so every later candidate more than kSkip below it is skipped.
     const int32_t jo = A.dense_of[zi];
     PickState st;
     {

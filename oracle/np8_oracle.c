@@ -1068,7 +1068,7 @@ static int niw_draw_impl(const np8o_ctx *c, uint64_t i, uint32_t t, uint32_t str
 /* Candidate table: live slots in ascending order, log n_k, log(n_k - 1) (weight 0 as the finite
  * NP8O_ZERO_LW), and the isotropy flag (off-diagonals of P' exactly 0, one common diagonal). */
 #define NP8O_ZERO_LW (-1.0e300)
-#define NP8O_SKIP 800.0
+#define NP8O_SKIP 80.0 /* skip rule: relative weight below e^-80 (np8_device.h kSkip) */
 
 /* Slot s from auxiliary m of item i (NIW prior). */
 static void niw_slot_from_aux(np8o_ctx *c, int s, uint64_t i, uint32_t t, int m) {
@@ -1289,8 +1289,8 @@ static void aux_ll(const np8o_ctx *c, const double *x, uint64_t i, uint32_t t, d
  * Equal in distribution to dim1algebra.hpp:2078-2104 (inverse CDF over the linear weights) but one
  * pass: state (T, S, u) with S = sum of exp(lw_j - T) so far and u ~ U(0,1) independent of the
  * current pick; candidate j replaces the pick with probability w_j / S_new and u is renormalised
- * into the chosen sub-interval.  A candidate with lw <= T - 800 has exp(lw - T) == 0 in double and
- * leaves the state unchanged. */
+ * into the chosen sub-interval.  A candidate with lw <= T - 80 (relative weight below 1.8e-35, beyond
+ * the resolution of the reference's one double uniform) is skipped. */
 typedef struct {
     double T, S, u;
     int32_t pick;

@@ -1,6 +1,6 @@
 """The candidate-pruning bound of np8_prune (DESIGN.md "Pruning"), checked on oracle states: every
 row the bound leaves out of cluster k0's list must be skipped by pick_step for every item of k0
-(log-weight at least 800 below the item's own).  CPU only; the GPU parity tests then check that the
+(log-weight at least kSkip = 80 below the item's own).  CPU only; the GPU parity tests then check that the
 pruned sweep equals the oracle's unpruned one bit for bit."""
 import numpy as np
 import pytest
@@ -8,7 +8,7 @@ import pytest
 import oracle as O
 from noparama_amd import datasets
 
-SKIP, MARGIN = 800.0, 2.0
+SKIP, MARGIN = 80.0, 2.0
 
 
 def _violations(chain, X, D):
