@@ -764,9 +764,11 @@ int launch_total_loglik(np8_ctx *c) {
     A.dense_of = c->dense_of;
     A.partial = c->partial;
     A.n_loc = c->n_loc;
-    if (c->wide)
-        HIPC(c, np8_launch_loglik_wide(A, wide_args(c), c->D, c->stream));
-    else
+    if (c->wide) {  // the own-cluster MFMA passes, on the label-sorted layout after a synchronous sweep
+        AssignArgs W = assign_args(c, 0, c->n_loc, nullptr, false);
+        W.sorted = (c->use_sorted && c->sorted_valid) ? 1 : 0;
+        HIPC(c, np8_launch_loglik_wide_mfma(W, c->D, c->partial, c->stream));
+    } else
         HIPC(c, np8_launch_loglik(A, c->D, c->stream));
     HIPC(c, np8_launch_loglik_reduce(c->partial, (c->n_loc + 255) / 256, &c->ctl->L_local, c->stream));
     if (c->world > 1 && c->comm) {

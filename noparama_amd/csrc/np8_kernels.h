@@ -237,6 +237,7 @@ hipError_t np8_launch_assign_wide(const np8::AssignArgs &A, int D, int M, int pr
 hipError_t np8_launch_loglik_matrix_wide(const np8::AssignArgs &A, const np8::WideArgs &W, int D, int M, int prior,
                                          const int64_t *idx, int64_t n, double *out, hipStream_t s);
 hipError_t np8_launch_loglik_wide(const np8::LoglikArgs &L, const np8::WideArgs &W, int D, hipStream_t s);
+hipError_t np8_launch_loglik_wide_mfma(const np8::AssignArgs &A, int D, double *partial, hipStream_t s);
 hipError_t np8_launch_wide_refresh(const np8::WideArgs &W, hipStream_t s);
 size_t np8_niw_lds_bytes(int D);
 hipError_t np8_niw_prepare(int D);

@@ -684,9 +684,10 @@ __global__ __launch_bounds__(kFinThreads) void np8_finalize(FinArgs F) {
         }
     }
     __syncthreads();
-    // mu and P' of every live row, all threads
+    // mu and P' of every live row, all threads (not on the wide path: its kernels read the fp32 factor
+    // rows of np8_wide_rows, and 4 MB of P' at D = 64 would keep this one workgroup busy for 0.3 ms)
     const int W = D + DP;
-    for (int idx = tid; idx < nlive * W; idx += kFinThreads) {
+    for (int idx = tid; idx < (F.frame_payload ? 0 : nlive * W); idx += kFinThreads) {
         const int r = idx / W, f = idx - r * W, s = live_s[r];
         F.cand[(int64_t)r * CS + f] = (f < D) ? F.slot_mu[(int64_t)s * D + f] : F.slot_P[(int64_t)s * DP + (f - D)];
     }

@@ -430,6 +430,66 @@ __global__ __launch_bounds__(64) void np8_loglik_matrix_wide(AssignArgs A, WideA
     for (int m = 0; m < M; ++m) out[r * (K + M) + K + m] = wide_aux_ll<D, PRIOR>(A.hyp, ny, A.seed, (uint64_t)(A.offset + il), t, m);
 }
 
+// ---- max likelihood on the matrix cores -------------------------------------------------------------
+// sum_i ll(x_i | theta_{z_i}) (MCMC::considerMaxLikelihood, np_mcmc.cpp:187-203): the own-cluster passes
+// of np8_assign_wide (one MFMA pass per distinct own slot of a wave; one on the label-sorted layout),
+// a fixed-order block reduction into partial[block] (reduced by np8_loglik_reduce).
+template <int D>
+__global__ __launch_bounds__(256) void np8_loglik_wide_mfma(AssignArgs A, double *__restrict__ partial) {
+    using W = Wide<D>;
+    constexpr int CS = W::CS, F = W::F;
+    __shared__ double red[256];
+    const int lane = threadIdx.x & 63, g = lane >> 4, col = lane & 15;
+    const int64_t pw = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63);
+    const int64_t p = pw + lane;
+    const bool valid = p < A.n_loc;
+    const bool sorted = A.sorted != 0;
+    const int cur = sorted ? A.ctl->cur : 0;
+    const int32_t *__restrict__ zs = cur ? A.zs[1] : A.zs[0];
+    const float *__restrict__ X = reinterpret_cast<const float *>(sorted ? (cur ? A.Xs[1] : A.Xs[0]) : A.X);
+    const int64_t n = A.n_loc;
+    double ll = 0.0;
+    if (pw < n) {  // wave-uniform
+        const int64_t pc = valid ? p : pw;
+        const int32_t zi = sorted ? zs[pc] : A.z[pc];
+        float xb[4][W::S];
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) {
+            int64_t pq = pw + nt * 16 + col;
+            if (pq >= n) pq = pc;
+#pragma unroll
+            for (int st = 0; st < W::S; ++st) xb[nt][st] = X[(int64_t)(4 * st + g) * n + pq];
+        }
+        uint64_t pend = __ballot(valid);
+        while (pend) {
+            const int32_t sj = __shfl(zi, __ffsll((unsigned long long)pend) - 1);
+            const double q = wide_pass<D>(A.wfrag + (int64_t)sj * W::ROW, xb, lane);
+            const bool mine = valid && zi == sj;
+            if (mine) ll = fma(-0.5, q, A.cand[(int64_t)A.dense_of[sj] * CS + F + kFieldC]);
+            pend &= ~__ballot(mine);
+        }
+    }
+    red[threadIdx.x] = ll;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (threadIdx.x < o) red[threadIdx.x] = red[threadIdx.x] + red[threadIdx.x + o];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) partial[blockIdx.x] = red[0];
+}
+
+hipError_t np8_launch_loglik_wide_mfma(const AssignArgs &A, int D, double *partial, hipStream_t s) {
+    const int64_t nb = (A.n_loc + 255) / 256;
+    if (nb <= 0) return hipSuccess;
+    if (D == 32)
+        hipLaunchKernelGGL((np8_loglik_wide_mfma<32>), dim3((unsigned)nb), dim3(256), 0, s, A, partial);
+    else if (D == 64)
+        hipLaunchKernelGGL((np8_loglik_wide_mfma<64>), dim3((unsigned)nb), dim3(256), 0, s, A, partial);
+    else
+        return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+
 // ---- sufficient statistics on the fp64 matrix cores (niw_conjugate on the wide path) -------------------
 // Per slot: s1 = sum d, S = sum d d^T (packed upper) with d = x - mu_slot in fp64 (the layout of
 // np8_suffstats / np8o_suffstats).  One wave walks kSuffChunks chunks of 64 consecutive positions of
