@@ -41,15 +41,17 @@ __device__ __forceinline__ void zero_block(double *p, int n) {
 
 // P' = packed sym(F F^T), off-diagonals doubled, into the slot table and its candidate row.  Returns
 // the candidate table's isotropy value: P'_00 when P' is a multiple of I, else 0 (block-uniform).
-__device__ double write_pprime(int D, const double *F, double *slotP, double *candP) {
+__device__ double write_pprime(int D, int LD, const double *F, double *slotP, double *candP) {
     bool iso = true;
     double p00 = 0.0;  // the same chain as element (0, 0) below
+    #pragma unroll 8
     for (int k = 0; k < D; ++k) p00 = fma(F[k], F[k], p00);
     for (int e = threadIdx.x; e < D * D; e += blockDim.x) {
         const int a = e / D, b = e - a * D;
         if (b < a) continue;
         double s = 0.0;
-        for (int k = 0; k < D; ++k) s = fma(F[a * D + k], F[b * D + k], s);
+        #pragma unroll 8
+        for (int k = 0; k < D; ++k) s = fma(F[a * LD + k], F[b * LD + k], s);
         const double v = (a == b) ? s : 2.0 * s;
         slotP[pix(D, a, b)] = v;
         if (candP) candP[pix(D, a, b)] = v;
@@ -59,18 +61,20 @@ __device__ double write_pprime(int D, const double *F, double *slotP, double *ca
 }
 
 // Sigma = T^T T, B T = Rhs (B lower triangular): one thread per column of T, then per element.
-__device__ void write_sigma(int D, const double *B, const double *Rhs, bool rhs_transposed, double *T, double *Sigma) {
+__device__ void write_sigma(int D, int LD, const double *B, const double *Rhs, bool rhs_transposed, double *T, double *Sigma) {
     for (int j = threadIdx.x; j < D; j += blockDim.x)
         for (int a = 0; a < D; ++a) {
-            double s = rhs_transposed ? Rhs[j * D + a] : Rhs[a * D + j];
-            for (int k = 0; k < a; ++k) s = fma(-B[a * D + k], T[k * D + j], s);
-            T[a * D + j] = s / B[a * D + a];
+            double s = rhs_transposed ? Rhs[j * LD + a] : Rhs[a * LD + j];
+            #pragma unroll 8
+            for (int k = 0; k < a; ++k) s = fma(-B[a * LD + k], T[k * LD + j], s);
+            T[a * LD + j] = s / B[a * LD + a];
         }
     __syncthreads();
     for (int e = threadIdx.x; e < D * D; e += blockDim.x) {
         const int a = e / D, b = e - a * D;
         double s = 0.0;
-        for (int k = 0; k < D; ++k) s = fma(T[k * D + a], T[k * D + b], s);
+        #pragma unroll 8
+        for (int k = 0; k < D; ++k) s = fma(T[k * LD + a], T[k * LD + b], s);
         Sigma[e] = s;
     }
 }
@@ -89,13 +93,15 @@ __device__ __forceinline__ void write_row_scalars(const NiwArgs &A, int s, int r
 
 }  // namespace
 
-size_t np8_niw_lds_bytes(int D) { return sizeof(double) * (4 * (size_t)D * D + 10 * (size_t)D); }
+// LDS matrices use the leading dimension D + 1: row-strided reads by consecutive threads fall into
+// different banks (a stride of D doubles put every lane of a wave on one bank).
+size_t np8_niw_lds_bytes(int D) { return sizeof(double) * (4 * (size_t)D * (D + 1) + 10 * (size_t)D); }
 
 // ---- posterior (and prior) draw -------------------------------------------------------------------
 // Block b: init mode (A.init_k > 0) draws G0 sample b into slot init_map[b] on stream INIT_THETA;
 // otherwise slot b's posterior on stream PARAM at the current epoch (oracle niw_draw_impl).
 __global__ __launch_bounds__(kNiwThreads) void np8_niw_post(NiwArgs A) {
-    const int D = A.D, W = D + D * (D + 1) / 2;
+    const int D = A.D, W = D + D * (D + 1) / 2, LD = D + 1;
     int s;
     int64_t n;
     uint64_t i;
@@ -117,8 +123,8 @@ __global__ __launch_bounds__(kNiwThreads) void np8_niw_post(NiwArgs A) {
         stream = kStreamParam;
     }
     extern __shared__ __attribute__((aligned(16))) double sm[];
-    double *L = sm, *Li = L + D * D, *B = Li + D * D, *F = B + D * D;
-    double *xb = F + D * D, *dm = xb + D, *mun = dm + D, *gv = mun + D, *z = gv + D, *y = z + D, *s1 = y + D,
+    double *L = sm, *Li = L + D * LD, *B = Li + D * LD, *F = B + D * LD;
+    double *xb = F + D * LD, *dm = xb + D, *mun = dm + D, *gv = mun + D, *z = gv + D, *y = z + D, *s1 = y + D,
            *anc = s1 + D;
     __shared__ double sh[4];
     __shared__ int bad;
@@ -128,7 +134,7 @@ __global__ __launch_bounds__(kNiwThreads) void np8_niw_post(NiwArgs A) {
     const double k0 = A.kappa0, nd = (double)n;
     const double kn = k0 + nd, nun = A.nu0 + nd;
     const double kf = (k0 * nd) / kn;
-    zero_block(L, 3 * D * D);  // L, Li, B: upper triangles stay 0
+    zero_block(L, 3 * D * LD);  // L, Li, B: upper triangles stay 0
     for (int a = tid; a < D; a += blockDim.x) {
         anc[a] = (n > 0) ? A.slot_mu[(int64_t)s * D + a] : 0.0;
         s1[a] = (n > 0) ? acc[a] : 0.0;
@@ -138,24 +144,33 @@ __global__ __launch_bounds__(kNiwThreads) void np8_niw_post(NiwArgs A) {
     }
     if (tid == 0) bad = 0;
     __syncthreads();
-    // Cholesky of Psin, left-looking: the diagonal of column j, then its rows below
+    // Psin's lower triangle formed in LDS by all threads (the statistics and Psi0 come from HBM once),
+    // then the left-looking Cholesky in place: the diagonal of column j, then its rows below -- the
+    // operations of the oracle's loop, in its order
+    for (int e = tid; e < D * D; e += blockDim.x) {
+        const int r = e / D, j = e - r * D;
+        if (j > r) continue;
+        const double sc = (n > 0) ? S[pix(D, j, r)] - (s1[r] * s1[j]) / nd : 0.0;
+        L[r * LD + j] = fma(kf, dm[r] * dm[j], A.Psi0[r * D + j] + sc);
+    }
+    __syncthreads();
     for (int j = 0; j < D; ++j) {
         if (tid == 0) {
-            const double sc = (n > 0) ? S[pix(D, j, j)] - (s1[j] * s1[j]) / nd : 0.0;
-            double v = fma(kf, dm[j] * dm[j], A.Psi0[j * D + j] + sc);
-            for (int k = 0; k < j; ++k) v = fma(-L[j * D + k], L[j * D + k], v);
+            double v = L[j * LD + j];
+            #pragma unroll 8
+            for (int k = 0; k < j; ++k) v = fma(-L[j * LD + k], L[j * LD + k], v);
             if (!(v > 0.0)) {
                 bad = 1;
                 v = 1.0;
             }
-            L[j * D + j] = sqrt(v);
+            L[j * LD + j] = sqrt(v);
         }
         __syncthreads();
         for (int r = j + 1 + tid; r < D; r += blockDim.x) {
-            const double sc = (n > 0) ? S[pix(D, j, r)] - (s1[r] * s1[j]) / nd : 0.0;
-            double v = fma(kf, dm[r] * dm[j], A.Psi0[r * D + j] + sc);
-            for (int k = 0; k < j; ++k) v = fma(-L[r * D + k], L[j * D + k], v);
-            L[r * D + j] = v / L[j * D + j];
+            double v = L[r * LD + j];
+            #pragma unroll 8
+            for (int k = 0; k < j; ++k) v = fma(-L[r * LD + k], L[j * LD + k], v);
+            L[r * LD + j] = v / L[j * LD + j];
         }
         __syncthreads();
     }
@@ -165,22 +180,23 @@ __global__ __launch_bounds__(kNiwThreads) void np8_niw_post(NiwArgs A) {
         return;
     }
     for (int j = tid; j < D; j += blockDim.x) {  // Li = L^{-1}, one column per thread
-        Li[j * D + j] = 1.0 / L[j * D + j];
+        Li[j * LD + j] = 1.0 / L[j * LD + j];
         for (int r = j + 1; r < D; ++r) {
             double v = 0.0;
-            for (int k = j; k < r; ++k) v = fma(-L[r * D + k], Li[k * D + j], v);
-            Li[r * D + j] = v / L[r * D + r];
+            #pragma unroll 8
+            for (int k = j; k < r; ++k) v = fma(-L[r * LD + k], Li[k * LD + j], v);
+            Li[r * LD + j] = v / L[r * LD + r];
         }
     }
     for (int a = tid; a < D; a += blockDim.x) {  // Bartlett diagonal
         const double g = chi2_mt(A.seed, i, t, stream, kNiwGammaCalls * (uint32_t)a, nun - a);
         gv[a] = g;
-        B[a * D + a] = sqrt(g);
+        B[a * LD + a] = sqrt(g);
     }
     for (int e = tid; e < D * (D - 1) / 2; e += blockDim.x) {
         int a, b;
         lower_index(e, a, b);
-        B[a * D + b] = normal_at(A.seed, i, t, stream, kNiwNormalCall0, (uint32_t)e);
+        B[a * LD + b] = normal_at(A.seed, i, t, stream, kNiwNormalCall0, (uint32_t)e);
     }
     for (int j = tid; j < D; j += blockDim.x)
         z[j] = normal_at(A.seed, i, t, stream, kNiwNormalCall0, (uint32_t)(D * (D - 1) / 2 + j));
@@ -193,33 +209,36 @@ __global__ __launch_bounds__(kNiwThreads) void np8_niw_post(NiwArgs A) {
     for (int e = tid; e < D * D; e += blockDim.x) {  // F = Li^T B
         const int a = e / D, b = e - a * D;
         double v = 0.0;
-        for (int k = (a > b ? a : b); k < D; ++k) v = fma(Li[k * D + a], B[k * D + b], v);
-        F[e] = v;
+        #pragma unroll 8
+        for (int k = (a > b ? a : b); k < D; ++k) v = fma(Li[k * LD + a], B[k * LD + b], v);
+        F[a * LD + b] = v;
     }
     __syncthreads();
     const int row = A.write_cand ? A.dense_of[s] : -1;
-    const double iso = write_pprime(D, F, A.slot_P + (int64_t)s * (D * (D + 1) / 2),
+    const double iso = write_pprime(D, LD, F, A.slot_P + (int64_t)s * (D * (D + 1) / 2),
                                     row >= 0 ? A.cand + (int64_t)row * cand_stride(D) + D : nullptr);
     if (tid == 0) {  // y = B^{-T} z / sqrt(kn)
         const double rskn = 1.0 / sqrt(kn);
         for (int a = D - 1; a >= 0; --a) {
             double v = z[a] * rskn;
-            for (int k = a + 1; k < D; ++k) v = fma(-B[k * D + a], y[k], v);
-            y[a] = v / B[a * D + a];
+            #pragma unroll 8
+            for (int k = a + 1; k < D; ++k) v = fma(-B[k * LD + a], y[k], v);
+            y[a] = v / B[a * LD + a];
         }
     }
     __syncthreads();
     for (int a = tid; a < D; a += blockDim.x) {
         double v = 0.0;
-        for (int k = 0; k <= a; ++k) v = fma(L[a * D + k], y[k], v);
+        #pragma unroll 8
+        for (int k = 0; k <= a; ++k) v = fma(L[a * LD + k], y[k], v);
         const double m = mun[a] + v;
         A.slot_mu[(int64_t)s * D + a] = m;
         if (row >= 0) A.cand[(int64_t)row * cand_stride(D) + a] = m;
     }
-    write_sigma(D, B, L, true, F, A.slot_sigma + (int64_t)s * D * D);  // T = B^{-1} L^T
+    write_sigma(D, LD, B, L, true, F, A.slot_sigma + (int64_t)s * D * D);  // T = B^{-1} L^T
     if (tid == 0) {
         double sl = 0.0;
-        for (int a = 0; a < D; ++a) sl += log_pos(L[a * D + a]);
+        for (int a = 0; a < D; ++a) sl += log_pos(L[a * LD + a]);
         write_row_scalars(A, s, row, fma(0.5, sh[0], fma(-0.5 * (double)D, kLog2Pi, -sl)), iso);
     }
     if (n > 0)
@@ -228,11 +247,11 @@ __global__ __launch_bounds__(kNiwThreads) void np8_niw_post(NiwArgs A) {
 
 // ---- picked auxiliaries -> slots (oracle niw_aux_slot) ------------------------------------------------
 __global__ __launch_bounds__(kNiwThreads) void np8_niw_aux_slots(NiwArgs A) {
-    const int D = A.D;
+    const int D = A.D, LD = D + 1;
     const int npend = A.ctl->n_pend;
     extern __shared__ __attribute__((aligned(16))) double sm[];
-    double *B = sm, *RB = B + D * D, *F = RB + D * D;
-    double *gv = F + D * D, *z = gv + D, *h = z + D, *cs = h + D, *y = cs + D, *ry = y + D, *eps = ry + D, *dt = eps + D;
+    double *B = sm, *RB = B + D * LD, *F = RB + D * LD;
+    double *gv = F + D * LD, *z = gv + D, *h = z + D, *cs = h + D, *y = cs + D, *ry = y + D, *eps = ry + D, *dt = eps + D;
     __shared__ double sh[8];
     const int tid = threadIdx.x;
     const uint32_t t = A.ctl->t_base + A.t;
@@ -243,13 +262,13 @@ __global__ __launch_bounds__(kNiwThreads) void np8_niw_aux_slots(NiwArgs A) {
         const int m = (int)pe[2], s = (int)pe[3];
         const uint32_t base = (uint32_t)m * kNiwAuxCalls;
         __syncthreads();  // LDS of the previous request fully consumed
-        zero_block(B, D * D);
+        zero_block(B, D * LD);
         for (int a = tid; a < D; a += blockDim.x) dt[a] = vmu[1 + a];
         __syncthreads();
         for (int a = tid; a < D; a += blockDim.x) {
             const double g = chi2_mt(A.seed, i, t, kStreamAuxNiw, base + kNiwGammaCalls * (uint32_t)a, A.nu0 - a);
             gv[a] = g;
-            B[a * D + a] = sqrt(g);
+            B[a * LD + a] = sqrt(g);
         }
         if (tid == blockDim.x - 1) {
             sh[1] = niw_chi_perp(A.seed, i, t, kStreamAuxNiw, base, D);
@@ -258,7 +277,7 @@ __global__ __launch_bounds__(kNiwThreads) void np8_niw_aux_slots(NiwArgs A) {
         for (int e = tid; e < D * (D - 1) / 2; e += blockDim.x) {
             int a, b;
             lower_index(e, a, b);
-            B[a * D + b] = normal_at(A.seed, i, t, kStreamAuxDir, base, (uint32_t)e);
+            B[a * LD + b] = normal_at(A.seed, i, t, kStreamAuxDir, base, (uint32_t)e);
         }
         for (int j = tid; j + 1 < D; j += blockDim.x)
             z[1 + j] = normal_at(A.seed, i, t, kStreamAuxDir, base, (uint32_t)(D * (D - 1) / 2 + j));
@@ -292,36 +311,40 @@ __global__ __launch_bounds__(kNiwThreads) void np8_niw_aux_slots(NiwArgs A) {
         const double beta = sh[3];
         for (int b = tid; b < D; b += blockDim.x) {  // column sums h^T B
             double v = 0.0;
-            for (int k = b; k < D; ++k) v = fma(h[k], B[k * D + b], v);
+            #pragma unroll 8
+            for (int k = b; k < D; ++k) v = fma(h[k], B[k * LD + b], v);
             cs[b] = v;
         }
         __syncthreads();
         for (int e = tid; e < D * D; e += blockDim.x) {
             const int a = e / D, b = e - a * D;
-            RB[e] = fma(-(beta * h[a]), cs[b], B[e]);
+            RB[a * LD + b] = fma(-(beta * h[a]), cs[b], B[a * LD + b]);
         }
         __syncthreads();
         for (int e = tid; e < D * D; e += blockDim.x) {  // F = U RB
             const int a = e / D, b = e - a * D;
             double v = 0.0;
-            for (int k = 0; k <= a; ++k) v = fma(A.U[a * D + k], RB[k * D + b], v);
-            F[e] = v;
+            #pragma unroll 8
+            for (int k = 0; k <= a; ++k) v = fma(A.U[a * D + k], RB[k * LD + b], v);
+            F[a * LD + b] = v;
         }
         __syncthreads();
         const int row = A.dense_of[s];
-        const double iso = write_pprime(D, F, A.slot_P + (int64_t)s * (D * (D + 1) / 2),
+        const double iso = write_pprime(D, LD, F, A.slot_P + (int64_t)s * (D * (D + 1) / 2),
                                         row >= 0 ? A.cand + (int64_t)row * cand_stride(D) + D : nullptr);
         if (tid == 0) {  // mu = mu0 + U^{-T} R B^{-T} z / sqrt(kappa0)
             for (int a = D - 1; a >= 0; --a) {
                 double v = z[a] * A.rsk;
-                for (int k = a + 1; k < D; ++k) v = fma(-B[k * D + a], y[k], v);
-                y[a] = v / B[a * D + a];
+                #pragma unroll 8
+                for (int k = a + 1; k < D; ++k) v = fma(-B[k * LD + a], y[k], v);
+                y[a] = v / B[a * LD + a];
             }
             double hy = 0.0;
             for (int k = 0; k < D; ++k) hy = fma(h[k], y[k], hy);
             for (int a = 0; a < D; ++a) ry[a] = fma(-(beta * h[a]), hy, y[a]);
             for (int a = D - 1; a >= 0; --a) {
                 double v = ry[a];
+                #pragma unroll 8
                 for (int k = a + 1; k < D; ++k) v = fma(-A.U[k * D + a], eps[k], v);
                 eps[a] = v / A.U[a * D + a];
             }
@@ -333,16 +356,17 @@ __global__ __launch_bounds__(kNiwThreads) void np8_niw_aux_slots(NiwArgs A) {
         }
         for (int b = tid; b < D; b += blockDim.x) {  // R U^{-1}
             double v = 0.0;
+            #pragma unroll 8
             for (int k = b; k < D; ++k) v = fma(h[k], A.Uinv[k * D + b], v);
             cs[b] = v;
         }
         __syncthreads();
         for (int e = tid; e < D * D; e += blockDim.x) {
             const int a = e / D, b = e - a * D;
-            RB[e] = fma(-(beta * h[a]), cs[b], A.Uinv[e]);
+            RB[a * LD + b] = fma(-(beta * h[a]), cs[b], A.Uinv[e]);
         }
         __syncthreads();
-        write_sigma(D, B, RB, false, F, A.slot_sigma + (int64_t)s * D * D);
+        write_sigma(D, LD, B, RB, false, F, A.slot_sigma + (int64_t)s * D * D);
         if (tid == 0) write_row_scalars(A, s, row, fma(0.5, sh[0], A.caux), iso);
     }
 }
