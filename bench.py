@@ -47,6 +47,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget (0 = skip)")
     ap.add_argument("--traffic-json", default=None,
                     help="HBM bytes per assign launch from the committed PMC profile of this config")
+    ap.add_argument("--sampler", default="neal8", choices=["neal8", "jain_neal"],
+                    help="jain_neal: split-merge sweeps (np8_sm_sweep, one rank) instead of the Gibbs sweep")
     ap.add_argument("--param-update", default="frozen", choices=["frozen", "mh_g0", "niw_conjugate"],
                     help="cluster-parameter update after every sweep (frozen = the reference's effective one)")
     a = ap.parse_args()
@@ -75,6 +77,8 @@ def workload(args):
 
 def main():
     args = parse()
+    if args.sampler == "jain_neal":
+        return main_sm(args)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -239,6 +243,100 @@ def main():
         print(json.dumps(out))
     if dist:
         dist.destroy_process_group()
+
+
+def main_sm(args):
+    """Split-merge sweeps/sec (np8_sm_sweep: N Jain-Neal attempts + the end-of-sweep step per sweep) on
+    the C2/C3 workload and warm state, one GPU.  Roofline of the state rebuild (np8_sm_own/np8_sm_cross:
+    N (K + 1) fp64 likelihoods per launch, the sampler's compute-bound part); the attempt batches are
+    latency-bound (the sequential SAMS allocation of a split, one lane per attempt)."""
+    import torch
+
+    from noparama_amd import JainNealAlgorithm
+
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        raise SystemExit("--sampler jain_neal runs on one rank")
+    torch.cuda.set_device(0)
+    N, D, K = args.n, args.d, args.k
+    X, z, mu, sig, opts = workload(args)
+    if opts:
+        raise SystemExit("--sampler jain_neal: reference prior, fp64 configurations only")
+    smp = JainNealAlgorithm(D, seed=args.seed, device=0, param_update=args.param_update, kcap=max(256, 4 * K))
+    smp.set_data(X)
+    smp.set_state(z, mu, sig)
+    smp.sweep(args.warmup)
+    smp.set_timing(True)
+    st0, o0 = smp.stats(), smp.sm_stats()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    smp.sweep(args.steps)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    st1, o1 = smp.stats(), smp.sm_stats()
+    d = {k: o1[k] - o0[k] for k in o1}
+    nm = st1["n_timed_sm_members"] - st0["n_timed_sm_members"]
+    ne = st1["n_timed_sm_eval"] - st0["n_timed_sm_eval"]
+    ms_m = (st1["ms_sm_members"] - st0["ms_sm_members"]) / max(nm, 1)
+    ms_e = (st1["ms_sm_eval"] - st0["ms_sm_eval"]) / max(ne, 1)
+    Kf = st1["K"]
+    flops = float(N) * (Kf + 1) * (D * D + 2 * D + 4)  # cross matrix + own likelihoods per rebuild
+    achieved = flops / (ms_m * 1e-3) / 1e12 if ms_m > 0 else 0.0
+    cpu = cpu_baseline_sm(X, z, mu, sig, D, args.seed, args.cpu_seconds) if args.cpu_seconds > 0 else None
+    out = {
+        "metric": f"split-merge sweeps/sec (Jain-Neal, N={N:.0e} attempts/sweep, D={D})".replace("+0", ""),
+        "value": args.steps / dt,
+        "unit": "sweeps/s",
+        "n_gpus": 1,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": dt / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "replicas only",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic",
+        "config": {
+            "workload": f"{args.config}: N={N} D={D} K~{K} mixture, warm state, Jain-Neal split-merge "
+                        f"(sams_prior, reference rules), {args.param_update} cluster parameters",
+            "N": N, "D": D, "K_final": Kf, "attempt_outcomes": d,
+            "state_rebuilds": nm, "attempt_batches": ne,
+            "ms_per_rebuild": ms_m, "ms_per_batch": ms_e,
+        },
+        "roofline": {
+            "bound": "mfma",
+            "note": "fp64 compute roof of the state rebuild (np8_sm_own + np8_sm_cross); attempt batches "
+                    "(np8_sm_eval) are latency-bound by the sequential SAMS allocation",
+            "achieved": achieved,
+            "peak": FP64_PEAK_TFLOPS,
+            "unit": "TFLOP/s",
+            "frac": achieved / FP64_PEAK_TFLOPS,
+            "traffic": None,
+            "algorithmic_flops_per_launch": flops,
+        },
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(out))
+
+
+def cpu_baseline_sm(X, z, mu, sig, D, seed, budget_s):
+    """The oracle's sequential split-merge attempts (np8o_sm_attempts, one core) on the same data and
+    state: the first attempts of one sweep, doubling until the budget, extrapolated to N attempts."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O  # test infrastructure: timed as the CPU baseline only
+
+    c = O.Chain(D, seed=seed, kcap=4096)
+    c.set_data(X)
+    c.set_state(z, mu, sig)
+    N = X.shape[0]
+    done, a, t0 = 0, 64, time.perf_counter()
+    while time.perf_counter() - t0 < budget_s and done < N:
+        b = min(N, done + a)
+        c.sm_attempts(done, b)
+        done, a = b, 2 * a
+    el = time.perf_counter() - t0
+    return {"value": done / el / N, "unit": "sweeps/s", "cores": 1, "kind": "port",
+            "sample": f"the first {done} of the N={N} split-merge attempts of one sweep in {el:.1f}s on 1 core, "
+                      f"extrapolated"}
 
 
 def cpu_baseline(X, z, mu, sig, D, seed, budget_s, opts):

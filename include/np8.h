@@ -102,6 +102,10 @@ typedef struct {
     /* launches behind ms_assign, ms_finalize, ms_loglik, ms_params: every launch when sweeps run one
      * by one; one np8_assign launch per replay when they run from a captured 20-sweep graph */
     int64_t n_timed_assign, n_timed_finalize, n_timed_loglik, n_timed_params;
+    /* split-merge (np8_sm_sweep): device time of the state rebuilds (member lists, own and cross
+     * likelihoods) and of the attempt batches, and the launches behind them */
+    double ms_sm_members, ms_sm_eval;
+    int64_t n_timed_sm_members, n_timed_sm_eval;
 } np8_stats_t;
 
 /* Create / destroy.  Replaces NealAlgorithm8::NealAlgorithm8 (np_neal_algorithm8.cpp:17-34). */
@@ -131,6 +135,21 @@ int np8_init_random(np8_ctx *ctx, int32_t K_init);
  * including the max-likelihood check every 5th sweep (np_mcmc.cpp:172-174).  Asynchronous on the
  * context's stream; errors raised on the device are reported by the next np8_sync(). */
 int np8_sweep(np8_ctx *ctx, int32_t n_sweeps);
+
+/* Jain-Neal split-merge sweeps: the reference's `-a jain_neal_split` population update
+ * (class JainNealAlgorithm, include/np_jain_neal_algorithm.h:52-98, update() at
+ * src/np_jain_neal_algorithm.cpp:424-502), driven as src/np_mcmc.cpp:117-164 drives it (subset_count = 2,
+ * np_main.cpp:440-445): each sweep makes N attempts on the item pairs of two scan permutations -- a
+ * split of their common cluster (sams_prior allocation, new cluster from G0) or a merge of the first
+ * item's cluster into the second's -- then the end-of-sweep step of np8_sweep (parameter update,
+ * max-likelihood check).  Single rank, reference prior, fp64 contraction (D in {1,2,3,4,8,16}).
+ * Synchronous: returns when the sweeps are done. */
+int np8_sm_sweep(np8_ctx *ctx, int32_t n_sweeps);
+/* Cumulative attempt outcomes (the reference's _statistics.step[], np_jain_neal_algorithm.cpp:505-530):
+ * [0] pairs skipped (equal items, np_mcmc.cpp:153-156), [1] splits rejected, [2] merges rejected,
+ * [3] splits accepted, [4] merges accepted, [5] splits accepted by the ratio but dropped for want of a
+ * free slot (kcap live clusters). */
+int np8_sm_stats(np8_ctx *ctx, int64_t out[6]);
 
 /* The reference's per-call granularity: sequential single-point updates of the listed items, in
  * order, at the current epoch (NealAlgorithm8::update with data_ids.size()==1).  Call

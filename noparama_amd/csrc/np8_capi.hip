@@ -112,8 +112,19 @@ struct np8_ctx {
     bool timing = false;
     std::vector<Timer> timers;
     std::vector<hipEvent_t> event_pool;
-    double ms[4] = {0, 0, 0, 0};  // assign, finalize, loglik, params
-    int64_t n_timed[4] = {0, 0, 0, 0};
+    double ms[6] = {0, 0, 0, 0, 0, 0};  // assign, finalize, loglik, params, sm members, sm eval
+    int64_t n_timed[6] = {0, 0, 0, 0, 0, 0};
+    // Jain-Neal split-merge (np8_sm_sweep): member lists, own/cross likelihoods, batch outcomes
+    int32_t *sm_hist = nullptr, *sm_mem = nullptr, *sm_off = nullptr, *sm_live = nullptr;
+    double *sm_Xm = nullptr, *sm_ownm = nullptr, *sm_cross = nullptr;
+    int64_t *sm_slist = nullptr;
+    double *sm_stheta = nullptr;
+    SmCtl *sm_ctl = nullptr;
+    uint8_t *sm_typ = nullptr;
+    int64_t *sm_first_host = nullptr;  // pinned
+    int64_t sm_n = -1, sm_cross_cap = 0;
+    int32_t sm_batch = 1024;
+    int32_t sm_K = 0;
     std::string err;
 };
 
@@ -350,9 +361,21 @@ void free_device(np8_ctx *c) {
                     c->cnt,    c->cnt_best, c->mu_best, c->sigma_best, c->cand, c->ctl,    c->hyp,
                     c->d_mu0,  c->d_LT,    c->d_Gp,   c->d_LTL,   c->rec,     c->gath,    c->order,
                     c->partial, c->dense_of, c->Xs[0], c->Xs[1], c->zs[0], c->zs[1], c->ids[0], c->ids[1],
-                    c->s_hist, c->s_cursor, c->s_off, c->slot_iso, c->acc, c->r2, c->plist, c->plen};
+                    c->s_hist, c->s_cursor, c->s_off, c->slot_iso, c->acc, c->r2, c->plist, c->plen,
+                    c->sm_hist, c->sm_mem, c->sm_off, c->sm_live, c->sm_Xm, c->sm_ownm, c->sm_cross, c->sm_ctl,
+                    c->sm_typ, c->sm_slist, c->sm_stheta};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
+    if (c->sm_first_host) (void)hipHostFree(c->sm_first_host);
+    c->sm_hist = c->sm_mem = c->sm_off = c->sm_live = nullptr;
+    c->sm_Xm = c->sm_ownm = c->sm_cross = nullptr;
+    c->sm_slist = nullptr;
+    c->sm_stheta = nullptr;
+    c->sm_ctl = nullptr;
+    c->sm_typ = nullptr;
+    c->sm_first_host = nullptr;
+    c->sm_n = -1;
+    c->sm_cross_cap = 0;
     for (int b = 0; b < 2; ++b) {
         c->Xs[b] = nullptr;
         c->zs[b] = c->ids[b] = nullptr;
@@ -1499,6 +1522,10 @@ int np8_stats(np8_ctx *c, np8_stats_t *out) {
     out->n_timed_finalize = c->n_timed[1];
     out->n_timed_loglik = c->n_timed[2];
     out->n_timed_params = c->n_timed[3];
+    out->ms_sm_members = c->ms[4];
+    out->ms_sm_eval = c->ms[5];
+    out->n_timed_sm_members = c->n_timed[4];
+    out->n_timed_sm_eval = c->n_timed[5];
     out->mh_accepted = h.mh_accepted;
     return NP8_OK;
 }
@@ -1614,6 +1641,145 @@ int np8_step_merge(np8_ctx *c, const void *records, int32_t world) {
     int r = launch_finalize(c, c->gath, world);
     if (r) return r;
     HIPC(c, hipStreamSynchronize(c->stream));
+    return NP8_OK;
+}
+
+// ---- Jain-Neal split-merge (np8_sm.hip; DESIGN.md "Split-merge") ------------------------------------
+static SmArgs sm_args(np8_ctx *c) {
+    SmArgs A;
+    std::memset(&A, 0, sizeof(A));
+    A.D = c->D;
+    A.kcap = c->kcap;
+    A.N = (int32_t)c->n_loc;
+    A.K = c->sm_K;
+    A.X = c->X;
+    A.z = c->z;
+    A.cnt = c->cnt;
+    A.slot_mu = c->slot_mu;
+    A.slot_P = c->slot_P;
+    A.slot_c = c->slot_c;
+    A.slot_iso = c->slot_iso;
+    A.gp_iso = c->gp_iso;
+    A.LT = c->d_LT;
+    A.Gp = c->d_Gp;
+    A.mu0 = c->d_mu0;
+    A.caux = c->caux;
+    A.rsk = c->rsk;
+    A.nu = c->nu;
+    A.log_alpha = std::log(c->alpha);
+    A.seed = c->seed;
+    A.t = c->epoch;
+    A.perm0 = make_perm(c->seed ^ kSmPermKey[0], c->epoch, (uint32_t)c->n_loc);
+    A.perm1 = make_perm(c->seed ^ kSmPermKey[1], c->epoch, (uint32_t)c->n_loc);
+    A.hist = c->sm_hist;
+    A.nbk = (int32_t)((c->n_loc + 4095) / 4096);
+    A.mem = c->sm_mem;
+    A.off = c->sm_off;
+    A.dense = c->dense_of;
+    A.live = c->sm_live;
+    A.Xm = c->sm_Xm;
+    A.ownm = c->sm_ownm;
+    A.slist = c->sm_slist;
+    A.stheta = c->sm_stheta;
+    A.cross = c->sm_cross;
+    A.sc = c->sm_ctl;
+    A.typ = c->sm_typ;
+    return A;
+}
+
+static constexpr int32_t kSmBatchMax = 1 << 20, kSmBatchMin = 1024;
+
+static int sm_buffers(np8_ctx *c) {
+    if (c->sm_n == c->n_loc) return NP8_OK;
+    const int64_t nbk = (c->n_loc + 4095) / 4096;
+    int r;
+    if ((r = dalloc(c, &c->sm_hist, (size_t)(c->kcap * (nbk > 0 ? nbk : 1)))) || (r = dalloc(c, &c->sm_mem, (size_t)c->n_loc)) ||
+        (r = dalloc(c, &c->sm_off, (size_t)c->kcap + 1)) || (r = dalloc(c, &c->sm_live, (size_t)c->kcap)) ||
+        (r = dalloc(c, &c->sm_ownm, (size_t)c->n_loc)) || (r = dalloc(c, &c->sm_Xm, (size_t)c->n_loc * c->D)) ||
+        (r = dalloc(c, &c->sm_typ, (size_t)kSmBatchMax)) || (r = dalloc(c, &c->sm_slist, (size_t)kSmBatchMax)) ||
+        (r = dalloc(c, &c->sm_stheta, (size_t)kSmBatchMax * (c->D + 1))))
+        return r;
+    if (!c->sm_ctl) {
+        if ((r = dalloc(c, &c->sm_ctl, 1))) return r;
+        HIPC(c, hipHostMalloc((void **)&c->sm_first_host, sizeof(int64_t)));
+    }
+    c->sm_n = c->n_loc;
+    return NP8_OK;
+}
+
+// The state the attempts of a batch see: dense table, live count, member lists, own and cross.
+static int sm_rebuild(np8_ctx *c) {
+    int r = rebuild(c);
+    if (r) return r;
+    Ctl h;
+    if ((r = read_ctl(c, &h))) return r;
+    c->sm_K = h.K;
+    if ((int64_t)h.K * h.K > c->sm_cross_cap) {
+        const int64_t cap = std::max<int64_t>((int64_t)h.K * h.K, 64 * 64);
+        if ((r = dalloc(c, &c->sm_cross, (size_t)cap))) return r;
+        c->sm_cross_cap = cap;
+    }
+    Timer t;
+    timer_begin(c, 4, t);
+    HIPC(c, np8_launch_sm_members(sm_args(c), c->stream));
+    timer_end(c, t);
+    return NP8_OK;
+}
+
+int np8_sm_sweep(np8_ctx *c, int32_t n_sweeps) {
+    if (!c) return NP8_ERR_ARG;
+    if (!c->have_state) return fail(c, NP8_ERR_STATE, "np8_sm_sweep: no state (np8_set_state/np8_init_random)");
+    if (c->world > 1) return fail(c, NP8_ERR_ARG, "np8_sm_sweep: split-merge runs on one rank");
+    if (c->wide || c->prior != NP8_PRIOR_REFERENCE)
+        return fail(c, NP8_ERR_ARG, "np8_sm_sweep: needs the reference prior and the fp64 contraction");
+    if (c->n_loc > INT32_MAX) return fail(c, NP8_ERR_ARG, "np8_sm_sweep: at most 2^31-1 items");
+    int r = sm_buffers(c);
+    if (r) return r;
+    const int64_t N = c->n_loc;
+    for (int s = 0; s < n_sweeps; ++s) {
+        // the split-merge moves change z and the counts behind the label-sorted layout and the lists
+        c->use_sorted = false;
+        c->sorted_valid = false;
+        c->lists_valid = c->r2_zero = c->collecting = false;
+        if ((r = sm_rebuild(c))) return r;
+        int64_t a = 0;
+        while (a < N) {
+            const int32_t nb = (int32_t)std::min<int64_t>(c->sm_batch, N - a);
+            SmArgs A = sm_args(c);
+            A.a0 = a;
+            A.nb = nb;
+            Timer t;
+            timer_begin(c, 5, t);
+            HIPC(c, np8_launch_sm_eval(A, c->stream));
+            timer_end(c, t);
+            HIPC(c, hipMemcpyAsync(c->sm_first_host, &c->sm_ctl->first, sizeof(int64_t), hipMemcpyDeviceToHost,
+                                   c->stream));
+            HIPC(c, hipStreamSynchronize(c->stream));
+            const int64_t first = *c->sm_first_host;
+            if (first == INT64_MAX) {
+                a += nb;
+                c->sm_batch = (int32_t)std::min<int64_t>(2ll * c->sm_batch, kSmBatchMax);
+                continue;
+            }
+            FinArgs F = fin_args(c, c->rec, 1);
+            HIPC(c, np8_launch_sm_apply(A, F, first, c->stream));
+            if ((r = sm_rebuild(c))) return r;
+            c->sm_batch = (int32_t)std::max<int64_t>(kSmBatchMin, std::min<int64_t>(kSmBatchMax, 2 * (first - a + 1)));
+            a = first + 1;
+        }
+        if ((r = end_sweep(c))) return r;
+    }
+    return NP8_OK;
+}
+
+int np8_sm_stats(np8_ctx *c, int64_t out[6]) {
+    if (!c || !out) return NP8_ERR_ARG;
+    for (int k = 0; k < 6; ++k) out[k] = 0;
+    if (!c->sm_ctl) return NP8_OK;
+    SmCtl h;
+    HIPC(c, hipMemcpyAsync(&h, c->sm_ctl, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    for (int k = 0; k < 6; ++k) out[k] = h.stats[k];
     return NP8_OK;
 }
 

@@ -147,6 +147,60 @@ struct FinArgs {
     int32_t *wdirty;
 };
 
+// Auxiliary draw m of (item i, epoch t) -> a slot: the G0 draw of normalinvwishart.h:44-64 in the
+// factored form (DESIGN.md "G0").
+__device__ __forceinline__ void write_new_slot(const FinArgs &F, const double *vmu, int s) {
+    const int D = F.D, DP = D * (D + 1) / 2;
+    const double v = vmu[0];
+    for (int a = 0; a < D; ++a) F.slot_mu[(int64_t)s * D + a] = vmu[1 + a];
+    const double v2 = v * v;
+    for (int k = 0; k < DP; ++k) F.slot_P[(int64_t)s * DP + k] = F.Gp[k] / v2;
+    F.slot_c[s] = fma(-(double)D, log_pos(fabs(v)), F.caux);
+    for (int k = 0; k < D * D; ++k) F.slot_sigma[(int64_t)s * D * D + k] = v2 * F.LTL[k];
+    F.slot_iso[s] = (F.gp_iso > 0.0) ? F.Gp[0] / v2 : 0.0;
+    if (F.r2) F.r2[s] = __longlong_as_double(0x7FF0000000000000ll);  // radius unknown until a sweep measures it
+}
+
+// Jain-Neal split-merge (np8_sm.hip, DESIGN.md "Split-merge").
+// keys of the two scan permutations: make_perm(seed ^ kSmPermKey[r], epoch, N)
+constexpr uint64_t kSmPermKey[2] = {0x4A4E53504C495430ull, 0x4A4E53504C495431ull};
+
+struct SmCtl {
+    int64_t first;     // lowest accepted attempt of the batch (INT64_MAX: none)
+    int64_t stats[6];  // outcomes: skipped, split rej, merge rej, split acc, merge acc, split at kcap
+    int32_t nsplit;    // splits queued by np8_sm_classify
+    int32_t pad;
+};
+
+struct SmArgs {
+    int32_t D, kcap;
+    int32_t N, K;      // local items; live slots (host copy of ctl->K after the last table rebuild)
+    const double *X;   // [D][N] (structure of arrays)
+    int32_t *z, *cnt;
+    const double *slot_mu, *slot_P, *slot_c, *slot_iso;
+    const double *LT, *Gp, *mu0;  // LT: D*D row-major; Gp packed
+    double gp_iso;                // diagonal of Gp when it is a multiple of I, else 0
+    double caux, rsk, nu, log_alpha;
+    uint64_t seed;
+    uint32_t t, pad;
+    Perm perm0, perm1;  // the two scan permutations of the sweep (np_mcmc.cpp:118-125)
+    int32_t *hist;      // [kcap][nbk] block histograms -> scatter bases
+    int32_t nbk, pad2;
+    int32_t *mem;       // [N] members of every slot, ascending item order
+    int32_t *off;       // [kcap + 1]
+    const int32_t *dense;  // slot -> live rank (np8_finalize's dense_of)
+    int32_t *live;      // [kcap] live rank -> slot
+    double *Xm;         // [D][N] items in member order
+    double *ownm;       // [N] ll of member p under its own slot
+    int64_t *slist;     // [batch] queued split attempts
+    double *stheta;     // [batch][D + 1] their new clusters' (v, mu)
+    double *cross;      // [K][K] canon_sum over row r's members of ll under live slot k
+    SmCtl *sc;
+    uint8_t *typ;       // [batch] attempt outcomes
+    int64_t a0;
+    int32_t nb, pad3;
+};
+
 // NIW prior kernels (np8_niw.hip): posterior / prior draws per slot and picked auxiliaries -> slots.
 struct NiwArgs {
     int32_t D, kcap;
@@ -257,3 +311,6 @@ hipError_t np8_launch_suffstats_wide(const np8::ParamArgs &P, hipStream_t s);
 hipError_t np8_launch_mh_g0(const np8::ParamArgs &A, hipStream_t s);
 hipError_t np8_launch_advance_epoch(np8::Ctl *ctl, uint32_t n, hipStream_t s);
 hipError_t np8_launch_prune(const np8::PruneArgs &A, int kcap, hipStream_t s);
+hipError_t np8_launch_sm_members(const np8::SmArgs &A, hipStream_t s);
+hipError_t np8_launch_sm_eval(const np8::SmArgs &A, hipStream_t s);
+hipError_t np8_launch_sm_apply(const np8::SmArgs &A, const np8::FinArgs &F, int64_t a, hipStream_t s);

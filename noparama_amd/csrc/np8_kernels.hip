@@ -517,20 +517,6 @@ __device__ const double *request_vmu(const FinArgs &F, const int *base, int q) {
            (int64_t)(q - base[r]) * (F.D + 1);
 }
 
-// Auxiliary draw m of (item i, epoch t) -> a slot: the G0 draw of normalinvwishart.h:44-64 in the
-// factored form (DESIGN.md "G0").
-__device__ void write_new_slot(const FinArgs &F, const double *vmu, int s) {
-    const int D = F.D, DP = D * (D + 1) / 2;
-    const double v = vmu[0];
-    for (int a = 0; a < D; ++a) F.slot_mu[(int64_t)s * D + a] = vmu[1 + a];
-    const double v2 = v * v;
-    for (int k = 0; k < DP; ++k) F.slot_P[(int64_t)s * DP + k] = F.Gp[k] / v2;
-    F.slot_c[s] = fma(-(double)D, log_pos(fabs(v)), F.caux);
-    for (int k = 0; k < D * D; ++k) F.slot_sigma[(int64_t)s * D * D + k] = v2 * F.LTL[k];
-    F.slot_iso[s] = (F.gp_iso > 0.0) ? F.Gp[0] / v2 : 0.0;
-    if (F.r2) F.r2[s] = __longlong_as_double(0x7FF0000000000000ll);  // radius unknown until a sweep measures it
-}
-
 // Wide path, reference prior: (v, mu) of auxiliary m of item i from the item frame (|y0|, y0) its
 // rank recorded (aux_params of the narrow path, with the frame read back instead of recomputed).
 template <int D>

@@ -1,0 +1,534 @@
+// np8_sm.hip -- Jain-Neal split-merge on the device (DESIGN.md "Split-merge"; the reference's
+// JainNealAlgorithm, src/np_jain_neal_algorithm.cpp, driven by src/np_mcmc.cpp:117-164 with two scan
+// permutations).  The attempts of a sweep form one sequential Metropolis-Hastings chain; the host runs
+// them in speculative batches: every attempt of a batch is evaluated against the batch-start state
+// (np8_sm_eval), the lowest accepted one is applied (np8_sm_apply) and the batch restarts after it.
+// Attempts before the first acceptance see exactly the state the sequential chain would show them, so
+// the result equals oracle/np8_oracle.c np8o_sm_sweep attempt for attempt.
+//
+// Per state (rebuilt after every accepted attempt, np8_launch_sm_members):
+//   mem/off   members of every slot in ascending item order (a stable counting sort of z),
+//   own[i]    ll of item i under its own slot,
+//   cross     cross[r][k] = canon_sum over the members of live slot r of ll under live slot k:
+//             a merge attempt is then O(1); a split walks its cluster's members once.
+// canon_sum: 256 lane-strided partials (ascending member rank), then a pairwise tree -- the block
+// reduction both kernels use, restated by the oracle.
+#include <algorithm>
+
+#include "np8_kernels.h"
+
+namespace np8 {
+namespace {
+
+constexpr int kSmThreads = 256;
+constexpr int kMemItems = 4096;  // items per block of the member-list sort
+constexpr int kCrossTile = 8;    // live slots per cross-matrix block
+constexpr int kSplitBlocks = 8192;  // waves walking queued splits (32 per CU)
+constexpr uint32_t kStreamSmTheta = 9, kStreamSmAlloc = 10, kStreamSmAccept = 11;
+
+// ll of x under (mu, P' packed upper with doubled off-diagonals, c): the oracle's slot_ll order.
+template <int D>
+__device__ __forceinline__ double packed_ll(const double (&x)[D], const double *mu, const double *P, double c) {
+    double d[D];
+#pragma unroll
+    for (int a = 0; a < D; ++a) d[a] = x[a] - mu[a];
+    double q = 0.0;
+    int k = 0;
+#pragma unroll
+    for (int a = 0; a < D; ++a) {
+        double t = P[k++] * d[a];
+#pragma unroll
+        for (int b = a + 1; b < D; ++b) t = fma(P[k++], d[b], t);
+        q = fma(t, d[a], q);
+    }
+    return fma(-0.5, q, c);
+}
+
+// The sweep's candidate form: isotropic rows (P' = iso I) by the |d|^2 shortcut, else packed.
+template <int D>
+__device__ __forceinline__ double sm_ll(const double (&x)[D], const double *mu, const double *P, double c, double iso) {
+    if (iso > 0.0) {
+        double d0 = x[0] - mu[0];
+        double acc = d0 * d0;
+#pragma unroll
+        for (int a = 1; a < D; ++a) {
+            const double d = x[a] - mu[a];
+            acc = fma(d, d, acc);
+        }
+        return fma(-0.5, acc * iso, c);
+    }
+    return packed_ll<D>(x, mu, P, c);
+}
+
+template <int D>
+__device__ __forceinline__ void load_x(const SmArgs &A, int32_t i, double (&x)[D]) {
+#pragma unroll
+    for (int a = 0; a < D; ++a) x[a] = A.X[(int64_t)a * A.N + i];
+}
+
+// Block tree over s[0..256): s[t] += s[t + h], h = 128 .. 1.  Every thread must call it.
+__device__ __forceinline__ double tree256(double *s, double v) {
+    const int t = threadIdx.x;
+    s[t] = v;
+    __syncthreads();
+    for (int h = kSmThreads / 2; h >= 1; h >>= 1) {
+        if (t < h) s[t] += s[t + h];
+        __syncthreads();
+    }
+    const double r = s[0];
+    __syncthreads();
+    return r;
+}
+
+__device__ __forceinline__ bool sm_accept(double x, double u) { return (x >= 0.0) || !(exp_le0(x) < u); }
+
+// ---- member lists: stable counting sort of the items by slot ------------------------------------------
+__global__ __launch_bounds__(kSmThreads) void np8_sm_hist(SmArgs A) {
+    extern __shared__ int lh[];
+    for (int s = threadIdx.x; s < A.kcap; s += kSmThreads) lh[s] = 0;
+    __syncthreads();
+    const int64_t i0 = (int64_t)blockIdx.x * kMemItems;
+    for (int k = threadIdx.x; k < kMemItems; k += kSmThreads)
+        if (i0 + k < A.N) atomicAdd(&lh[A.z[i0 + k]], 1);
+    __syncthreads();
+    for (int s = threadIdx.x; s < A.kcap; s += kSmThreads) A.hist[(int64_t)s * A.nbk + blockIdx.x] = lh[s];
+}
+
+// One block of 1024: slot totals, exclusive scan over slots, per-(slot, block) bases, live list.
+__global__ __launch_bounds__(1024) void np8_sm_scan(SmArgs A) {
+    __shared__ int part[1024];
+    const int t = threadIdx.x;
+    const int per = (A.kcap + 1023) / 1024;
+    const int s0 = min(A.kcap, t * per), s1 = min(A.kcap, s0 + per);
+    int sum = 0;
+    for (int s = s0; s < s1; ++s) {
+        int tot = 0;
+        for (int b = 0; b < A.nbk; ++b) tot += A.hist[(int64_t)s * A.nbk + b];
+        A.off[s] = tot;  // temporarily the total
+        sum += tot;
+    }
+    part[t] = sum;
+    __syncthreads();
+    for (int h = 1; h < 1024; h <<= 1) {  // inclusive Hillis-Steele scan
+        const int v = (t >= h) ? part[t - h] : 0;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    int run = part[t] - sum;
+    for (int s = s0; s < s1; ++s) {
+        const int tot = A.off[s];
+        A.off[s] = run;
+        int r = run;
+        for (int b = 0; b < A.nbk; ++b) {
+            const int64_t k = (int64_t)s * A.nbk + b;
+            const int h = A.hist[k];
+            A.hist[k] = r;
+            r += h;
+        }
+        run += tot;
+        const int d = A.dense[s];
+        if (d >= 0) A.live[d] = s;
+    }
+    if (t == 1023) A.off[A.kcap] = part[1023];
+}
+
+// One wave per block of kMemItems items, 64 at a time in item order: rank among equal slots of the
+// lower lanes, the last lane of each slot advances the base.
+__global__ __launch_bounds__(64) void np8_sm_scatter(SmArgs A) {
+    extern __shared__ int base[];
+    const int lane = threadIdx.x;
+    for (int s = lane; s < A.kcap; s += 64) base[s] = A.hist[(int64_t)s * A.nbk + blockIdx.x];
+    __syncthreads();
+    const int64_t i0 = (int64_t)blockIdx.x * kMemItems;
+    for (int c = 0; c < kMemItems; c += 64) {
+        const int64_t i = i0 + c + lane;
+        const int key = (i < A.N) ? A.z[i] : -1;
+        int below = 0, above = 0;
+        for (int l = 0; l < 64; ++l) {
+            const int kl = __shfl(key, l);
+            below += (l < lane && kl == key);
+            above += (l > lane && kl == key);
+        }
+        if (key >= 0) {
+            const int pos = base[key] + below;
+            A.mem[pos] = (int32_t)i;
+        }
+        __syncthreads();
+        if (key >= 0 && above == 0) base[key] += below + 1;
+        __syncthreads();
+    }
+}
+
+// Items and own likelihoods in member order: Xm[a][p] = X[a][mem[p]], ownm[p] = ll(x | own slot).
+template <int D>
+__global__ __launch_bounds__(kSmThreads) void np8_sm_gather(SmArgs A) {
+    const int64_t p = (int64_t)blockIdx.x * kSmThreads + threadIdx.x;
+    if (p >= A.N) return;
+    const int32_t i = A.mem[p];
+    double x[D];
+    load_x<D>(A, i, x);
+#pragma unroll
+    for (int a = 0; a < D; ++a) A.Xm[(int64_t)a * A.N + p] = x[a];
+    const int s = A.z[i];
+    constexpr int DP = D * (D + 1) / 2;
+    A.ownm[p] = sm_ll<D>(x, A.slot_mu + (int64_t)s * D, A.slot_P + (int64_t)s * DP, A.slot_c[s], A.slot_iso[s]);
+}
+
+template <int D>
+__device__ __forceinline__ void load_xm(const SmArgs &A, int64_t p, double (&x)[D]) {
+#pragma unroll
+    for (int a = 0; a < D; ++a) x[a] = A.Xm[(int64_t)a * A.N + p];
+}
+
+// Block (row r, tile of kCrossTile live slots): cross[r][k0 + kk].
+template <int D>
+__global__ __launch_bounds__(kSmThreads) void np8_sm_cross(SmArgs A) {
+    constexpr int DP = D * (D + 1) / 2;
+    __shared__ double th[kCrossTile][D + DP + 2];  // mu | P' | c | iso
+    __shared__ double red[kSmThreads];
+    const int r = blockIdx.x, k0 = blockIdx.y * kCrossTile;
+    const int nk = min(kCrossTile, A.K - k0);
+    for (int e = threadIdx.x; e < kCrossTile * (D + DP + 2); e += kSmThreads) {
+        const int kk = e / (D + DP + 2), f = e - kk * (D + DP + 2);
+        const int s = A.live[min(k0 + kk, A.K - 1)];  // padding rows repeat the last slot (unused)
+        th[kk][f] = (f < D) ? A.slot_mu[(int64_t)s * D + f]
+                            : (f < D + DP ? A.slot_P[(int64_t)s * DP + (f - D)]
+                                          : (f == D + DP ? A.slot_c[s] : A.slot_iso[s]));
+    }
+    __syncthreads();
+    const int sr = A.live[r];
+    const int b = A.off[sr], n = A.off[sr + 1] - b;
+    double acc[kCrossTile];
+#pragma unroll
+    for (int kk = 0; kk < kCrossTile; ++kk) acc[kk] = 0.0;
+    for (int p = threadIdx.x; p < n; p += kSmThreads) {
+        double x[D];
+        load_xm<D>(A, b + p, x);
+#pragma unroll
+        for (int kk = 0; kk < kCrossTile; ++kk) {
+            // re-read the parameters from LDS for every member (hoisting 8 x 45 doubles would spill)
+            __asm__ __volatile__("" ::: "memory");
+            acc[kk] += sm_ll<D>(x, &th[kk][0], &th[kk][D], th[kk][D + DP], th[kk][D + DP + 1]);
+        }
+    }
+#pragma unroll
+    for (int kk = 0; kk < kCrossTile; ++kk) {
+        const double v = tree256(red, acc[kk]);
+        if (kk < nk && threadIdx.x == 0) A.cross[(int64_t)r * A.K + k0 + kk] = v;
+    }
+}
+
+// ---- attempts ----------------------------------------------------------------------------------------------
+// Outcome codes as np8o_sm_sweep: 0 skipped, 1 split rejected, 2 merge rejected, 3 split accepted,
+// 4 merge accepted, 5 split rejected for want of a free slot; kPending: a split not evaluated (its
+// attempt lies after an accepted one).
+constexpr uint8_t kPending = 255;
+
+struct Pair {
+    int32_t i, j, ci, cj;
+};
+
+__device__ __forceinline__ Pair sm_pair(const SmArgs &A, int64_t a) {
+    Pair q;
+    q.i = (int32_t)perm_apply(A.perm0, (uint32_t)a);
+    q.j = (int32_t)perm_apply(A.perm1, (uint32_t)a);
+    q.ci = A.z[q.i];
+    q.cj = A.z[q.j];
+    return q;
+}
+
+// merge ci into cj (np_jain_neal_algorithm.cpp:353-429): O(1) from the cross matrix
+__device__ __forceinline__ bool sm_merge_accept(const SmArgs &A, const Pair &q, int64_t a) {
+    const int r0 = A.dense[q.ci], r1 = A.dense[q.cj];
+    const double lsrc = A.cross[(int64_t)r0 * A.K + r0], ldest = A.cross[(int64_t)r0 * A.K + r1];
+    const int n0 = A.off[q.ci + 1] - A.off[q.ci], n1 = A.off[q.cj + 1] - A.off[q.cj];
+    const double pr = A.log_alpha + lgamma_int(n0) + lgamma_int(n1) - lgamma_int((int64_t)n0 + n1);
+    return sm_accept(-pr + (ldest - lsrc), uniform(A.seed, (uint64_t)a, A.t, kStreamSmAccept, 0));
+}
+
+// The new cluster of split attempt a: a G0 draw (v, mu) on stream SM_THETA (the oracle's sm_theta).
+template <int D>
+__device__ void sm_theta(const SmArgs &A, int64_t a, double *vmu) {
+    double g[4 * ((D + 4) / 4)];
+    for (int call = 0; call < g0_calls(D); ++call) {
+        double q[4];
+        normal_quad(A.seed, (uint64_t)a, A.t, kStreamSmTheta, (uint32_t)call, q);
+        for (int e = 0; e < 4; ++e) g[4 * call + e] = q[e];
+    }
+    const double v = fma(A.nu, g[0], (double)D);
+    const double sc = fabs(v) * A.rsk;
+    for (int aa = 0; aa < D; ++aa) {
+        double t0 = A.LT[aa * D + aa] * g[1 + aa];
+        for (int bb = aa + 1; bb < D; ++bb) t0 = fma(A.LT[aa * D + bb], g[1 + bb], t0);
+        vmu[1 + aa] = fma(sc, t0, A.mu0[aa]);
+    }
+    vmu[0] = v;
+}
+
+// One thread per attempt: pairs, skips and merges decided here, splits queued (with their new
+// cluster's G0 draw) for np8_sm_split.
+template <int D>
+__global__ __launch_bounds__(kSmThreads) void np8_sm_classify(SmArgs A) {
+    const int q = blockIdx.x * kSmThreads + threadIdx.x;
+    if (q >= A.nb) return;
+    const int64_t a = A.a0 + q;
+    const Pair p = sm_pair(A, a);
+    uint8_t out;
+    if (p.i == p.j) {
+        out = 0;
+    } else if (p.ci != p.cj) {
+        out = sm_merge_accept(A, p, a) ? 4 : 2;
+        if (out == 4) atomicMin(reinterpret_cast<unsigned long long *>(&A.sc->first), (unsigned long long)a);
+    } else {
+        out = kPending;
+        const int e = atomicAdd(&A.sc->nsplit, 1);
+        A.slist[e] = a;
+        sm_theta<D>(A, a, A.stheta + (int64_t)e * (D + 1));
+    }
+    A.typ[q] = out;
+}
+
+// Split of the common cluster c of (i, j) (np_jain_neal_algorithm.cpp:251-351), one wave.  The new
+// cluster is a G0 draw.  Members are visited in ascending item order, 64 per step, one per lane: each
+// lane computes its member's likelihood under the new cluster and its allocation uniform, then the
+// wave resolves the sequential allocation (:146-171) of the 64 by fixpoint iteration: a lane's
+// decision depends only on the decisions of the lanes before it (through the set sizes), so
+// re-deciding every lane from the previous round's prefix counts fixes at least one more lane per
+// round and stops at the unique fixpoint -- the sequential result, usually after 2 rounds.  Masked
+// sums go to 256 canonical partials (member rank mod 256) reduced by canon_sum's tree.
+// APPLY: write the moves.
+template <int D, bool APPLY>
+__device__ int sm_split(const SmArgs &A, const FinArgs *F, const Pair &pq, int64_t a, const double *vmu) {
+    constexpr int DP = D * (D + 1) / 2;
+    __shared__ double s_red[2][256];
+    __shared__ double s_th[D + DP + 3];  // mu' | P' | c' | v | iso'
+    __shared__ int s_new_slot;
+    const int lane = threadIdx.x;
+    const int ci = pq.ci;
+    if (lane == 0) {
+        const double v = vmu[0];
+        for (int aa = 0; aa < D; ++aa) s_th[aa] = vmu[1 + aa];
+        const double v2 = v * v;
+#pragma unroll 1
+        for (int k = 0; k < DP; ++k) s_th[D + k] = A.Gp[k] / v2;
+        s_th[D + DP] = fma(-(double)D, log_pos(fabs(v)), A.caux);
+        s_th[D + DP + 1] = v;
+        s_th[D + DP + 2] = (A.gp_iso > 0.0) ? A.gp_iso / v2 : 0.0;
+        if (APPLY) {
+            int s = -1;
+            for (int k = 0; k < A.kcap; ++k)
+                if (A.cnt[k] == 0) {
+                    s = k;
+                    break;
+                }
+            s_new_slot = s;
+        }
+    }
+    __syncthreads();
+    const int snew = APPLY ? s_new_slot : -1;
+    const int b0 = A.off[ci], n0 = A.off[ci + 1] - b0;
+    const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));  // lanes < this one
+    double dm = 1.0, dr = 1.0;  // sizes of the move (holds i) and remain (holds j) sets, wave-uniform
+    double ps[4] = {0.0, 0.0, 0.0, 0.0}, pd[4] = {0.0, 0.0, 0.0, 0.0};  // partials lane + 64 k
+    for (int cb = 0; cb < n0; cb += 64) {
+        const int k = (cb >> 6) & 3;
+        {
+            const int p = cb + lane;
+            const bool valid = p < n0;
+            int32_t id = -1;
+            double own = 0.0, nw = 0.0, u = 0.0;
+            if (valid) {
+                __asm__ __volatile__("" ::: "memory");  // the new cluster's P' stays in LDS (occupancy)
+                double x[D];
+                load_xm<D>(A, b0 + p, x);
+                id = A.mem[b0 + p];
+                own = A.ownm[b0 + p];
+                nw = sm_ll<D>(x, s_th, s_th + D, s_th[D + DP], s_th[D + DP + 2]);
+                u = uniform(A.seed, (uint64_t)a, A.t, kStreamSmAlloc, (uint32_t)p);
+            }
+            const bool isI = id == pq.i, isJ = id == pq.j;
+            const bool regular = valid && !isI && !isJ;
+            const uint64_t reg = __ballot(regular);
+            const int cnt = __popcll(reg & below);
+            uint64_t mv = 0;  // regular lanes that move, as last decided
+            for (int it = 0; it <= 64; ++it) {
+                const int dl = __popcll(mv & below);
+                const double a0 = own + (dr + (double)(cnt - dl)), a1 = nw + (dm + (double)dl);
+                const double tot = a0 + a1;
+                const double w = u * tot;
+                const bool d = regular && ((tot < w) || (a0 < w));  // lower_bound over {a0, a0 + a1} > 0
+                const uint64_t nmv = __ballot(d);
+                if (nmv == mv) break;  // wave-uniform
+                mv = nmv;
+            }
+            const bool moves = isI || ((mv >> lane) & 1ull);
+            const int nm = __popcll(mv);
+            dm += (double)nm;
+            dr += (double)(__popcll(reg) - nm);
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) {  // static register indices
+                ps[kk] = (moves && kk == k) ? ps[kk] + own : ps[kk];
+                pd[kk] = (moves && kk == k) ? pd[kk] + nw : pd[kk];
+            }
+            if (APPLY && moves && snew >= 0) A.z[id] = snew;
+        }
+    }
+    // canon_sum: partial t = lane + 64 k, then the pairwise tree
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        s_red[0][lane + 64 * k] = ps[k];
+        s_red[1][lane + 64 * k] = pd[k];
+    }
+    __syncthreads();
+    for (int h = 128; h >= 1; h >>= 1) {
+        for (int t = lane; t < h; t += 64) {
+            s_red[0][t] += s_red[0][t + h];
+            s_red[1][t] += s_red[1][t + h];
+        }
+        __syncthreads();
+    }
+    const double lsrc = s_red[0][0], ldest = s_red[1][0];
+    const int64_t m = (int64_t)dm, r = (int64_t)dr;
+    int out = 1;
+    if (lane == 0) {
+        const double pr = A.log_alpha + lgamma_int(m) + lgamma_int(r) - lgamma_int(n0);
+        const bool acc = sm_accept(pr + (ldest - lsrc), uniform(A.seed, (uint64_t)a, A.t, kStreamSmAccept, 0));
+        out = !acc ? 1 : (A.K < A.kcap ? 3 : 5);
+        if (APPLY && out == 3 && snew >= 0) {
+            write_new_slot(*F, vmu, snew);
+            if (F->wdirty) F->wdirty[snew] = 1;
+            A.cnt[ci] -= (int32_t)m;
+            A.cnt[snew] = (int32_t)m;
+        }
+    }
+    __syncthreads();
+    return out;  // lane 0's value
+}
+
+// The queued splits of the batch, one wave each (persistent over the queue); a split after an
+// already accepted attempt is left pending -- the batch restarts before it.
+template <int D>
+__global__ __launch_bounds__(64) void np8_sm_split(SmArgs A) {
+    const int ns = A.sc->nsplit;
+    for (int e = blockIdx.x; e < ns; e += gridDim.x) {
+        const int64_t a = A.slist[e];
+        unsigned long long first = 0;
+        if (threadIdx.x == 0) first = *reinterpret_cast<volatile unsigned long long *>(&A.sc->first);
+        first = __shfl(first, 0);
+        if ((unsigned long long)a > first) continue;  // wave-uniform
+        const Pair p = sm_pair(A, a);
+        const int out = sm_split<D, false>(A, nullptr, p, a, A.stheta + (int64_t)e * (D + 1));
+        if (threadIdx.x == 0) {
+            A.typ[a - A.a0] = (uint8_t)out;
+            if (out == 3) atomicMin(reinterpret_cast<unsigned long long *>(&A.sc->first), (unsigned long long)a);
+        }
+    }
+}
+
+// Outcome counts of the attempts up to and including the first accepted one (grid-stride, one
+// 64-bit atomic per block and outcome).
+__global__ __launch_bounds__(kSmThreads) void np8_sm_tally(SmArgs A) {
+    __shared__ int cnt[6];
+    if (threadIdx.x < 6) cnt[threadIdx.x] = 0;
+    __syncthreads();
+    const int64_t first = A.sc->first;
+    const int lim = (first == INT64_MAX) ? A.nb : (int)(first - A.a0 + 1);
+    int c[6] = {0, 0, 0, 0, 0, 0};
+    for (int q = blockIdx.x * kSmThreads + threadIdx.x; q < lim; q += gridDim.x * kSmThreads) {
+        const uint8_t t = A.typ[q];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) c[k] += (t == k);
+    }
+#pragma unroll
+    for (int k = 0; k < 6; ++k)
+        if (c[k]) atomicAdd(&cnt[k], c[k]);
+    __syncthreads();
+    if (threadIdx.x < 6 && cnt[threadIdx.x])
+        atomicAdd(reinterpret_cast<unsigned long long *>(&A.sc->stats[threadIdx.x]), (unsigned long long)cnt[threadIdx.x]);
+}
+
+// The batch's first accepted attempt, re-evaluated by one wave and applied.
+template <int D>
+__global__ __launch_bounds__(64) void np8_sm_apply(SmArgs A, FinArgs F, int64_t a) {
+    const Pair p = sm_pair(A, a);
+    __syncthreads();  // the apply rewrites z: every lane has read z[i], z[j] first
+    int out;
+    if (p.i == p.j) {
+        out = 0;
+    } else if (p.ci != p.cj) {
+        out = sm_merge_accept(A, p, a) ? 4 : 2;
+        if (out == 4) {
+            const int b0 = A.off[p.ci], n0 = A.off[p.ci + 1] - b0;
+            for (int q = threadIdx.x; q < n0; q += 64) A.z[A.mem[b0 + q]] = p.cj;
+            if (threadIdx.x == 0) {
+                A.cnt[p.cj] += n0;
+                A.cnt[p.ci] = 0;
+            }
+        }
+    } else {
+        __shared__ double vmu[D + 1];
+        if (threadIdx.x == 0) sm_theta<D>(A, a, vmu);
+        __syncthreads();
+        out = sm_split<D, true>(A, &F, p, a, vmu);
+    }
+    if (threadIdx.x == 0 && out != 3 && out != 4) F.ctl->err |= kErrCapacity;  // cannot happen: re-evaluation
+}
+
+__global__ void np8_sm_reset(SmCtl *sc) {
+    sc->first = INT64_MAX;
+    sc->nsplit = 0;
+}
+
+}  // namespace
+}  // namespace np8
+
+using namespace np8;
+
+#define NP8_SM_FOR_EACH_D(X) X(1) X(2) X(3) X(4) X(8) X(16)
+
+hipError_t np8_launch_sm_members(const SmArgs &A, hipStream_t s) {
+    if (A.N <= 0) return hipSuccess;
+    hipLaunchKernelGGL(np8_sm_hist, dim3(A.nbk), dim3(kSmThreads), sizeof(int) * A.kcap, s, A);
+    hipLaunchKernelGGL(np8_sm_scan, dim3(1), dim3(1024), 0, s, A);
+    hipLaunchKernelGGL(np8_sm_scatter, dim3(A.nbk), dim3(64), sizeof(int) * A.kcap, s, A);
+    const dim3 gi((unsigned)((A.N + kSmThreads - 1) / kSmThreads));
+    const dim3 gc((unsigned)A.K, (unsigned)((A.K + kCrossTile - 1) / kCrossTile));
+#define X(d)                                                                                \
+    if (A.D == d) {                                                                         \
+        hipLaunchKernelGGL(np8_sm_gather<d>, gi, dim3(kSmThreads), 0, s, A);                \
+        if (A.K > 0) hipLaunchKernelGGL(np8_sm_cross<d>, gc, dim3(kSmThreads), 0, s, A);    \
+        return hipGetLastError();                                                           \
+    }
+    NP8_SM_FOR_EACH_D(X)
+#undef X
+    return hipErrorInvalidValue;
+}
+
+hipError_t np8_launch_sm_eval(const SmArgs &A, hipStream_t s) {
+    if (A.nb <= 0) return hipSuccess;
+    hipLaunchKernelGGL(np8_sm_reset, dim3(1), dim3(1), 0, s, A.sc);
+    const unsigned gs = (unsigned)std::min(A.nb, kSplitBlocks);
+    const dim3 gq((unsigned)((A.nb + kSmThreads - 1) / kSmThreads));
+#define X(d)                                                                   \
+    if (A.D == d) {                                                            \
+        hipLaunchKernelGGL(np8_sm_classify<d>, gq, dim3(kSmThreads), 0, s, A); \
+        hipLaunchKernelGGL(np8_sm_split<d>, dim3(gs), dim3(64), 0, s, A);      \
+        hipLaunchKernelGGL(np8_sm_tally, dim3(256), dim3(kSmThreads), 0, s, A); \
+        return hipGetLastError();                                              \
+    }
+    NP8_SM_FOR_EACH_D(X)
+#undef X
+    return hipErrorInvalidValue;
+}
+
+hipError_t np8_launch_sm_apply(const SmArgs &A, const FinArgs &F, int64_t a, hipStream_t s) {
+#define X(d)                                                                    \
+    if (A.D == d) {                                                             \
+        hipLaunchKernelGGL(np8_sm_apply<d>, dim3(1), dim3(64), 0, s, A, F, a);  \
+        return hipGetLastError();                                               \
+    }
+    NP8_SM_FOR_EACH_D(X)
+#undef X
+    return hipErrorInvalidValue;
+}

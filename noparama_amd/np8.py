@@ -89,6 +89,10 @@ class Stats(C.Structure):
         ("n_timed_finalize", C.c_int64),
         ("n_timed_loglik", C.c_int64),
         ("n_timed_params", C.c_int64),
+        ("ms_sm_members", C.c_double),
+        ("ms_sm_eval", C.c_double),
+        ("n_timed_sm_members", C.c_int64),
+        ("n_timed_sm_eval", C.c_int64),
     ]
 
 
@@ -137,6 +141,8 @@ def lib():
         "np8_param_stats_bytes": ([vp], i64),
         "np8_param_stats_local": ([vp, vp], i32),
         "np8_end_sweep_stats": ([vp, vp], i32),
+        "np8_sm_sweep": ([vp, i32], i32),
+        "np8_sm_stats": ([vp, vp], i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -250,6 +256,19 @@ class NealAlgorithm8:
     def sync(self):
         self._check(lib().np8_sync(self._h))
 
+    def sm_sweep(self, n=1):
+        """n Jain-Neal split-merge sweeps (np8_sm_sweep): N split/merge attempts each, then the
+        end-of-sweep step.  Synchronous."""
+        self._check(lib().np8_sm_sweep(self._h, int(n)))
+
+    def sm_stats(self):
+        """Cumulative split-merge outcomes: skipped, split_rejected, merge_rejected, split_accepted,
+        merge_accepted, split_no_slot (np8_sm_stats)."""
+        out = np.zeros(6, dtype=np.int64)
+        self._check(lib().np8_sm_stats(self._h, _p(out)))
+        return dict(zip(("skipped", "split_rejected", "merge_rejected", "split_accepted", "merge_accepted",
+                         "split_no_slot"), (int(v) for v in out)))
+
     def update_points(self, ids):
         ids = np.ascontiguousarray(ids, dtype=np.int64)
         self._check(lib().np8_update_points(self._h, _p(ids), ids.size))
@@ -342,6 +361,39 @@ class NealAlgorithm8:
         print("Statistics:")
         print(f" # of new cluster events accepted: {s['new_clusters']}")
         print(f" # of rejected new-cluster requests: {s['rejected_requests']}")
+
+
+class JainNealAlgorithm(NealAlgorithm8):
+    """The reference's split-merge population update (class JainNealAlgorithm,
+    include/np_jain_neal_algorithm.h:52-98; `-a jain_neal_split`) on the same device context: one
+    sweep = N split/merge attempts on the item pairs of two scan permutations (np_mcmc.cpp:117-164),
+    then the end-of-sweep parameter step and max-likelihood check.  Reference prior, fp64 contraction,
+    one rank.  The Gibbs sweep of the base class stays available (sweep_gibbs)."""
+
+    def sweep(self, n=1, sync=True):
+        self.sm_sweep(n)
+
+    def sweep_gibbs(self, n=1, sync=True):
+        NealAlgorithm8.sweep(self, n, sync)
+
+    def update(self, cluster_matrix, data_ids):
+        """UpdateClusterPopulation::update at sweep granularity: data_ids must be a permutation of all
+        items (the pairs of one sweep come from the library's own permutations).  The reference's
+        per-pair call (np_jain_neal_algorithm.cpp:424) has no sweep-parallel form."""
+        ids = np.asarray(data_ids, dtype=np.int64).reshape(-1)
+        if not (ids.size == self.N and np.array_equal(np.sort(ids), np.arange(self.N))):
+            raise ValueError("JainNealAlgorithm.update: pass a permutation of all items (one split-merge sweep)")
+        self.sm_sweep(1)
+        if cluster_matrix is not None:
+            cluster_matrix.load(self.state(params=False))
+
+    def printStatistics(self):
+        s = self.sm_stats()
+        print("Statistics:")
+        print(f" # of merge attempts: {s['merge_accepted'] + s['merge_rejected']}")
+        print(f"   o of accepted merge cluster events: {s['merge_accepted']}")
+        print(f" # of split attempts: {s['split_accepted'] + s['split_rejected'] + s['split_no_slot']}")
+        print(f"   o of accepted split cluster events: {s['split_accepted']}")
 
 
 class membertrix:

@@ -405,6 +405,12 @@ struct np8o_ctx {
     int64_t *rq_pos, *rq_i;
     int32_t *rq_m, *rq_zold;
     int64_t mh_accepted;
+    /* split-merge (np8o_sm_sweep): member lists, per-member scratch, outcome counts */
+    int64_t *sm_off, *sm_cur, *sm_mem;
+    double *sm_v0, *sm_v1;
+    unsigned char *sm_flag;
+    int64_t sm_stats[6];
+    double sm_log_alpha;
 };
 
 static int packed_index(int D, int a, int b) { /* upper triangle, row-major, a <= b */
@@ -547,6 +553,9 @@ np8o_ctx *np8o_create(const np8o_config *cfg) {
     c->mu_best = (double *)calloc((size_t)K * D, sizeof(double));
     c->sigma_best = (double *)calloc((size_t)K * D * D, sizeof(double));
     c->delta = (int32_t *)calloc((size_t)K, sizeof(int32_t));
+    c->sm_off = (int64_t *)calloc((size_t)K + 1, sizeof(int64_t));
+    c->sm_cur = (int64_t *)calloc((size_t)K, sizeof(int64_t));
+    c->sm_log_alpha = log(cfg->alpha);
     if (cfg->contraction == NP8O_CONTRACT_F32) {
         c->wA = (float *)calloc((size_t)K * D * D, sizeof(float));
         c->wmu = (float *)calloc((size_t)K * D, sizeof(float));
@@ -582,6 +591,12 @@ void np8o_destroy(np8o_ctx *c) {
     free(c->rq_i);
     free(c->rq_m);
     free(c->rq_zold);
+    free(c->sm_off);
+    free(c->sm_cur);
+    free(c->sm_mem);
+    free(c->sm_v0);
+    free(c->sm_v1);
+    free(c->sm_flag);
     free(c);
 }
 
@@ -593,6 +608,10 @@ int np8o_set_data(np8o_ctx *c, const double *X, int64_t N) {
     free(c->rq_i);
     free(c->rq_m);
     free(c->rq_zold);
+    free(c->sm_mem);
+    free(c->sm_v0);
+    free(c->sm_v1);
+    free(c->sm_flag);
     c->N = N;
     c->X = (double *)malloc(sizeof(double) * (size_t)(N > 0 ? N : 1) * c->D);
     if (N > 0) memcpy(c->X, X, sizeof(double) * (size_t)N * c->D);
@@ -604,6 +623,10 @@ int np8o_set_data(np8o_ctx *c, const double *X, int64_t N) {
     c->rq_i = (int64_t *)malloc(sizeof(int64_t) * (size_t)(N > 0 ? N : 1));
     c->rq_m = (int32_t *)malloc(sizeof(int32_t) * (size_t)(N > 0 ? N : 1));
     c->rq_zold = (int32_t *)malloc(sizeof(int32_t) * (size_t)(N > 0 ? N : 1));
+    c->sm_mem = (int64_t *)malloc(sizeof(int64_t) * (size_t)(N > 0 ? N : 1));
+    c->sm_v0 = (double *)malloc(sizeof(double) * (size_t)(N > 0 ? N : 1));
+    c->sm_v1 = (double *)malloc(sizeof(double) * (size_t)(N > 0 ? N : 1));
+    c->sm_flag = (unsigned char *)malloc((size_t)(N > 0 ? N : 1));
     return 0;
 }
 
@@ -1763,4 +1786,218 @@ int np8o_loglik_matrix_ref(np8o_ctx *c, const int64_t *idx, int64_t n, double *o
                 np8o_mvn_logprobability_ref(x, amu + (size_t)m * D, asig + (size_t)m * D * D, D);
     }
     return 0;
+}
+
+/* ================================================================================================
+ * Jain-Neal split-merge: src/np_jain_neal_algorithm.cpp driven by
+ * src/np_mcmc.cpp:117-164 with subset_count = 2 (src/np_main.cpp:440-445).  One sweep = N attempts;
+ * attempt a takes the pair (pi0(a), pi1(a)) of two independent scan permutations (np_mcmc.cpp:118-125,
+ * 142-148; a pair with equal items is skipped, :153-156).  Same cluster: split (:251-351) with the
+ * sams_prior allocation (:146-171); different clusters: merge of the first item's cluster into the
+ * second's (:353-429).  The reference's own rules are kept (DESIGN.md "Split-merge"): the SAMS weights
+ * are log-likelihood + count fed to the linear-weight pick (:157-168 with dim1algebra.hpp:2078-2104,
+ * including lower_bound on a non-monotone cumulative sum), the proposal ratio is 0 (:57-59) and the
+ * acceptance is exp(q + p + lratio) >= u (:306-316, :398-408).  Members are visited in ascending item
+ * order (the reference shuffles them, :121; the data are permuted at load, np_main.cpp:283-295);
+ * sums over members use canon_sum (256 lane-strided partials, then a pairwise tree) -- the order the
+ * device reduces in.  The cluster log-likelihoods use the sweep's candidate form (isotropic rows by
+ * the |d|^2 shortcut, others by the packed table form).
+ * ============================================================================================== */
+static const double kLgammaTab[33] = {
+    0.0, /* unused: n >= 1 */
+    0.0, 0.0, 0.693147180559945, 1.7917594692280554, 3.178053830347945, 4.787491742782047,
+    6.579251212010102, 8.525161361065415, 10.604602902745249, 12.801827480081467, 15.104412573075514,
+    17.502307845873887, 19.987214495661885, 22.55216385312342, 25.191221182738683, 27.89927138384089,
+    30.671860106080672, 33.50507345013689, 36.39544520803305, 39.339884187199495, 42.335616460753485,
+    45.38013889847691, 48.47118135183522, 51.60667556776438, 54.78472939811232, 58.00360522298052,
+    61.26170176100201, 64.55753862700634, 67.88974313718153, 71.257038967168, 74.65823634883017,
+    78.0922235533153};
+
+/* log Gamma(n) for an integer n >= 1 (std::lgamma at np_jain_neal_algorithm.cpp:48): table to 32,
+ * Stirling's series beyond (truncation error < 1e-17 relative for n > 32). */
+double np8o_lgamma_int(int64_t n) {
+    if (n <= 32) return kLgammaTab[n < 1 ? 1 : n];
+    const double x = (double)n;
+    const double r = 1.0 / x, r2 = r * r;
+    const double s = r * (0.083333333333333333 - r2 * (0.0027777777777777778 - r2 * (0.00079365079365079365 - r2 * 0.00059523809523809524)));
+    return ((x - 0.5) * np8o_log_pos(x) - x) + 0.91893853320467274178 + s;
+}
+
+/* Canonical sum of v[0..n) (only entries with keep[p] != 0 when keep is given): partial t sums
+ * p = t, t+256, .. in ascending order, then partial[t] += partial[t+h] for h = 128, 64, .., 1. */
+static double canon_sum(const double *v, const unsigned char *keep, int64_t n) {
+    double part[256];
+    for (int t = 0; t < 256; ++t) part[t] = 0.0;
+    for (int64_t p = 0; p < n; ++p)
+        if (!keep || keep[p]) part[p & 255] += v[p];
+    for (int h = 128; h >= 1; h >>= 1)
+        for (int t = 0; t < h; ++t) part[t] += part[t + h];
+    return part[0];
+}
+
+double np8o_canon_sum(const double *v, int64_t n) { return canon_sum(v, NULL, n); }
+
+static const uint64_t kSmPermKey[2] = {0x4A4E53504C495430ull, 0x4A4E53504C495431ull};
+
+/* Members of every slot in ascending item order: mem[off[s] .. off[s+1]). */
+static void sm_members(np8o_ctx *c) {
+    int64_t *off = c->sm_off;
+    for (int s = 0; s <= c->kcap; ++s) off[s] = 0;
+    for (int64_t i = 0; i < c->N; ++i) off[c->z[i] + 1]++;
+    for (int s = 0; s < c->kcap; ++s) off[s + 1] += off[s];
+    int64_t *cur = c->sm_cur;
+    for (int s = 0; s < c->kcap; ++s) cur[s] = off[s];
+    for (int64_t i = 0; i < c->N; ++i) c->sm_mem[cur[c->z[i]]++] = i;
+}
+
+/* Cluster log-likelihood of the split-merge moves: the sweep's candidate form (cand_ll) -- the
+ * isotropic shortcut for rows whose P' is a multiple of I, else the packed quadratic form. */
+static double sm_iso_ll(const double *x, const double *mu, int D, double iso, double cc) {
+    double d0 = x[0] - mu[0];
+    double acc = d0 * d0;
+    for (int a = 1; a < D; ++a) {
+        const double d = x[a] - mu[a];
+        acc = fma(d, d, acc);
+    }
+    return fma(-0.5, acc * iso, cc);
+}
+
+static double sm_slot_ll(const np8o_ctx *c, const double *x, int s) {
+    const double iso = c->iso[c->dense_of[s]];
+    if (iso > 0.0) return sm_iso_ll(x, c->slot_mu + (size_t)s * c->D, c->D, iso, c->slot_c[s]);
+    return slot_ll(c, x, s);
+}
+
+/* Gp = (L^T L)^{-1} a multiple of I: its diagonal, else 0 (the new slots' isotropic factor). */
+static double sm_gp_iso(const np8o_ctx *c) {
+    const int D = c->D;
+    for (int a = 0; a < D; ++a)
+        for (int b = 0; b < D; ++b)
+            if ((a == b) ? c->Gp[a * D + b] != c->Gp[0] : c->Gp[a * D + b] != 0.0) return 0.0;
+    return c->Gp[0];
+}
+
+/* accept iff exp(x) >= u (x > 0: always) */
+static int sm_accept(double x, double u) { return (x >= 0.0) || !(np8o_exp_le0(x) < u); }
+
+/* The new cluster of a split attempt: a G0 draw on stream SM_THETA (i = attempt, t = epoch). */
+static void sm_theta(const np8o_ctx *c, uint64_t a, double *v, double *mu) {
+    double g[NP8O_DMAX + 4];
+    for (int call = 0; call < g0_calls(c->D); ++call)
+        normal_quad(c->cfg.seed, a, c->t, NP8O_STREAM_SM_THETA, (uint32_t)call, g + 4 * call);
+    aux_from_normals(c, g[0], g + 1, v, mu);
+}
+
+/* One attempt.  Returns 0 skipped, 1 split rejected, 2 merge rejected, 3 split accepted,
+ * 4 merge accepted, 5 split rejected for want of a free slot. */
+static int sm_attempt(np8o_ctx *c, uint64_t a) {
+    const int D = c->D;
+    const uint32_t N = (uint32_t)c->N;
+    const int64_t i = np8o_perm(c->cfg.seed ^ kSmPermKey[0], c->t, N, (uint32_t)a);
+    const int64_t j = np8o_perm(c->cfg.seed ^ kSmPermKey[1], c->t, N, (uint32_t)a);
+    if (i == j) return 0;
+    const int ci = c->z[i], cj = c->z[j];
+    const double u_acc = np8o_uniform(c->cfg.seed, a, c->t, NP8O_STREAM_SM_ACCEPT, 0);
+    const int64_t *L = c->sm_mem + c->sm_off[ci];
+    const int64_t n0 = c->sm_off[ci + 1] - c->sm_off[ci];
+    double *own = c->sm_v0, *nw = c->sm_v1;
+    if (ci != cj) { /* merge ci into cj */
+        for (int64_t p = 0; p < n0; ++p) {
+            const double *x = c->X + (size_t)L[p] * D;
+            own[p] = sm_slot_ll(c, x, ci);
+            nw[p] = sm_slot_ll(c, x, cj);
+        }
+        const double lsrc = canon_sum(own, NULL, n0), ldest = canon_sum(nw, NULL, n0);
+        const int64_t n1 = c->cnt[cj];
+        const double pr = c->sm_log_alpha + np8o_lgamma_int(n0) + np8o_lgamma_int(n1) - np8o_lgamma_int(n0 + n1);
+        if (!sm_accept(-pr + (ldest - lsrc), u_acc)) return 2;
+        for (int64_t p = 0; p < n0; ++p) c->z[L[p]] = cj;
+        c->cnt[cj] += (int32_t)n0;
+        c->cnt[ci] = 0;
+        return 4;
+    }
+    /* split: the move set starts with i, the remaining set with j */
+    double v, mu[NP8O_DMAX];
+    sm_theta(c, a, &v, mu);
+    double Pn[NP8O_DMAX * (NP8O_DMAX + 1) / 2];
+    const double v2 = v * v;
+    for (int q = 0, aa = 0; aa < D; ++aa)
+        for (int b = aa; b < D; ++b, ++q) Pn[q] = c->Gp[aa * D + b] / v2;
+    const double cn = fma(-(double)D, np8o_log_pos(fabs(v)), c->caux);
+    const double gi = sm_gp_iso(c), isn = (gi > 0.0) ? gi / v2 : 0.0;
+    unsigned char *mv = c->sm_flag;
+    int64_t m = 1, r = 1;
+    for (int64_t p = 0; p < n0; ++p) {
+        const double *x = c->X + (size_t)L[p] * D;
+        own[p] = sm_slot_ll(c, x, ci);
+        nw[p] = (isn > 0.0) ? sm_iso_ll(x, mu, D, isn, cn) : fma(-0.5, quad_form(c, x, mu, Pn), cn);
+        if (L[p] == i) {
+            mv[p] = 1;
+            continue;
+        }
+        if (L[p] == j) {
+            mv[p] = 0;
+            continue;
+        }
+        const double a0 = own[p] + (double)r, a1 = nw[p] + (double)m;
+        const double tot = a0 + a1;
+        const double w = np8o_uniform(c->cfg.seed, a, c->t, NP8O_STREAM_SM_ALLOC, (uint32_t)p) * tot;
+        const int idx = (tot < w) ? 2 : ((a0 < w) ? 1 : 0); /* std::lower_bound over {a0, a0+a1} */
+        mv[p] = (unsigned char)(idx != 0);
+        if (idx != 0)
+            ++m;
+        else
+            ++r;
+    }
+    const double lsrc = canon_sum(own, mv, n0), ldest = canon_sum(nw, mv, n0);
+    const double pr = c->sm_log_alpha + np8o_lgamma_int(m) + np8o_lgamma_int(r) - np8o_lgamma_int(n0);
+    if (!sm_accept(pr + (ldest - lsrc), u_acc)) return 1;
+    int s = -1;
+    for (int k = 0; k < c->kcap; ++k)
+        if (c->cnt[k] == 0) {
+            s = k;
+            break;
+        }
+    if (s < 0) return 5;
+    slot_from_aux(c, s, v, mu);
+    for (int64_t p = 0; p < n0; ++p)
+        if (mv[p]) c->z[L[p]] = s;
+    c->cnt[ci] -= (int32_t)m;
+    c->cnt[s] = (int32_t)m;
+    return 3;
+}
+
+int np8o_sm_sweep(np8o_ctx *c, int32_t n) {
+    if (c->cfg.prior != NP8O_PRIOR_REFERENCE || c->cfg.contraction != NP8O_CONTRACT_F64) return -1;
+    for (int s = 0; s < n; ++s) {
+        sm_members(c);
+        for (int64_t a = 0; a < c->N; ++a) {
+            const int o = sm_attempt(c, (uint64_t)a);
+            c->sm_stats[o]++;
+            if (o == 3 || o == 4) {
+                rebuild_dense(c);
+                sm_members(c);
+            }
+        }
+        np8o_end_sweep(c);
+    }
+    return 0;
+}
+
+int np8o_sm_attempts(np8o_ctx *c, int64_t a0, int64_t a1) {
+    if (c->cfg.prior != NP8O_PRIOR_REFERENCE || c->cfg.contraction != NP8O_CONTRACT_F64) return -1;
+    sm_members(c);
+    for (int64_t a = a0; a < a1 && a < c->N; ++a) {
+        const int o = sm_attempt(c, (uint64_t)a);
+        c->sm_stats[o]++;
+        if (o == 3 || o == 4) {
+            rebuild_dense(c);
+            sm_members(c);
+        }
+    }
+    return 0;
+}
+
+void np8o_sm_get_stats(np8o_ctx *c, int64_t out[6]) {
+    for (int k = 0; k < 6; ++k) out[k] = c->sm_stats[k];
 }

@@ -47,7 +47,10 @@ enum {
     NP8O_STREAM_PARAM_U = 6, /* MH acceptance uniform: i = slot, call = step */
     NP8O_STREAM_AUX_DIR = 7, /* direction of a picked auxiliary's xi orthogonal to the item; NIW:
                                 the Bartlett off-diagonals and z_perp direction of a picked auxiliary */
-    NP8O_STREAM_AUX_NIW = 8  /* NIW prior: the auxiliary's Bartlett chi^2 draws, chi^2_{D-1}, z_1 */
+    NP8O_STREAM_AUX_NIW = 8, /* NIW prior: the auxiliary's Bartlett chi^2 draws, chi^2_{D-1}, z_1 */
+    NP8O_STREAM_SM_THETA = 9,  /* split-merge: G0 draw of a split's new cluster (i = attempt) */
+    NP8O_STREAM_SM_ALLOC = 10, /* split-merge: SAMS allocation uniforms (i = attempt, call = member rank) */
+    NP8O_STREAM_SM_ACCEPT = 11 /* split-merge: acceptance uniform (i = attempt) */
 };
 
 /* Base measure G0 (DESIGN.md "Priors").
@@ -170,6 +173,18 @@ double np8o_gamma_mt(uint64_t seed, uint64_t i, uint32_t t, uint32_t stream, uin
  * draw for n = 0.  Outputs mu [D], Sigma [D*D].  Does not change the chain.  0 = ok. */
 int np8o_niw_draw(np8o_ctx *c, uint64_t i, uint32_t t, uint32_t stream, int64_t n, const double *stats,
                   const double *anchor, double *mu, double *Sigma);
+
+/* ---- Jain-Neal split-merge (src/np_jain_neal_algorithm.cpp; DESIGN.md "Split-merge") ------- */
+/* n sweeps of N split/merge attempts each, every sweep followed by np8o_end_sweep.  Reference prior,
+ * fp64 contraction.  0 = ok, -1 = unsupported configuration. */
+int np8o_sm_sweep(np8o_ctx *c, int32_t n);
+/* Attempts [a0, a1) of the current sweep without the end-of-sweep step (timed CPU samples). */
+int np8o_sm_attempts(np8o_ctx *c, int64_t a0, int64_t a1);
+/* Cumulative attempt outcomes: [0] skipped (equal items), [1] split rejected, [2] merge rejected,
+ * [3] split accepted, [4] merge accepted, [5] split rejected for want of a free slot. */
+void np8o_sm_get_stats(np8o_ctx *c, int64_t out[6]);
+double np8o_lgamma_int(int64_t n);
+double np8o_canon_sum(const double *v, int64_t n);
 
 #ifdef __cplusplus
 }

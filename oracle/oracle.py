@@ -108,6 +108,13 @@ def lib():
         L.np8o_gamma_mt.argtypes = [u64, u64, u32, u32, u32, d]
         L.np8o_gamma_mt.restype = d
         L.np8o_niw_draw.argtypes = [vp, u64, u32, u32, i64, vp, vp, vp, vp]
+        L.np8o_sm_sweep.argtypes = [vp, i32]
+        L.np8o_sm_get_stats.argtypes = [vp, vp]
+        L.np8o_sm_attempts.argtypes = [vp, i64, i64]
+        L.np8o_lgamma_int.argtypes = [i64]
+        L.np8o_lgamma_int.restype = d
+        L.np8o_canon_sum.argtypes = [vp, i64]
+        L.np8o_canon_sum.restype = d
         _lib = L
     return _lib
 
@@ -150,6 +157,15 @@ def mvn_probability_ref(x, mu, sigma):
 def mvn_logprobability_ref(x, mu, sigma):
     x, mu, sigma = (np.ascontiguousarray(a, dtype=np.float64) for a in (x, mu, sigma))
     return lib().np8o_mvn_logprobability_ref(_p(x), _p(mu), _p(sigma), x.size)
+
+
+def lgamma_int(n):
+    return lib().np8o_lgamma_int(int(n))
+
+
+def canon_sum(v):
+    v = np.ascontiguousarray(v, dtype=np.float64)
+    return lib().np8o_canon_sum(_p(v), v.size)
 
 
 def weighted_pick_ref(w, u):
@@ -233,6 +249,25 @@ class Chain:
 
     def sweep(self, n=1):
         return lib().np8o_sweep(self._h, n)
+
+    def sm_sweep(self, n=1):
+        """n Jain-Neal split-merge sweeps (N attempts each, then the end-of-sweep step)."""
+        r = lib().np8o_sm_sweep(self._h, n)
+        if r:
+            raise ValueError(f"oracle sm_sweep: {r}")
+
+    def sm_attempts(self, a0, a1):
+        """Attempts [a0, a1) of the current split-merge sweep (no end-of-sweep step)."""
+        r = lib().np8o_sm_attempts(self._h, int(a0), int(a1))
+        if r:
+            raise ValueError(f"oracle sm_attempts: {r}")
+
+    @property
+    def sm_stats(self):
+        """[skipped, split rejected, merge rejected, split accepted, merge accepted, split at kcap]"""
+        out = np.zeros(6, dtype=np.int64)
+        lib().np8o_sm_get_stats(self._h, _p(out))
+        return out
 
     def update_points(self, ids):
         ids = np.ascontiguousarray(ids, dtype=np.int64)
