@@ -220,6 +220,27 @@ void NealAlgorithm8Hip::printStatistics() {
     std::cout << " live clusters: " << s.K << ", sweeps: " << s.epoch << std::endl;
 }
 
+// A whole permutation = one split-merge sweep (N attempts on the library's two scan permutations,
+// np_mcmc.cpp:117-164 with subset_count = 2).  The reference's per-pair call has no sweep-parallel form.
+void JainNealAlgorithmHip::update(membertrix &cluster_matrix, const data_ids_t &data_ids) {
+    (void)cluster_matrix;
+    if ((int64_t)data_ids.size() != numItems())
+        throw std::runtime_error("JainNealAlgorithmHip::update: pass all items (one split-merge sweep)");
+    if (np8_sm_sweep(ctx(), 1) != NP8_OK) throw std::runtime_error(std::string("np8_sm_sweep: ") + np8_last_error(ctx()));
+}
+
+// The reference's statistics (np_jain_neal_algorithm.cpp:505-530).
+void JainNealAlgorithmHip::printStatistics() {
+    int64_t o[6];
+    if (np8_sm_stats(ctx(), o) != NP8_OK) throw std::runtime_error(std::string("np8_sm_stats: ") + np8_last_error(ctx()));
+    std::cout << "Statistics:" << std::endl;
+    std::cout << " # of merge attempts: " << o[2] + o[4] << std::endl;
+    std::cout << "   o of accepted merge cluster events: " << o[4] << std::endl;
+    std::cout << " # of split attempts: " << o[1] + o[3] + o[5] << std::endl;
+    std::cout << "   o of accepted split cluster events: " << o[3] << std::endl;
+    std::cout << " live clusters: " << stats().K << ", sweeps: " << stats().epoch << std::endl;
+}
+
 // ---- MCMC ----------------------------------------------------------------------------------------
 MCMC::MCMC(NealAlgorithm8Hip &sampler, int k_init) : _sampler(sampler), _k_init(k_init) {}
 

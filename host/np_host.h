@@ -113,6 +113,7 @@ class NealAlgorithm8Hip : public UpdateClusterPopulation {
     void exportState(membertrix &trix, int which);  // 0 current, 1 max-likelihood snapshot
     np8_stats_t stats();
     np8_ctx *ctx() { return _ctx; }
+    int64_t numItems() const { return _N; }
 
    private:
     void check(int r, const char *what);
@@ -120,6 +121,16 @@ class NealAlgorithm8Hip : public UpdateClusterPopulation {
     np8_prior _prior;
     int64_t _N = 0;
     int _kcap = 2048;
+};
+
+// The reference's split-merge population update (class JainNealAlgorithm,
+// include/np_jain_neal_algorithm.h:52-98; `-a jain_neal_split`) on the same device context: each
+// sweep-granular update() runs N split/merge attempts (np8_sm_sweep, include/np8.h).
+class JainNealAlgorithmHip : public NealAlgorithm8Hip {
+   public:
+    using NealAlgorithm8Hip::NealAlgorithm8Hip;
+    void update(membertrix &cluster_matrix, const data_ids_t &data_ids) override;
+    void printStatistics() override;
 };
 
 class MCMC {

@@ -17,7 +17,7 @@ def run(args, **kw):
 def test_cli_contract_without_gpu(tmp_path):
     assert os.path.exists(EXE), "host driver not built (__graft_entry__.build())"
     assert run([]).returncode == 1  # usage (np_main.cpp:216-218)
-    assert run(["-d", DATA, "-a", "triadic"]).returncode == 1  # unknown algorithm (np_main.cpp:231-233)
+    assert run(["-d", DATA, "-a", "triadic"]).returncode == 1  # not built here (np_main.cpp:231-233)
     assert run(["-d", DATA, "-a", "algorithm8", "-c", "regression", "-w", str(tmp_path / "w")]).returncode == 107
     existing = tmp_path / "exists"
     existing.mkdir()
@@ -103,3 +103,16 @@ def test_twogaussians_niw_conjugate_end_to_end(tmp_path):
 def test_cli_rejects_bad_prior_and_contraction(tmp_path):
     assert run(["-d", DATA, "-a", "algorithm8", "-p", "dirichlet", "-w", str(tmp_path / "a")]).returncode == 1
     assert run(["-d", DATA, "-a", "algorithm8", "-x", "bf16", "-w", str(tmp_path / "b")]).returncode == 1
+
+
+@pytest.mark.gpu
+def test_jain_neal_split_end_to_end(tmp_path):
+    """`-a jain_neal_split` (np_main.cpp:440-445): the split-merge population update through the same
+    MCMC driver; results written in the reference's layout and statistics printed."""
+    ws = str(tmp_path / "ws") + "/"
+    r = run(["-d", DATA, "-a", "jain_neal_split", "-T", "200", "-c", "clustering", "-s", "5", "-w", ws])
+    assert r.returncode == 0, r.stderr + r.stdout
+    assert "# of merge attempts" in r.stdout
+    score = open(os.path.join(ws, "LATEST", "results.score.txt")).read()
+    vals = dict(ln.split(": ") for ln in score.strip().splitlines())
+    assert 0.5 <= float(vals["Purity"]) <= 1.0
