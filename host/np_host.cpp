@@ -241,6 +241,28 @@ void JainNealAlgorithmHip::printStatistics() {
     std::cout << " live clusters: " << stats().K << ", sweeps: " << stats().epoch << std::endl;
 }
 
+// A whole permutation = one triadic split-merge sweep (N attempts on item triples, subset_count = 3).
+void TriadicAlgorithmHip::update(membertrix &cluster_matrix, const data_ids_t &data_ids) {
+    (void)cluster_matrix;
+    if ((int64_t)data_ids.size() != numItems())
+        throw std::runtime_error("TriadicAlgorithmHip::update: pass all items (one split-merge sweep)");
+    if (np8_tri_sweep(ctx(), 1) != NP8_OK) throw std::runtime_error(std::string("np8_tri_sweep: ") + np8_last_error(ctx()));
+}
+
+// The reference's statistics (np_triadic_algorithm.cpp:797-832): merge 2 -> 1, split 1 -> 2,
+// merge 3 -> 2, split 2 -> 3.
+void TriadicAlgorithmHip::printStatistics() {
+    int64_t o[10];
+    if (np8_tri_stats(ctx(), o) != NP8_OK) throw std::runtime_error(std::string("np8_tri_stats: ") + np8_last_error(ctx()));
+    const char *name[4] = {"merge (2 -> 1)", "split (1 -> 2)", "merge (3 -> 2)", "split (2 -> 3)"};
+    std::cout << "Statistics:" << std::endl;
+    for (int k = 0; k < 4; ++k) {
+        std::cout << " # of " << name[k] << " attempts: " << o[1 + 2 * k] + o[2 + 2 * k] << std::endl;
+        std::cout << "   o of accepted " << name[k] << " cluster events: " << o[2 + 2 * k] << std::endl;
+    }
+    std::cout << " live clusters: " << stats().K << ", sweeps: " << stats().epoch << std::endl;
+}
+
 // ---- MCMC ----------------------------------------------------------------------------------------
 MCMC::MCMC(NealAlgorithm8Hip &sampler, int k_init) : _sampler(sampler), _k_init(k_init) {}
 

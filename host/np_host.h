@@ -133,6 +133,15 @@ class JainNealAlgorithmHip : public NealAlgorithm8Hip {
     void printStatistics() override;
 };
 
+// The reference's triadic split-merge update (class TriadicAlgorithm, `-a triadic`): each sweep-granular
+// update() runs N attempts on item triples (np8_tri_sweep, include/np8.h).
+class TriadicAlgorithmHip : public NealAlgorithm8Hip {
+   public:
+    using NealAlgorithm8Hip::NealAlgorithm8Hip;
+    void update(membertrix &cluster_matrix, const data_ids_t &data_ids) override;
+    void printStatistics() override;
+};
+
 class MCMC {
    public:
     MCMC(NealAlgorithm8Hip &sampler, int k_init = 20);

@@ -26,7 +26,7 @@
 #include "np_results.h"
 
 static void usage(const char *p) {
-    std::cerr << "usage: " << p << " -d <datafile> -a algorithm8|jain_neal_split [-T sweeps=2000] [-c clustering] [-s seed]"
+    std::cerr << "usage: " << p << " -d <datafile> -a algorithm8|jain_neal_split|triadic [-T sweeps=2000] [-c clustering] [-s seed]"
               << " [-C chunk (0 = data-parallel sweep, 1 = sequential)] [-D dims=2] [-w workspace]"
               << " [-u frozen|mh_g0|niw_conjugate (cluster-parameter update)] [-p reference|niw (base measure)]"
               << " [-x f64|f32 (cluster likelihoods; f32 = fp32 matrix cores, D in {32, 64})]"
@@ -113,9 +113,8 @@ int main(int argc, char *argv[]) {
         usage(argv[0]);
         return 1;
     }
-    if (algo != "algorithm8" && algo != "jain_neal_split") {  // np_main.cpp:222-234
-        std::cerr << "Unknown algorithm: " << algo << " (this build implements algorithm8, jain_neal_split)"
-                  << std::endl;
+    if (algo != "algorithm8" && algo != "jain_neal_split" && algo != "triadic") {  // np_main.cpp:222-234
+        std::cerr << "Unknown algorithm: " << algo << std::endl;
         return 1;
     }
     if (mode != "clustering") {
@@ -167,6 +166,8 @@ int main(int argc, char *argv[]) {
         std::unique_ptr<NealAlgorithm8Hip> smp;
         if (algo == "jain_neal_split")
             smp.reset(new JainNealAlgorithmHip(seed, prior, chunk));
+        else if (algo == "triadic")
+            smp.reset(new TriadicAlgorithmHip(seed, prior, chunk));
         else
             smp.reset(new NealAlgorithm8Hip(seed, prior, chunk));
         NealAlgorithm8Hip &sampler = *smp;

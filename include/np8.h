@@ -151,6 +151,19 @@ int np8_sm_sweep(np8_ctx *ctx, int32_t n_sweeps);
  * free slot (kcap live clusters). */
 int np8_sm_stats(np8_ctx *ctx, int64_t out[6]);
 
+/* Triadic split-merge sweeps: the reference's `-a triadic` population update (class TriadicAlgorithm,
+ * include/np_triadic_algorithm.h, update() at src/np_triadic_algorithm.cpp:633-795), driven with
+ * subset_count = 3 (np_main.cpp:447-455): each sweep makes N attempts on the item triples of three scan
+ * permutations -- a dyadic split 1 -> 2, a dyadic merge 2 -> 1 (probability beta = 0.5), a triadic
+ * split 2 -> 3 or a triadic merge 3 -> 2, every member of the involved clusters reallocated by the
+ * sams_prior proposal -- then the end-of-sweep step.  Same restrictions as np8_sm_sweep. */
+int np8_tri_sweep(np8_ctx *ctx, int32_t n_sweeps);
+/* Cumulative outcomes (the reference's _statistics.step[0..3], np_triadic_algorithm.cpp:797-832):
+ * [0] triples skipped, [1]/[2] dyadic merges rejected/accepted, [3]/[4] dyadic splits, [5]/[6] triadic
+ * merges (3 -> 2), [7]/[8] triadic splits (2 -> 3), [9] splits accepted by the ratio but dropped for want
+ * of a free slot. */
+int np8_tri_stats(np8_ctx *ctx, int64_t out[10]);
+
 /* The reference's per-call granularity: sequential single-point updates of the listed items, in
  * order, at the current epoch (NealAlgorithm8::update with data_ids.size()==1).  Call
  * np8_end_sweep() after the last point of a sweep. */

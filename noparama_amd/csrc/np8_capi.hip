@@ -1671,6 +1671,12 @@ static SmArgs sm_args(np8_ctx *c) {
     A.t = c->epoch;
     A.perm0 = make_perm(c->seed ^ kSmPermKey[0], c->epoch, (uint32_t)c->n_loc);
     A.perm1 = make_perm(c->seed ^ kSmPermKey[1], c->epoch, (uint32_t)c->n_loc);
+    for (int r = 0; r < 3; ++r) A.tperm[r] = make_perm(c->seed ^ kTriPermKey[r], c->epoch, (uint32_t)c->n_loc);
+    // triadic rR (np_triadic_algorithm.cpp:116-131, beta = 0.5 at :63): 2 -> 1, 1 -> 2, 3 -> 2, 2 -> 3
+    A.lrr[0] = -std::log(0.5);
+    A.lrr[1] = std::log(0.5);
+    A.lrr[2] = std::log(1.0 - 0.5);
+    A.lrr[3] = -std::log(1.0 - 0.5);
     A.hist = c->sm_hist;
     A.nbk = (int32_t)((c->n_loc + 4095) / 4096);
     A.mem = c->sm_mem;
@@ -1726,13 +1732,16 @@ static int sm_rebuild(np8_ctx *c) {
     return NP8_OK;
 }
 
-int np8_sm_sweep(np8_ctx *c, int32_t n_sweeps) {
+// n split-merge sweeps of one sampler: speculative attempt batches, the first accepted attempt
+// applied, the state rebuilt, the batch restarted after it.
+static int split_merge_sweeps(np8_ctx *c, int32_t n_sweeps, bool triadic) {
+    const char *who = triadic ? "np8_tri_sweep" : "np8_sm_sweep";
     if (!c) return NP8_ERR_ARG;
-    if (!c->have_state) return fail(c, NP8_ERR_STATE, "np8_sm_sweep: no state (np8_set_state/np8_init_random)");
-    if (c->world > 1) return fail(c, NP8_ERR_ARG, "np8_sm_sweep: split-merge runs on one rank");
+    if (!c->have_state) return fail(c, NP8_ERR_STATE, std::string(who) + ": no state (np8_set_state/np8_init_random)");
+    if (c->world > 1) return fail(c, NP8_ERR_ARG, std::string(who) + ": split-merge runs on one rank");
     if (c->wide || c->prior != NP8_PRIOR_REFERENCE)
-        return fail(c, NP8_ERR_ARG, "np8_sm_sweep: needs the reference prior and the fp64 contraction");
-    if (c->n_loc > INT32_MAX) return fail(c, NP8_ERR_ARG, "np8_sm_sweep: at most 2^31-1 items");
+        return fail(c, NP8_ERR_ARG, std::string(who) + ": needs the reference prior and the fp64 contraction");
+    if (c->n_loc > INT32_MAX) return fail(c, NP8_ERR_ARG, std::string(who) + ": at most 2^31-1 items");
     int r = sm_buffers(c);
     if (r) return r;
     const int64_t N = c->n_loc;
@@ -1750,7 +1759,7 @@ int np8_sm_sweep(np8_ctx *c, int32_t n_sweeps) {
             A.nb = nb;
             Timer t;
             timer_begin(c, 5, t);
-            HIPC(c, np8_launch_sm_eval(A, c->stream));
+            HIPC(c, triadic ? np8_launch_tri_eval(A, c->stream) : np8_launch_sm_eval(A, c->stream));
             timer_end(c, t);
             HIPC(c, hipMemcpyAsync(c->sm_first_host, &c->sm_ctl->first, sizeof(int64_t), hipMemcpyDeviceToHost,
                                    c->stream));
@@ -1762,13 +1771,28 @@ int np8_sm_sweep(np8_ctx *c, int32_t n_sweeps) {
                 continue;
             }
             FinArgs F = fin_args(c, c->rec, 1);
-            HIPC(c, np8_launch_sm_apply(A, F, first, c->stream));
+            HIPC(c, triadic ? np8_launch_tri_apply(A, F, first, c->stream) : np8_launch_sm_apply(A, F, first, c->stream));
             if ((r = sm_rebuild(c))) return r;
             c->sm_batch = (int32_t)std::max<int64_t>(kSmBatchMin, std::min<int64_t>(kSmBatchMax, 2 * (first - a + 1)));
             a = first + 1;
         }
         if ((r = end_sweep(c))) return r;
     }
+    return NP8_OK;
+}
+
+int np8_sm_sweep(np8_ctx *c, int32_t n_sweeps) { return split_merge_sweeps(c, n_sweeps, false); }
+
+int np8_tri_sweep(np8_ctx *c, int32_t n_sweeps) { return split_merge_sweeps(c, n_sweeps, true); }
+
+int np8_tri_stats(np8_ctx *c, int64_t out[10]) {
+    if (!c || !out) return NP8_ERR_ARG;
+    for (int k = 0; k < 10; ++k) out[k] = 0;
+    if (!c->sm_ctl) return NP8_OK;
+    SmCtl h;
+    HIPC(c, hipMemcpyAsync(&h, c->sm_ctl, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    for (int k = 0; k < 10; ++k) out[k] = h.tstats[k];
     return NP8_OK;
 }
 

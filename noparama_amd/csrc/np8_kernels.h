@@ -164,10 +164,13 @@ __device__ __forceinline__ void write_new_slot(const FinArgs &F, const double *v
 // Jain-Neal split-merge (np8_sm.hip, DESIGN.md "Split-merge").
 // keys of the two scan permutations: make_perm(seed ^ kSmPermKey[r], epoch, N)
 constexpr uint64_t kSmPermKey[2] = {0x4A4E53504C495430ull, 0x4A4E53504C495431ull};
+// ... and the triadic sampler's three: make_perm(seed ^ kTriPermKey[r], epoch, N)
+constexpr uint64_t kTriPermKey[3] = {0x5452494144494330ull, 0x5452494144494331ull, 0x5452494144494332ull};
 
 struct SmCtl {
     int64_t first;     // lowest accepted attempt of the batch (INT64_MAX: none)
     int64_t stats[6];  // outcomes: skipped, split rej, merge rej, split acc, merge acc, split at kcap
+    int64_t tstats[10];  // triadic outcomes (np8_tri_stats order)
     int32_t nsplit;    // splits queued by np8_sm_classify
     int32_t pad;
 };
@@ -184,6 +187,8 @@ struct SmArgs {
     uint64_t seed;
     uint32_t t, pad;
     Perm perm0, perm1;  // the two scan permutations of the sweep (np_mcmc.cpp:118-125)
+    Perm tperm[3];      // triadic: three permutations
+    double lrr[4];      // triadic rR for dyadic merge, dyadic split, triadic merge, triadic split
     int32_t *hist;      // [kcap][nbk] block histograms -> scatter bases
     int32_t nbk, pad2;
     int32_t *mem;       // [N] members of every slot, ascending item order
@@ -314,3 +319,5 @@ hipError_t np8_launch_prune(const np8::PruneArgs &A, int kcap, hipStream_t s);
 hipError_t np8_launch_sm_members(const np8::SmArgs &A, hipStream_t s);
 hipError_t np8_launch_sm_eval(const np8::SmArgs &A, hipStream_t s);
 hipError_t np8_launch_sm_apply(const np8::SmArgs &A, const np8::FinArgs &F, int64_t a, hipStream_t s);
+hipError_t np8_launch_tri_eval(const np8::SmArgs &A, hipStream_t s);
+hipError_t np8_launch_tri_apply(const np8::SmArgs &A, const np8::FinArgs &F, int64_t a, hipStream_t s);

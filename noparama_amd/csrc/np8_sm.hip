@@ -475,7 +475,354 @@ __global__ __launch_bounds__(64) void np8_sm_apply(SmArgs A, FinArgs F, int64_t 
     if (threadIdx.x == 0 && out != 3 && out != 4) F.ctl->err |= kErrCapacity;  // cannot happen: re-evaluation
 }
 
-__global__ void np8_sm_reset(SmCtl *sc) {
+// ---- triadic split-merge (src/np_triadic_algorithm.cpp; the oracle's tri_attempt) ------------------------
+// Outcomes: 0 skipped, 1/2 dyadic merge rejected/accepted, 3/4 dyadic split, 5/6 triadic merge (3 -> 2),
+// 7/8 triadic split (2 -> 3), 9 split without a free slot.
+struct Tri {
+    int kind;  // -1 skipped, 0 dyadic merge, 1 dyadic split, 2 triadic merge, 3 triadic split
+    int ns, Q;  // source clusters, target clusters
+    int32_t pk[3];
+    int cl[3];
+};
+
+__device__ __forceinline__ int tri_dup(const int (&c)[3]) {
+    if (c[1] == c[0]) return 1;
+    return 2;  // c[2] repeats an earlier id, or all differ (duplicate_pick returns the last index)
+}
+
+__device__ Tri tri_case(const SmArgs &A, int64_t a) {
+    Tri T;
+#pragma unroll
+    for (int r = 0; r < 3; ++r) T.pk[r] = (int32_t)perm_apply(A.tperm[r], (uint32_t)a);
+    T.kind = -1;
+    T.ns = T.Q = 0;
+    if (T.pk[0] == T.pk[1] || T.pk[0] == T.pk[2] || T.pk[1] == T.pk[2]) return T;
+#pragma unroll
+    for (int r = 0; r < 3; ++r) T.cl[r] = A.z[T.pk[r]];
+    const int uniq = 1 + (T.cl[1] != T.cl[0]) + (T.cl[2] != T.cl[0] && T.cl[2] != T.cl[1]);
+    const double ub = uniform(A.seed, (uint64_t)a, A.t, kStreamSmAccept, 1);
+    if (uniq == 1) {
+        T.kind = 1;
+        T.pk[1] = T.pk[2];
+        T.cl[1] = T.cl[2];
+    } else if (ub < 0.5) {
+        T.kind = 0;
+        if (tri_dup(T.cl) == 1) {
+            T.pk[1] = T.pk[2];
+            T.cl[1] = T.cl[2];
+        }
+    } else if (uniq == 2) {
+        T.kind = 3;
+        if (tri_dup(T.cl) == 1) {  // swap positions 1 and 2 (the duplicate goes last)
+            const int32_t tp = T.pk[1];
+            const int tc = T.cl[1];
+            T.pk[1] = T.pk[2];
+            T.cl[1] = T.cl[2];
+            T.pk[2] = tp;
+            T.cl[2] = tc;
+        }
+    } else {
+        T.kind = 2;
+    }
+    T.ns = (T.kind == 1) ? 1 : (T.kind == 2 ? 3 : 2);
+    T.Q = (T.kind == 0) ? 1 : (T.kind == 3 ? 3 : 2);
+    return T;
+}
+
+__device__ __forceinline__ double tri_own(const SmArgs &A, int s) {
+    const int r = A.dense[s];
+    return A.cross[(int64_t)r * A.K + r];
+}
+
+// dyadic merge 2 -> 1 (:470-631 with C = 2): O(1) from the cross matrix
+__device__ __forceinline__ bool tri_dyadic_merge_accept(const SmArgs &A, const Tri &T, int64_t a) {
+    const int ra = A.dense[T.cl[0]], rb = A.dense[T.cl[1]];
+    const double ld0 = A.cross[(int64_t)ra * A.K + ra], ld1 = A.cross[(int64_t)rb * A.K + rb];
+    const double lp0 = (0.0 + ld0) + A.cross[(int64_t)rb * A.K + ra];
+    const int na = A.off[T.cl[0] + 1] - A.off[T.cl[0]], nb = A.off[T.cl[1] + 1] - A.off[T.cl[1]];
+    const double frac = ((0.0 + lgamma_int(na)) + lgamma_int(nb)) - lgamma_int((int64_t)na + nb);
+    const double rP = -(A.log_alpha + frac);
+    const double rLd = (0.0 + ld0) + ld1, rLdp = 0.0 + lp0;
+    const double x = ((0.0 + rP) + A.lrr[0]) + (rLdp - rLd);
+    return sm_accept(x, uniform(A.seed, (uint64_t)a, A.t, kStreamSmAccept, 0));
+}
+
+template <int D>
+__global__ __launch_bounds__(kSmThreads) void np8_tri_classify(SmArgs A) {
+    const int q = blockIdx.x * kSmThreads + threadIdx.x;
+    if (q >= A.nb) return;
+    const int64_t a = A.a0 + q;
+    const Tri T = tri_case(A, a);
+    uint8_t out;
+    if (T.kind < 0) {
+        out = 0;
+    } else if (T.kind == 0) {
+        out = tri_dyadic_merge_accept(A, T, a) ? 2 : 1;
+        if (out == 2) atomicMin(reinterpret_cast<unsigned long long *>(&A.sc->first), (unsigned long long)a);
+    } else {
+        out = kPending;
+        const int e = atomicAdd(&A.sc->nsplit, 1);
+        A.slist[e] = a;
+        if (T.kind & 1) sm_theta<D>(A, a, A.stheta + (int64_t)e * (D + 1));
+    }
+    A.typ[q] = out;
+}
+
+// A walk move (dyadic split, triadic merge or split), one wave: every member of the sources is
+// reallocated over the targets (picks fixed), 64 members per step resolved by fixpoint iteration
+// over the target-size prefix counts; after-move likelihood sums per source in canon_sum order.
+template <int D, bool APPLY>
+__device__ int tri_walk(const SmArgs &A, const FinArgs *F, const Tri &T, int64_t a, const double *vmu) {
+    constexpr int DP = D * (D + 1) / 2, W = D + DP + 2;  // mu | P' | c | iso
+    __shared__ double s_tg[3][W];
+    __shared__ double s_red[3][256];
+    __shared__ int s_slot[3];
+    __shared__ int s_new_slot;
+    const int lane = threadIdx.x;
+    const bool split = (T.kind & 1) != 0;
+    const int Q = T.Q, ns = T.ns;
+    // the case in scalars (indexing the struct with a loop variable would place it in scratch)
+    const int32_t pk0 = T.pk[0], pk1 = T.pk[1], pk2 = T.pk[2];
+    const int cl0 = T.cl[0], cl1 = T.cl[1], cl2 = T.cl[2];
+    if (lane == 0) {
+        for (int q = 0; q < Q; ++q) {
+            const int s = (split && q == Q - 1) ? -1 : (q == 0 ? cl0 : (q == 1 ? cl1 : cl2));
+            s_slot[q] = s;
+            if (s >= 0) {
+                for (int f = 0; f < D; ++f) s_tg[q][f] = A.slot_mu[(int64_t)s * D + f];
+#pragma unroll 1
+                for (int f = 0; f < DP; ++f) s_tg[q][D + f] = A.slot_P[(int64_t)s * DP + f];
+                s_tg[q][D + DP] = A.slot_c[s];
+                s_tg[q][D + DP + 1] = A.slot_iso[s];
+            } else {
+                const double v = vmu[0], v2 = v * v;
+                for (int f = 0; f < D; ++f) s_tg[q][f] = vmu[1 + f];
+#pragma unroll 1
+                for (int f = 0; f < DP; ++f) s_tg[q][D + f] = A.Gp[f] / v2;
+                s_tg[q][D + DP] = fma(-(double)D, log_pos(fabs(v)), A.caux);
+                s_tg[q][D + DP + 1] = (A.gp_iso > 0.0) ? A.gp_iso / v2 : 0.0;
+            }
+        }
+        if (APPLY) {
+            int s = -1;
+            if (split)
+                for (int k = 0; k < A.kcap; ++k)
+                    if (A.cnt[k] == 0) {
+                        s = k;
+                        break;
+                    }
+            s_new_slot = s;
+        }
+    }
+    __syncthreads();
+    const int snew = APPLY ? s_new_slot : -1;
+    const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    double Nq[3] = {1.0, 1.0, 1.0};  // target sizes, wave-uniform (each pick starts its target)
+    double lp[3] = {0.0, 0.0, 0.0};  // lane 0
+    int rank = 0;
+    int nsrc[3] = {0, 0, 0};
+    for (int si = 0; si < ns; ++si) {
+        const int s = (si == 0) ? cl0 : (si == 1 ? cl1 : cl2);
+        const int b0 = A.off[s], n = A.off[s + 1] - b0;
+        double ps[3][4];
+#pragma unroll
+        for (int q = 0; q < 3; ++q)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) ps[q][k] = 0.0;
+        for (int cb = 0; cb < n; cb += 64) {
+            const int k = (cb >> 6) & 3;
+            const int p = cb + lane;
+            const bool valid = p < n;
+            int32_t id = -1;
+            double ll[3] = {0.0, 0.0, 0.0}, u = 0.0;
+            if (valid) {
+                double x[D];
+                load_xm<D>(A, b0 + p, x);
+                id = A.mem[b0 + p];
+#pragma unroll
+                for (int q = 0; q < 3; ++q) {
+                    if (q >= Q) break;
+                    __asm__ __volatile__("" ::: "memory");  // target parameters stay in LDS
+                    ll[q] = sm_ll<D>(x, &s_tg[q][0], &s_tg[q][D], s_tg[q][D + DP], s_tg[q][D + DP + 1]);
+                }
+                u = uniform(A.seed, (uint64_t)a, A.t, kStreamSmAlloc, (uint32_t)(rank + p));
+            }
+            int pq = -1;
+#pragma unroll
+            for (int q = 0; q < 3; ++q) pq = (q < Q && valid && id == (q == 0 ? pk0 : (q == 1 ? pk1 : pk2))) ? q : pq;
+            const bool regular = valid && pq < 0;
+            uint64_t m0 = 0, m1 = 0, m2 = 0;
+            int d = 0;
+            for (int it = 0; it <= 64; ++it) {
+                const double n0 = Nq[0] + (double)__popcll(m0 & below), n1 = Nq[1] + (double)__popcll(m1 & below),
+                             n2 = Nq[2] + (double)__popcll(m2 & below);
+                const double lw0 = ll[0] + log_pos(n0), lw1 = ll[1] + log_pos(n1),
+                             lw2 = (Q > 2) ? ll[2] + log_pos(n2) : 0.0;
+                double mx = fmax(-__builtin_huge_val(), lw0);
+                mx = fmax(mx, lw1);
+                if (Q > 2) mx = fmax(mx, lw2);
+                double tot = 0.0;
+                tot += exp_le0(lw0 - mx);
+                const double c0 = tot;
+                tot += exp_le0(lw1 - mx);
+                const double c1 = tot;
+                if (Q > 2) tot += exp_le0(lw2 - mx);
+                const double w = u * tot;
+                d = (c0 >= w) ? 0 : ((c1 >= w || Q == 2) ? 1 : 2);
+                const uint64_t n0m = __ballot(regular && d == 0), n1m = __ballot(regular && d == 1),
+                               n2m = __ballot(regular && d == 2);
+                if (n0m == m0 && n1m == m1 && n2m == m2) break;  // wave-uniform
+                m0 = n0m;
+                m1 = n1m;
+                m2 = n2m;
+            }
+            Nq[0] += (double)__popcll(m0);
+            Nq[1] += (double)__popcll(m1);
+            Nq[2] += (double)__popcll(m2);
+            const int dd = (pq >= 0) ? pq : d;
+#pragma unroll
+            for (int q = 0; q < 3; ++q)
+#pragma unroll
+                for (int kk = 0; kk < 4; ++kk) ps[q][kk] = (valid && dd == q && kk == k) ? ps[q][kk] + ll[q] : ps[q][kk];
+            if (APPLY && valid) {
+                const int ts = s_slot[dd];
+                A.z[id] = (ts >= 0) ? ts : snew;
+            }
+        }
+        // this source's canonical sums, per target
+#pragma unroll
+        for (int q = 0; q < 3; ++q)
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) s_red[q][lane + 64 * kk] = ps[q][kk];
+        __syncthreads();
+        for (int h = 128; h >= 1; h >>= 1) {
+            for (int t = lane; t < h; t += 64)
+#pragma unroll
+                for (int q = 0; q < 3; ++q) s_red[q][t] += s_red[q][t + h];
+            __syncthreads();
+        }
+        if (lane == 0) {
+#pragma unroll
+            for (int q = 0; q < 3; ++q)
+                if (q < Q) lp[q] += s_red[q][0];
+        }
+        __syncthreads();
+        nsrc[0] = (si == 0) ? n : nsrc[0];
+        nsrc[1] = (si == 1) ? n : nsrc[1];
+        nsrc[2] = (si == 2) ? n : nsrc[2];
+        rank += n;
+    }
+    int out = 0;
+    if (lane == 0) {
+        double frac = 0.0;
+        if (split) {
+#pragma unroll
+            for (int q = 0; q < 3; ++q)
+                if (q < Q) frac += lgamma_int((int64_t)Nq[q]);
+#pragma unroll
+            for (int i = 0; i < 3; ++i)
+                if (i < ns) frac -= lgamma_int(nsrc[i]);
+        } else {
+#pragma unroll
+            for (int i = 0; i < 3; ++i)
+                if (i < ns) frac += lgamma_int(nsrc[i]);
+#pragma unroll
+            for (int q = 0; q < 3; ++q)
+                if (q < Q) frac -= lgamma_int((int64_t)Nq[q]);
+        }
+        const double rP = split ? A.log_alpha + frac : -(A.log_alpha + frac);
+        double rLd = 0.0, rLdp = 0.0;
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+            if (i < ns) rLd += tri_own(A, i == 0 ? cl0 : (i == 1 ? cl1 : cl2));
+#pragma unroll
+        for (int q = 0; q < 3; ++q)
+            if (q < Q) rLdp += lp[q];
+        const double lrr = (T.kind == 0) ? A.lrr[0] : (T.kind == 1 ? A.lrr[1] : (T.kind == 2 ? A.lrr[2] : A.lrr[3]));
+        const double x = ((0.0 + rP) + lrr) + (rLdp - rLd);
+        const bool acc = sm_accept(x, uniform(A.seed, (uint64_t)a, A.t, kStreamSmAccept, 0));
+        out = !acc ? 1 + 2 * T.kind : ((split && A.K >= A.kcap) ? 9 : 2 + 2 * T.kind);
+        if (APPLY && out == 2 + 2 * T.kind) {
+            if (split && snew >= 0) {
+                write_new_slot(*F, vmu, snew);
+                if (F->wdirty) F->wdirty[snew] = 1;
+            }
+#pragma unroll
+            for (int i = 0; i < 3; ++i)
+                if (i < ns) A.cnt[i == 0 ? cl0 : (i == 1 ? cl1 : cl2)] = 0;
+#pragma unroll
+            for (int q = 0; q < 3; ++q)
+                if (q < Q) A.cnt[s_slot[q] >= 0 ? s_slot[q] : snew] = (int32_t)Nq[q];
+        }
+    }
+    __syncthreads();
+    return out;  // lane 0's value
+}
+
+template <int D>
+__global__ __launch_bounds__(64) void np8_tri_walk(SmArgs A) {
+    const int ns = A.sc->nsplit;
+    for (int e = blockIdx.x; e < ns; e += gridDim.x) {
+        const int64_t a = A.slist[e];
+        unsigned long long first = 0;
+        if (threadIdx.x == 0) first = *reinterpret_cast<volatile unsigned long long *>(&A.sc->first);
+        first = __shfl(first, 0);
+        if ((unsigned long long)a > first) continue;  // wave-uniform
+        const Tri T = tri_case(A, a);
+        const int out = tri_walk<D, false>(A, nullptr, T, a, A.stheta + (int64_t)e * (D + 1));
+        if (threadIdx.x == 0) {
+            A.typ[a - A.a0] = (uint8_t)out;
+            if (out == 4 || out == 6 || out == 8)
+                atomicMin(reinterpret_cast<unsigned long long *>(&A.sc->first), (unsigned long long)a);
+        }
+    }
+}
+
+__global__ __launch_bounds__(kSmThreads) void np8_tri_tally(SmArgs A) {
+    __shared__ int cnt[10];
+    if (threadIdx.x < 10) cnt[threadIdx.x] = 0;
+    __syncthreads();
+    const int64_t first = A.sc->first;
+    const int lim = (first == INT64_MAX) ? A.nb : (int)(first - A.a0 + 1);
+    int c[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    for (int q = blockIdx.x * kSmThreads + threadIdx.x; q < lim; q += gridDim.x * kSmThreads) {
+        const uint8_t t = A.typ[q];
+#pragma unroll
+        for (int k = 0; k < 10; ++k) c[k] += (t == k);
+    }
+#pragma unroll
+    for (int k = 0; k < 10; ++k)
+        if (c[k]) atomicAdd(&cnt[k], c[k]);
+    __syncthreads();
+    if (threadIdx.x < 10 && cnt[threadIdx.x])
+        atomicAdd(reinterpret_cast<unsigned long long *>(&A.sc->tstats[threadIdx.x]), (unsigned long long)cnt[threadIdx.x]);
+}
+
+template <int D>
+__global__ __launch_bounds__(64) void np8_tri_apply(SmArgs A, FinArgs F, int64_t a) {
+    const Tri T = tri_case(A, a);
+    __syncthreads();  // the apply rewrites z: every lane has read the picks' clusters first
+    int out = 0;
+    if (T.kind == 0) {
+        out = tri_dyadic_merge_accept(A, T, a) ? 2 : 1;
+        if (out == 2) {
+            const int b0 = A.off[T.cl[1]], n1 = A.off[T.cl[1] + 1] - b0;
+            for (int q = threadIdx.x; q < n1; q += 64) A.z[A.mem[b0 + q]] = T.cl[0];
+            if (threadIdx.x == 0) {
+                A.cnt[T.cl[0]] += n1;
+                A.cnt[T.cl[1]] = 0;
+            }
+        }
+    } else if (T.kind > 0) {
+        __shared__ double vmu[D + 1];
+        if (threadIdx.x == 0 && (T.kind & 1)) sm_theta<D>(A, a, vmu);
+        __syncthreads();
+        out = tri_walk<D, true>(A, &F, T, a, vmu);
+    }
+    if (threadIdx.x == 0 && out != 2 && out != 4 && out != 6 && out != 8) F.ctl->err |= kErrCapacity;  // cannot happen
+}
+
+__global__ void np8_sm_reset(SmCtl *sc) {  // (both samplers)
     sc->first = INT64_MAX;
     sc->nsplit = 0;
 }
@@ -527,6 +874,34 @@ hipError_t np8_launch_sm_apply(const SmArgs &A, const FinArgs &F, int64_t a, hip
     if (A.D == d) {                                                             \
         hipLaunchKernelGGL(np8_sm_apply<d>, dim3(1), dim3(64), 0, s, A, F, a);  \
         return hipGetLastError();                                               \
+    }
+    NP8_SM_FOR_EACH_D(X)
+#undef X
+    return hipErrorInvalidValue;
+}
+
+hipError_t np8_launch_tri_eval(const SmArgs &A, hipStream_t s) {
+    if (A.nb <= 0) return hipSuccess;
+    hipLaunchKernelGGL(np8_sm_reset, dim3(1), dim3(1), 0, s, A.sc);
+    const unsigned gs = (unsigned)std::min(A.nb, kSplitBlocks);
+    const dim3 gq((unsigned)((A.nb + kSmThreads - 1) / kSmThreads));
+#define X(d)                                                                    \
+    if (A.D == d) {                                                             \
+        hipLaunchKernelGGL(np8_tri_classify<d>, gq, dim3(kSmThreads), 0, s, A); \
+        hipLaunchKernelGGL(np8_tri_walk<d>, dim3(gs), dim3(64), 0, s, A);       \
+        hipLaunchKernelGGL(np8_tri_tally, dim3(256), dim3(kSmThreads), 0, s, A); \
+        return hipGetLastError();                                               \
+    }
+    NP8_SM_FOR_EACH_D(X)
+#undef X
+    return hipErrorInvalidValue;
+}
+
+hipError_t np8_launch_tri_apply(const SmArgs &A, const FinArgs &F, int64_t a, hipStream_t s) {
+#define X(d)                                                                     \
+    if (A.D == d) {                                                              \
+        hipLaunchKernelGGL(np8_tri_apply<d>, dim3(1), dim3(64), 0, s, A, F, a);  \
+        return hipGetLastError();                                                \
     }
     NP8_SM_FOR_EACH_D(X)
 #undef X

@@ -143,6 +143,8 @@ def lib():
         "np8_end_sweep_stats": ([vp, vp], i32),
         "np8_sm_sweep": ([vp, i32], i32),
         "np8_sm_stats": ([vp, vp], i32),
+        "np8_tri_sweep": ([vp, i32], i32),
+        "np8_tri_stats": ([vp, vp], i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -394,6 +396,43 @@ class JainNealAlgorithm(NealAlgorithm8):
         print(f"   o of accepted merge cluster events: {s['merge_accepted']}")
         print(f" # of split attempts: {s['split_accepted'] + s['split_rejected'] + s['split_no_slot']}")
         print(f"   o of accepted split cluster events: {s['split_accepted']}")
+
+
+class TriadicAlgorithm(NealAlgorithm8):
+    """The reference's triadic split-merge population update (class TriadicAlgorithm,
+    src/np_triadic_algorithm.cpp; `-a triadic`): one sweep = N attempts on the item triples of three
+    scan permutations (dyadic 1 <-> 2 and triadic 2 <-> 3 split/merge moves), then the end-of-sweep
+    step.  Reference prior, fp64 contraction, one rank."""
+
+    def sweep(self, n=1, sync=True):
+        self._check(lib().np8_tri_sweep(self._h, int(n)))
+
+    def sweep_gibbs(self, n=1, sync=True):
+        NealAlgorithm8.sweep(self, n, sync)
+
+    def tri_stats(self):
+        out = np.zeros(10, dtype=np.int64)
+        self._check(lib().np8_tri_stats(self._h, _p(out)))
+        keys = ("skipped", "dyadic_merge_rejected", "dyadic_merge_accepted", "dyadic_split_rejected",
+                "dyadic_split_accepted", "triadic_merge_rejected", "triadic_merge_accepted",
+                "triadic_split_rejected", "triadic_split_accepted", "split_no_slot")
+        return dict(zip(keys, (int(v) for v in out)))
+
+    def update(self, cluster_matrix, data_ids):
+        """Sweep granularity (a permutation of all items), as JainNealAlgorithm.update."""
+        ids = np.asarray(data_ids, dtype=np.int64).reshape(-1)
+        if not (ids.size == self.N and np.array_equal(np.sort(ids), np.arange(self.N))):
+            raise ValueError("TriadicAlgorithm.update: pass a permutation of all items (one split-merge sweep)")
+        self.sweep(1)
+        if cluster_matrix is not None:
+            cluster_matrix.load(self.state(params=False))
+
+    def printStatistics(self):
+        s = self.tri_stats()
+        print("Statistics:")
+        for kind in ("dyadic_merge", "dyadic_split", "triadic_merge", "triadic_split"):
+            print(f" # of {kind.replace('_', ' ')} attempts: {s[kind + '_accepted'] + s[kind + '_rejected']}")
+            print(f"   o of accepted cluster events: {s[kind + '_accepted']}")
 
 
 class membertrix:

@@ -411,6 +411,8 @@ struct np8o_ctx {
     unsigned char *sm_flag;
     int64_t sm_stats[6];
     double sm_log_alpha;
+    int32_t *tri_asg; /* triadic: target of every member of the sources */
+    int64_t tri_stats[10];
 };
 
 static int packed_index(int D, int a, int b) { /* upper triangle, row-major, a <= b */
@@ -597,6 +599,7 @@ void np8o_destroy(np8o_ctx *c) {
     free(c->sm_v0);
     free(c->sm_v1);
     free(c->sm_flag);
+    free(c->tri_asg);
     free(c);
 }
 
@@ -612,6 +615,7 @@ int np8o_set_data(np8o_ctx *c, const double *X, int64_t N) {
     free(c->sm_v0);
     free(c->sm_v1);
     free(c->sm_flag);
+    free(c->tri_asg);
     c->N = N;
     c->X = (double *)malloc(sizeof(double) * (size_t)(N > 0 ? N : 1) * c->D);
     if (N > 0) memcpy(c->X, X, sizeof(double) * (size_t)N * c->D);
@@ -627,6 +631,7 @@ int np8o_set_data(np8o_ctx *c, const double *X, int64_t N) {
     c->sm_v0 = (double *)malloc(sizeof(double) * (size_t)(N > 0 ? N : 1));
     c->sm_v1 = (double *)malloc(sizeof(double) * (size_t)(N > 0 ? N : 1));
     c->sm_flag = (unsigned char *)malloc((size_t)(N > 0 ? N : 1));
+    c->tri_asg = (int32_t *)malloc(sizeof(int32_t) * (size_t)(N > 0 ? N : 1));
     return 0;
 }
 
@@ -2000,4 +2005,265 @@ int np8o_sm_attempts(np8o_ctx *c, int64_t a0, int64_t a1) {
 
 void np8o_sm_get_stats(np8o_ctx *c, int64_t out[6]) {
     for (int k = 0; k < 6; ++k) out[k] = c->sm_stats[k];
+}
+
+/* ================================================================================================
+ * Triadic split-merge: src/np_triadic_algorithm.cpp driven by
+ * src/np_mcmc.cpp:117-164 with subset_count = 3 (np_main.cpp:447-455).  Attempt a takes the items of
+ * three independent scan permutations (skipped unless all distinct, np_mcmc.cpp:153-156) and a
+ * uniform u_b (stream SM_ACCEPT, call 1; the reference's first draw in update(), :676):
+ *   one cluster             -> dyadic split 1 -> 2 of it (:679-699), picks (p0, p2)
+ *   else u_b < beta (0.5)   -> dyadic merge 2 -> 1 (:701-724): the pair left after duplicate_pick
+ *                              (dim1algebra.hpp:2117-2137) removes one; all items go to the first's
+ *   else two clusters       -> triadic split 2 -> 3 (:731-755), the duplicate moved last
+ *   else three clusters     -> triadic merge 3 -> 2 (:757-775): clusters 0, 1 keep, 2 dissolves
+ * A move reallocates every member of its source clusters (sams_prior, propose_split :208-296 and
+ * propose_merge :135-206): pick q starts target q (q < Q), the other members -- those of the sources
+ * in order, ascending item order within each (the reference shuffles them) -- go to target q with
+ * weight p(x | theta_q) |target q| (linear probabilities as the reference; drawn here from
+ * w_q = exp(lw_q - max lw), lw_q = ll_q + log|target q|, by one uniform over the cumulative sum --
+ * the same pick without the reference's all-underflow fallback to index 0).  Acceptance
+ * exp(rQ + rP + rR + rL) >= u (:414-425, :577-590) with rQ = 0 (sams_prior :100-102),
+ * rP = +-(log alpha + sum lgamma(larger partition sizes) - sum lgamma(smaller)) (:78-94),
+ * rR = log beta, -log(1-beta), -log beta, log(1-beta) for 1->2, 2->3, 2->1, 3->2 (:116-131),
+ * rL = sum of the after-move log-likelihoods - sum of the before ones; sums over members of several
+ * clusters are the sums, in source order, of per-source canon_sums.
+ * ============================================================================================== */
+static const uint64_t kTriPermKey[3] = {0x5452494144494330ull, 0x5452494144494331ull, 0x5452494144494332ull};
+#define TRI_BETA 0.5
+
+/* ll of x under target q: an existing slot, or the new cluster (mu, isotropic factor / packed P, c) */
+typedef struct {
+    int slot; /* -1: new cluster */
+    const double *mu, *P;
+    double iso, cc;
+} tri_target;
+
+static double tri_ll(const np8o_ctx *c, const double *x, const tri_target *tg) {
+    if (tg->slot >= 0) return sm_slot_ll(c, x, tg->slot);
+    if (tg->iso > 0.0) return sm_iso_ll(x, tg->mu, c->D, tg->iso, tg->cc);
+    return fma(-0.5, quad_form(c, x, tg->mu, tg->P), tg->cc);
+}
+
+/* Reallocate the members of sources src[0..ns) over targets tg[0..Q) (picks[q] starts target q; the
+ * other members in order by the max-shifted weighted pick).  asg[...] receives the target of every
+ * member (concatenated source order); np[q] the target sizes; lp[q] the after-move log-likelihoods. */
+static void tri_walk(np8o_ctx *c, uint64_t a, const int *src, int ns, const tri_target *tg, int Q,
+                     const int64_t *picks, int32_t *asg, int64_t *np, double *lp) {
+    const int D = c->D;
+    for (int q = 0; q < Q; ++q) {
+        np[q] = 1;
+        lp[q] = 0.0;
+    }
+    int64_t rank = 0;
+    double *v = c->sm_v0;
+    for (int si = 0; si < ns; ++si) {
+        const int64_t *L = c->sm_mem + c->sm_off[src[si]];
+        const int64_t n = c->sm_off[src[si] + 1] - c->sm_off[src[si]];
+        for (int64_t p = 0; p < n; ++p, ++rank) {
+            const double *x = c->X + (size_t)L[p] * D;
+            int pq = -1;
+            for (int q = 0; q < Q; ++q)
+                if (L[p] == picks[q]) pq = q;
+            int32_t d;
+            if (pq >= 0) {
+                d = pq;
+            } else {
+                double lw[3], mx = -INFINITY;
+                for (int q = 0; q < Q; ++q) {
+                    lw[q] = tri_ll(c, x, tg + q) + np8o_log_pos((double)np[q]);
+                    mx = fmax(mx, lw[q]);
+                }
+                double cum[3], tot = 0.0;
+                for (int q = 0; q < Q; ++q) {
+                    tot += np8o_exp_le0(lw[q] - mx);
+                    cum[q] = tot;
+                }
+                const double w = np8o_uniform(c->cfg.seed, a, c->t, NP8O_STREAM_SM_ALLOC, (uint32_t)rank) * tot;
+                d = Q - 1;
+                for (int q = 0; q < Q; ++q)
+                    if (cum[q] >= w) {
+                        d = q;
+                        break;
+                    }
+                np[d]++;
+            }
+            asg[rank] = d;
+        }
+    }
+    /* per-source canonical sums of the after-move likelihoods */
+    rank = 0;
+    for (int si = 0; si < ns; ++si) {
+        const int64_t *L = c->sm_mem + c->sm_off[src[si]];
+        const int64_t n = c->sm_off[src[si] + 1] - c->sm_off[src[si]];
+        for (int q = 0; q < Q; ++q) {
+            for (int64_t p = 0; p < n; ++p) {
+                c->sm_flag[p] = (unsigned char)(asg[rank + p] == q);
+                v[p] = c->sm_flag[p] ? tri_ll(c, c->X + (size_t)L[p] * D, tg + q) : 0.0;
+            }
+            lp[q] += canon_sum(v, c->sm_flag, n);
+        }
+        rank += n;
+    }
+}
+
+/* Before-move log-likelihood of source s: canon_sum of its members under its own parameters. */
+static double tri_own(np8o_ctx *c, int s) {
+    const int64_t *L = c->sm_mem + c->sm_off[s];
+    const int64_t n = c->sm_off[s + 1] - c->sm_off[s];
+    for (int64_t p = 0; p < n; ++p) c->sm_v0[p] = sm_slot_ll(c, c->X + (size_t)L[p] * c->D, s);
+    return canon_sum(c->sm_v0, NULL, n);
+}
+
+/* first index whose cluster id repeats an earlier one; the last index when all differ */
+static int tri_duplicate_pick(const int *ids, int n) {
+    for (int i = 1; i < n; ++i)
+        for (int j = 0; j < i; ++j)
+            if (ids[j] == ids[i]) return i;
+    return n - 1;
+}
+
+/* Outcomes: 0 skipped, 1/2 dyadic merge rejected/accepted, 3/4 dyadic split rejected/accepted,
+ * 5/6 triadic merge rejected/accepted, 7/8 triadic split rejected/accepted, 9 split accepted by the
+ * ratio but dropped for want of a free slot. */
+static int tri_attempt(np8o_ctx *c, uint64_t a) {
+    const int D = c->D;
+    const uint32_t N = (uint32_t)c->N;
+    int64_t pk[3];
+    int cl[3];
+    for (int r = 0; r < 3; ++r) pk[r] = np8o_perm(c->cfg.seed ^ kTriPermKey[r], c->t, N, (uint32_t)a);
+    if (pk[0] == pk[1] || pk[0] == pk[2] || pk[1] == pk[2]) return 0;
+    for (int r = 0; r < 3; ++r) cl[r] = c->z[pk[r]];
+    const int uniq = 1 + (cl[1] != cl[0]) + (cl[2] != cl[0] && cl[2] != cl[1]);
+    const double ub = np8o_uniform(c->cfg.seed, a, c->t, NP8O_STREAM_SM_ACCEPT, 1);
+    const double u = np8o_uniform(c->cfg.seed, a, c->t, NP8O_STREAM_SM_ACCEPT, 0);
+    int kind; /* 0 dyadic merge, 1 dyadic split, 2 triadic merge, 3 triadic split */
+    if (uniq == 1) {
+        kind = 1;
+        pk[1] = pk[2]; /* duplicate_pick([c,c,c]) = 1 is removed */
+        cl[1] = cl[2];
+    } else if (ub < TRI_BETA) {
+        kind = 0;
+        const int rm = tri_duplicate_pick(cl, 3);
+        for (int r = rm; r < 2; ++r) {
+            pk[r] = pk[r + 1];
+            cl[r] = cl[r + 1];
+        }
+    } else if (uniq == 2) {
+        kind = 3;
+        const int dp = tri_duplicate_pick(cl, 3);
+        int64_t tp = pk[dp];
+        pk[dp] = pk[2];
+        pk[2] = tp;
+        int tc = cl[dp];
+        cl[dp] = cl[2];
+        cl[2] = tc;
+    } else {
+        kind = 2;
+    }
+    const int split = (kind & 1);
+    const int ns = (kind == 0) ? 2 : (kind == 1 ? 1 : (kind == 2 ? 3 : 2)); /* sources */
+    const int Q = (kind == 0) ? 1 : (kind == 1 ? 2 : (kind == 2 ? 2 : 3));  /* targets */
+    int src[3];
+    for (int i = 0; i < ns; ++i) src[i] = cl[i];
+    tri_target tg[3];
+    double v = 0.0, mu[NP8O_DMAX], Pn[NP8O_DMAX * (NP8O_DMAX + 1) / 2];
+    for (int q = 0; q < Q; ++q) {
+        tg[q].slot = (split && q == Q - 1) ? -1 : cl[q];
+        tg[q].mu = tg[q].P = NULL;
+        tg[q].iso = tg[q].cc = 0.0;
+    }
+    if (split) {
+        sm_theta(c, a, &v, mu);
+        const double v2 = v * v;
+        for (int q = 0, aa = 0; aa < D; ++aa)
+            for (int b = aa; b < D; ++b, ++q) Pn[q] = c->Gp[aa * D + b] / v2;
+        const double gi = sm_gp_iso(c);
+        tg[Q - 1].mu = mu;
+        tg[Q - 1].P = Pn;
+        tg[Q - 1].iso = (gi > 0.0) ? gi / v2 : 0.0;
+        tg[Q - 1].cc = fma(-(double)D, np8o_log_pos(fabs(v)), c->caux);
+    }
+    int64_t nsrc[3], np[3], ntot = 0;
+    double ld[3], lp[3];
+    for (int i = 0; i < ns; ++i) {
+        nsrc[i] = c->sm_off[src[i] + 1] - c->sm_off[src[i]];
+        ntot += nsrc[i];
+        ld[i] = tri_own(c, src[i]);
+    }
+    int32_t *asg = c->tri_asg;
+    tri_walk(c, a, src, ns, tg, Q, pk, asg, np, lp);
+    /* rP (:78-94): more = the larger partition, less = the smaller */
+    double frac = 0.0;
+    if (split) {
+        for (int q = 0; q < Q; ++q) frac += np8o_lgamma_int(np[q]);
+        for (int i = 0; i < ns; ++i) frac -= np8o_lgamma_int(nsrc[i]);
+    } else {
+        for (int i = 0; i < ns; ++i) frac += np8o_lgamma_int(nsrc[i]);
+        for (int q = 0; q < Q; ++q) frac -= np8o_lgamma_int(np[q]);
+    }
+    const double rP = split ? c->sm_log_alpha + frac : -(c->sm_log_alpha + frac);
+    const double rR = (kind == 1) ? log(TRI_BETA) : (kind == 3) ? -log(1.0 - TRI_BETA)
+                                                 : (kind == 0) ? -log(TRI_BETA) : log(1.0 - TRI_BETA);
+    double rLd = 0.0, rLdp = 0.0;
+    for (int i = 0; i < ns; ++i) rLd += ld[i];
+    for (int q = 0; q < Q; ++q) rLdp += lp[q];
+    const double x = ((0.0 + rP) + rR) + (rLdp - rLd);
+    if (!sm_accept(x, u)) return 1 + 2 * kind;
+    int snew = -1;
+    if (split) {
+        for (int k = 0; k < c->kcap; ++k)
+            if (c->cnt[k] == 0) {
+                snew = k;
+                break;
+            }
+        if (snew < 0) return 9;
+        slot_from_aux(c, snew, v, mu);
+    }
+    int64_t rank = 0;
+    for (int i = 0; i < ns; ++i) {
+        const int64_t *L = c->sm_mem + c->sm_off[src[i]];
+        for (int64_t p = 0; p < nsrc[i]; ++p, ++rank) {
+            const int d = asg[rank];
+            c->z[L[p]] = (tg[d].slot >= 0) ? tg[d].slot : snew;
+        }
+    }
+    for (int i = 0; i < ns; ++i) c->cnt[src[i]] = 0;
+    for (int q = 0; q < Q; ++q) c->cnt[(tg[q].slot >= 0) ? tg[q].slot : snew] = (int32_t)np[q];
+    return 2 + 2 * kind;
+}
+
+int np8o_tri_sweep(np8o_ctx *c, int32_t n) {
+    if (c->cfg.prior != NP8O_PRIOR_REFERENCE || c->cfg.contraction != NP8O_CONTRACT_F64) return -1;
+    for (int s = 0; s < n; ++s) {
+        sm_members(c);
+        for (int64_t a = 0; a < c->N; ++a) {
+            const int o = tri_attempt(c, (uint64_t)a);
+            c->tri_stats[o]++;
+            if (o > 0 && o < 9 && (o & 1) == 0) {
+                rebuild_dense(c);
+                sm_members(c);
+            }
+        }
+        np8o_end_sweep(c);
+    }
+    return 0;
+}
+
+int np8o_tri_attempts(np8o_ctx *c, int64_t a0, int64_t a1) {
+    if (c->cfg.prior != NP8O_PRIOR_REFERENCE || c->cfg.contraction != NP8O_CONTRACT_F64) return -1;
+    sm_members(c);
+    for (int64_t a = a0; a < a1 && a < c->N; ++a) {
+        const int o = tri_attempt(c, (uint64_t)a);
+        c->tri_stats[o]++;
+        if (o > 0 && o < 9 && (o & 1) == 0) {
+            rebuild_dense(c);
+            sm_members(c);
+        }
+    }
+    return 0;
+}
+
+void np8o_tri_get_stats(np8o_ctx *c, int64_t out[10]) {
+    for (int k = 0; k < 10; ++k) out[k] = c->tri_stats[k];
 }

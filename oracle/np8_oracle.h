@@ -183,6 +183,13 @@ int np8o_sm_attempts(np8o_ctx *c, int64_t a0, int64_t a1);
 /* Cumulative attempt outcomes: [0] skipped (equal items), [1] split rejected, [2] merge rejected,
  * [3] split accepted, [4] merge accepted, [5] split rejected for want of a free slot. */
 void np8o_sm_get_stats(np8o_ctx *c, int64_t out[6]);
+/* Triadic split-merge (src/np_triadic_algorithm.cpp; DESIGN.md "Split-merge"): n sweeps of N attempts
+ * on item triples, each sweep followed by np8o_end_sweep; np8o_tri_attempts runs attempts [a0, a1) of
+ * the current sweep.  Outcomes: [0] skipped, [1]/[2] dyadic merge rejected/accepted, [3]/[4] dyadic
+ * split, [5]/[6] triadic merge (3 -> 2), [7]/[8] triadic split (2 -> 3), [9] split without a free slot. */
+int np8o_tri_sweep(np8o_ctx *c, int32_t n);
+int np8o_tri_attempts(np8o_ctx *c, int64_t a0, int64_t a1);
+void np8o_tri_get_stats(np8o_ctx *c, int64_t out[10]);
 double np8o_lgamma_int(int64_t n);
 double np8o_canon_sum(const double *v, int64_t n);
 

@@ -111,6 +111,9 @@ def lib():
         L.np8o_sm_sweep.argtypes = [vp, i32]
         L.np8o_sm_get_stats.argtypes = [vp, vp]
         L.np8o_sm_attempts.argtypes = [vp, i64, i64]
+        L.np8o_tri_sweep.argtypes = [vp, i32]
+        L.np8o_tri_attempts.argtypes = [vp, i64, i64]
+        L.np8o_tri_get_stats.argtypes = [vp, vp]
         L.np8o_lgamma_int.argtypes = [i64]
         L.np8o_lgamma_int.restype = d
         L.np8o_canon_sum.argtypes = [vp, i64]
@@ -261,6 +264,25 @@ class Chain:
         r = lib().np8o_sm_attempts(self._h, int(a0), int(a1))
         if r:
             raise ValueError(f"oracle sm_attempts: {r}")
+
+    def tri_sweep(self, n=1):
+        """n triadic split-merge sweeps (N attempts on item triples each, then the end-of-sweep step)."""
+        r = lib().np8o_tri_sweep(self._h, n)
+        if r:
+            raise ValueError(f"oracle tri_sweep: {r}")
+
+    def tri_attempts(self, a0, a1):
+        r = lib().np8o_tri_attempts(self._h, int(a0), int(a1))
+        if r:
+            raise ValueError(f"oracle tri_attempts: {r}")
+
+    @property
+    def tri_stats(self):
+        """[skipped, dyadic merge rej/acc, dyadic split rej/acc, triadic merge rej/acc,
+        triadic split rej/acc, split without a free slot]"""
+        out = np.zeros(10, dtype=np.int64)
+        lib().np8o_tri_get_stats(self._h, _p(out))
+        return out
 
     @property
     def sm_stats(self):

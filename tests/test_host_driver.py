@@ -17,7 +17,7 @@ def run(args, **kw):
 def test_cli_contract_without_gpu(tmp_path):
     assert os.path.exists(EXE), "host driver not built (__graft_entry__.build())"
     assert run([]).returncode == 1  # usage (np_main.cpp:216-218)
-    assert run(["-d", DATA, "-a", "triadic"]).returncode == 1  # not built here (np_main.cpp:231-233)
+    assert run(["-d", DATA, "-a", "algorithm2"]).returncode == 1  # unknown algorithm (np_main.cpp:231-233)
     assert run(["-d", DATA, "-a", "algorithm8", "-c", "regression", "-w", str(tmp_path / "w")]).returncode == 107
     existing = tmp_path / "exists"
     existing.mkdir()
@@ -116,3 +116,15 @@ def test_jain_neal_split_end_to_end(tmp_path):
     score = open(os.path.join(ws, "LATEST", "results.score.txt")).read()
     vals = dict(ln.split(": ") for ln in score.strip().splitlines())
     assert 0.5 <= float(vals["Purity"]) <= 1.0
+
+
+@pytest.mark.gpu
+def test_triadic_end_to_end(tmp_path):
+    """`-a triadic` (np_main.cpp:447-455): the triadic split-merge update through the MCMC driver."""
+    ws = str(tmp_path / "ws") + "/"
+    r = run(["-d", DATA, "-a", "triadic", "-T", "200", "-c", "clustering", "-s", "5", "-w", ws])
+    assert r.returncode == 0, r.stderr + r.stdout
+    assert "split (2 -> 3) attempts" in r.stdout
+    score = open(os.path.join(ws, "LATEST", "results.score.txt")).read()
+    vals = dict(ln.split(": ") for ln in score.strip().splitlines())
+    assert float(vals["Purity"]) > 0.9  # the proper SAMS weights find the two components
