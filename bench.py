@@ -47,8 +47,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget (0 = skip)")
     ap.add_argument("--traffic-json", default=None,
                     help="HBM bytes per assign launch from the committed PMC profile of this config")
-    ap.add_argument("--sampler", default="neal8", choices=["neal8", "jain_neal"],
-                    help="jain_neal: split-merge sweeps (np8_sm_sweep, one rank) instead of the Gibbs sweep")
+    ap.add_argument("--sampler", default="neal8", choices=["neal8", "jain_neal", "triadic"],
+                    help="jain_neal / triadic: split-merge sweeps (np8_sm_sweep / np8_tri_sweep, one rank) "
+                         "instead of the Gibbs sweep")
     ap.add_argument("--param-update", default="frozen", choices=["frozen", "mh_g0", "niw_conjugate"],
                     help="cluster-parameter update after every sweep (frozen = the reference's effective one)")
     a = ap.parse_args()
@@ -77,7 +78,7 @@ def workload(args):
 
 def main():
     args = parse()
-    if args.sampler == "jain_neal":
+    if args.sampler in ("jain_neal", "triadic"):
         return main_sm(args)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -252,27 +253,30 @@ def main_sm(args):
     latency-bound (the sequential SAMS allocation of a split, one lane per attempt)."""
     import torch
 
-    from noparama_amd import JainNealAlgorithm
+    from noparama_amd import JainNealAlgorithm, TriadicAlgorithm
 
+    tri = args.sampler == "triadic"
     if int(os.environ.get("WORLD_SIZE", "1")) > 1:
-        raise SystemExit("--sampler jain_neal runs on one rank")
+        raise SystemExit("--sampler jain_neal/triadic runs on one rank")
     torch.cuda.set_device(0)
     N, D, K = args.n, args.d, args.k
     X, z, mu, sig, opts = workload(args)
     if opts:
-        raise SystemExit("--sampler jain_neal: reference prior, fp64 configurations only")
-    smp = JainNealAlgorithm(D, seed=args.seed, device=0, param_update=args.param_update, kcap=max(256, 4 * K))
+        raise SystemExit("--sampler jain_neal/triadic: reference prior, fp64 configurations only")
+    cls = TriadicAlgorithm if tri else JainNealAlgorithm
+    smp = cls(D, seed=args.seed, device=0, param_update=args.param_update, kcap=max(256, 4 * K))
+    outcomes = smp.tri_stats if tri else smp.sm_stats
     smp.set_data(X)
     smp.set_state(z, mu, sig)
     smp.sweep(args.warmup)
     smp.set_timing(True)
-    st0, o0 = smp.stats(), smp.sm_stats()
+    st0, o0 = smp.stats(), outcomes()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     smp.sweep(args.steps)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    st1, o1 = smp.stats(), smp.sm_stats()
+    st1, o1 = smp.stats(), outcomes()
     d = {k: o1[k] - o0[k] for k in o1}
     nm = st1["n_timed_sm_members"] - st0["n_timed_sm_members"]
     ne = st1["n_timed_sm_eval"] - st0["n_timed_sm_eval"]
@@ -281,9 +285,10 @@ def main_sm(args):
     Kf = st1["K"]
     flops = float(N) * (Kf + 1) * (D * D + 2 * D + 4)  # cross matrix + own likelihoods per rebuild
     achieved = flops / (ms_m * 1e-3) / 1e12 if ms_m > 0 else 0.0
-    cpu = cpu_baseline_sm(X, z, mu, sig, D, args.seed, args.cpu_seconds) if args.cpu_seconds > 0 else None
+    cpu = cpu_baseline_sm(X, z, mu, sig, D, args.seed, args.cpu_seconds, tri) if args.cpu_seconds > 0 else None
+    name = "triadic" if tri else "Jain-Neal"
     out = {
-        "metric": f"split-merge sweeps/sec (Jain-Neal, N={N:.0e} attempts/sweep, D={D})".replace("+0", ""),
+        "metric": f"split-merge sweeps/sec ({name}, N={N:.0e} attempts/sweep, D={D})".replace("+0", ""),
         "value": args.steps / dt,
         "unit": "sweeps/s",
         "n_gpus": 1,
@@ -296,7 +301,7 @@ def main_sm(args):
         "dtype": "f64",
         "data": "synthetic",
         "config": {
-            "workload": f"{args.config}: N={N} D={D} K~{K} mixture, warm state, Jain-Neal split-merge "
+            "workload": f"{args.config}: N={N} D={D} K~{K} mixture, warm state, {name} split-merge "
                         f"(sams_prior, reference rules), {args.param_update} cluster parameters",
             "N": N, "D": D, "K_final": Kf, "attempt_outcomes": d,
             "state_rebuilds": nm, "attempt_batches": ne,
@@ -318,9 +323,10 @@ def main_sm(args):
     print(json.dumps(out))
 
 
-def cpu_baseline_sm(X, z, mu, sig, D, seed, budget_s):
-    """The oracle's sequential split-merge attempts (np8o_sm_attempts, one core) on the same data and
-    state: the first attempts of one sweep, doubling until the budget, extrapolated to N attempts."""
+def cpu_baseline_sm(X, z, mu, sig, D, seed, budget_s, tri=False):
+    """The oracle's sequential split-merge attempts (np8o_sm_attempts / np8o_tri_attempts, one core) on
+    the same data and state: the first attempts of one sweep, doubling until the budget, extrapolated
+    to N attempts."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O  # test infrastructure: timed as the CPU baseline only
 
@@ -331,7 +337,7 @@ def cpu_baseline_sm(X, z, mu, sig, D, seed, budget_s):
     done, a, t0 = 0, 64, time.perf_counter()
     while time.perf_counter() - t0 < budget_s and done < N:
         b = min(N, done + a)
-        c.sm_attempts(done, b)
+        (c.tri_attempts if tri else c.sm_attempts)(done, b)
         done, a = b, 2 * a
     el = time.perf_counter() - t0
     return {"value": done / el / N, "unit": "sweeps/s", "cores": 1, "kind": "port",
