@@ -653,11 +653,13 @@ __device__ int tri_walk(const SmArgs &A, const FinArgs *F, const Tri &T, int64_t
             const bool regular = valid && pq < 0;
             uint64_t m0 = 0, m1 = 0, m2 = 0;
             int d = 0;
+            // log of every target size this step can see (base + 0..63), one per lane, fetched by shuffle
+            const double tl0 = log_pos(Nq[0] + (double)lane), tl1 = log_pos(Nq[1] + (double)lane),
+                         tl2 = (Q > 2) ? log_pos(Nq[2] + (double)lane) : 0.0;
             for (int it = 0; it <= 64; ++it) {
-                const double n0 = Nq[0] + (double)__popcll(m0 & below), n1 = Nq[1] + (double)__popcll(m1 & below),
-                             n2 = Nq[2] + (double)__popcll(m2 & below);
-                const double lw0 = ll[0] + log_pos(n0), lw1 = ll[1] + log_pos(n1),
-                             lw2 = (Q > 2) ? ll[2] + log_pos(n2) : 0.0;
+                const double lw0 = ll[0] + __shfl(tl0, __popcll(m0 & below)),
+                             lw1 = ll[1] + __shfl(tl1, __popcll(m1 & below)),
+                             lw2 = (Q > 2) ? ll[2] + __shfl(tl2, __popcll(m2 & below)) : 0.0;
                 double mx = fmax(-__builtin_huge_val(), lw0);
                 mx = fmax(mx, lw1);
                 if (Q > 2) mx = fmax(mx, lw2);
