@@ -29,7 +29,8 @@ struct Ctl {
                           // replayed sweep graphs, np8_advance_epoch)
     int32_t lists_ok;     // the candidate lists describe the current table (set by the prune pass)
     int32_t n_pend;       // NIW prior: accepted requests waiting for np8_niw_aux_slots (set by np8_finalize)
-    int32_t pad3;
+    int32_t cand_fresh;   // the candidate rows' mu/P' match the slot tables (0 after a state upload:
+                          // np8_finalize then copies them; parameter updates patch rows in place)
 };
 
 enum : int32_t { kErrCapacity = 1, kErrSigma = 2 };

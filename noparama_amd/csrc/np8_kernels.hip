@@ -577,10 +577,11 @@ __global__ __launch_bounds__(kFinThreads) void np8_finalize(FinArgs F) {
         for (int q = tid; q < nreq; q += kFinThreads) atomicSub(&cnt_s[request_at(F, base, q)->zold], 1);
     }
     __syncthreads();
-    int nf = 0;
-    for (int s = s0; s < s1; ++s) nf += (cnt_s[s] == 0);
-    int nfree;
-    int frank = block_excl_scan(nf, sh, &nfree);
+    int nf = 0, nfree = 0, frank = 0;
+    if (try_accept) {  // block-uniform: the free slots are only needed when requests can be accepted
+        for (int s = s0; s < s1; ++s) nf += (cnt_s[s] == 0);
+        frank = block_excl_scan(nf, sh, &nfree);
+    }
     const bool accept = try_accept && (nreq <= nfree);
     if (try_accept && !accept) {
         for (int q = tid; q < nreq; q += kFinThreads) atomicAdd(&cnt_s[request_at(F, base, q)->zold], 1);
@@ -650,8 +651,14 @@ __global__ __launch_bounds__(kFinThreads) void np8_finalize(FinArgs F) {
     }
     __syncthreads();
     // write counts back and rebuild the dense candidate table in ascending slot order
-    int nl = 0;
-    for (int s = s0; s < s1; ++s) nl += (cnt_s[s] > 0);
+    int nl = 0, lchange = 0;
+    for (int s = s0; s < s1; ++s) {
+        nl += (cnt_s[s] > 0);
+        lchange |= ((cnt_s[s] > 0) != (F.cnt[s] > 0));  // a slot became live or empty
+    }
+    // the live rows keep their order and parameters unless a slot changed liveness, requests were
+    // accepted or the state was uploaded: then mu/P' of every row are copied below
+    const bool copy_rows = __syncthreads_or(lchange | (accept ? 1 : 0) | (F.ctl->cand_fresh ? 0 : 1)) != 0;
     int nlive;
     int k = block_excl_scan(nl, sh, &nlive);
     for (int s = s0; s < s1; ++s) {
@@ -673,12 +680,13 @@ __global__ __launch_bounds__(kFinThreads) void np8_finalize(FinArgs F) {
     // mu and P' of every live row, all threads (not on the wide path: its kernels read the fp32 factor
     // rows of np8_wide_rows, and 4 MB of P' at D = 64 would keep this one workgroup busy for 0.3 ms)
     const int W = D + DP;
-    for (int idx = tid; idx < (F.frame_payload ? 0 : nlive * W); idx += kFinThreads) {
+    for (int idx = tid; idx < ((F.frame_payload || !copy_rows) ? 0 : nlive * W); idx += kFinThreads) {
         const int r = idx / W, f = idx - r * W, s = live_s[r];
         F.cand[(int64_t)r * CS + f] = (f < D) ? F.slot_mu[(int64_t)s * D + f] : F.slot_P[(int64_t)s * DP + (f - D)];
     }
     if (tid == 0) {
         F.ctl->K = nlive;
+        F.ctl->cand_fresh = 1;
         F.ctl->n_pend = (F.prior == kPriorNiw && accept) ? nreq : 0;
     }
     if (F.prune) {  // candidate lists for the next sweep, one wave per row (block-uniform branch)

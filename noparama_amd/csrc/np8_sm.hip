@@ -472,7 +472,10 @@ __global__ __launch_bounds__(64) void np8_sm_apply(SmArgs A, FinArgs F, int64_t 
         __syncthreads();
         out = sm_split<D, true>(A, &F, p, a, vmu);
     }
-    if (threadIdx.x == 0 && out != 3 && out != 4) F.ctl->err |= kErrCapacity;  // cannot happen: re-evaluation
+    if (threadIdx.x == 0) {
+        if (out != 3 && out != 4) F.ctl->err |= kErrCapacity;  // cannot happen: re-evaluation
+        F.ctl->cand_fresh = 0;  // counts and slots changed behind np8_finalize: recopy the rows
+    }
 }
 
 // ---- triadic split-merge (src/np_triadic_algorithm.cpp; the oracle's tri_attempt) ------------------------
@@ -821,7 +824,10 @@ __global__ __launch_bounds__(64) void np8_tri_apply(SmArgs A, FinArgs F, int64_t
         __syncthreads();
         out = tri_walk<D, true>(A, &F, T, a, vmu);
     }
-    if (threadIdx.x == 0 && out != 2 && out != 4 && out != 6 && out != 8) F.ctl->err |= kErrCapacity;  // cannot happen
+    if (threadIdx.x == 0) {
+        if (out != 2 && out != 4 && out != 6 && out != 8) F.ctl->err |= kErrCapacity;  // cannot happen
+        F.ctl->cand_fresh = 0;  // counts and slots changed behind np8_finalize: recopy the rows
+    }
 }
 
 __global__ void np8_sm_reset(SmCtl *sc) {  // (both samplers)
