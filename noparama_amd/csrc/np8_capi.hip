@@ -793,12 +793,10 @@ int launch_total_loglik(np8_ctx *c) {
         HIPC(c, np8_launch_loglik_wide_mfma(W, c->D, c->partial, c->stream));
     } else
         HIPC(c, np8_launch_loglik(A, c->D, c->stream));
-    HIPC(c, np8_launch_loglik_reduce(c->partial, (c->n_loc + 255) / 256, &c->ctl->L_local, c->stream));
-    if (c->world > 1 && c->comm) {
-        NCCLC(c, ncclAllReduce(&c->ctl->L_local, &c->ctl->L, 1, ncclFloat64, ncclSum, c->comm, c->stream));
-    } else {
-        HIPC(c, hipMemcpyAsync(&c->ctl->L, &c->ctl->L_local, sizeof(double), hipMemcpyDeviceToDevice, c->stream));
-    }
+    const bool sum_ranks = c->world > 1 && c->comm;
+    HIPC(c, np8_launch_loglik_reduce(c->partial, (c->n_loc + 255) / 256, &c->ctl->L_local,
+                                     sum_ranks ? nullptr : &c->ctl->L, c->stream));
+    if (sum_ranks) NCCLC(c, ncclAllReduce(&c->ctl->L_local, &c->ctl->L, 1, ncclFloat64, ncclSum, c->comm, c->stream));
     timer_end(c, t);
     return NP8_OK;
 }

@@ -310,7 +310,7 @@ hipError_t np8_launch_loglik_matrix(const np8::AssignArgs &A, int D, int M, int 
 size_t np8_finalize_lds_bytes(int kcap);
 hipError_t np8_launch_finalize(const np8::FinArgs &F, hipStream_t s);
 hipError_t np8_launch_loglik(const np8::LoglikArgs &A, int D, hipStream_t s);
-hipError_t np8_launch_loglik_reduce(const double *partial, int64_t nb, double *out, hipStream_t s);
+hipError_t np8_launch_loglik_reduce(const double *partial, int64_t nb, double *out, double *out2, hipStream_t s);
 hipError_t np8_launch_snapshot(const np8::SnapArgs &A, hipStream_t s);
 hipError_t np8_launch_suffstats(const np8::ParamArgs &A, hipStream_t s);
 hipError_t np8_launch_suffstats_wide(const np8::ParamArgs &P, hipStream_t s);

@@ -729,7 +729,7 @@ __global__ __launch_bounds__(256) void np8_loglik(LoglikArgs A) {
 }
 
 __global__ __launch_bounds__(1024) void np8_loglik_reduce(const double *__restrict__ partial, int64_t nb,
-                                                          double *__restrict__ out) {
+                                                          double *__restrict__ out, double *__restrict__ out2) {
     __shared__ double red[1024];
     double s = 0.0;
     for (int64_t b = threadIdx.x; b < nb; b += blockDim.x) s = s + partial[b];
@@ -739,7 +739,10 @@ __global__ __launch_bounds__(1024) void np8_loglik_reduce(const double *__restri
         if (threadIdx.x < o) red[threadIdx.x] = red[threadIdx.x] + red[threadIdx.x + o];
         __syncthreads();
     }
-    if (threadIdx.x == 0) *out = red[0];
+    if (threadIdx.x == 0) {
+        *out = red[0];
+        if (out2) *out2 = red[0];  // one rank: the global sum too
+    }
 }
 
 // Every block decides from (L, best[par]); block 0 publishes best[par^1].
@@ -1112,8 +1115,8 @@ hipError_t np8_launch_loglik(const LoglikArgs &A, int D, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t np8_launch_loglik_reduce(const double *partial, int64_t nb, double *out, hipStream_t s) {
-    hipLaunchKernelGGL(np8_loglik_reduce, dim3(1), dim3(1024), 0, s, partial, nb, out);
+hipError_t np8_launch_loglik_reduce(const double *partial, int64_t nb, double *out, double *out2, hipStream_t s) {
+    hipLaunchKernelGGL(np8_loglik_reduce, dim3(1), dim3(1024), 0, s, partial, nb, out, out2);
     return hipGetLastError();
 }
 
