@@ -1676,7 +1676,7 @@ static SmArgs sm_args(np8_ctx *c) {
     A.lrr[2] = std::log(1.0 - 0.5);
     A.lrr[3] = -std::log(1.0 - 0.5);
     A.hist = c->sm_hist;
-    A.nbk = (int32_t)((c->n_loc + 4095) / 4096);
+    A.nbk = (int32_t)((c->n_loc + kSmMemItems - 1) / kSmMemItems);
     A.mem = c->sm_mem;
     A.off = c->sm_off;
     A.dense = c->dense_of;
@@ -1695,7 +1695,7 @@ static constexpr int32_t kSmBatchMax = 1 << 20, kSmBatchMin = 1024;
 
 static int sm_buffers(np8_ctx *c) {
     if (c->sm_n == c->n_loc) return NP8_OK;
-    const int64_t nbk = (c->n_loc + 4095) / 4096;
+    const int64_t nbk = (c->n_loc + kSmMemItems - 1) / kSmMemItems;
     int r;
     if ((r = dalloc(c, &c->sm_hist, (size_t)(c->kcap * (nbk > 0 ? nbk : 1)))) || (r = dalloc(c, &c->sm_mem, (size_t)c->n_loc)) ||
         (r = dalloc(c, &c->sm_off, (size_t)c->kcap + 1)) || (r = dalloc(c, &c->sm_live, (size_t)c->kcap)) ||

@@ -168,6 +168,8 @@ constexpr uint64_t kSmPermKey[2] = {0x4A4E53504C495430ull, 0x4A4E53504C495431ull
 // ... and the triadic sampler's three: make_perm(seed ^ kTriPermKey[r], epoch, N)
 constexpr uint64_t kTriPermKey[3] = {0x5452494144494330ull, 0x5452494144494331ull, 0x5452494144494332ull};
 
+constexpr int kSmMemItems = 512;  // items per block of the member-list counting sort (np8_sm_hist/scatter)
+
 struct SmCtl {
     int64_t first;     // lowest accepted attempt of the batch (INT64_MAX: none)
     int64_t stats[6];  // outcomes: skipped, split rej, merge rej, split acc, merge acc, split at kcap

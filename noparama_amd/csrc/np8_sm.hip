@@ -21,7 +21,7 @@ namespace np8 {
 namespace {
 
 constexpr int kSmThreads = 256;
-constexpr int kMemItems = 4096;  // items per block of the member-list sort
+constexpr int kMemItems = kSmMemItems;
 constexpr int kCrossTile = 8;    // live slots per cross-matrix block
 constexpr int kSplitBlocks = 8192;  // waves walking queued splits (32 per CU)
 constexpr uint32_t kStreamSmTheta = 9, kStreamSmAlloc = 10, kStreamSmAccept = 11;
@@ -94,19 +94,38 @@ __global__ __launch_bounds__(kSmThreads) void np8_sm_hist(SmArgs A) {
     for (int s = threadIdx.x; s < A.kcap; s += kSmThreads) A.hist[(int64_t)s * A.nbk + blockIdx.x] = lh[s];
 }
 
-// One block of 1024: slot totals, exclusive scan over slots, per-(slot, block) bases, live list.
-__global__ __launch_bounds__(1024) void np8_sm_scan(SmArgs A) {
+// One block per slot: exclusive scan of its per-block counts (bases relative to the slot's start)
+// and the slot total (into off[s], turned into the slot offset by np8_sm_scan_slots).
+__global__ __launch_bounds__(kSmThreads) void np8_sm_scan_blocks(SmArgs A) {
+    __shared__ int sc[kSmThreads];
+    const int s = blockIdx.x, t = threadIdx.x;
+    int carry = 0;
+    for (int b0 = 0; b0 < A.nbk; b0 += kSmThreads) {
+        const int64_t k = (int64_t)s * A.nbk + b0 + t;
+        const int h = (b0 + t < A.nbk) ? A.hist[k] : 0;
+        sc[t] = h;
+        __syncthreads();
+        for (int o = 1; o < kSmThreads; o <<= 1) {  // inclusive Hillis-Steele
+            const int v = (t >= o) ? sc[t - o] : 0;
+            __syncthreads();
+            sc[t] += v;
+            __syncthreads();
+        }
+        if (b0 + t < A.nbk) A.hist[k] = carry + sc[t] - h;
+        carry += sc[kSmThreads - 1];
+        __syncthreads();
+    }
+    if (t == 0) A.off[s] = carry;
+}
+
+// One block of 1024: exclusive scan of the slot totals into off[], the live list.
+__global__ __launch_bounds__(1024) void np8_sm_scan_slots(SmArgs A) {
     __shared__ int part[1024];
     const int t = threadIdx.x;
     const int per = (A.kcap + 1023) / 1024;
     const int s0 = min(A.kcap, t * per), s1 = min(A.kcap, s0 + per);
     int sum = 0;
-    for (int s = s0; s < s1; ++s) {
-        int tot = 0;
-        for (int b = 0; b < A.nbk; ++b) tot += A.hist[(int64_t)s * A.nbk + b];
-        A.off[s] = tot;  // temporarily the total
-        sum += tot;
-    }
+    for (int s = s0; s < s1; ++s) sum += A.off[s];
     part[t] = sum;
     __syncthreads();
     for (int h = 1; h < 1024; h <<= 1) {  // inclusive Hillis-Steele scan
@@ -119,13 +138,6 @@ __global__ __launch_bounds__(1024) void np8_sm_scan(SmArgs A) {
     for (int s = s0; s < s1; ++s) {
         const int tot = A.off[s];
         A.off[s] = run;
-        int r = run;
-        for (int b = 0; b < A.nbk; ++b) {
-            const int64_t k = (int64_t)s * A.nbk + b;
-            const int h = A.hist[k];
-            A.hist[k] = r;
-            r += h;
-        }
         run += tot;
         const int d = A.dense[s];
         if (d >= 0) A.live[d] = s;
@@ -135,10 +147,14 @@ __global__ __launch_bounds__(1024) void np8_sm_scan(SmArgs A) {
 
 // One wave per block of kMemItems items, 64 at a time in item order: rank among equal slots of the
 // lower lanes, the last lane of each slot advances the base.
+// ... and each item's row and own-slot likelihood into member order as it is placed (item-order reads
+// coalesced; Xm[a][pos] = X[a][i], ownm[pos] = ll(x_i | z_i)).
+template <int D>
 __global__ __launch_bounds__(64) void np8_sm_scatter(SmArgs A) {
+    constexpr int DP = D * (D + 1) / 2;
     extern __shared__ int base[];
     const int lane = threadIdx.x;
-    for (int s = lane; s < A.kcap; s += 64) base[s] = A.hist[(int64_t)s * A.nbk + blockIdx.x];
+    for (int s = lane; s < A.kcap; s += 64) base[s] = A.off[s] + A.hist[(int64_t)s * A.nbk + blockIdx.x];
     __syncthreads();
     const int64_t i0 = (int64_t)blockIdx.x * kMemItems;
     for (int c = 0; c < kMemItems; c += 64) {
@@ -153,26 +169,17 @@ __global__ __launch_bounds__(64) void np8_sm_scatter(SmArgs A) {
         if (key >= 0) {
             const int pos = base[key] + below;
             A.mem[pos] = (int32_t)i;
+            double x[D];
+            load_x<D>(A, (int32_t)i, x);
+#pragma unroll
+            for (int a = 0; a < D; ++a) A.Xm[(int64_t)a * A.N + pos] = x[a];
+            A.ownm[pos] = sm_ll<D>(x, A.slot_mu + (int64_t)key * D, A.slot_P + (int64_t)key * DP, A.slot_c[key],
+                                   A.slot_iso[key]);
         }
         __syncthreads();
         if (key >= 0 && above == 0) base[key] += below + 1;
         __syncthreads();
     }
-}
-
-// Items and own likelihoods in member order: Xm[a][p] = X[a][mem[p]], ownm[p] = ll(x | own slot).
-template <int D>
-__global__ __launch_bounds__(kSmThreads) void np8_sm_gather(SmArgs A) {
-    const int64_t p = (int64_t)blockIdx.x * kSmThreads + threadIdx.x;
-    if (p >= A.N) return;
-    const int32_t i = A.mem[p];
-    double x[D];
-    load_x<D>(A, i, x);
-#pragma unroll
-    for (int a = 0; a < D; ++a) A.Xm[(int64_t)a * A.N + p] = x[a];
-    const int s = A.z[i];
-    constexpr int DP = D * (D + 1) / 2;
-    A.ownm[p] = sm_ll<D>(x, A.slot_mu + (int64_t)s * D, A.slot_P + (int64_t)s * DP, A.slot_c[s], A.slot_iso[s]);
 }
 
 template <int D>
@@ -845,13 +852,12 @@ using namespace np8;
 hipError_t np8_launch_sm_members(const SmArgs &A, hipStream_t s) {
     if (A.N <= 0) return hipSuccess;
     hipLaunchKernelGGL(np8_sm_hist, dim3(A.nbk), dim3(kSmThreads), sizeof(int) * A.kcap, s, A);
-    hipLaunchKernelGGL(np8_sm_scan, dim3(1), dim3(1024), 0, s, A);
-    hipLaunchKernelGGL(np8_sm_scatter, dim3(A.nbk), dim3(64), sizeof(int) * A.kcap, s, A);
-    const dim3 gi((unsigned)((A.N + kSmThreads - 1) / kSmThreads));
+    hipLaunchKernelGGL(np8_sm_scan_blocks, dim3(A.kcap), dim3(kSmThreads), 0, s, A);
+    hipLaunchKernelGGL(np8_sm_scan_slots, dim3(1), dim3(1024), 0, s, A);
     const dim3 gc((unsigned)A.K, (unsigned)((A.K + kCrossTile - 1) / kCrossTile));
 #define X(d)                                                                                \
     if (A.D == d) {                                                                         \
-        hipLaunchKernelGGL(np8_sm_gather<d>, gi, dim3(kSmThreads), 0, s, A);                \
+        hipLaunchKernelGGL(np8_sm_scatter<d>, dim3(A.nbk), dim3(64), sizeof(int) * A.kcap, s, A); \
         if (A.K > 0) hipLaunchKernelGGL(np8_sm_cross<d>, gc, dim3(kSmThreads), 0, s, A);    \
         return hipGetLastError();                                                           \
     }
