@@ -60,6 +60,19 @@ __device__ __forceinline__ double sm_ll(const double (&x)[D], const double *mu, 
     return packed_ll<D>(x, mu, P, c);
 }
 
+// the isotropic branch of sm_ll alone
+template <int D>
+__device__ __forceinline__ double iso_ll(const double (&x)[D], const double *mu, double c, double iso) {
+    double d0 = x[0] - mu[0];
+    double acc = d0 * d0;
+#pragma unroll
+    for (int a = 1; a < D; ++a) {
+        const double d = x[a] - mu[a];
+        acc = fma(d, d, acc);
+    }
+    return fma(-0.5, acc * iso, c);
+}
+
 template <int D>
 __device__ __forceinline__ void load_x(const SmArgs &A, int32_t i, double (&x)[D]) {
 #pragma unroll
@@ -305,7 +318,7 @@ __global__ __launch_bounds__(kSmThreads) void np8_sm_classify(SmArgs A) {
 // round and stops at the unique fixpoint -- the sequential result, usually after 2 rounds.  Masked
 // sums go to 256 canonical partials (member rank mod 256) reduced by canon_sum's tree.
 // APPLY: write the moves.
-template <int D, bool APPLY>
+template <int D, bool APPLY, bool ISO = false>  // ISO: the new cluster's P' is a multiple of I (gp_iso > 0)
 __device__ int sm_split(const SmArgs &A, const FinArgs *F, const Pair &pq, int64_t a, const double *vmu) {
     constexpr int DP = D * (D + 1) / 2;
     __shared__ double s_red[2][256];
@@ -351,7 +364,8 @@ __device__ int sm_split(const SmArgs &A, const FinArgs *F, const Pair &pq, int64
                 load_xm<D>(A, b0 + p, x);
                 id = A.mem[b0 + p];
                 own = A.ownm[b0 + p];
-                nw = sm_ll<D>(x, s_th, s_th + D, s_th[D + DP], s_th[D + DP + 2]);
+                nw = ISO ? iso_ll<D>(x, s_th, s_th[D + DP], s_th[D + DP + 2])
+                         : sm_ll<D>(x, s_th, s_th + D, s_th[D + DP], s_th[D + DP + 2]);
                 u = uniform(A.seed, (uint64_t)a, A.t, kStreamSmAlloc, (uint32_t)p);
             }
             const bool isI = id == pq.i, isJ = id == pq.j;
@@ -415,7 +429,7 @@ __device__ int sm_split(const SmArgs &A, const FinArgs *F, const Pair &pq, int64
 
 // The queued splits of the batch, one wave each (persistent over the queue); a split after an
 // already accepted attempt is left pending -- the batch restarts before it.
-template <int D>
+template <int D, bool ISO>
 __global__ __launch_bounds__(64) void np8_sm_split(SmArgs A) {
     const int ns = A.sc->nsplit;
     for (int e = blockIdx.x; e < ns; e += gridDim.x) {
@@ -425,7 +439,7 @@ __global__ __launch_bounds__(64) void np8_sm_split(SmArgs A) {
         first = __shfl(first, 0);
         if ((unsigned long long)a > first) continue;  // wave-uniform
         const Pair p = sm_pair(A, a);
-        const int out = sm_split<D, false>(A, nullptr, p, a, A.stheta + (int64_t)e * (D + 1));
+        const int out = sm_split<D, false, ISO>(A, nullptr, p, a, A.stheta + (int64_t)e * (D + 1));
         if (threadIdx.x == 0) {
             A.typ[a - A.a0] = (uint8_t)out;
             if (out == 3) atomicMin(reinterpret_cast<unsigned long long *>(&A.sc->first), (unsigned long long)a);
@@ -874,7 +888,10 @@ hipError_t np8_launch_sm_eval(const SmArgs &A, hipStream_t s) {
 #define X(d)                                                                   \
     if (A.D == d) {                                                            \
         hipLaunchKernelGGL(np8_sm_classify<d>, gq, dim3(kSmThreads), 0, s, A); \
-        hipLaunchKernelGGL(np8_sm_split<d>, dim3(gs), dim3(64), 0, s, A);      \
+        if (A.gp_iso > 0.0)                                                    \
+            hipLaunchKernelGGL((np8_sm_split<d, true>), dim3(gs), dim3(64), 0, s, A); \
+        else                                                                   \
+            hipLaunchKernelGGL((np8_sm_split<d, false>), dim3(gs), dim3(64), 0, s, A); \
         hipLaunchKernelGGL(np8_sm_tally, dim3(256), dim3(kSmThreads), 0, s, A); \
         return hipGetLastError();                                              \
     }
