@@ -125,6 +125,7 @@ struct np8_ctx {
     int64_t sm_n = -1, sm_cross_cap = 0;
     int32_t sm_batch = 1024;
     int32_t sm_K = 0;
+    bool sm_all_iso = false;
     std::string err;
 };
 
@@ -1688,6 +1689,7 @@ static SmArgs sm_args(np8_ctx *c) {
     A.cross = c->sm_cross;
     A.sc = c->sm_ctl;
     A.typ = c->sm_typ;
+    A.iso_walk = (c->sm_all_iso && c->gp_iso > 0.0) ? 1 : 0;
     return A;
 }
 
@@ -1727,6 +1729,10 @@ static int sm_rebuild(np8_ctx *c) {
     timer_begin(c, 4, t);
     HIPC(c, np8_launch_sm_members(sm_args(c), c->stream));
     timer_end(c, t);
+    int32_t all_iso = 0;  // every live slot isotropic: the triadic walk's fast form applies
+    HIPC(c, hipMemcpyAsync(&all_iso, &c->sm_ctl->all_iso, sizeof(all_iso), hipMemcpyDeviceToHost, c->stream));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    c->sm_all_iso = all_iso != 0;
     return NP8_OK;
 }
 

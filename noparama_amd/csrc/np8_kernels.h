@@ -175,7 +175,7 @@ struct SmCtl {
     int64_t stats[6];  // outcomes: skipped, split rej, merge rej, split acc, merge acc, split at kcap
     int64_t tstats[10];  // triadic outcomes (np8_tri_stats order)
     int32_t nsplit;    // splits queued by np8_sm_classify
-    int32_t pad;
+    int32_t all_iso;   // every live slot has an isotropic P' (set by the member-list build)
 };
 
 struct SmArgs {
@@ -206,7 +206,8 @@ struct SmArgs {
     SmCtl *sc;
     uint8_t *typ;       // [batch] attempt outcomes
     int64_t a0;
-    int32_t nb, pad3;
+    int32_t nb;
+    int32_t iso_walk;   // triadic: every target isotropic (all live slots and G0), the walk's fast form
 };
 
 // NIW prior kernels (np8_niw.hip): posterior / prior draws per slot and picked auxiliaries -> slots.

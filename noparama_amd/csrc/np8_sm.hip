@@ -147,15 +147,20 @@ __global__ __launch_bounds__(1024) void np8_sm_scan_slots(SmArgs A) {
         part[t] += v;
         __syncthreads();
     }
-    int run = part[t] - sum;
+    int run = part[t] - sum, iso = 1;
     for (int s = s0; s < s1; ++s) {
         const int tot = A.off[s];
         A.off[s] = run;
         run += tot;
         const int d = A.dense[s];
-        if (d >= 0) A.live[d] = s;
+        if (d >= 0) {
+            A.live[d] = s;
+            iso &= (A.slot_iso[s] > 0.0) ? 1 : 0;
+        }
     }
+    iso = __syncthreads_and(iso);
     if (t == 1023) A.off[A.kcap] = part[1023];
+    if (t == 0) A.sc->all_iso = iso;
 }
 
 // One wave per block of kMemItems items, 64 at a time in item order: rank among equal slots of the
@@ -595,7 +600,7 @@ __global__ __launch_bounds__(kSmThreads) void np8_tri_classify(SmArgs A) {
 // A walk move (dyadic split, triadic merge or split), one wave: every member of the sources is
 // reallocated over the targets (picks fixed), 64 members per step resolved by fixpoint iteration
 // over the target-size prefix counts; after-move likelihood sums per source in canon_sum order.
-template <int D, bool APPLY>
+template <int D, bool APPLY, bool ISO = false>  // ISO: every target's P' is a multiple of I
 __device__ int tri_walk(const SmArgs &A, const FinArgs *F, const Tri &T, int64_t a, const double *vmu) {
     constexpr int DP = D * (D + 1) / 2, W = D + DP + 2;  // mu | P' | c | iso
     __shared__ double s_tg[3][W];
@@ -667,7 +672,8 @@ __device__ int tri_walk(const SmArgs &A, const FinArgs *F, const Tri &T, int64_t
                 for (int q = 0; q < 3; ++q) {
                     if (q >= Q) break;
                     __asm__ __volatile__("" ::: "memory");  // target parameters stay in LDS
-                    ll[q] = sm_ll<D>(x, &s_tg[q][0], &s_tg[q][D], s_tg[q][D + DP], s_tg[q][D + DP + 1]);
+                    ll[q] = ISO ? iso_ll<D>(x, &s_tg[q][0], s_tg[q][D + DP], s_tg[q][D + DP + 1])
+                                : sm_ll<D>(x, &s_tg[q][0], &s_tg[q][D], s_tg[q][D + DP], s_tg[q][D + DP + 1]);
                 }
                 u = uniform(A.seed, (uint64_t)a, A.t, kStreamSmAlloc, (uint32_t)(rank + p));
             }
@@ -785,7 +791,7 @@ __device__ int tri_walk(const SmArgs &A, const FinArgs *F, const Tri &T, int64_t
     return out;  // lane 0's value
 }
 
-template <int D>
+template <int D, bool ISO>
 __global__ __launch_bounds__(64) void np8_tri_walk(SmArgs A) {
     const int ns = A.sc->nsplit;
     for (int e = blockIdx.x; e < ns; e += gridDim.x) {
@@ -795,7 +801,7 @@ __global__ __launch_bounds__(64) void np8_tri_walk(SmArgs A) {
         first = __shfl(first, 0);
         if ((unsigned long long)a > first) continue;  // wave-uniform
         const Tri T = tri_case(A, a);
-        const int out = tri_walk<D, false>(A, nullptr, T, a, A.stheta + (int64_t)e * (D + 1));
+        const int out = tri_walk<D, false, ISO>(A, nullptr, T, a, A.stheta + (int64_t)e * (D + 1));
         if (threadIdx.x == 0) {
             A.typ[a - A.a0] = (uint8_t)out;
             if (out == 4 || out == 6 || out == 8)
@@ -919,7 +925,10 @@ hipError_t np8_launch_tri_eval(const SmArgs &A, hipStream_t s) {
 #define X(d)                                                                    \
     if (A.D == d) {                                                             \
         hipLaunchKernelGGL(np8_tri_classify<d>, gq, dim3(kSmThreads), 0, s, A); \
-        hipLaunchKernelGGL(np8_tri_walk<d>, dim3(gs), dim3(64), 0, s, A);       \
+        if (A.iso_walk)                                                         \
+            hipLaunchKernelGGL((np8_tri_walk<d, true>), dim3(gs), dim3(64), 0, s, A); \
+        else                                                                    \
+            hipLaunchKernelGGL((np8_tri_walk<d, false>), dim3(gs), dim3(64), 0, s, A); \
         hipLaunchKernelGGL(np8_tri_tally, dim3(256), dim3(kSmThreads), 0, s, A); \
         return hipGetLastError();                                               \
     }
