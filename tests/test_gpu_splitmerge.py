@@ -119,3 +119,16 @@ def test_far_cluster_splits(D):
     o.sm_sweep(2)
     assert_same(g, o)
     assert o.sm_stats[3] >= 2
+
+
+def test_kcap_saturation_parity():
+    """kcap = the live clusters: accepted splits find no free slot (outcome 5) until merges free one."""
+    X, _, _, _ = datasets.mixture(600, 2, 4, 0.3, 6.0, seed=11)
+    g, o = pair(2, seed=21, kcap=20)
+    for c in (g, o):
+        c.set_data(X)
+        c.init_random(20)
+    for s in range(3):
+        g.sweep(1)
+        o.sm_sweep(1)
+        assert_same(g, o)

@@ -97,3 +97,15 @@ def test_rejects_niw():
     g.init_random(5)
     with pytest.raises(NP8Error):
         g.sweep(1)
+
+
+def test_kcap_saturation_parity():
+    X, _, _, _ = datasets.mixture(500, 2, 4, 0.3, 6.0, seed=11)
+    g, o = pair(2, seed=21, kcap=20)
+    for c in (g, o):
+        c.set_data(X)
+        c.init_random(20)
+    for s in range(3):
+        g.sweep(1)
+        o.tri_sweep(1)
+        assert_same(g, o)
