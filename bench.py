@@ -43,6 +43,7 @@ def parse():
     ap.add_argument("--d", type=int, default=None, help="default: 8 (C3) / 64 (C5)")
     ap.add_argument("--k", type=int, default=None, help="default: 64 (C3) / 256 (C5)")
     ap.add_argument("--seed", type=int, default=20261015)
+    ap.add_argument("--kcap", type=int, default=0, help="cluster capacity (0: the library default)")
     ap.add_argument("--config", default="C3", help="config tag for the JSON line (BASELINE.json configs)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget (0 = skip)")
     ap.add_argument("--traffic-json", default=None,
@@ -73,7 +74,7 @@ def workload(args):
         return X, z, mu, sig, opts
     s, r = (0.3, 15.0) if D == 2 else (0.8, 20.0)
     X, z, mu, sig = datasets.mixture(N, D, K, s, r, seed=args.seed)
-    return X, z, mu, sig, {}
+    return X, z, mu, sig, ({"kcap": args.kcap} if args.kcap else {})
 
 
 def main():
@@ -261,10 +262,10 @@ def main_sm(args):
     torch.cuda.set_device(0)
     N, D, K = args.n, args.d, args.k
     X, z, mu, sig, opts = workload(args)
-    if opts:
+    if any(k != "kcap" for k in opts):
         raise SystemExit("--sampler jain_neal/triadic: reference prior, fp64 configurations only")
     cls = TriadicAlgorithm if tri else JainNealAlgorithm
-    smp = cls(D, seed=args.seed, device=0, param_update=args.param_update, kcap=max(256, 4 * K))
+    smp = cls(D, seed=args.seed, device=0, param_update=args.param_update, kcap=opts.get("kcap", max(256, 4 * K)))
     outcomes = smp.tri_stats if tri else smp.sm_stats
     smp.set_data(X)
     smp.set_state(z, mu, sig)
