@@ -441,6 +441,7 @@ __device__ int block_excl_scan(int v, int *sh /* >= 16 ints */, int *total) {
 // arithmetic is ~1e-15 relative).  Non-isotropic rows and singletons (own weight 0) keep every row.
 // One wave builds one row's list (ascending j) and clears the row's radius for the next sweep.
 constexpr int kPruneFusedMaxK = 512;
+constexpr int kPruneBlocks = 32;  // np8_prune grid: 128 rows per pass
 
 __device__ void prune_row(const double *__restrict__ cand, double *__restrict__ r2, int32_t *__restrict__ plist,
                           int32_t *__restrict__ plen, int ls, int D, int K, int k0) {
@@ -1152,18 +1153,20 @@ hipError_t np8_launch_mh_g0(const ParamArgs &A, hipStream_t s) {
 }
 
 // Standalone pass (after the mh_g0 update has moved means): four rows per block.
+// A small grid strides over the live rows (one wave per row): K is only known on the device, and a
+// grid sized for kcap would mostly launch blocks that exit at once.
 __global__ __launch_bounds__(256) void np8_prune(PruneArgs A) {
     const int K = A.ctl->K;
-    const int k0 = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (blockIdx.x == 0 && threadIdx.x == 0) A.ctl->lists_ok = 1;
-    if (k0 >= K) return;
-    prune_row(A.cand, A.r2, A.plist, A.plen, A.ls, A.D, K, k0);
+    for (int k0 = blockIdx.x * 4 + (threadIdx.x >> 6); k0 < K; k0 += gridDim.x * 4)  // wave-uniform
+        prune_row(A.cand, A.r2, A.plist, A.plen, A.ls, A.D, K, k0);
 }
 
 __global__ void np8_advance_epoch(Ctl *ctl, uint32_t n) { ctl->t_base += n; }
 
 hipError_t np8_launch_prune(const PruneArgs &A, int kcap, hipStream_t s) {
-    hipLaunchKernelGGL(np8_prune, dim3((unsigned)((kcap + 3) / 4)), dim3(256), 0, s, A);
+    const int nb = (kcap + 3) / 4;
+    hipLaunchKernelGGL(np8_prune, dim3((unsigned)(nb < kPruneBlocks ? nb : kPruneBlocks)), dim3(256), 0, s, A);
     return hipGetLastError();
 }
 
