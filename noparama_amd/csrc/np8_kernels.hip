@@ -443,8 +443,11 @@ __device__ int block_excl_scan(int v, int *sh /* >= 16 ints */, int *total) {
 constexpr int kPruneFusedMaxK = 512;
 constexpr int kPruneBlocks = 32;  // np8_prune grid: 128 rows per pass
 
+// DT > 0: the dimension as a template constant (loops unrolled, the row loads issued together)
+template <int DT = 0>
 __device__ void prune_row(const double *__restrict__ cand, double *__restrict__ r2, int32_t *__restrict__ plist,
-                          int32_t *__restrict__ plen, int ls, int D, int K, int k0) {
+                          int32_t *__restrict__ plen, int ls, int Drt, int K, int k0) {
+    const int D = DT > 0 ? DT : Drt;
     const int DP = D * (D + 1) / 2, CS = cand_stride(D), F = D + DP;
     const int lane = threadIdx.x & 63;
     const double *e0 = cand + (int64_t)k0 * CS;
@@ -463,7 +466,12 @@ __device__ void prune_row(const double *__restrict__ cand, double *__restrict__ 
             const double isoj = ej[F + kFieldIso];
             if (isoj > 0.0) {
                 double dist2 = 0.0;
-                for (int a = 0; a < D; ++a) {
+#pragma unroll
+                for (int a = 0; a < (DT > 0 ? DT : 1); ++a) {  // DT: fully unrolled
+                    const double dd = ej[a] - e0[a];
+                    dist2 = fma(dd, dd, dist2);
+                }
+                for (int a = (DT > 0 ? DT : 1); a < D; ++a) {  // runtime D (only when DT == 0)
                     const double dd = ej[a] - e0[a];
                     dist2 = fma(dd, dd, dist2);
                 }
@@ -1155,18 +1163,29 @@ hipError_t np8_launch_mh_g0(const ParamArgs &A, hipStream_t s) {
 // Standalone pass (after the mh_g0 update has moved means): four rows per block.
 // A small grid strides over the live rows (one wave per row): K is only known on the device, and a
 // grid sized for kcap would mostly launch blocks that exit at once.
+template <int DT>
 __global__ __launch_bounds__(256) void np8_prune(PruneArgs A) {
     const int K = A.ctl->K;
     if (blockIdx.x == 0 && threadIdx.x == 0) A.ctl->lists_ok = 1;
     for (int k0 = blockIdx.x * 4 + (threadIdx.x >> 6); k0 < K; k0 += gridDim.x * 4)  // wave-uniform
-        prune_row(A.cand, A.r2, A.plist, A.plen, A.ls, A.D, K, k0);
+        prune_row<DT>(A.cand, A.r2, A.plist, A.plen, A.ls, A.D, K, k0);
 }
 
 __global__ void np8_advance_epoch(Ctl *ctl, uint32_t n) { ctl->t_base += n; }
 
 hipError_t np8_launch_prune(const PruneArgs &A, int kcap, hipStream_t s) {
     const int nb = (kcap + 3) / 4;
-    hipLaunchKernelGGL(np8_prune, dim3((unsigned)(nb < kPruneBlocks ? nb : kPruneBlocks)), dim3(256), 0, s, A);
+    const dim3 g((unsigned)(nb < kPruneBlocks ? nb : kPruneBlocks));
+    switch (A.D) {
+#define Y(d)                                                              \
+    case d:                                                               \
+        hipLaunchKernelGGL((np8_prune<d>), g, dim3(256), 0, s, A);        \
+        break;
+        Y(1) Y(2) Y(3) Y(4) Y(8) Y(16)
+#undef Y
+        default:
+            hipLaunchKernelGGL((np8_prune<0>), g, dim3(256), 0, s, A);
+    }
     return hipGetLastError();
 }
 
