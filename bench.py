@@ -46,6 +46,8 @@ def parse():
     ap.add_argument("--kcap", type=int, default=0, help="cluster capacity (0: the library default)")
     ap.add_argument("--config", default="C3", help="config tag for the JSON line (BASELINE.json configs)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget (0 = skip)")
+    ap.add_argument("--cold-sweeps", type=int, default=20,
+                    help="cold leg: sweeps from the reference's initialisation (init_random(20)), 0 = skip")
     ap.add_argument("--traffic-json", default=None,
                     help="HBM bytes per assign launch from the committed PMC profile of this config")
     ap.add_argument("--sampler", default="neal8", choices=["neal8", "jain_neal", "triadic"],
@@ -113,11 +115,17 @@ def main():
 
         uid = [comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
+        # the multi-GPU configuration is the RCCL-over-xGMI exchange: with one GPU per rank, an RCCL failure
+        # is an error, not a silent fall-back.  Only rehearsals with more ranks than GPUs (RCCL refuses
+        # two ranks on one device) move the same record over gloo, and say so in "exchange".
+        rehearsal = world > torch.cuda.device_count()
         try:
             smp.comm_init(uid[0], rank, world)
             ok = True
         except NP8Error as e:
-            print(f"rank {rank}: RCCL unavailable ({e}); exchanging records over gloo", file=sys.stderr)
+            if not rehearsal:
+                raise
+            print(f"rank {rank}: RCCL unavailable ({e}); rehearsal exchanging records over gloo", file=sys.stderr)
             ok = False
         flags = [None] * world
         dist.all_gather_object(flags, ok)
@@ -148,9 +156,14 @@ def main():
                 dist.all_reduce(st)
                 smp.end_sweep_stats(st.numpy())
 
-    sweeps(args.warmup)  # includes np8_sync
-    torch.cuda.synchronize()
+    # timing (event pairs around one assign launch per graph replay, plus the executed-work counters)
+    # is on from the start, so the timed region replays the graph warm-up captured; np8_prepare_sweeps
+    # captures and uploads the graph of the timed sweeps if the warm-up did not (warm-up < 20 sweeps)
     smp.set_timing(True)
+    sweeps(args.warmup)  # includes np8_sync
+    if transport != "gloo":
+        smp.prepare_sweeps(args.steps)
+    torch.cuda.synchronize()
     st0 = smp.stats()
     if dist:
         dist.barrier()
@@ -186,10 +199,17 @@ def main():
     achieved = flops / (ms_assign * 1e-3) / 1e12 if ms_assign > 0 else 0.0
     peak = FP32_MFMA_PEAK_TFLOPS if wide else FP64_PEAK_TFLOPS
     xbytes = 4 * D if wide else 8 * D
-    traffic = None
+    # executed work: quadratic forms the kernel evaluated (device counters), at their real cost
+    # (isotropic rows: D subtractions + D multiply-adds + scale, weight = 3D + 3 flops)
+    nq = st1["n_quad"] - st0["n_quad"]
+    nq_iso = st1["n_quad_iso"] - st0["n_quad_iso"]
+    exec_flops = ((nq - nq_iso) * (D * D + 2 * D + 4) + nq_iso * (3 * D + 3)) / max(n_launch, 1) if not wide else None
+    traffic = traffic_src = None
     if os.path.exists(args.traffic_json):
         try:
-            traffic = json.load(open(args.traffic_json)).get("assign_bytes_per_launch")
+            tj = json.load(open(args.traffic_json))
+            traffic = tj.get("assign_bytes_per_launch")
+            traffic_src = f"{os.path.relpath(args.traffic_json, ROOT)} (rocprofv3 PMC pass, {tj.get('commit', 'commit n/a')})"
         except Exception:
             traffic = None
 
@@ -237,14 +257,55 @@ def main():
                 "mfma_executed_tflops": (mfma_flops / (ms_assign * 1e-3) / 1e12) if (wide and ms_assign > 0) else None,
                 "assign_launches_timed": n_launch,
                 "algorithmic_flops_per_launch": flops,
+                "traffic_source": traffic_src,
+                "executed": None if wide else {
+                    "note": "what np8_assign executed: quadratic forms after exact candidate pruning "
+                            "(device counters), at their real cost; the M auxiliary G0 draws per item "
+                            "(Philox, Box-Muller, chi^2 logs) are not flops of this count",
+                    "quad_forms_per_item": nq / max(n_launch, 1) / max(n_items, 1),
+                    "iso_fraction": nq_iso / max(nq, 1),
+                    "tflops": exec_flops / (ms_assign * 1e-3) / 1e12 if ms_assign > 0 else None,
+                    "frac_of_peak": exec_flops / (ms_assign * 1e-3) / 1e12 / peak if ms_assign > 0 else None,
+                },
                 "hbm_frac_algorithmic": (n_items * (xbytes + 8)) / (ms_assign * 1e-3) / 1e9 / HBM_PEAK_GBS
                 if ms_assign > 0 else None,
             },
             "cpu_baseline": cpu,
         }
+        if world == 1 and not wide and args.cold_sweeps > 0:
+            out["cold_start"] = cold_start(args, X, D, opts, local_rank)
         print(json.dumps(out))
     if dist:
         dist.destroy_process_group()
+
+
+def cold_start(args, X, D, opts, device):
+    """The reference's flow from its initialisation (np_mcmc.cpp:49-92: K = 20 random G0 clusters, uniform
+    labels), the first sweeps of the chain: per sweep the time, K and the new-cluster requests accepted
+    and deferred.  Each sweep is synchronised (K is read back), so the rate includes one host round trip
+    per sweep."""
+    from noparama_amd import NealAlgorithm8
+
+    smp = NealAlgorithm8(D, seed=args.seed + 1, device=device, param_update=args.param_update, **opts)
+    smp.set_data(X)
+    smp.init_random(20)
+    per, Ks, acc, dfr = [], [], [], []
+    s0 = smp.stats()
+    for _ in range(args.cold_sweeps):
+        t0 = time.perf_counter()
+        smp.sweep(1)  # synchronous
+        per.append((time.perf_counter() - t0) * 1e3)
+        s1 = smp.stats()
+        Ks.append(s1["K"])
+        acc.append(s1["new_clusters"] - s0["new_clusters"])
+        dfr.append(s1["rejected_requests"] - s0["rejected_requests"])
+        s0 = s1
+    tot = sum(per) * 1e-3
+    smp.close()
+    return {"sweeps": args.cold_sweeps, "value": args.cold_sweeps / tot, "unit": "sweeps/s",
+            "ms_per_sweep": [round(v, 3) for v in per], "K_per_sweep": Ks,
+            "new_clusters_per_sweep": acc, "deferred_requests_per_sweep": dfr,
+            "req_max": smp.req_max, "init": "init_random(20) (np_mcmc.cpp:49-92)"}
 
 
 def main_sm(args):

@@ -30,13 +30,14 @@ typedef enum {
     NP8_ERR_ARG = -1,      /* bad argument / unsupported configuration */
     NP8_ERR_SIGMA = -2,    /* a covariance with det <= 0 (reference would produce NaN weights) */
     NP8_ERR_RANGE = -3,    /* label or point index out of range */
-    NP8_ERR_CAPACITY = -4, /* new-cluster requests exceeded free slots or NP8_REQ_MAX in a chunk */
+    NP8_ERR_CAPACITY = -4, /* a fixed-size table is full (kcap / NP8_REQ_MAX limits of an entry point) */
     NP8_ERR_STATE = -5,    /* call order (no data / no state / no max-likelihood snapshot yet) */
     NP8_ERR_HIP = -6,      /* HIP runtime error (message has the HIP error string) */
     NP8_ERR_COMM = -7      /* RCCL error */
 } np8_status;
 
-#define NP8_REQ_MAX 4096 /* new-cluster requests one synchronous step can accept */
+#define NP8_REQ_MAX 4096     /* upper bound of np8_config.req_max */
+#define NP8_REQ_DEFAULT 1024 /* req_max when the configuration gives 0 */
 
 typedef struct {
     int32_t D;            /* dimension of the data items (data_t, include/np_data.h:9) */
@@ -55,6 +56,11 @@ typedef struct {
     int32_t mh_steps;     /* MH steps per cluster and sweep for NP8_PARAM_MH_G0; 0 -> 20 (np_mcmc.cpp:54) */
     int32_t prior;        /* NP8_PRIOR_*: the base measure G0 */
     int32_t contraction;  /* NP8_CONTRACT_*: arithmetic of the cluster likelihoods */
+    int32_t req_max;      /* new clusters one synchronous step may create (0 -> NP8_REQ_DEFAULT, at most
+                             NP8_REQ_MAX).  A step accepts the min(req_max, free slots, requests) requests of
+                             lowest scan position; the other requesters keep their cluster until their next
+                             update (DESIGN.md "Finalize").  Part of the chain's specification: the same
+                             value gives the same chain on any number of ranks. */
 } np8_config;
 
 /* Cluster-likelihood arithmetic (DESIGN.md "Wide path").
@@ -93,7 +99,8 @@ typedef struct {
     uint32_t epoch;             /* sweeps completed */
     int64_t new_clusters;       /* cumulative "new cluster" events (np_statistics.h step[0].accept) */
     int64_t existing_picks;     /* cumulative "existing cluster" events (step[0].reject) */
-    int64_t rejected_requests;  /* requests dropped by NP8_ERR_CAPACITY */
+    int64_t rejected_requests;  /* new-cluster requests not accepted in their step (req_max or no free slot):
+                                   those items kept their cluster until their next update */
     double best_loglik;         /* max over checks of sum_i log p(x_i | theta_z_i) (np_mcmc.cpp:187-203) */
     double last_loglik;
     double ms_assign, ms_finalize, ms_loglik; /* accumulated device time (when timing is enabled) */
@@ -106,6 +113,10 @@ typedef struct {
      * likelihoods) and of the attempt batches, and the launches behind them */
     double ms_sm_members, ms_sm_eval;
     int64_t n_timed_sm_members, n_timed_sm_eval;
+    /* executed work of the assign kernel while timing is enabled (cumulative): cluster quadratic forms
+     * evaluated per item (its own cluster included; rows left out by candidate pruning are not), and
+     * how many of them took the isotropic form iso |x - mu|^2 */
+    int64_t n_quad, n_quad_iso;
 } np8_stats_t;
 
 /* Create / destroy.  Replaces NealAlgorithm8::NealAlgorithm8 (np_neal_algorithm8.cpp:17-34). */
@@ -135,6 +146,10 @@ int np8_init_random(np8_ctx *ctx, int32_t K_init);
  * including the max-likelihood check every 5th sweep (np_mcmc.cpp:172-174).  Asynchronous on the
  * context's stream; errors raised on the device are reported by the next np8_sync(). */
 int np8_sweep(np8_ctx *ctx, int32_t n_sweeps);
+/* Prepares the next np8_sweep(ctx, n_sweeps) without running anything: captures and uploads the
+ * 20-sweep graph it would replay (whole synchronous sweeps on one rank), so that capture and
+ * instantiation are not paid inside the caller's timed region.  A no-op when no graph applies. */
+int np8_prepare_sweeps(np8_ctx *ctx, int32_t n_sweeps);
 
 /* Jain-Neal split-merge sweeps: the reference's `-a jain_neal_split` population update
  * (class JainNealAlgorithm, include/np_jain_neal_algorithm.h:52-98, update() at

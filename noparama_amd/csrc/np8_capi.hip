@@ -36,7 +36,9 @@ struct Timer {
 
 struct np8_ctx {
     // configuration
-    int D = 0, M = 0, DP = 0, CS = 0, kcap = 0, rec_cap = 0;
+    int D = 0, M = 0, DP = 0, CS = 0, kcap = 0;
+    int64_t rec_cap = 0;  // requests the exchanged record holds (one rank: every item of a step)
+    int req_max = NP8_REQ_DEFAULT;
     double alpha = 1.0, kappa = 1.0, nu = 1.0;
     uint64_t seed = 0;
     int64_t chunk = 0;
@@ -56,6 +58,7 @@ struct np8_ctx {
     // candidate pruning (np8_prune): per-slot radii and per-row candidate lists
     double *r2 = nullptr;
     int32_t *plist = nullptr, *plen = nullptr;
+    unsigned long long *evalc = nullptr;  // [kEvalSlots][2] executed-work counters (timing mode)
     bool prune_on = false;     // kcap small enough for kcap x kcap lists
     bool lists_valid = false;  // plist/plen describe the current table and membership
     bool r2_zero = false;      // r2 is 0 for every live slot (ready to collect)
@@ -84,6 +87,12 @@ struct np8_ctx {
     double *hyp = nullptr, *d_mu0 = nullptr, *d_LT = nullptr, *d_Gp = nullptr, *d_LTL = nullptr;
     unsigned char *rec = nullptr, *gath = nullptr;
     int64_t rec_bytes = 0;
+    // several ranks: the assign kernels append to the staging record (every item of a step), and
+    // np8_req_select moves this rank's req_max lowest-position requests into rec
+    unsigned char *stage = nullptr;
+    int64_t stage_cap = 0;
+    // np8_update_points: visits of each item within the current epoch (tag = epoch + 1)
+    std::vector<uint32_t> vis_tag, vis_n;
     int64_t *order = nullptr;
     int64_t order_cap = 0;
     double *partial = nullptr;
@@ -364,7 +373,7 @@ void free_device(np8_ctx *c) {
                     c->partial, c->dense_of, c->Xs[0], c->Xs[1], c->zs[0], c->zs[1], c->ids[0], c->ids[1],
                     c->s_hist, c->s_cursor, c->s_off, c->slot_iso, c->acc, c->r2, c->plist, c->plen,
                     c->sm_hist, c->sm_mem, c->sm_off, c->sm_live, c->sm_Xm, c->sm_ownm, c->sm_cross, c->sm_ctl,
-                    c->sm_typ, c->sm_slist, c->sm_stheta};
+                    c->sm_typ, c->sm_slist, c->sm_stheta, c->stage, c->evalc};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     if (c->sm_first_host) (void)hipHostFree(c->sm_first_host);
@@ -393,7 +402,8 @@ void free_device(np8_ctx *c) {
     c->mu_best = c->sigma_best = c->cand = nullptr;
     c->ctl = nullptr;
     c->hyp = c->d_mu0 = c->d_LT = c->d_Gp = c->d_LTL = nullptr;
-    c->rec = c->gath = nullptr;
+    c->rec = c->gath = c->stage = nullptr;
+    c->evalc = nullptr;
     c->order = nullptr;
     c->partial = nullptr;
     c->dense_of = nullptr;
@@ -407,6 +417,28 @@ int dalloc(np8_ctx *c, T **p, size_t n) {
     }
     HIPC(c, hipMalloc((void **)p, sizeof(T) * (n ? n : 1)));
     HIPC(c, hipMemsetAsync(*p, 0, sizeof(T) * (n ? n : 1), c->stream));
+    return NP8_OK;
+}
+
+// Exchange records (DESIGN.md "Finalize").  One rank: rec holds every item of a step (the assign kernel
+// appends there).  Several ranks: rec holds the req_max requests np8_req_select picks and is what the
+// ranks exchange; the staging record holds every item of a step.
+int alloc_records(np8_ctx *c) {
+    const int64_t items = c->n_loc > 0 ? c->n_loc : 1;
+    if (items > 0x7FFFFFFFll) return fail(c, NP8_ERR_ARG, "more than 2^31 items on one rank");
+    c->rec_cap = c->world > 1 ? c->req_max : (items > c->req_max ? items : c->req_max);
+    c->stage_cap = c->world > 1 ? items : 0;
+    c->rec_bytes = record_bytes(c->kcap, (int)c->rec_cap, c->D);
+    int r = dalloc(c, &c->rec, (size_t)c->rec_bytes);
+    if (r) return r;
+    if (c->world > 1) {
+        if ((r = dalloc(c, &c->gath, (size_t)c->rec_bytes * c->world)) ||
+            (r = dalloc(c, &c->stage, (size_t)record_bytes(c->kcap, (int)c->stage_cap, c->D))))
+            return r;
+    } else if (c->stage) {
+        (void)hipFree(c->stage);
+        c->stage = nullptr;
+    }
     return NP8_OK;
 }
 
@@ -514,7 +546,7 @@ FinArgs fin_args(np8_ctx *c, const unsigned char *recs, int world) {
     F.local_rec = c->rec;
     F.rec_bytes = c->rec_bytes;
     F.world = world;
-    F.rec_cap = c->rec_cap;
+    F.rec_cap = (int32_t)c->rec_cap;
     F.kcap = c->kcap;
     F.D = c->D;
     F.M = c->M;
@@ -548,7 +580,7 @@ FinArgs fin_args(np8_ctx *c, const unsigned char *recs, int world) {
     F.plist = c->plist;
     F.plen = c->plen;
     F.prior = c->prior;
-    F.pad2 = 0;
+    F.req_max = c->req_max;
     F.pend = c->pend;
     F.frame_payload = c->wide ? 1 : 0;
     F.pad3 = 0;
@@ -626,6 +658,14 @@ AssignArgs assign_args(np8_ctx *c, int64_t p0, int64_t p1, const int64_t *order,
     A.hyp = c->hyp;
     A.order = order;
     A.rec = c->rec;
+    {  // request area: the record itself (one rank) or the staging record
+        unsigned char *area = c->stage ? c->stage : c->rec;
+        const int64_t cap = c->stage ? c->stage_cap : c->rec_cap;
+        A.nreq = &reinterpret_cast<RecHeader *>(area)->nreq;
+        A.req = reinterpret_cast<Request *>(area + kRecHeaderBytes + 4ll * c->kcap);
+        A.vmu = reinterpret_cast<double *>(area + record_vmu_offset(c->kcap, (int)cap));
+        A.req_cap = (int32_t)cap;
+    }
     A.n_loc = c->n_loc;
     A.offset = c->offset;
     A.p0 = p0;
@@ -635,13 +675,13 @@ AssignArgs assign_args(np8_ctx *c, int64_t p0, int64_t p1, const int64_t *order,
     A.seed = c->seed;
     A.t = c->epoch - c->t_base;
     A.kcap = c->kcap;
-    A.rec_cap = c->rec_cap;
     A.plist = c->plist;
     A.plen = c->plen;
     A.ls = c->kcap;
     A.use_lists = 0;
     A.collect_r2 = 0;
-    A.pad = 0;
+    A.count_eval = c->timing ? 1 : 0;
+    A.evalc = c->evalc;
     A.r2 = c->r2;
     A.wfrag = c->wfrag;
     return A;
@@ -671,9 +711,11 @@ int launch_finalize(np8_ctx *c, const unsigned char *recs, int world) {
     return NP8_OK;
 }
 
-// Empty record: rebuild the candidate table from the slot arrays (after host uploads).
+// Empty record: rebuild the candidate table from the slot arrays (after host uploads).  Only the header
+// and the deltas are read (requests up to the header's count).
 int rebuild(np8_ctx *c) {
-    HIPC(c, hipMemsetAsync(c->rec, 0, c->rec_bytes, c->stream));
+    HIPC(c, hipMemsetAsync(c->rec, 0, kRecHeaderBytes + 4ull * c->kcap, c->stream));
+    if (c->stage) HIPC(c, hipMemsetAsync(c->stage, 0, kRecHeaderBytes, c->stream));
     return launch_finalize(c, c->rec, 1);
 }
 
@@ -759,6 +801,7 @@ int step(np8_ctx *c, int64_t p0, int64_t p1, const int64_t *order, bool use_perm
     if (r) return r;
     if (c->world > 1) {
         if (!c->comm) return fail(c, NP8_ERR_STATE, "host-exchange mode: use np8_step_local/np8_step_merge");
+        HIPC(c, np8_launch_req_select(c->stage, c->stage_cap, c->rec, c->rec_cap, c->kcap, c->D, c->req_max, c->stream));
         NCCLC(c, ncclAllGather(c->rec, c->gath, (size_t)c->rec_bytes, ncclUint8, c->comm, c->stream));
         return launch_finalize(c, c->gath, c->world);
     }
@@ -992,6 +1035,15 @@ int capture_graph(np8_ctx *c) {
     return NP8_OK;
 }
 
+// The graph for the sweeps starting at the current epoch (captured when missing or captured at another
+// phase, check parity or timing setting).
+int ensure_graph(np8_ctx *c) {
+    if (!c->graph || c->graph_par != (c->checks & 1) || c->graph_phase != (int)(c->epoch % kGraphSweeps) ||
+        c->graph_timing != c->timing)
+        return capture_graph(c);
+    return NP8_OK;
+}
+
 int run_graph(np8_ctx *c) {
     if (c->t_base != c->epoch) {  // the graph's epoch offsets are 0 .. kGraphSweeps-1
         HIPC(c, hipMemsetD32Async(reinterpret_cast<int *>(&c->ctl->t_base), (int)c->epoch, 1, c->stream));
@@ -1038,10 +1090,13 @@ int np8_create(np8_ctx **out, const np8_config *cfg) {
     c->CS = cand_stride(c->D);
     c->kcap = cfg->kcap > 0 ? cfg->kcap : (cfg->contraction == NP8_CONTRACT_F32_MFMA ? 512 : 2048);
 
-    if (c->kcap > 12288) {  // np8_finalize keeps two int[kcap] arrays in LDS beside 64 KB of request space
+    // np8_finalize keeps two int[kcap] arrays in dynamic LDS beside 64 KB of request space, plus its
+    // static shared memory: the whole must fit gfx950's 160 KB
+    if (np8_finalize_lds_bytes(c->kcap) + 1024 > 160 * 1024 || cfg->req_max < 0 || cfg->req_max > NP8_REQ_MAX) {
         delete c;
         return NP8_ERR_ARG;
     }
+    c->req_max = cfg->req_max > 0 ? cfg->req_max : NP8_REQ_DEFAULT;
     c->alpha = cfg->alpha;
     c->kappa = cfg->kappa;
     c->nu = cfg->nu;
@@ -1092,8 +1147,8 @@ int np8_create(np8_ctx **out, const np8_config *cfg) {
     c->own_stream = true;
     c->graphs_off = std::getenv("NP8_NO_GRAPH") != nullptr;  // A/B switch for launch-by-launch sweeps
     c->prune_on = !c->wide && c->kcap <= kPruneMaxKcap && std::getenv("NP8_NO_PRUNE") == nullptr;
-    c->rec_cap = kReqMax;
-    c->rec_bytes = record_bytes(c->kcap, c->rec_cap, c->D);
+    c->rec_cap = c->req_max;  // grown to the item count by np8_set_data (one rank)
+    c->rec_bytes = record_bytes(c->kcap, (int)c->rec_cap, c->D);
     int r = 0;
     const int D = c->D, DP = c->DP, kc = c->kcap;
     if ((r = dalloc(c, &c->slot_mu, (size_t)kc * D)) || (r = dalloc(c, &c->slot_P, (size_t)kc * DP)) ||
@@ -1102,7 +1157,7 @@ int np8_create(np8_ctx **out, const np8_config *cfg) {
         (r = dalloc(c, &c->mu_best, (size_t)kc * D)) || (r = dalloc(c, &c->sigma_best, (size_t)kc * D * D)) ||
         (r = dalloc(c, &c->cand, (size_t)kc * c->CS)) || (r = dalloc(c, &c->ctl, 1)) ||
         (r = dalloc(c, &c->dense_of, (size_t)kc)) || (r = dalloc(c, &c->slot_iso, (size_t)kc)) ||
-        (r = dalloc(c, &c->rec, (size_t)c->rec_bytes)) ||
+        (r = dalloc(c, &c->rec, (size_t)c->rec_bytes)) || (r = dalloc(c, &c->evalc, (size_t)2 * kEvalSlots)) ||
         (c->param_update != NP8_PARAM_FROZEN && (r = dalloc(c, &c->acc, (size_t)kc * (D + DP)))) ||
         (kc <= kPruneMaxKcap && ((r = dalloc(c, &c->r2, (size_t)kc)) || (r = dalloc(c, &c->plen, (size_t)kc)) ||
                                  (r = dalloc(c, &c->plist, (size_t)kc * kc))))) {
@@ -1199,8 +1254,10 @@ int np8_set_data(np8_ctx *c, const double *X, int64_t n, int32_t D, int64_t offs
             (r = dalloc(c, &c->ids[b], (size_t)n)))
             return r;
     if ((r = dalloc(c, &c->s_hist, (size_t)c->kcap)) || (r = dalloc(c, &c->s_cursor, (size_t)c->kcap)) ||
-        (r = dalloc(c, &c->s_off, (size_t)c->kcap)))
+        (r = dalloc(c, &c->s_off, (size_t)c->kcap)) || (r = alloc_records(c)))
         return r;
+    c->vis_tag.assign((size_t)n, 0u);
+    c->vis_n.assign((size_t)n, 0u);
     c->sorted_valid = false;
     if (c->wide) {  // rounded to fp32 (round to nearest even), as oracle/np8_oracle.c set_data does
         std::vector<float> soa((size_t)n * D);
@@ -1352,11 +1409,8 @@ int np8_sweep(np8_ctx *c, int32_t n_sweeps) {
     if (!sync && c->world > 1) return fail(c, NP8_ERR_ARG, "np8_sweep: chunk < N is single-rank only");
     for (int s = 0; s < n_sweeps; ++s) {
         if (graph_eligible(c, sync) && (uint32_t)(n_sweeps - s) >= kGraphSweeps) {
-            if (!c->graph || c->graph_par != (c->checks & 1) || c->graph_phase != (int)(c->epoch % kGraphSweeps) ||
-                c->graph_timing != c->timing) {
-                int r = capture_graph(c);
-                if (r) return r;
-            }
+            int r = ensure_graph(c);
+            if (r) return r;
             if (c->graph) {
                 int r = run_graph(c);
                 if (r) return r;
@@ -1380,6 +1434,18 @@ int np8_sweep(np8_ctx *c, int32_t n_sweeps) {
     return NP8_OK;
 }
 
+int np8_prepare_sweeps(np8_ctx *c, int32_t n_sweeps) {
+    if (!c) return NP8_ERR_ARG;
+    if (!c->have_state) return fail(c, NP8_ERR_STATE, "np8_prepare_sweeps: no state");
+    const int64_t chunk = (c->chunk <= 0 || c->chunk >= c->n_glob) ? c->n_loc : c->chunk;
+    if (!graph_eligible(c, chunk >= c->n_loc) || (uint32_t)n_sweeps < kGraphSweeps) return NP8_OK;
+    int r = ensure_graph(c);
+    if (r) return r;
+    if (c->graph) HIPC(c, hipGraphUpload(c->graph, c->stream));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    return NP8_OK;
+}
+
 int np8_update_points(np8_ctx *c, const int64_t *ids, int64_t n) {
     if (!c) return NP8_ERR_ARG;
     if (!c->have_state) return fail(c, NP8_ERR_STATE, "np8_update_points: no state");
@@ -1392,7 +1458,19 @@ int np8_update_points(np8_ctx *c, const int64_t *ids, int64_t n) {
         if (r) return r;
         c->order_cap = n;
     }
-    HIPC(c, hipMemcpyAsync(c->order, ids, sizeof(int64_t) * n, hipMemcpyHostToDevice, c->stream));
+    // the k-th visit of an item within this epoch draws with item key index | k << 32 (fresh auxiliaries
+    // and pick uniform for every visit, also when the caller never ends the sweep)
+    std::vector<int64_t> keys((size_t)n);
+    const uint32_t tag = c->epoch + 1u;
+    for (int64_t k = 0; k < n; ++k) {
+        const int64_t i = ids[k];
+        if (c->vis_tag[i] != tag) {
+            c->vis_tag[i] = tag;
+            c->vis_n[i] = 0;
+        }
+        keys[k] = i | ((int64_t)c->vis_n[i]++ << 32);
+    }
+    HIPC(c, hipMemcpyAsync(c->order, keys.data(), sizeof(int64_t) * n, hipMemcpyHostToDevice, c->stream));
     for (int64_t k = 0; k < n; ++k) {
         int r = step(c, k, k + 1, c->order, false);
         if (r) return r;
@@ -1417,10 +1495,7 @@ int np8_sync(np8_ctx *c) {
         HIPC(c, hipMemcpy(&c->ctl->err, &zero, sizeof(zero), hipMemcpyHostToDevice));
         if (h.err & kErrSigma)
             return fail(c, NP8_ERR_SIGMA, "a cluster precision is not numerically positive definite (wide path factor)");
-        if (h.err & kErrCapacity)
-            return fail(c, NP8_ERR_CAPACITY,
-                        "new-cluster requests exceeded the free slots or NP8_REQ_MAX in a step; those items kept "
-                        "their cluster (raise kcap or lower chunk)");
+        if (h.err & kErrCapacity) return fail(c, NP8_ERR_CAPACITY, "a device table is full");
     }
     return NP8_OK;
 }
@@ -1526,6 +1601,14 @@ int np8_stats(np8_ctx *c, np8_stats_t *out) {
     out->n_timed_sm_members = c->n_timed[4];
     out->n_timed_sm_eval = c->n_timed[5];
     out->mh_accepted = h.mh_accepted;
+    {
+        std::vector<unsigned long long> ev((size_t)2 * kEvalSlots);
+        HIPC(c, hipMemcpy(ev.data(), c->evalc, sizeof(unsigned long long) * ev.size(), hipMemcpyDeviceToHost));
+        for (int k = 0; k < kEvalSlots; ++k) {
+            out->n_quad += (int64_t)ev[2 * k];
+            out->n_quad_iso += (int64_t)ev[2 * k + 1];
+        }
+    }
     return NP8_OK;
 }
 
@@ -1554,21 +1637,17 @@ int np8_comm_unique_id(uint8_t out[128]) {
 }
 
 static int resize_records(np8_ctx *c, int world) {
+    drop_graph(c);  // a captured graph references the old records
     c->world = world;
-    c->rec_cap = world > 1 ? (kReqMax / world > 64 ? kReqMax / world : 64) : kReqMax;
-    c->rec_bytes = record_bytes(c->kcap, c->rec_cap, c->D);
-    int r = dalloc(c, &c->rec, (size_t)c->rec_bytes);
+    int r = alloc_records(c);
     if (r) return r;
-    if (world > 1) {
-        r = dalloc(c, &c->gath, (size_t)c->rec_bytes * world);
-        if (r) return r;
-    }
     HIPC(c, hipStreamSynchronize(c->stream));
     return NP8_OK;
 }
 
 int np8_comm_init(np8_ctx *c, const uint8_t id[128], int32_t rank, int32_t world) {
-    if (!c || world < 1 || rank < 0 || rank >= world) return NP8_ERR_ARG;
+    // np8_finalize walks at most 64 records (base[65] in LDS)
+    if (!c || world < 1 || world > 64 || rank < 0 || rank >= world) return NP8_ERR_ARG;
     if (!id) {  // host-exchange mode: the caller moves records (np8_step_local / np8_step_merge)
         c->rank = rank;
         return resize_records(c, world);
@@ -1595,6 +1674,8 @@ int np8_step_local(np8_ctx *c, void *record_out) {
     c->lists_valid = c->r2_zero = false;
     int r = launch_assign(c, 0, c->n_loc, nullptr, false);
     if (r) return r;
+    if (c->stage)
+        HIPC(c, np8_launch_req_select(c->stage, c->stage_cap, c->rec, c->rec_cap, c->kcap, c->D, c->req_max, c->stream));
     HIPC(c, hipMemcpyAsync(record_out, c->rec, (size_t)c->rec_bytes, hipMemcpyDeviceToHost, c->stream));
     HIPC(c, hipStreamSynchronize(c->stream));
     return NP8_OK;

@@ -33,12 +33,22 @@ struct Ctl {
                           // np8_finalize then copies them; parameter updates patch rows in place)
 };
 
+// Executed work of np8_assign when AssignArgs::count_eval is set (timing mode): per wave, the cluster
+// quadratic forms its items evaluated (own rows included) and how many took the isotropic form, added
+// to counter pair (wave id mod kEvalSlots) -- spread over many addresses: one counter pair for every wave
+// of the grid serialises the atomics in one L2 channel (4x the kernel time at C3).
+constexpr int kEvalSlots = 1024;
+
 enum : int32_t { kErrCapacity = 1, kErrSigma = 2 };
 
 // Exchange record of one rank for one synchronous step:
 //   RecHeader | int32 delta[kcap] | Request req[rec_cap] | double vmu[rec_cap][D+1]
 // vmu[q] = (v, mu) of the auxiliary request q asks to become a cluster (computed by the rank that
-// owns the item: mu needs the item's data, DESIGN.md "G0").
+// owns the item: mu needs the item's data, DESIGN.md "G0").  One rank: rec_cap >= the items of a
+// step, the assign kernel appends every request in arrival order.  Several ranks: the assign kernel
+// appends to a staging record of the same layout and np8_req_select copies this rank's req_max
+// requests of lowest scan position into the exchanged record (ascending), which is all np8_finalize
+// can accept from it (DESIGN.md "Finalize").
 struct RecHeader {
     int32_t nreq;
     int32_t pad[3];
@@ -47,12 +57,17 @@ constexpr int kRecHeaderBytes = 16;
 
 struct Request {
     int64_t pos;   // global scan position (orders requests across ranks)
-    int64_t i;     // global item index (Philox key of the auxiliary draw)
+    int64_t i;     // item key: global item index | visit << 32 (the Philox key of the auxiliary draw)
     int32_t m;     // which auxiliary
     int32_t zold;  // slot the item leaves
     int32_t lpos;  // position in the owner's label-sorted layout (-1: none)
     int32_t pad;
 };
+
+// Item keys (DESIGN.md "Randomness"): the Philox item counter of every per-item draw is
+// global index | visit << 32, visit = how often the item was already updated in this epoch (0 in every
+// sweep; repeated np8_update_points calls within one epoch carry it in the high word of the order entry).
+NP8_HD int64_t key_item(int64_t key) { return (int64_t)((uint64_t)key & 0xFFFFFFFFull); }
 
 NP8_HD int64_t record_vmu_offset(int kcap, int rec_cap) {
     return (kRecHeaderBytes + 4ll * kcap + (int64_t)sizeof(Request) * rec_cap + 15) & ~15ll;
@@ -74,21 +89,26 @@ struct AssignArgs {
     const int32_t *dense_of;  // slot -> row of the candidate table
     Ctl *ctl;
     const double *hyp; // mu0 | UinvT packed | caux | rsk | logam | nu
-    const int64_t *order;
-    unsigned char *rec;
+    const int64_t *order;  // explicit scan order: local item | visit << 32
+    unsigned char *rec;    // this rank's record (header, delta)
+    // where new-cluster requests are appended: the record itself (one rank) or the staging record
+    int32_t *nreq;
+    Request *req;
+    double *vmu;
     int64_t n_loc, offset;
     int64_t p0, p1;
     int32_t use_perm;
     Perm perm;
     uint64_t seed;
     uint32_t t;  // epoch offset: epoch = ctl->t_base + t
-    int32_t kcap, rec_cap;
+    int32_t kcap, req_cap;  // req_cap: entries of the request area (>= the items of the step)
     // candidate pruning (DESIGN.md "Pruning"): a wave whose items all sit in dense row k0 walks
     // plist[k0*ls .. +plen[k0]] instead of every row; r2 collects max |x - mu|^2 per slot for the
     // lists of the next sweep
     const int32_t *plist, *plen;
-    int32_t ls, use_lists, collect_r2, pad;
+    int32_t ls, use_lists, collect_r2, count_eval;
     double *r2;
+    unsigned long long *evalc;  // [kEvalSlots][2]: quadratic forms, isotropic ones
     // wide path (np8_wide.hip): per slot, the used MFMA fragment chunks of the fp32 factor followed by
     // the fp32 mean in fragment order (Wide<D>::ROW floats)
     const float *wfrag;
@@ -139,7 +159,7 @@ struct FinArgs {
     int32_t *plist, *plen;
     // NIW prior: accepted requests are listed in pend[4 q] = (byte offset of the request's record
     // payload in recs, item, m, slot) for np8_niw_aux_slots instead of being written here
-    int32_t prior, pad2;
+    int32_t prior, req_max;  // req_max: new clusters one step may create
     int64_t *pend;
     // wide path: request payloads are the item frame (|y0|, y0); slots created here are flagged for
     // the table refresh
@@ -312,6 +332,8 @@ hipError_t np8_launch_loglik_matrix(const np8::AssignArgs &A, int D, int M, int 
                                     double *out, hipStream_t s);
 size_t np8_finalize_lds_bytes(int kcap);
 hipError_t np8_launch_finalize(const np8::FinArgs &F, hipStream_t s);
+hipError_t np8_launch_req_select(const unsigned char *stage, int64_t stage_cap, unsigned char *rec, int64_t rec_cap,
+                                 int kcap, int D, int req_max, hipStream_t s);
 hipError_t np8_launch_loglik(const np8::LoglikArgs &A, int D, hipStream_t s);
 hipError_t np8_launch_loglik_reduce(const double *partial, int64_t nb, double *out, double *out2, hipStream_t s);
 hipError_t np8_launch_snapshot(const np8::SnapArgs &A, hipStream_t s);

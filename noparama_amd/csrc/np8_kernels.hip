@@ -141,6 +141,7 @@ __device__ __forceinline__ double norm_of(const double (&y0)[D]) {
     return sqrt(n2);
 }
 
+// Scan position -> local item | visit << 32 (the visit is non-zero only for explicit orders).
 __device__ __forceinline__ int64_t position_to_local(const AssignArgs &A, int64_t p) {
     if (A.order) return A.order[p];
     if (A.use_perm) return (int64_t)perm_apply(A.perm, (uint32_t)p);
@@ -159,9 +160,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void n
     const int cur = sorted ? A.ctl->cur : 0;
     int32_t *__restrict__ zs = cur ? A.zs[1] : A.zs[0];
     const int32_t *__restrict__ ids = cur ? A.ids[1] : A.ids[0];
-    const int64_t il = sorted ? (int64_t)ids[p] : position_to_local(A, p);
+    const int64_t lk = sorted ? (int64_t)ids[p] : position_to_local(A, p);
+    const int64_t il = key_item(lk);
     const int64_t xr = sorted ? p : il;
-    const uint64_t ig = (uint64_t)(A.offset + il);
+    const uint64_t ig = (uint64_t)(A.offset + lk);  // item key: global index | visit << 32
     const double *__restrict__ X = sorted ? (cur ? A.Xs[1] : A.Xs[0]) : A.X;
     const double *__restrict__ cand = A.cand;
     const double *__restrict__ hyp = A.hyp;
@@ -188,8 +190,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void n
     // a wave whose items share their cluster (the label-sorted layout) walks that cluster's pruned
     // candidate list: the rows left out are skipped by every lane's pick_step anyway (np8_prune)
     const int32_t z0 = __builtin_amdgcn_readfirstlane(zi);
-    if (A.use_lists && A.ctl->lists_ok && __ballot(zi != z0) == 0) {
-        const int32_t j0 = __builtin_amdgcn_readfirstlane(jo);
+    const bool walk_list = A.use_lists && A.ctl->lists_ok && __ballot(zi != z0) == 0;
+    const int32_t j0 = __builtin_amdgcn_readfirstlane(jo);
+    if (walk_list) {
         const int32_t nl = A.plen[j0];
         const int32_t *__restrict__ lst = A.plist + (int64_t)j0 * A.ls;
         for (int q = 0; q < nl; ++q) {
@@ -204,6 +207,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void n
             if (e[F + kFieldSlot] != zslot) pick_step(st, lw, j);
         }
     }
+    if (A.count_eval) {  // timing mode: the quadratic forms this wave executed (own row + walked rows)
+        const int nrow = walk_list ? A.plen[j0] : K;
+        int64_t nq = 0, niso = 0;
+        for (int q = 0; q < nrow; ++q) {
+            const int j = walk_list ? A.plist[(int64_t)j0 * A.ls + q] : q;
+            nq += 1;
+            niso += (cand[(int64_t)j * CS + F + kFieldIso] > 0.0) ? 1 : 0;
+        }
+        const uint64_t lanes = __ballot(1);
+        const int nl = __popcll(lanes);
+        const bool own_iso = cand[(int64_t)jo * CS + F + kFieldIso] > 0.0;
+        const int n_own_iso = __popcll(__ballot(own_iso));
+        if ((threadIdx.x & 63) == (__ffsll((unsigned long long)lanes) - 1)) {
+            unsigned long long *ec = A.evalc + 2 * ((blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) % kEvalSlots);
+            atomicAdd(ec, (unsigned long long)(nq * nl + nl));
+            atomicAdd(ec + 1, (unsigned long long)(niso * nl + n_own_iso));
+        }
+    }
     double y0[D];
     whiten<D>(hyp, x, y0);
     const double ny = norm_of<D>(y0);
@@ -213,7 +234,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void n
         for (int m = 0; m < M; ++m) pick_step(st, prior_aux_ll<D, PRIOR>(hyp, ny, A.seed, ig, t, m) + logam, K + m);
     }
 
-    RecHeader *hdr = reinterpret_cast<RecHeader *>(A.rec);
     int32_t *delta = reinterpret_cast<int32_t *>(A.rec + kRecHeaderBytes);
     const int32_t snew = (st.pick < K) ? (int32_t)cand[(int64_t)st.pick * CS + F + kFieldSlot] : -1;
     if (A.collect_r2) {
@@ -252,9 +272,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void n
             if (sorted) zs[p] = s;
         }
     } else {
-        const int q = atomicAdd(&hdr->nreq, 1);
-        if (q < A.rec_cap) {
-            Request *req = reinterpret_cast<Request *>(A.rec + kRecHeaderBytes + (int64_t)A.kcap * 4);
+        const int q = atomicAdd(A.nreq, 1);
+        if (q < A.req_cap) {  // always: the area holds every item of the step
             Request r;
             r.pos = sorted ? (int64_t)ig : A.offset + p;  // synchronous sweep: scan position = item index
             r.i = (int64_t)ig;
@@ -262,8 +281,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void n
             r.zold = zi;
             r.lpos = sorted ? (int32_t)p : -1;
             r.pad = 0;
-            req[q] = r;
-            double *vmu = reinterpret_cast<double *>(A.rec + record_vmu_offset(A.kcap, A.rec_cap)) + (int64_t)q * (D + 1);
+            A.req[q] = r;
+            double *vmu = A.vmu + (int64_t)q * (D + 1);
             if constexpr (PRIOR == kPriorNiw) {  // the item's frame; np8_niw_aux_slots builds the slot
                 vmu[0] = ny;
 #pragma unroll
@@ -544,8 +563,91 @@ __device__ void frame_to_vmu(const FinArgs &F, const double *frame, int64_t i, i
 
 }  // namespace
 
+// ---- request selection ------------------------------------------------------------------------------
+namespace {
+
+// The k-th smallest (1 <= k <= n) of n distinct scan positions (all < 2^33) held by pos_at(q), q < n:
+// three passes of an 11-bit radix histogram (2048 bins in LDS) over the entries that share the bits
+// fixed so far.  One workgroup of kFinThreads; every thread returns the same value.
+template <class PosAt>
+__device__ int64_t select_kth_pos(PosAt pos_at, int n, int k, int *hist /* 2048 */, int *sh /* >= 20 */) {
+    const int tid = threadIdx.x;
+    int64_t prefix = 0;
+    for (int pass = 0; pass < 3; ++pass) {
+        const int shift = 22 - 11 * pass;  // bits [shift, shift + 11)
+        const int64_t fixed = ~((1ll << (shift + 11)) - 1);
+        for (int b = tid; b < 2048; b += kFinThreads) hist[b] = 0;
+        __syncthreads();
+        for (int q = tid; q < n; q += kFinThreads) {
+            const int64_t pos = pos_at(q);
+            if ((pos & fixed) == prefix) atomicAdd(&hist[(pos >> shift) & 2047], 1);
+        }
+        __syncthreads();
+        const int h0 = hist[2 * tid], h1 = hist[2 * tid + 1];
+        int tot;
+        const int ex = block_excl_scan(h0 + h1, sh, &tot);
+        if (ex < k && k <= ex + h0) {
+            sh[18] = 2 * tid;
+            sh[19] = k - ex;
+        } else if (ex + h0 < k && k <= ex + h0 + h1) {
+            sh[18] = 2 * tid + 1;
+            sh[19] = k - ex - h0;
+        }
+        __syncthreads();
+        prefix |= (int64_t)sh[18] << shift;
+        k = sh[19];
+        __syncthreads();
+    }
+    return prefix;
+}
+
+}  // namespace
+
+// Several ranks: this rank's requests of the step (staging record, arrival order) -> the req_max of
+// lowest scan position in the exchanged record (the only ones np8_finalize can accept from this rank,
+// DESIGN.md "Finalize"); clears the staging count.  One workgroup; dynamic LDS: hist int[2048].
+__global__ __launch_bounds__(kFinThreads) void np8_req_select(const unsigned char *__restrict__ stage, int64_t stage_cap,
+                                                              unsigned char *__restrict__ rec, int64_t rec_cap, int kcap,
+                                                              int D, int req_max) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    int *hist = reinterpret_cast<int *>(smem);
+    __shared__ int sh[32];
+    __shared__ int s_cnt;
+    RecHeader *sh_hdr = reinterpret_cast<RecHeader *>(const_cast<unsigned char *>(stage));
+    const Request *sreq = reinterpret_cast<const Request *>(stage + kRecHeaderBytes + 4ll * kcap);
+    const double *svmu = reinterpret_cast<const double *>(stage + record_vmu_offset(kcap, (int)stage_cap));
+    Request *rreq = reinterpret_cast<Request *>(rec + kRecHeaderBytes + 4ll * kcap);
+    double *rvmu = reinterpret_cast<double *>(rec + record_vmu_offset(kcap, (int)rec_cap));
+    const int n = (int)min((int64_t)sh_hdr->nreq, stage_cap);
+    const int k = min(n, req_max);
+    int64_t T = INT64_MAX;
+    if (n > k && k > 0) T = select_kth_pos([&](int q) { return sreq[q].pos; }, n, k, hist, sh);
+    if (threadIdx.x == 0) s_cnt = 0;
+    __syncthreads();
+    for (int q = threadIdx.x; q < (k > 0 ? n : 0); q += kFinThreads) {
+        const Request r = sreq[q];
+        if (r.pos > T) continue;
+        const int o = atomicAdd(&s_cnt, 1);
+        rreq[o] = r;
+        for (int a = 0; a <= D; ++a) rvmu[(int64_t)o * (D + 1) + a] = svmu[(int64_t)q * (D + 1) + a];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        reinterpret_cast<RecHeader *>(rec)->nreq = k;
+        sh_hdr->nreq = 0;
+    }
+}
+
+namespace {
+__device__ int64_t request_pos(const FinArgs &F, const int *base, int q) { return request_at(F, base, q)->pos; }
+}  // namespace
+
 // One workgroup of 1024 threads.  Dynamic LDS: sort keys int64[kReqMax] | sort idx int[kReqMax] |
-// free slots int[kReqMax] | cnt int[kcap].
+// free slots int[kReqMax] (first the selection histogram, int[2048]) | cnt int[kcap] | live int[kcap].
+// New-cluster requests (DESIGN.md "Finalize"): the deltas are applied first and the free slots counted
+// with every requester still in its old slot; the A = min(req_max, free, requests) requests of lowest
+// scan position are accepted, in position order, into the lowest free slots in ascending order; each
+// accepted requester leaves its old slot; the others keep their cluster (deferred to their next update).
 __global__ __launch_bounds__(kFinThreads) void np8_finalize(FinArgs F) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     int64_t *keys = reinterpret_cast<int64_t *>(smem);
@@ -555,7 +657,7 @@ __global__ __launch_bounds__(kFinThreads) void np8_finalize(FinArgs F) {
     int *live_s = cnt_s + F.kcap;
     __shared__ int sh[32];
     __shared__ int base[65];
-    __shared__ int s_flags[4];  // nreq, overflow, accept, free
+    __shared__ int s_flags[4];  // nreq, gathered
     const int tid = threadIdx.x;
     const int kcap = F.kcap;
     const int D = F.D, DP = D * (D + 1) / 2, CS = cand_stride(D);
@@ -563,16 +665,14 @@ __global__ __launch_bounds__(kFinThreads) void np8_finalize(FinArgs F) {
     const int s0 = min(kcap, tid * per), s1 = min(kcap, s0 + per);
 
     if (tid == 0) {
-        int n = 0, of = 0;
+        int n = 0;
         for (int r = 0; r < F.world; ++r) {
-            const int nr = rec_header(F, r)->nreq;
-            of |= (nr > F.rec_cap);
             base[r] = n;
-            n += min(nr, F.rec_cap);
+            n += min(rec_header(F, r)->nreq, F.rec_cap);
         }
         base[F.world] = n;
         s_flags[0] = n;
-        s_flags[1] = of;
+        s_flags[1] = 0;
     }
     for (int s = s0; s < s1; ++s) {
         int c = F.cnt[s];
@@ -581,39 +681,40 @@ __global__ __launch_bounds__(kFinThreads) void np8_finalize(FinArgs F) {
     }
     __syncthreads();
     const int nreq = s_flags[0];
-    const bool try_accept = (nreq > 0) && (s_flags[1] == 0) && (nreq <= kReqMax);
-    if (try_accept) {  // block-uniform
-        for (int q = tid; q < nreq; q += kFinThreads) atomicSub(&cnt_s[request_at(F, base, q)->zold], 1);
-    }
-    __syncthreads();
     int nf = 0, nfree = 0, frank = 0;
-    if (try_accept) {  // block-uniform: the free slots are only needed when requests can be accepted
+    if (nreq > 0) {  // block-uniform: the free slots are only needed when there are requests
         for (int s = s0; s < s1; ++s) nf += (cnt_s[s] == 0);
         frank = block_excl_scan(nf, sh, &nfree);
     }
-    const bool accept = try_accept && (nreq <= nfree);
-    if (try_accept && !accept) {
-        for (int q = tid; q < nreq; q += kFinThreads) atomicAdd(&cnt_s[request_at(F, base, q)->zold], 1);
-    }
+    const int A = min(min(nreq, F.req_max), nfree);  // accepted this step (block-uniform)
     if (tid == 0) {
-        if (nreq > 0 && !accept) {
-            F.ctl->err |= kErrCapacity;
-            F.ctl->n_rejected += (s_flags[1] ? (int64_t)nreq + 1 : (int64_t)nreq);
-        }
-        if (accept) F.ctl->n_new += nreq;
+        F.ctl->n_new += A;
+        F.ctl->n_rejected += nreq - A;
     }
-    if (accept) {  // block-uniform
+    if (A > 0) {  // block-uniform
+        // the A requests of lowest scan position: all of them, or those up to the A-th smallest
+        const int64_t T = (nreq > A) ? select_kth_pos([&](int q) { return request_pos(F, base, q); }, nreq, A,
+                                                      freeslot, sh)
+                                     : INT64_MAX;
+        for (int q = tid; q < nreq; q += kFinThreads) {
+            const int64_t pos = request_pos(F, base, q);
+            if (pos > T) continue;
+            const int o = atomicAdd(&s_flags[1], 1);
+            keys[o] = pos;
+            kidx[o] = q;
+        }
+        __syncthreads();
+        int n2 = 1;
+        while (n2 < A) n2 <<= 1;
+        for (int q = A + tid; q < n2; q += kFinThreads) {
+            keys[q] = INT64_MAX;
+            kidx[q] = -1;
+        }
         for (int s = s0; s < s1; ++s)
             if (cnt_s[s] == 0) {
-                if (frank < nreq) freeslot[frank] = s;
+                if (frank < A) freeslot[frank] = s;
                 ++frank;
             }
-        int n2 = 1;
-        while (n2 < nreq) n2 <<= 1;
-        for (int q = tid; q < n2; q += kFinThreads) {
-            keys[q] = (q < nreq) ? request_at(F, base, q)->pos : INT64_MAX;
-            kidx[q] = q;
-        }
         __syncthreads();
         for (int k = 2; k <= n2; k <<= 1) {
             for (int j = k >> 1; j > 0; j >>= 1) {
@@ -634,7 +735,7 @@ __global__ __launch_bounds__(kFinThreads) void np8_finalize(FinArgs F) {
                 __syncthreads();
             }
         }
-        for (int q = tid; q < nreq; q += kFinThreads) {
+        for (int q = tid; q < A; q += kFinThreads) {
             const Request r = *request_at(F, base, kidx[q]);
             const int s = freeslot[q];
             if (F.prior == kPriorNiw) {  // built by np8_niw_aux_slots (O(D^3) per slot)
@@ -652,8 +753,10 @@ __global__ __launch_bounds__(kFinThreads) void np8_finalize(FinArgs F) {
             }
             if (F.wdirty) F.wdirty[s] = 1;
             cnt_s[s] = 1;
-            if (r.i >= F.offset && r.i < F.offset + F.n_loc) {
-                F.z[r.i - F.offset] = s;
+            atomicSub(&cnt_s[r.zold], 1);  // a live slot (the requester is in it), never one of the free ones
+            const int64_t item = key_item(r.i);
+            if (item >= F.offset && item < F.offset + F.n_loc) {
+                F.z[item - F.offset] = s;
                 if (F.zs[0] && r.lpos >= 0) (F.ctl->cur ? F.zs[1] : F.zs[0])[r.lpos] = s;
             }
         }
@@ -667,7 +770,7 @@ __global__ __launch_bounds__(kFinThreads) void np8_finalize(FinArgs F) {
     }
     // the live rows keep their order and parameters unless a slot changed liveness, requests were
     // accepted or the state was uploaded: then mu/P' of every row are copied below
-    const bool copy_rows = __syncthreads_or(lchange | (accept ? 1 : 0) | (F.ctl->cand_fresh ? 0 : 1)) != 0;
+    const bool copy_rows = __syncthreads_or(lchange | (A > 0 ? 1 : 0) | (F.ctl->cand_fresh ? 0 : 1)) != 0;
     int nlive;
     int k = block_excl_scan(nl, sh, &nlive);
     for (int s = s0; s < s1; ++s) {
@@ -696,7 +799,7 @@ __global__ __launch_bounds__(kFinThreads) void np8_finalize(FinArgs F) {
     if (tid == 0) {
         F.ctl->K = nlive;
         F.ctl->cand_fresh = 1;
-        F.ctl->n_pend = (F.prior == kPriorNiw && accept) ? nreq : 0;
+        F.ctl->n_pend = (F.prior == kPriorNiw) ? A : 0;
     }
     if (F.prune) {  // candidate lists for the next sweep, one wave per row (block-uniform branch)
         __syncthreads();
@@ -1105,6 +1208,13 @@ size_t np8_finalize_lds_bytes(int kcap) {
 
 hipError_t np8_launch_finalize(const FinArgs &F, hipStream_t s) {
     hipLaunchKernelGGL(np8_finalize, dim3(1), dim3(kFinThreads), np8_finalize_lds_bytes(F.kcap), s, F);
+    return hipGetLastError();
+}
+
+hipError_t np8_launch_req_select(const unsigned char *stage, int64_t stage_cap, unsigned char *rec, int64_t rec_cap,
+                                 int kcap, int D, int req_max, hipStream_t s) {
+    hipLaunchKernelGGL(np8_req_select, dim3(1), dim3(kFinThreads), sizeof(int) * 2048, s, stage, stage_cap, rec, rec_cap,
+                       kcap, D, req_max);
     return hipGetLastError();
 }
 

@@ -260,9 +260,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void n
 
     // the lane's own item (lanes past the end of the range mirror the wave's first item)
     const int64_t pc = valid ? p : (wave_live ? pw : A.p0);
-    const int64_t il = sorted ? (int64_t)ids[pc] : wpos_to_local(A, pc);
+    const int64_t lk = sorted ? (int64_t)ids[pc] : wpos_to_local(A, pc);
+    const int64_t il = key_item(lk);
     const int64_t xr = sorted ? pc : il;
-    const uint64_t ig = (uint64_t)(A.offset + il);
+    const uint64_t ig = (uint64_t)(A.offset + lk);  // item key: global index | visit << 32
     const int32_t zi = sorted ? zs[pc] : A.z[il];
     const int32_t jo = A.dense_of[zi];
 
@@ -290,7 +291,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void n
     for (int nt = 0; nt < 4; ++nt) {
         int64_t pq = pw + nt * 16 + col;
         if (pq >= A.p1) pq = pc;  // padding column: any valid item, result unused
-        const int64_t xq = sorted ? pq : wpos_to_local(A, pq);
+        const int64_t xq = sorted ? pq : key_item(wpos_to_local(A, pq));
 #pragma unroll
         for (int st = 0; st < W::S; ++st) xb[nt][st] = X[(int64_t)(4 * st + g) * n + xq];
     }
@@ -334,7 +335,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void n
     for (int m = 0; m < M; ++m) pick_step(st, lwa[m], K + m);
     if (!valid) return;
 
-    RecHeader *hdr = reinterpret_cast<RecHeader *>(A.rec);
     int32_t *delta = reinterpret_cast<int32_t *>(A.rec + kRecHeaderBytes);
     const int32_t snew = (st.pick < K) ? (int32_t)cand[(int64_t)st.pick * CS + F + kFieldSlot] : -1;
     const uint64_t mv = __ballot(snew != zi);
@@ -348,9 +348,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void n
             if (sorted) zs[pc] = snew;
         }
     } else {
-        const int q = atomicAdd(&hdr->nreq, 1);
-        if (q < A.rec_cap) {
-            Request *req = reinterpret_cast<Request *>(A.rec + kRecHeaderBytes + (int64_t)A.kcap * 4);
+        const int q = atomicAdd(A.nreq, 1);
+        if (q < A.req_cap) {  // always: the area holds every item of the step
             Request r;
             r.pos = sorted ? (int64_t)ig : A.offset + p;
             r.i = (int64_t)ig;
@@ -358,8 +357,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void n
             r.zold = zi;
             r.lpos = sorted ? (int32_t)pc : -1;
             r.pad = 0;
-            req[q] = r;
-            double *vmu = reinterpret_cast<double *>(A.rec + record_vmu_offset(A.kcap, A.rec_cap)) + (int64_t)q * (D + 1);
+            A.req[q] = r;
+            double *vmu = A.vmu + (int64_t)q * (D + 1);
             wide_frame_payload<D>(hyp, X, n, xr, vmu);
         }
     }

@@ -28,6 +28,7 @@ NP8_ERR_STATE = -5
 NP8_ERR_HIP = -6
 NP8_ERR_COMM = -7
 NP8_REQ_MAX = 4096
+NP8_REQ_DEFAULT = 1024
 
 _ERRNAMES = {
     NP8_ERR_ARG: "NP8_ERR_ARG",
@@ -63,6 +64,7 @@ class _Config(C.Structure):
         ("mh_steps", C.c_int32),
         ("prior", C.c_int32),
         ("contraction", C.c_int32),
+        ("req_max", C.c_int32),
     ]
 
 
@@ -93,6 +95,8 @@ class Stats(C.Structure):
         ("ms_sm_eval", C.c_double),
         ("n_timed_sm_members", C.c_int64),
         ("n_timed_sm_eval", C.c_int64),
+        ("n_quad", C.c_int64),
+        ("n_quad_iso", C.c_int64),
     ]
 
 
@@ -124,6 +128,7 @@ def lib():
         "np8_set_state_counts": ([vp, vp, i32, vp, vp, vp], i32),
         "np8_init_random": ([vp, i32], i32),
         "np8_sweep": ([vp, i32], i32),
+        "np8_prepare_sweeps": ([vp, i32], i32),
         "np8_update_points": ([vp, vp, i64], i32),
         "np8_end_sweep": ([vp], i32),
         "np8_sync": ([vp], i32),
@@ -175,13 +180,16 @@ class NealAlgorithm8:
     `param_update`: "frozen" (the reference's effective behaviour), "mh_g0" (UpdateClusters as
     intended: `mh_steps` G0-proposal MH steps per cluster after every sweep, np_update_clusters.cpp) or
     "niw_conjugate" (prior="niw": exact posterior draw per cluster, normalinvwishart.h:66-75).
+    `req_max`: new clusters one synchronous step may create (0: NP8_REQ_DEFAULT); requests beyond it
+    or beyond the free slots are deferred to the item's next update (lowest scan positions first).
     `prior`: "reference" (the reference's G0 as it draws) or "niw" (a proper Normal-Inverse-Wishart with
     kappa0 = kappa, nu0 = nu >= D + 1, Psi0 = Lambda).  `contraction`: "f64" (D <= 16) or "f32" (D in
     {32, 64}: items in fp32, cluster likelihoods on the fp32 matrix cores; config C5).
     """
 
     def __init__(self, D, M=3, alpha=1.0, mu0=None, kappa=1.0 / 500, nu=4.0, Lambda=None, seed=0, kcap=None,
-                 chunk=0, device=-1, param_update="frozen", mh_steps=20, prior="reference", contraction="f64"):
+                 chunk=0, device=-1, param_update="frozen", mh_steps=20, prior="reference", contraction="f64",
+                 req_max=0):
         if kcap is None:  # the library's default: 512 on the wide path (kcap^2 x D offset table), else 2048
             kcap = 512 if contraction == "f32" else 2048
         self.D, self.M, self.kcap = int(D), int(M), int(kcap)
@@ -202,6 +210,8 @@ class NealAlgorithm8:
         if contraction not in CONTRACTION:
             raise ValueError(f"contraction must be one of {sorted(CONTRACTION)}")
         cfg.contraction = CONTRACTION[contraction]
+        cfg.req_max = int(req_max)
+        self.req_max = int(req_max) or NP8_REQ_DEFAULT
         h = C.c_void_p()
         r = lib().np8_create(C.byref(h), C.byref(cfg))
         if r:
@@ -257,6 +267,10 @@ class NealAlgorithm8:
 
     def sync(self):
         self._check(lib().np8_sync(self._h))
+
+    def prepare_sweeps(self, n):
+        """Capture/upload the sweep graph the next sweep(n) replays (no sweep runs)."""
+        self._check(lib().np8_prepare_sweeps(self._h, int(n)))
 
     def sm_sweep(self, n=1):
         """n Jain-Neal split-merge sweeps (np8_sm_sweep): N split/merge attempts each, then the
@@ -362,7 +376,7 @@ class NealAlgorithm8:
         s = self.stats()
         print("Statistics:")
         print(f" # of new cluster events accepted: {s['new_clusters']}")
-        print(f" # of rejected new-cluster requests: {s['rejected_requests']}")
+        print(f" # of deferred new-cluster requests: {s['rejected_requests']}")
 
 
 class JainNealAlgorithm(NealAlgorithm8):

@@ -405,6 +405,10 @@ struct np8o_ctx {
     int64_t *rq_pos, *rq_i;
     int32_t *rq_m, *rq_zold;
     int64_t mh_accepted;
+    int64_t n_new, n_deferred; /* accepted / not accepted new-cluster requests (cumulative) */
+    int32_t req_max;
+    /* per-item visits within the epoch (np8o_update_points): tag = epoch + 1, count */
+    uint32_t *vis_tag, *vis_n;
     /* split-merge (np8o_sm_sweep): member lists, per-member scratch, outcome counts */
     int64_t *sm_off, *sm_cur, *sm_mem;
     double *sm_v0, *sm_v1;
@@ -486,8 +490,10 @@ np8o_ctx *np8o_create(const np8o_config *cfg) {
         !(cfg->contraction == NP8O_CONTRACT_F32 && (cfg->D == 32 || cfg->D == 64) &&
           cfg->param_update != NP8O_PARAM_MH_G0))
         return NULL;
+    if (cfg->req_max < 0 || cfg->req_max > NP8O_REQMAX) return NULL;
     np8o_ctx *c = (np8o_ctx *)calloc(1, sizeof(np8o_ctx));
     c->cfg = *cfg;
+    c->req_max = cfg->req_max > 0 ? cfg->req_max : NP8O_REQ_DEFAULT;
     const int D = cfg->D;
     c->D = D;
     c->M = cfg->M;
@@ -600,6 +606,8 @@ void np8o_destroy(np8o_ctx *c) {
     free(c->sm_v1);
     free(c->sm_flag);
     free(c->tri_asg);
+    free(c->vis_tag);
+    free(c->vis_n);
     free(c);
 }
 
@@ -616,6 +624,10 @@ int np8o_set_data(np8o_ctx *c, const double *X, int64_t N) {
     free(c->sm_v1);
     free(c->sm_flag);
     free(c->tri_asg);
+    free(c->vis_tag);
+    free(c->vis_n);
+    c->vis_tag = (uint32_t *)calloc((size_t)(N > 0 ? N : 1), sizeof(uint32_t));
+    c->vis_n = (uint32_t *)calloc((size_t)(N > 0 ? N : 1), sizeof(uint32_t));
     c->N = N;
     c->X = (double *)malloc(sizeof(double) * (size_t)(N > 0 ? N : 1) * c->D);
     if (N > 0) memcpy(c->X, X, sizeof(double) * (size_t)N * c->D);
@@ -756,10 +768,10 @@ static void aux_xi(const np8o_ctx *c, uint64_t i, uint32_t t, int m, const doubl
     for (int a = 0; a < D; ++a) xi[a] = fma(xpar, yh[a], sc * w[a]);
 }
 
-/* The M auxiliary draws of item i (local data row) at epoch t: v[m], mu[m*D..]. */
+/* The M auxiliary draws of item key i (data row NP8O_ITEM(i)) at epoch t: v[m], mu[m*D..]. */
 static void aux_draws(const np8o_ctx *c, uint64_t i, uint32_t t, double *v, double *mu /* M*D */) {
     double y0[NP8O_DMAX];
-    const double ny = whiten(c, c->X + (size_t)i * c->D, y0);
+    const double ny = whiten(c, c->X + (size_t)NP8O_ITEM(i) * c->D, y0);
     for (int m = 0; m < c->M; ++m) {
         double xpar, chi2, xi[NP8O_DMAX];
         aux_core(c, i, t, m, v + m, &xpar, &chi2);
@@ -1102,7 +1114,7 @@ static int niw_draw_impl(const np8o_ctx *c, uint64_t i, uint32_t t, uint32_t str
 static void niw_slot_from_aux(np8o_ctx *c, int s, uint64_t i, uint32_t t, int m) {
     const int D = c->D;
     double dt[NP8O_DMAX];
-    whiten(c, c->X + (size_t)i * D, dt);
+    whiten(c, c->X + (size_t)NP8O_ITEM(i) * D, dt);
     niw_aux_slot(c, i, t, m, dt, c->slot_mu + (size_t)s * D, c->slot_P + (size_t)s * c->DP,
                  c->slot_sigma + (size_t)s * D * D, c->slot_c + s);
     if (c->wdirty) c->wdirty[s] = 1;
@@ -1348,20 +1360,20 @@ static inline void pick_step(pick_state *st, double lw, int32_t j) {
  * the reference deletes on retract, membertrix.cpp:200-203), then every other live cluster in
  * ascending slot order (weight n_k), then the M auxiliaries (weight alpha/M).  Returns the candidate
  * row (< K existing, >= K auxiliary). */
-static int32_t choose(const np8o_ctx *c, int64_t i, const double *x, int32_t zi) {
+static int32_t choose(const np8o_ctx *c, int64_t key, const double *x, int32_t zi) {
     const int K = c->K, M = c->M;
     const int jo = c->dense_of[zi];
     pick_state st;
     st.T = cand_ll(c, x, jo, jo) + c->logn1[jo];
     st.S = 1.0;
-    st.u = np8o_uniform(c->cfg.seed, (uint64_t)i, c->t, NP8O_STREAM_PICK, 0);
+    st.u = np8o_uniform(c->cfg.seed, (uint64_t)key, c->t, NP8O_STREAM_PICK, 0);
     st.pick = jo;
     for (int j = 0; j < K; ++j) {
         if (j == jo) continue;
         pick_step(&st, cand_ll(c, x, jo, j) + c->logn[j], j);
     }
     double lla[NP8O_MMAX];
-    aux_ll(c, x, (uint64_t)i, c->t, lla);
+    aux_ll(c, x, (uint64_t)key, c->t, lla);
     for (int m = 0; m < M; ++m) pick_step(&st, lla[m] + c->logam, K + m);
     return st.pick;
 }
@@ -1383,10 +1395,10 @@ static int assign_range_impl(np8o_ctx *c, int64_t p0, int64_t p1, int sync, cons
          * (finalize orders requests by position) */
 #pragma omp parallel for schedule(static)
         for (int64_t p = p0; p < p1; ++p) {
-            const int64_t i = position_to_point(c, p, sync, order);
+            const int64_t key = position_to_point(c, p, sync, order), i = NP8O_ITEM(key);
             const double *x = c->X + (size_t)i * c->D;
             const int32_t zi = c->z[i];
-            const int32_t j = choose(c, i, x, zi);
+            const int32_t j = choose(c, key, x, zi);
             if (j < c->K) {
                 const int32_t s = c->live[j];
                 if (s != zi) {
@@ -1402,7 +1414,7 @@ static int assign_range_impl(np8o_ctx *c, int64_t p0, int64_t p1, int sync, cons
                 q = nr++;
                 if (q < req_cap) {
                     req_pos[q] = p;
-                    req_i[q] = i;
+                    req_i[q] = key;
                     req_m[q] = j - c->K;
                     req_zold[q] = zi;
                 }
@@ -1412,10 +1424,10 @@ static int assign_range_impl(np8o_ctx *c, int64_t p0, int64_t p1, int sync, cons
         return err;
     }
     for (int64_t p = p0; p < p1; ++p) {
-        int64_t i = position_to_point(c, p, sync, order);
+        const int64_t key = position_to_point(c, p, sync, order), i = NP8O_ITEM(key);
         const double *x = c->X + (size_t)i * c->D;
         int32_t zi = c->z[i];
-        int32_t j = choose(c, i, x, zi);
+        int32_t j = choose(c, key, x, zi);
         if (j < c->K) {
             int32_t s = c->live[j];
             if (s != zi) {
@@ -1426,11 +1438,11 @@ static int assign_range_impl(np8o_ctx *c, int64_t p0, int64_t p1, int sync, cons
         } else {
             if (nr < req_cap) {
                 req_pos[nr] = p;
-                req_i[nr] = i;
+                req_i[nr] = key;
                 req_m[nr] = j - c->K;
                 req_zold[nr] = zi;
             }
-            ++nr; /* counted even past the capacity: finalize then rejects the whole list */
+            ++nr; /* counted even past the capacity */
         }
     }
     *n_req = nr;
@@ -1443,8 +1455,12 @@ int np8o_assign_range(np8o_ctx *c, int64_t p0, int64_t p1, int32_t *delta, int64
     return assign_range_impl(c, p0, p1, chunk >= c->N, NULL, delta, req_pos, req_i, req_m, req_zold, req_cap, n_req);
 }
 
-/* Requests are accepted all-or-none: at most NP8O_REQMAX per finalize and no more than the free
- * slots left once every requester has left its old slot (DESIGN.md "Finalize"). */
+/* New-cluster requests (DESIGN.md "Finalize"): the deltas are applied first; the free slots are
+ * counted then, with every requester still in its old slot; the A = min(req_max, free, n_req)
+ * requests of lowest scan position are accepted and take the lowest free slots in ascending order
+ * (position order); each accepted requester leaves its old slot (which may become free for the next
+ * step); the remaining requesters keep their cluster -- their update is deferred to the next time they
+ * are visited (the next step or sweep), like an item whose draw picked its own cluster. */
 static int cmp_req(const void *a, const void *b) {
     const int64_t *x = (const int64_t *)a, *y = (const int64_t *)b;
     return (x[0] > y[0]) - (x[0] < y[0]);
@@ -1453,46 +1469,44 @@ static int cmp_req(const void *a, const void *b) {
 int np8o_finalize(np8o_ctx *c, const int32_t *delta, const int64_t *req_pos, const int64_t *req_i,
                   const int32_t *req_m, const int32_t *req_zold, int32_t n_req, int64_t owner_lo, int64_t owner_hi) {
     const int D = c->D;
-    int err = 0;
     for (int s = 0; s < c->kcap; ++s) c->cnt[s] += delta[s];
-    int accept = (n_req <= NP8O_REQMAX);
-    if (n_req > 0 && accept) {
-        for (int32_t q = 0; q < n_req; ++q) c->cnt[req_zold[q]] -= 1;
-        int32_t nfree = 0;
-        for (int s = 0; s < c->kcap; ++s) nfree += (c->cnt[s] == 0);
-        if (n_req > nfree) {
-            accept = 0;
-            for (int32_t q = 0; q < n_req; ++q) c->cnt[req_zold[q]] += 1;
-        }
-    }
-    if (n_req > 0 && !accept) err = -4;
-    if (n_req > 0 && accept) {
+    int32_t nfree = 0;
+    for (int s = 0; s < c->kcap; ++s) nfree += (c->cnt[s] == 0);
+    int32_t A = n_req < c->req_max ? n_req : c->req_max;
+    if (A > nfree) A = nfree;
+    if (A > 0) {
         int64_t *ord = (int64_t *)malloc(sizeof(int64_t) * 2 * (size_t)n_req);
         for (int32_t q = 0; q < n_req; ++q) {
             ord[2 * q] = req_pos[q];
             ord[2 * q + 1] = q;
         }
         qsort(ord, (size_t)n_req, 2 * sizeof(int64_t), cmp_req);
-        int32_t q = 0;
-        for (int s = 0; s < c->kcap && q < n_req; ++s) {
-            if (c->cnt[s] != 0) continue;
-            int64_t r = ord[2 * q + 1];
-            int64_t i = req_i[r];
+        /* the free slots before any requester leaves (a slot emptied by a departure is free next step) */
+        int32_t *freeslot = (int32_t *)malloc(sizeof(int32_t) * (size_t)A);
+        for (int s = 0, f = 0; s < c->kcap && f < A; ++s)
+            if (c->cnt[s] == 0) freeslot[f++] = s;
+        for (int32_t q = 0; q < A; ++q) {
+            const int s = freeslot[q];
+            const int64_t r = ord[2 * q + 1];
+            const int64_t key = req_i[r], i = NP8O_ITEM(key);
             if (c->cfg.prior == NP8O_PRIOR_NIW) {
-                niw_slot_from_aux(c, s, (uint64_t)i, c->t, req_m[r]);
+                niw_slot_from_aux(c, s, (uint64_t)key, c->t, req_m[r]);
             } else {
                 double vv[NP8O_MMAX], mm[NP8O_MMAX * NP8O_DMAX];
-                aux_draws(c, (uint64_t)i, c->t, vv, mm);
+                aux_draws(c, (uint64_t)key, c->t, vv, mm);
                 slot_from_aux(c, s, vv[req_m[r]], mm + (size_t)req_m[r] * D);
             }
             c->cnt[s] = 1;
+            c->cnt[req_zold[r]] -= 1;
             if (owner_hi < 0 || (i >= owner_lo && i < owner_hi)) c->z[i] = s;
-            ++q;
         }
+        free(freeslot);
         free(ord);
     }
+    c->n_new += A;
+    c->n_deferred += n_req - A;
     rebuild_dense(c);
-    return err;
+    return n_req - A;
 }
 
 double np8o_total_loglik(np8o_ctx *c) {
@@ -1668,9 +1682,8 @@ static int run_chunks(np8o_ctx *c, const int64_t *order, int64_t npos, int64_t c
         int32_t nr = 0;
         int e1 = assign_range_impl(c, p0, p1, sync, order, c->delta, c->rq_pos, c->rq_i, c->rq_m, c->rq_zold,
                                    (int32_t)(p1 - p0), &nr);
-        int e2 = np8o_finalize(c, c->delta, c->rq_pos, c->rq_i, c->rq_m, c->rq_zold, nr, 0, -1);
+        (void)np8o_finalize(c, c->delta, c->rq_pos, c->rq_i, c->rq_m, c->rq_zold, nr, 0, -1);
         if (e1) err = e1;
-        if (e2) err = e2;
     }
     return err;
 }
@@ -1692,7 +1705,24 @@ int np8o_sweep(np8o_ctx *c, int32_t n) {
 int np8o_update_points(np8o_ctx *c, const int64_t *ids, int64_t n) {
     for (int64_t k = 0; k < n; ++k)
         if (ids[k] < 0 || ids[k] >= c->N) return -3;
-    return run_chunks(c, ids, n, 1);
+    /* item keys: the k-th visit of an item within this epoch draws with visit index k */
+    int64_t *keys = (int64_t *)malloc(sizeof(int64_t) * (size_t)(n > 0 ? n : 1));
+    for (int64_t k = 0; k < n; ++k) {
+        const int64_t i = ids[k];
+        if (c->vis_tag[i] != c->t + 1u) {
+            c->vis_tag[i] = c->t + 1u;
+            c->vis_n[i] = 0;
+        }
+        keys[k] = i | ((int64_t)c->vis_n[i]++ << 32);
+    }
+    const int r = run_chunks(c, keys, n, 1);
+    free(keys);
+    return r;
+}
+
+void np8o_request_stats(np8o_ctx *c, int64_t out[2]) {
+    out[0] = c->n_new;
+    out[1] = c->n_deferred;
 }
 
 int np8o_get_state(np8o_ctx *c, int32_t which, int32_t *z, int32_t *K, double *mu, double *Sigma,

@@ -35,7 +35,12 @@ extern "C" {
 
 #define NP8O_DMAX 64
 #define NP8O_MMAX 8
-#define NP8O_REQMAX 4096 /* new-cluster requests one finalize accepts (must match) */
+#define NP8O_REQMAX 4096 /* upper bound of req_max (must match NP8_REQ_MAX) */
+#define NP8O_REQ_DEFAULT 1024 /* default req_max (must match NP8_REQ_DEFAULT) */
+/* Item keys: the Philox item counter of a draw is key = item | (visit << 32), visit = how many times
+ * the item was already updated in this epoch (0 in every sweep; repeated np8o_update_points calls on
+ * the same item within one epoch get fresh draws). */
+#define NP8O_ITEM(key) ((int64_t)((uint64_t)(key) & 0xFFFFFFFFull))
 
 /* Philox stream ids (high byte of counter word 3). */
 enum {
@@ -107,6 +112,7 @@ typedef struct {
     int32_t mh_steps;     /* MH steps per cluster and sweep (np_mcmc.cpp:54: 20); 0 -> 20 */
     int32_t prior;        /* NP8O_PRIOR_* */
     int32_t contraction;  /* NP8O_CONTRACT_*: arithmetic of the cluster likelihoods */
+    int32_t req_max;      /* new clusters one step may create (0 -> NP8O_REQ_DEFAULT, <= NP8O_REQMAX) */
 } np8o_config;
 
 /* Cluster-likelihood arithmetic (DESIGN.md "Wide path").
@@ -151,8 +157,12 @@ int np8o_aux_params(np8o_ctx *c, int64_t i, double *mu, double *Sigma);
  * (pos, i, m, old slot); *n_req counts every request, also those past req_cap. */
 int np8o_assign_range(np8o_ctx *c, int64_t p0, int64_t p1, int32_t *delta, int64_t *req_pos,
                       int64_t *req_i, int32_t *req_m, int32_t *req_zold, int32_t req_cap, int32_t *n_req);
-/* Apply summed deltas and the concatenated (pos-sorted) request list; rebuild the candidate table.
- * owner_lo/owner_hi: only points in [owner_lo, owner_hi) get z written (all if owner_hi<0). */
+/* Apply summed deltas and the concatenated request list (any order); rebuild the candidate table.
+ * Requests are accepted in ascending scan position, at most A = min(req_max, free slots, n_req) of
+ * them, where the free slots are counted after the deltas and before any requester leaves its slot;
+ * the other requesters keep their cluster (deferred to their next update).  req_i holds item keys
+ * (NP8O_ITEM).  owner_lo/owner_hi: only points in [owner_lo, owner_hi) get z written (all if
+ * owner_hi<0).  Returns the number of requests not accepted. */
 int np8o_finalize(np8o_ctx *c, const int32_t *delta, const int64_t *req_pos, const int64_t *req_i,
                   const int32_t *req_m, const int32_t *req_zold, int32_t n_req, int64_t owner_lo, int64_t owner_hi);
 /* Advance the epoch (end of sweep): cluster-parameter update (np_mcmc.cpp:170) when configured,
@@ -165,6 +175,8 @@ int np8o_suffstats(np8o_ctx *c, double *out);
  * returns the number of accepted proposals. */
 int64_t np8o_param_update(np8o_ctx *c, const double *stats);
 int32_t *np8o_z_ptr(np8o_ctx *c);
+/* Cumulative new-cluster requests: out[0] accepted, out[1] deferred (not accepted in their step). */
+void np8o_request_stats(np8o_ctx *c, int64_t out[2]);
 
 /* ---- NIW prior primitives (for distribution tests) ------------------------------------------- */
 /* Marsaglia-Tsang Gamma(alpha, 1), alpha >= 1, from Philox calls call0, call0+1, .. of (i, t, stream). */

@@ -35,6 +35,7 @@ class _Config(C.Structure):
         ("mh_steps", C.c_int32),
         ("prior", C.c_int32),
         ("contraction", C.c_int32),
+        ("req_max", C.c_int32),
     ]
 
 
@@ -118,6 +119,7 @@ def lib():
         L.np8o_lgamma_int.restype = d
         L.np8o_canon_sum.argtypes = [vp, i64]
         L.np8o_canon_sum.restype = d
+        L.np8o_request_stats.argtypes = [vp, vp]
         _lib = L
     return _lib
 
@@ -204,8 +206,10 @@ class Chain:
     """The oracle chain (np8o_ctx).  Same constructor parameters as noparama_amd.NealAlgorithm8."""
 
     def __init__(self, D, M=3, alpha=1.0, mu0=None, kappa=1.0 / 500, nu=4.0, Lambda=None, seed=0,
-                 kcap=4096, chunk=0, param_update="frozen", mh_steps=20, prior="reference", contraction="f64"):
+                 kcap=4096, chunk=0, param_update="frozen", mh_steps=20, prior="reference", contraction="f64",
+                 req_max=0):
         cfg = _Config()
+        cfg.req_max = req_max
         cfg.contraction = CONTRACTION[contraction]
         cfg.param_update = PARAM_UPDATE[param_update]
         cfg.prior = PRIOR[prior]
@@ -303,6 +307,13 @@ class Chain:
         return lib().np8o_num_clusters(self._h)
 
     @property
+    def request_stats(self):
+        """[accepted new-cluster requests, requests deferred (not accepted)], cumulative."""
+        out = np.zeros(2, dtype=np.int64)
+        lib().np8o_request_stats(self._h, _p(out))
+        return out
+
+    @property
     def mh_accepted(self):
         return lib().np8o_mh_accepted(self._h)
 
@@ -388,7 +399,4 @@ class Chain:
         rm = np.ascontiguousarray(rm, dtype=np.int32)
         rz = np.ascontiguousarray(rz, dtype=np.int32)
         n = rp.size if n_req is None else n_req
-        r = lib().np8o_finalize(self._h, _p(delta), _p(rp), _p(ri), _p(rm), _p(rz), n, owner_lo, owner_hi)
-        if r not in (0, -4):
-            raise ValueError(f"oracle finalize: {r}")
-        return r  # -4: the step's new-cluster requests were rejected (capacity), state consistent
+        return lib().np8o_finalize(self._h, _p(delta), _p(rp), _p(ri), _p(rm), _p(rz), n, owner_lo, owner_hi)

@@ -169,32 +169,81 @@ def test_errors_are_reported():
         NealAlgorithm8(5, seed=0, device=0)  # no kernel instantiated for D = 5
 
 
-def test_capacity_rejection_matches_oracle():
-    """More new-cluster requests than free slots: the whole step's requests are rejected (a huge
-    alpha makes most items ask for a new cluster)."""
+def test_partial_accept_at_kcap_matches_oracle():
+    """More new-cluster requests than free slots (a huge alpha makes most items ask for a new
+    cluster): the requests of lowest scan position fill the free slots, the rest are deferred."""
     X, _ = datasets.twogaussians(5)
     g, o = pair(2, 17, kcap=24, alpha=1e6)
     for s in (g, o):
         s.set_data(X)
         s.init_random(20)
-    with pytest.raises(NP8Error) as e:
-        g.sweep(2)
-    assert e.value.code == -4
-    assert o.sweep(2) == -4
+    g.sweep(2)
+    assert o.sweep(2) == 0
+    assert_same_state(g, o)
+    st = g.stats()
+    assert st["rejected_requests"] > 0
+    assert [st["new_clusters"], st["rejected_requests"]] == list(o.request_stats)
+
+
+@pytest.mark.parametrize("D,N,req_max", [(2, 100_000, 0), (8, 100_000, 0), (8, 100_000, 300)])
+def test_cold_start_from_init_random_bit_exact(D, N, req_max):
+    """the reference's initialisation (np_mcmc.cpp:49-92, K=20 random G0 clusters) at
+    N = 1e5 sends thousands of new-cluster requests in the first sweep; round 1 rejected them all
+    (K stuck at 20).  Now: partial acceptance in scan order, bit-exact against the oracle."""
+    X = (datasets.config_c2(N=N) if D == 2 else datasets.config_c3(N=N))[0]
+    O.set_threads(8)
+    g, o = pair(D, 23, req_max=req_max)
+    for s in (g, o):
+        s.set_data(X)
+        s.init_random(20)
+    for t in range(3):
+        g.sweep(1)
+        assert o.sweep(1) == 0
+        sg, so = g.state(params=False), o.state()
+        assert sg["K"] == so["K"], (t, sg["K"], so["K"])
+        assert np.array_equal(sg["z"], so["z"]), t
+        assert np.array_equal(sg["counts"], so["counts"])
+    st = g.stats()
+    assert [st["new_clusters"], st["rejected_requests"]] == list(o.request_stats)
+    assert st["rejected_requests"] > 0 and g.K > 20
     assert_same_state(g, o)
 
 
-def test_host_exchange_two_ranks_equals_one():
+def test_update_points_repeated_visits_bit_exact():
+    """repeated np8_update_points without np8_end_sweep draws afresh at every visit (item key
+    index | visit << 32), identically on the device and in the oracle, and does not cycle."""
+    X, _ = datasets.twogaussians()
+    g, o = pair(2, 29, kcap=256)
+    for s in (g, o):
+        s.set_data(X)
+        s.init_random(20)
+    ids = np.arange(X.shape[0], dtype=np.int64)
+    seen = set()
+    for k in range(6):
+        sub = ids if k % 2 == 0 else ids[::-3]
+        g.update_points(sub)
+        o.update_points(sub)
+        assert_same_state(g, o)
+        seen.add(g.state()["z"].tobytes())
+    assert len(seen) == 6
+
+
+@pytest.mark.parametrize("req_max", [0, 40])
+def test_host_exchange_two_ranks_equals_one(req_max):
     """The multi-GPU protocol (exchange record, rank-ordered requests) with two contexts on one GPU
-    and a host all-gather: identical to the single-rank sweep."""
+    and a host all-gather: identical to the single-rank sweep.  req_max = 40: most requests of the
+    first sweeps are deferred, and each rank's record carries only its 40 lowest-position requests
+    (np8_req_select)."""
     X, _, mu, sig = datasets.mixture(5000, 8, 12, 0.8, 6.0, seed=9)
     z = np.random.default_rng(2).integers(0, 12, size=5000).astype(np.int32)
-    one = NealAlgorithm8(8, seed=77, device=0)
+    one = NealAlgorithm8(8, seed=77, device=0, req_max=req_max)
     one.set_data(X)
     one.init_random(12)
     one.sweep(3)
+    if req_max:
+        assert one.stats()["rejected_requests"] > 0
     half = 2600
-    ranks = [NealAlgorithm8(8, seed=77, device=0) for _ in range(2)]
+    ranks = [NealAlgorithm8(8, seed=77, device=0, req_max=req_max) for _ in range(2)]
     for r, c in enumerate(ranks):
         c.comm_init(None, r, 2)
         lo, hi = (0, half) if r == 0 else (half, 5000)

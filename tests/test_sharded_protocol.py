@@ -17,6 +17,7 @@ import torch.multiprocessing as mp
 from noparama_amd import datasets
 
 N, D, SWEEPS, SEED, KCAP = 3000, 3, 5, 31, 2048
+REQ_MAX = 64  # small: the first sweeps from init_random defer most requests (partial acceptance)
 
 
 def _free_port():
@@ -33,7 +34,7 @@ def _rank(rank, world, port, X, outdir):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     lo, hi = (N * rank) // world, (N * (rank + 1)) // world
-    c = O.Chain(D, seed=SEED, kcap=KCAP)
+    c = O.Chain(D, seed=SEED, kcap=KCAP, req_max=REQ_MAX)
     c.set_data(X)  # replica of the data: only [lo, hi) is evaluated or owned
     c.init_random(20)
     codes = []
@@ -48,7 +49,7 @@ def _rank(rank, world, port, X, outdir):
         c.end_sweep()
     z = c.state()["z"]
     np.save(os.path.join(outdir, f"z{rank}.npy"), z[lo:hi])
-    np.save(os.path.join(outdir, f"k{rank}.npy"), np.array([c.K] + codes))
+    np.save(os.path.join(outdir, f"k{rank}.npy"), np.array([c.K] + codes + list(c.request_stats)))
     dist.destroy_process_group()
 
 
@@ -56,14 +57,20 @@ def test_two_rank_gloo_sweeps_equal_single_process(tmp_path):
     import oracle as O
 
     X, _, _, _ = datasets.mixture(N, D, 8, 0.6, 4.0, seed=3)
-    one = O.Chain(D, seed=SEED, kcap=KCAP)
+    one = O.Chain(D, seed=SEED, kcap=KCAP, req_max=REQ_MAX)
     one.set_data(X)
     one.init_random(20)
-    codes = [one.sweep(1) for _ in range(SWEEPS)]
+    deferred = []
+    for _ in range(SWEEPS):
+        before = one.request_stats[1]
+        assert one.sweep(1) == 0
+        deferred.append(int(one.request_stats[1] - before))
+    assert deferred[0] > 0  # the protocol's partial acceptance is exercised
     ref = one.state()
     mp.spawn(_rank, args=(2, _free_port(), X, str(tmp_path)), nprocs=2, join=True)
     z = np.concatenate([np.load(tmp_path / f"z{r}.npy") for r in range(2)])
     assert np.array_equal(z, ref["z"])
     for r in range(2):
         k = np.load(tmp_path / f"k{r}.npy")
-        assert int(k[0]) == ref["K"] and list(k[1:]) == codes
+        assert int(k[0]) == ref["K"] and list(k[1:1 + SWEEPS]) == deferred
+        assert list(k[1 + SWEEPS:]) == list(one.request_stats)

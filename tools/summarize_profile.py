@@ -9,6 +9,7 @@ import csv
 import json
 import os
 import shutil
+import subprocess
 import sys
 from collections import defaultdict
 
@@ -38,8 +39,22 @@ if assign:
     if fetch is not None:
         out["assign_bytes_per_launch"] = (2.0 * fetch + write) * 1024.0
     if "SQ_INSTS_VALU" in a and "SQ_WAVES" in a:
-        out["assign_valu_insts_per_item"] = a["SQ_INSTS_VALU"]["mean"] / a["SQ_WAVES"]["mean"]
+        # SQ_INSTS_VALU counts wave-instructions: per wave, and per item (64 items per wave)
+        out["assign_valu_insts_per_wave"] = a["SQ_INSTS_VALU"]["mean"] / a["SQ_WAVES"]["mean"]
+        out["assign_valu_insts_per_item"] = out["assign_valu_insts_per_wave"] / 64.0
+    if "SQ_ACTIVE_INST_VALU" in a and "GRBM_GUI_ACTIVE" in a:
+        # VALU issue utilisation (MI355X_MICROARCH.md counter units): SQ_ACTIVE_INST_VALU is summed over
+        # waves in quad-cycles; GRBM_GUI_ACTIVE is summed over the 8 XCDs; 1024 SIMDs
+        cyc = a["GRBM_GUI_ACTIVE"]["mean"] / 8.0
+        out["assign_valu_issue_frac"] = 4.0 * a["SQ_ACTIVE_INST_VALU"]["mean"] / (1024.0 * cyc)
+try:
+    commit = subprocess.run(["git", "-C", ROOT, "rev-parse", "--short", "HEAD"], capture_output=True,
+                            text=True).stdout.strip()
+except Exception:
+    commit = None
+out["commit"] = f"profiled at {commit}" if commit else None
 json.dump(out, open(os.path.join(dst, f"{tag}_counters.json"), "w"), indent=1)
-json.dump({"assign_bytes_per_launch": out.get("assign_bytes_per_launch"), "source": f"profiles/{tag}_counters.json"},
+json.dump({"assign_bytes_per_launch": out.get("assign_bytes_per_launch"), "source": f"profiles/{tag}_counters.json",
+           "commit": out["commit"]},
           open(os.path.join(dst, f"traffic_{tag}.json"), "w"), indent=1)
 print(json.dumps({k: v for k, v in out.items() if k != "counters"}, indent=1))
