@@ -182,6 +182,14 @@ def main():
         dt = float(tt.item())
     st1 = smp.stats()
     Kfinal = st1["K"]
+    # executed-work counters over separate (untimed) sweeps: they add scalar loads and atomics per wave
+    cnt_sweeps = 20 if (transport != "gloo" and not wide) else 0
+    if cnt_sweeps:
+        smp.set_timing(True, counters=True)
+        sc0 = smp.stats()
+        sweeps(cnt_sweeps)
+        sc1 = smp.stats()
+        smp.set_timing(True)
 
     # roofline of the dominant kernel (np8_assign): algorithmic flops per launch / avg launch time
     # every launch is timed when sweeps go one by one; one per 20-sweep graph replay otherwise
@@ -201,9 +209,9 @@ def main():
     xbytes = 4 * D if wide else 8 * D
     # executed work: quadratic forms the kernel evaluated (device counters), at their real cost
     # (isotropic rows: D subtractions + D multiply-adds + scale, weight = 3D + 3 flops)
-    nq = st1["n_quad"] - st0["n_quad"]
-    nq_iso = st1["n_quad_iso"] - st0["n_quad_iso"]
-    exec_flops = ((nq - nq_iso) * (D * D + 2 * D + 4) + nq_iso * (3 * D + 3)) / max(n_launch, 1) if not wide else None
+    nq = (sc1["n_quad"] - sc0["n_quad"]) / cnt_sweeps if cnt_sweeps else 0.0  # per sweep (= per launch)
+    nq_iso = (sc1["n_quad_iso"] - sc0["n_quad_iso"]) / cnt_sweeps if cnt_sweeps else 0.0
+    exec_flops = ((nq - nq_iso) * (D * D + 2 * D + 4) + nq_iso * (3 * D + 3)) if cnt_sweeps else None
     traffic = traffic_src = None
     if os.path.exists(args.traffic_json):
         try:
@@ -258,11 +266,12 @@ def main():
                 "assign_launches_timed": n_launch,
                 "algorithmic_flops_per_launch": flops,
                 "traffic_source": traffic_src,
-                "executed": None if wide else {
+                "executed": None if not cnt_sweeps else {
                     "note": "what np8_assign executed: quadratic forms after exact candidate pruning "
-                            "(device counters), at their real cost; the M auxiliary G0 draws per item "
-                            "(Philox, Box-Muller, chi^2 logs) are not flops of this count",
-                    "quad_forms_per_item": nq / max(n_launch, 1) / max(n_items, 1),
+                            "(device counters over 20 untimed sweeps after the timed ones), at their real "
+                            "cost, over the timed launch time; the M auxiliary G0 draws per item (Philox, "
+                            "Box-Muller, chi^2 logs) are not flops of this count",
+                    "quad_forms_per_item": nq / max(n_items, 1),
                     "iso_fraction": nq_iso / max(nq, 1),
                     "tflops": exec_flops / (ms_assign * 1e-3) / 1e12 if ms_assign > 0 else None,
                     "frac_of_peak": exec_flops / (ms_assign * 1e-3) / 1e12 / peak if ms_assign > 0 else None,

@@ -113,7 +113,7 @@ typedef struct {
      * likelihoods) and of the attempt batches, and the launches behind them */
     double ms_sm_members, ms_sm_eval;
     int64_t n_timed_sm_members, n_timed_sm_eval;
-    /* executed work of the assign kernel while timing is enabled (cumulative): cluster quadratic forms
+    /* executed work of the assign kernel while NP8_TIMING_COUNTERS is on (cumulative): cluster quadratic forms
      * evaluated per item (its own cluster included; rows left out by candidate pruning are not), and
      * how many of them took the isotropic form iso |x - mu|^2 */
     int64_t n_quad, n_quad_iso;
@@ -202,7 +202,12 @@ int np8_loglik_matrix(np8_ctx *ctx, const int64_t *idx, int64_t n, double *out);
 int np8_total_loglik(np8_ctx *ctx, double *out);
 
 int np8_stats(np8_ctx *ctx, np8_stats_t *out);
-/* Device-event timing of the kernels (adds events around each launch). */
+/* enable = NP8_TIMING_EVENTS: device-event timing of the kernels (event pairs around each launch, or
+ * around one assign launch per replayed sweep graph); NP8_TIMING_COUNTERS: the assign kernel counts the
+ * quadratic forms it executes (np8_stats_t.n_quad; a few scalar loads and two atomics per wave); 0 = off.
+ * Any non-zero value without the counter bit is the events alone. */
+#define NP8_TIMING_EVENTS 1
+#define NP8_TIMING_COUNTERS 2
 int np8_set_timing(np8_ctx *ctx, int32_t enable);
 /* Launch on this stream instead of the context's own (hipStream_t as void*). */
 int np8_set_stream(np8_ctx *ctx, void *stream);

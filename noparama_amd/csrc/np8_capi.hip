@@ -111,14 +111,15 @@ struct np8_ctx {
     int capture_timed_left = 0;
     int graph_par = -1;          // max-likelihood check parity the graph was captured at
     int graph_phase = -1;        // epoch mod kGraphSweeps the graph was captured at
-    bool graph_mh = false, graph_timing = false;
+    bool graph_mh = false;
+    int graph_timing = 0;
     bool capturing = false, graphs_off = false;
     std::vector<Timer> graph_timers;
     // multi-GPU
     ncclComm_t comm = nullptr;
     int rank = 0, world = 1;
-    // timing
-    bool timing = false;
+    // timing: event pairs around launches; count_eval: the assign kernels' executed-work counters
+    bool timing = false, count_eval = false;
     std::vector<Timer> timers;
     std::vector<hipEvent_t> event_pool;
     double ms[6] = {0, 0, 0, 0, 0, 0};  // assign, finalize, loglik, params, sm members, sm eval
@@ -680,7 +681,7 @@ AssignArgs assign_args(np8_ctx *c, int64_t p0, int64_t p1, const int64_t *order,
     A.ls = c->kcap;
     A.use_lists = 0;
     A.collect_r2 = 0;
-    A.count_eval = c->timing ? 1 : 0;
+    A.count_eval = c->count_eval ? 1 : 0;
     A.evalc = c->evalc;
     A.r2 = c->r2;
     A.wfrag = c->wfrag;
@@ -1025,7 +1026,7 @@ int capture_graph(np8_ctx *c) {
         g = nullptr;
         c->graph_par = ch0 & 1;
         c->graph_phase = (int)(e0 % kGraphSweeps);
-        c->graph_timing = c->timing;
+        c->graph_timing = (c->timing ? 1 : 0) | (c->count_eval ? 2 : 0);
     } else {
         c->graph_timers.clear();
         c->graphs_off = true;
@@ -1039,7 +1040,7 @@ int capture_graph(np8_ctx *c) {
 // phase, check parity or timing setting).
 int ensure_graph(np8_ctx *c) {
     if (!c->graph || c->graph_par != (c->checks & 1) || c->graph_phase != (int)(c->epoch % kGraphSweeps) ||
-        c->graph_timing != c->timing)
+        c->graph_timing != ((c->timing ? 1 : 0) | (c->count_eval ? 2 : 0)))
         return capture_graph(c);
     return NP8_OK;
 }
@@ -1614,7 +1615,8 @@ int np8_stats(np8_ctx *c, np8_stats_t *out) {
 
 int np8_set_timing(np8_ctx *c, int32_t enable) {
     if (!c) return NP8_ERR_ARG;
-    c->timing = enable != 0;
+    c->timing = (enable & NP8_TIMING_EVENTS) != 0;
+    c->count_eval = (enable & NP8_TIMING_COUNTERS) != 0;
     return NP8_OK;
 }
 

@@ -326,8 +326,9 @@ class NealAlgorithm8:
         self._check(lib().np8_total_loglik(self._h, C.byref(v)))
         return v.value
 
-    def set_timing(self, on=True):
-        self._check(lib().np8_set_timing(self._h, 1 if on else 0))
+    def set_timing(self, on=True, counters=False):
+        """on: device-event timing; counters: the assign kernel's executed-work counters (n_quad)."""
+        self._check(lib().np8_set_timing(self._h, (1 if on else 0) | (2 if counters else 0)))
 
     # -- multi-rank ----------------------------------------------------------------------------
     def comm_init(self, uid, rank, world):

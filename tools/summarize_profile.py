@@ -39,9 +39,9 @@ if assign:
     if fetch is not None:
         out["assign_bytes_per_launch"] = (2.0 * fetch + write) * 1024.0
     if "SQ_INSTS_VALU" in a and "SQ_WAVES" in a:
-        # SQ_INSTS_VALU counts wave-instructions: per wave, and per item (64 items per wave)
+        # SQ_INSTS_VALU counts wave-instructions; one item per lane, so this is also the VALU instruction
+        # count of one item's lane
         out["assign_valu_insts_per_wave"] = a["SQ_INSTS_VALU"]["mean"] / a["SQ_WAVES"]["mean"]
-        out["assign_valu_insts_per_item"] = out["assign_valu_insts_per_wave"] / 64.0
     if "SQ_ACTIVE_INST_VALU" in a and "GRBM_GUI_ACTIVE" in a:
         # VALU issue utilisation (MI355X_MICROARCH.md counter units): SQ_ACTIVE_INST_VALU is summed over
         # waves in quad-cycles; GRBM_GUI_ACTIVE is summed over the 8 XCDs; 1024 SIMDs
