@@ -117,6 +117,9 @@ typedef struct {
      * evaluated per item (its own cluster included; rows left out by candidate pruning are not), and
      * how many of them took the isotropic form iso |x - mu|^2 */
     int64_t n_quad, n_quad_iso;
+    /* NP8_TIMING_COUNTERS self-check of the auxiliary screen (DESIGN.md "Auxiliary screen"): lanes whose
+     * screened-out auxiliary would not have been skipped by the pick.  0 unless the screen's margin is wrong. */
+    int64_t screen_violations;
 } np8_stats_t;
 
 /* Create / destroy.  Replaces NealAlgorithm8::NealAlgorithm8 (np_neal_algorithm8.cpp:17-34). */

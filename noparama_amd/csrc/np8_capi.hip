@@ -1602,6 +1602,7 @@ int np8_stats(np8_ctx *c, np8_stats_t *out) {
     out->n_timed_sm_members = c->n_timed[4];
     out->n_timed_sm_eval = c->n_timed[5];
     out->mh_accepted = h.mh_accepted;
+    out->screen_violations = (int64_t)h.n_screen_viol;
     {
         std::vector<unsigned long long> ev((size_t)2 * kEvalSlots);
         HIPC(c, hipMemcpy(ev.data(), c->evalc, sizeof(unsigned long long) * ev.size(), hipMemcpyDeviceToHost));

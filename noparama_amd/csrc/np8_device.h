@@ -195,34 +195,72 @@ NP8_HD int g0_calls(int D) { return (D + 4) / 4; }
 // Auxiliary m of item i is theta = (v, mu0 + (|v|/sqrt kappa) L^T xi), xi ~ N(0, I_D).  With the item
 // whitened, y0 = (L^T)^{-1}(x - mu0), the likelihood depends on xi only through xi_par = xi . y0/|y0|
 // ~ N(0,1) and chi2 = |xi_perp|^2 ~ chi^2_{D-1}:  |y0 - s xi|^2 = (|y0| - s xi_par)^2 + s^2 chi2.  So
-// the draw is (v, xi_par, chi2): call m*aux_calls(D) gives normals (v-normal, xi_par, g_odd, -);
-// chi^2_{2k}, k = (D-1)/2, is -2 log of the product of k 32-bit uniforms (calls m*aux_calls(D)+1 ..,
-// products of at most 16 per log), plus g_odd^2 when D-1 is odd.  Only a picked auxiliary needs xi
-// itself: xi = xi_par yhat + sqrt(chi2) w_perp/|w_perp| with w ~ N(0, I_D) on stream AUX_DIR
-// (exactly N(0, I) in distribution: independent radial, parallel and direction parts).
-NP8_HD int aux_calls(int D) { return 1 + ((D - 1) / 2 + 3) / 4; }
+// the draw is (v, xi_par, chi2), from calls m*Qa .. m*Qa + Qa - 1 of stream AUX:
+//   call 0: Box-Muller pair of words (0, 1) -> (v-normal, xi_par) = (r cos, r sin); words 2, 3 -> the
+//           first two of the k = (D-1)/2 uniforms whose product gives chi^2_{2k} = -2 log(prod)
+//   call 1 (when D-1 is odd or k > 2): words (0, 1) -> g_odd = r cos (chi^2 gets g_odd^2 for odd D-1);
+//           words 2, 3 -> uniforms 2, 3
+//   call 2 + c: uniforms 4 + 4c .. 7 + 4c
+// (logs over products of at most 16 uniforms).  Everything an upper bound of the log-likelihood needs --
+// v, xi_par and a lower bound of chi2 -- comes from call 0 (aux_screen_skips in np8_kernels.hip).
+// Only a picked auxiliary needs xi itself: xi = xi_par yhat + sqrt(chi2) w_perp/|w_perp| with
+// w ~ N(0, I_D) on stream AUX_DIR (exactly N(0, I) in distribution: independent radial, parallel and
+// direction parts).
+NP8_HD int aux_calls(int D) {
+    const int k = (D - 1) / 2;
+    return 1 + ((((D - 1) & 1) || k > 2) ? 1 : 0) + (k > 4 ? (k - 1) / 4 : 0);
+}
 NP8_HD int dir_calls(int D) { return (D + 3) / 4; }
 
+// w0: the words of call m*Qa when the caller has them already (else null).
 NP8_HD void aux_core(uint64_t seed, uint64_t i, uint32_t t, int m, int D, double nu, double &v, double &xpar,
-                     double &chi2) {
+                     double &chi2, const uint32_t *w0 = nullptr) {
     const int Qa = aux_calls(D), k = (D - 1) / 2;
-    double g[4];
-    normal_quad(seed, i, t, kStreamAux, (uint32_t)(m * Qa), g);
-    v = fma(nu, g[0], (double)D);
-    xpar = g[1];
+    const bool odd = ((D - 1) & 1) != 0;
+    const uint32_t base = (uint32_t)(m * Qa);
+    uint32_t w[4], w1[4] = {0u, 0u, 0u, 0u}, wc[4] = {0u, 0u, 0u, 0u};
+    if (w0) {
+        for (int h = 0; h < 4; ++h) w[h] = w0[h];
+    } else {
+        philox_call(seed, i, t, kStreamAux, base, w);
+    }
+    {
+        const double r = sqrt(-2.0 * log_pos(u32_01(w[0])));
+        double sn, cs;
+        sincos_2pi(u32_01(w[1]), sn, cs);
+        v = fma(nu, r * cs, (double)D);
+        xpar = r * sn;
+    }
+    double godd = 0.0;
+    if (odd || k > 2) {
+        philox_call(seed, i, t, kStreamAux, base + 1u, w1);
+        if (odd) {
+            const double r = sqrt(-2.0 * log_pos(u32_01(w1[0])));
+            double sn, cs;
+            sincos_2pi(u32_01(w1[1]), sn, cs);
+            godd = r * cs;
+        }
+    }
     double c2 = 0.0, prod = 1.0;
-    uint32_t w[4] = {0u, 0u, 0u, 0u};
     int in_chunk = 0;
     for (int j = 0; j < k; ++j) {
-        if ((j & 3) == 0) philox_call(seed, i, t, kStreamAux, (uint32_t)(m * Qa + 1 + (j >> 2)), w);
-        prod *= u32_01(w[j & 3]);
+        uint32_t word;
+        if (j < 2) {
+            word = w[2 + j];
+        } else if (j < 4) {
+            word = w1[j];
+        } else {
+            if (((j - 4) & 3) == 0) philox_call(seed, i, t, kStreamAux, base + 2u + (uint32_t)((j - 4) >> 2), wc);
+            word = wc[(j - 4) & 3];
+        }
+        prod *= u32_01(word);
         if (++in_chunk == 16 || j == k - 1) {
             c2 = fma(-2.0, log_pos(prod), c2);
             prod = 1.0;
             in_chunk = 0;
         }
     }
-    if ((D - 1) & 1) c2 = fma(g[2], g[2], c2);
+    if (odd) c2 = fma(godd, godd, c2);
     chi2 = c2;
 }
 

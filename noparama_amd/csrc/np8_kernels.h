@@ -31,6 +31,8 @@ struct Ctl {
     int32_t n_pend;       // NIW prior: accepted requests waiting for np8_niw_aux_slots (set by np8_finalize)
     int32_t cand_fresh;   // the candidate rows' mu/P' match the slot tables (0 after a state upload:
                           // np8_finalize then copies them; parameter updates patch rows in place)
+    unsigned long long n_screen_viol;  // count_eval runs: lanes with a screened auxiliary that pick_step would
+                                       // not have skipped (the auxiliary screen's self-check; must stay 0)
 };
 
 // Executed work of np8_assign when AssignArgs::count_eval is set (timing mode): per wave, the cluster

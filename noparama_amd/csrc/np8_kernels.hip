@@ -103,6 +103,46 @@ __device__ __forceinline__ double niw_aux_ll(const double *__restrict__ hyp, dou
     return niw_aux_loglik(nd, sumlog, b00, chi, z1, hyp[H::kRsk], hyp[H::kCaux]);
 }
 
+// Screen of auxiliary m from the words w of its first Philox call (DESIGN.md "Auxiliary screen"): true
+// when its exact log-likelihood (aux_core + aux_loglik, fp64) is certainly <= thr, so that pick_step
+// would skip it.  From call 0 alone: v and xi_par exactly, chi2 >= -2 log(u_0 u_1) (the remaining
+// uniforms are <= 1 and g_odd^2 >= 0), hence
+//   ll = caux - D log|v| - q/2,  q = (ny/|v| - rsk xi_par)^2 + rsk^2 chi2  >=  the same with chi2's bound.
+// Evaluated in fp32 on the transcendental units (v_log_f32, v_sqrt_f32, v_cos_f32/v_sin_f32 in
+// revolutions, v_rcp_f32), with an error margin that covers those approximations with a factor of ten:
+// |error of r cos, r sin| <= 4e-3 (3.5e-4 from rounding u0 to fp32 near 1), relative 1e-4 elsewhere.
+// No screen near v = 0 (|v| < 1/4), where log|v| and ny/|v| are ill-conditioned.
+template <int D>
+__device__ __forceinline__ bool aux_screen_skips(const uint32_t (&w)[4], float ny, float nu, float rsk, float caux,
+                                                 float thr) {
+    constexpr float kLn2 = 0.693147180559945f;
+    constexpr int k = (D - 1) / 2;
+    const float u0 = fmaf((float)w[0], 0x1.0p-32f, 0x1.0p-33f);
+    const float u1 = fmaf((float)w[1], 0x1.0p-32f, 0x1.0p-33f);
+    const float r = __builtin_amdgcn_sqrtf(-2.0f * kLn2 * __builtin_amdgcn_logf(u0));
+    const float g0 = r * __builtin_amdgcn_cosf(u1);
+    const float xp = r * __builtin_amdgcn_sinf(u1);
+    const float v = fmaf(nu, g0, (float)D);
+    const float av = fabsf(v);
+    float chi = 0.0f;
+    if constexpr (k >= 2) {
+        const float ua = fmaf((float)w[2], 0x1.0p-32f, 0x1.0p-33f), ub = fmaf((float)w[3], 0x1.0p-32f, 0x1.0p-33f);
+        chi = -2.0f * kLn2 * __builtin_amdgcn_logf(ua * ub);
+    } else if constexpr (k == 1) {
+        chi = -2.0f * kLn2 * __builtin_amdgcn_logf(fmaf((float)w[2], 0x1.0p-32f, 0x1.0p-33f));
+    }
+    const float iv = __builtin_amdgcn_rcpf(av);
+    const float lnv = kLn2 * __builtin_amdgcn_logf(av);
+    const float nyv = ny * iv;
+    const float a = nyv - rsk * xp;
+    const float qlb = fmaf(a, a, rsk * rsk * chi);
+    const float ub_ll = fmaf(-0.5f, qlb, caux - (float)D * lnv);
+    const float ea = 4e-3f * fmaf(nyv * nu, iv, rsk);
+    const float err = 1.0f + (float)D * 4e-3f * nu * iv + fabsf(a) * ea + ea * ea +
+                      1e-4f * (qlb + fabsf(caux) + (float)D * fabsf(lnv) + fabsf(thr));
+    return av >= 0.25f && ub_ll + err <= thr;
+}
+
 template <int D, int PRIOR>
 __device__ __forceinline__ double prior_aux_ll(const double *__restrict__ hyp, double ny, uint64_t seed, uint64_t ig,
                                                uint32_t t, int m) {
@@ -148,7 +188,9 @@ __device__ __forceinline__ int64_t position_to_local(const AssignArgs &A, int64_
     return p;
 }
 
-template <int D, int M, int PRIOR>
+// COUNT: the executed-work counters and the auxiliary screen's self-check (NP8_TIMING_COUNTERS), compiled
+// into a separate instance so that the timed kernel carries none of their registers.
+template <int D, int M, int PRIOR, bool COUNT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void np8_assign(AssignArgs A) {
     constexpr int DP = D * (D + 1) / 2;
     constexpr int CS = (D + DP + 5 + 1) & ~1;
@@ -207,7 +249,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void n
             if (e[F + kFieldSlot] != zslot) pick_step(st, lw, j);
         }
     }
-    if (A.count_eval) {  // timing mode: the quadratic forms this wave executed (own row + walked rows)
+    if constexpr (COUNT) {  // the quadratic forms this wave executed (own row + walked rows)
         const int nrow = walk_list ? A.plen[j0] : K;
         int64_t nq = 0, niso = 0;
         for (int q = 0; q < nrow; ++q) {
@@ -230,8 +272,38 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void n
     const double ny = norm_of<D>(y0);
     {
         const double logam = hyp[HypView<D>::kLogam];
+        if constexpr (PRIOR == kPriorNiw) {
 #pragma unroll 1
-        for (int m = 0; m < M; ++m) pick_step(st, prior_aux_ll<D, PRIOR>(hyp, ny, A.seed, ig, t, m) + logam, K + m);
+            for (int m = 0; m < M; ++m) pick_step(st, prior_aux_ll<D, PRIOR>(hyp, ny, A.seed, ig, t, m) + logam, K + m);
+        } else {
+            // the first Philox call of every auxiliary bounds its log-likelihood (aux_screen_skips);
+            // only lanes whose auxiliary may come within kSkip of the running maximum finish the draw
+            using H = HypView<D>;
+            const double nu = hyp[H::kNu], rsk = hyp[H::kRsk], caux = hyp[H::kCaux];
+            const float thr = (float)(st.T - kSkip - logam);  // T only grows: conservative for every m
+            const int Qa = aux_calls(D);
+            int64_t n_viol = 0;
+#pragma unroll 1
+            for (int m = 0; m < M; ++m) {
+                uint32_t w[4];
+                philox_call(A.seed, ig, t, kStreamAux, (uint32_t)(m * Qa), w);
+                const bool skip = aux_screen_skips<D>(w, (float)ny, (float)nu, (float)rsk, (float)caux, thr);
+                if (!skip || COUNT) {
+                    double v, xpar, chi2;
+                    aux_core(A.seed, ig, t, m, D, nu, v, xpar, chi2, w);
+                    const double lw = aux_loglik(ny, v, xpar, chi2, D, rsk, caux) + logam;
+                    if (!skip)
+                        pick_step(st, lw, K + m);
+                    else if (lw - st.T > -kSkip)
+                        ++n_viol;  // debug count: a screened auxiliary pick_step would not have skipped
+                }
+            }
+            if constexpr (COUNT) {
+                const int nv = __popcll(__ballot(n_viol > 0));
+                if (nv && (threadIdx.x & 63) == (__ffsll((unsigned long long)__ballot(1)) - 1))
+                    atomicAdd(&A.ctl->n_screen_viol, (unsigned long long)nv);
+            }
+        }
     }
 
     int32_t *delta = reinterpret_cast<int32_t *>(A.rec + kRecHeaderBytes);
@@ -1161,13 +1233,15 @@ hipError_t np8_launch_assign(const AssignArgs &A, int D, int M, int prior, hipSt
     const int64_t n = A.p1 - A.p0;
     if (n <= 0) return hipSuccess;
     const dim3 grid((unsigned)((n + 255) / 256)), block(256);
-#define X(d, m)                                                                           \
-    if (D == d && M == m) {                                                               \
-        if (prior == kPriorNiw)                                                           \
-            hipLaunchKernelGGL((np8_assign<d, m, kPriorNiw>), grid, block, 0, s, A);       \
-        else                                                                              \
-            hipLaunchKernelGGL((np8_assign<d, m, kPriorReference>), grid, block, 0, s, A); \
-        return hipGetLastError();                                                         \
+#define X(d, m)                                                                                        \
+    if (D == d && M == m) {                                                                            \
+        if (prior == kPriorNiw)                                                                        \
+            hipLaunchKernelGGL((np8_assign<d, m, kPriorNiw, false>), grid, block, 0, s, A);             \
+        else if (A.count_eval)                                                                         \
+            hipLaunchKernelGGL((np8_assign<d, m, kPriorReference, true>), grid, block, 0, s, A);        \
+        else                                                                                           \
+            hipLaunchKernelGGL((np8_assign<d, m, kPriorReference, false>), grid, block, 0, s, A);       \
+        return hipGetLastError();                                                                      \
     }
     NP8_FOR_EACH_DM(X)
 #undef X

@@ -97,6 +97,7 @@ class Stats(C.Structure):
         ("n_timed_sm_eval", C.c_int64),
         ("n_quad", C.c_int64),
         ("n_quad_iso", C.c_int64),
+        ("screen_violations", C.c_int64),
     ]
 
 

@@ -694,32 +694,62 @@ static void slot_from_aux(np8o_ctx *c, int s, double v, const double *mu) {
 /* ---- auxiliary draws in the item's frame (DESIGN.md "G0") ----------------------------------------
  * Auxiliary m of item i is theta = (v, mu0 + (|v|/sqrt kappa) L^T xi), xi ~ N(0, I_D).  With
  * y0 = (L^T)^{-1}(x - mu0) the likelihood needs only xi_par = xi . y0/|y0| ~ N(0,1) and
- * chi2 = |xi_perp|^2 ~ chi^2_{D-1}: |y0 - s xi|^2 = (|y0| - s xi_par)^2 + s^2 chi2.  Call m*Qa of
- * stream AUX gives the normals (v-normal, xi_par, g_odd, -); chi^2_{2k}, k = (D-1)/2, is -2 log of the
- * product of k 32-bit uniforms (calls m*Qa+1 .., at most 16 per log), plus g_odd^2 for odd D-1.  A
- * picked auxiliary's xi = xi_par yhat + sqrt(chi2) w_perp/|w_perp|, w ~ N(0,I) on stream AUX_DIR. */
-static inline int aux_calls(int D) { return 1 + ((D - 1) / 2 + 3) / 4; }
+ * chi2 = |xi_perp|^2 ~ chi^2_{D-1}: |y0 - s xi|^2 = (|y0| - s xi_par)^2 + s^2 chi2.  Calls m*Qa .. of
+ * stream AUX: call 0 words (0,1) -> Box-Muller (v-normal, xi_par) = (r cos, r sin), words 2,3 -> the
+ * first two of the k = (D-1)/2 uniforms whose product gives chi^2_{2k} = -2 log(prod); call 1 (odd D-1
+ * or k > 2): words (0,1) -> g_odd = r cos (chi2 += g_odd^2 for odd D-1), words 2,3 -> uniforms 2,3;
+ * call 2+c: uniforms 4+4c .. 7+4c; logs over products of at most 16 uniforms.  Call 0 alone bounds the
+ * log-likelihood from above (the device screens far auxiliaries with it; results unchanged).  A picked
+ * auxiliary's xi = xi_par yhat + sqrt(chi2) w_perp/|w_perp|, w ~ N(0,I) on stream AUX_DIR. */
+static inline int aux_calls(int D) {
+    const int k = (D - 1) / 2;
+    return 1 + ((((D - 1) & 1) || k > 2) ? 1 : 0) + (k > 4 ? (k - 1) / 4 : 0);
+}
 static inline int dir_calls(int D) { return (D + 3) / 4; }
 
 static void aux_core(const np8o_ctx *c, uint64_t i, uint32_t t, int m, double *v, double *xpar, double *chi2) {
-    const int D = c->D, Qa = aux_calls(D), k = (D - 1) / 2;
-    double g[4];
-    normal_quad(c->cfg.seed, i, t, NP8O_STREAM_AUX, (uint32_t)(m * Qa), g);
-    *v = fma(c->cfg.nu, g[0], (double)D);
-    *xpar = g[1];
+    const int D = c->D, Qa = aux_calls(D), k = (D - 1) / 2, odd = (D - 1) & 1;
+    const uint32_t base = (uint32_t)(m * Qa);
+    uint32_t w[4], w1[4] = {0u, 0u, 0u, 0u}, wc[4] = {0u, 0u, 0u, 0u};
+    philox_call(c->cfg.seed, i, t, NP8O_STREAM_AUX, base, w);
+    {
+        const double r = sqrt(-2.0 * np8o_log_pos(u32_01(w[0])));
+        double sn, cs;
+        np8o_sincos_2pi(u32_01(w[1]), &sn, &cs);
+        *v = fma(c->cfg.nu, r * cs, (double)D);
+        *xpar = r * sn;
+    }
+    double godd = 0.0;
+    if (odd || k > 2) {
+        philox_call(c->cfg.seed, i, t, NP8O_STREAM_AUX, base + 1u, w1);
+        if (odd) {
+            const double r = sqrt(-2.0 * np8o_log_pos(u32_01(w1[0])));
+            double sn, cs;
+            np8o_sincos_2pi(u32_01(w1[1]), &sn, &cs);
+            godd = r * cs;
+        }
+    }
     double c2 = 0.0, prod = 1.0;
-    uint32_t w[4] = {0u, 0u, 0u, 0u};
     int in_chunk = 0;
     for (int j = 0; j < k; ++j) {
-        if ((j & 3) == 0) philox_call(c->cfg.seed, i, t, NP8O_STREAM_AUX, (uint32_t)(m * Qa + 1 + (j >> 2)), w);
-        prod *= u32_01(w[j & 3]);
+        uint32_t word;
+        if (j < 2) {
+            word = w[2 + j];
+        } else if (j < 4) {
+            word = w1[j];
+        } else {
+            if (((j - 4) & 3) == 0)
+                philox_call(c->cfg.seed, i, t, NP8O_STREAM_AUX, base + 2u + (uint32_t)((j - 4) >> 2), wc);
+            word = wc[(j - 4) & 3];
+        }
+        prod *= u32_01(word);
         if (++in_chunk == 16 || j == k - 1) {
             c2 = fma(-2.0, np8o_log_pos(prod), c2);
             prod = 1.0;
             in_chunk = 0;
         }
     }
-    if ((D - 1) & 1) c2 = fma(g[2], g[2], c2);
+    if (odd) c2 = fma(godd, godd, c2);
     *chi2 = c2;
 }
 
