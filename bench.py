@@ -272,6 +272,10 @@ def main():
                             "cost, over the timed launch time; the M auxiliary G0 draws per item (Philox, "
                             "Box-Muller, chi^2 logs) are not flops of this count",
                     "quad_forms_per_item": nq / max(n_items, 1),
+                    "aux_exact_per_item": (sc1["aux_exact_lanes"] - sc0["aux_exact_lanes"]) / cnt_sweeps / max(n_items, 1),
+                    "aux_exact_wave_frac": (sc1["aux_exact_waves"] - sc0["aux_exact_waves"]) / cnt_sweeps
+                    / max(((n_items + 63) // 64) * smp.M, 1),
+                    "aux_screen_violations": sc1["screen_violations"] - sc0["screen_violations"],
                     "iso_fraction": nq_iso / max(nq, 1),
                     "tflops": exec_flops / (ms_assign * 1e-3) / 1e12 if ms_assign > 0 else None,
                     "frac_of_peak": exec_flops / (ms_assign * 1e-3) / 1e12 / peak if ms_assign > 0 else None,

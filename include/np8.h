@@ -120,6 +120,9 @@ typedef struct {
     /* NP8_TIMING_COUNTERS self-check of the auxiliary screen (DESIGN.md "Auxiliary screen"): lanes whose
      * screened-out auxiliary would not have been skipped by the pick.  0 unless the screen's margin is wrong. */
     int64_t screen_violations;
+    /* NP8_TIMING_COUNTERS: (item, auxiliary) pairs the screen did not skip (the exact fp64 draw ran), and
+     * (wave, auxiliary) pairs where at least one of the wave's 64 items needed it */
+    int64_t aux_exact_lanes, aux_exact_waves;
 } np8_stats_t;
 
 /* Create / destroy.  Replaces NealAlgorithm8::NealAlgorithm8 (np_neal_algorithm8.cpp:17-34). */

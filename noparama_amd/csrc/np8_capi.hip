@@ -1158,7 +1158,7 @@ int np8_create(np8_ctx **out, const np8_config *cfg) {
         (r = dalloc(c, &c->mu_best, (size_t)kc * D)) || (r = dalloc(c, &c->sigma_best, (size_t)kc * D * D)) ||
         (r = dalloc(c, &c->cand, (size_t)kc * c->CS)) || (r = dalloc(c, &c->ctl, 1)) ||
         (r = dalloc(c, &c->dense_of, (size_t)kc)) || (r = dalloc(c, &c->slot_iso, (size_t)kc)) ||
-        (r = dalloc(c, &c->rec, (size_t)c->rec_bytes)) || (r = dalloc(c, &c->evalc, (size_t)2 * kEvalSlots)) ||
+        (r = dalloc(c, &c->rec, (size_t)c->rec_bytes)) || (r = dalloc(c, &c->evalc, (size_t)4 * kEvalSlots)) ||
         (c->param_update != NP8_PARAM_FROZEN && (r = dalloc(c, &c->acc, (size_t)kc * (D + DP)))) ||
         (kc <= kPruneMaxKcap && ((r = dalloc(c, &c->r2, (size_t)kc)) || (r = dalloc(c, &c->plen, (size_t)kc)) ||
                                  (r = dalloc(c, &c->plist, (size_t)kc * kc))))) {
@@ -1604,11 +1604,13 @@ int np8_stats(np8_ctx *c, np8_stats_t *out) {
     out->mh_accepted = h.mh_accepted;
     out->screen_violations = (int64_t)h.n_screen_viol;
     {
-        std::vector<unsigned long long> ev((size_t)2 * kEvalSlots);
+        std::vector<unsigned long long> ev((size_t)4 * kEvalSlots);
         HIPC(c, hipMemcpy(ev.data(), c->evalc, sizeof(unsigned long long) * ev.size(), hipMemcpyDeviceToHost));
         for (int k = 0; k < kEvalSlots; ++k) {
             out->n_quad += (int64_t)ev[2 * k];
             out->n_quad_iso += (int64_t)ev[2 * k + 1];
+            out->aux_exact_lanes += (int64_t)ev[2 * kEvalSlots + 2 * k];
+            out->aux_exact_waves += (int64_t)ev[2 * kEvalSlots + 2 * k + 1];
         }
     }
     return NP8_OK;

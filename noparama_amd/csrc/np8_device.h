@@ -212,18 +212,18 @@ NP8_HD int aux_calls(int D) {
 }
 NP8_HD int dir_calls(int D) { return (D + 3) / 4; }
 
-// w0: the words of call m*Qa when the caller has them already (else null).
-NP8_HD void aux_core(uint64_t seed, uint64_t i, uint32_t t, int m, int D, double nu, double &v, double &xpar,
-                     double &chi2, const uint32_t *w0 = nullptr) {
-    const int Qa = aux_calls(D), k = (D - 1) / 2;
-    const bool odd = ((D - 1) & 1) != 0;
+// w: the words of call m*Qa; w1g the words of call m*Qa + 1 when have_w1 (else drawn here).  Arrays by
+// reference, never through a pointer: a pointer to a register array would move it to scratch memory.
+// D is a template constant: the chi^2 loop unrolls and every word index is static (a run-time index
+// into a register array would move the array to scratch memory).
+template <int D>
+NP8_HD void aux_core_w(uint64_t seed, uint64_t i, uint32_t t, int m, double nu, double &v, double &xpar,
+                       double &chi2, const uint32_t (&w)[4], bool have_w1, const uint32_t (&w1g)[4]) {
+    constexpr int k = (D - 1) / 2;
+    constexpr bool odd = ((D - 1) & 1) != 0;
+    const int Qa = aux_calls(D);
     const uint32_t base = (uint32_t)(m * Qa);
-    uint32_t w[4], w1[4] = {0u, 0u, 0u, 0u}, wc[4] = {0u, 0u, 0u, 0u};
-    if (w0) {
-        for (int h = 0; h < 4; ++h) w[h] = w0[h];
-    } else {
-        philox_call(seed, i, t, kStreamAux, base, w);
-    }
+    uint32_t w1[4] = {0u, 0u, 0u, 0u}, wc[4] = {0u, 0u, 0u, 0u};
     {
         const double r = sqrt(-2.0 * log_pos(u32_01(w[0])));
         double sn, cs;
@@ -233,7 +233,11 @@ NP8_HD void aux_core(uint64_t seed, uint64_t i, uint32_t t, int m, int D, double
     }
     double godd = 0.0;
     if (odd || k > 2) {
-        philox_call(seed, i, t, kStreamAux, base + 1u, w1);
+        if (have_w1) {
+            for (int h = 0; h < 4; ++h) w1[h] = w1g[h];
+        } else {
+            philox_call(seed, i, t, kStreamAux, base + 1u, w1);
+        }
         if (odd) {
             const double r = sqrt(-2.0 * log_pos(u32_01(w1[0])));
             double sn, cs;
@@ -243,6 +247,7 @@ NP8_HD void aux_core(uint64_t seed, uint64_t i, uint32_t t, int m, int D, double
     }
     double c2 = 0.0, prod = 1.0;
     int in_chunk = 0;
+#pragma unroll
     for (int j = 0; j < k; ++j) {
         uint32_t word;
         if (j < 2) {
@@ -262,6 +267,14 @@ NP8_HD void aux_core(uint64_t seed, uint64_t i, uint32_t t, int m, int D, double
     }
     if (odd) c2 = fma(godd, godd, c2);
     chi2 = c2;
+}
+
+template <int D>
+NP8_HD void aux_core(uint64_t seed, uint64_t i, uint32_t t, int m, double nu, double &v, double &xpar, double &chi2) {
+    uint32_t w[4];
+    const uint32_t none[4] = {0u, 0u, 0u, 0u};
+    philox_call(seed, i, t, kStreamAux, (uint32_t)(m * aux_calls(D)), w);
+    aux_core_w<D>(seed, i, t, m, nu, v, xpar, chi2, w, false, none);
 }
 
 // Log-likelihood of the item under auxiliary (v, xi_par, chi2); ny = |y0|.

@@ -33,6 +33,8 @@ struct Ctl {
                           // np8_finalize then copies them; parameter updates patch rows in place)
     unsigned long long n_screen_viol;  // count_eval runs: lanes with a screened auxiliary that pick_step would
                                        // not have skipped (the auxiliary screen's self-check; must stay 0)
+    unsigned long long n_aux_exact[2]; // count_eval runs: (lane, auxiliary) pairs the screen did not skip,
+                                       // and (wave, auxiliary) pairs in which at least one lane was not skipped
 };
 
 // Executed work of np8_assign when AssignArgs::count_eval is set (timing mode): per wave, the cluster

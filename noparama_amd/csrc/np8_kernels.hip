@@ -89,7 +89,7 @@ __device__ __forceinline__ double aux_ll(const double *__restrict__ hyp, double 
                                          uint32_t t, int m) {
     using H = HypView<D>;
     double v, xpar, chi2;
-    aux_core(seed, ig, t, m, D, hyp[H::kNu], v, xpar, chi2);
+    aux_core<D>(seed, ig, t, m, hyp[H::kNu], v, xpar, chi2);
     return aux_loglik(ny, v, xpar, chi2, D, hyp[H::kRsk], hyp[H::kCaux]);
 }
 
@@ -103,18 +103,18 @@ __device__ __forceinline__ double niw_aux_ll(const double *__restrict__ hyp, dou
     return niw_aux_loglik(nd, sumlog, b00, chi, z1, hyp[H::kRsk], hyp[H::kCaux]);
 }
 
-// Screen of auxiliary m from the words w of its first Philox call (DESIGN.md "Auxiliary screen"): true
-// when its exact log-likelihood (aux_core + aux_loglik, fp64) is certainly <= thr, so that pick_step
-// would skip it.  From call 0 alone: v and xi_par exactly, chi2 >= -2 log(u_0 u_1) (the remaining
-// uniforms are <= 1 and g_odd^2 >= 0), hence
+// Screen of an auxiliary (DESIGN.md "Auxiliary screen"): an upper bound (plus its error margin) of the
+// exact fp64 log-likelihood aux_core + aux_loglik computes.  From the words w of call 0: v and xi_par
+// exactly, chi2 >= -2 log(u_0 u_1) (the other uniforms are <= 1, g_odd^2 >= 0) plus chi_extra, what the
+// caller adds from call 1 (level 2), so
 //   ll = caux - D log|v| - q/2,  q = (ny/|v| - rsk xi_par)^2 + rsk^2 chi2  >=  the same with chi2's bound.
-// Evaluated in fp32 on the transcendental units (v_log_f32, v_sqrt_f32, v_cos_f32/v_sin_f32 in
-// revolutions, v_rcp_f32), with an error margin that covers those approximations with a factor of ten:
-// |error of r cos, r sin| <= 4e-3 (3.5e-4 from rounding u0 to fp32 near 1), relative 1e-4 elsewhere.
-// No screen near v = 0 (|v| < 1/4), where log|v| and ny/|v| are ill-conditioned.
+// fp32 on the transcendental units (v_log_f32, v_sqrt_f32, v_cos_f32/v_sin_f32 in revolutions,
+// v_rcp_f32); the margin covers those approximations with a factor of ten: |error of r cos, r sin| <=
+// 4e-3 (3.5e-4 from rounding u0 to fp32 near 1), relative 1e-4 elsewhere, chi_extra_err for chi_extra.
+// Returns +inf (no screen) near v = 0 (|v| < 1/4), where log|v| and ny/|v| are ill-conditioned.
 template <int D>
-__device__ __forceinline__ bool aux_screen_skips(const uint32_t (&w)[4], float ny, float nu, float rsk, float caux,
-                                                 float thr) {
+__device__ __forceinline__ float aux_screen_ub(const uint32_t (&w)[4], float chi_extra, float chi_extra_err, float ny,
+                                               float nu, float rsk, float caux, float thr) {
     constexpr float kLn2 = 0.693147180559945f;
     constexpr int k = (D - 1) / 2;
     const float u0 = fmaf((float)w[0], 0x1.0p-32f, 0x1.0p-33f);
@@ -124,23 +124,52 @@ __device__ __forceinline__ bool aux_screen_skips(const uint32_t (&w)[4], float n
     const float xp = r * __builtin_amdgcn_sinf(u1);
     const float v = fmaf(nu, g0, (float)D);
     const float av = fabsf(v);
-    float chi = 0.0f;
+    float chi = chi_extra;
     if constexpr (k >= 2) {
         const float ua = fmaf((float)w[2], 0x1.0p-32f, 0x1.0p-33f), ub = fmaf((float)w[3], 0x1.0p-32f, 0x1.0p-33f);
-        chi = -2.0f * kLn2 * __builtin_amdgcn_logf(ua * ub);
+        chi = fmaf(-2.0f * kLn2, __builtin_amdgcn_logf(ua * ub), chi);
     } else if constexpr (k == 1) {
-        chi = -2.0f * kLn2 * __builtin_amdgcn_logf(fmaf((float)w[2], 0x1.0p-32f, 0x1.0p-33f));
+        chi = fmaf(-2.0f * kLn2, __builtin_amdgcn_logf(fmaf((float)w[2], 0x1.0p-32f, 0x1.0p-33f)), chi);
     }
-    const float iv = __builtin_amdgcn_rcpf(av);
-    const float lnv = kLn2 * __builtin_amdgcn_logf(av);
-    const float nyv = ny * iv;
-    const float a = nyv - rsk * xp;
-    const float qlb = fmaf(a, a, rsk * rsk * chi);
+    // interval bounds: |v| in [av_lo, av_hi], xi_par in [xp - dg, xp + dg] (dg = 4e-3 covers r cos, r sin)
+    constexpr float dg = 4e-3f;
+    const float dv = nu * dg;
+    const float av_lo = av - dv, av_hi = av + dv;
+    const float a_lo = fmaf(-rsk, xp + dg, ny * __builtin_amdgcn_rcpf(av_hi));  // ny / |v| - rsk xi_par
+    const float a_hi = fmaf(-rsk, xp - dg, ny * __builtin_amdgcn_rcpf(av_lo));
+    const float amin = (a_lo > 0.0f) ? a_lo : ((a_hi < 0.0f) ? -a_hi : 0.0f);
+    const float lnv = kLn2 * __builtin_amdgcn_logf(av_lo);  // -D log|v| <= -D log av_lo
+    const float rsk2 = rsk * rsk;
+    const float qlb = fmaf(amin, amin, rsk2 * fmaxf(chi - chi_extra_err, 0.0f));
     const float ub_ll = fmaf(-0.5f, qlb, caux - (float)D * lnv);
-    const float ea = 4e-3f * fmaf(nyv * nu, iv, rsk);
-    const float err = 1.0f + (float)D * 4e-3f * nu * iv + fabsf(a) * ea + ea * ea +
-                      1e-4f * (qlb + fabsf(caux) + (float)D * fabsf(lnv) + fabsf(thr));
-    return av >= 0.25f && ub_ll + err <= thr;
+    const float err = 1.0f + 1e-4f * (qlb + fabsf(caux) + (float)D * fabsf(lnv) + fabsf(thr));
+    return (av_lo >= 0.02f) ? ub_ll + err : __builtin_inff();
+}
+
+// Level 2 of the screen from the words w1 of call 1: the further chi^2 terms it holds (uniforms 2, 3 and
+// g_odd^2 for odd D - 1; exact chi2 for D <= 9) and their fp32 error.
+template <int D>
+__device__ __forceinline__ float aux_screen_chi1(const uint32_t (&w1)[4], float &err) {
+    constexpr float kLn2 = 0.693147180559945f;
+    constexpr int k = (D - 1) / 2;
+    constexpr bool odd = ((D - 1) & 1) != 0;
+    float chi = 0.0f;
+    err = 0.0f;
+    if constexpr (odd) {
+        const float u0 = fmaf((float)w1[0], 0x1.0p-32f, 0x1.0p-33f);
+        const float u1 = fmaf((float)w1[1], 0x1.0p-32f, 0x1.0p-33f);
+        const float g = __builtin_amdgcn_sqrtf(-2.0f * kLn2 * __builtin_amdgcn_logf(u0)) * __builtin_amdgcn_cosf(u1);
+        chi = g * g;
+        err = fmaf(8e-3f, fabsf(g), 2e-5f) + 1e-4f * chi;
+    }
+    if constexpr (k >= 3) {
+        float p = fmaf((float)w1[2], 0x1.0p-32f, 0x1.0p-33f);
+        if constexpr (k >= 4) p *= fmaf((float)w1[3], 0x1.0p-32f, 0x1.0p-33f);
+        const float c = -2.0f * kLn2 * __builtin_amdgcn_logf(p);
+        chi += c;
+        err += 1e-4f * c + 1e-6f;
+    }
+    return chi;
 }
 
 template <int D, int PRIOR>
@@ -158,7 +187,7 @@ __device__ __forceinline__ void aux_params(const double *__restrict__ hyp, const
                                            uint64_t seed, uint64_t ig, uint32_t t, int m, double *vmu) {
     using H = HypView<D>;
     double v, xpar, chi2, xi[D];
-    aux_core(seed, ig, t, m, D, hyp[H::kNu], v, xpar, chi2);
+    aux_core<D>(seed, ig, t, m, hyp[H::kNu], v, xpar, chi2);
     aux_xi<D>(seed, ig, t, m, D, y0, ny, xpar, chi2, xi);
     const double sc = fabs(v) * hyp[H::kRsk];
     const double *LT = hyp + H::kLT;
@@ -182,6 +211,22 @@ __device__ __forceinline__ double norm_of(const double (&y0)[D]) {
 }
 
 // Scan position -> local item | visit << 32 (the visit is non-zero only for explicit orders).
+// The pick's uniform (stream PICK, call 0) is drawn when a candidate first survives the skip rule: an
+// item whose draw never leaves its own cluster does not need it (same value as drawing it up front).
+// Wave-uniform branch: when any lane needs it, every lane without it draws it.
+// (out of line: the Philox rounds would otherwise be inlined into every candidate loop, and their
+// registers counted against the loops' live state)
+__device__ __forceinline__ double pick_uniform(uint64_t seed, uint64_t ig, uint32_t t) {
+    return uniform(seed, ig, t, kStreamPick, 0);
+}
+
+__device__ __forceinline__ void ensure_u(PickState &st, double lw, uint64_t seed, uint64_t ig, uint32_t t) {
+    const bool need = st.u < 0.0 && lw - st.T > -kSkip;
+    if (__ballot(need)) {
+        if (st.u < 0.0) st.u = pick_uniform(seed, ig, t);
+    }
+}
+
 __device__ __forceinline__ int64_t position_to_local(const AssignArgs &A, int64_t p) {
     if (A.order) return A.order[p];
     if (A.use_perm) return (int64_t)perm_apply(A.perm, (uint32_t)p);
@@ -221,10 +266,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void n
     const int32_t jo = A.dense_of[zi];
     PickState st;
     {
-        const double *eo = cand + (int64_t)jo * CS;
-        st.T = cand_ll<D>(eo, x) + eo[F + kFieldLogn1];
+        // one pass per distinct own row of the wave (one in the label-sorted layout), the row read with
+        // scalar loads: a per-lane row would hold all D + D(D+1)/2 of its doubles in vector registers
+        uint64_t pend = __ballot(1);
+        while (pend) {
+            const int32_t j = __builtin_amdgcn_readlane(jo, __ffsll((unsigned long long)pend) - 1);
+            const double *eo = cand + (int64_t)j * CS;
+            const double lw = cand_ll<D>(eo, x) + eo[F + kFieldLogn1];
+            if (jo == j) st.T = lw;
+            pend &= ~__ballot(jo == j);
+        }
         st.S = 1.0;
-        st.u = uniform(A.seed, ig, t, kStreamPick, 0);
+        st.u = -1.0;  // drawn when a candidate first survives the skip rule (ensure_u)
         st.pick = jo;
     }
     const double zslot = (double)zi;
@@ -240,13 +293,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void n
         for (int q = 0; q < nl; ++q) {
             const int j = lst[q];  // wave-uniform: scalar loads
             const double *e = cand + (int64_t)j * CS;
-            pick_step(st, cand_ll<D>(e, x) + e[F + kFieldLogn], j);
+            const double lw = cand_ll<D>(e, x) + e[F + kFieldLogn];
+            ensure_u(st, lw, A.seed, ig, t);
+            pick_step(st, lw, j);
         }
     } else {
         for (int j = 0; j < K; ++j) {
             const double *e = cand + (int64_t)j * CS;  // wave-uniform: scalar loads
             const double lw = cand_ll<D>(e, x) + e[F + kFieldLogn];
-            if (e[F + kFieldSlot] != zslot) pick_step(st, lw, j);
+            if (e[F + kFieldSlot] != zslot) {
+                ensure_u(st, lw, A.seed, ig, t);
+                pick_step(st, lw, j);
+            }
         }
     }
     if constexpr (COUNT) {  // the quadratic forms this wave executed (own row + walked rows)
@@ -267,41 +325,80 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void n
             atomicAdd(ec + 1, (unsigned long long)(niso * nl + n_own_iso));
         }
     }
-    double y0[D];
-    whiten<D>(hyp, x, y0);
-    const double ny = norm_of<D>(y0);
+    double ny;
+    {
+        double y0[D];
+        whiten<D>(hyp, x, y0);
+        ny = norm_of<D>(y0);
+    }
     {
         const double logam = hyp[HypView<D>::kLogam];
         if constexpr (PRIOR == kPriorNiw) {
 #pragma unroll 1
-            for (int m = 0; m < M; ++m) pick_step(st, prior_aux_ll<D, PRIOR>(hyp, ny, A.seed, ig, t, m) + logam, K + m);
+            for (int m = 0; m < M; ++m) {
+                const double lw = prior_aux_ll<D, PRIOR>(hyp, ny, A.seed, ig, t, m) + logam;
+                ensure_u(st, lw, A.seed, ig, t);
+                pick_step(st, lw, K + m);
+            }
         } else {
-            // the first Philox call of every auxiliary bounds its log-likelihood (aux_screen_skips);
-            // only lanes whose auxiliary may come within kSkip of the running maximum finish the draw
+            // the first Philox call of every auxiliary bounds its log-likelihood (aux_screen_ub); lanes
+            // it cannot rule out take call 1 (level 2), and only the lanes still left finish the fp64
+            // draw -- those whose auxiliary may come within kSkip of the running maximum
             using H = HypView<D>;
             const double nu = hyp[H::kNu], rsk = hyp[H::kRsk], caux = hyp[H::kCaux];
             const float thr = (float)(st.T - kSkip - logam);  // T only grows: conservative for every m
-            const int Qa = aux_calls(D);
-            int64_t n_viol = 0;
+            const float nyf = (float)ny, nuf = (float)nu, rskf = (float)rsk, cauxf = (float)caux;
+            constexpr int Qa = (1 + ((((D - 1) & 1) || (D - 1) / 2 > 2) ? 1 : 0) + ((D - 1) / 2 > 4 ? ((D - 1) / 2 - 1) / 4 : 0));
+            constexpr bool has_call1 = Qa > 1;
+            // level 1 for every auxiliary at once (M independent Philox chains): a bit per auxiliary the
+            // screen cannot rule out
+            uint32_t need = 0u;
 #pragma unroll 1
             for (int m = 0; m < M; ++m) {
                 uint32_t w[4];
                 philox_call(A.seed, ig, t, kStreamAux, (uint32_t)(m * Qa), w);
-                const bool skip = aux_screen_skips<D>(w, (float)ny, (float)nu, (float)rsk, (float)caux, thr);
+                if (!(aux_screen_ub<D>(w, 0.0f, 0.0f, nyf, nuf, rskf, cauxf, thr) <= thr)) need |= 1u << m;
+            }
+            int64_t n_viol = 0, n_ex_lane = 0, n_ex_wave = 0;
+#pragma unroll 1
+            for (int m = 0; m < M; ++m) {
+                bool skip = ((need >> m) & 1u) == 0u;
+                if (!COUNT && __ballot(!skip) == 0ull) continue;  // wave-uniform: the common case
+                uint32_t w0[4], w1[4] = {0u, 0u, 0u, 0u};
+                philox_call(A.seed, ig, t, kStreamAux, (uint32_t)(m * Qa), w0);
+                const bool l2 = has_call1 && !skip;
+                if (l2) {  // level 2: the chi^2 terms of call 1
+                    philox_call(A.seed, ig, t, kStreamAux, (uint32_t)(m * Qa + 1), w1);
+                    float e1;
+                    const float c1 = aux_screen_chi1<D>(w1, e1);
+                    skip = aux_screen_ub<D>(w0, c1, e1, nyf, nuf, rskf, cauxf, thr) <= thr;
+                }
+                if constexpr (COUNT) {
+                    const uint64_t b = __ballot(!skip);
+                    n_ex_lane += __popcll(b);
+                    n_ex_wave += (b != 0ull) ? 1 : 0;
+                }
                 if (!skip || COUNT) {
                     double v, xpar, chi2;
-                    aux_core(A.seed, ig, t, m, D, nu, v, xpar, chi2, w);
+                    aux_core_w<D>(A.seed, ig, t, m, nu, v, xpar, chi2, w0, l2, w1);
                     const double lw = aux_loglik(ny, v, xpar, chi2, D, rsk, caux) + logam;
-                    if (!skip)
+                    if (!skip) {
+                        ensure_u(st, lw, A.seed, ig, t);
                         pick_step(st, lw, K + m);
-                    else if (lw - st.T > -kSkip)
+                    } else if (lw - st.T > -kSkip) {
                         ++n_viol;  // debug count: a screened auxiliary pick_step would not have skipped
+                    }
                 }
             }
             if constexpr (COUNT) {
                 const int nv = __popcll(__ballot(n_viol > 0));
-                if (nv && (threadIdx.x & 63) == (__ffsll((unsigned long long)__ballot(1)) - 1))
-                    atomicAdd(&A.ctl->n_screen_viol, (unsigned long long)nv);
+                if ((threadIdx.x & 63) == (__ffsll((unsigned long long)__ballot(1)) - 1)) {
+                    if (nv) atomicAdd(&A.ctl->n_screen_viol, (unsigned long long)nv);
+                    unsigned long long *ec = A.evalc + 2 * kEvalSlots +
+                                             2 * ((blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) % kEvalSlots);
+                    atomicAdd(ec, (unsigned long long)n_ex_lane);
+                    atomicAdd(ec + 1, (unsigned long long)n_ex_wave);
+                }
             }
         }
     }
@@ -355,6 +452,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void n
             r.pad = 0;
             A.req[q] = r;
             double *vmu = A.vmu + (int64_t)q * (D + 1);
+            double y0[D];  // the item's frame again (not kept live through the draw: registers)
+            whiten<D>(hyp, x, y0);
             if constexpr (PRIOR == kPriorNiw) {  // the item's frame; np8_niw_aux_slots builds the slot
                 vmu[0] = ny;
 #pragma unroll

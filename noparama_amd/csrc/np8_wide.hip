@@ -94,7 +94,7 @@ __device__ __forceinline__ double wide_aux_ll(const double *__restrict__ hyp, do
         return niw_aux_loglik(ny, sumlog, b00, chi, z1, rsk, caux);
     } else {
         double v, xpar, chi2;
-        aux_core(seed, ig, t, m, D, nu, v, xpar, chi2);
+        aux_core<D>(seed, ig, t, m, nu, v, xpar, chi2);
         return aux_loglik(ny, v, xpar, chi2, D, rsk, caux);
     }
 }

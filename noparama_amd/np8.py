@@ -98,6 +98,8 @@ class Stats(C.Structure):
         ("n_quad", C.c_int64),
         ("n_quad_iso", C.c_int64),
         ("screen_violations", C.c_int64),
+        ("aux_exact_lanes", C.c_int64),
+        ("aux_exact_waves", C.c_int64),
     ]
 
 
