@@ -204,6 +204,14 @@ int np8_get_state(np8_ctx *ctx, int32_t which, int32_t *z, int32_t *K, double *m
  * out is n x (K+M) with K = current live count.  Same arithmetic as the sweep kernel. */
 int np8_loglik_matrix(np8_ctx *ctx, const int64_t *idx, int64_t n, double *out);
 
+/* Parity/debug: the sweep's categorical draw (DESIGN.md "Pick": the single-uniform reservoir over
+ * log-weights with the -80 skip rule, np8_assign's pick_step) on caller-given log-weights: out[k] = the
+ * candidate picked from lw[0..n) with uniform u[k] in (0,1), candidate 0 taking the place of the item's own
+ * cluster.  Replaces algebra::random_weighted_pick (include/helper/dim1algebra.hpp:2078-2104) called at
+ * np_neal_algorithm8.cpp:126; tests/test_gpu_pick.py checks it against the oracle and, in distribution,
+ * against the reference function itself. */
+int np8_pick_batch(np8_ctx *ctx, const double *lw, int32_t n, const double *u, int64_t n_draws, int32_t *out);
+
 /* Sum over items of log p(x_i | theta_{z_i}) for the current state (MCMC::considerMaxLikelihood). */
 int np8_total_loglik(np8_ctx *ctx, double *out);
 

@@ -57,6 +57,7 @@ struct np8_ctx {
     double *acc = nullptr;  // [kcap][D + DP] parameter-update statistics
     // candidate pruning (np8_prune): per-slot radii and per-row candidate lists
     double *r2 = nullptr;
+    WaveR2 *wr2 = nullptr;  // per-wave radius records of the sweep's assign (ceil(n_loc / 64))
     int32_t *plist = nullptr, *plen = nullptr;
     unsigned long long *evalc = nullptr;  // [kEvalSlots][2] executed-work counters (timing mode)
     bool prune_on = false;     // kcap small enough for kcap x kcap lists
@@ -372,7 +373,7 @@ void free_device(np8_ctx *c) {
                     c->cnt,    c->cnt_best, c->mu_best, c->sigma_best, c->cand, c->ctl,    c->hyp,
                     c->d_mu0,  c->d_LT,    c->d_Gp,   c->d_LTL,   c->rec,     c->gath,    c->order,
                     c->partial, c->dense_of, c->Xs[0], c->Xs[1], c->zs[0], c->zs[1], c->ids[0], c->ids[1],
-                    c->s_hist, c->s_cursor, c->s_off, c->slot_iso, c->acc, c->r2, c->plist, c->plen,
+                    c->s_hist, c->s_cursor, c->s_off, c->slot_iso, c->acc, c->r2, c->wr2, c->plist, c->plen,
                     c->sm_hist, c->sm_mem, c->sm_off, c->sm_live, c->sm_Xm, c->sm_ownm, c->sm_cross, c->sm_ctl,
                     c->sm_typ, c->sm_slist, c->sm_stheta, c->stage, c->evalc};
     for (void *p : ptrs)
@@ -395,6 +396,7 @@ void free_device(np8_ctx *c) {
     c->slot_iso = nullptr;
     c->acc = nullptr;
     c->r2 = nullptr;
+    c->wr2 = nullptr;
     c->plist = c->plen = nullptr;
     c->X = nullptr;
     c->z = c->z_best = nullptr;
@@ -576,10 +578,6 @@ FinArgs fin_args(np8_ctx *c, const unsigned char *recs, int world) {
     F.seed = c->seed;
     F.t = c->epoch - c->t_base;
     F.r2 = c->r2;
-    F.prune = 0;
-    F.ls = c->kcap;
-    F.plist = c->plist;
-    F.plen = c->plen;
     F.prior = c->prior;
     F.req_max = c->req_max;
     F.pend = c->pend;
@@ -684,6 +682,7 @@ AssignArgs assign_args(np8_ctx *c, int64_t p0, int64_t p1, const int64_t *order,
     A.count_eval = c->count_eval ? 1 : 0;
     A.evalc = c->evalc;
     A.r2 = c->r2;
+    A.wr2 = c->wr2;
     A.wfrag = c->wfrag;
     return A;
 }
@@ -692,9 +691,6 @@ int launch_finalize(np8_ctx *c, const unsigned char *recs, int world) {
     Timer t;
     timer_begin(c, 1, t);
     FinArgs F = fin_args(c, recs, world);
-    // Fused list building (F.prune) is available but off: one workgroup walks the rows 16 at a time,
-    // slower (≈+10 µs at K = 64) than the standalone np8_prune launch with one wave per row.
-    F.prune = 0;
     HIPC(c, np8_launch_finalize(F, c->stream));
     if (c->prior == NP8_PRIOR_NIW) {  // the accepted auxiliaries' full parameters
         NiwArgs A = niw_args(c);
@@ -705,10 +701,6 @@ int launch_finalize(np8_ctx *c, const unsigned char *recs, int world) {
     int r = refresh_wide(c, false);  // the slots created here
     if (r) return r;
     timer_end(c, t);
-    if (F.prune) {
-        c->lists_valid = true;
-        c->r2_zero = true;
-    }
     return NP8_OK;
 }
 
@@ -742,6 +734,9 @@ int launch_prune(np8_ctx *c) {
     P.cand = c->cand;
     P.ctl = c->ctl;
     P.r2 = c->r2;
+    P.wr2 = c->wr2;
+    P.n_waves = (c->n_loc + 63) / 64;
+    P.kcap = c->kcap;
     P.plist = c->plist;
     P.plen = c->plen;
     P.ls = c->kcap;
@@ -1248,7 +1243,7 @@ int np8_set_data(np8_ctx *c, const double *X, int64_t n, int32_t D, int64_t offs
     int r = 0;
     const size_t nx = c->wide ? ((size_t)n * D + 1) / 2 : (size_t)n * D;  // wide path: fp32 items
     if ((r = dalloc(c, &c->X, nx)) || (r = dalloc(c, &c->z, (size_t)n)) ||
-        (r = dalloc(c, &c->z_best, (size_t)n)))
+        (r = dalloc(c, &c->z_best, (size_t)n)) || (r = dalloc(c, &c->wr2, (size_t)((n + 63) / 64))))
         return r;
     for (int b = 0; b < 2; ++b)
         if ((r = dalloc(c, &c->Xs[b], nx)) || (r = dalloc(c, &c->zs[b], (size_t)n)) ||
@@ -1559,6 +1554,26 @@ int np8_loglik_matrix(np8_ctx *c, const int64_t *idx, int64_t n, double *out) {
     HIPC(c, hipStreamSynchronize(c->stream));
     HIPC(c, hipMemcpy(out, d_out, sizeof(double) * n * w, hipMemcpyDeviceToHost));
     (void)hipFree(d_idx);
+    (void)hipFree(d_out);
+    return NP8_OK;
+}
+
+int np8_pick_batch(np8_ctx *c, const double *lw, int32_t n, const double *u, int64_t n_draws, int32_t *out) {
+    if (!c || !lw || !u || !out || n < 1 || n_draws < 0 || n_draws > (int64_t)1 << 31)
+        return c ? fail(c, NP8_ERR_ARG, "np8_pick_batch: bad arguments") : NP8_ERR_ARG;
+    if (n_draws == 0) return NP8_OK;
+    double *d_lw = nullptr, *d_u = nullptr;
+    int32_t *d_out = nullptr;
+    HIPC(c, hipMalloc(&d_lw, sizeof(double) * n));
+    HIPC(c, hipMalloc(&d_u, sizeof(double) * n_draws));
+    HIPC(c, hipMalloc(&d_out, sizeof(int32_t) * n_draws));
+    HIPC(c, hipMemcpy(d_lw, lw, sizeof(double) * n, hipMemcpyHostToDevice));
+    HIPC(c, hipMemcpy(d_u, u, sizeof(double) * n_draws, hipMemcpyHostToDevice));
+    HIPC(c, np8_launch_pick_batch(d_lw, n, d_u, n_draws, d_out, c->stream));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    HIPC(c, hipMemcpy(out, d_out, sizeof(int32_t) * n_draws, hipMemcpyDeviceToHost));
+    (void)hipFree(d_lw);
+    (void)hipFree(d_u);
     (void)hipFree(d_out);
     return NP8_OK;
 }

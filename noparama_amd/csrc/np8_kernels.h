@@ -82,6 +82,15 @@ NP8_HD int64_t record_bytes(int kcap, int rec_cap, int D) {
     return (b + 15) & ~15ll;
 }
 
+// Radius record of one assign wave (candidate pruning): the largest |x - mu|^2 over its 64 items and the
+// slot they all sit in, or slot -1 when they do not share one (those items went to r2 by atomics).
+// Plain stores instead of one device-scope atomic per wave on a handful of addresses: those serialise
+// at the memory side and cost the sweep ~50 us at C3.
+struct WaveR2 {
+    double d2;
+    int32_t slot, pad;
+};
+
 struct AssignArgs {
     const double *X;   // [D][n_loc] (structure of arrays), item order
     int32_t *z;        // [n_loc] slot ids, item order
@@ -111,7 +120,8 @@ struct AssignArgs {
     // lists of the next sweep
     const int32_t *plist, *plen;
     int32_t ls, use_lists, collect_r2, count_eval;
-    double *r2;
+    double *r2;      // per slot; only waves whose items are not all in one slot add to it (atomicMax)
+    WaveR2 *wr2;     // [ceil(n_loc / 64)]: a wave whose 64 items sit in one slot stores its maximum here
     unsigned long long *evalc;  // [kEvalSlots][2]: quadratic forms, isotropic ones
     // wide path (np8_wide.hip): per slot, the used MFMA fragment chunks of the fp32 factor followed by
     // the fp32 mean in fragment order (Wide<D>::ROW floats)
@@ -134,8 +144,10 @@ struct PruneArgs {
     const double *cand;
     Ctl *ctl;
     double *r2;
+    const WaveR2 *wr2;  // the sweep's per-wave maxima (AssignArgs::wr2), n_waves of them
+    int64_t n_waves;
     int32_t *plist, *plen;
-    int32_t ls, D;
+    int32_t ls, D, kcap;
 };
 
 struct FinArgs {
@@ -157,10 +169,6 @@ struct FinArgs {
     uint64_t seed;
     uint32_t t;  // epoch offset: epoch = ctl->t_base + t
     double *r2;  // pruning radii: +inf for every slot created here (unknown radius)
-    // fused candidate pruning after the table rebuild (whole synchronous sweep, no parameter update
-    // to follow); skipped -- lists marked stale -- above kPruneFusedMaxK rows
-    int32_t prune, ls;
-    int32_t *plist, *plen;
     // NIW prior: accepted requests are listed in pend[4 q] = (byte offset of the request's record
     // payload in recs, item, m, slot) for np8_niw_aux_slots instead of being written here
     int32_t prior, req_max;  // req_max: new clusters one step may create
@@ -332,6 +340,9 @@ hipError_t np8_launch_niw_post(const np8::NiwArgs &A, int nblocks, hipStream_t s
 hipError_t np8_launch_niw_aux_slots(const np8::NiwArgs &A, hipStream_t s);
 hipError_t np8_launch_resort(const SortArgs &S, hipStream_t s);
 hipError_t np8_launch_assign(const np8::AssignArgs &A, int D, int M, int prior, hipStream_t s);
+// Parity/debug: the sweep's categorical draw (pick_step) on given log-weights, one lane per draw.
+hipError_t np8_launch_pick_batch(const double *lw, int32_t n, const double *u, int64_t n_draws, int32_t *out,
+                                 hipStream_t s);
 hipError_t np8_launch_loglik_matrix(const np8::AssignArgs &A, int D, int M, int prior, const int64_t *idx, int64_t n,
                                     double *out, hipStream_t s);
 size_t np8_finalize_lds_bytes(int kcap);

@@ -236,7 +236,10 @@ __device__ __forceinline__ int64_t position_to_local(const AssignArgs &A, int64_
 // COUNT: the executed-work counters and the auxiliary screen's self-check (NP8_TIMING_COUNTERS), compiled
 // into a separate instance so that the timed kernel carries none of their registers.
 template <int D, int M, int PRIOR, bool COUNT>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void np8_assign(AssignArgs A) {
+#ifndef NP8_ASSIGN_WAVES
+#define NP8_ASSIGN_WAVES 4
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NP8_ASSIGN_WAVES))) void np8_assign(AssignArgs A) {
     constexpr int DP = D * (D + 1) / 2;
     constexpr int CS = (D + DP + 5 + 1) & ~1;
     constexpr int F = D + DP;
@@ -288,7 +291,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void n
     const bool walk_list = A.use_lists && A.ctl->lists_ok && __ballot(zi != z0) == 0;
     const int32_t j0 = __builtin_amdgcn_readfirstlane(jo);
     if (walk_list) {
+#ifdef NP8_EXP_NO_WALK
+        const int32_t nl = COUNT ? A.plen[j0] : 0;
+#else
         const int32_t nl = A.plen[j0];
+#endif
         const int32_t *__restrict__ lst = A.plist + (int64_t)j0 * A.ls;
         for (int q = 0; q < nl; ++q) {
             const int j = lst[q];  // wave-uniform: scalar loads
@@ -353,8 +360,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void n
             // level 1 for every auxiliary at once (M independent Philox chains): a bit per auxiliary the
             // screen cannot rule out
             uint32_t need = 0u;
+#ifdef NP8_EXP_UNROLL
+#pragma unroll
+#else
 #pragma unroll 1
+#endif
             for (int m = 0; m < M; ++m) {
+#ifdef NP8_EXP_NO_AUX
+                if (!COUNT) break;
+#endif
                 uint32_t w[4];
                 philox_call(A.seed, ig, t, kStreamAux, (uint32_t)(m * Qa), w);
                 if (!(aux_screen_ub<D>(w, 0.0f, 0.0f, nyf, nuf, rskf, cauxf, thr) <= thr)) need |= 1u << m;
@@ -364,6 +378,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void n
             for (int m = 0; m < M; ++m) {
                 bool skip = ((need >> m) & 1u) == 0u;
                 if (!COUNT && __ballot(!skip) == 0ull) continue;  // wave-uniform: the common case
+#ifdef NP8_EXP_NO_EXACT
+                if (!COUNT) continue;
+#endif
                 uint32_t w0[4], w1[4] = {0u, 0u, 0u, 0u};
                 philox_call(A.seed, ig, t, kStreamAux, (uint32_t)(m * Qa), w0);
                 const bool l2 = has_call1 && !skip;
@@ -405,7 +422,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void n
 
     int32_t *delta = reinterpret_cast<int32_t *>(A.rec + kRecHeaderBytes);
     const int32_t snew = (st.pick < K) ? (int32_t)cand[(int64_t)st.pick * CS + F + kFieldSlot] : -1;
+#ifdef NP8_EXP_NO_R2
+    if (A.collect_r2 && COUNT) {
+#else
     if (A.collect_r2) {
+#endif
         // radius of the item's cluster for the next sweep's lists: its distance to the mean of the row
         // it joins (an item that asked for a new cluster counts for its old one, in case the request
         // is rejected; the new slot's radius is set to +inf by np8_finalize)
@@ -419,13 +440,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void n
             d2 = fma(dd, dd, d2);
         }
         const int32_t t0 = __builtin_amdgcn_readfirstlane(ts);
-        if (__ballot(1) == ~0ull && __ballot(ts != t0) == 0) {  // full wave, one slot: one atomic
+        const bool one = __ballot(1) == ~0ull && __ballot(ts != t0) == 0;  // full wave, one slot
+        if (one) {
 #pragma unroll
             for (int o = 32; o > 0; o >>= 1) d2 = fmax(d2, __shfl_xor(d2, o));
-            if ((threadIdx.x & 63) == 0)
-                atomicMax(reinterpret_cast<unsigned long long *>(A.r2 + t0), (unsigned long long)__double_as_longlong(d2));
         } else {
             atomicMax(reinterpret_cast<unsigned long long *>(A.r2 + ts), (unsigned long long)__double_as_longlong(d2));
+        }
+        if ((threadIdx.x & 63) == (__ffsll((unsigned long long)__ballot(1)) - 1)) {  // the wave's record
+            WaveR2 w;
+            w.d2 = one ? d2 : 0.0;
+            w.slot = one ? t0 : -1;
+            w.pad = 0;
+            A.wr2[(p - A.p0) >> 6] = w;
         }
     }
     // items leaving their cluster, counted per wave (drives the re-sort of the layout)
@@ -630,19 +657,18 @@ __device__ int block_excl_scan(int v, int *sh /* >= 16 ints */, int *total) {
 // -kSkip by a margin of 2 nats plus 1e-9 of the terms' magnitude (rounding of the kernel's own
 // arithmetic is ~1e-15 relative).  Non-isotropic rows and singletons (own weight 0) keep every row.
 // One wave builds one row's list (ascending j) and clears the row's radius for the next sweep.
-constexpr int kPruneFusedMaxK = 512;
 constexpr int kPruneBlocks = 32;  // np8_prune grid: 128 rows per pass
 
 // DT > 0: the dimension as a template constant (loops unrolled, the row loads issued together)
 template <int DT = 0>
-__device__ void prune_row(const double *__restrict__ cand, double *__restrict__ r2, int32_t *__restrict__ plist,
-                          int32_t *__restrict__ plen, int ls, int Drt, int K, int k0) {
+__device__ void prune_row(const double *__restrict__ cand, double *__restrict__ r2, const double *__restrict__ lr2,
+                          int32_t *__restrict__ plist, int32_t *__restrict__ plen, int ls, int Drt, int K, int k0) {
     const int D = DT > 0 ? DT : Drt;
     const int DP = D * (D + 1) / 2, CS = cand_stride(D), F = D + DP;
     const int lane = threadIdx.x & 63;
     const double *e0 = cand + (int64_t)k0 * CS;
     const int slot0 = (int)e0[F + kFieldSlot];
-    const double R2 = r2[slot0];
+    const double R2 = fmax(r2[slot0], lr2[slot0]);  // atomics of mixed waves, records of one-slot waves
     const double iso0 = e0[F + kFieldIso];
     const double base0 = e0[F + kFieldC] + e0[F + kFieldLogn1];
     const bool prunable = iso0 > 0.0 && R2 < 1e300 && base0 > -1e299;
@@ -971,14 +997,6 @@ __global__ __launch_bounds__(kFinThreads) void np8_finalize(FinArgs F) {
         F.ctl->K = nlive;
         F.ctl->cand_fresh = 1;
         F.ctl->n_pend = (F.prior == kPriorNiw) ? A : 0;
-    }
-    if (F.prune) {  // candidate lists for the next sweep, one wave per row (block-uniform branch)
-        __syncthreads();
-        if (nlive <= kPruneFusedMaxK) {
-            for (int k0 = tid >> 6; k0 < nlive; k0 += kFinThreads / 64)
-                prune_row(F.cand, F.r2, F.plist, F.plen, F.ls, D, nlive, k0);
-        }
-        if (tid == 0) F.ctl->lists_ok = (nlive <= kPruneFusedMaxK) ? 1 : 0;
     }
     // clear the local record for the next step (all reads of it are behind the barriers above)
     if (F.local_rec) {
@@ -1347,6 +1365,30 @@ hipError_t np8_launch_assign(const AssignArgs &A, int D, int M, int prior, hipSt
     return hipErrorInvalidValue;
 }
 
+// The draw exactly as np8_assign runs it: state at candidate 0 (the item's own cluster), then pick_step over
+// candidates 1..n-1 in order (skip rule included).
+__global__ __launch_bounds__(256) void np8_pick_batch(const double *__restrict__ lw, int32_t n,
+                                                      const double *__restrict__ u, int64_t n_draws,
+                                                      int32_t *__restrict__ out) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n_draws) return;
+    PickState st;
+    st.T = lw[0];
+    st.S = 1.0;
+    st.u = u[k];
+    st.pick = 0;
+    for (int32_t j = 1; j < n; ++j) pick_step(st, lw[j], j);
+    out[k] = st.pick;
+}
+
+hipError_t np8_launch_pick_batch(const double *lw, int32_t n, const double *u, int64_t n_draws, int32_t *out,
+                                 hipStream_t s) {
+    if (n_draws <= 0) return hipSuccess;
+    hipLaunchKernelGGL(np8_pick_batch, dim3((unsigned)((n_draws + 255) / 256)), dim3(256), 0, s, lw, n, u, n_draws,
+                       out);
+    return hipGetLastError();
+}
+
 hipError_t np8_launch_loglik_matrix(const AssignArgs &A, int D, int M, int prior, const int64_t *idx, int64_t n,
                                     double *out, hipStream_t s) {
     if (n <= 0) return hipSuccess;
@@ -1446,12 +1488,36 @@ hipError_t np8_launch_mh_g0(const ParamArgs &A, hipStream_t s) {
 // Standalone pass (after the mh_g0 update has moved means): four rows per block.
 // A small grid strides over the live rows (one wave per row): K is only known on the device, and a
 // grid sized for kcap would mostly launch blocks that exit at once.
+// Every block first folds the sweep's per-wave radius records into an LDS table (each thread walks a
+// contiguous run of records and flushes its running maximum when the slot changes: in the label-sorted
+// layout consecutive waves share their slot, so a run costs one or two LDS atomics).
 template <int DT>
 __global__ __launch_bounds__(256) void np8_prune(PruneArgs A) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    unsigned long long *lr2 = reinterpret_cast<unsigned long long *>(smem);
     const int K = A.ctl->K;
     if (blockIdx.x == 0 && threadIdx.x == 0) A.ctl->lists_ok = 1;
+    for (int s = threadIdx.x; s < A.kcap; s += blockDim.x) lr2[s] = 0ull;
+    __syncthreads();
+    const int64_t per = (A.n_waves + blockDim.x - 1) / blockDim.x;
+    const int64_t w0 = (int64_t)threadIdx.x * per, w1 = (w0 + per < A.n_waves) ? w0 + per : A.n_waves;
+    int32_t cs = -1;
+    unsigned long long cm = 0ull;
+    for (int64_t w = w0; w < w1; ++w) {
+        const WaveR2 r = A.wr2[w];
+        if (r.slot != cs) {
+            if (cs >= 0) atomicMax(&lr2[cs], cm);
+            cs = r.slot;
+            cm = 0ull;
+        }
+        // non-negative doubles order like their bit patterns
+        const unsigned long long b = (unsigned long long)__double_as_longlong(r.d2);
+        cm = b > cm ? b : cm;
+    }
+    if (cs >= 0) atomicMax(&lr2[cs], cm);
+    __syncthreads();
     for (int k0 = blockIdx.x * 4 + (threadIdx.x >> 6); k0 < K; k0 += gridDim.x * 4)  // wave-uniform
-        prune_row<DT>(A.cand, A.r2, A.plist, A.plen, A.ls, A.D, K, k0);
+        prune_row<DT>(A.cand, A.r2, reinterpret_cast<const double *>(lr2), A.plist, A.plen, A.ls, A.D, K, k0);
 }
 
 __global__ void np8_advance_epoch(Ctl *ctl, uint32_t n) { ctl->t_base += n; }
@@ -1462,7 +1528,7 @@ hipError_t np8_launch_prune(const PruneArgs &A, int kcap, hipStream_t s) {
     switch (A.D) {
 #define Y(d)                                                              \
     case d:                                                               \
-        hipLaunchKernelGGL((np8_prune<d>), g, dim3(256), 0, s, A);        \
+        hipLaunchKernelGGL((np8_prune<d>), g, dim3(256), sizeof(double) * A.kcap, s, A); \
         break;
         Y(1) Y(2) Y(3) Y(4) Y(8) Y(16)
 #undef Y

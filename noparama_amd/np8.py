@@ -16,7 +16,7 @@ import re
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libnp8.so")
+LIB_PATH = os.environ.get("NP8_LIB_OVERRIDE") or os.path.join(_HERE, "lib", "libnp8.so")  # override: A/B experiments
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "np8.h")
 
 NP8_OK = 0
@@ -138,6 +138,7 @@ def lib():
         "np8_get_state": ([vp, i32, vp, vp, vp, vp, vp], i32),
         "np8_loglik_matrix": ([vp, vp, i64, vp], i32),
         "np8_total_loglik": ([vp, P(d)], i32),
+        "np8_pick_batch": ([vp, vp, i32, vp, i64, vp], i32),
         "np8_stats": ([vp, P(Stats)], i32),
         "np8_set_timing": ([vp, i32], i32),
         "np8_set_stream": ([vp, vp], i32),
@@ -322,6 +323,15 @@ class NealAlgorithm8:
         K = self.K
         out = np.zeros((idx.size, K + self.M))
         self._check(lib().np8_loglik_matrix(self._h, _p(idx), idx.size, _p(out)))
+        return out
+
+    def pick_batch(self, lw, u):
+        """Parity/debug: the sweep's categorical draw over log-weights lw (candidate 0 = the own cluster),
+        one draw per uniform in u (np8_pick_batch)."""
+        lw = np.ascontiguousarray(lw, dtype=np.float64)
+        u = np.ascontiguousarray(u, dtype=np.float64)
+        out = np.zeros(u.size, dtype=np.int32)
+        self._check(lib().np8_pick_batch(self._h, _p(lw), lw.size, _p(u), u.size, _p(out)))
         return out
 
     def total_loglik(self):

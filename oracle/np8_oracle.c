@@ -477,6 +477,7 @@ static int niw_prepare(np8o_ctx *c) {
 
 np8o_ctx *np8o_create(const np8o_config *cfg) {
     if (cfg->D < 1 || cfg->D > NP8O_DMAX || cfg->M < 1 || cfg->M > NP8O_MMAX || cfg->kcap < 1) return NULL;
+    if (cfg->pick != NP8O_PICK_RESERVOIR && (cfg->pick != NP8O_PICK_INVCDF || cfg->kcap > NP8O_KCAP_PICK)) return NULL;
     if (cfg->param_update < NP8O_PARAM_FROZEN || cfg->param_update > NP8O_PARAM_NIW_CONJUGATE || cfg->mh_steps < 0)
         return NULL;
     if (cfg->prior != NP8O_PRIOR_REFERENCE && cfg->prior != NP8O_PRIOR_NIW) return NULL;
@@ -1390,9 +1391,49 @@ static inline void pick_step(pick_state *st, double lw, int32_t j) {
  * the reference deletes on retract, membertrix.cpp:200-203), then every other live cluster in
  * ascending slot order (weight n_k), then the M auxiliaries (weight alpha/M).  Returns the candidate
  * row (< K existing, >= K auxiliary). */
+int64_t np8o_pick_reservoir(const double *lw, int64_t n, double u) {
+    if (n <= 0) return 0;
+    pick_state st = {lw[0], 1.0, u, 0};
+    for (int64_t j = 1; j < n; ++j) pick_step(&st, lw[j], (int32_t)j);
+    return st.pick;
+}
+
+void np8o_pick_reservoir_batch(const double *lw, int64_t n, const double *u, int64_t n_draws, int32_t *out) {
+    for (int64_t k = 0; k < n_draws; ++k) out[k] = (int32_t)np8o_pick_reservoir(lw, n, u[k]);
+}
+
+/* NP8O_PICK_INVCDF: the reference's inverse-CDF rule over exp(lw - max), candidates in the order
+ * choose() visits them (own, other live slots ascending, auxiliaries); returns the candidate row. */
+static int32_t choose_invcdf(const np8o_ctx *c, int64_t key, const double *x, int32_t jo) {
+    const int K = c->K, M = c->M;
+    double lw[NP8O_KCAP_PICK + NP8O_MMAX];
+    int32_t row[NP8O_KCAP_PICK + NP8O_MMAX];
+    int n = 0;
+    lw[n] = cand_ll(c, x, jo, jo) + c->logn1[jo];
+    row[n++] = jo;
+    for (int j = 0; j < K; ++j) {
+        if (j == jo) continue;
+        lw[n] = cand_ll(c, x, jo, j) + c->logn[j];
+        row[n++] = j;
+    }
+    double lla[NP8O_MMAX];
+    aux_ll(c, x, (uint64_t)key, c->t, lla);
+    for (int m = 0; m < M; ++m) {
+        lw[n] = lla[m] + c->logam;
+        row[n++] = K + m;
+    }
+    double mx = lw[0];
+    for (int j = 1; j < n; ++j) mx = fmax(mx, lw[j]);
+    double w[NP8O_KCAP_PICK + NP8O_MMAX];
+    for (int j = 0; j < n; ++j) w[j] = exp(lw[j] - mx);
+    const double u = np8o_uniform(c->cfg.seed, (uint64_t)key, c->t, NP8O_STREAM_PICK, 0);
+    return row[np8o_weighted_pick_ref(w, n, u)];
+}
+
 static int32_t choose(const np8o_ctx *c, int64_t key, const double *x, int32_t zi) {
     const int K = c->K, M = c->M;
     const int jo = c->dense_of[zi];
+    if (c->cfg.pick == NP8O_PICK_INVCDF) return choose_invcdf(c, key, x, jo);
     pick_state st;
     st.T = cand_ll(c, x, jo, jo) + c->logn1[jo];
     st.S = 1.0;

@@ -35,6 +35,7 @@ extern "C" {
 
 #define NP8O_DMAX 64
 #define NP8O_MMAX 8
+#define NP8O_KCAP_PICK 4096 /* kcap limit of NP8O_PICK_INVCDF (the weights of one update live on the stack) */
 #define NP8O_REQMAX 4096 /* upper bound of req_max (must match NP8_REQ_MAX) */
 #define NP8O_REQ_DEFAULT 1024 /* default req_max (must match NP8_REQ_DEFAULT) */
 /* Item keys: the Philox item counter of a draw is key = item | (visit << 32), visit = how many times
@@ -91,6 +92,12 @@ double np8o_mvn_probability_ref(const double *x, const double *mu, const double 
 double np8o_mvn_logprobability_ref(const double *x, const double *mu, const double *Sigma, int D);
 /* dim1algebra.hpp:2078-2104 with the uniform u supplied by the caller. */
 int64_t np8o_weighted_pick_ref(const double *w, int64_t n, double u);
+/* The specification's reservoir pick (DESIGN.md "Pick") over log-weights lw[0..n) with uniform u:
+ * the state starts at candidate 0 (T = lw[0], S = 1), then candidates 1..n-1 in order, skip rule
+ * included.  Exactly what a point update runs (candidate 0 = the item's own cluster). */
+int64_t np8o_pick_reservoir(const double *lw, int64_t n, double u);
+/* Batch form: out[k] = np8o_pick_reservoir(lw, n, u[k]) for k < n_draws. */
+void np8o_pick_reservoir_batch(const double *lw, int64_t n, const double *u, int64_t n_draws, int32_t *out);
 /* LU with partial pivoting (Eigen PartialPivLU): inverse (row-major) and determinant. 0 = ok. */
 int np8o_lu_inverse_det(const double *A, int D, double *inv, double *det);
 /* clustering_performance.cpp:14-82 in int64/double: out = {purity, rand_index, adjusted_rand_index}. */
@@ -113,7 +120,15 @@ typedef struct {
     int32_t prior;        /* NP8O_PRIOR_* */
     int32_t contraction;  /* NP8O_CONTRACT_*: arithmetic of the cluster likelihoods */
     int32_t req_max;      /* new clusters one step may create (0 -> NP8O_REQ_DEFAULT, <= NP8O_REQMAX) */
+    int32_t pick;         /* NP8O_PICK_*: the categorical draw of a point update */
 } np8o_config;
+
+/* Categorical draw of a point update.
+ *   RESERVOIR: the specification (DESIGN.md "Pick"), what the HIP path runs.
+ *   INVCDF:    the reference's own rule (dim1algebra.hpp:2078-2104: cumulative sum of linear weights,
+ *              lower_bound of u * total) over w_j = exp(lw_j - max lw) in the candidate order, with the
+ *              same uniform -- an independent sampler to compare chains with in distribution. */
+enum { NP8O_PICK_RESERVOIR = 0, NP8O_PICK_INVCDF = 1 };
 
 /* Cluster-likelihood arithmetic (DESIGN.md "Wide path").
  *   F64: fp64 table form, packed sym(Sigma^{-1}) (D <= 16 on the device).

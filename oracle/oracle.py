@@ -36,12 +36,14 @@ class _Config(C.Structure):
         ("prior", C.c_int32),
         ("contraction", C.c_int32),
         ("req_max", C.c_int32),
+        ("pick", C.c_int32),
     ]
 
 
 PARAM_UPDATE = {"frozen": 0, "mh_g0": 1, "niw_conjugate": 2}
 PRIOR = {"reference": 0, "niw": 1}
 CONTRACTION = {"f64": 0, "f32": 1}
+PICK = {"reservoir": 0, "invcdf": 1}
 
 
 def build() -> None:
@@ -75,6 +77,9 @@ def lib():
         L.np8o_mvn_logprobability_ref.restype = d
         L.np8o_weighted_pick_ref.argtypes = [vp, i64, d]
         L.np8o_weighted_pick_ref.restype = i64
+        L.np8o_pick_reservoir.argtypes = [vp, i64, d]
+        L.np8o_pick_reservoir.restype = i64
+        L.np8o_pick_reservoir_batch.argtypes = [vp, i64, vp, i64, vp]
         L.np8o_lu_inverse_det.argtypes = [vp, C.c_int, vp, vp]
         L.np8o_similarity.argtypes = [vp, vp, i64, vp]
         L.np8o_create.argtypes = [P(_Config)]
@@ -178,6 +183,21 @@ def weighted_pick_ref(w, u):
     return int(lib().np8o_weighted_pick_ref(_p(w), w.size, float(u)))
 
 
+def pick_reservoir(lw, u):
+    """The specification's reservoir pick over log-weights lw (candidate 0 first) with uniform u."""
+    lw = np.ascontiguousarray(lw, dtype=np.float64)
+    return int(lib().np8o_pick_reservoir(_p(lw), lw.size, float(u)))
+
+
+def pick_reservoir_batch(lw, u):
+    """pick_reservoir(lw, u_k) for every uniform u_k (int32 array)."""
+    lw = np.ascontiguousarray(lw, dtype=np.float64)
+    u = np.ascontiguousarray(u, dtype=np.float64)
+    out = np.zeros(u.size, dtype=np.int32)
+    lib().np8o_pick_reservoir_batch(_p(lw), lw.size, _p(u), u.size, _p(out))
+    return out
+
+
 def set_threads(n):
     """OpenMP threads of the oracle's synchronous step (the cpu_par baseline); results unchanged."""
     lib().np8o_set_threads(int(n))
@@ -207,9 +227,10 @@ class Chain:
 
     def __init__(self, D, M=3, alpha=1.0, mu0=None, kappa=1.0 / 500, nu=4.0, Lambda=None, seed=0,
                  kcap=4096, chunk=0, param_update="frozen", mh_steps=20, prior="reference", contraction="f64",
-                 req_max=0):
+                 req_max=0, pick="reservoir"):
         cfg = _Config()
         cfg.req_max = req_max
+        cfg.pick = PICK[pick]
         cfg.contraction = CONTRACTION[contraction]
         cfg.param_update = PARAM_UPDATE[param_update]
         cfg.prior = PRIOR[prior]
