@@ -2,6 +2,7 @@
 #include "np_host.h"
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <fstream>
@@ -38,6 +39,8 @@ membertrix &membertrix::operator=(const membertrix &other) {
         ++k;
     }
     _next_id = k;
+    _generation = other._generation;
+    _relabels = other._relabels;
     _z.resize(other._z.size());
     for (size_t i = 0; i < _z.size(); ++i) _z[i] = other._z[i] < 0 ? -1 : remap[other._z[i]];
     return *this;
@@ -98,8 +101,48 @@ int membertrix::cleanup() {
 }
 
 void membertrix::relabel() {
+    std::map<cluster_id_t, cluster_id_t> remap;  // the copy's renumbering: live ids ascending -> 0..K-1
+    cluster_id_t k = 0;
+    for (const auto &kv : std::map<cluster_id_t, cluster_t *>(_clusters.begin(), _clusters.end()))
+        if (count(kv.first) > 0) remap[kv.first] = k++;
+    const int gen = _generation + 1;
+    auto relabels = _relabels;
     membertrix tmp(*this);
     *this = tmp;
+    _relabels = relabels;
+    _generation = gen;
+    _relabels.emplace_back(gen, remap);
+}
+
+std::vector<std::pair<int, std::map<cluster_id_t, cluster_id_t>>> membertrix::relabelsSince(int generation) const {
+    std::vector<std::pair<int, std::map<cluster_id_t, cluster_id_t>>> out;
+    for (const auto &r : _relabels)
+        if (r.first > generation) out.push_back(r);
+    return out;
+}
+
+void membertrix::clearClusters() {
+    clear_clusters();
+    std::fill(_z.begin(), _z.end(), -1);
+}
+
+void membertrix::dense(std::vector<int32_t> &z, std::vector<int64_t> &counts, std::vector<double> &mu,
+                       std::vector<double> &sigma) const {
+    std::map<cluster_id_t, int32_t> lab;
+    for (const auto &kv : _clusters) lab[kv.first] = 0;
+    int32_t k = 0;
+    for (auto &kv : lab) kv.second = k++;
+    z.resize(_z.size());
+    for (size_t i = 0; i < _z.size(); ++i) z[i] = _z[i] < 0 ? -1 : lab.at(_z[i]);
+    counts.assign((size_t)k, 0);
+    mu.clear();
+    sigma.clear();
+    for (const auto &kv : lab) {
+        counts[(size_t)kv.second] = (int64_t)count(kv.first);
+        const cluster_t *c = _clusters.at(kv.first);
+        mu.insert(mu.end(), c->mu.begin(), c->mu.end());
+        sigma.insert(sigma.end(), c->sigma.begin(), c->sigma.end());
+    }
 }
 
 void membertrix::setState(const std::vector<int32_t> &z, const std::vector<cluster_t> &clusters) {
@@ -142,6 +185,25 @@ NealAlgorithm8Hip::NealAlgorithm8Hip(uint64_t seed, const np8_prior &prior, int6
     check(np8_create(&_ctx, &cfg), "np8_create");
 }
 
+namespace {
+np8_prior prior_of(const multivariate_normal_distribution &likelihood, const dirichlet_process &dp) {
+    np8_prior p;
+    p.D = (int)dp.base.mu0.size();
+    p.alpha = dp.alpha;
+    p.mu0 = dp.base.mu0;
+    p.kappa = dp.base.kappa;
+    p.nu = dp.base.nu;
+    p.Lambda = dp.base.Lambda;
+    p.prior = dp.base.prior;
+    p.contraction = likelihood.contraction;
+    return p;
+}
+}  // namespace
+
+NealAlgorithm8Hip::NealAlgorithm8Hip(random_engine_t &generator, const multivariate_normal_distribution &likelihood,
+                                     const dirichlet_process &nonparametrics, int64_t chunk, int device, int kcap)
+    : NealAlgorithm8Hip((uint64_t)generator(), prior_of(likelihood, nonparametrics), chunk, device, kcap) {}
+
 NealAlgorithm8Hip::~NealAlgorithm8Hip() { np8_destroy(_ctx); }
 
 void NealAlgorithm8Hip::check(int r, const char *what) {
@@ -177,17 +239,64 @@ void NealAlgorithm8Hip::setState(const membertrix &trix) {
 
 void NealAlgorithm8Hip::sweep(int n) { check(np8_sweep(_ctx, n), "np8_sweep"); }
 
-// UpdateClusterPopulation::update: a whole permutation = one data-parallel sweep (the MCMC driver
-// passes it once per sweep because sweepGranular() is true); otherwise the listed items are updated
-// sequentially with the reference's per-point semantics.
+// UpdateClusterPopulation::update: all items = one population sweep (the MCMC driver passes them once
+// per sweep because sweepGranular() is true); otherwise the listed items are updated sequentially with
+// the reference's per-point semantics.  Then the membertrix is patched from the change log.
 void NealAlgorithm8Hip::update(membertrix &cluster_matrix, const data_ids_t &data_ids) {
-    (void)cluster_matrix;  // the device owns the state; import with exportState()
     if ((int64_t)data_ids.size() == _N) {
-        check(np8_sweep(_ctx, 1), "np8_sweep");
-        return;
+        check(np8_population_sweep(_ctx), "np8_population_sweep");
+    } else {
+        std::vector<int64_t> ids(data_ids.begin(), data_ids.end());
+        check(np8_update_points(_ctx, ids.data(), (int64_t)ids.size()), "np8_update_points");
     }
-    std::vector<int64_t> ids(data_ids.begin(), data_ids.end());
-    check(np8_update_points(_ctx, ids.data(), (int64_t)ids.size()), "np8_update_points");
+    patch(cluster_matrix);
+}
+
+void NealAlgorithm8Hip::endSweep(membertrix &cluster_matrix) {
+    check(np8_end_sweep(_ctx), "np8_end_sweep");
+    patch(cluster_matrix);
+}
+
+// The change log applied to the membertrix: new clusters first (membertrix::addCluster), then the moved
+// items (retract without auto-remove, assign), then the emptied clusters (remove) and new parameters.
+void NealAlgorithm8Hip::patch(membertrix &trix) {
+    const int D = _prior.D;
+    if (_tracked != &trix) {  // first contact: the whole state, from an empty baseline
+        check(np8_track_changes(_ctx, NP8_CHANGES_FROM_EMPTY), "np8_track_changes");
+        trix.clearClusters();
+        _tracked = &trix;
+        _slot_id.clear();
+        _gen = trix.generation();
+    }
+    for (const auto &r : trix.relabelsSince(_gen)) {  // relabel() renamed the clusters meanwhile
+        for (auto &kv : _slot_id) kv.second = r.second.at(kv.second);
+        _gen = r.first;
+    }
+    std::vector<int64_t> item((size_t)std::max<int64_t>(_N, 1));
+    std::vector<int32_t> slot(item.size()), created((size_t)_kcap), removed((size_t)_kcap), updated((size_t)_kcap);
+    std::vector<double> mu((size_t)_kcap * D), sg((size_t)_kcap * D * D);
+    np8_changes_t ch{};
+    check(np8_changes(_ctx, (int64_t)item.size(), item.data(), slot.data(), created.data(), removed.data(),
+                      updated.data(), mu.data(), sg.data(), &ch),
+          "np8_changes");
+    auto params = [&](int q) {
+        cluster_t c;
+        c.mu.assign(mu.begin() + (size_t)q * D, mu.begin() + (size_t)(q + 1) * D);
+        c.sigma.assign(sg.begin() + (size_t)q * D * D, sg.begin() + (size_t)(q + 1) * D * D);
+        return c;
+    };
+    for (int q = 0; q < ch.n_created; ++q) _slot_id[created[q]] = trix.addCluster(new cluster_t(params(q)));
+    for (int q = 0; q < ch.n_updated; ++q) trix.setCluster(_slot_id.at(updated[q]), params(ch.n_created + q));
+    for (int64_t k = 0; k < ch.n_moved; ++k) {
+        const data_id_t i = (data_id_t)item[k];
+        if (trix.assigned(i)) trix.retract(i, false);
+        trix.assign(_slot_id.at(slot[k]), i);
+    }
+    for (int q = 0; q < ch.n_removed; ++q) {
+        const np_error_t e = trix.remove(_slot_id.at(removed[q]));
+        if (e != error_none) throw std::runtime_error("patch: an emptied cluster still has items");
+        _slot_id.erase(removed[q]);
+    }
 }
 
 void NealAlgorithm8Hip::exportState(membertrix &trix, int which) {
@@ -221,12 +330,13 @@ void NealAlgorithm8Hip::printStatistics() {
 }
 
 // A whole permutation = one split-merge sweep (N attempts on the library's two scan permutations,
-// np_mcmc.cpp:117-164 with subset_count = 2).  The reference's per-pair call has no sweep-parallel form.
+// np_mcmc.cpp:117-164 with subset_count = 2), the end-of-sweep step included.  The reference's per-pair
+// call has no sweep-parallel form.
 void JainNealAlgorithmHip::update(membertrix &cluster_matrix, const data_ids_t &data_ids) {
-    (void)cluster_matrix;
     if ((int64_t)data_ids.size() != numItems())
         throw std::runtime_error("JainNealAlgorithmHip::update: pass all items (one split-merge sweep)");
-    if (np8_sm_sweep(ctx(), 1) != NP8_OK) throw std::runtime_error(std::string("np8_sm_sweep: ") + np8_last_error(ctx()));
+    check(np8_sm_sweep(ctx(), 1), "np8_sm_sweep");
+    patch(cluster_matrix);
 }
 
 // The reference's statistics (np_jain_neal_algorithm.cpp:505-530).
@@ -243,10 +353,10 @@ void JainNealAlgorithmHip::printStatistics() {
 
 // A whole permutation = one triadic split-merge sweep (N attempts on item triples, subset_count = 3).
 void TriadicAlgorithmHip::update(membertrix &cluster_matrix, const data_ids_t &data_ids) {
-    (void)cluster_matrix;
     if ((int64_t)data_ids.size() != numItems())
         throw std::runtime_error("TriadicAlgorithmHip::update: pass all items (one split-merge sweep)");
-    if (np8_tri_sweep(ctx(), 1) != NP8_OK) throw std::runtime_error(std::string("np8_tri_sweep: ") + np8_last_error(ctx()));
+    check(np8_tri_sweep(ctx(), 1), "np8_tri_sweep");
+    patch(cluster_matrix);
 }
 
 // The reference's statistics (np_triadic_algorithm.cpp:797-832): merge 2 -> 1, split 1 -> 2,
@@ -264,33 +374,132 @@ void TriadicAlgorithmHip::printStatistics() {
 }
 
 // ---- MCMC ----------------------------------------------------------------------------------------
-MCMC::MCMC(NealAlgorithm8Hip &sampler, int k_init) : _sampler(sampler), _k_init(k_init) {}
+MCMC::MCMC(NealAlgorithm8Hip &sampler, int k_init)
+    : _sampler(sampler), _update_clusters(sampler), _k_init(k_init),
+      _max_likelihood(-std::numeric_limits<double>::infinity()) {}
 
 void MCMC::run(dataset_t &dataset, int T) {
-    for (auto *d : dataset) {
-        _membertrix.addData(*d);
-        _max_likelihood_membertrix.addData(*d);
-    }
+    const int N = (int)dataset.size();
+    for (auto *d : dataset) _membertrix.addData(*d);  // np_mcmc.cpp:57-62
     _sampler.setData(dataset);
+    // np_mcmc.cpp:64-92: K_init G0 clusters, uniform assignment, cleanup (on the device), loaded whole
     _sampler.initRandom(_k_init);
-    data_ids_t all(dataset.size());
+    _sampler.patch(_membertrix);
+    const int number_mh_steps = 20;  // np_mcmc.cpp:54
+    const int cycle_print = 10, cycle_max_likelihood = 5;
+    data_ids_t all((size_t)N);
     std::iota(all.begin(), all.end(), 0);
     for (int t = 0; t < T; ++t) {
-        // relabel every 10 sweeps (np_mcmc.cpp:111-114) has no effect on the device state (slots are
-        // reused in ascending order); the permutation of np_mcmc.cpp:120-125 is the device's.
+        const auto t0 = std::chrono::steady_clock::now();
+        const np8_stats_t s0 = _sampler.stats();
+        if (t % cycle_print == 0) _membertrix.relabel();  // np_mcmc.cpp:111-114
+        // np_mcmc.cpp:117-164: every item once; the scan order (random_order) is the device's permutation
         if (_sampler.sweepGranular()) {
             _sampler.update(_membertrix, all);
         } else {
             for (data_id_t i : all) _sampler.update(_membertrix, {i});
         }
+        if (_verify) verify(t, "population update");
+        _update_clusters.update(_membertrix, number_mh_steps);  // np_mcmc.cpp:170
+        if (_verify) verify(t, "cluster update");
+        if (t % cycle_max_likelihood == 0) considerMaxLikelihood(t);  // np_mcmc.cpp:172-174
+        if (_log) {
+            const np8_stats_t s1 = _sampler.stats();
+            const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+            *_log << "{\"sweep\": " << t << ", \"K\": " << s1.K << ", \"new_clusters\": " << s1.new_clusters - s0.new_clusters
+                  << ", \"deferred_requests\": " << s1.rejected_requests - s0.rejected_requests
+                  << ", \"existing_picks\": " << s1.existing_picks - s0.existing_picks;
+            if (t % cycle_max_likelihood == 0) *_log << ", \"loglik\": " << s1.last_loglik;
+            *_log << ", \"ms\": " << ms << "}" << std::endl;
+        }
     }
-    _sampler.exportState(_membertrix, 0);
+}
+
+// np_mcmc.cpp:187-203: the log-likelihood of the membertrix's state is the device's check of this sweep
+// (np8_end_sweep ran it on the same state); an improvement clones the membertrix.
+void MCMC::considerMaxLikelihood(int t) {
+    (void)t;
+    const double L = _sampler.stats().last_loglik;
+    if (L > _max_likelihood) {
+        _max_likelihood = L;
+        _max_likelihood_membertrix = _membertrix;
+    }
+}
+
+namespace {
+// Clusters renamed in order of their first item (ids are names: creation order and relabel() on the host,
+// slots on the device); counts and parameters permuted alike.
+void canonicalize(std::vector<int32_t> &z, std::vector<int64_t> &cnt, std::vector<double> &mu, std::vector<double> &sg,
+                  int K, int D) {
+    std::vector<int32_t> lut((size_t)K, -1), perm;
+    for (int32_t &l : z) {
+        if (lut[(size_t)l] < 0) {
+            lut[(size_t)l] = (int32_t)perm.size();
+            perm.push_back(l);
+        }
+        l = lut[(size_t)l];
+    }
+    std::vector<int64_t> c2(perm.size());
+    std::vector<double> m2(perm.size() * D), s2(perm.size() * D * D);
+    for (size_t k = 0; k < perm.size(); ++k) {
+        c2[k] = cnt[(size_t)perm[k]];
+        std::copy(mu.begin() + (size_t)perm[k] * D, mu.begin() + (size_t)(perm[k] + 1) * D, m2.begin() + k * D);
+        std::copy(sg.begin() + (size_t)perm[k] * D * D, sg.begin() + (size_t)(perm[k] + 1) * D * D, s2.begin() + k * D * D);
+    }
+    cnt.swap(c2);
+    mu.swap(m2);
+    sg.swap(s2);
+}
+}  // namespace
+
+void MCMC::verify(int t, const char *where) {
+    np8_ctx *c = _sampler.ctx();
+    const int64_t N = _sampler.numItems();
+    std::vector<int32_t> z((size_t)N), zd;
+    int32_t K = 0;
+    const size_t kc = (size_t)_sampler.kcap();
+    const int D = (int)(_membertrix.count() ? _membertrix.getDatum(0)->size() : 0);
+    std::vector<double> mu(kc * D), sg(kc * D * D), mud, sgd;
+    std::vector<int64_t> cnt(kc), cntd;
+    if (np8_sync(c) != NP8_OK || np8_get_state(c, 0, z.data(), &K, mu.data(), sg.data(), cnt.data()) != NP8_OK)
+        throw std::runtime_error(std::string("verify: np8_get_state: ") + np8_last_error(c));
+    _membertrix.dense(zd, cntd, mud, sgd);
+    bool ok = (int)cntd.size() == K;
+    if (ok) {
+        cnt.resize((size_t)K);
+        mu.resize((size_t)K * D);
+        sg.resize((size_t)K * D * D);
+        canonicalize(z, cnt, mu, sg, K, D);
+        canonicalize(zd, cntd, mud, sgd, K, D);
+        ok = zd == z && cntd == cnt && mud == mu && sgd == sg;
+    }
+    if (!ok)
+        throw std::runtime_error("verify: membertrix differs from the device state after the " + std::string(where) +
+                                 " of sweep " + std::to_string(t));
 }
 
 const membertrix &MCMC::getMembershipMatrix() { return _membertrix; }
 
 const membertrix &MCMC::getMaxLikelihoodMatrix() {
-    _sampler.exportState(_max_likelihood_membertrix, 1);
+    if (_verify) {  // the host's clone equals the device's own snapshot (np8_get_state(which = 1))
+        np8_ctx *c = _sampler.ctx();
+        std::vector<int32_t> z((size_t)_sampler.numItems()), zd;
+        int32_t K = 0;
+        std::vector<int64_t> cntd;
+        std::vector<double> mud, sgd;
+        if (np8_get_state(c, 1, z.data(), &K, nullptr, nullptr, nullptr) != NP8_OK)
+            throw std::runtime_error(std::string("verify: np8_get_state(1): ") + np8_last_error(c));
+        _max_likelihood_membertrix.dense(zd, cntd, mud, sgd);
+        if ((int)cntd.size() != K) throw std::runtime_error("verify: max-likelihood snapshot differs");
+        std::vector<int64_t> cnt((size_t)K, 0);
+        std::vector<double> mu, sg;
+        for (int32_t l : z) cnt[(size_t)l] += 1;
+        mud.clear();
+        sgd.clear();
+        canonicalize(z, cnt, mu, sg, K, 0);
+        canonicalize(zd, cntd, mud, sgd, K, 0);
+        if (zd != z || cntd != cnt) throw std::runtime_error("verify: max-likelihood snapshot differs");
+    }
     return _max_likelihood_membertrix;
 }
 

@@ -30,7 +30,7 @@ static void usage(const char *p) {
               << " [-C chunk (0 = data-parallel sweep, 1 = sequential)] [-D dims=2] [-w workspace]"
               << " [-u frozen|mh_g0|niw_conjugate (cluster-parameter update)] [-p reference|niw (base measure)]"
               << " [-x f64|f32 (cluster likelihoods; f32 = fp32 matrix cores, D in {32, 64})]"
-              << " [-n subsample size=200, 0 = all items]; data: 'x_1 .. x_D label' text or [N][D+1] .f64"
+              << " [-n subsample size=200, 0 = all items] [-j per-sweep JSONL file] [-V (check the membertrix against the device after every update)]; data: 'x_1 .. x_D label' text or [N][D+1] .f64"
               << std::endl;
 }
 
@@ -90,9 +90,10 @@ int main(int argc, char *argv[]) {
     int T = 2000, D = 2, nsub = 200;
     long long chunk = 0;
     unsigned long long seed = 0;
-    bool seeded = false;
+    bool seeded = false, verify = false;
+    std::string jsonl;
     int tok;
-    while ((tok = getopt(argc, argv, "d:a:T:c:s:C:D:w:u:n:p:x:h?")) != EOF) {
+    while ((tok = getopt(argc, argv, "d:a:T:c:s:C:D:w:u:n:p:x:j:Vh?")) != EOF) {
         switch (tok) {
             case 'd': data = optarg; break;
             case 'a': algo = optarg; break;
@@ -106,6 +107,8 @@ int main(int argc, char *argv[]) {
             case 'n': nsub = std::stoi(optarg); break;
             case 'p': base = optarg; break;
             case 'x': contr = optarg; break;
+            case 'j': jsonl = optarg; break;
+            case 'V': verify = true; break;
             default: usage(argv[0]); return 1;
         }
     }
@@ -172,6 +175,12 @@ int main(int argc, char *argv[]) {
             smp.reset(new NealAlgorithm8Hip(seed, prior, chunk));
         NealAlgorithm8Hip &sampler = *smp;
         MCMC mcmc(sampler);
+        mcmc.setVerify(verify);
+        std::ofstream jf;
+        if (!jsonl.empty()) {
+            jf.open(jsonl);
+            mcmc.setSweepLog(&jf);
+        }
         auto t0 = std::chrono::steady_clock::now();
         mcmc.run(dataset, T);
         double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();

@@ -6,7 +6,7 @@
  *                                   virtual void printStatistics() = 0; }
  *   (reference include/np_update_cluster_population.h:13-44; Neal-8 implementation
  *    src/np_neal_algorithm8.cpp:17-176, constructed in src/np_main.cpp:433-438).
- * A C++ caller wraps it as `NealAlgorithm8Hip : UpdateClusterPopulation` (host/np_neal_algorithm8_hip.h);
+ * A C++ caller wraps it as `NealAlgorithm8Hip : UpdateClusterPopulation` (host/np_host.h);
  * a ctypes caller binds it directly (noparama_amd/np8.py).  Plain pointers and sizes only: the
  * library owns its device memory and copies host buffers in and out.
  *
@@ -184,6 +184,39 @@ int np8_tri_sweep(np8_ctx *ctx, int32_t n_sweeps);
  * merges (3 -> 2), [7]/[8] triadic splits (2 -> 3), [9] splits accepted by the ratio but dropped for want
  * of a free slot. */
 int np8_tri_stats(np8_ctx *ctx, int64_t out[10]);
+
+/* The population update of one sweep alone (np_mcmc.cpp:146-164: every item once, in chunks of `chunk`
+ * against the state frozen at chunk start; chunk 0 = one data-parallel step), without the end-of-sweep
+ * step: np8_sweep(ctx, 1) == np8_population_sweep + np8_end_sweep.  For callers that drive the reference's
+ * MCMC::run loop themselves (UpdateClusters and considerMaxLikelihood on their own membertrix). */
+int np8_population_sweep(np8_ctx *ctx);
+
+/* Membership change log, for callers that keep their own membertrix coherent with the device (the
+ * reference's MCMC::run reads it back every sweep: relabel np_mcmc.cpp:111-114, UpdateClusters :170,
+ * considerMaxLikelihood :172-203; the plug-in mutates it in place, np_neal_algorithm8.cpp:62-64,139-157).
+ * np8_track_changes(ctx, NP8_CHANGES_FROM_NOW) takes the current state as the baseline;
+ * NP8_CHANGES_FROM_EMPTY starts from "no item assigned, no cluster", so the first np8_changes delivers the
+ * whole state; 0 stops tracking.  np8_changes reports what differs from the baseline and makes the
+ * current state the new baseline:
+ *   item[0..n_moved) ascending, slot[..]: items (local indices) whose cluster changed and their new slot;
+ *   created[0..n_created): slots that became live (membertrix::addCluster, membertrix.cpp:87-100);
+ *   removed[0..n_removed): slots that became empty (retract's auto-remove, membertrix.cpp:200-203);
+ *   updated[0..n_updated): slots live before and after whose parameters changed (the parameter update,
+ *   or a slot emptied and re-used in between);
+ *   mu [(n_created + n_updated) * D], Sigma [.. * D * D]: parameters of the created, then updated slots.
+ * Slot ids are stable while a cluster lives: they are the cluster ids of a coherent membertrix.
+ * created/removed/updated need room for kcap entries and mu/Sigma for kcap clusters (either may be NULL).
+ * More moved items than item_cap: NP8_ERR_CAPACITY, out->n_moved set, the baseline unchanged.
+ * Cost: one pass over the labels and the slot tables on the device; transfers O(changes). */
+#define NP8_CHANGES_FROM_NOW 1
+#define NP8_CHANGES_FROM_EMPTY 2
+typedef struct {
+    int64_t n_moved;
+    int32_t n_created, n_removed, n_updated, pad;
+} np8_changes_t;
+int np8_track_changes(np8_ctx *ctx, int32_t mode);
+int np8_changes(np8_ctx *ctx, int64_t item_cap, int64_t *item, int32_t *slot, int32_t *created, int32_t *removed,
+                int32_t *updated, double *mu, double *Sigma, np8_changes_t *out);
 
 /* The reference's per-call granularity: sequential single-point updates of the listed items, in
  * order, at the current epoch (NealAlgorithm8::update with data_ids.size()==1).  Call

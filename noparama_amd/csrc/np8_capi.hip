@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -137,6 +138,14 @@ struct np8_ctx {
     int32_t sm_batch = 1024;
     int32_t sm_K = 0;
     bool sm_all_iso = false;
+    // membership change log (np8_track_changes / np8_changes): the baseline state and the output staging
+    int track = 0;
+    int32_t *z_base = nullptr, *cnt_base = nullptr, *chg_slot = nullptr;
+    double *mu_base = nullptr, *sigma_base = nullptr;
+    int64_t *chg_item = nullptr;
+    int64_t chg_cap = 0;
+    unsigned long long *chg_count = nullptr;
+    uint8_t *chg_flags = nullptr;
     std::string err;
 };
 
@@ -375,7 +384,8 @@ void free_device(np8_ctx *c) {
                     c->partial, c->dense_of, c->Xs[0], c->Xs[1], c->zs[0], c->zs[1], c->ids[0], c->ids[1],
                     c->s_hist, c->s_cursor, c->s_off, c->slot_iso, c->acc, c->r2, c->wr2, c->plist, c->plen,
                     c->sm_hist, c->sm_mem, c->sm_off, c->sm_live, c->sm_Xm, c->sm_ownm, c->sm_cross, c->sm_ctl,
-                    c->sm_typ, c->sm_slist, c->sm_stheta, c->stage, c->evalc};
+                    c->sm_typ, c->sm_slist, c->sm_stheta, c->stage, c->evalc, c->z_base, c->cnt_base,
+                    c->chg_slot, c->mu_base, c->sigma_base, c->chg_item, c->chg_count, c->chg_flags};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     if (c->sm_first_host) (void)hipHostFree(c->sm_first_host);
@@ -397,6 +407,13 @@ void free_device(np8_ctx *c) {
     c->acc = nullptr;
     c->r2 = nullptr;
     c->wr2 = nullptr;
+    c->z_base = c->cnt_base = c->chg_slot = nullptr;
+    c->mu_base = c->sigma_base = nullptr;
+    c->chg_item = nullptr;
+    c->chg_count = nullptr;
+    c->chg_flags = nullptr;
+    c->chg_cap = 0;
+    c->track = 0;
     c->plist = c->plen = nullptr;
     c->X = nullptr;
     c->z = c->z_best = nullptr;
@@ -1252,6 +1269,7 @@ int np8_set_data(np8_ctx *c, const double *X, int64_t n, int32_t D, int64_t offs
     if ((r = dalloc(c, &c->s_hist, (size_t)c->kcap)) || (r = dalloc(c, &c->s_cursor, (size_t)c->kcap)) ||
         (r = dalloc(c, &c->s_off, (size_t)c->kcap)) || (r = alloc_records(c)))
         return r;
+    c->track = 0;  // a change log needs a new baseline for the new items
     c->vis_tag.assign((size_t)n, 0u);
     c->vis_n.assign((size_t)n, 0u);
     c->sorted_valid = false;
@@ -1427,6 +1445,121 @@ int np8_sweep(np8_ctx *c, int32_t n_sweeps) {
         int r = end_sweep(c);
         if (r) return r;
     }
+    return NP8_OK;
+}
+
+int np8_population_sweep(np8_ctx *c) {
+    if (!c) return NP8_ERR_ARG;
+    if (!c->have_state) return fail(c, NP8_ERR_STATE, "np8_population_sweep: no state (np8_set_state/np8_init_random)");
+    const int64_t N = c->n_loc;
+    const int64_t chunk = (c->chunk <= 0 || c->chunk >= c->n_glob) ? N : c->chunk;
+    const bool sync = chunk >= N;
+    if (!sync && c->world > 1) return fail(c, NP8_ERR_ARG, "np8_population_sweep: chunk < N is single-rank only");
+    if (N > 0) {
+        for (int64_t p0 = 0; p0 < N; p0 += chunk) {
+            const int64_t p1 = (p0 + chunk < N) ? p0 + chunk : N;
+            int r = step(c, p0, p1, nullptr, !sync);
+            if (r) return r;
+        }
+    } else if (c->world > 1) {
+        return step(c, 0, 0, nullptr, false);
+    }
+    return NP8_OK;
+}
+
+int np8_track_changes(np8_ctx *c, int32_t mode) {
+    if (!c) return NP8_ERR_ARG;
+    if (mode < 0 || mode > NP8_CHANGES_FROM_EMPTY) return fail(c, NP8_ERR_ARG, "np8_track_changes: bad mode");
+    c->track = mode ? 1 : 0;
+    if (!mode) return NP8_OK;
+    if (!c->have_data) return fail(c, NP8_ERR_STATE, "np8_track_changes: no data");
+    const int D = c->D, kc = c->kcap;
+    int r = 0;
+    if ((r = dalloc(c, &c->z_base, (size_t)c->n_loc)) || (r = dalloc(c, &c->cnt_base, (size_t)kc)) ||
+        (r = dalloc(c, &c->mu_base, (size_t)kc * D)) || (r = dalloc(c, &c->sigma_base, (size_t)kc * D * D)) ||
+        (r = dalloc(c, &c->chg_count, 1)) || (r = dalloc(c, &c->chg_flags, (size_t)kc)))
+        return r;
+    if (mode == NP8_CHANGES_FROM_EMPTY || !c->have_state) {  // every item unassigned, no live slot
+        if (c->n_loc > 0) HIPC(c, hipMemsetD32Async(reinterpret_cast<int *>(c->z_base), -1, c->n_loc, c->stream));
+    } else {
+        HIPC(c, hipMemcpyAsync(c->z_base, c->z, sizeof(int32_t) * c->n_loc, hipMemcpyDeviceToDevice, c->stream));
+        HIPC(c, hipMemcpyAsync(c->cnt_base, c->cnt, sizeof(int32_t) * kc, hipMemcpyDeviceToDevice, c->stream));
+        HIPC(c, hipMemcpyAsync(c->mu_base, c->slot_mu, sizeof(double) * kc * D, hipMemcpyDeviceToDevice, c->stream));
+        HIPC(c, hipMemcpyAsync(c->sigma_base, c->slot_sigma, sizeof(double) * kc * D * D, hipMemcpyDeviceToDevice,
+                               c->stream));
+    }
+    HIPC(c, hipStreamSynchronize(c->stream));
+    return NP8_OK;
+}
+
+int np8_changes(np8_ctx *c, int64_t item_cap, int64_t *item, int32_t *slot, int32_t *created, int32_t *removed,
+                int32_t *updated, double *mu, double *Sigma, np8_changes_t *out) {
+    if (!c || !out) return NP8_ERR_ARG;
+    std::memset(out, 0, sizeof(*out));
+    if (!c->track) return fail(c, NP8_ERR_STATE, "np8_changes: change tracking is off (np8_track_changes)");
+    if (!c->have_state) return fail(c, NP8_ERR_STATE, "np8_changes: no state");
+    if (item_cap < 0 || (item_cap > 0 && (!item || !slot)) || !created || !removed || !updated)
+        return fail(c, NP8_ERR_ARG, "np8_changes: bad arguments");
+    const int D = c->D, kc = c->kcap;
+    // staging for the moved items: grows to the largest request seen
+    const int64_t need = item_cap < c->n_loc ? item_cap : c->n_loc;
+    if (need > c->chg_cap) {
+        int r = 0;
+        if ((r = dalloc(c, &c->chg_item, (size_t)need)) || (r = dalloc(c, &c->chg_slot, (size_t)need))) return r;
+        c->chg_cap = need;
+    }
+    HIPC(c, hipMemsetAsync(c->chg_count, 0, sizeof(unsigned long long), c->stream));
+    HIPC(c, np8_launch_changes(c->z, c->z_base, c->n_loc, c->chg_item, c->chg_slot, need, c->chg_count, c->cnt, c->cnt_base,
+                               c->slot_mu, c->mu_base, c->slot_sigma, c->sigma_base, D, kc, c->chg_flags, c->stream));
+    unsigned long long nm = 0;
+    std::vector<uint8_t> fl((size_t)kc);
+    HIPC(c, hipMemcpyAsync(&nm, c->chg_count, sizeof(nm), hipMemcpyDeviceToHost, c->stream));
+    HIPC(c, hipMemcpyAsync(fl.data(), c->chg_flags, (size_t)kc, hipMemcpyDeviceToHost, c->stream));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    out->n_moved = (int64_t)nm;
+    if ((int64_t)nm > item_cap) return fail(c, NP8_ERR_CAPACITY, "np8_changes: more moved items than item_cap");
+    if (nm > 0) {
+        std::vector<int64_t> it((size_t)nm);
+        std::vector<int32_t> sl((size_t)nm);
+        HIPC(c, hipMemcpy(it.data(), c->chg_item, sizeof(int64_t) * nm, hipMemcpyDeviceToHost));
+        HIPC(c, hipMemcpy(sl.data(), c->chg_slot, sizeof(int32_t) * nm, hipMemcpyDeviceToHost));
+        std::vector<int64_t> ord((size_t)nm);
+        for (size_t k = 0; k < nm; ++k) ord[k] = (int64_t)k;
+        std::sort(ord.begin(), ord.end(), [&](int64_t a, int64_t b) { return it[a] < it[b]; });  // ascending items
+        for (size_t k = 0; k < nm; ++k) {
+            item[k] = it[ord[k]];
+            slot[k] = sl[ord[k]];
+        }
+    }
+    std::vector<int32_t> par;  // created then updated slots: their parameters go out
+    for (int s = 0; s < kc; ++s) {
+        if (fl[s] == 1) {
+            created[out->n_created++] = s;
+            par.push_back(s);
+        } else if (fl[s] == 2) {
+            removed[out->n_removed++] = s;
+        }
+    }
+    for (int s = 0; s < kc; ++s)
+        if (fl[s] == 3) {
+            updated[out->n_updated++] = s;
+            par.push_back(s);
+        }
+    if (!par.empty() && (mu || Sigma)) {
+        std::vector<double> m((size_t)kc * D), sg((size_t)kc * D * D);
+        HIPC(c, hipMemcpy(m.data(), c->slot_mu, sizeof(double) * m.size(), hipMemcpyDeviceToHost));
+        HIPC(c, hipMemcpy(sg.data(), c->slot_sigma, sizeof(double) * sg.size(), hipMemcpyDeviceToHost));
+        for (size_t q = 0; q < par.size(); ++q) {
+            if (mu) std::memcpy(mu + q * D, &m[(size_t)par[q] * D], sizeof(double) * D);
+            if (Sigma) std::memcpy(Sigma + q * D * D, &sg[(size_t)par[q] * D * D], sizeof(double) * D * D);
+        }
+    }
+    // the current state becomes the baseline
+    HIPC(c, hipMemcpyAsync(c->z_base, c->z, sizeof(int32_t) * c->n_loc, hipMemcpyDeviceToDevice, c->stream));
+    HIPC(c, hipMemcpyAsync(c->cnt_base, c->cnt, sizeof(int32_t) * kc, hipMemcpyDeviceToDevice, c->stream));
+    HIPC(c, hipMemcpyAsync(c->mu_base, c->slot_mu, sizeof(double) * kc * D, hipMemcpyDeviceToDevice, c->stream));
+    HIPC(c, hipMemcpyAsync(c->sigma_base, c->slot_sigma, sizeof(double) * kc * D * D, hipMemcpyDeviceToDevice, c->stream));
+    HIPC(c, hipStreamSynchronize(c->stream));
     return NP8_OK;
 }
 

@@ -340,6 +340,12 @@ hipError_t np8_launch_niw_post(const np8::NiwArgs &A, int nblocks, hipStream_t s
 hipError_t np8_launch_niw_aux_slots(const np8::NiwArgs &A, hipStream_t s);
 hipError_t np8_launch_resort(const SortArgs &S, hipStream_t s);
 hipError_t np8_launch_assign(const np8::AssignArgs &A, int D, int M, int prior, hipStream_t s);
+// Membership change log (np8_changes): items whose slot differs from the baseline (wave-aggregated append,
+// out[0..cap) kept, *count = all of them), and per slot 0 / 1 created / 2 removed / 3 parameters changed.
+hipError_t np8_launch_changes(const int32_t *z, const int32_t *z_base, int64_t n, int64_t *out_item, int32_t *out_slot,
+                              int64_t cap, unsigned long long *count, const int32_t *cnt, const int32_t *cnt_base,
+                              const double *mu, const double *mu_base, const double *sg, const double *sg_base, int D,
+                              int kcap, uint8_t *flags, hipStream_t s);
 // Parity/debug: the sweep's categorical draw (pick_step) on given log-weights, one lane per draw.
 hipError_t np8_launch_pick_batch(const double *lw, int32_t n, const double *u, int64_t n_draws, int32_t *out,
                                  hipStream_t s);

@@ -457,6 +457,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NP8_ASSIGN_
     }
     // items leaving their cluster, counted per wave (drives the re-sort of the layout)
     const uint64_t mv = __ballot(snew != zi);
+#ifdef NP8_EXP_NO_MOVED
+    if (COUNT)
+#endif
     if (mv && (threadIdx.x & 63) == (__ffsll((unsigned long long)__ballot(1)) - 1))
         atomicAdd(reinterpret_cast<unsigned long long *>(&A.ctl->moved), (unsigned long long)__popcll(mv));
     if (st.pick < K) {
@@ -1363,6 +1366,60 @@ hipError_t np8_launch_assign(const AssignArgs &A, int D, int M, int prior, hipSt
     NP8_FOR_EACH_DM(X)
 #undef X
     return hipErrorInvalidValue;
+}
+
+// ---- membership change log (np8_changes) --------------------------------------------------------------
+// One lane per item; a wave with moved items takes its output range with one atomic.
+__global__ __launch_bounds__(256) void np8_changes_items(const int32_t *__restrict__ z, const int32_t *__restrict__ zb,
+                                                         int64_t n, int64_t *__restrict__ oi, int32_t *__restrict__ os,
+                                                         int64_t cap, unsigned long long *count) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool moved = i < n && z[i] != zb[i];
+    const uint64_t b = __ballot(moved);
+    if (b == 0ull) return;
+    const int lane = threadIdx.x & 63, lead = __ffsll((unsigned long long)b) - 1;
+    unsigned long long base = 0ull;
+    if (lane == lead) base = atomicAdd(count, (unsigned long long)__popcll(b));
+    base = __shfl(base, lead);
+    const int64_t q = (int64_t)base + __popcll(b & ((1ull << lane) - 1ull));
+    if (moved && q < cap) {
+        oi[q] = i;
+        os[q] = z[i];
+    }
+}
+
+__global__ __launch_bounds__(256) void np8_changes_slots(const int32_t *__restrict__ cnt, const int32_t *__restrict__ cb,
+                                                         const double *__restrict__ mu, const double *__restrict__ mb,
+                                                         const double *__restrict__ sg, const double *__restrict__ sb,
+                                                         int D, int kcap, uint8_t *__restrict__ flags) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= kcap) return;
+    const bool live = cnt[s] > 0, was = cb[s] > 0;
+    uint8_t f = 0;
+    if (live && !was) {
+        f = 1;
+    } else if (!live && was) {
+        f = 2;
+    } else if (live) {  // same slot live before and after: bitwise comparison of the parameters
+        bool diff = false;
+        for (int a = 0; a < D; ++a) diff |= __double_as_longlong(mu[(int64_t)s * D + a]) != __double_as_longlong(mb[(int64_t)s * D + a]);
+        for (int a = 0; a < D * D; ++a)
+            diff |= __double_as_longlong(sg[(int64_t)s * D * D + a]) != __double_as_longlong(sb[(int64_t)s * D * D + a]);
+        f = diff ? 3 : 0;
+    }
+    flags[s] = f;
+}
+
+hipError_t np8_launch_changes(const int32_t *z, const int32_t *z_base, int64_t n, int64_t *out_item, int32_t *out_slot,
+                              int64_t cap, unsigned long long *count, const int32_t *cnt, const int32_t *cnt_base,
+                              const double *mu, const double *mu_base, const double *sg, const double *sg_base, int D,
+                              int kcap, uint8_t *flags, hipStream_t s) {
+    if (n > 0)
+        hipLaunchKernelGGL(np8_changes_items, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, z, z_base, n, out_item,
+                           out_slot, cap, count);
+    hipLaunchKernelGGL(np8_changes_slots, dim3((unsigned)((kcap + 255) / 256)), dim3(256), 0, s, cnt, cnt_base, mu, mu_base,
+                       sg, sg_base, D, kcap, flags);
+    return hipGetLastError();
 }
 
 // The draw exactly as np8_assign runs it: state at candidate 0 (the item's own cluster), then pick_step over

@@ -47,6 +47,11 @@ class NP8Error(RuntimeError):
         self.code = code
 
 
+class _ChangesT(C.Structure):
+    _fields_ = [("n_moved", C.c_int64), ("n_created", C.c_int32), ("n_removed", C.c_int32),
+                ("n_updated", C.c_int32), ("pad", C.c_int32)]
+
+
 class _Config(C.Structure):
     _fields_ = [
         ("D", C.c_int32),
@@ -134,6 +139,9 @@ def lib():
         "np8_prepare_sweeps": ([vp, i32], i32),
         "np8_update_points": ([vp, vp, i64], i32),
         "np8_end_sweep": ([vp], i32),
+        "np8_population_sweep": ([vp], i32),
+        "np8_track_changes": ([vp, i32], i32),
+        "np8_changes": ([vp, i64, vp, vp, vp, vp, vp, vp, vp, vp], i32),
         "np8_sync": ([vp], i32),
         "np8_get_state": ([vp, i32, vp, vp, vp, vp, vp], i32),
         "np8_loglik_matrix": ([vp, vp, i64, vp], i32),
@@ -374,17 +382,67 @@ class NealAlgorithm8:
         summed = np.ascontiguousarray(summed, dtype=np.float64)
         self._check(lib().np8_end_sweep_stats(self._h, _p(summed)))
 
+    def population_sweep(self):
+        """The population update of one sweep without the end-of-sweep step (np8_population_sweep)."""
+        self._check(lib().np8_population_sweep(self._h))
+
+    def track_changes(self, mode="now"):
+        """Start (mode "now" / "empty") or stop (None) the membership change log (np8_track_changes)."""
+        self._check(lib().np8_track_changes(self._h, {None: 0, "now": 1, "empty": 2}[mode]))
+
+    def changes(self):
+        """What changed since the last call (np8_changes): moved items and their new slots, created /
+        removed / updated slots, and the parameters of the created and updated ones."""
+        cs = _ChangesT()
+        kc, D = self.kcap, self.D
+        cr, rm, up = (np.zeros(kc, dtype=np.int32) for _ in range(3))
+        mu, sg = np.zeros((kc, D)), np.zeros((kc, D, D))
+        cap = max(self.N, 1)
+        item, slot = np.zeros(cap, dtype=np.int64), np.zeros(cap, dtype=np.int32)
+        self._check(lib().np8_changes(self._h, cap, _p(item), _p(slot), _p(cr), _p(rm), _p(up), _p(mu), _p(sg),
+                                      C.byref(cs)))
+        nc, nu = cs.n_created, cs.n_updated
+        return {"item": item[:cs.n_moved].copy(), "slot": slot[:cs.n_moved].copy(), "created": cr[:nc].copy(),
+                "removed": rm[:cs.n_removed].copy(), "updated": up[:nu].copy(), "mu": mu[:nc + nu].copy(),
+                "sigma": sg[:nc + nu].copy()}
+
     # -- reference plug-in interface (np_update_cluster_population.h:35-43) --------------------
     def update(self, cluster_matrix, data_ids):
-        """UpdateClusterPopulation::update.  A full permutation of the items runs one data-parallel
-        sweep; a single id runs the exact sequential step of NealAlgorithm8::update."""
+        """UpdateClusterPopulation::update: the population update of the listed items, then the caller's
+        membertrix patched in place with what changed (O(changes), np8_changes), as the reference's
+        update mutates it (retract / addCluster / assign, np_neal_algorithm8.cpp:62-64,139-157).
+        A full permutation of the items is one population sweep (np8_population_sweep: data-parallel
+        steps of `chunk` items); anything else runs the exact sequential steps of NealAlgorithm8::update.
+        The end-of-sweep step (UpdateClusters, the max-likelihood check) stays with the caller."""
         ids = np.asarray(data_ids, dtype=np.int64).reshape(-1)
         if ids.size == self.N and self.N > 0 and np.array_equal(np.sort(ids), np.arange(self.N)):
-            self.sweep(1)
+            self.population_sweep()
         else:
             self.update_points(ids)
         if cluster_matrix is not None:
-            cluster_matrix.load(self.state(params=False))
+            self.patch(cluster_matrix)
+
+    def patch(self, cluster_matrix):
+        """Bring cluster_matrix (a membertrix this sampler keeps coherent) up to the device state."""
+        if getattr(self, "_tracked", None) is not cluster_matrix:  # first contact: the whole state
+            self.track_changes("empty")
+            self._tracked, self._slot_id, self._gen = cluster_matrix, {}, cluster_matrix.generation
+            cluster_matrix.clear_clusters()
+        for g, remap in cluster_matrix.relabels_since(self._gen):  # ids renamed by relabel() meanwhile
+            self._slot_id = {s: remap[i] for s, i in self._slot_id.items()}
+            self._gen = g
+        ch = self.changes()
+        nc = ch["created"].size
+        for q, s in enumerate(ch["created"]):
+            self._slot_id[int(s)] = cluster_matrix.addCluster((ch["mu"][q].copy(), ch["sigma"][q].copy()))
+        for q, s in enumerate(ch["updated"]):
+            cluster_matrix.setCluster(self._slot_id[int(s)], (ch["mu"][nc + q].copy(), ch["sigma"][nc + q].copy()))
+        for i, s in zip(ch["item"], ch["slot"]):
+            if cluster_matrix.assigned(int(i)):
+                cluster_matrix.retract(int(i), auto_remove=False)
+            cluster_matrix.assign(self._slot_id[int(s)], int(i))
+        for s in ch["removed"]:
+            cluster_matrix.remove(self._slot_id.pop(int(s)))
 
     def printStatistics(self):
         s = self.stats()
@@ -415,7 +473,7 @@ class JainNealAlgorithm(NealAlgorithm8):
             raise ValueError("JainNealAlgorithm.update: pass a permutation of all items (one split-merge sweep)")
         self.sm_sweep(1)
         if cluster_matrix is not None:
-            cluster_matrix.load(self.state(params=False))
+            self.patch(cluster_matrix)
 
     def printStatistics(self):
         s = self.sm_stats()
@@ -453,7 +511,7 @@ class TriadicAlgorithm(NealAlgorithm8):
             raise ValueError("TriadicAlgorithm.update: pass a permutation of all items (one split-merge sweep)")
         self.sweep(1)
         if cluster_matrix is not None:
-            cluster_matrix.load(self.state(params=False))
+            self.patch(cluster_matrix)
 
     def printStatistics(self):
         s = self.tri_stats()
@@ -464,22 +522,114 @@ class TriadicAlgorithm(NealAlgorithm8):
 
 
 class membertrix:
-    """Host view of the membership state (reference include/membertrix.h:52-313), kept as labels and
-    counts instead of the dense N x C bool matrix (membertrix.h:30)."""
+    """Host mirror of the reference's membership state (include/membertrix.h:52-313, src/membertrix.cpp):
+    labels per item and a map cluster id -> parameters (mu, Sigma) instead of the dense N x C bool matrix
+    (membertrix.h:30).  Cluster ids come from addCluster in increasing order (the reference appends a
+    column, membertrix.cpp:87-100); relabel() renames the live clusters 0..K-1 in ascending id order (the
+    copy constructor's renumbering, membertrix.cpp:34-55) and records the renaming so that a sampler
+    patching this membertrix can follow it (relabels_since)."""
 
-    def __init__(self):
-        self.z = np.zeros(0, dtype=np.int32)
-        self.counts = np.zeros(0, dtype=np.int64)
+    def __init__(self, n_items=0):
+        self.z = np.full(int(n_items), -1, dtype=np.int64)
+        self.clusters = {}
+        self.counts = {}
+        self._next = 0
+        self.generation = 0
+        self._relabels = []
 
-    def load(self, st):
-        self.z = np.asarray(st["z"], dtype=np.int32).copy()
-        self.counts = np.asarray(st["counts"], dtype=np.int64).copy()
+    def addData(self, n=1):
+        first = self.z.size
+        self.z = np.concatenate([self.z, np.full(int(n), -1, dtype=np.int64)])
+        return first
+
+    def clear_clusters(self):
+        self.z[:] = -1
+        self.clusters, self.counts = {}, {}
+
+    def addCluster(self, cluster):
+        cid = self._next
+        self._next += 1
+        self.clusters[cid] = cluster
+        self.counts[cid] = 0
+        return cid
+
+    def getCluster(self, cluster_id):
+        return self.clusters[cluster_id]
+
+    def setCluster(self, cluster_id, cluster):
+        self.clusters[cluster_id] = cluster
+
+    def assign(self, cluster_id, data_id):
+        if self.z[data_id] >= 0:
+            raise ValueError("already assigned")  # error_already_assigned
+        self.z[data_id] = cluster_id
+        self.counts[cluster_id] += 1
+
+    def assigned(self, data_id):
+        return bool(self.z[data_id] >= 0)
+
+    def retract(self, data_id, auto_remove=True):
+        c = int(self.z[data_id])
+        if c < 0:
+            raise ValueError("assignment absent")
+        self.z[data_id] = -1
+        self.counts[c] -= 1
+        if auto_remove and self.counts[c] == 0:  # membertrix.cpp:200-203
+            self.remove(c)
+
+    def remove(self, cluster_id):
+        if self.counts.get(cluster_id, 0) != 0:
+            raise ValueError("assignment remaining")
+        self.clusters.pop(cluster_id, None)
+        self.counts.pop(cluster_id, None)
+
+    def cleanup(self):
+        empty = [c for c, n in self.counts.items() if n == 0]
+        for c in empty:
+            self.remove(c)
+        return len(empty)
+
+    def relabel(self):
+        remap = {c: k for k, c in enumerate(sorted(c for c, n in self.counts.items() if n > 0))}
+        self.clusters = {remap[c]: v for c, v in self.clusters.items() if c in remap}
+        self.counts = {remap[c]: n for c, n in self.counts.items() if c in remap}
+        lut = np.full(self._next + 1, -1, dtype=np.int64)
+        for c, k in remap.items():
+            lut[c] = k
+        self.z = np.where(self.z >= 0, lut[np.maximum(self.z, 0)], -1)
+        self._next = len(remap)
+        self.generation += 1
+        self._relabels.append((self.generation, remap))
+
+    def relabels_since(self, generation):
+        return [(g, m) for g, m in self._relabels if g > generation]
 
     def count(self, cluster_id=None):
-        return int(self.z.size if cluster_id is None else self.counts[cluster_id])
+        return int(self.z.size if cluster_id is None else self.counts.get(cluster_id, 0))
 
     def getClusterId(self, data_id):
         return int(self.z[data_id])
 
+    def getClusters(self):
+        return self.clusters
+
     def getClusterCount(self):
-        return int((self.counts > 0).sum())
+        return len(self.clusters)
+
+    def dense(self):
+        """(labels 0..K-1 in ascending id order, counts, mu [K, D], Sigma [K, D, D]) -- np8_get_state's form."""
+        ids = sorted(self.clusters)
+        lut = {c: k for k, c in enumerate(ids)}
+        z = np.array([lut[int(c)] for c in self.z], dtype=np.int32)
+        mu = np.array([self.clusters[c][0] for c in ids])
+        sg = np.array([self.clusters[c][1] for c in ids])
+        return z, np.array([self.counts[c] for c in ids], dtype=np.int64), mu, sg
+
+    def load(self, st):
+        """Replace the whole state by a dense one (labels 0..K-1, counts; parameters if present)."""
+        K = int(st["K"]) if "K" in st else len(st["counts"])
+        self.clusters = {k: (st["mu"][k] if "mu" in st else None, st["sigma"][k] if "sigma" in st else None)
+                         for k in range(K)}
+        self.counts = {k: int(st["counts"][k]) for k in range(K)}
+        self.z = np.asarray(st["z"], dtype=np.int64).copy()
+        self._next = K

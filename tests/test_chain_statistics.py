@@ -52,3 +52,17 @@ def test_sequential_chain_is_a_valid_partition():
     assert st["counts"].sum() == 200 and (st["counts"] > 0).all()
     assert st["z"].min() == 0 and st["z"].max() == st["K"] - 1
     assert np.array_equal(np.bincount(st["z"], minlength=st["K"]), st["counts"])
+
+
+def test_golden_sequential_statistics_regenerate():
+    """tests/golden/twogaussians_seq_stats.json (the reference's algorithm: chunk = 1, pick = invcdf) is what
+    the oracle produces: two seeds re-run bit for bit."""
+    import json
+    import sys
+
+    sys.path.insert(0, GOLD)
+    import make_chain_stats as M
+
+    g = json.load(open(os.path.join(GOLD, "twogaussians_seq_stats.json")))
+    for s in (0, 7):
+        assert M.run(s) == g["seeds"][str(s)], s

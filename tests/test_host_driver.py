@@ -128,3 +128,23 @@ def test_triadic_end_to_end(tmp_path):
     score = open(os.path.join(ws, "LATEST", "results.score.txt")).read()
     vals = dict(ln.split(": ") for ln in score.strip().splitlines())
     assert float(vals["Purity"]) > 0.9  # the proper SAMS weights find the two components
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("algo,extra", [("algorithm8", []), ("algorithm8", ["-u", "mh_g0"]),
+                                        ("algorithm8", ["-C", "1"]), ("jain_neal_split", []), ("triadic", [])])
+def test_membertrix_coherent_through_reference_loop(tmp_path, algo, extra):
+    """MCMC::run in the reference's structure (np_mcmc.cpp:109-175: relabel every 10 sweeps, update of all
+    items, UpdateClusters, considerMaxLikelihood every 5 sweeps on the membertrix) with -V: after every
+    population update and every cluster update the host membertrix -- patched from np8_changes -- equals
+    np8_get_state, and the host's max-likelihood clone equals the device snapshot.  -j writes one JSON
+    line per sweep."""
+    import json
+
+    ws = str(tmp_path / "ws") + "/"
+    jl = str(tmp_path / "sweeps.jsonl")
+    r = run(["-d", DATA, "-a", algo, "-T", "60", "-s", "11", "-V", "-j", jl, "-w", ws] + extra)
+    assert r.returncode == 0, r.stderr + r.stdout
+    recs = [json.loads(ln) for ln in open(jl)]
+    assert [x["sweep"] for x in recs] == list(range(60))
+    assert all(x["K"] >= 1 for x in recs) and all("loglik" in x for x in recs[::5])

@@ -16,7 +16,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def test_library_exports_every_declared_symbol():
     L = noparama_amd.lib()
     declared = noparama_amd.header_symbols()
-    assert len(declared) == 31
+    assert len(declared) == 34
     for name in declared:
         assert hasattr(L, name), name
     out = subprocess.run(["nm", "-D", "--defined-only", np8.LIB_PATH], capture_output=True, text=True,
@@ -73,3 +73,26 @@ def test_membertrix_host_view():
     m = noparama_amd.membertrix()
     m.load({"z": np.array([0, 1, 1, 2]), "counts": np.array([1, 2, 1])})
     assert m.count() == 4 and m.count(1) == 2 and m.getClusterId(2) == 1 and m.getClusterCount() == 3
+
+
+def test_membertrix_mirror_follows_reference_semantics():
+    """test/test_membertrix.cpp:16-93 analogue: addCluster ids in order, assign / retract with auto-remove,
+    error on double assignment, cleanup of empty clusters, relabel to 0..K-1 in ascending id order."""
+    m = noparama_amd.membertrix(5)
+    a, b, c = (m.addCluster((np.zeros(2), np.eye(2))) for _ in range(3))
+    assert (a, b, c) == (0, 1, 2)
+    m.assign(a, 0)
+    m.assign(c, 1)
+    m.assign(c, 2)
+    try:
+        m.assign(b, 0)
+        raise AssertionError("double assignment accepted")
+    except ValueError:
+        pass
+    assert m.cleanup() == 1 and m.getClusterCount() == 2  # b never got an item
+    m.retract(0)  # a empties and is auto-removed (membertrix.cpp:200-203)
+    assert a not in m.getClusters() and m.getClusterCount() == 1
+    m.assign(c, 0)
+    m.relabel()
+    assert m.getClusters().keys() == {0} and m.getClusterId(1) == 0 and m.count(0) == 3
+    assert m.relabels_since(0) == [(1, {c: 0})]
