@@ -44,6 +44,8 @@ def parse():
     ap.add_argument("--k", type=int, default=None, help="default: 64 (C3) / 256 (C5)")
     ap.add_argument("--seed", type=int, default=20261015)
     ap.add_argument("--kcap", type=int, default=0, help="cluster capacity (0: the library default)")
+    ap.add_argument("--substeps", type=int, default=1,
+                    help="the data-parallel sweep as S synchronous sub-steps (np8_config.substeps)")
     ap.add_argument("--config", default="C3", help="config tag for the JSON line (BASELINE.json configs)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget (0 = skip)")
     ap.add_argument("--cold-sweeps", type=int, default=20,
@@ -76,7 +78,10 @@ def workload(args):
         return X, z, mu, sig, opts
     s, r = (0.3, 15.0) if D == 2 else (0.8, 20.0)
     X, z, mu, sig = datasets.mixture(N, D, K, s, r, seed=args.seed)
-    return X, z, mu, sig, ({"kcap": args.kcap} if args.kcap else {})
+    opts = {"kcap": args.kcap} if args.kcap else {}
+    if args.substeps > 1:
+        opts["substeps"] = args.substeps
+    return X, z, mu, sig, opts
 
 
 def main():
@@ -245,6 +250,7 @@ def main():
                                "mh_g0": "mh_g0 cluster-parameter update (20 MH steps/cluster/sweep)",
                                "niw_conjugate": "niw_conjugate cluster-parameter update"}[args.param_update],
                 "N": N, "D": D, "K_final": Kfinal, "parallelism": f"data-sharded x{world}",
+                "substeps": args.substeps,
                 "exchange": transport,
                 "param_update": args.param_update,
                 "params_ms_per_timed_sweep": ((st1["ms_params"] - st0["ms_params"])

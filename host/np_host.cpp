@@ -182,6 +182,7 @@ NealAlgorithm8Hip::NealAlgorithm8Hip(uint64_t seed, const np8_prior &prior, int6
     cfg.mh_steps = prior.mh_steps;
     cfg.prior = prior.prior;
     cfg.contraction = prior.contraction;
+    cfg.substeps = prior.substeps;
     check(np8_create(&_ctx, &cfg), "np8_create");
 }
 

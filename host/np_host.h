@@ -105,6 +105,7 @@ struct np8_prior {
     double nu = 4.0;
     std::vector<double> Lambda;    // default 0.01 I
     int M = 3;                     // np_neal_algorithm8.cpp:33
+    int substeps = 1;              // the data-parallel sweep as S synchronous sub-steps (np8_config)
     int param_update = NP8_PARAM_FROZEN;  // UpdateClusters mode (np_mcmc.cpp:170), include/np8.h
     int mh_steps = 20;                    // np_mcmc.cpp:54
     int prior = NP8_PRIOR_REFERENCE;      // base measure (include/np8.h NP8_PRIOR_*)

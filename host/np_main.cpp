@@ -30,7 +30,7 @@ static void usage(const char *p) {
               << " [-C chunk (0 = data-parallel sweep, 1 = sequential)] [-D dims=2] [-w workspace]"
               << " [-u frozen|mh_g0|niw_conjugate (cluster-parameter update)] [-p reference|niw (base measure)]"
               << " [-x f64|f32 (cluster likelihoods; f32 = fp32 matrix cores, D in {32, 64})]"
-              << " [-n subsample size=200, 0 = all items] [-j per-sweep JSONL file] [-V (check the membertrix against the device after every update)]; data: 'x_1 .. x_D label' text or [N][D+1] .f64"
+              << " [-n subsample size=200, 0 = all items] [-S sub-steps of the data-parallel sweep=1] [-j per-sweep JSONL file] [-V (check the membertrix against the device after every update)]; data: 'x_1 .. x_D label' text or [N][D+1] .f64"
               << std::endl;
 }
 
@@ -87,13 +87,13 @@ static void subsample(dataset_t &ds, std::vector<int> &gt, int n, uint64_t seed)
 
 int main(int argc, char *argv[]) {
     std::string data, algo, mode = "clustering", ws, upd = "frozen", base = "reference", contr = "f64";
-    int T = 2000, D = 2, nsub = 200;
+    int T = 2000, D = 2, nsub = 200, substeps = 1;
     long long chunk = 0;
     unsigned long long seed = 0;
     bool seeded = false, verify = false;
     std::string jsonl;
     int tok;
-    while ((tok = getopt(argc, argv, "d:a:T:c:s:C:D:w:u:n:p:x:j:Vh?")) != EOF) {
+    while ((tok = getopt(argc, argv, "d:a:T:c:s:C:D:w:u:n:p:x:j:S:Vh?")) != EOF) {
         switch (tok) {
             case 'd': data = optarg; break;
             case 'a': algo = optarg; break;
@@ -109,6 +109,7 @@ int main(int argc, char *argv[]) {
             case 'x': contr = optarg; break;
             case 'j': jsonl = optarg; break;
             case 'V': verify = true; break;
+            case 'S': substeps = std::stoi(optarg); break;
             default: usage(argv[0]); return 1;
         }
     }
@@ -140,6 +141,7 @@ int main(int argc, char *argv[]) {
     subsample(dataset, gt, nsub, seed);
     np8_prior prior;
     prior.D = D;
+    prior.substeps = substeps;
     if (upd == "mh_g0") {
         prior.param_update = NP8_PARAM_MH_G0;
     } else if (upd == "niw_conjugate") {

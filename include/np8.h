@@ -61,7 +61,15 @@ typedef struct {
                              lowest scan position; the other requesters keep their cluster until their next
                              update (DESIGN.md "Finalize").  Part of the chain's specification: the same
                              value gives the same chain on any number of ranks. */
+    int32_t substeps;     /* the data-parallel sweep (chunk 0) as S synchronous sub-steps (0, 1 -> one step;
+                             at most NP8_SUBSTEPS_MAX, and S * kcap <= 16384): sub-step s updates the items
+                             with a fixed hash of the item index equal to s, against the state the earlier
+                             sub-steps left (DESIGN.md "Sub-steps").  One step updates every item against
+                             the same state; more sub-steps bring the chain's statistics to the sequential
+                             sweep's (tests/test_gpu_chain_stats.py) at S launches of each step kernel. */
 } np8_config;
+
+#define NP8_SUBSTEPS_MAX 64
 
 /* Cluster-likelihood arithmetic (DESIGN.md "Wide path").
  * F64:      fp64 table form (packed sym(Sigma^{-1})), D in {1,2,3,4,8,16}.
@@ -266,9 +274,10 @@ int np8_comm_unique_id(uint8_t out[128]);
 int np8_comm_init(np8_ctx *ctx, const uint8_t id[128], int32_t rank, int32_t world);
 
 /* Host-exchange variant of the same protocol (for callers that move the record themselves, e.g.
- * over MPI or gloo): np8_comm_init(ctx, NULL, rank, world), then per sweep np8_step_local (writes
- * this rank's record), the caller all-gathers np8_record_bytes() bytes from every rank in rank
- * order, np8_step_merge(gathered, world), np8_end_sweep.  The max-likelihood check then uses this
+ * over MPI or gloo): np8_comm_init(ctx, NULL, rank, world), then per sweep, once per sub-step
+ * (np8_config.substeps times), np8_step_local (writes this rank's record), the caller all-gathers
+ * np8_record_bytes() bytes from every rank in rank order, np8_step_merge(gathered, world); then
+ * np8_end_sweep.  The max-likelihood check then uses this
  * rank's partial sum only. */
 int64_t np8_record_bytes(np8_ctx *ctx);
 int np8_step_local(np8_ctx *ctx, void *record_out);

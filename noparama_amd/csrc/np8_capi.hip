@@ -63,8 +63,15 @@ struct np8_ctx {
     unsigned long long *evalc = nullptr;  // [kEvalSlots][2] executed-work counters (timing mode)
     bool prune_on = false;     // kcap small enough for kcap x kcap lists
     bool lists_valid = false;  // plist/plen describe the current table and membership
-    bool r2_zero = false;      // r2 is 0 for every live slot (ready to collect)
+    bool r2_zero = false;      // the radius buffers are in a consistent collecting state (cleared at (re)start)
     bool collecting = false;   // the running sweep collects r2 (a whole synchronous sweep)
+    bool r2_prev_ok = false;   // the last sweep's radius buffer is complete (intermediate sub-step prunes)
+    int64_t assign_waves = 0;  // waves of the last assign launch (its radius records)
+    // data-parallel sweep in `substeps` synchronous sub-steps (np8_config.substeps): sub-step s is the
+    // contiguous range [sub_start[s], sub_start[s+1]) of the label-sorted layout (sorted by sub-step, slot)
+    int substeps = 1;
+    std::vector<int64_t> sub_start;
+    int sub_next = 0;  // host-exchange path: the sub-step np8_step_local runs next
     std::vector<double> mu0, Lambda;
     // base-measure precomputes (DESIGN.md "G0")
     std::vector<double> Lc, LT, UinvT, Gp, LTL;  // D*D row-major
@@ -735,32 +742,34 @@ int launch_assign(np8_ctx *c, int64_t p0, int64_t p1, const int64_t *order, bool
     AssignArgs A = assign_args(c, p0, p1, order, use_perm);
     A.collect_r2 = c->collecting ? 1 : 0;
     A.use_lists = (c->collecting && c->lists_valid) ? 1 : 0;
+    c->assign_waves = (p1 - p0 + 63) / 64;
     if (c->wide)
         HIPC(c, np8_launch_assign_wide(A, c->D, c->M, c->prior, c->stream));
     else
         HIPC(c, np8_launch_assign(A, c->D, c->M, c->prior, c->stream));
     timer_end(c, t);
-    if (c->collecting) c->r2_zero = false;
     return NP8_OK;
 }
 
 // Candidate lists for the next sweep from the radii this sweep collected (after every change of
 // the table: finalize and the parameter update).
-int launch_prune(np8_ctx *c) {
+int launch_prune(np8_ctx *c, bool last) {
     PruneArgs P;
     P.cand = c->cand;
     P.ctl = c->ctl;
     P.r2 = c->r2;
     P.wr2 = c->wr2;
-    P.n_waves = (c->n_loc + 63) / 64;
+    P.n_waves = c->assign_waves;
     P.kcap = c->kcap;
+    P.t = c->epoch - c->t_base;
+    P.last = last ? 1 : 0;
     P.plist = c->plist;
     P.plen = c->plen;
     P.ls = c->kcap;
     P.D = c->D;
     HIPC(c, np8_launch_prune(P, c->kcap, c->stream));
     c->lists_valid = true;
-    c->r2_zero = true;
+    if (last) c->r2_prev_ok = true;
     return NP8_OK;
 }
 
@@ -786,6 +795,10 @@ int prepare_sorted(np8_ctx *c) {
     S.kcap = c->kcap;
     S.D = c->D;
     S.esz = c->wide ? 4 : 8;
+    S.nsub = c->substeps;
+    S.pad = 0;
+    S.offset = c->offset;
+    S.seed = c->seed;
     S.force = stale ? 1 : 0;  // otherwise the device re-sorts only if > n/32 items moved
     HIPC(c, np8_launch_resort(S, c->stream));
     c->sorted_valid = true;
@@ -794,20 +807,30 @@ int prepare_sorted(np8_ctx *c) {
 
 // One synchronous step over local positions [p0,p1): assign, exchange, finalize.  A whole-sweep
 // step (no order, no permutation) runs on the label-sorted layout.
-int step(np8_ctx *c, int64_t p0, int64_t p1, const int64_t *order, bool use_perm) {
-    c->use_sorted = (order == nullptr) && !use_perm && p0 == 0 && p1 == c->n_loc && c->n_loc > 0;
+// One synchronous step.  sub >= 0: sub-step `sub` of a data-parallel sweep (positions of the label-sorted
+// layout); otherwise local positions [p0,p1) of the chunked or explicit-order walk, and the whole
+// data-parallel sweep when [p0,p1) = [0,n) with no order (substeps == 1).
+int step(np8_ctx *c, int64_t p0, int64_t p1, const int64_t *order, bool use_perm, int sub = -1) {
+    if (sub >= 0) {
+        p0 = c->sub_start[(size_t)sub];
+        p1 = c->sub_start[(size_t)sub + 1];
+    }
+    c->use_sorted = sub >= 0 || ((order == nullptr) && !use_perm && p0 == 0 && p1 == c->n_loc && c->n_loc > 0);
     if (c->use_sorted) {
-        int r = prepare_sorted(c);
-        if (r) return r;
+        if (sub <= 0) {  // the layout is refreshed at the start of a sweep only
+            int r = prepare_sorted(c);
+            if (r) return r;
+        }
     } else {
         c->sorted_valid = false;
     }
-    // candidate pruning runs on whole synchronous sweeps; any other step changes the membership
-    // behind the lists' back
+    // candidate pruning runs on data-parallel sweeps; any other step changes the membership behind the
+    // lists' back
     c->collecting = c->prune_on && c->use_sorted;
     if (!c->use_sorted) c->lists_valid = c->r2_zero = false;
     if (c->collecting && !c->r2_zero) {
-        HIPC(c, hipMemsetAsync(c->r2, 0, sizeof(double) * c->kcap, c->stream));
+        HIPC(c, hipMemsetAsync(c->r2, 0, 2 * sizeof(double) * c->kcap, c->stream));
+        c->r2_prev_ok = false;
         c->r2_zero = true;
     }
     int r = launch_assign(c, p0, p1, order, use_perm);
@@ -816,9 +839,42 @@ int step(np8_ctx *c, int64_t p0, int64_t p1, const int64_t *order, bool use_perm
         if (!c->comm) return fail(c, NP8_ERR_STATE, "host-exchange mode: use np8_step_local/np8_step_merge");
         HIPC(c, np8_launch_req_select(c->stage, c->stage_cap, c->rec, c->rec_cap, c->kcap, c->D, c->req_max, c->stream));
         NCCLC(c, ncclAllGather(c->rec, c->gath, (size_t)c->rec_bytes, ncclUint8, c->comm, c->stream));
-        return launch_finalize(c, c->gath, c->world);
+        r = launch_finalize(c, c->gath, c->world);
+    } else {
+        r = launch_finalize(c, c->rec, 1);
     }
-    return launch_finalize(c, c->rec, 1);
+    if (r) return r;
+    if (c->collecting && sub >= 0 && sub + 1 < c->substeps && c->r2_prev_ok)
+        return launch_prune(c, false);  // lists for the next sub-step from the last sweep's radii
+    // the table changed: lists are valid again after the next prune (end of sweep or of a sub-step)
+    c->lists_valid = false;
+    return NP8_OK;
+}
+
+// The population update of one sweep (np_mcmc.cpp:146-164): chunks of `chunk` items in a keyed permutation,
+// or the data-parallel sweep -- one synchronous step, or `substeps` of them.
+int population(np8_ctx *c) {
+    const int64_t N = c->n_loc;
+    const int64_t chunk = (c->chunk <= 0 || c->chunk >= c->n_glob) ? N : c->chunk;
+    const bool sync = chunk >= N;
+    if (!sync && c->world > 1) return fail(c, NP8_ERR_ARG, "chunk < N is single-rank only");
+    if (sync && c->substeps > 1) {
+        for (int k = 0; k < c->substeps; ++k) {
+            int r = step(c, 0, 0, nullptr, false, k);
+            if (r) return r;
+        }
+        return NP8_OK;
+    }
+    if (N > 0) {
+        for (int64_t p0 = 0; p0 < N; p0 += chunk) {
+            const int64_t p1 = (p0 + chunk < N) ? p0 + chunk : N;
+            int r = step(c, p0, p1, nullptr, !sync);
+            if (r) return r;
+        }
+    } else if (c->world > 1) {
+        return step(c, 0, 0, nullptr, false);  // still take part in the exchange
+    }
+    return NP8_OK;
 }
 
 int ensure_partial(np8_ctx *c) {
@@ -934,7 +990,7 @@ int end_sweep(np8_ctx *c, bool stats_given = false) {
     int r0 = param_update(c, stats_given ? 2 : 0);
     if (r0) return r0;
     if (c->collecting) {  // after finalize and the parameter update: the table is final
-        r0 = launch_prune(c);
+        r0 = launch_prune(c, true);
         if (r0) return r0;
         c->collecting = false;
     }
@@ -1000,7 +1056,7 @@ void drop_graph(np8_ctx *c) {
 
 bool graph_eligible(np8_ctx *c, bool sync) {
     return sync && !c->graphs_off && c->world == 1 && c->n_loc > 0 && c->sorted_valid &&
-           (!c->prune_on || (c->lists_valid && c->r2_zero));
+           (!c->prune_on || (c->lists_valid && c->r2_zero && (c->substeps == 1 || c->r2_prev_ok)));
 }
 
 // Captures kGraphSweeps sweeps starting at the current epoch.  Nothing runs during capture; on any
@@ -1022,7 +1078,7 @@ int capture_graph(np8_ctx *c) {
     c->capturing = true;
     c->capture_timed_left = 1;
     for (uint32_t i = 0; i < kGraphSweeps && !r; ++i) {
-        r = step(c, 0, c->n_loc, nullptr, false);
+        r = population(c);
         if (!r) r = end_sweep(c);
     }
     if (!r && np8_launch_advance_epoch(c->ctl, kGraphSweeps, c->stream) != hipSuccess) r = NP8_ERR_HIP;
@@ -1110,6 +1166,12 @@ int np8_create(np8_ctx **out, const np8_config *cfg) {
         return NP8_ERR_ARG;
     }
     c->req_max = cfg->req_max > 0 ? cfg->req_max : NP8_REQ_DEFAULT;
+    c->substeps = cfg->substeps > 1 ? cfg->substeps : 1;
+    // the label-sorted layout is sorted by (sub-step, slot): substeps * kcap bins in the sort's LDS
+    if (cfg->substeps < 0 || cfg->substeps > NP8_SUBSTEPS_MAX || (int64_t)c->substeps * c->kcap > 16384) {
+        delete c;
+        return NP8_ERR_ARG;
+    }
     c->alpha = cfg->alpha;
     c->kappa = cfg->kappa;
     c->nu = cfg->nu;
@@ -1172,7 +1234,7 @@ int np8_create(np8_ctx **out, const np8_config *cfg) {
         (r = dalloc(c, &c->dense_of, (size_t)kc)) || (r = dalloc(c, &c->slot_iso, (size_t)kc)) ||
         (r = dalloc(c, &c->rec, (size_t)c->rec_bytes)) || (r = dalloc(c, &c->evalc, (size_t)4 * kEvalSlots)) ||
         (c->param_update != NP8_PARAM_FROZEN && (r = dalloc(c, &c->acc, (size_t)kc * (D + DP)))) ||
-        (kc <= kPruneMaxKcap && ((r = dalloc(c, &c->r2, (size_t)kc)) || (r = dalloc(c, &c->plen, (size_t)kc)) ||
+        (kc <= kPruneMaxKcap && ((r = dalloc(c, &c->r2, 2 * (size_t)kc)) || (r = dalloc(c, &c->plen, (size_t)kc)) ||
                                  (r = dalloc(c, &c->plist, (size_t)kc * kc))))) {
         free_device(c);
         delete c;
@@ -1266,9 +1328,14 @@ int np8_set_data(np8_ctx *c, const double *X, int64_t n, int32_t D, int64_t offs
         if ((r = dalloc(c, &c->Xs[b], nx)) || (r = dalloc(c, &c->zs[b], (size_t)n)) ||
             (r = dalloc(c, &c->ids[b], (size_t)n)))
             return r;
-    if ((r = dalloc(c, &c->s_hist, (size_t)c->kcap)) || (r = dalloc(c, &c->s_cursor, (size_t)c->kcap)) ||
-        (r = dalloc(c, &c->s_off, (size_t)c->kcap)) || (r = alloc_records(c)))
+    const size_t bins = (size_t)c->kcap * c->substeps;  // sort keys (sub-step, slot)
+    if ((r = dalloc(c, &c->s_hist, bins)) || (r = dalloc(c, &c->s_cursor, bins)) || (r = dalloc(c, &c->s_off, bins)) ||
+        (r = alloc_records(c)))
         return r;
+    c->sub_start.assign((size_t)c->substeps + 1, 0);  // the sub-steps' ranges of the sorted layout
+    for (int64_t p = 0; p < n; ++p) c->sub_start[substep_of(c->seed, offset + p, (uint32_t)c->substeps) + 1] += 1;
+    for (int k = 0; k < c->substeps; ++k) c->sub_start[(size_t)k + 1] += c->sub_start[(size_t)k];
+    c->sub_next = 0;
     c->track = 0;  // a change log needs a new baseline for the new items
     c->vis_tag.assign((size_t)n, 0u);
     c->vis_n.assign((size_t)n, 0u);
@@ -1432,17 +1499,9 @@ int np8_sweep(np8_ctx *c, int32_t n_sweeps) {
                 continue;
             }
         }
-        if (N > 0) {
-            for (int64_t p0 = 0; p0 < N; p0 += chunk) {
-                const int64_t p1 = (p0 + chunk < N) ? p0 + chunk : N;
-                int r = step(c, p0, p1, nullptr, !sync);
-                if (r) return r;
-            }
-        } else if (c->world > 1) {
-            int r = step(c, 0, 0, nullptr, false);  // still take part in the exchange
-            if (r) return r;
-        }
-        int r = end_sweep(c);
+        int r = population(c);
+        if (r) return r;
+        r = end_sweep(c);
         if (r) return r;
     }
     return NP8_OK;
@@ -1451,20 +1510,7 @@ int np8_sweep(np8_ctx *c, int32_t n_sweeps) {
 int np8_population_sweep(np8_ctx *c) {
     if (!c) return NP8_ERR_ARG;
     if (!c->have_state) return fail(c, NP8_ERR_STATE, "np8_population_sweep: no state (np8_set_state/np8_init_random)");
-    const int64_t N = c->n_loc;
-    const int64_t chunk = (c->chunk <= 0 || c->chunk >= c->n_glob) ? N : c->chunk;
-    const bool sync = chunk >= N;
-    if (!sync && c->world > 1) return fail(c, NP8_ERR_ARG, "np8_population_sweep: chunk < N is single-rank only");
-    if (N > 0) {
-        for (int64_t p0 = 0; p0 < N; p0 += chunk) {
-            const int64_t p1 = (p0 + chunk < N) ? p0 + chunk : N;
-            int r = step(c, p0, p1, nullptr, !sync);
-            if (r) return r;
-        }
-    } else if (c->world > 1) {
-        return step(c, 0, 0, nullptr, false);
-    }
-    return NP8_OK;
+    return population(c);
 }
 
 int np8_track_changes(np8_ctx *c, int32_t mode) {
@@ -1818,14 +1864,16 @@ int64_t np8_record_bytes(np8_ctx *c) { return c ? c->rec_bytes : 0; }
 int np8_step_local(np8_ctx *c, void *record_out) {
     if (!c || !record_out) return NP8_ERR_ARG;
     if (!c->have_state) return fail(c, NP8_ERR_STATE, "np8_step_local: no state");
+    const int sub = c->sub_next;  // sub-step sub of the data-parallel sweep (0 with one step)
+    const int64_t p0 = c->sub_start[(size_t)sub], p1 = c->sub_start[(size_t)sub + 1];
     c->use_sorted = c->n_loc > 0;
-    if (c->use_sorted) {
+    if (c->use_sorted && sub == 0) {
         int r0 = prepare_sorted(c);
         if (r0) return r0;
     }
     c->collecting = false;  // no pruning on the host-exchange path
     c->lists_valid = c->r2_zero = false;
-    int r = launch_assign(c, 0, c->n_loc, nullptr, false);
+    int r = launch_assign(c, p0, p1, nullptr, false);
     if (r) return r;
     if (c->stage)
         HIPC(c, np8_launch_req_select(c->stage, c->stage_cap, c->rec, c->rec_cap, c->kcap, c->D, c->req_max, c->stream));
@@ -1866,6 +1914,7 @@ int np8_end_sweep_stats(np8_ctx *c, const double *summed) {
 int np8_step_merge(np8_ctx *c, const void *records, int32_t world) {
     if (!c || !records || world < 1) return NP8_ERR_ARG;
     if (world != c->world) return fail(c, NP8_ERR_ARG, "np8_step_merge: world differs from np8_comm_init");
+    c->sub_next = (c->sub_next + 1) % c->substeps;
     if (world == 1) {
         HIPC(c, hipMemcpyAsync(c->rec, records, (size_t)c->rec_bytes, hipMemcpyHostToDevice, c->stream));
         return launch_finalize(c, c->rec, 1);

@@ -445,6 +445,14 @@ NP8_HD uint32_t fmix32(uint32_t h) {
     return h;
 }
 
+// Sub-step of item i (global index) in a data-parallel sweep of S synchronous sub-steps: a fixed hash
+// partition of the items (identical in oracle/np8_oracle.c np8o_substep_of).
+NP8_HD uint32_t substep_of(uint64_t seed, int64_t i, uint32_t S) {
+    if (S <= 1) return 0;
+    const uint32_t h = fmix32(fmix32((uint32_t)i ^ 0x5EB57E95u ^ (uint32_t)(seed >> 32)) ^ (uint32_t)seed);
+    return (uint32_t)(((uint64_t)h * S) >> 32);
+}
+
 // Scan-order bijection of a chunked sweep (replaces the reference's std::shuffle,
 // include/helper/dim1algebra.hpp:2066-2073).
 struct Perm {

@@ -120,7 +120,7 @@ struct AssignArgs {
     // lists of the next sweep
     const int32_t *plist, *plen;
     int32_t ls, use_lists, collect_r2, count_eval;
-    double *r2;      // per slot; only waves whose items are not all in one slot add to it (atomicMax)
+    double *r2;      // [2][kcap] by epoch parity; only waves whose items do not share one slot add to it (atomicMax)
     WaveR2 *wr2;     // [ceil(n_loc / 64)]: a wave whose 64 items sit in one slot stores its maximum here
     unsigned long long *evalc;  // [kEvalSlots][2]: quadratic forms, isotropic ones
     // wide path (np8_wide.hip): per slot, the used MFMA fragment chunks of the fp32 factor followed by
@@ -143,11 +143,13 @@ struct WideArgs {
 struct PruneArgs {
     const double *cand;
     Ctl *ctl;
-    double *r2;
-    const WaveR2 *wr2;  // the sweep's per-wave maxima (AssignArgs::wr2), n_waves of them
+    double *r2;         // [2][kcap]: buffer (epoch & 1) collects this sweep, the other holds the last sweep
+    const WaveR2 *wr2;  // per-wave maxima of the step just assigned (AssignArgs::wr2), n_waves of them
     int64_t n_waves;
     int32_t *plist, *plen;
     int32_t ls, D, kcap;
+    uint32_t t;     // epoch offset: epoch = ctl->t_base + t
+    int32_t last;   // the sweep's last step: lists for the next sweep from this sweep's radii
 };
 
 struct FinArgs {
@@ -182,6 +184,14 @@ struct FinArgs {
 
 // Auxiliary draw m of (item i, epoch t) -> a slot: the G0 draw of normalinvwishart.h:44-64 in the
 // factored form (DESIGN.md "G0").
+// Pruning radii (DESIGN.md "Candidate pruning") live in two buffers of kcap, by sweep parity: a slot whose
+// parameters are new is unprunable (+inf) in both until a whole sweep has measured it.
+__device__ __forceinline__ void r2_unknown(double *r2, int kcap, int s) {
+    if (!r2) return;
+    r2[s] = __longlong_as_double(0x7FF0000000000000ll);
+    r2[kcap + s] = __longlong_as_double(0x7FF0000000000000ll);
+}
+
 __device__ __forceinline__ void write_new_slot(const FinArgs &F, const double *vmu, int s) {
     const int D = F.D, DP = D * (D + 1) / 2;
     const double v = vmu[0];
@@ -191,7 +201,7 @@ __device__ __forceinline__ void write_new_slot(const FinArgs &F, const double *v
     F.slot_c[s] = fma(-(double)D, log_pos(fabs(v)), F.caux);
     for (int k = 0; k < D * D; ++k) F.slot_sigma[(int64_t)s * D * D + k] = v2 * F.LTL[k];
     F.slot_iso[s] = (F.gp_iso > 0.0) ? F.Gp[0] / v2 : 0.0;
-    if (F.r2) F.r2[s] = __longlong_as_double(0x7FF0000000000000ll);  // radius unknown until a sweep measures it
+    r2_unknown(F.r2, F.kcap, s);  // radius unknown until a sweep measures it
 }
 
 // Jain-Neal split-merge (np8_sm.hip, DESIGN.md "Split-merge").
@@ -324,6 +334,10 @@ struct SortArgs {
     int64_t n;
     int32_t kcap, D, force;
     int32_t esz;  // bytes per element of X: 8 (fp64) or 4 (wide path, fp32)
+    // data-parallel sub-steps: the layout is sorted by (sub-step of the item, slot), nsub * kcap bins
+    int32_t nsub, pad;
+    int64_t offset;  // global index of local item 0
+    uint64_t seed;
 };
 
 bool np8_supported(int D, int M);

@@ -227,6 +227,9 @@ __device__ __forceinline__ void ensure_u(PickState &st, double lw, uint64_t seed
     }
 }
 
+// Own rows per wave up to which the lanes walk their rows' pruned lists group by group (np8_assign).
+constexpr int kMaxListGroups = 3;
+
 __device__ __forceinline__ int64_t position_to_local(const AssignArgs &A, int64_t p) {
     if (A.order) return A.order[p];
     if (A.use_perm) return (int64_t)perm_apply(A.perm, (uint32_t)p);
@@ -285,24 +288,40 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NP8_ASSIGN_
     }
     const double zslot = (double)zi;
     const int K = A.ctl->K;
-    // a wave whose items share their cluster (the label-sorted layout) walks that cluster's pruned
-    // candidate list: the rows left out are skipped by every lane's pick_step anyway (np8_prune)
-    const int32_t z0 = __builtin_amdgcn_readfirstlane(zi);
-    const bool walk_list = A.use_lists && A.ctl->lists_ok && __ballot(zi != z0) == 0;
-    const int32_t j0 = __builtin_amdgcn_readfirstlane(jo);
-    if (walk_list) {
+    // with candidate lists (np8_prune), the lanes of each distinct own row of the wave walk that row's
+    // pruned list (one group in the label-sorted layout, two or three at cluster boundaries): the rows
+    // left out are those every such lane's pick_step skips anyway, and the order is ascending as in the
+    // full walk.  Lists hold for every item of the row, whatever its wave (np8_prune: the radius covers
+    // each item the last sweep left in the row).
+    int32_t nq_lane = 0, niso_lane = 0;  // COUNT: quadratic forms this lane evaluated
+    // (a wave of many own rows -- a stale layout, a cold start -- walks the table once instead)
+    int ngroups = 0;
+    for (uint64_t pend = __ballot(1); pend && ngroups <= kMaxListGroups; ++ngroups)
+        pend &= ~__ballot(jo == __builtin_amdgcn_readlane(jo, __ffsll((unsigned long long)pend) - 1));
+    if (A.use_lists && A.ctl->lists_ok && ngroups <= kMaxListGroups) {
+        uint64_t pend = __ballot(1);
+        while (pend) {
+            const int32_t j0 = __builtin_amdgcn_readlane(jo, __ffsll((unsigned long long)pend) - 1);
+            pend &= ~__ballot(jo == j0);
+            if (jo == j0) {
 #ifdef NP8_EXP_NO_WALK
-        const int32_t nl = COUNT ? A.plen[j0] : 0;
+                const int32_t nl = COUNT ? A.plen[j0] : 0;
 #else
-        const int32_t nl = A.plen[j0];
+                const int32_t nl = A.plen[j0];
 #endif
-        const int32_t *__restrict__ lst = A.plist + (int64_t)j0 * A.ls;
-        for (int q = 0; q < nl; ++q) {
-            const int j = lst[q];  // wave-uniform: scalar loads
-            const double *e = cand + (int64_t)j * CS;
-            const double lw = cand_ll<D>(e, x) + e[F + kFieldLogn];
-            ensure_u(st, lw, A.seed, ig, t);
-            pick_step(st, lw, j);
+                const int32_t *__restrict__ lst = A.plist + (int64_t)j0 * A.ls;
+                for (int q = 0; q < nl; ++q) {
+                    const int j = lst[q];  // uniform across the group: scalar loads
+                    const double *e = cand + (int64_t)j * CS;
+                    const double lw = cand_ll<D>(e, x) + e[F + kFieldLogn];
+                    ensure_u(st, lw, A.seed, ig, t);
+                    pick_step(st, lw, j);
+                    if constexpr (COUNT) {
+                        nq_lane += 1;
+                        niso_lane += (e[F + kFieldIso] > 0.0) ? 1 : 0;
+                    }
+                }
+            }
         }
     } else {
         for (int j = 0; j < K; ++j) {
@@ -312,24 +331,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NP8_ASSIGN_
                 ensure_u(st, lw, A.seed, ig, t);
                 pick_step(st, lw, j);
             }
+            if constexpr (COUNT) {
+                nq_lane += 1;
+                niso_lane += (e[F + kFieldIso] > 0.0) ? 1 : 0;
+            }
         }
     }
     if constexpr (COUNT) {  // the quadratic forms this wave executed (own row + walked rows)
-        const int nrow = walk_list ? A.plen[j0] : K;
+        nq_lane += 1;
+        niso_lane += (cand[(int64_t)jo * CS + F + kFieldIso] > 0.0) ? 1 : 0;
         int64_t nq = 0, niso = 0;
-        for (int q = 0; q < nrow; ++q) {
-            const int j = walk_list ? A.plist[(int64_t)j0 * A.ls + q] : q;
-            nq += 1;
-            niso += (cand[(int64_t)j * CS + F + kFieldIso] > 0.0) ? 1 : 0;
-        }
         const uint64_t lanes = __ballot(1);
-        const int nl = __popcll(lanes);
-        const bool own_iso = cand[(int64_t)jo * CS + F + kFieldIso] > 0.0;
-        const int n_own_iso = __popcll(__ballot(own_iso));
+        for (uint64_t act = lanes; act; act &= act - 1ull) {  // sums over the active lanes
+            const int l = __ffsll((unsigned long long)act) - 1;
+            nq += __builtin_amdgcn_readlane(nq_lane, l);
+            niso += __builtin_amdgcn_readlane(niso_lane, l);
+        }
         if ((threadIdx.x & 63) == (__ffsll((unsigned long long)lanes) - 1)) {
             unsigned long long *ec = A.evalc + 2 * ((blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) % kEvalSlots);
-            atomicAdd(ec, (unsigned long long)(nq * nl + nl));
-            atomicAdd(ec + 1, (unsigned long long)(niso * nl + n_own_iso));
+            atomicAdd(ec, (unsigned long long)nq);
+            atomicAdd(ec + 1, (unsigned long long)niso);
         }
     }
     double ny;
@@ -445,7 +466,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NP8_ASSIGN_
 #pragma unroll
             for (int o = 32; o > 0; o >>= 1) d2 = fmax(d2, __shfl_xor(d2, o));
         } else {
-            atomicMax(reinterpret_cast<unsigned long long *>(A.r2 + ts), (unsigned long long)__double_as_longlong(d2));
+            atomicMax(reinterpret_cast<unsigned long long *>(A.r2 + (int64_t)(t & 1u) * A.kcap + ts),
+                      (unsigned long long)__double_as_longlong(d2));
         }
         if ((threadIdx.x & 63) == (__ffsll((unsigned long long)__ballot(1)) - 1)) {  // the wave's record
             WaveR2 w;
@@ -502,27 +524,40 @@ constexpr int kSortThreads = 1024, kSortItems = 4;  // 4096 items per block
 
 __device__ __forceinline__ bool sort_needed(const SortArgs &S) { return S.force || S.ctl->moved * 32 > S.n; }
 
+// Sort key of position p: the slot, after the item's data-parallel sub-step (sub-steps are contiguous
+// ranges of the layout, clusters contiguous inside each).  ids = null: p is the local item itself.
+__device__ __forceinline__ int sort_key(const SortArgs &S, const int32_t *__restrict__ z, const int32_t *__restrict__ ids,
+                                        int64_t p) {
+    const int32_t slot = z[p];
+    if (S.nsub <= 1) return slot;
+    const int64_t item = S.offset + (ids ? (int64_t)ids[p] : p);
+    return (int)substep_of(S.seed, item, (uint32_t)S.nsub) * S.kcap + slot;
+}
+
 __global__ __launch_bounds__(kSortThreads) void np8_sort_hist(SortArgs S) {
     if (!sort_needed(S)) return;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     int *lh = reinterpret_cast<int *>(smem);
+    const int nb = S.kcap * S.nsub;
     const int32_t *z = S.force ? S.z : (S.ctl->cur ? S.zs[1] : S.zs[0]);
-    for (int s = threadIdx.x; s < S.kcap; s += kSortThreads) lh[s] = 0;
+    const int32_t *ids = S.force ? nullptr : (S.ctl->cur ? S.ids[1] : S.ids[0]);
+    for (int s = threadIdx.x; s < nb; s += kSortThreads) lh[s] = 0;
     __syncthreads();
     for (int k = 0; k < kSortItems; ++k) {
         const int64_t p = ((int64_t)blockIdx.x * kSortItems + k) * kSortThreads + threadIdx.x;
-        if (p < S.n) atomicAdd(&lh[z[p]], 1);
+        if (p < S.n) atomicAdd(&lh[sort_key(S, z, ids, p)], 1);
     }
     __syncthreads();
-    for (int s = threadIdx.x; s < S.kcap; s += kSortThreads)
+    for (int s = threadIdx.x; s < nb; s += kSortThreads)
         if (lh[s]) atomicAdd(&S.hist[s], lh[s]);
 }
 
 __global__ __launch_bounds__(kSortThreads) void np8_sort_scatter(SortArgs S) {
     if (!S.ctl->do_sort) return;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int nb = S.kcap * S.nsub;
     int *lh = reinterpret_cast<int *>(smem);
-    int *lbase = lh + S.kcap;
+    int *lbase = lh + nb;
     const int src = S.ctl->cur, dst = src ^ 1;
     const int32_t *z = S.force ? S.z : (src ? S.zs[1] : S.zs[0]);
     const int32_t *ids = S.force ? nullptr : (src ? S.ids[1] : S.ids[0]);
@@ -530,23 +565,23 @@ __global__ __launch_bounds__(kSortThreads) void np8_sort_scatter(SortArgs S) {
     int32_t *zo = dst ? S.zs[1] : S.zs[0];
     int32_t *ido = dst ? S.ids[1] : S.ids[0];
     double *Xo = dst ? S.Xs[1] : S.Xs[0];
-    for (int s = threadIdx.x; s < S.kcap; s += kSortThreads) lh[s] = 0;
+    for (int s = threadIdx.x; s < nb; s += kSortThreads) lh[s] = 0;
     __syncthreads();
-    int zp[kSortItems], rk[kSortItems];
+    int zp[kSortItems], rk[kSortItems];  // sort keys, ranks in the block
     for (int k = 0; k < kSortItems; ++k) {
         const int64_t p = ((int64_t)blockIdx.x * kSortItems + k) * kSortThreads + threadIdx.x;
-        zp[k] = (p < S.n) ? z[p] : -1;
+        zp[k] = (p < S.n) ? sort_key(S, z, ids, p) : -1;
         rk[k] = (zp[k] >= 0) ? atomicAdd(&lh[zp[k]], 1) : 0;
     }
     __syncthreads();
-    for (int s = threadIdx.x; s < S.kcap; s += kSortThreads)
+    for (int s = threadIdx.x; s < nb; s += kSortThreads)
         if (lh[s]) lbase[s] = atomicAdd(&S.cursor[s], lh[s]);
     __syncthreads();
     for (int k = 0; k < kSortItems; ++k) {
         if (zp[k] < 0) continue;
         const int64_t p = ((int64_t)blockIdx.x * kSortItems + k) * kSortThreads + threadIdx.x;
         const int64_t q = (int64_t)S.off[zp[k]] + lbase[zp[k]] + rk[k];
-        zo[q] = zp[k];
+        zo[q] = z[p];
         ido[q] = ids ? ids[p] : (int32_t)p;
         if (S.esz == 4) {  // wide path: fp32 items
             const float *Xf = reinterpret_cast<const float *>(X);
@@ -576,8 +611,9 @@ __global__ __launch_bounds__(1024) void np8_sort_scan(SortArgs S) {
     }
     if (!need) return;
     __shared__ int sh[32];
-    const int per = (S.kcap + 1023) / 1024;
-    const int s0 = min(S.kcap, (int)threadIdx.x * per), s1 = min(S.kcap, s0 + per);
+    const int nb = S.kcap * S.nsub;
+    const int per = (nb + 1023) / 1024;
+    const int s0 = min(nb, (int)threadIdx.x * per), s1 = min(nb, s0 + per);
     int v = 0;
     for (int s = s0; s < s1; ++s) v += S.hist[s];
     int tot;
@@ -663,15 +699,16 @@ __device__ int block_excl_scan(int v, int *sh /* >= 16 ints */, int *total) {
 constexpr int kPruneBlocks = 32;  // np8_prune grid: 128 rows per pass
 
 // DT > 0: the dimension as a template constant (loops unrolled, the row loads issued together)
-template <int DT = 0>
-__device__ void prune_row(const double *__restrict__ cand, double *__restrict__ r2, const double *__restrict__ lr2,
-                          int32_t *__restrict__ plist, int32_t *__restrict__ plen, int ls, int Drt, int K, int k0) {
+// R2of(slot): the squared radius of the slot's items that will walk the list.
+template <int DT = 0, typename R2of>
+__device__ void prune_row(const double *__restrict__ cand, R2of R2of_slot, int32_t *__restrict__ plist,
+                          int32_t *__restrict__ plen, int ls, int Drt, int K, int k0) {
     const int D = DT > 0 ? DT : Drt;
     const int DP = D * (D + 1) / 2, CS = cand_stride(D), F = D + DP;
     const int lane = threadIdx.x & 63;
     const double *e0 = cand + (int64_t)k0 * CS;
     const int slot0 = (int)e0[F + kFieldSlot];
-    const double R2 = fmax(r2[slot0], lr2[slot0]);  // atomics of mixed waves, records of one-slot waves
+    const double R2 = R2of_slot(slot0);
     const double iso0 = e0[F + kFieldIso];
     const double base0 = e0[F + kFieldC] + e0[F + kFieldLogn1];
     const bool prunable = iso0 > 0.0 && R2 < 1e300 && base0 > -1e299;
@@ -708,10 +745,7 @@ __device__ void prune_row(const double *__restrict__ cand, double *__restrict__ 
         if (keep) plist[(int64_t)k0 * ls + count + __popcll(b & ((1ull << lane) - 1ull))] = j;
         count += __popcll(b);
     }
-    if (lane == 0) {
-        plen[k0] = count;
-        r2[slot0] = 0.0;  // collected afresh by the next sweep
-    }
+    if (lane == 0) plen[k0] = count;
 }
 
 // ---- finalize --------------------------------------------------------------------------------------
@@ -1307,7 +1341,7 @@ __global__ __launch_bounds__(64) void np8_mh_g0(ParamArgs A) {
         const double iso = (A.gp_iso > 0.0) ? A.Gp[0] / v2 : 0.0;
         A.slot_c[s] = c;
         A.slot_iso[s] = iso;
-        if (A.r2) A.r2[s] = __longlong_as_double(0x7FF0000000000000ll);  // the mean moved
+        r2_unknown(A.r2, A.kcap, s);  // the mean moved
         crow[D + DP + kFieldC] = c;
         crow[D + DP + kFieldIso] = iso;
         atomicAdd(reinterpret_cast<unsigned long long *>(&A.ctl->mh_accepted), (unsigned long long)s_nacc);
@@ -1468,9 +1502,10 @@ hipError_t np8_launch_resort(const SortArgs &S, hipStream_t s) {
     if (S.n <= 0) return hipSuccess;
     const int64_t per = (int64_t)kSortThreads * kSortItems;
     const unsigned nb = (unsigned)((S.n + per - 1) / per);
-    hipLaunchKernelGGL(np8_sort_hist, dim3(nb), dim3(kSortThreads), sizeof(int) * S.kcap, s, S);
+    const size_t bins = (size_t)S.kcap * S.nsub;
+    hipLaunchKernelGGL(np8_sort_hist, dim3(nb), dim3(kSortThreads), sizeof(int) * bins, s, S);
     hipLaunchKernelGGL(np8_sort_scan, dim3(1), dim3(1024), 0, s, S);
-    hipLaunchKernelGGL(np8_sort_scatter, dim3(nb), dim3(kSortThreads), 2 * sizeof(int) * S.kcap, s, S);
+    hipLaunchKernelGGL(np8_sort_scatter, dim3(nb), dim3(kSortThreads), 2 * sizeof(int) * bins, s, S);
     return hipGetLastError();
 }
 
@@ -1545,9 +1580,14 @@ hipError_t np8_launch_mh_g0(const ParamArgs &A, hipStream_t s) {
 // Standalone pass (after the mh_g0 update has moved means): four rows per block.
 // A small grid strides over the live rows (one wave per row): K is only known on the device, and a
 // grid sized for kcap would mostly launch blocks that exit at once.
-// Every block first folds the sweep's per-wave radius records into an LDS table (each thread walks a
+// Every block first folds the step's per-wave radius records into an LDS table (each thread walks a
 // contiguous run of records and flushes its running maximum when the slot changes: in the label-sorted
-// layout consecutive waves share their slot, so a run costs one or two LDS atomics).
+// layout consecutive waves share their slot, so a run costs one or two LDS atomics); block 0 adds the
+// fold to this sweep's radii.  Radius of a row (DESIGN.md "Candidate pruning"):
+//   after an intermediate sub-step: the last sweep's radii -- the items of the sub-steps still to come
+//     sit where the last sweep left them (they move only in their own sub-step);
+//   after the sweep's last step: this sweep's radii including the fold -- every item has been placed;
+//     block 0 then clears the last sweep's buffer, which collects the next sweep.
 template <int DT>
 __global__ __launch_bounds__(256) void np8_prune(PruneArgs A) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1573,8 +1613,22 @@ __global__ __launch_bounds__(256) void np8_prune(PruneArgs A) {
     }
     if (cs >= 0) atomicMax(&lr2[cs], cm);
     __syncthreads();
+    const uint32_t par = (A.ctl->t_base + A.t) & 1u;
+    unsigned long long *cur = reinterpret_cast<unsigned long long *>(A.r2 + (int64_t)par * A.kcap);
+    const double *prev = A.r2 + (int64_t)(par ^ 1u) * A.kcap;
+    if (blockIdx.x == 0) {
+        for (int s = threadIdx.x; s < A.kcap; s += blockDim.x) {
+            if (lr2[s] > cur[s]) cur[s] = lr2[s];
+            if (A.last) reinterpret_cast<unsigned long long *>(A.r2 + (int64_t)(par ^ 1u) * A.kcap)[s] = 0ull;
+        }
+    }
+    // (other blocks may read cur while block 0 raises it: either value, maxed with their own fold, is the same)
+    const bool last = A.last != 0;
+    auto R2of = [&](int slot) {
+        return last ? __longlong_as_double((long long)(cur[slot] > lr2[slot] ? cur[slot] : lr2[slot])) : prev[slot];
+    };
     for (int k0 = blockIdx.x * 4 + (threadIdx.x >> 6); k0 < K; k0 += gridDim.x * 4)  // wave-uniform
-        prune_row<DT>(A.cand, A.r2, reinterpret_cast<const double *>(lr2), A.plist, A.plen, A.ls, A.D, K, k0);
+        prune_row<DT>(A.cand, R2of, A.plist, A.plen, A.ls, A.D, K, k0);
 }
 
 __global__ void np8_advance_epoch(Ctl *ctl, uint32_t n) { ctl->t_base += n; }

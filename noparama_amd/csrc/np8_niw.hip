@@ -83,7 +83,7 @@ __device__ void write_sigma(int D, int LD, const double *B, const double *Rhs, b
 __device__ __forceinline__ void write_row_scalars(const NiwArgs &A, int s, int row, double c, double iso) {
     A.slot_c[s] = c;
     A.slot_iso[s] = iso;
-    if (A.r2) A.r2[s] = __longlong_as_double(0x7FF0000000000000ll);  // radius unknown: no pruning yet
+    r2_unknown(A.r2, A.kcap, s);  // radius unknown: no pruning yet
     if (row >= 0) {
         double *e = A.cand + (int64_t)row * cand_stride(A.D) + A.D + A.D * (A.D + 1) / 2;
         e[kFieldC] = c;

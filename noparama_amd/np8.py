@@ -70,6 +70,7 @@ class _Config(C.Structure):
         ("prior", C.c_int32),
         ("contraction", C.c_int32),
         ("req_max", C.c_int32),
+        ("substeps", C.c_int32),
     ]
 
 
@@ -197,11 +198,13 @@ class NealAlgorithm8:
     `prior`: "reference" (the reference's G0 as it draws) or "niw" (a proper Normal-Inverse-Wishart with
     kappa0 = kappa, nu0 = nu >= D + 1, Psi0 = Lambda).  `contraction`: "f64" (D <= 16) or "f32" (D in
     {32, 64}: items in fp32, cluster likelihoods on the fp32 matrix cores; config C5).
+    `substeps`: the data-parallel sweep (chunk 0) as S synchronous sub-steps over a fixed hash partition of
+    the items (DESIGN.md "Sub-steps"); 1 = one step against the sweep-start state.
     """
 
     def __init__(self, D, M=3, alpha=1.0, mu0=None, kappa=1.0 / 500, nu=4.0, Lambda=None, seed=0, kcap=None,
                  chunk=0, device=-1, param_update="frozen", mh_steps=20, prior="reference", contraction="f64",
-                 req_max=0):
+                 req_max=0, substeps=1):
         if kcap is None:  # the library's default: 512 on the wide path (kcap^2 x D offset table), else 2048
             kcap = 512 if contraction == "f32" else 2048
         self.D, self.M, self.kcap = int(D), int(M), int(kcap)
@@ -224,6 +227,8 @@ class NealAlgorithm8:
         cfg.contraction = CONTRACTION[contraction]
         cfg.req_max = int(req_max)
         self.req_max = int(req_max) or NP8_REQ_DEFAULT
+        cfg.substeps = int(substeps)
+        self.substeps = max(int(substeps), 1)
         h = C.c_void_p()
         r = lib().np8_create(C.byref(h), C.byref(cfg))
         if r:

@@ -169,6 +169,12 @@ static inline uint32_t fmix32(uint32_t h) {
     return h;
 }
 
+uint32_t np8o_substep_of(uint64_t seed, int64_t i, uint32_t S) {
+    if (S <= 1) return 0;
+    const uint32_t h = fmix32(fmix32((uint32_t)i ^ 0x5EB57E95u ^ (uint32_t)(seed >> 32)) ^ (uint32_t)seed);
+    return (uint32_t)(((uint64_t)h * S) >> 32);
+}
+
 /* Scan order of a chunked sweep (replaces dim1algebra.hpp:2066-2073 random_order): a keyed 4-round
  * Feistel bijection on [0,2^b), cycle-walked into [0,N). */
 uint32_t np8o_perm(uint64_t seed, uint32_t t, uint32_t N, uint32_t p) {
@@ -409,6 +415,7 @@ struct np8o_ctx {
     int32_t req_max;
     /* per-item visits within the epoch (np8o_update_points): tag = epoch + 1, count */
     uint32_t *vis_tag, *vis_n;
+    int64_t *sub_items, *sub_start; /* items of each data-parallel sub-step (ascending), CSR */
     /* split-merge (np8o_sm_sweep): member lists, per-member scratch, outcome counts */
     int64_t *sm_off, *sm_cur, *sm_mem;
     double *sm_v0, *sm_v1;
@@ -478,6 +485,7 @@ static int niw_prepare(np8o_ctx *c) {
 np8o_ctx *np8o_create(const np8o_config *cfg) {
     if (cfg->D < 1 || cfg->D > NP8O_DMAX || cfg->M < 1 || cfg->M > NP8O_MMAX || cfg->kcap < 1) return NULL;
     if (cfg->pick != NP8O_PICK_RESERVOIR && (cfg->pick != NP8O_PICK_INVCDF || cfg->kcap > NP8O_KCAP_PICK)) return NULL;
+    if (cfg->substeps < 0 || cfg->substeps > 64) return NULL;
     if (cfg->param_update < NP8O_PARAM_FROZEN || cfg->param_update > NP8O_PARAM_NIW_CONJUGATE || cfg->mh_steps < 0)
         return NULL;
     if (cfg->prior != NP8O_PRIOR_REFERENCE && cfg->prior != NP8O_PRIOR_NIW) return NULL;
@@ -607,6 +615,8 @@ void np8o_destroy(np8o_ctx *c) {
     free(c->sm_v1);
     free(c->sm_flag);
     free(c->tri_asg);
+    free(c->sub_items);
+    free(c->sub_start);
     free(c->vis_tag);
     free(c->vis_n);
     free(c);
@@ -627,6 +637,19 @@ int np8o_set_data(np8o_ctx *c, const double *X, int64_t N) {
     free(c->tri_asg);
     free(c->vis_tag);
     free(c->vis_n);
+    free(c->sub_items);
+    free(c->sub_start);
+    {
+        const uint32_t S = c->cfg.substeps > 1 ? (uint32_t)c->cfg.substeps : 1u;
+        c->sub_items = (int64_t *)malloc(sizeof(int64_t) * (size_t)(N > 0 ? N : 1));
+        c->sub_start = (int64_t *)calloc(S + 1, sizeof(int64_t));
+        for (int64_t i = 0; i < N; ++i) c->sub_start[np8o_substep_of(c->cfg.seed, i, S) + 1] += 1;
+        for (uint32_t k = 0; k < S; ++k) c->sub_start[k + 1] += c->sub_start[k];
+        int64_t *fill = (int64_t *)malloc(sizeof(int64_t) * S);
+        for (uint32_t k = 0; k < S; ++k) fill[k] = c->sub_start[k];
+        for (int64_t i = 0; i < N; ++i) c->sub_items[fill[np8o_substep_of(c->cfg.seed, i, S)]++] = i;
+        free(fill);
+    }
     c->vis_tag = (uint32_t *)calloc((size_t)(N > 0 ? N : 1), sizeof(uint32_t));
     c->vis_n = (uint32_t *)calloc((size_t)(N > 0 ? N : 1), sizeof(uint32_t));
     c->N = N;
@@ -1759,13 +1782,31 @@ static int run_chunks(np8o_ctx *c, const int64_t *order, int64_t npos, int64_t c
     return err;
 }
 
+/* The data-parallel sweep in S sub-steps: one synchronous step per sub-step over its items (ascending;
+ * scan position = rank in that list, so requests are accepted in ascending item order). */
+static int run_substeps(np8o_ctx *c) {
+    int err = 0;
+    const int S = c->cfg.substeps > 1 ? c->cfg.substeps : 1;
+    for (int k = 0; k < S; ++k) {
+        const int64_t *items = c->sub_items + c->sub_start[k];
+        const int64_t n = c->sub_start[k + 1] - c->sub_start[k];
+        memset(c->delta, 0, sizeof(int32_t) * c->kcap);
+        int32_t nr = 0;
+        int e1 = assign_range_impl(c, 0, n, 1, items, c->delta, c->rq_pos, c->rq_i, c->rq_m, c->rq_zold,
+                                   (int32_t)(n > 0 ? n : 1), &nr);
+        (void)np8o_finalize(c, c->delta, c->rq_pos, c->rq_i, c->rq_m, c->rq_zold, nr, 0, -1);
+        if (e1) err = e1;
+    }
+    return err;
+}
+
 int np8o_sweep(np8o_ctx *c, int32_t n) {
     int err = 0;
     int64_t chunk = c->cfg.chunk <= 0 ? c->N : c->cfg.chunk;
     if (chunk > c->N) chunk = c->N;
     for (int s = 0; s < n; ++s) {
         if (c->N > 0) {
-            int e = run_chunks(c, NULL, c->N, chunk);
+            int e = (chunk >= c->N && c->cfg.substeps > 1) ? run_substeps(c) : run_chunks(c, NULL, c->N, chunk);
             if (e) err = e;
         }
         np8o_end_sweep(c);

@@ -121,7 +121,14 @@ typedef struct {
     int32_t contraction;  /* NP8O_CONTRACT_*: arithmetic of the cluster likelihoods */
     int32_t req_max;      /* new clusters one step may create (0 -> NP8O_REQ_DEFAULT, <= NP8O_REQMAX) */
     int32_t pick;         /* NP8O_PICK_*: the categorical draw of a point update */
+    int32_t substeps;     /* data-parallel sweep (chunk = 0) in S synchronous sub-steps (0, 1 -> one step):
+                             sub-step s updates the items i with np8o_substep_of(seed, i, S) == s, in
+                             ascending s, each against the state the previous sub-steps left */
 } np8o_config;
+
+/* Sub-step of item i in a data-parallel sweep of S sub-steps: a fixed hash partition of the items
+ * (identical in noparama_amd/csrc/np8_device.h substep_of). */
+uint32_t np8o_substep_of(uint64_t seed, int64_t i, uint32_t S);
 
 /* Categorical draw of a point update.
  *   RESERVOIR: the specification (DESIGN.md "Pick"), what the HIP path runs.

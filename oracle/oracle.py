@@ -37,6 +37,7 @@ class _Config(C.Structure):
         ("contraction", C.c_int32),
         ("req_max", C.c_int32),
         ("pick", C.c_int32),
+        ("substeps", C.c_int32),
     ]
 
 
@@ -80,6 +81,8 @@ def lib():
         L.np8o_pick_reservoir.argtypes = [vp, i64, d]
         L.np8o_pick_reservoir.restype = i64
         L.np8o_pick_reservoir_batch.argtypes = [vp, i64, vp, i64, vp]
+        L.np8o_substep_of.argtypes = [u64, i64, u32]
+        L.np8o_substep_of.restype = u32
         L.np8o_lu_inverse_det.argtypes = [vp, C.c_int, vp, vp]
         L.np8o_similarity.argtypes = [vp, vp, i64, vp]
         L.np8o_create.argtypes = [P(_Config)]
@@ -198,6 +201,10 @@ def pick_reservoir_batch(lw, u):
     return out
 
 
+def substep_of(seed, i, S):
+    return lib().np8o_substep_of(seed, i, S)
+
+
 def set_threads(n):
     """OpenMP threads of the oracle's synchronous step (the cpu_par baseline); results unchanged."""
     lib().np8o_set_threads(int(n))
@@ -227,8 +234,9 @@ class Chain:
 
     def __init__(self, D, M=3, alpha=1.0, mu0=None, kappa=1.0 / 500, nu=4.0, Lambda=None, seed=0,
                  kcap=4096, chunk=0, param_update="frozen", mh_steps=20, prior="reference", contraction="f64",
-                 req_max=0, pick="reservoir"):
+                 req_max=0, pick="reservoir", substeps=1):
         cfg = _Config()
+        cfg.substeps = substeps
         cfg.req_max = req_max
         cfg.pick = PICK[pick]
         cfg.contraction = CONTRACTION[contraction]

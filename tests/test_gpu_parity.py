@@ -336,3 +336,51 @@ def test_sweep_graph_mh_g0_bit_exact():
     o.sweep(45)
     assert_same_state(g, o)
     assert g.stats()["mh_accepted"] == o.mh_accepted
+
+
+@pytest.mark.parametrize("S", [2, 8])
+def test_substeps_twogaussians_bit_exact(S):
+    """The data-parallel sweep in S synchronous sub-steps (np8_config.substeps, DESIGN.md "Sub-steps"):
+    sub-step s = the items with substep_of(seed, i, S) == s, a contiguous range of the layout sorted by
+    (sub-step, slot).  From the reference's init, eager sweeps then a graph replay, bit-exact."""
+    X, _ = datasets.twogaussians()
+    g, o = pair(2, 31, kcap=512, substeps=S)
+    for s in (g, o):
+        s.set_data(X)
+        s.init_random(20)
+    for n in (3, 20, 5):
+        g.sweep(n)
+        o.sweep(n)
+        assert_same_state(g, o)
+        assert_same_state(g, o, which=1)
+
+
+@pytest.mark.parametrize("S,param_update", [(4, "frozen"), (8, "frozen"), (8, "mh_g0")])
+def test_substeps_warm_c3_shape_bit_exact(S, param_update):
+    """C3's shape (D = 8, K = 64) from the warm state with candidate pruning across sub-steps (lists
+    rebuilt after every sub-step from the last sweep's radii) and the 20-sweep graph."""
+    X, z, mu, sig = datasets.mixture(20000, 8, 64, 0.8, 20.0, seed=8)
+    g, o = pair(8, 108, substeps=S, param_update=param_update)
+    for c in (g, o):
+        c.set_data(X)
+        c.set_state(z, mu, sig if param_update == "frozen" else sig * 4.0)
+    for n in (2, 21):
+        g.sweep(n)
+        o.sweep(n)
+        assert_same_state(g, o)
+    np.testing.assert_allclose(g.total_loglik(), o.total_loglik(), rtol=1e-11)
+
+
+def test_substeps_cold_start_bit_exact():
+    X = datasets.config_c3(N=100_000)[0]
+    O.set_threads(8)
+    g, o = pair(8, 29, substeps=8)
+    for s in (g, o):
+        s.set_data(X)
+        s.init_random(20)
+    for _ in range(3):
+        g.sweep(1)
+        o.sweep(1)
+        sg, so = g.state(params=False), o.state()
+        assert sg["K"] == so["K"] and np.array_equal(sg["z"], so["z"])
+    assert [g.stats()["new_clusters"], g.stats()["rejected_requests"]] == list(o.request_stats)
