@@ -44,6 +44,9 @@ def parse():
     ap.add_argument("--k", type=int, default=None, help="default: 64 (C3) / 256 (C5)")
     ap.add_argument("--seed", type=int, default=20261015)
     ap.add_argument("--kcap", type=int, default=0, help="cluster capacity (0: the library default)")
+    ap.add_argument("--exchange", default="auto", choices=["auto", "rccl"],
+                    help="rccl: with one GPU too, exchange the step records through a one-rank RCCL communicator "
+                         "(the multi-GPU code path, collectives captured in the sweep graph)")
     ap.add_argument("--substeps", type=int, default=1,
                     help="the data-parallel sweep as S synchronous sub-steps (np8_config.substeps)")
     ap.add_argument("--config", default="C3", help="config tag for the JSON line (BASELINE.json configs)")
@@ -139,6 +142,9 @@ def main():
             smp.close()
             smp = NealAlgorithm8(D, seed=args.seed, device=local_rank, param_update=args.param_update, **opts)
             smp.comm_init(None, rank, world)
+    if world == 1 and args.exchange == "rccl":
+        smp.comm_init(comm_unique_id(), 0, 1)
+        transport = "rccl"
     smp.set_data(X[lo:hi], offset=lo, n_global=N)
     if transport == "gloo":
         smp.set_state(z[lo:hi], mu, sig, counts=np.bincount(z, minlength=mu.shape[0]))

@@ -232,6 +232,23 @@ int np8_changes(np8_ctx *ctx, int64_t item_cap, int64_t *item, int32_t *slot, in
 int np8_update_points(np8_ctx *ctx, const int64_t *ids, int64_t n);
 int np8_end_sweep(np8_ctx *ctx);
 
+/* Checkpoint / resume: the complete chain state -- labels as slots, every slot's parameters
+ * and count, the epoch, the max-likelihood snapshot and its log-likelihood, the cumulative counters --
+ * as raw bits in a flat buffer of np8_checkpoint_bytes() bytes.  np8_restore on a context of the same
+ * configuration, seed and data (np8_set_data first) continues the chain bit for bit as if it had never
+ * stopped (every draw is a function of (seed, item, epoch); the slot layout is kept). */
+int64_t np8_checkpoint_bytes(np8_ctx *ctx);
+int np8_checkpoint(np8_ctx *ctx, void *out, int64_t bytes);
+int np8_restore(np8_ctx *ctx, const void *in, int64_t bytes);
+
+/* Debug invariants: every label names a live slot, the live slots' counts equal the label
+ * histogram (one rank) and sum to the global item count, K equals the live slots, the dense candidate
+ * table holds exactly the live slots.  out[0]: violated bits (1 labels, 2 histogram, 4 sum, 8 K/table),
+ * out[1] bad labels, out[2] slots whose count differs, out[3] the sum of counts.  NP8_ERR_STATE when
+ * violated.  With the environment variable NP8_DEBUG_INVARIANTS=1 the check also runs at the end of every
+ * sweep and a violation is reported by the next np8_sync. */
+int np8_check_invariants(np8_ctx *ctx, int64_t out[4]);
+
 /* Waits for queued work; returns the first device-side error since the last sync. */
 int np8_sync(np8_ctx *ctx);
 

@@ -153,6 +153,10 @@ struct np8_ctx {
     int64_t chg_cap = 0;
     unsigned long long *chg_count = nullptr;
     uint8_t *chg_flags = nullptr;
+    // debug invariants (np8_check_invariants; every sweep with NP8_DEBUG_INVARIANTS=1)
+    bool debug_inv = false;
+    int32_t *inv_hist = nullptr;
+    unsigned long long *inv_out = nullptr;
     std::string err;
 };
 
@@ -392,7 +396,8 @@ void free_device(np8_ctx *c) {
                     c->s_hist, c->s_cursor, c->s_off, c->slot_iso, c->acc, c->r2, c->wr2, c->plist, c->plen,
                     c->sm_hist, c->sm_mem, c->sm_off, c->sm_live, c->sm_Xm, c->sm_ownm, c->sm_cross, c->sm_ctl,
                     c->sm_typ, c->sm_slist, c->sm_stheta, c->stage, c->evalc, c->z_base, c->cnt_base,
-                    c->chg_slot, c->mu_base, c->sigma_base, c->chg_item, c->chg_count, c->chg_flags};
+                    c->chg_slot, c->mu_base, c->sigma_base, c->chg_item, c->chg_count, c->chg_flags,
+                    c->inv_hist, c->inv_out};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     if (c->sm_first_host) (void)hipHostFree(c->sm_first_host);
@@ -419,6 +424,8 @@ void free_device(np8_ctx *c) {
     c->chg_item = nullptr;
     c->chg_count = nullptr;
     c->chg_flags = nullptr;
+    c->inv_hist = nullptr;
+    c->inv_out = nullptr;
     c->chg_cap = 0;
     c->track = 0;
     c->plist = c->plen = nullptr;
@@ -453,12 +460,15 @@ int dalloc(np8_ctx *c, T **p, size_t n) {
 int alloc_records(np8_ctx *c) {
     const int64_t items = c->n_loc > 0 ? c->n_loc : 1;
     if (items > 0x7FFFFFFFll) return fail(c, NP8_ERR_ARG, "more than 2^31 items on one rank");
-    c->rec_cap = c->world > 1 ? c->req_max : (items > c->req_max ? items : c->req_max);
-    c->stage_cap = c->world > 1 ? items : 0;
+    // exchanged records (several ranks, or an RCCL communicator of any size): a rank sends at most req_max
+    // requests, its lowest scan positions (np8_req_select from the staging record)
+    const bool exch = c->world > 1 || c->comm;
+    c->rec_cap = exch ? c->req_max : (items > c->req_max ? items : c->req_max);
+    c->stage_cap = exch ? items : 0;
     c->rec_bytes = record_bytes(c->kcap, (int)c->rec_cap, c->D);
     int r = dalloc(c, &c->rec, (size_t)c->rec_bytes);
     if (r) return r;
-    if (c->world > 1) {
+    if (exch) {
         if ((r = dalloc(c, &c->gath, (size_t)c->rec_bytes * c->world)) ||
             (r = dalloc(c, &c->stage, (size_t)record_bytes(c->kcap, (int)c->stage_cap, c->D))))
             return r;
@@ -569,6 +579,7 @@ void collect_timers(np8_ctx *c) {
 
 FinArgs fin_args(np8_ctx *c, const unsigned char *recs, int world) {
     FinArgs F;
+    std::memset(&F, 0, sizeof(F));
     F.recs = recs;
     F.local_rec = c->rec;
     F.rec_bytes = c->rec_bytes;
@@ -715,6 +726,8 @@ int launch_finalize(np8_ctx *c, const unsigned char *recs, int world) {
     Timer t;
     timer_begin(c, 1, t);
     FinArgs F = fin_args(c, recs, world);
+    F.wr2 = c->wr2;
+    F.n_waves = c->collecting ? c->assign_waves : 0;
     HIPC(c, np8_launch_finalize(F, c->stream));
     if (c->prior == NP8_PRIOR_NIW) {  // the accepted auxiliaries' full parameters
         NiwArgs A = niw_args(c);
@@ -758,8 +771,6 @@ int launch_prune(np8_ctx *c, bool last) {
     P.cand = c->cand;
     P.ctl = c->ctl;
     P.r2 = c->r2;
-    P.wr2 = c->wr2;
-    P.n_waves = c->assign_waves;
     P.kcap = c->kcap;
     P.t = c->epoch - c->t_base;
     P.last = last ? 1 : 0;
@@ -835,8 +846,8 @@ int step(np8_ctx *c, int64_t p0, int64_t p1, const int64_t *order, bool use_perm
     }
     int r = launch_assign(c, p0, p1, order, use_perm);
     if (r) return r;
-    if (c->world > 1) {
-        if (!c->comm) return fail(c, NP8_ERR_STATE, "host-exchange mode: use np8_step_local/np8_step_merge");
+    if (c->world > 1 && !c->comm) return fail(c, NP8_ERR_STATE, "host-exchange mode: use np8_step_local/np8_step_merge");
+    if (c->comm) {  // the exchange over RCCL (also with a one-rank communicator)
         HIPC(c, np8_launch_req_select(c->stage, c->stage_cap, c->rec, c->rec_cap, c->kcap, c->D, c->req_max, c->stream));
         NCCLC(c, ncclAllGather(c->rec, c->gath, (size_t)c->rec_bytes, ncclUint8, c->comm, c->stream));
         r = launch_finalize(c, c->gath, c->world);
@@ -871,7 +882,7 @@ int population(np8_ctx *c) {
             int r = step(c, p0, p1, nullptr, !sync);
             if (r) return r;
         }
-    } else if (c->world > 1) {
+    } else if (c->comm) {
         return step(c, 0, 0, nullptr, false);  // still take part in the exchange
     }
     return NP8_OK;
@@ -906,7 +917,7 @@ int launch_total_loglik(np8_ctx *c) {
         HIPC(c, np8_launch_loglik_wide_mfma(W, c->D, c->partial, c->stream));
     } else
         HIPC(c, np8_launch_loglik(A, c->D, c->stream));
-    const bool sum_ranks = c->world > 1 && c->comm;
+    const bool sum_ranks = c->comm != nullptr;
     HIPC(c, np8_launch_loglik_reduce(c->partial, (c->n_loc + 255) / 256, &c->ctl->L_local,
                                      sum_ranks ? nullptr : &c->ctl->L, c->stream));
     if (sum_ranks) NCCLC(c, ncclAllReduce(&c->ctl->L_local, &c->ctl->L, 1, ncclFloat64, ncclSum, c->comm, c->stream));
@@ -974,7 +985,7 @@ int param_update(np8_ctx *c, int stats_mode = 0) {
         timer_end(c, t);
         return NP8_OK;
     }
-    if (stats_mode == 0 && c->world > 1)
+    if (stats_mode == 0 && c->comm)
         NCCLC(c, ncclAllReduce(c->acc, c->acc, nacc, ncclFloat64, ncclSum, c->comm, c->stream));
     if (c->param_update == NP8_PARAM_NIW_CONJUGATE)
         HIPC(c, np8_launch_niw_post(niw_args(c), c->kcap, c->stream));
@@ -986,6 +997,14 @@ int param_update(np8_ctx *c, int stats_mode = 0) {
     return NP8_OK;
 }
 
+int launch_invariants(np8_ctx *c) {
+    int r = 0;
+    if (!c->inv_hist && ((r = dalloc(c, &c->inv_hist, (size_t)c->kcap)) || (r = dalloc(c, &c->inv_out, 4)))) return r;
+    HIPC(c, np8_launch_invariants(c->z, c->n_loc, c->cnt, c->dense_of, c->cand, c->CS, c->D, c->kcap, c->n_glob,
+                                  c->world == 1 ? 1 : 0, c->inv_hist, c->inv_out, c->ctl, c->stream));
+    return NP8_OK;
+}
+
 int end_sweep(np8_ctx *c, bool stats_given = false) {
     int r0 = param_update(c, stats_given ? 2 : 0);
     if (r0) return r0;
@@ -994,6 +1013,7 @@ int end_sweep(np8_ctx *c, bool stats_given = false) {
         if (r0) return r0;
         c->collecting = false;
     }
+    if (c->debug_inv && (r0 = launch_invariants(c))) return r0;
     if (c->epoch % 5u == 0u) {  // np_mcmc.cpp:172-174
         int r = launch_total_loglik(c);
         if (r) return r;
@@ -1055,7 +1075,8 @@ void drop_graph(np8_ctx *c) {
 }
 
 bool graph_eligible(np8_ctx *c, bool sync) {
-    return sync && !c->graphs_off && c->world == 1 && c->n_loc > 0 && c->sorted_valid &&
+    // sharded runs are captured with their RCCL collectives; the host-exchange path is not (host transport)
+    return sync && !c->graphs_off && (c->world == 1 || c->comm) && c->n_loc > 0 && c->sorted_valid &&
            (!c->prune_on || (c->lists_valid && c->r2_zero && (c->substeps == 1 || c->r2_prev_ok)));
 }
 
@@ -1167,6 +1188,7 @@ int np8_create(np8_ctx **out, const np8_config *cfg) {
     }
     c->req_max = cfg->req_max > 0 ? cfg->req_max : NP8_REQ_DEFAULT;
     c->substeps = cfg->substeps > 1 ? cfg->substeps : 1;
+    c->debug_inv = std::getenv("NP8_DEBUG_INVARIANTS") != nullptr && std::getenv("NP8_DEBUG_INVARIANTS")[0] == '1';
     // the label-sorted layout is sorted by (sub-step, slot): substeps * kcap bins in the sort's LDS
     if (cfg->substeps < 0 || cfg->substeps > NP8_SUBSTEPS_MAX || (int64_t)c->substeps * c->kcap > 16384) {
         delete c;
@@ -1424,7 +1446,7 @@ int np8_set_state_counts(np8_ctx *c, const int32_t *z, int32_t K, const double *
     }
     if (c->world > 1 && !c->comm)
         return fail(c, NP8_ERR_STATE, "np8_set_state: host-exchange mode needs np8_set_state_counts");
-    if (c->world > 1) {  // counts are global
+    if (c->comm) {  // counts are global
         int32_t *d = nullptr;
         HIPC(c, hipMalloc(&d, sizeof(int32_t) * K));
         HIPC(c, hipMemcpy(d, cnt.data(), sizeof(int32_t) * K, hipMemcpyHostToDevice));
@@ -1504,6 +1526,153 @@ int np8_sweep(np8_ctx *c, int32_t n_sweeps) {
         r = end_sweep(c);
         if (r) return r;
     }
+    return NP8_OK;
+}
+
+int np8_check_invariants(np8_ctx *c, int64_t out[4]) {
+    if (!c || !out) return NP8_ERR_ARG;
+    if (!c->have_state) return fail(c, NP8_ERR_STATE, "np8_check_invariants: no state");
+    int r = launch_invariants(c);
+    if (r) return r;
+    unsigned long long h[4];
+    HIPC(c, hipMemcpyAsync(h, c->inv_out, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+    HIPC(c, hipMemsetAsync(c->inv_out, 0, sizeof(h), c->stream));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    for (int k = 0; k < 4; ++k) out[k] = (int64_t)h[k];
+    if (h[0]) {
+        Ctl tmp;
+        (void)read_ctl(c, &tmp);
+        int32_t zero = 0;
+        HIPC(c, hipMemcpy(&c->ctl->err, &zero, sizeof(zero), hipMemcpyHostToDevice));
+        return fail(c, NP8_ERR_STATE, "np8_check_invariants: violated (bits " + std::to_string(h[0]) + ")");
+    }
+    return NP8_OK;
+}
+
+}  // extern "C"
+
+namespace {
+// Checkpoint layout: header, then z [n_loc] int32 (slots), cnt [kcap] int32, slot_mu, slot_P, slot_c,
+// slot_sigma, slot_iso, z_best, cnt_best, mu_best, sigma_best -- raw device bits.
+struct CkptHeader {
+    char magic[8];
+    int32_t D, M, kcap, substeps, prior, contraction, checks, have_best;
+    int64_t n_loc, offset, n_glob, n_new, n_rejected, mh_accepted;
+    uint64_t seed;
+    uint32_t epoch, pad;
+    double L, best[2];
+};
+
+struct CkptPart {
+    void *dev;
+    size_t bytes;
+};
+
+std::vector<CkptPart> ckpt_parts(np8_ctx *c) {
+    const size_t kc = (size_t)c->kcap, D = (size_t)c->D, DP = (size_t)c->DP, n = (size_t)c->n_loc;
+    return {{c->z, 4 * n},
+            {c->cnt, 4 * kc},
+            {c->slot_mu, 8 * kc * D},
+            {c->slot_P, 8 * kc * DP},
+            {c->slot_c, 8 * kc},
+            {c->slot_sigma, 8 * kc * D * D},
+            {c->slot_iso, 8 * kc},
+            {c->z_best, 4 * n},
+            {c->cnt_best, 4 * kc},
+            {c->mu_best, 8 * kc * D},
+            {c->sigma_best, 8 * kc * D * D}};
+}
+}  // namespace
+
+extern "C" {
+
+int64_t np8_checkpoint_bytes(np8_ctx *c) {
+    if (!c || !c->have_data) return 0;
+    int64_t b = (int64_t)sizeof(CkptHeader);
+    for (const CkptPart &p : ckpt_parts(c)) b += (int64_t)p.bytes;
+    return b;
+}
+
+int np8_checkpoint(np8_ctx *c, void *out, int64_t bytes) {
+    if (!c || !out) return NP8_ERR_ARG;
+    if (!c->have_state) return fail(c, NP8_ERR_STATE, "np8_checkpoint: no state");
+    if (bytes < np8_checkpoint_bytes(c)) return fail(c, NP8_ERR_ARG, "np8_checkpoint: buffer too small");
+    Ctl h;
+    int r = read_ctl(c, &h);
+    if (r) return r;
+    CkptHeader H;
+    std::memset(&H, 0, sizeof(H));
+    std::memcpy(H.magic, "NP8CKPT1", 8);
+    H.D = c->D;
+    H.M = c->M;
+    H.kcap = c->kcap;
+    H.substeps = c->substeps;
+    H.prior = c->prior;
+    H.contraction = c->contraction;
+    H.checks = c->checks;
+    H.have_best = h.have_best;
+    H.n_loc = c->n_loc;
+    H.offset = c->offset;
+    H.n_glob = c->n_glob;
+    H.n_new = h.n_new;
+    H.n_rejected = h.n_rejected;
+    H.mh_accepted = h.mh_accepted;
+    H.seed = c->seed;
+    H.epoch = c->epoch;
+    H.L = h.L;
+    H.best[0] = h.best[0];
+    H.best[1] = h.best[1];
+    unsigned char *o = static_cast<unsigned char *>(out);
+    std::memcpy(o, &H, sizeof(H));
+    o += sizeof(H);
+    for (const CkptPart &p : ckpt_parts(c)) {
+        HIPC(c, hipMemcpy(o, p.dev, p.bytes, hipMemcpyDeviceToHost));
+        o += p.bytes;
+    }
+    return NP8_OK;
+}
+
+int np8_restore(np8_ctx *c, const void *in, int64_t bytes) {
+    if (!c || !in) return NP8_ERR_ARG;
+    if (!c->have_data) return fail(c, NP8_ERR_STATE, "np8_restore: no data (np8_set_data with the same items first)");
+    if (bytes < (int64_t)sizeof(CkptHeader) || bytes != np8_checkpoint_bytes(c))
+        return fail(c, NP8_ERR_ARG, "np8_restore: size differs from this context's checkpoint");
+    CkptHeader H;
+    std::memcpy(&H, in, sizeof(H));
+    if (std::memcmp(H.magic, "NP8CKPT1", 8) != 0 || H.D != c->D || H.M != c->M || H.kcap != c->kcap ||
+        H.substeps != c->substeps || H.prior != c->prior || H.contraction != c->contraction || H.n_loc != c->n_loc ||
+        H.offset != c->offset || H.n_glob != c->n_glob || H.seed != c->seed)
+        return fail(c, NP8_ERR_ARG, "np8_restore: checkpoint of another configuration, seed or data shard");
+    drop_graph(c);
+    HIPC(c, hipStreamSynchronize(c->stream));
+    const unsigned char *p = static_cast<const unsigned char *>(in) + sizeof(H);
+    for (const CkptPart &q : ckpt_parts(c)) {
+        HIPC(c, hipMemcpy(q.dev, p, q.bytes, hipMemcpyHostToDevice));
+        p += q.bytes;
+    }
+    c->sorted_valid = false;
+    c->use_sorted = false;
+    c->lists_valid = c->r2_zero = c->collecting = false;
+    c->epoch = H.epoch;
+    c->checks = H.checks;
+    c->t_base = H.epoch;
+    Ctl h;
+    std::memset(&h, 0, sizeof(h));
+    h.have_best = H.have_best;
+    h.n_new = H.n_new;
+    h.n_rejected = H.n_rejected;
+    h.mh_accepted = H.mh_accepted;
+    h.L = H.L;
+    h.best[0] = H.best[0];
+    h.best[1] = H.best[1];
+    h.t_base = H.epoch;
+    HIPC(c, hipMemcpyAsync(c->ctl, &h, sizeof(h), hipMemcpyHostToDevice, c->stream));  // (stream-ordered)
+    HIPC(c, hipStreamSynchronize(c->stream));
+    c->have_state = true;
+    int r = rebuild(c);  // the dense table from the restored slots
+    if (r) return r;
+    if ((r = refresh_wide(c, true))) return r;
+    HIPC(c, hipStreamSynchronize(c->stream));
     return NP8_OK;
 }
 
@@ -1671,6 +1840,8 @@ int np8_sync(np8_ctx *c) {
         if (h.err & kErrSigma)
             return fail(c, NP8_ERR_SIGMA, "a cluster precision is not numerically positive definite (wide path factor)");
         if (h.err & kErrCapacity) return fail(c, NP8_ERR_CAPACITY, "a device table is full");
+        if (h.err & kErrInvariant)
+            return fail(c, NP8_ERR_STATE, "a debug invariant failed (np8_check_invariants: labels, counts, K, table)");
     }
     return NP8_OK;
 }

@@ -43,7 +43,7 @@ struct Ctl {
 // of the grid serialises the atomics in one L2 channel (4x the kernel time at C3).
 constexpr int kEvalSlots = 1024;
 
-enum : int32_t { kErrCapacity = 1, kErrSigma = 2 };
+enum : int32_t { kErrCapacity = 1, kErrSigma = 2, kErrInvariant = 4 };
 
 // Exchange record of one rank for one synchronous step:
 //   RecHeader | int32 delta[kcap] | Request req[rec_cap] | double vmu[rec_cap][D+1]
@@ -144,8 +144,6 @@ struct PruneArgs {
     const double *cand;
     Ctl *ctl;
     double *r2;         // [2][kcap]: buffer (epoch & 1) collects this sweep, the other holds the last sweep
-    const WaveR2 *wr2;  // per-wave maxima of the step just assigned (AssignArgs::wr2), n_waves of them
-    int64_t n_waves;
     int32_t *plist, *plen;
     int32_t ls, D, kcap;
     uint32_t t;     // epoch offset: epoch = ctl->t_base + t
@@ -170,7 +168,11 @@ struct FinArgs {
     double gp_iso;  // common diagonal of Gp when (L^T L)^{-1} is a multiple of I, else 0
     uint64_t seed;
     uint32_t t;  // epoch offset: epoch = ctl->t_base + t
-    double *r2;  // pruning radii: +inf for every slot created here (unknown radius)
+    double *r2;  // pruning radii [2][kcap]: +inf for every slot created here (unknown radius)
+    // the radius records of the step's assign waves (n_waves; 0 when the step collects none): folded into
+    // this sweep's radius buffer here, by the only block, at one atomic per 64 records of one slot
+    const WaveR2 *wr2;
+    int64_t n_waves;
     // NIW prior: accepted requests are listed in pend[4 q] = (byte offset of the request's record
     // payload in recs, item, m, slot) for np8_niw_aux_slots instead of being written here
     int32_t prior, req_max;  // req_max: new clusters one step may create
@@ -354,6 +356,13 @@ hipError_t np8_launch_niw_post(const np8::NiwArgs &A, int nblocks, hipStream_t s
 hipError_t np8_launch_niw_aux_slots(const np8::NiwArgs &A, hipStream_t s);
 hipError_t np8_launch_resort(const SortArgs &S, hipStream_t s);
 hipError_t np8_launch_assign(const np8::AssignArgs &A, int D, int M, int prior, hipStream_t s);
+// Debug invariants (np8_config / NP8_DEBUG_INVARIANTS): every label a live slot, the live slots' counts the
+// label histogram (one rank) and summing to n_global, K the live slots, the dense table live slots only.
+// Violations: bits in out[0] (1 label out of range or in an empty slot, 2 histogram != counts, 4 sum of
+// counts != n_global, 8 K or the dense table wrong), counts in out[1..3]; ctl->err |= kErrInvariant.
+hipError_t np8_launch_invariants(const int32_t *z, int64_t n, const int32_t *cnt, const int32_t *dense_of,
+                                 const double *cand, int CS, int D, int kcap, int64_t n_global, int check_hist,
+                                 int32_t *hist, unsigned long long *out, np8::Ctl *ctl, hipStream_t s);
 // Membership change log (np8_changes): items whose slot differs from the baseline (wave-aggregated append,
 // out[0..cap) kept, *count = all of them), and per slot 0 / 1 created / 2 removed / 3 parameters changed.
 hipError_t np8_launch_changes(const int32_t *z, const int32_t *z_base, int64_t n, int64_t *out_item, int32_t *out_slot,

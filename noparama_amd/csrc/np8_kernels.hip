@@ -908,6 +908,41 @@ __global__ __launch_bounds__(kFinThreads) void np8_finalize(FinArgs F) {
         s_flags[0] = n;
         s_flags[1] = 0;
     }
+    if (F.n_waves > 0) {  // the step's radius records into this sweep's buffer (before any slot is created)
+        // folded in LDS (the request-key area, free until the requests are read; pruning runs with
+        // kcap <= kPruneMaxKcap <= kReqMax), one LDS atomic per 64 records of one slot, then written back
+        // with plain stores: this block is the only writer
+        unsigned long long *fold = reinterpret_cast<unsigned long long *>(keys);
+        for (int s = tid; s < kcap; s += kFinThreads) fold[s] = 0ull;
+        __syncthreads();
+        const int lane = tid & 63;
+        for (int64_t w0 = (int64_t)(tid >> 6) * 64; w0 < F.n_waves; w0 += kFinThreads) {
+            const int64_t w = w0 + lane;
+            WaveR2 r;
+            r.slot = -1;
+            r.d2 = 0.0;
+            if (w < F.n_waves) r = F.wr2[w];
+            const unsigned long long b = (unsigned long long)__double_as_longlong(r.d2);
+            const int32_t s_first = __builtin_amdgcn_readfirstlane(r.slot);
+            if (__ballot(r.slot != s_first && w < F.n_waves) == 0ull) {  // one slot: one atomic
+                unsigned long long m = b;
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) {
+                    const unsigned long long v = __shfl_xor(m, o);
+                    m = v > m ? v : m;
+                }
+                if (lane == 0 && s_first >= 0) atomicMax(fold + s_first, m);
+            } else if (r.slot >= 0) {
+                atomicMax(fold + r.slot, b);
+            }
+        }
+        __syncthreads();
+        unsigned long long *cur = reinterpret_cast<unsigned long long *>(
+            F.r2 + (int64_t)((F.ctl->t_base + F.t) & 1u) * kcap);
+        for (int s = tid; s < kcap; s += kFinThreads)
+            if (fold[s] > cur[s]) cur[s] = fold[s];
+        __syncthreads();
+    }
     for (int s = s0; s < s1; ++s) {
         int c = F.cnt[s];
         for (int r = 0; r < F.world; ++r) c += rec_delta(F, r)[s];
@@ -1402,6 +1437,69 @@ hipError_t np8_launch_assign(const AssignArgs &A, int D, int M, int prior, hipSt
     return hipErrorInvalidValue;
 }
 
+// ---- debug invariants (np8_check_invariants) -----------------------------------------------------------
+__global__ __launch_bounds__(256) void np8_inv_items(const int32_t *__restrict__ z, int64_t n, const int32_t *__restrict__ cnt,
+                                                     int kcap, int32_t *__restrict__ hist, unsigned long long *out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int32_t s = z[i];
+    if (s < 0 || s >= kcap || cnt[s] <= 0) {
+        atomicOr(out, 1ull);
+        atomicAdd(out + 1, 1ull);
+        return;
+    }
+    atomicAdd(hist + s, 1);
+}
+
+__global__ __launch_bounds__(1024) void np8_inv_slots(const int32_t *__restrict__ cnt, const int32_t *__restrict__ dense_of,
+                                                      const double *__restrict__ cand, int CS, int D, int kcap,
+                                                      int64_t n_global, int check_hist, int32_t *__restrict__ hist,
+                                                      unsigned long long *out, Ctl *ctl) {
+    __shared__ unsigned long long tot, live;
+    __shared__ int bad;
+    if (threadIdx.x == 0) {
+        tot = live = 0ull;
+        bad = 0;
+    }
+    __syncthreads();
+    const int DP = D * (D + 1) / 2;
+    for (int s = threadIdx.x; s < kcap; s += blockDim.x) {
+        const int c = cnt[s];
+        if (c > 0) {
+            atomicAdd(&tot, (unsigned long long)c);
+            atomicAdd(&live, 1ull);
+            const int r = dense_of[s];  // the dense row of a live slot names the slot back
+            if (r < 0 || (int)cand[(int64_t)r * CS + D + DP + kFieldSlot] != s) atomicOr(&bad, 8);
+        } else if (dense_of[s] >= 0) {
+            atomicOr(&bad, 8);
+        }
+        if (check_hist && hist[s] != (c > 0 ? c : 0)) {
+            atomicOr(&bad, 2);
+            atomicAdd(out + 2, 1ull);
+        }
+        hist[s] = 0;  // ready for the next check
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int b = bad;
+        if ((int64_t)tot != n_global) b |= 4;
+        if ((int64_t)live != ctl->K) b |= 8;
+        out[3] = tot;
+        if (b) atomicOr(out, (unsigned long long)b);
+        if (b || out[0]) atomicOr(&ctl->err, kErrInvariant);
+    }
+}
+
+hipError_t np8_launch_invariants(const int32_t *z, int64_t n, const int32_t *cnt, const int32_t *dense_of,
+                                 const double *cand, int CS, int D, int kcap, int64_t n_global, int check_hist,
+                                 int32_t *hist, unsigned long long *out, Ctl *ctl, hipStream_t s) {
+    if (n > 0)
+        hipLaunchKernelGGL(np8_inv_items, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, z, n, cnt, kcap, hist, out);
+    hipLaunchKernelGGL(np8_inv_slots, dim3(1), dim3(1024), 0, s, cnt, dense_of, cand, CS, D, kcap, n_global, check_hist,
+                       hist, out, ctl);
+    return hipGetLastError();
+}
+
 // ---- membership change log (np8_changes) --------------------------------------------------------------
 // One lane per item; a wave with moved items takes its output range with one atomic.
 __global__ __launch_bounds__(256) void np8_changes_items(const int32_t *__restrict__ z, const int32_t *__restrict__ zb,
@@ -1580,53 +1678,23 @@ hipError_t np8_launch_mh_g0(const ParamArgs &A, hipStream_t s) {
 // Standalone pass (after the mh_g0 update has moved means): four rows per block.
 // A small grid strides over the live rows (one wave per row): K is only known on the device, and a
 // grid sized for kcap would mostly launch blocks that exit at once.
-// Every block first folds the step's per-wave radius records into an LDS table (each thread walks a
-// contiguous run of records and flushes its running maximum when the slot changes: in the label-sorted
-// layout consecutive waves share their slot, so a run costs one or two LDS atomics); block 0 adds the
-// fold to this sweep's radii.  Radius of a row (DESIGN.md "Candidate pruning"):
+// Radius of a row (DESIGN.md "Candidate pruning"; np8_finalize has folded the step's wave records in):
 //   after an intermediate sub-step: the last sweep's radii -- the items of the sub-steps still to come
 //     sit where the last sweep left them (they move only in their own sub-step);
-//   after the sweep's last step: this sweep's radii including the fold -- every item has been placed;
-//     block 0 then clears the last sweep's buffer, which collects the next sweep.
+//   after the sweep's last step: this sweep's radii -- every item has been placed; block 0 then clears the
+//     last sweep's buffer, which collects the next sweep.
 template <int DT>
 __global__ __launch_bounds__(256) void np8_prune(PruneArgs A) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    unsigned long long *lr2 = reinterpret_cast<unsigned long long *>(smem);
     const int K = A.ctl->K;
     if (blockIdx.x == 0 && threadIdx.x == 0) A.ctl->lists_ok = 1;
-    for (int s = threadIdx.x; s < A.kcap; s += blockDim.x) lr2[s] = 0ull;
-    __syncthreads();
-    const int64_t per = (A.n_waves + blockDim.x - 1) / blockDim.x;
-    const int64_t w0 = (int64_t)threadIdx.x * per, w1 = (w0 + per < A.n_waves) ? w0 + per : A.n_waves;
-    int32_t cs = -1;
-    unsigned long long cm = 0ull;
-    for (int64_t w = w0; w < w1; ++w) {
-        const WaveR2 r = A.wr2[w];
-        if (r.slot != cs) {
-            if (cs >= 0) atomicMax(&lr2[cs], cm);
-            cs = r.slot;
-            cm = 0ull;
-        }
-        // non-negative doubles order like their bit patterns
-        const unsigned long long b = (unsigned long long)__double_as_longlong(r.d2);
-        cm = b > cm ? b : cm;
-    }
-    if (cs >= 0) atomicMax(&lr2[cs], cm);
-    __syncthreads();
     const uint32_t par = (A.ctl->t_base + A.t) & 1u;
-    unsigned long long *cur = reinterpret_cast<unsigned long long *>(A.r2 + (int64_t)par * A.kcap);
-    const double *prev = A.r2 + (int64_t)(par ^ 1u) * A.kcap;
-    if (blockIdx.x == 0) {
-        for (int s = threadIdx.x; s < A.kcap; s += blockDim.x) {
-            if (lr2[s] > cur[s]) cur[s] = lr2[s];
-            if (A.last) reinterpret_cast<unsigned long long *>(A.r2 + (int64_t)(par ^ 1u) * A.kcap)[s] = 0ull;
-        }
+    const double *cur = A.r2 + (int64_t)par * A.kcap, *prev = A.r2 + (int64_t)(par ^ 1u) * A.kcap;
+    const double *src = A.last ? cur : prev;
+    if (A.last && blockIdx.x == 0) {  // no block reads prev in this pass
+        double *clr = A.r2 + (int64_t)(par ^ 1u) * A.kcap;
+        for (int s = threadIdx.x; s < A.kcap; s += blockDim.x) clr[s] = 0.0;
     }
-    // (other blocks may read cur while block 0 raises it: either value, maxed with their own fold, is the same)
-    const bool last = A.last != 0;
-    auto R2of = [&](int slot) {
-        return last ? __longlong_as_double((long long)(cur[slot] > lr2[slot] ? cur[slot] : lr2[slot])) : prev[slot];
-    };
+    auto R2of = [&](int slot) { return src[slot]; };
     for (int k0 = blockIdx.x * 4 + (threadIdx.x >> 6); k0 < K; k0 += gridDim.x * 4)  // wave-uniform
         prune_row<DT>(A.cand, R2of, A.plist, A.plen, A.ls, A.D, K, k0);
 }
@@ -1639,7 +1707,7 @@ hipError_t np8_launch_prune(const PruneArgs &A, int kcap, hipStream_t s) {
     switch (A.D) {
 #define Y(d)                                                              \
     case d:                                                               \
-        hipLaunchKernelGGL((np8_prune<d>), g, dim3(256), sizeof(double) * A.kcap, s, A); \
+        hipLaunchKernelGGL((np8_prune<d>), g, dim3(256), 0, s, A);        \
         break;
         Y(1) Y(2) Y(3) Y(4) Y(8) Y(16)
 #undef Y

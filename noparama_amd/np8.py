@@ -141,6 +141,10 @@ def lib():
         "np8_update_points": ([vp, vp, i64], i32),
         "np8_end_sweep": ([vp], i32),
         "np8_population_sweep": ([vp], i32),
+        "np8_checkpoint_bytes": ([vp], i64),
+        "np8_checkpoint": ([vp, vp, i64], i32),
+        "np8_restore": ([vp, vp, i64], i32),
+        "np8_check_invariants": ([vp, vp], i32),
         "np8_track_changes": ([vp, i32], i32),
         "np8_changes": ([vp, i64, vp, vp, vp, vp, vp, vp, vp, vp], i32),
         "np8_sync": ([vp], i32),
@@ -386,6 +390,27 @@ class NealAlgorithm8:
         """End the sweep with the statistics summed over ranks (parameter update, bookkeeping)."""
         summed = np.ascontiguousarray(summed, dtype=np.float64)
         self._check(lib().np8_end_sweep_stats(self._h, _p(summed)))
+
+    def checkpoint(self):
+        """The complete chain state as bytes (np8_checkpoint); restore() continues it bit for bit."""
+        n = int(lib().np8_checkpoint_bytes(self._h))
+        buf = np.zeros(n, dtype=np.uint8)
+        self._check(lib().np8_checkpoint(self._h, _p(buf), n))
+        return buf.tobytes()
+
+    def restore(self, ckpt):
+        """Continue the chain of a checkpoint (same configuration, seed and data: set_data first)."""
+        buf = np.frombuffer(ckpt, dtype=np.uint8).copy()
+        self._check(lib().np8_restore(self._h, _p(buf), buf.size))
+
+    def check_invariants(self, raise_on_violation=True):
+        """Debug invariants (np8_check_invariants): [violated bits, bad labels, slots with a wrong count,
+        sum of counts]."""
+        out = np.zeros(4, dtype=np.int64)
+        r = lib().np8_check_invariants(self._h, _p(out))
+        if r and raise_on_violation:
+            self._check(r)
+        return out
 
     def population_sweep(self):
         """The population update of one sweep without the end-of-sweep step (np8_population_sweep)."""

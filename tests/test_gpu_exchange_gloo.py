@@ -1,8 +1,8 @@
-"""The multi-rank path of np8_sweep in separate processes: RCCL (np8_comm_init + one ncclAllGather per
-sweep) where the platform allows it, otherwise the same exchange records moved over gloo
-(np8_step_local / np8_step_merge).  The driver's scaling runs use one GPU per rank; this box has
-one GPU, where RCCL refuses two ranks on the same device, so the gloo transport is what runs here.
-Either way the sharded result must equal the single-rank sweep bit for bit."""
+"""The multi-rank exchange in two processes on this box's one GPU: RCCL refuses two ranks on the same
+device, so what runs here is the host-exchange transport -- the same per-step records moved over gloo
+(np8_step_local / np8_step_merge).  (The RCCL code path itself runs in tests/test_gpu_rccl_one_rank.py with
+a one-rank communicator; the driver's scaling runs use one GPU per rank.)  The sharded result must equal
+the single-rank sweep bit for bit."""
 import os
 import socket
 

@@ -1,0 +1,39 @@
+"""The RCCL exchange path on one GPU: a one-rank communicator (np8_comm_init with world = 1) sends every
+step's record through ncclAllGather, the max-likelihood sum and the parameter statistics through
+ncclAllReduce, and runs of 20 sweeps replay a hipGraph with those collectives captured -- the code the
+driver's multi-GPU runs execute on each rank.  Results must equal the oracle bit for bit."""
+import numpy as np
+import pytest
+
+import oracle as O
+from noparama_amd import NealAlgorithm8, comm_unique_id, datasets
+
+pytestmark = pytest.mark.gpu
+
+
+def assert_same(g, o, which=0):
+    a, b = g.state(which), o.state(which)
+    assert a["K"] == b["K"] and np.array_equal(a["z"], b["z"]) and np.array_equal(a["counts"], b["counts"])
+    np.testing.assert_allclose(a["mu"], b["mu"], rtol=1e-13, atol=1e-13)
+
+
+@pytest.mark.parametrize("param_update,substeps", [("frozen", 1), ("mh_g0", 1), ("frozen", 4)])
+def test_one_rank_rccl_sweeps_and_graph_bit_exact(param_update, substeps):
+    X, z, mu, sig = datasets.mixture(20000, 8, 24, 0.8, 12.0, seed=3)
+    g = NealAlgorithm8(8, seed=71, kcap=1024, device=0, param_update=param_update, substeps=substeps)
+    o = O.Chain(8, seed=71, kcap=1024, param_update=param_update, substeps=substeps)
+    try:
+        g.comm_init(comm_unique_id(), 0, 1)
+        for c in (g, o):
+            c.set_data(X)
+            c.init_random(20)
+        for n in (3, 20, 22):  # eager, one graph replay, graph + eager
+            g.sweep(n)
+            o.sweep(n)
+            assert_same(g, o)
+            assert_same(g, o, which=1)
+        np.testing.assert_allclose(g.stats()["best_loglik"], o.best_loglik(), rtol=1e-11)
+        if param_update == "mh_g0":
+            assert g.stats()["mh_accepted"] == o.mh_accepted
+    finally:
+        g.close()
