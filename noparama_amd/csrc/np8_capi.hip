@@ -26,6 +26,7 @@ namespace {
 
 constexpr double kLog2PiC = 1.8378770664093454835606594728112;
 constexpr int kPruneMaxKcap = 4096;  // kcap x kcap int32 candidate lists (64 MB at the limit)
+constexpr uint32_t kGatherEvery = 4;  // data-parallel sweeps per gathering of fresh pruning radii
 
 struct Timer {
     hipEvent_t a = nullptr, b = nullptr;
@@ -63,10 +64,11 @@ struct np8_ctx {
     unsigned long long *evalc = nullptr;  // [kEvalSlots][2] executed-work counters (timing mode)
     bool prune_on = false;     // kcap small enough for kcap x kcap lists
     bool lists_valid = false;  // plist/plen describe the current table and membership
-    bool r2_zero = false;      // the radius buffers are in a consistent collecting state (cleared at (re)start)
-    bool collecting = false;   // the running sweep collects r2 (a whole synchronous sweep)
-    bool r2_prev_ok = false;   // the last sweep's radius buffer is complete (intermediate sub-step prunes)
+    bool r2_zero = false;      // the radii in use are initialised (cleared at (re)start: every lane walks all)
+    bool collecting = false;   // the running sweep prunes (a data-parallel sweep): lists after every step
+    bool gather = false;       // ... and gathers fresh radii (every kGatherEvery-th sweep, or after a restart)
     int64_t assign_waves = 0;  // waves of the last assign launch (its radius records)
+    double *plr2 = nullptr;    // per dense row: the squared radius its candidate list assumes
     // data-parallel sweep in `substeps` synchronous sub-steps (np8_config.substeps): sub-step s is the
     // contiguous range [sub_start[s], sub_start[s+1]) of the label-sorted layout (sorted by sub-step, slot)
     int substeps = 1;
@@ -393,7 +395,7 @@ void free_device(np8_ctx *c) {
                     c->cnt,    c->cnt_best, c->mu_best, c->sigma_best, c->cand, c->ctl,    c->hyp,
                     c->d_mu0,  c->d_LT,    c->d_Gp,   c->d_LTL,   c->rec,     c->gath,    c->order,
                     c->partial, c->dense_of, c->Xs[0], c->Xs[1], c->zs[0], c->zs[1], c->ids[0], c->ids[1],
-                    c->s_hist, c->s_cursor, c->s_off, c->slot_iso, c->acc, c->r2, c->wr2, c->plist, c->plen,
+                    c->s_hist, c->s_cursor, c->s_off, c->slot_iso, c->acc, c->r2, c->wr2, c->plist, c->plen, c->plr2,
                     c->sm_hist, c->sm_mem, c->sm_off, c->sm_live, c->sm_Xm, c->sm_ownm, c->sm_cross, c->sm_ctl,
                     c->sm_typ, c->sm_slist, c->sm_stheta, c->stage, c->evalc, c->z_base, c->cnt_base,
                     c->chg_slot, c->mu_base, c->sigma_base, c->chg_item, c->chg_count, c->chg_flags,
@@ -429,6 +431,7 @@ void free_device(np8_ctx *c) {
     c->chg_cap = 0;
     c->track = 0;
     c->plist = c->plen = nullptr;
+    c->plr2 = nullptr;
     c->X = nullptr;
     c->z = c->z_best = nullptr;
     c->slot_mu = c->slot_P = c->slot_c = c->slot_sigma = nullptr;
@@ -711,6 +714,7 @@ AssignArgs assign_args(np8_ctx *c, int64_t p0, int64_t p1, const int64_t *order,
     A.kcap = c->kcap;
     A.plist = c->plist;
     A.plen = c->plen;
+    A.plr2 = c->plr2;
     A.ls = c->kcap;
     A.use_lists = 0;
     A.collect_r2 = 0;
@@ -726,8 +730,8 @@ int launch_finalize(np8_ctx *c, const unsigned char *recs, int world) {
     Timer t;
     timer_begin(c, 1, t);
     FinArgs F = fin_args(c, recs, world);
-    F.wr2 = c->wr2;
-    F.n_waves = c->collecting ? c->assign_waves : 0;
+    if (c->gather)  // the step's radius records (any order with finalize: both only raise the gathered radii)
+        HIPC(c, np8_launch_fold_r2(c->wr2, c->assign_waves, c->r2, c->kcap, c->stream));
     HIPC(c, np8_launch_finalize(F, c->stream));
     if (c->prior == NP8_PRIOR_NIW) {  // the accepted auxiliaries' full parameters
         NiwArgs A = niw_args(c);
@@ -753,7 +757,7 @@ int launch_assign(np8_ctx *c, int64_t p0, int64_t p1, const int64_t *order, bool
     Timer t;
     timer_begin(c, 0, t);
     AssignArgs A = assign_args(c, p0, p1, order, use_perm);
-    A.collect_r2 = c->collecting ? 1 : 0;
+    A.collect_r2 = c->gather ? 1 : 0;
     A.use_lists = (c->collecting && c->lists_valid) ? 1 : 0;
     c->assign_waves = (p1 - p0 + 63) / 64;
     if (c->wide)
@@ -771,16 +775,15 @@ int launch_prune(np8_ctx *c, bool last) {
     P.cand = c->cand;
     P.ctl = c->ctl;
     P.r2 = c->r2;
-    P.kcap = c->kcap;
-    P.t = c->epoch - c->t_base;
-    P.last = last ? 1 : 0;
     P.plist = c->plist;
     P.plen = c->plen;
+    P.plr2 = c->plr2;
     P.ls = c->kcap;
     P.D = c->D;
+    P.kcap = c->kcap;
+    P.gathered = (last && c->gather) ? 1 : 0;
     HIPC(c, np8_launch_prune(P, c->kcap, c->stream));
     c->lists_valid = true;
-    if (last) c->r2_prev_ok = true;
     return NP8_OK;
 }
 
@@ -839,10 +842,13 @@ int step(np8_ctx *c, int64_t p0, int64_t p1, const int64_t *order, bool use_perm
     // lists' back
     c->collecting = c->prune_on && c->use_sorted;
     if (!c->use_sorted) c->lists_valid = c->r2_zero = false;
-    if (c->collecting && !c->r2_zero) {
-        HIPC(c, hipMemsetAsync(c->r2, 0, 2 * sizeof(double) * c->kcap, c->stream));
-        c->r2_prev_ok = false;
-        c->r2_zero = true;
+    if (c->collecting && sub <= 0) {  // the start of a data-parallel sweep: gather radii on this one?
+        c->gather = !c->r2_zero || c->epoch % kGatherEvery == 0;
+        if (!c->r2_zero) {  // no radii yet: every lane walks the table until the first gathered sweep ends
+            HIPC(c, hipMemsetAsync(c->r2, 0, sizeof(double) * c->kcap, c->stream));
+            c->r2_zero = true;
+        }
+        if (c->gather) HIPC(c, hipMemsetAsync(c->r2 + c->kcap, 0, sizeof(double) * c->kcap, c->stream));
     }
     int r = launch_assign(c, p0, p1, order, use_perm);
     if (r) return r;
@@ -855,8 +861,8 @@ int step(np8_ctx *c, int64_t p0, int64_t p1, const int64_t *order, bool use_perm
         r = launch_finalize(c, c->rec, 1);
     }
     if (r) return r;
-    if (c->collecting && sub >= 0 && sub + 1 < c->substeps && c->r2_prev_ok)
-        return launch_prune(c, false);  // lists for the next sub-step from the last sweep's radii
+    if (c->collecting && sub >= 0 && sub + 1 < c->substeps)
+        return launch_prune(c, false);  // lists for the next sub-step (the radii in use)
     // the table changed: lists are valid again after the next prune (end of sweep or of a sub-step)
     c->lists_valid = false;
     return NP8_OK;
@@ -1011,7 +1017,7 @@ int end_sweep(np8_ctx *c, bool stats_given = false) {
     if (c->collecting) {  // after finalize and the parameter update: the table is final
         r0 = launch_prune(c, true);
         if (r0) return r0;
-        c->collecting = false;
+        c->collecting = c->gather = false;
     }
     if (c->debug_inv && (r0 = launch_invariants(c))) return r0;
     if (c->epoch % 5u == 0u) {  // np_mcmc.cpp:172-174
@@ -1077,7 +1083,7 @@ void drop_graph(np8_ctx *c) {
 bool graph_eligible(np8_ctx *c, bool sync) {
     // sharded runs are captured with their RCCL collectives; the host-exchange path is not (host transport)
     return sync && !c->graphs_off && (c->world == 1 || c->comm) && c->n_loc > 0 && c->sorted_valid &&
-           (!c->prune_on || (c->lists_valid && c->r2_zero && (c->substeps == 1 || c->r2_prev_ok)));
+           (!c->prune_on || (c->lists_valid && c->r2_zero));
 }
 
 // Captures kGraphSweeps sweeps starting at the current epoch.  Nothing runs during capture; on any
@@ -1257,6 +1263,7 @@ int np8_create(np8_ctx **out, const np8_config *cfg) {
         (r = dalloc(c, &c->rec, (size_t)c->rec_bytes)) || (r = dalloc(c, &c->evalc, (size_t)4 * kEvalSlots)) ||
         (c->param_update != NP8_PARAM_FROZEN && (r = dalloc(c, &c->acc, (size_t)kc * (D + DP)))) ||
         (kc <= kPruneMaxKcap && ((r = dalloc(c, &c->r2, 2 * (size_t)kc)) || (r = dalloc(c, &c->plen, (size_t)kc)) ||
+                                (r = dalloc(c, &c->plr2, (size_t)kc)) ||
                                  (r = dalloc(c, &c->plist, (size_t)kc * kc))))) {
         free_device(c);
         delete c;

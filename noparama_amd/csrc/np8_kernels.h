@@ -85,7 +85,7 @@ NP8_HD int64_t record_bytes(int kcap, int rec_cap, int D) {
 // Radius record of one assign wave (candidate pruning): the largest |x - mu|^2 over its 64 items and the
 // slot they all sit in, or slot -1 when they do not share one (those items went to r2 by atomics).
 // Plain stores instead of one device-scope atomic per wave on a handful of addresses: those serialise
-// at the memory side and cost the sweep ~50 us at C3.
+// at the memory side and cost the sweep ~50 us at C3.  Written only on gathering sweeps.
 struct WaveR2 {
     double d2;
     int32_t slot, pad;
@@ -119,8 +119,9 @@ struct AssignArgs {
     // plist[k0*ls .. +plen[k0]] instead of every row; r2 collects max |x - mu|^2 per slot for the
     // lists of the next sweep
     const int32_t *plist, *plen;
+    const double *plr2;  // per dense row: the squared radius its list assumes (+inf: a full list)
     int32_t ls, use_lists, collect_r2, count_eval;
-    double *r2;      // [2][kcap] by epoch parity; only waves whose items do not share one slot add to it (atomicMax)
+    double *r2;      // [2][kcap]: radii in use | gathered this sweep (collect_r2: mixed waves atomicMax here)
     WaveR2 *wr2;     // [ceil(n_loc / 64)]: a wave whose 64 items sit in one slot stores its maximum here
     unsigned long long *evalc;  // [kEvalSlots][2]: quadratic forms, isotropic ones
     // wide path (np8_wide.hip): per slot, the used MFMA fragment chunks of the fp32 factor followed by
@@ -143,11 +144,12 @@ struct WideArgs {
 struct PruneArgs {
     const double *cand;
     Ctl *ctl;
-    double *r2;         // [2][kcap]: buffer (epoch & 1) collects this sweep, the other holds the last sweep
+    double *r2;         // [2][kcap]: radii in use | gathered this sweep
     int32_t *plist, *plen;
+    double *plr2;       // per dense row: the squared radius the list was built for
     int32_t ls, D, kcap;
-    uint32_t t;     // epoch offset: epoch = ctl->t_base + t
-    int32_t last;   // the sweep's last step: lists for the next sweep from this sweep's radii
+    int32_t gathered;   // the sweep's last step of a gathering sweep: lists from the gathered radii, which
+                        // then become the radii in use
 };
 
 struct FinArgs {
@@ -169,10 +171,6 @@ struct FinArgs {
     uint64_t seed;
     uint32_t t;  // epoch offset: epoch = ctl->t_base + t
     double *r2;  // pruning radii [2][kcap]: +inf for every slot created here (unknown radius)
-    // the radius records of the step's assign waves (n_waves; 0 when the step collects none): folded into
-    // this sweep's radius buffer here, by the only block, at one atomic per 64 records of one slot
-    const WaveR2 *wr2;
-    int64_t n_waves;
     // NIW prior: accepted requests are listed in pend[4 q] = (byte offset of the request's record
     // payload in recs, item, m, slot) for np8_niw_aux_slots instead of being written here
     int32_t prior, req_max;  // req_max: new clusters one step may create
@@ -356,6 +354,8 @@ hipError_t np8_launch_niw_post(const np8::NiwArgs &A, int nblocks, hipStream_t s
 hipError_t np8_launch_niw_aux_slots(const np8::NiwArgs &A, hipStream_t s);
 hipError_t np8_launch_resort(const SortArgs &S, hipStream_t s);
 hipError_t np8_launch_assign(const np8::AssignArgs &A, int D, int M, int prior, hipStream_t s);
+// Pruning radii: the step's per-wave records (AssignArgs::wr2) into the gathered radii (r2 + kcap).
+hipError_t np8_launch_fold_r2(const np8::WaveR2 *wr2, int64_t n, double *r2, int kcap, hipStream_t s);
 // Debug invariants (np8_config / NP8_DEBUG_INVARIANTS): every label a live slot, the live slots' counts the
 // label histogram (one rank) and summing to n_global, K the live slots, the dense table live slots only.
 // Violations: bits in out[0] (1 label out of range or in an empty slot, 2 histogram != counts, 4 sum of

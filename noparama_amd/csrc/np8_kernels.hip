@@ -269,7 +269,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NP8_ASSIGN_
 
     // The item's own cluster enters the draw first (weight n_k - 1): its log-weight is a lower bound
     // of the final maximum, so every later candidate more than kSkip below it is skipped.
-    const int32_t jo = A.dense_of[zi];
+    // the own row: a scalar load when the wave's items share their slot (the label-sorted layout)
+    const int32_t zf = __builtin_amdgcn_readfirstlane(zi);
+    const int32_t jo = (__ballot(zi != zf) == 0ull) ? A.dense_of[zf] : A.dense_of[zi];
     PickState st;
     {
         // one pass per distinct own row of the wave (one in the label-sorted layout), the row read with
@@ -294,42 +296,59 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NP8_ASSIGN_
     // full walk.  Lists hold for every item of the row, whatever its wave (np8_prune: the radius covers
     // each item the last sweep left in the row).
     int32_t nq_lane = 0, niso_lane = 0;  // COUNT: quadratic forms this lane evaluated
+    int32_t pslot = zi;                  // slot of the picked row (no reload of the row at the end)
     // (a wave of many own rows -- a stale layout, a cold start -- walks the table once instead)
     int ngroups = 0;
     for (uint64_t pend = __ballot(1); pend && ngroups <= kMaxListGroups; ++ngroups)
         pend &= ~__ballot(jo == __builtin_amdgcn_readlane(jo, __ffsll((unsigned long long)pend) - 1));
+    bool full = true;  // this lane walks the whole table
     if (A.use_lists && A.ctl->lists_ok && ngroups <= kMaxListGroups) {
         uint64_t pend = __ballot(1);
         while (pend) {
             const int32_t j0 = __builtin_amdgcn_readlane(jo, __ffsll((unsigned long long)pend) - 1);
             pend &= ~__ballot(jo == j0);
             if (jo == j0) {
+                // the list holds for items within the radius it was built for: a lane outside it (an item
+                // that arrived since the radii were gathered) walks the whole table below
+                const double *e0 = cand + (int64_t)j0 * CS;
+                double d2 = 0.0;
+#pragma unroll
+                for (int a = 0; a < D; ++a) {
+                    const double dd = x[a] - e0[a];
+                    d2 = fma(dd, dd, d2);
+                }
+                full = !(d2 <= A.plr2[j0]);
+                if (!full) {
 #ifdef NP8_EXP_NO_WALK
-                const int32_t nl = COUNT ? A.plen[j0] : 0;
+                    const int32_t nl = COUNT ? A.plen[j0] : 0;
 #else
-                const int32_t nl = A.plen[j0];
+                    const int32_t nl = A.plen[j0];
 #endif
-                const int32_t *__restrict__ lst = A.plist + (int64_t)j0 * A.ls;
-                for (int q = 0; q < nl; ++q) {
-                    const int j = lst[q];  // uniform across the group: scalar loads
-                    const double *e = cand + (int64_t)j * CS;
-                    const double lw = cand_ll<D>(e, x) + e[F + kFieldLogn];
-                    ensure_u(st, lw, A.seed, ig, t);
-                    pick_step(st, lw, j);
-                    if constexpr (COUNT) {
-                        nq_lane += 1;
-                        niso_lane += (e[F + kFieldIso] > 0.0) ? 1 : 0;
+                    const int32_t *__restrict__ lst = A.plist + (int64_t)j0 * A.ls;
+                    for (int q = 0; q < nl; ++q) {
+                        const int j = lst[q];  // uniform across the group: scalar loads
+                        const double *e = cand + (int64_t)j * CS;
+                        const double lw = cand_ll<D>(e, x) + e[F + kFieldLogn];
+                        ensure_u(st, lw, A.seed, ig, t);
+                        pick_step(st, lw, j);
+                        pslot = (st.pick == j) ? (int32_t)e[F + kFieldSlot] : pslot;
+                        if constexpr (COUNT) {
+                            nq_lane += 1;
+                            niso_lane += (e[F + kFieldIso] > 0.0) ? 1 : 0;
+                        }
                     }
                 }
             }
         }
-    } else {
+    }
+    if (full) {  // wave-uniform row loop (scalar loads) over the lanes that need it
         for (int j = 0; j < K; ++j) {
-            const double *e = cand + (int64_t)j * CS;  // wave-uniform: scalar loads
+            const double *e = cand + (int64_t)j * CS;
             const double lw = cand_ll<D>(e, x) + e[F + kFieldLogn];
             if (e[F + kFieldSlot] != zslot) {
                 ensure_u(st, lw, A.seed, ig, t);
                 pick_step(st, lw, j);
+                pslot = (st.pick == j) ? (int32_t)e[F + kFieldSlot] : pslot;
             }
             if constexpr (COUNT) {
                 nq_lane += 1;
@@ -442,7 +461,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NP8_ASSIGN_
     }
 
     int32_t *delta = reinterpret_cast<int32_t *>(A.rec + kRecHeaderBytes);
-    const int32_t snew = (st.pick < K) ? (int32_t)cand[(int64_t)st.pick * CS + F + kFieldSlot] : -1;
+    const int32_t snew = (st.pick < K) ? pslot : -1;
 #ifdef NP8_EXP_NO_R2
     if (A.collect_r2 && COUNT) {
 #else
@@ -466,8 +485,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NP8_ASSIGN_
 #pragma unroll
             for (int o = 32; o > 0; o >>= 1) d2 = fmax(d2, __shfl_xor(d2, o));
         } else {
-            atomicMax(reinterpret_cast<unsigned long long *>(A.r2 + (int64_t)(t & 1u) * A.kcap + ts),
-                      (unsigned long long)__double_as_longlong(d2));
+            atomicMax(reinterpret_cast<unsigned long long *>(A.r2 + A.kcap + ts), (unsigned long long)__double_as_longlong(d2));
         }
         if ((threadIdx.x & 63) == (__ffsll((unsigned long long)__ballot(1)) - 1)) {  // the wave's record
             WaveR2 w;
@@ -702,7 +720,7 @@ constexpr int kPruneBlocks = 32;  // np8_prune grid: 128 rows per pass
 // R2of(slot): the squared radius of the slot's items that will walk the list.
 template <int DT = 0, typename R2of>
 __device__ void prune_row(const double *__restrict__ cand, R2of R2of_slot, int32_t *__restrict__ plist,
-                          int32_t *__restrict__ plen, int ls, int Drt, int K, int k0) {
+                          int32_t *__restrict__ plen, double *__restrict__ plr2, int ls, int Drt, int K, int k0) {
     const int D = DT > 0 ? DT : Drt;
     const int DP = D * (D + 1) / 2, CS = cand_stride(D), F = D + DP;
     const int lane = threadIdx.x & 63;
@@ -745,7 +763,10 @@ __device__ void prune_row(const double *__restrict__ cand, R2of R2of_slot, int32
         if (keep) plist[(int64_t)k0 * ls + count + __popcll(b & ((1ull << lane) - 1ull))] = j;
         count += __popcll(b);
     }
-    if (lane == 0) plen[k0] = count;
+    if (lane == 0) {
+        plen[k0] = count;
+        plr2[k0] = prunable ? R2 : __longlong_as_double(0x7FF0000000000000ll);  // +inf: every row is listed
+    }
 }
 
 // ---- finalize --------------------------------------------------------------------------------------
@@ -907,41 +928,6 @@ __global__ __launch_bounds__(kFinThreads) void np8_finalize(FinArgs F) {
         base[F.world] = n;
         s_flags[0] = n;
         s_flags[1] = 0;
-    }
-    if (F.n_waves > 0) {  // the step's radius records into this sweep's buffer (before any slot is created)
-        // folded in LDS (the request-key area, free until the requests are read; pruning runs with
-        // kcap <= kPruneMaxKcap <= kReqMax), one LDS atomic per 64 records of one slot, then written back
-        // with plain stores: this block is the only writer
-        unsigned long long *fold = reinterpret_cast<unsigned long long *>(keys);
-        for (int s = tid; s < kcap; s += kFinThreads) fold[s] = 0ull;
-        __syncthreads();
-        const int lane = tid & 63;
-        for (int64_t w0 = (int64_t)(tid >> 6) * 64; w0 < F.n_waves; w0 += kFinThreads) {
-            const int64_t w = w0 + lane;
-            WaveR2 r;
-            r.slot = -1;
-            r.d2 = 0.0;
-            if (w < F.n_waves) r = F.wr2[w];
-            const unsigned long long b = (unsigned long long)__double_as_longlong(r.d2);
-            const int32_t s_first = __builtin_amdgcn_readfirstlane(r.slot);
-            if (__ballot(r.slot != s_first && w < F.n_waves) == 0ull) {  // one slot: one atomic
-                unsigned long long m = b;
-#pragma unroll
-                for (int o = 32; o > 0; o >>= 1) {
-                    const unsigned long long v = __shfl_xor(m, o);
-                    m = v > m ? v : m;
-                }
-                if (lane == 0 && s_first >= 0) atomicMax(fold + s_first, m);
-            } else if (r.slot >= 0) {
-                atomicMax(fold + r.slot, b);
-            }
-        }
-        __syncthreads();
-        unsigned long long *cur = reinterpret_cast<unsigned long long *>(
-            F.r2 + (int64_t)((F.ctl->t_base + F.t) & 1u) * kcap);
-        for (int s = tid; s < kcap; s += kFinThreads)
-            if (fold[s] > cur[s]) cur[s] = fold[s];
-        __syncthreads();
     }
     for (int s = s0; s < s1; ++s) {
         int c = F.cnt[s];
@@ -1437,6 +1423,52 @@ hipError_t np8_launch_assign(const AssignArgs &A, int D, int M, int prior, hipSt
     return hipErrorInvalidValue;
 }
 
+// ---- pruning radii: the step's wave records into this sweep's buffer (DESIGN.md "Candidate pruning") ----
+// One lane per record (the label-sorted layout makes runs of one slot); a wave whose 64
+// records share one slot raises the slot's radius with one atomic, others lane by lane.  Many small waves:
+// one workgroup reading all records (250 KB at C3) took 14 us, latency bound.
+constexpr int kFoldPer = 1;
+
+__global__ __launch_bounds__(256) void np8_fold_r2(const WaveR2 *__restrict__ wr2, int64_t n, double *r2, int kcap) {
+    const int64_t k0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * kFoldPer;
+    unsigned long long *cur = reinterpret_cast<unsigned long long *>(r2 + kcap);
+    int32_t sl = -1;
+    unsigned long long m = 0ull;
+    bool one = true;  // this lane's records share slot sl (or it has none)
+#pragma unroll
+    for (int u = 0; u < kFoldPer; ++u) {
+        if (k0 + u >= n) break;
+        const WaveR2 r = wr2[k0 + u];
+        if (r.slot < 0) continue;
+        const unsigned long long b = (unsigned long long)__double_as_longlong(r.d2);
+        if (sl < 0 || sl == r.slot) {
+            sl = r.slot;
+            m = b > m ? b : m;
+        } else {
+            one = false;
+            atomicMax(cur + r.slot, b);
+        }
+    }
+    const int32_t s0 = __builtin_amdgcn_readfirstlane(sl);
+    if (__ballot(!one || (sl >= 0 && sl != s0)) == 0ull) {  // the wave's runs are one slot: one atomic
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const unsigned long long v = __shfl_xor(m, o);
+            m = v > m ? v : m;
+        }
+        if ((threadIdx.x & 63) == 0 && s0 >= 0) atomicMax(cur + s0, m);
+    } else if (sl >= 0) {
+        atomicMax(cur + sl, m);
+    }
+}
+
+hipError_t np8_launch_fold_r2(const WaveR2 *wr2, int64_t n, double *r2, int kcap, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    const int64_t lanes = (n + kFoldPer - 1) / kFoldPer;
+    hipLaunchKernelGGL(np8_fold_r2, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, s, wr2, n, r2, kcap);
+    return hipGetLastError();
+}
+
 // ---- debug invariants (np8_check_invariants) -----------------------------------------------------------
 __global__ __launch_bounds__(256) void np8_inv_items(const int32_t *__restrict__ z, int64_t n, const int32_t *__restrict__ cnt,
                                                      int kcap, int32_t *__restrict__ hist, unsigned long long *out) {
@@ -1678,25 +1710,19 @@ hipError_t np8_launch_mh_g0(const ParamArgs &A, hipStream_t s) {
 // Standalone pass (after the mh_g0 update has moved means): four rows per block.
 // A small grid strides over the live rows (one wave per row): K is only known on the device, and a
 // grid sized for kcap would mostly launch blocks that exit at once.
-// Radius of a row (DESIGN.md "Candidate pruning"; np8_finalize has folded the step's wave records in):
-//   after an intermediate sub-step: the last sweep's radii -- the items of the sub-steps still to come
-//     sit where the last sweep left them (they move only in their own sub-step);
-//   after the sweep's last step: this sweep's radii -- every item has been placed; block 0 then clears the
-//     last sweep's buffer, which collects the next sweep.
+// Lists from the radii in use; after the last step of a gathering sweep from the radii just gathered, which
+// block 0 then makes the radii in use (no other block reads those in this pass).  Any radius is safe: a
+// lane checks its own distance against the radius its list was built for (np8_assign).
 template <int DT>
 __global__ __launch_bounds__(256) void np8_prune(PruneArgs A) {
     const int K = A.ctl->K;
     if (blockIdx.x == 0 && threadIdx.x == 0) A.ctl->lists_ok = 1;
-    const uint32_t par = (A.ctl->t_base + A.t) & 1u;
-    const double *cur = A.r2 + (int64_t)par * A.kcap, *prev = A.r2 + (int64_t)(par ^ 1u) * A.kcap;
-    const double *src = A.last ? cur : prev;
-    if (A.last && blockIdx.x == 0) {  // no block reads prev in this pass
-        double *clr = A.r2 + (int64_t)(par ^ 1u) * A.kcap;
-        for (int s = threadIdx.x; s < A.kcap; s += blockDim.x) clr[s] = 0.0;
-    }
+    const double *src = A.r2 + (A.gathered ? A.kcap : 0);
+    if (A.gathered && blockIdx.x == 0)
+        for (int s = threadIdx.x; s < A.kcap; s += blockDim.x) A.r2[s] = A.r2[A.kcap + s];
     auto R2of = [&](int slot) { return src[slot]; };
     for (int k0 = blockIdx.x * 4 + (threadIdx.x >> 6); k0 < K; k0 += gridDim.x * 4)  // wave-uniform
-        prune_row<DT>(A.cand, R2of, A.plist, A.plen, A.ls, A.D, K, k0);
+        prune_row<DT>(A.cand, R2of, A.plist, A.plen, A.plr2, A.ls, A.D, K, k0);
 }
 
 __global__ void np8_advance_epoch(Ctl *ctl, uint32_t n) { ctl->t_base += n; }
