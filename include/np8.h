@@ -72,7 +72,8 @@ typedef struct {
 #define NP8_SUBSTEPS_MAX 64
 
 /* Cluster-likelihood arithmetic (DESIGN.md "Wide path").
- * F64:      fp64 table form (packed sym(Sigma^{-1})), D in {1,2,3,4,8,16}.
+ * F64:      fp64 table form (packed sym(Sigma^{-1})), any D from 1 to 16 with M = 3 (the reference's), and
+ *           M in {1, 2, 3, 4} for D in {1, 2, 3, 4, 8, 16}.
  * F32_MFMA: D in {32, 64} (config C5): items held in fp32, (x-mu)^T Sigma^{-1} (x-mu) = |A (x-mu)|^2 with
  *           A = fp32(chol(sym Sigma^{-1})) contracted on the matrix cores (v_mfma_f32_32x32x2_f32),
  *           |.|^2 in fp32, the draws and the pick in fp64; bit-exact against oracle/ (NP8O_CONTRACT_F32)
@@ -171,7 +172,7 @@ int np8_prepare_sweeps(np8_ctx *ctx, int32_t n_sweeps);
  * np_main.cpp:440-445): each sweep makes N attempts on the item pairs of two scan permutations -- a
  * split of their common cluster (sams_prior allocation, new cluster from G0) or a merge of the first
  * item's cluster into the second's -- then the end-of-sweep step of np8_sweep (parameter update,
- * max-likelihood check).  Single rank, reference prior, fp64 contraction (D in {1,2,3,4,8,16}).
+ * max-likelihood check).  Single rank, reference prior, fp64 contraction (any D <= 16).
  * Synchronous: returns when the sweeps are done. */
 int np8_sm_sweep(np8_ctx *ctx, int32_t n_sweeps);
 /* Cumulative attempt outcomes (the reference's _statistics.step[], np_jain_neal_algorithm.cpp:505-530):

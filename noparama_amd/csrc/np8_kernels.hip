@@ -1394,7 +1394,8 @@ __global__ __launch_bounds__(256) void np8_loglik_matrix_kernel(AssignArgs A, co
 // ---- dispatch ----------------------------------------------------------------------------------------
 #define NP8_FOR_EACH_DM(X) \
     X(1, 1) X(1, 2) X(1, 3) X(1, 4) X(2, 1) X(2, 2) X(2, 3) X(2, 4) X(3, 1) X(3, 2) X(3, 3) X(3, 4) X(4, 1) \
-    X(4, 2) X(4, 3) X(4, 4) X(8, 1) X(8, 2) X(8, 3) X(8, 4) X(16, 1) X(16, 2) X(16, 3) X(16, 4)
+    X(4, 2) X(4, 3) X(4, 4) X(8, 1) X(8, 2) X(8, 3) X(8, 4) X(16, 1) X(16, 2) X(16, 3) X(16, 4)         \
+    X(5, 3) X(6, 3) X(7, 3) X(9, 3) X(10, 3) X(11, 3) X(12, 3) X(13, 3) X(14, 3) X(15, 3)
 
 bool np8_supported(int D, int M) {
 #define X(d, m) \
@@ -1663,7 +1664,7 @@ hipError_t np8_launch_loglik(const LoglikArgs &A, int D, hipStream_t s) {
     case d:                                                                        \
         hipLaunchKernelGGL((np8_loglik<d>), dim3((unsigned)nb), dim3(256), 0, s, A); \
         break;
-        Y(1) Y(2) Y(3) Y(4) Y(8) Y(16)
+        Y(1) Y(2) Y(3) Y(4) Y(5) Y(6) Y(7) Y(8) Y(9) Y(10) Y(11) Y(12) Y(13) Y(14) Y(15) Y(16)
 #undef Y
         default:
             return hipErrorInvalidValue;
@@ -1685,7 +1686,7 @@ hipError_t np8_launch_suffstats(const ParamArgs &A, hipStream_t s) {
     case d:                                                                           \
         hipLaunchKernelGGL((np8_suffstats<d>), dim3((unsigned)nb), dim3(64), 0, s, A); \
         break;
-        Y(1) Y(2) Y(3) Y(4) Y(8) Y(16)
+        Y(1) Y(2) Y(3) Y(4) Y(5) Y(6) Y(7) Y(8) Y(9) Y(10) Y(11) Y(12) Y(13) Y(14) Y(15) Y(16)
 #undef Y
         default:
             return hipErrorInvalidValue;
@@ -1699,7 +1700,7 @@ hipError_t np8_launch_mh_g0(const ParamArgs &A, hipStream_t s) {
     case d:                                                                        \
         hipLaunchKernelGGL((np8_mh_g0<d>), dim3((unsigned)A.kcap), dim3(64), 0, s, A); \
         break;
-        Y(1) Y(2) Y(3) Y(4) Y(8) Y(16)
+        Y(1) Y(2) Y(3) Y(4) Y(5) Y(6) Y(7) Y(8) Y(9) Y(10) Y(11) Y(12) Y(13) Y(14) Y(15) Y(16)
 #undef Y
         default:
             return hipErrorInvalidValue;
@@ -1735,7 +1736,7 @@ hipError_t np8_launch_prune(const PruneArgs &A, int kcap, hipStream_t s) {
     case d:                                                               \
         hipLaunchKernelGGL((np8_prune<d>), g, dim3(256), 0, s, A);        \
         break;
-        Y(1) Y(2) Y(3) Y(4) Y(8) Y(16)
+        Y(1) Y(2) Y(3) Y(4) Y(5) Y(6) Y(7) Y(8) Y(9) Y(10) Y(11) Y(12) Y(13) Y(14) Y(15) Y(16)
 #undef Y
         default:
             hipLaunchKernelGGL((np8_prune<0>), g, dim3(256), 0, s, A);

@@ -867,7 +867,8 @@ __global__ void np8_sm_reset(SmCtl *sc) {  // (both samplers)
 
 using namespace np8;
 
-#define NP8_SM_FOR_EACH_D(X) X(1) X(2) X(3) X(4) X(8) X(16)
+#define NP8_SM_FOR_EACH_D(X) \
+    X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15) X(16)
 
 hipError_t np8_launch_sm_members(const SmArgs &A, hipStream_t s) {
     if (A.N <= 0) return hipSuccess;

@@ -166,7 +166,9 @@ def test_errors_are_reported():
     with pytest.raises(NP8Error):
         g.set_state(np.zeros(4, np.int32), np.zeros((1, 2)), np.zeros((1, 2, 2)))  # det = 0
     with pytest.raises(NP8Error):
-        NealAlgorithm8(5, seed=0, device=0)  # no kernel instantiated for D = 5
+        NealAlgorithm8(17, seed=0, device=0)  # the fp64 path covers D <= 16 (D 32 / 64: the wide path)
+    with pytest.raises(NP8Error):
+        NealAlgorithm8(5, M=2, seed=0, device=0)  # D outside {1, 2, 3, 4, 8, 16} runs M = 3 (the reference's)
 
 
 def test_partial_accept_at_kcap_matches_oracle():
@@ -384,3 +386,31 @@ def test_substeps_cold_start_bit_exact():
         sg, so = g.state(params=False), o.state()
         assert sg["K"] == so["K"] and np.array_equal(sg["z"], so["z"])
     assert [g.stats()["new_clusters"], g.stats()["rejected_requests"]] == list(o.request_stats)
+
+
+@pytest.mark.parametrize("D", [5, 6, 7, 9, 12, 15])
+def test_every_dimension_up_to_16_bit_exact(D):
+    """Any D from 1 to 16 on the fp64 path (the reference's data_t has any length, np_data.h:9): warm and
+    random starts, mh_g0 and a split-merge sweep, bit-exact against the oracle."""
+    X, z, mu, sig = datasets.mixture(6000, D, 6, 0.6, 6.0, seed=D)
+    g, o = pair(D, 300 + D, kcap=512)
+    for c in (g, o):
+        c.set_data(X)
+        c.set_state(z, mu, sig)
+    g.sweep(3)
+    o.sweep(3)
+    assert_same_state(g, o)
+    for c in (g, o):
+        c.init_random(20)
+    g.sweep(22)
+    o.sweep(22)
+    assert_same_state(g, o)
+    np.testing.assert_allclose(g.loglik_matrix(np.arange(32)), o.loglik_matrix(np.arange(32)), rtol=LL_RTOL,
+                               atol=1e-12)
+    gm, om = pair(D, 400 + D, kcap=512, param_update="mh_g0")
+    for c in (gm, om):
+        c.set_data(X)
+        c.set_state(z, mu, sig * 2.0)
+    gm.sweep(4)
+    om.sweep(4)
+    assert_same_state(gm, om)
