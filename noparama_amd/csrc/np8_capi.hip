@@ -56,6 +56,7 @@ struct np8_ctx {
     bool wide = false;
     float *wA = nullptr, *wfrag = nullptr, *wmu = nullptr;
     int32_t *wdirty = nullptr;
+    double *lam_lo = nullptr, *wdist = nullptr;  // wide-path candidate pruning (np8_wide_dist)
     double *acc = nullptr;  // [kcap][D + DP] parameter-update statistics
     // candidate pruning (np8_prune): per-slot radii and per-row candidate lists
     double *r2 = nullptr;
@@ -63,6 +64,7 @@ struct np8_ctx {
     int32_t *plist = nullptr, *plen = nullptr;
     unsigned long long *evalc = nullptr;  // [kEvalSlots][2] executed-work counters (timing mode)
     bool prune_on = false;     // kcap small enough for kcap x kcap lists
+    bool wide_prune_off = false;  // NP8_NO_PRUNE=1: the wide path evaluates every row (A/B runs)
     bool lists_valid = false;  // plist/plen describe the current table and membership
     bool r2_zero = false;      // the radii in use are initialised (cleared at (re)start: every lane walks all)
     bool collecting = false;   // the running sweep prunes (a data-parallel sweep): lists after every step
@@ -384,13 +386,14 @@ bool slot_from_sigma(const np8_ctx *c, const double *mu, const double *Sigma, Sl
 }
 
 void free_device(np8_ctx *c) {
-    void *niw_ptrs[] = {c->d_U, c->d_Uinv, c->d_Psi0, c->pend, c->wA, c->wfrag, c->wmu, c->wdirty};
+    void *niw_ptrs[] = {c->d_U, c->d_Uinv, c->d_Psi0, c->pend, c->wA, c->wfrag, c->wmu, c->wdirty, c->lam_lo, c->wdist};
     for (void *p : niw_ptrs)
         if (p) (void)hipFree(p);
     c->d_U = c->d_Uinv = c->d_Psi0 = nullptr;
     c->pend = nullptr;
     c->wA = c->wfrag = c->wmu = nullptr;
     c->wdirty = nullptr;
+    c->lam_lo = c->wdist = nullptr;
     void *ptrs[] = {c->X,      c->z,       c->z_best, c->slot_mu, c->slot_P,  c->slot_c,  c->slot_sigma,
                     c->cnt,    c->cnt_best, c->mu_best, c->sigma_best, c->cand, c->ctl,    c->hyp,
                     c->d_mu0,  c->d_LT,    c->d_Gp,   c->d_LTL,   c->rec,     c->gath,    c->order,
@@ -637,7 +640,10 @@ WideArgs wide_args(np8_ctx *c) {
     W.wA = c->wA;
     W.wfrag = c->wfrag;
     W.wmu = c->wmu;
+    W.lam_lo = c->lam_lo;
     W.ctl = c->ctl;
+    W.cand = c->cand;
+    W.wdist = c->wdist;
     return W;
 }
 
@@ -723,6 +729,9 @@ AssignArgs assign_args(np8_ctx *c, int64_t p0, int64_t p1, const int64_t *order,
     A.r2 = c->r2;
     A.wr2 = c->wr2;
     A.wfrag = c->wfrag;
+    A.wmu = c->wmu;
+    A.lam_lo = c->lam_lo;
+    A.wdist = nullptr;  // set by launch_assign on the wide path (after np8_wide_dist)
     return A;
 }
 
@@ -760,8 +769,13 @@ int launch_assign(np8_ctx *c, int64_t p0, int64_t p1, const int64_t *order, bool
     A.collect_r2 = c->gather ? 1 : 0;
     A.use_lists = (c->collecting && c->lists_valid) ? 1 : 0;
     c->assign_waves = (p1 - p0 + 63) / 64;
-    if (c->wide)
+    if (c->wide) {
+        if (c->wdist && !c->wide_prune_off) {  // distances between the current rows' means (pruning)
+            HIPC(c, np8_launch_wide_dist(wide_args(c), c->stream));
+            A.wdist = c->wdist;
+        }
         HIPC(c, np8_launch_assign_wide(A, c->D, c->M, c->prior, c->stream));
+    }
     else
         HIPC(c, np8_launch_assign(A, c->D, c->M, c->prior, c->stream));
     timer_end(c, t);
@@ -1250,6 +1264,7 @@ int np8_create(np8_ctx **out, const np8_config *cfg) {
     c->own_stream = true;
     c->graphs_off = std::getenv("NP8_NO_GRAPH") != nullptr;  // A/B switch for launch-by-launch sweeps
     c->prune_on = !c->wide && c->kcap <= kPruneMaxKcap && std::getenv("NP8_NO_PRUNE") == nullptr;
+    c->wide_prune_off = std::getenv("NP8_NO_PRUNE") != nullptr;
     c->rec_cap = c->req_max;  // grown to the item count by np8_set_data (one rank)
     c->rec_bytes = record_bytes(c->kcap, (int)c->rec_cap, c->D);
     int r = 0;
@@ -1291,7 +1306,8 @@ int np8_create(np8_ctx **out, const np8_config *cfg) {
           (r = dalloc(c, &c->d_Psi0, (size_t)D * D)) || (r = dalloc(c, &c->pend, (size_t)4 * kReqMax)))) ||
         (c->wide && ((r = dalloc(c, &c->wA, (size_t)kc * D * D)) ||
                      (r = dalloc(c, &c->wfrag, (size_t)kc * (D * D + D))) ||  // >= the compact rows
-                     (r = dalloc(c, &c->wmu, (size_t)kc * D)) ||
+                     (r = dalloc(c, &c->wmu, (size_t)kc * D)) || (r = dalloc(c, &c->lam_lo, (size_t)kc)) ||
+                     (r = dalloc(c, &c->wdist, (size_t)kc * kc)) ||
                      (r = dalloc(c, &c->wdirty, (size_t)kc))))) {
         free_device(c);
         delete c;

@@ -127,6 +127,9 @@ struct AssignArgs {
     // wide path (np8_wide.hip): per slot, the used MFMA fragment chunks of the fp32 factor followed by
     // the fp32 mean in fragment order (Wide<D>::ROW floats)
     const float *wfrag;
+    const float *wmu;          // natural fp32 means [kcap][D]
+    const double *lam_lo;      // [kcap] precision eigenvalue lower bounds (np8_wide_rows)
+    const double *wdist;       // [K][kcap] squared distances between row means (np8_wide_dist); null: no pruning
 };
 
 // Wide-path tables (np8_wide.hip), maintained for the slots flagged in dirty.
@@ -136,7 +139,11 @@ struct WideArgs {
     const int32_t *cnt;
     const double *slot_P, *slot_mu;
     float *wA, *wfrag, *wmu;  // wA natural [D][D]; wfrag as AssignArgs::wfrag; wmu natural [D]
+    double *lam_lo;           // [kcap]: a lower bound of the smallest eigenvalue of the slot's precision
     Ctl *ctl;
+    // candidate pruning (np8_wide_dist): squared distances between the fp32 means of dense rows [K][kcap]
+    const double *cand;
+    double *wdist;
 };
 
 // Builds the candidate lists of every live dense row from the radii r2 collected by the sweep
@@ -343,6 +350,8 @@ struct SortArgs {
 bool np8_supported(int D, int M);
 bool np8_wide_supported(int D, int M);
 hipError_t np8_launch_assign_wide(const np8::AssignArgs &A, int D, int M, int prior, hipStream_t s);
+// Wide-path pruning: the distance table of the current dense rows (after every table change).
+hipError_t np8_launch_wide_dist(const np8::WideArgs &W, hipStream_t s);
 hipError_t np8_launch_loglik_matrix_wide(const np8::AssignArgs &A, const np8::WideArgs &W, int D, int M, int prior,
                                          const int64_t *idx, int64_t n, double *out, hipStream_t s);
 hipError_t np8_launch_loglik_wide(const np8::LoglikArgs &L, const np8::WideArgs &W, int D, hipStream_t s);

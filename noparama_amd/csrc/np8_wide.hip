@@ -209,6 +209,33 @@ __global__ __launch_bounds__(256) void np8_wide_rows(WideArgs W) {
             }
         __syncthreads();
     }
+    // candidate pruning: lam_lo <= the smallest eigenvalue of P = R^T R, as 1 / (a Gershgorin bound of the
+    // largest eigenvalue of P^{-1} = R^{-1} R^{-T}); R^{-1} by back substitution, one thread per column
+    if (W.lam_lo) {
+        double *Ri = R + D * D;  // [D][D] upper triangular inverse
+        for (int c = threadIdx.x; c < D; c += blockDim.x) {
+            for (int i = D - 1; i >= 0; --i) {
+                double v = (i == c) ? 1.0 : 0.0;
+                for (int k = i + 1; k <= c; ++k) v = fma(-R[i * D + k], Ri[k * D + c], v);
+                Ri[i * D + c] = (i > c) ? 0.0 : v / R[i * D + i];
+            }
+        }
+        __syncthreads();
+        __shared__ double rowmax;
+        if (threadIdx.x == 0) rowmax = 0.0;
+        __syncthreads();
+        for (int i = threadIdx.x; i < D; i += blockDim.x) {
+            double rs = 0.0;
+            for (int k = 0; k < D; ++k) {
+                double v = 0.0;  // (R^{-1} R^{-T})_ik
+                for (int m = (i > k ? i : k); m < D; ++m) v = fma(Ri[i * D + m], Ri[k * D + m], v);
+                rs += fabs(v);
+            }
+            atomicMax(reinterpret_cast<unsigned long long *>(&rowmax), (unsigned long long)__double_as_longlong(rs));
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) W.lam_lo[s] = (rowmax > 0.0) ? 0.99 / rowmax : 0.0;  // 1% for the fp32 factor
+    }
     float *An = W.wA + (int64_t)s * D * D;
     for (int k = threadIdx.x; k < D * D; k += blockDim.x) An[k] = (float)R[k];
     // fragment chunks (mt, s4), s4 >= mt, in compact order; in chunk c = chunk(mt, s4) lane l's float4
@@ -229,6 +256,26 @@ __global__ __launch_bounds__(256) void np8_wide_rows(WideArgs W) {
         Af[NCH * 256 + k] = (float)W.slot_mu[(int64_t)s * D + 4 * st + g];
     }
     for (int a = threadIdx.x; a < D; a += blockDim.x) W.wmu[(int64_t)s * D + a] = (float)W.slot_mu[(int64_t)s * D + a];
+}
+
+// Candidate pruning (DESIGN.md "Wide path"): squared distances between the fp32 means of the dense rows,
+// in fp64, wdist[j0 * kcap + j].  One block per row j0 (a grid of kcap; rows >= K exit).
+__global__ __launch_bounds__(256) void np8_wide_dist(WideArgs W) {
+    const int K = W.ctl->K, j0 = blockIdx.x;
+    if (j0 >= K) return;
+    const int D = W.D, DP = D * (D + 1) / 2, CS = cand_stride(D);
+    const int s0 = (int)W.cand[(int64_t)j0 * CS + D + DP + kFieldSlot];
+    const float *m0 = W.wmu + (int64_t)s0 * D;
+    for (int j = threadIdx.x; j < K; j += blockDim.x) {
+        const int sj = (int)W.cand[(int64_t)j * CS + D + DP + kFieldSlot];
+        const float *mj = W.wmu + (int64_t)sj * D;
+        double d2 = 0.0;
+        for (int a = 0; a < D; ++a) {
+            const double dd = (double)mj[a] - (double)m0[a];
+            d2 = fma(dd, dd, d2);
+        }
+        W.wdist[(int64_t)j0 * W.kcap + j] = d2;
+    }
 }
 
 __global__ void np8_wide_clean(WideArgs W) {
@@ -268,6 +315,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void n
     const int32_t jo = A.dense_of[zi];
 
     // auxiliaries first (fp64, per lane): only |U^T (x - mu0)| of the item is needed
+    double rown = 0.0;  // |x - muf_own|
     double lwa[M];
 #pragma unroll
     for (int m = 0; m < M; ++m) lwa[m] = 0.0;
@@ -276,6 +324,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void n
 #pragma unroll
         for (int a = 0; a < D; ++a) xf[a] = X[(int64_t)a * n + xr];
         const double ny = wide_whiten_norm<D>(hyp, xf);
+        if (A.wdist) {  // the item's distance to its own row's fp32 mean (candidate pruning)
+            const float *mo = A.wmu + (int64_t)zi * D;
+            double d2 = 0.0;
+#pragma unroll
+            for (int a = 0; a < D; ++a) {
+                const double dd = (double)xf[a] - (double)mo[a];
+                d2 = fma(dd, dd, d2);
+            }
+            rown = sqrt(d2);
+        }
         const double logam = hyp[D + W::DP + 2];
 #pragma unroll 1
         for (int m = 0; m < M; ++m) {
@@ -316,20 +374,62 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void n
         pend &= ~__ballot(mine);
     }
 
-    // every other candidate in ascending order, block-uniform: row j + 1 is copied into the other
-    // stage while the MFMAs of row j run; one barrier per row
-    row_glds<D>(A.wfrag, (int)cand[F + kFieldSlot], stage);
+    // candidate pruning: a row is evaluated for the block when one of its items may pick it.  For lane x
+    // with running maximum T >= lw_own(x): lw_j(x) <= c_j + log n_j - lam_j (|mu_j - mu_own| - |x - mu_own|)^2 / 2
+    // (triangle inequality, lam_j <= the smallest eigenvalue of row j's precision); a row below T - 80 - 2
+    // (and a relative margin) for every lane is one its pick_step would skip -- results unchanged.
+    // kMaskWords: up to 64 * 8 = 512 rows (kcap of the wide path).
+    constexpr int kMaskWords = 8;
+    __shared__ unsigned long long rmask[kMaskWords];
+    const bool prune = A.wdist != nullptr && K <= 64 * kMaskWords;
+    if (prune) {
+        if (threadIdx.x < kMaskWords) rmask[threadIdx.x] = 0ull;
+        __syncthreads();
+        const double Tl = st.T;
+        for (int j = 0; j < K; ++j) {
+            const double *e = cand + (int64_t)j * CS;  // block-uniform: scalar loads
+            const int32_t sj = (int32_t)e[F + kFieldSlot];
+            bool need = false;
+            if (wave_live && valid && sj != zi) {
+                const double base = e[F + kFieldC] + e[F + kFieldLogn];
+                const double gap = fmax(sqrt(A.wdist[(int64_t)jo * A.kcap + j]) - rown, 0.0);
+                const double far = 0.5 * A.lam_lo[sj] * gap * gap;
+                const double U = base - far - Tl;
+                need = !(U <= -kSkip - 2.0 - 1e-9 * (fabs(base) + fabs(Tl) + far));
+            }
+            if (__ballot(need) != 0ull && lane == 0) atomicOr(&rmask[j >> 6], 1ull << (j & 63));
+        }
+        __syncthreads();
+    }
+    // the next row to evaluate at or after j (block-uniform)
+    auto next_row = [&](int j) -> int {
+        if (!prune) return j;
+        while (j < K) {
+            const unsigned long long w = rmask[j >> 6] >> (j & 63);
+            if (w) return j + __ffsll(w) - 1;
+            j = (j | 63) + 1;
+        }
+        return K;
+    };
+
+    // the evaluated candidates in ascending order, block-uniform: the next one is copied into the other
+    // stage while the MFMAs of this one run; one barrier per row
+    int j = next_row(0), buf = 0;
+    if (j < K) row_glds<D>(A.wfrag, (int)cand[(int64_t)j * CS + F + kFieldSlot], stage);
     __syncthreads();
-    for (int j = 0; j < K; ++j) {
+    while (j < K) {
         const double *e = cand + (int64_t)j * CS;  // block-uniform: scalar loads
         const int32_t sj = (int32_t)e[F + kFieldSlot];
-        if (j + 1 < K) row_glds<D>(A.wfrag, (int)cand[(int64_t)(j + 1) * CS + F + kFieldSlot], stage + ((j + 1) & 1) * W::ROW);
-        const float *row = stage + (j & 1) * W::ROW;
+        const int jn = next_row(j + 1);
+        if (jn < K) row_glds<D>(A.wfrag, (int)cand[(int64_t)jn * CS + F + kFieldSlot], stage + (buf ^ 1) * W::ROW);
+        const float *row = stage + buf * W::ROW;
         if (wave_live) {
             const double q = wide_pass<D>(row, xb, lane);
             if (sj != zi) pick_step(st, fma(-0.5, q, e[F + kFieldC]) + e[F + kFieldLogn], j);
         }
         __syncthreads();  // the next row has landed (vmcnt(0)); this row's stage may be overwritten
+        j = jn;
+        buf ^= 1;
     }
 #pragma unroll
     for (int m = 0; m < M; ++m) pick_step(st, lwa[m], K + m);
@@ -657,8 +757,13 @@ hipError_t np8_launch_loglik_wide(const LoglikArgs &L, const WideArgs &W, int D,
     return hipGetLastError();
 }
 
+hipError_t np8_launch_wide_dist(const WideArgs &W, hipStream_t s) {
+    hipLaunchKernelGGL(np8_wide_dist, dim3((unsigned)W.kcap), dim3(256), 0, s, W);
+    return hipGetLastError();
+}
+
 hipError_t np8_launch_wide_refresh(const WideArgs &W, hipStream_t s) {
-    hipLaunchKernelGGL(np8_wide_rows, dim3((unsigned)W.kcap), dim3(256), sizeof(double) * W.D * W.D, s, W);
+    hipLaunchKernelGGL(np8_wide_rows, dim3((unsigned)W.kcap), dim3(256), 2 * sizeof(double) * W.D * W.D, s, W);
     hipLaunchKernelGGL(np8_wide_clean, dim3((unsigned)((W.kcap + 255) / 256)), dim3(256), 0, s, W);
     return hipGetLastError();
 }

@@ -16,16 +16,17 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
 
 
-def c1(seeds_gpu=20, seeds_seq=3, T=1000):
+def c1(seeds_gpu=20, seeds_seq=3, T=1000, substeps=16):
     import oracle as O
     from noparama_amd import NealAlgorithm8, datasets
 
     X, lab = datasets.read_data(os.path.join(ROOT, "tests", "golden", "twogaussians.data"))
     rows = {}
-    for name, chunk, seeds in (("gpu_sync", 0, seeds_gpu), ("gpu_sequential", 1, seeds_seq)):
+    for name, chunk, seeds, S in (("gpu_sync", 0, seeds_gpu, 1), (f"gpu_sync_substeps{substeps}", 0, seeds_gpu, substeps),
+                                  ("gpu_sequential", 1, seeds_seq, 1)):
         res, t0 = [], time.perf_counter()
         for s in range(seeds):
-            g = NealAlgorithm8(2, seed=s, chunk=chunk, kcap=1024, device=0)
+            g = NealAlgorithm8(2, seed=s, chunk=chunk, kcap=1024, device=0, substeps=S)
             g.set_data(X)
             g.init_random(20)
             g.sweep(T)
@@ -73,6 +74,22 @@ def main():
     print(json.dumps(out["C3_8e6"]), flush=True)
     out["C3_mh_g0"] = bench(["--config", "C3-mh_g0", "--param-update", "mh_g0", "--cpu-seconds", "0"])
     print(json.dumps(out["C3_mh_g0"]), flush=True)
+    for S, extra in ((8, []), (16, ["--kcap", "1024"])):
+        out[f"C3_substeps{S}"] = bench(["--config", f"C3-S{S}", "--substeps", str(S), "--cpu-seconds", "0",
+                                        "--cold-sweeps", "0"] + extra)
+        print(json.dumps(out[f"C3_substeps{S}"]), flush=True)
+    out["C3_rccl_one_rank"] = bench(["--config", "C3-rccl1", "--exchange", "rccl", "--cpu-seconds", "0",
+                                     "--cold-sweeps", "0"])
+    print(json.dumps(out["C3_rccl_one_rank"]), flush=True)
+    out["C5"] = bench(["--config", "C5", "--steps", "20", "--warmup", "5", "--cpu-seconds", "0"])
+    print(json.dumps(out["C5"]), flush=True)
+    out["C5_niw_conjugate"] = bench(["--config", "C5", "--param-update", "niw_conjugate", "--steps", "20",
+                                     "--warmup", "5", "--cpu-seconds", "0"])
+    print(json.dumps(out["C5_niw_conjugate"]), flush=True)
+    out["C3_jain_neal"] = bench(["--sampler", "jain_neal", "--steps", "10", "--warmup", "2", "--cpu-seconds", "0"])
+    print(json.dumps(out["C3_jain_neal"]), flush=True)
+    out["C3_triadic"] = bench(["--sampler", "triadic", "--steps", "3", "--warmup", "1", "--cpu-seconds", "0"])
+    print(json.dumps(out["C3_triadic"]), flush=True)
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     with open(os.path.join(ROOT, "gpurun_out", "measure.json"), "w") as f:
         json.dump(out, f, indent=1)
