@@ -194,7 +194,7 @@ def main():
     st1 = smp.stats()
     Kfinal = st1["K"]
     # executed-work counters over separate (untimed) sweeps: they add scalar loads and atomics per wave
-    cnt_sweeps = 20 if (transport != "gloo" and not wide) else 0
+    cnt_sweeps = 20 if transport != "gloo" else 0
     if cnt_sweeps:
         smp.set_timing(True, counters=True)
         sc0 = smp.stats()
@@ -222,7 +222,10 @@ def main():
     # (isotropic rows: D subtractions + D multiply-adds + scale, weight = 3D + 3 flops)
     nq = (sc1["n_quad"] - sc0["n_quad"]) / cnt_sweeps if cnt_sweeps else 0.0  # per sweep (= per launch)
     nq_iso = (sc1["n_quad_iso"] - sc0["n_quad_iso"]) / cnt_sweeps if cnt_sweeps else 0.0
-    exec_flops = ((nq - nq_iso) * (D * D + 2 * D + 4) + nq_iso * (3 * D + 3)) if cnt_sweeps else None
+    if wide:  # item-row contractions on the matrix cores (pruned rows skipped), at the MACs of the 16-row tiles
+        exec_flops = nq * 2 * sum(16 * (D - 16 * t) for t in range(D // 16)) if cnt_sweeps else None
+    else:
+        exec_flops = ((nq - nq_iso) * (D * D + 2 * D + 4) + nq_iso * (3 * D + 3)) if cnt_sweeps else None
     traffic = traffic_src = None
     if os.path.exists(args.traffic_json):
         try:
@@ -274,15 +277,20 @@ def main():
                 "frac": achieved / peak,
                 "traffic": traffic,
                 "assign_ms_per_launch": ms_assign,
-                "mfma_executed_tflops": (mfma_flops / (ms_assign * 1e-3) / 1e12) if (wide and ms_assign > 0) else None,
+                # wide path: the matrix-core work of every row, as if none were pruned (the executed work
+                # is in "executed": item-row contractions counted on the device)
+                "mfma_unpruned_tflops": (mfma_flops / (ms_assign * 1e-3) / 1e12) if (wide and ms_assign > 0) else None,
                 "assign_launches_timed": n_launch,
                 "algorithmic_flops_per_launch": flops,
                 "traffic_source": traffic_src,
                 "executed": None if not cnt_sweeps else {
-                    "note": "what np8_assign executed: quadratic forms after exact candidate pruning "
-                            "(device counters over 20 untimed sweeps after the timed ones), at their real "
-                            "cost, over the timed launch time; the M auxiliary G0 draws per item (Philox, "
-                            "Box-Muller, chi^2 logs) are not flops of this count",
+                    "note": ("what np8_assign_wide executed: item-row contractions on the matrix cores after exact "
+                             "candidate pruning (device counters over 20 untimed sweeps), at the MACs of the 16-row "
+                             "tiles, over the timed launch time" if wide else
+                             "what np8_assign executed: quadratic forms after exact candidate pruning "
+                             "(device counters over 20 untimed sweeps after the timed ones), at their real "
+                             "cost, over the timed launch time; the M auxiliary G0 draws per item (Philox, "
+                             "Box-Muller, chi^2 logs) are not flops of this count"),
                     "quad_forms_per_item": nq / max(n_items, 1),
                     "aux_exact_per_item": (sc1["aux_exact_lanes"] - sc0["aux_exact_lanes"]) / cnt_sweeps / max(n_items, 1),
                     "aux_exact_wave_frac": (sc1["aux_exact_waves"] - sc0["aux_exact_waves"]) / cnt_sweeps

@@ -362,7 +362,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void n
     st.u = uniform(A.seed, ig, t, kStreamPick, 0);
     st.pick = jo;
     uint64_t pend = wave_live ? __ballot(valid) : 0ull;
+    int own_passes = 0;  // executed-work counters (count_eval): the own-row passes of this wave
     while (pend) {
+        ++own_passes;
         const int lead = __ffsll((unsigned long long)pend) - 1;
         const int32_t sj = __shfl(zi, lead);
         const double q = wide_pass<D>(A.wfrag + (int64_t)sj * W::ROW, xb, lane);
@@ -414,7 +416,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void n
 
     // the evaluated candidates in ascending order, block-uniform: the next one is copied into the other
     // stage while the MFMAs of this one run; one barrier per row
-    int j = next_row(0), buf = 0;
+    int j = next_row(0), buf = 0, rows_done = 0;
     if (j < K) row_glds<D>(A.wfrag, (int)cand[(int64_t)j * CS + F + kFieldSlot], stage);
     __syncthreads();
     while (j < K) {
@@ -430,6 +432,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void n
         __syncthreads();  // the next row has landed (vmcnt(0)); this row's stage may be overwritten
         j = jn;
         buf ^= 1;
+        ++rows_done;
+    }
+    if (A.count_eval && wave_live) {  // item-row contractions this wave executed (own passes + evaluated rows)
+        const unsigned long long items = (unsigned long long)__popcll(__ballot(valid));
+        if (lane == 0) {
+            unsigned long long *ec = A.evalc + 2 * ((blockIdx.x * 4 + (threadIdx.x >> 6)) % kEvalSlots);
+            atomicAdd(ec, items * (unsigned long long)(rows_done + own_passes));
+        }
     }
 #pragma unroll
     for (int m = 0; m < M; ++m) pick_step(st, lwa[m], K + m);
