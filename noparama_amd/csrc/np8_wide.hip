@@ -209,8 +209,10 @@ __global__ __launch_bounds__(256) void np8_wide_rows(WideArgs W) {
             }
         __syncthreads();
     }
-    // candidate pruning: lam_lo <= the smallest eigenvalue of P = R^T R, as 1 / (a Gershgorin bound of the
-    // largest eigenvalue of P^{-1} = R^{-1} R^{-T}); R^{-1} by back substitution, one thread per column
+    // candidate pruning: lam_lo <= the smallest eigenvalue of P = R^T R.  Start: 1 / (a Gershgorin bound of
+    // the largest eigenvalue of P^{-1} = R^{-1} R^{-T}) -- valid, but loose by ~2x for a posterior draw at
+    // D = 64 -- then bisection towards min_i P_ii (an upper bound) by Cholesky tests: P - beta I positive
+    // definite <=> lambda_min(P) > beta.
     if (W.lam_lo) {
         double *Ri = R + D * D;  // [D][D] upper triangular inverse
         for (int c = threadIdx.x; c < D; c += blockDim.x) {
@@ -221,8 +223,12 @@ __global__ __launch_bounds__(256) void np8_wide_rows(WideArgs W) {
             }
         }
         __syncthreads();
-        __shared__ double rowmax;
-        if (threadIdx.x == 0) rowmax = 0.0;
+        __shared__ double rowmax, dmin;
+        __shared__ int pd;
+        if (threadIdx.x == 0) {
+            rowmax = 0.0;
+            dmin = 1e300;
+        }
         __syncthreads();
         for (int i = threadIdx.x; i < D; i += blockDim.x) {
             double rs = 0.0;
@@ -232,9 +238,40 @@ __global__ __launch_bounds__(256) void np8_wide_rows(WideArgs W) {
                 rs += fabs(v);
             }
             atomicMax(reinterpret_cast<unsigned long long *>(&rowmax), (unsigned long long)__double_as_longlong(rs));
+            const double pii = Pp[i * D - (i * (i - 1)) / 2];
+            atomicMin(reinterpret_cast<unsigned long long *>(&dmin), (unsigned long long)__double_as_longlong(pii));
         }
         __syncthreads();
-        if (threadIdx.x == 0) W.lam_lo[s] = (rowmax > 0.0) ? 0.99 / rowmax : 0.0;  // 1% for the fp32 factor
+        double lo = (rowmax > 0.0) ? 1.0 / rowmax : 0.0, hi = dmin;
+        double *Cw = Ri;  // the inverse is no longer needed: Cholesky workspace of P - beta I
+        for (int it = 0; it < 8 && hi > lo; ++it) {
+            const double beta = 0.5 * (lo + hi);
+            for (int k = threadIdx.x; k < D * D; k += blockDim.x) Cw[k] = 0.0;
+            if (threadIdx.x == 0) pd = 1;
+            __syncthreads();
+            for (int jj = 0; jj < D; ++jj) {
+                if (threadIdx.x == 0) {
+                    double v = Pp[jj * D - (jj * (jj - 1)) / 2] - beta;
+                    for (int k = 0; k < jj; ++k) v = fma(-Cw[k * D + jj], Cw[k * D + jj], v);
+                    if (!(v > 0.0)) pd = 0;
+                    Cw[jj * D + jj] = (v > 0.0) ? sqrt(v) : 1.0;
+                }
+                __syncthreads();
+                if (!pd) break;  // block-uniform (read after the barrier)
+                for (int i = jj + 1 + threadIdx.x; i < D; i += blockDim.x) {
+                    double w = 0.5 * Pp[jj * D - (jj * (jj - 1)) / 2 + (i - jj)];
+                    for (int k = 0; k < jj; ++k) w = fma(-Cw[k * D + jj], Cw[k * D + i], w);
+                    Cw[jj * D + i] = w / Cw[jj * D + jj];
+                }
+                __syncthreads();
+            }
+            if (pd) lo = beta;  // block-uniform
+            else hi = beta;
+            __syncthreads();
+        }
+        // 1% for the fp32 factor and the fp32 contraction, and the Cholesky's own rounding
+        if (threadIdx.x == 0) W.lam_lo[s] = 0.99 * lo;
+        __syncthreads();
     }
     float *An = W.wA + (int64_t)s * D * D;
     for (int k = threadIdx.x; k < D * D; k += blockDim.x) An[k] = (float)R[k];
