@@ -1284,7 +1284,7 @@ int np8_create(np8_ctx **out, const np8_config *cfg) {
         delete c;
         return r;
     }
-    // hyp: mu0 | UinvT packed | caux | rsk | logam | nu | LT packed
+    // hyp: mu0 | UinvT packed | caux | rsk | logam | nu | LT packed | NIW sum-log bound
     std::vector<double> hyp;
     hyp.insert(hyp.end(), c->mu0.begin(), c->mu0.end());
     for (int a = 0; a < D; ++a)
@@ -1295,6 +1295,21 @@ int np8_create(np8_ctx **out, const np8_config *cfg) {
     hyp.push_back(c->nu);
     for (int a = 0; a < D; ++a)
         for (int b = a; b < D; ++b) hyp.push_back(c->LT[a * D + b]);
+    // NIW auxiliary screen (DESIGN.md "Auxiliary screen"): sum over a = 1..D-1 of log of the largest chi^2
+    // value gamma_mt can return for nu0 - a degrees of freedom (its normals come from 32-bit uniforms:
+    // |x| <= sqrt(-2 log 2^-33)), with a relative margin
+    {
+        double smax = 0.0;
+        if (c->prior == NP8_PRIOR_NIW) {
+            const double rmax = std::sqrt(-2.0 * std::log(std::ldexp(1.0, -33))) * (1.0 + 1e-9);
+            for (int a = 1; a < D; ++a) {
+                const double d = 0.5 * (c->nu - a) - 1.0 / 3.0, cc = 1.0 / std::sqrt(9.0 * d);
+                const double v1 = 1.0 + cc * rmax;
+                smax += std::log(2.0 * d * std::max(1.0, v1 * v1 * v1) * (1.0 + 1e-9));
+            }
+        }
+        hyp.push_back(smax);
+    }
     std::vector<double> gp;
     for (int a = 0; a < D; ++a)
         for (int b = a; b < D; ++b) gp.push_back(c->Gp[a * D + b]);

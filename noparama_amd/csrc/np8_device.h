@@ -397,6 +397,12 @@ NP8_HD void niw_aux_core(uint64_t seed, uint64_t i, uint32_t t, int m, int D, do
     z1 = normal_at(seed, i, t, kStreamAuxNiw, base + kNiwAuxCalls - 1u, 0);
 }
 
+// Screened NIW auxiliary (DESIGN.md "Auxiliary screen"): the exact log-likelihood, or kZeroLogWeight when an
+// upper bound from the first Bartlett draw and z_1 alone (smax bounds the other D-1 log chi^2 draws, chi >=
+// 0) is at or below thr -- an auxiliary the pick would skip; then the other D chi^2 draws are not made.
+NP8_HD double niw_aux_ll_screened(uint64_t seed, uint64_t i, uint32_t t, int m, int D, double nu0, double nd,
+                                  double rsk, double caux, double smax, double thr);
+
 // ll = caux + sumlog/2 - q/2, q = (|dt| b00 - z1/sqrt(kappa0))^2 + chi/kappa0 (nd = |dt|).
 NP8_HD double niw_aux_loglik(double nd, double sumlog, double b00, double chi, double z1, double rsk, double caux) {
     const double e = fma(-z1, rsk, nd * b00);
@@ -406,6 +412,21 @@ NP8_HD double niw_aux_loglik(double nd, double sumlog, double b00, double chi, d
 
 // Log-weight standing for weight 0 (a singleton's own cluster): finite, so no -inf arithmetic.
 constexpr double kZeroLogWeight = -1.0e300;
+
+NP8_HD double niw_aux_ll_screened(uint64_t seed, uint64_t i, uint32_t t, int m, int D, double nu0, double nd,
+                                  double rsk, double caux, double smax, double thr) {
+    const uint32_t base = (uint32_t)m * kNiwAuxCalls;
+    const double g0 = chi2_mt(seed, i, t, kStreamAuxNiw, base, nu0);  // Bartlett a = 0, as niw_aux_core draws it
+    const double z1 = normal_at(seed, i, t, kStreamAuxNiw, base + kNiwAuxCalls - 1u, 0);
+    const double e = fma(-z1, rsk, nd * sqrt(g0));
+    const double l0 = log_pos(g0);
+    const double ub = fma(-0.5, e * e, fma(0.5, l0 + smax, caux));
+    const double mag = fabs(caux) + 0.5 * (fabs(l0) + fabs(smax)) + 0.5 * e * e;
+    if (ub + 1e-9 * mag + 1e-6 <= thr) return kZeroLogWeight;
+    double sumlog, b00, chi, zz;
+    niw_aux_core(seed, i, t, m, D, nu0, sumlog, b00, chi, zz);
+    return niw_aux_loglik(nd, sumlog, b00, chi, zz, rsk, caux);
+}
 // Candidates with log-weight <= running max - kSkip are skipped (DESIGN.md "Pick"): a relative weight
 // below e^-80 (1.8e-35) that no 53-bit uniform can resolve -- the reference's random_weighted_pick
 // (dim1algebra.hpp:2078-2104) draws one double u; skipping saves the exp and the division.

@@ -31,6 +31,7 @@ struct HypView {
     static constexpr int kLogam = kCaux + 2;
     static constexpr int kNu = kCaux + 3;
     static constexpr int kLT = kCaux + 4;
+    static constexpr int kSmax = kLT + DP;  // NIW screen: bound of the D-1 further log chi^2 draws
 };
 
 // ll = c - q/2 with q = d' P d.  Isotropic entries (iso > 0, a wave-uniform branch): q = iso * |d|^2;
@@ -382,8 +383,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NP8_ASSIGN_
         const double logam = hyp[HypView<D>::kLogam];
         if constexpr (PRIOR == kPriorNiw) {
 #pragma unroll 1
-            for (int m = 0; m < M; ++m) {
-                const double lw = prior_aux_ll<D, PRIOR>(hyp, ny, A.seed, ig, t, m) + logam;
+            for (int m = 0; m < M; ++m) {  // screened: T only grows, so a bound below T - kSkip now stays so
+                using H = HypView<D>;
+                const double lw = niw_aux_ll_screened(A.seed, ig, t, m, D, hyp[H::kNu], ny, hyp[H::kRsk], hyp[H::kCaux],
+                                                      hyp[H::kSmax], st.T - kSkip - logam) + logam;
                 ensure_u(st, lw, A.seed, ig, t);
                 pick_step(st, lw, K + m);
             }

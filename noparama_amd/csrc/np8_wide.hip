@@ -351,16 +351,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void n
     const int32_t zi = sorted ? zs[pc] : A.z[il];
     const int32_t jo = A.dense_of[zi];
 
-    // auxiliaries first (fp64, per lane): only |U^T (x - mu0)| of the item is needed
+    // the item's frame for the auxiliaries: only |U^T (x - mu0)| is needed
     double rown = 0.0;  // |x - muf_own|
-    double lwa[M];
-#pragma unroll
-    for (int m = 0; m < M; ++m) lwa[m] = 0.0;
+    double ny;
     {
         float xf[D];
 #pragma unroll
         for (int a = 0; a < D; ++a) xf[a] = X[(int64_t)a * n + xr];
-        const double ny = wide_whiten_norm<D>(hyp, xf);
+        ny = wide_whiten_norm<D>(hyp, xf);
         if (A.wdist) {  // the item's distance to its own row's fp32 mean (candidate pruning)
             const float *mo = A.wmu + (int64_t)zi * D;
             double d2 = 0.0;
@@ -370,13 +368,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void n
                 d2 = fma(dd, dd, d2);
             }
             rown = sqrt(d2);
-        }
-        const double logam = hyp[D + W::DP + 2];
-#pragma unroll 1
-        for (int m = 0; m < M; ++m) {
-            const double v = wide_aux_ll<D, PRIOR>(hyp, ny, A.seed, ig, t, m) + logam;
-#pragma unroll
-            for (int k = 0; k < M; ++k) lwa[k] = (k == m) ? v : lwa[k];  // no dynamic register index
         }
     }
 
@@ -411,6 +402,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void n
             st.T = fma(-0.5, q, e[F + kFieldC]) + e[F + kFieldLogn1];
         }
         pend &= ~__ballot(mine);
+    }
+
+    // the auxiliaries (fp64, per lane), after the own row: with the NIW prior each is screened against
+    // T_own - kSkip (the pick's T only grows), so most of them skip their D chi^2 draws
+    double lwa[M];
+    {
+        const double logam = hyp[D + W::DP + 2];
+#pragma unroll 1
+        for (int m = 0; m < M; ++m) {
+            double v;
+            if constexpr (PRIOR == kPriorNiw) {
+                const double caux = hyp[D + W::DP], rsk = hyp[D + W::DP + 1], nu = hyp[D + W::DP + 3];
+                const double smax = hyp[D + W::DP + 4 + W::DP];
+                v = niw_aux_ll_screened(A.seed, ig, t, m, D, nu, ny, rsk, caux, smax, st.T - kSkip - logam) + logam;
+            } else {
+                v = wide_aux_ll<D, PRIOR>(hyp, ny, A.seed, ig, t, m) + logam;
+            }
+#pragma unroll
+            for (int k = 0; k < M; ++k) lwa[k] = (k == m) ? v : lwa[k];  // no dynamic register index
+        }
     }
 
     // candidate pruning: a row is evaluated for the block when one of its items may pick it.  For lane x
