@@ -245,23 +245,32 @@ __global__ __launch_bounds__(256) void np8_wide_rows(WideArgs W) {
         double lo = (rowmax > 0.0) ? 1.0 / rowmax : 0.0, hi = dmin;
         double *Cw = Ri;  // the inverse is no longer needed: Cholesky workspace of P - beta I
         for (int it = 0; it < 8 && hi > lo; ++it) {
+            // right-looking Cholesky of P - beta I in LDS: a pivot, a row scaling and a trailing update per
+            // column, every step spread over the block (no long dependent chains)
             const double beta = 0.5 * (lo + hi);
-            for (int k = threadIdx.x; k < D * D; k += blockDim.x) Cw[k] = 0.0;
+            for (int k = threadIdx.x; k < D * D; k += blockDim.x) {
+                const int a = k / D, b = k - a * D;
+                const int i0 = a < b ? a : b, i1 = a < b ? b : a;
+                const double v = Pp[i0 * D - (i0 * (i0 - 1)) / 2 + (i1 - i0)];
+                Cw[k] = (a == b) ? v - beta : 0.5 * v;
+            }
             if (threadIdx.x == 0) pd = 1;
             __syncthreads();
             for (int jj = 0; jj < D; ++jj) {
                 if (threadIdx.x == 0) {
-                    double v = Pp[jj * D - (jj * (jj - 1)) / 2] - beta;
-                    for (int k = 0; k < jj; ++k) v = fma(-Cw[k * D + jj], Cw[k * D + jj], v);
+                    const double v = Cw[jj * D + jj];
                     if (!(v > 0.0)) pd = 0;
                     Cw[jj * D + jj] = (v > 0.0) ? sqrt(v) : 1.0;
                 }
                 __syncthreads();
                 if (!pd) break;  // block-uniform (read after the barrier)
-                for (int i = jj + 1 + threadIdx.x; i < D; i += blockDim.x) {
-                    double w = 0.5 * Pp[jj * D - (jj * (jj - 1)) / 2 + (i - jj)];
-                    for (int k = 0; k < jj; ++k) w = fma(-Cw[k * D + jj], Cw[k * D + i], w);
-                    Cw[jj * D + i] = w / Cw[jj * D + jj];
+                const double dj = Cw[jj * D + jj];
+                for (int i = jj + 1 + threadIdx.x; i < D; i += blockDim.x) Cw[jj * D + i] /= dj;
+                __syncthreads();
+                const int m = D - jj - 1;
+                for (int k = threadIdx.x; k < m * m; k += blockDim.x) {
+                    const int i = jj + 1 + k / m, l = jj + 1 + k % m;
+                    if (l >= i) Cw[i * D + l] = fma(-Cw[jj * D + i], Cw[jj * D + l], Cw[i * D + l]);
                 }
                 __syncthreads();
             }
