@@ -26,7 +26,13 @@ namespace {
 
 constexpr double kLog2PiC = 1.8378770664093454835606594728112;
 constexpr int kPruneMaxKcap = 4096;  // kcap x kcap int32 candidate lists (64 MB at the limit)
-constexpr uint32_t kGatherEvery = 4;  // data-parallel sweeps per gathering of fresh pruning radii
+#ifndef NP8_GATHER_EVERY
+#define NP8_GATHER_EVERY 10  // divides kGraphSweeps (the gathering pattern is baked into the sweep graph)
+#endif
+#ifndef NP8_RESORT_EVERY
+#define NP8_RESORT_EVERY 10
+#endif
+constexpr uint32_t kGatherEvery = NP8_GATHER_EVERY;  // data-parallel sweeps per gathering of fresh pruning radii
 
 struct Timer {
     hipEvent_t a = nullptr, b = nullptr;
@@ -69,6 +75,7 @@ struct np8_ctx {
     bool r2_zero = false;      // the radii in use are initialised (cleared at (re)start: every lane walks all)
     bool collecting = false;   // the running sweep prunes (a data-parallel sweep): lists after every step
     bool gather = false;       // ... and gathers fresh radii (every kGatherEvery-th sweep, or after a restart)
+    bool gath_clear = false;   // the last prune zeroed the gathered radius buffer for this sweep
     int64_t assign_waves = 0;  // waves of the last assign launch (its radius records)
     double *plr2 = nullptr;    // per dense row: the squared radius its candidate list assumes
     // data-parallel sweep in `substeps` synchronous sub-steps (np8_config.substeps): sub-step s is the
@@ -116,7 +123,7 @@ struct np8_ctx {
     int32_t *s_hist = nullptr, *s_cursor = nullptr, *s_off = nullptr;
     bool use_sorted = false;
     bool sorted_valid = false;
-    uint32_t resort_every = 4;
+    uint32_t resort_every = NP8_RESORT_EVERY;
     // sweep graphs: kGraphSweeps synchronous sweeps captured once and replayed (launch gaps)
     uint32_t t_base = 0;  // host mirror of ctl->t_base
     hipGraphExec_t graph = nullptr;
@@ -796,6 +803,10 @@ int launch_prune(np8_ctx *c, bool last) {
     P.D = c->D;
     P.kcap = c->kcap;
     P.gathered = (last && c->gather) ? 1 : 0;
+    // the next sweep gathers: clear its buffer here instead of with a memset node at its start (a stale
+    // buffer would only raise radii: pruning stays exact)
+    P.clear_next = (last && !P.gathered && c->r2_zero && (c->epoch + 1) % kGatherEvery == 0) ? 1 : 0;
+    c->gath_clear = P.clear_next != 0;
     HIPC(c, np8_launch_prune(P, c->kcap, c->stream));
     c->lists_valid = true;
     return NP8_OK;
@@ -858,11 +869,13 @@ int step(np8_ctx *c, int64_t p0, int64_t p1, const int64_t *order, bool use_perm
     if (!c->use_sorted) c->lists_valid = c->r2_zero = false;
     if (c->collecting && sub <= 0) {  // the start of a data-parallel sweep: gather radii on this one?
         c->gather = !c->r2_zero || c->epoch % kGatherEvery == 0;
+        const bool cleared = c->gath_clear && c->r2_zero;  // by the previous sweep's prune
+        c->gath_clear = false;
         if (!c->r2_zero) {  // no radii yet: every lane walks the table until the first gathered sweep ends
             HIPC(c, hipMemsetAsync(c->r2, 0, sizeof(double) * c->kcap, c->stream));
             c->r2_zero = true;
         }
-        if (c->gather) HIPC(c, hipMemsetAsync(c->r2 + c->kcap, 0, sizeof(double) * c->kcap, c->stream));
+        if (c->gather && !cleared) HIPC(c, hipMemsetAsync(c->r2 + c->kcap, 0, sizeof(double) * c->kcap, c->stream));
     }
     int r = launch_assign(c, p0, p1, order, use_perm);
     if (r) return r;

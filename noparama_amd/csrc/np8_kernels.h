@@ -157,6 +157,7 @@ struct PruneArgs {
     int32_t ls, D, kcap;
     int32_t gathered;   // the sweep's last step of a gathering sweep: lists from the gathered radii, which
                         // then become the radii in use
+    int32_t clear_next; // (not gathered) zero the gathered buffer for the next sweep, which gathers
 };
 
 struct FinArgs {

@@ -243,7 +243,10 @@ template <int D, int M, int PRIOR, bool COUNT>
 #ifndef NP8_ASSIGN_WAVES
 #define NP8_ASSIGN_WAVES 4
 #endif
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NP8_ASSIGN_WAVES))) void np8_assign(AssignArgs A) {
+#ifndef NP8_ASSIGN_BLOCK
+#define NP8_ASSIGN_BLOCK 64  // one wave per workgroup (256: 2% slower at C3)
+#endif
+__global__ __launch_bounds__(NP8_ASSIGN_BLOCK) __attribute__((amdgpu_waves_per_eu(NP8_ASSIGN_WAVES))) void np8_assign(AssignArgs A) {
     constexpr int DP = D * (D + 1) / 2;
     constexpr int CS = (D + DP + 5 + 1) & ~1;
     constexpr int F = D + DP;
@@ -1411,7 +1414,7 @@ bool np8_supported(int D, int M) {
 hipError_t np8_launch_assign(const AssignArgs &A, int D, int M, int prior, hipStream_t s) {
     const int64_t n = A.p1 - A.p0;
     if (n <= 0) return hipSuccess;
-    const dim3 grid((unsigned)((n + 255) / 256)), block(256);
+    const dim3 grid((unsigned)((n + NP8_ASSIGN_BLOCK - 1) / NP8_ASSIGN_BLOCK)), block(NP8_ASSIGN_BLOCK);
 #define X(d, m)                                                                                        \
     if (D == d && M == m) {                                                                            \
         if (prior == kPriorNiw)                                                                        \
@@ -1724,6 +1727,8 @@ __global__ __launch_bounds__(256) void np8_prune(PruneArgs A) {
     const double *src = A.r2 + (A.gathered ? A.kcap : 0);
     if (A.gathered && blockIdx.x == 0)
         for (int s = threadIdx.x; s < A.kcap; s += blockDim.x) A.r2[s] = A.r2[A.kcap + s];
+    if (A.clear_next && blockIdx.x == 0)  // only the radii in use are read here (not gathered)
+        for (int s = threadIdx.x; s < A.kcap; s += blockDim.x) A.r2[A.kcap + s] = 0.0;
     auto R2of = [&](int slot) { return src[slot]; };
     for (int k0 = blockIdx.x * 4 + (threadIdx.x >> 6); k0 < K; k0 += gridDim.x * 4)  // wave-uniform
         prune_row<DT>(A.cand, R2of, A.plist, A.plen, A.plr2, A.ls, A.D, K, k0);

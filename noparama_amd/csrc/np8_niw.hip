@@ -24,6 +24,15 @@ namespace {
 
 constexpr int kNiwThreads = 256;
 
+#ifdef NP8_EXP_NIW_TIMING  // experiment: phase cycle counts of np8_niw_post, block 0, printed
+#define NIW_T(k) \
+    if (threadIdx.x == 0) tph[k] = (long long)__builtin_amdgcn_s_memtime();
+#define NIW_SYNC() __syncthreads();
+#else
+#define NIW_T(k)
+#define NIW_SYNC()
+#endif
+
 __device__ __forceinline__ int pix(int D, int a, int b) { return a * D - (a * (a - 1)) / 2 + (b - a); }
 
 // (a, b), a > b, of the e-th strictly-lower element in row-major order (e = a(a-1)/2 + b).
@@ -60,22 +69,43 @@ __device__ double write_pprime(int D, int LD, const double *F, double *slotP, do
     return __syncthreads_and(iso ? 1 : 0) ? p00 : 0.0;
 }
 
-// Sigma = T^T T, B T = Rhs (B lower triangular): one thread per column of T, then per element.
+// Sigma = T^T T, B T = Rhs (B lower triangular).  T by right-looking forward substitution: row k is final
+// once divided by B_kk, then it updates every later row -- element (a, j) receives fma(-B_ak, T_kj, .) for
+// k = 0, ..., a - 1 in order from Rhs_aj, as the oracle's loop does.  Sigma in 2 x 2 blocks per thread (half
+// the LDS reads), each element one k-ordered chain.
 __device__ void write_sigma(int D, int LD, const double *B, const double *Rhs, bool rhs_transposed, double *T, double *Sigma) {
-    for (int j = threadIdx.x; j < D; j += blockDim.x)
-        for (int a = 0; a < D; ++a) {
-            double s = rhs_transposed ? Rhs[j * LD + a] : Rhs[a * LD + j];
-            #pragma unroll 8
-            for (int k = 0; k < a; ++k) s = fma(-B[a * LD + k], T[k * LD + j], s);
-            T[a * LD + j] = s / B[a * LD + a];
-        }
+    const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;  // 16 x 16 threads (no index division)
+    for (int a = ty; a < D; a += 16)
+        for (int j = tx; j < D; j += 16) T[a * LD + j] = rhs_transposed ? Rhs[j * LD + a] : Rhs[a * LD + j];
     __syncthreads();
-    for (int e = threadIdx.x; e < D * D; e += blockDim.x) {
-        const int a = e / D, b = e - a * D;
-        double s = 0.0;
-        #pragma unroll 8
-        for (int k = 0; k < D; ++k) s = fma(T[k * LD + a], T[k * LD + b], s);
-        Sigma[e] = s;
+    for (int k = 0; k < D; ++k) {
+        const double bkk = B[k * LD + k];
+        for (int j = threadIdx.x; j < D; j += blockDim.x) T[k * LD + j] = T[k * LD + j] / bkk;
+        __syncthreads();
+        for (int a = k + 1 + ty; a < D; a += 16)
+            for (int j = tx; j < D; j += 16) T[a * LD + j] = fma(-B[a * LD + k], T[k * LD + j], T[a * LD + j]);
+        __syncthreads();
+    }
+    const int H = (D + 1) / 2;  // 2 x 2 blocks (D even on every instantiated path; odd D: edge guarded)
+    for (int e = threadIdx.x; e < 16 * H; e += blockDim.x) {  // b-block e & 15 (+16 ...), a-block e >> 4
+      for (int bb = e & 15; bb < H; bb += 16) {
+        const int a = 2 * (e >> 4), b = 2 * bb;
+        const bool a1 = a + 1 < D, b1 = b + 1 < D;
+        double s00 = 0.0, s01 = 0.0, s10 = 0.0, s11 = 0.0;
+        #pragma unroll 4
+        for (int k = 0; k < D; ++k) {
+            const double ta0 = T[k * LD + a], ta1 = a1 ? T[k * LD + a + 1] : 0.0;
+            const double tb0 = T[k * LD + b], tb1 = b1 ? T[k * LD + b + 1] : 0.0;
+            s00 = fma(ta0, tb0, s00);
+            s01 = fma(ta0, tb1, s01);
+            s10 = fma(ta1, tb0, s10);
+            s11 = fma(ta1, tb1, s11);
+        }
+        Sigma[a * D + b] = s00;
+        if (b1) Sigma[a * D + b + 1] = s01;
+        if (a1) Sigma[(a + 1) * D + b] = s10;
+        if (a1 && b1) Sigma[(a + 1) * D + b + 1] = s11;
+      }
     }
 }
 
@@ -134,6 +164,10 @@ __global__ __launch_bounds__(kNiwThreads) void np8_niw_post(NiwArgs A) {
     const double k0 = A.kappa0, nd = (double)n;
     const double kn = k0 + nd, nun = A.nu0 + nd;
     const double kf = (k0 * nd) / kn;
+#ifdef NP8_EXP_NIW_TIMING
+    long long tph[12];
+#endif
+    NIW_T(0)
     zero_block(L, 3 * D * LD);  // L, Li, B: upper triangles stay 0
     for (int a = tid; a < D; a += blockDim.x) {
         anc[a] = (n > 0) ? A.slot_mu[(int64_t)s * D + a] : 0.0;
@@ -154,40 +188,45 @@ __global__ __launch_bounds__(kNiwThreads) void np8_niw_post(NiwArgs A) {
         L[r * LD + j] = fma(kf, dm[r] * dm[j], A.Psi0[r * D + j] + sc);
     }
     __syncthreads();
+    NIW_T(1)
+    // right-looking: per column the pivot and the scaled column, then the trailing update.  Element (r, c)
+    // receives fma(-L_rk, L_ck, .) for k = 0, 1, ... in order, then the division by its pivot: the
+    // operations of the oracle's left-looking loop, in its order.  (The pivot is read by every thread
+    // and written back after the barrier.)
     for (int j = 0; j < D; ++j) {
-        if (tid == 0) {
-            double v = L[j * LD + j];
-            #pragma unroll 8
-            for (int k = 0; k < j; ++k) v = fma(-L[j * LD + k], L[j * LD + k], v);
-            if (!(v > 0.0)) {
-                bad = 1;
-                v = 1.0;
-            }
-            L[j * LD + j] = sqrt(v);
+        const double v = L[j * LD + j];  // fully updated (behind the barrier)
+        if (!(v > 0.0)) {                // block-uniform
+            if (tid == 0) bad = 1;
+            break;
         }
+        const double dj = sqrt(v);
+        for (int r = j + 1 + tid; r < D; r += blockDim.x) L[r * LD + j] = L[r * LD + j] / dj;
         __syncthreads();
-        for (int r = j + 1 + tid; r < D; r += blockDim.x) {
-            double v = L[r * LD + j];
-            #pragma unroll 8
-            for (int k = 0; k < j; ++k) v = fma(-L[r * LD + k], L[j * LD + k], v);
-            L[r * LD + j] = v / L[j * LD + j];
-        }
+        if (tid == 0) L[j * LD + j] = dj;
+        for (int r = j + 1 + (tid >> 4); r < D; r += 16)  // 16 x 16 threads over (r, c), no index division
+            for (int c = j + 1 + (tid & 15); c <= r; c += 16) L[r * LD + c] = fma(-L[r * LD + j], L[c * LD + j], L[r * LD + c]);
         __syncthreads();
     }
+    __syncthreads();
+    NIW_T(2)
     if (bad) {  // block-uniform: not numerically positive definite, the slot keeps its parameters
         if (n > 0)
             for (int w = tid; w < W; w += blockDim.x) A.acc[(int64_t)s * W + w] = 0.0;
         return;
     }
-    for (int j = tid; j < D; j += blockDim.x) {  // Li = L^{-1}, one column per thread
-        Li[j * LD + j] = 1.0 / L[j * LD + j];
-        for (int r = j + 1; r < D; ++r) {
-            double v = 0.0;
-            #pragma unroll 8
-            for (int k = j; k < r; ++k) v = fma(-L[r * LD + k], Li[k * LD + j], v);
-            Li[r * LD + j] = v / L[r * LD + r];
-        }
+    // Li = L^{-1} (lower), right-looking over rows: row k is final once its sums are divided by L_kk, then
+    // it updates every later row -- element (r, j) receives fma(-L_rk, Li_kj, .) for k = j, ..., r - 1 in
+    // order from 0, as the oracle's column loop does
+    for (int k = 0; k < D; ++k) {
+        const double lkk = L[k * LD + k];
+        for (int j = tid; j <= k; j += blockDim.x) Li[k * LD + j] = (j == k) ? 1.0 / lkk : Li[k * LD + j] / lkk;
+        __syncthreads();
+        for (int r = k + 1 + (tid >> 4); r < D; r += 16)  // rows r > k, columns j <= k
+            for (int j = tid & 15; j <= k; j += 16) Li[r * LD + j] = fma(-L[r * LD + k], Li[k * LD + j], Li[r * LD + j]);
+        __syncthreads();
     }
+    NIW_SYNC()
+    NIW_T(3)
     for (int a = tid; a < D; a += blockDim.x) {  // Bartlett diagonal
         const double g = chi2_mt(A.seed, i, t, stream, kNiwGammaCalls * (uint32_t)a, nun - a);
         gv[a] = g;
@@ -201,6 +240,7 @@ __global__ __launch_bounds__(kNiwThreads) void np8_niw_post(NiwArgs A) {
     for (int j = tid; j < D; j += blockDim.x)
         z[j] = normal_at(A.seed, i, t, stream, kNiwNormalCall0, (uint32_t)(D * (D - 1) / 2 + j));
     __syncthreads();
+    NIW_T(4)
     if (tid == 0) {
         LogAcc la;
         for (int a = 0; a < D; ++a) la.add(gv[a], a, D - 1);
@@ -214,16 +254,18 @@ __global__ __launch_bounds__(kNiwThreads) void np8_niw_post(NiwArgs A) {
         F[a * LD + b] = v;
     }
     __syncthreads();
+    NIW_T(5)
     const int row = A.write_cand ? A.dense_of[s] : -1;
     const double iso = write_pprime(D, LD, F, A.slot_P + (int64_t)s * (D * (D + 1) / 2),
                                     row >= 0 ? A.cand + (int64_t)row * cand_stride(D) + D : nullptr);
-    if (tid == 0) {  // y = B^{-T} z / sqrt(kn)
+    NIW_T(6)
+    if (tid < 64) {  // y = B^{-T} z / sqrt(kn): one wave, lane a holds y_a's sum; column k leaves it as k falls
         const double rskn = 1.0 / sqrt(kn);
-        for (int a = D - 1; a >= 0; --a) {
-            double v = z[a] * rskn;
-            #pragma unroll 8
-            for (int k = a + 1; k < D; ++k) v = fma(-B[k * LD + a], y[k], v);
-            y[a] = v / B[a * LD + a];
+        double v = (tid < D) ? z[tid] * rskn : 0.0;
+        for (int k = D - 1; k >= 0; --k) {
+            const double yk = __shfl(v, k) / B[k * LD + k];
+            if (tid == k) y[k] = yk;
+            if (tid < k) v = fma(-B[k * LD + tid], yk, v);
         }
     }
     __syncthreads();
@@ -235,7 +277,17 @@ __global__ __launch_bounds__(kNiwThreads) void np8_niw_post(NiwArgs A) {
         A.slot_mu[(int64_t)s * D + a] = m;
         if (row >= 0) A.cand[(int64_t)row * cand_stride(D) + a] = m;
     }
+    NIW_SYNC()
+    NIW_T(7)
     write_sigma(D, LD, B, L, true, F, A.slot_sigma + (int64_t)s * D * D);  // T = B^{-1} L^T
+    NIW_SYNC()
+    NIW_T(8)
+#ifdef NP8_EXP_NIW_TIMING
+    if (tid == 0 && s < 2 && (t % 16) == 0)
+        printf("niw_post s=%d t=%u n=%ld phases %lld %lld %lld %lld %lld %lld %lld %lld\n", s, t, (long)n, tph[1] - tph[0],
+               tph[2] - tph[1], tph[3] - tph[2], tph[4] - tph[3], tph[5] - tph[4], tph[6] - tph[5], tph[7] - tph[6],
+               tph[8] - tph[7]);
+#endif
     if (tid == 0) {
         double sl = 0.0;
         for (int a = 0; a < D; ++a) sl += log_pos(L[a * LD + a]);

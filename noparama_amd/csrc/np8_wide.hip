@@ -182,105 +182,97 @@ __device__ __forceinline__ void row_glds(const float *__restrict__ wfrag, int sj
 }  // namespace
 
 // ---- table maintenance ---------------------------------------------------------------------------
+constexpr int kLamRounds = 5;  // eigenvalue-bound rounds of three concurrent Cholesky tests: 4^5 = 1024 steps
+
 // One block per slot (grid kcap): the slots flagged in wdirty get their factor and fp32 mean.
+// LDS: R [D][D] | three [D][D] workspaces.
 __global__ __launch_bounds__(256) void np8_wide_rows(WideArgs W) {
     const int s = blockIdx.x;
     if (!W.dirty[s] || W.cnt[s] <= 0) return;
-    const int D = W.D, DP = D * (D + 1) / 2;
+    const int D = W.D, DP = D * (D + 1) / 2, tid = threadIdx.x;
     extern __shared__ __attribute__((aligned(16))) double R[];
+    double *Wk = R + D * D;
     const double *Pp = W.slot_P + (int64_t)s * DP;
-    for (int k = threadIdx.x; k < D * D; k += blockDim.x) R[k] = 0.0;
-    __shared__ int ok_s;
+    auto pget = [&](int a, int b) {  // sym(P) upper element, a <= b (the packed P' doubles off-diagonals)
+        const double v = Pp[a * D - (a * (a - 1)) / 2 + (b - a)];
+        return (a == b) ? v : 0.5 * v;
+    };
+    for (int k = tid; k < D * D; k += blockDim.x) {
+        const int a = k / D, b = k - a * D;
+        R[k] = 0.0;
+        Wk[k] = (b >= a) ? pget(a, b) : 0.0;
+    }
     __syncthreads();
-    for (int j = 0; j < D; ++j) {
-        if (threadIdx.x == 0) {
-            double v = Pp[j * D - (j * (j - 1)) / 2];
-            for (int k = 0; k < j; ++k) v = fma(-R[k * D + j], R[k * D + j], v);
-            ok_s = v > 0.0;
-            if (!(v > 0.0)) atomicOr(&W.ctl->err, kErrSigma);
-            R[j * D + j] = (v > 0.0) ? sqrt(v) : 1e-300;
+    // R = chol_upper(P), right-looking: per column the pivot and the scaled row, then the trailing update.
+    // Element (i, l) receives its updates k = 0, 1, ... in order, each fma(-R_ki, R_kl, .), then the
+    // division by its pivot: the operations of the oracle's row-by-row form (np8o wide factor), in its order.
+    for (int jj = 0; jj < D; ++jj) {
+        const double v = Wk[jj * D + jj];  // fully updated (behind the barrier)
+        const bool ok = v > 0.0;           // block-uniform
+        const double dj = ok ? sqrt(v) : 1e-300;
+        if (tid == 0) {
+            R[jj * D + jj] = dj;
+            if (!ok) atomicOr(&W.ctl->err, kErrSigma);
         }
+        if (ok)
+            for (int i = jj + 1 + tid; i < D; i += blockDim.x) R[jj * D + i] = Wk[jj * D + i] / dj;
         __syncthreads();
-        if (ok_s)
-            for (int i = j + 1 + threadIdx.x; i < D; i += blockDim.x) {
-                double w = 0.5 * Pp[j * D - (j * (j - 1)) / 2 + (i - j)];
-                for (int k = 0; k < j; ++k) w = fma(-R[k * D + j], R[k * D + i], w);
-                R[j * D + i] = w / R[j * D + j];
-            }
+        if (ok)  // 16 x 16 threads over (i, l), l >= i (no index division)
+            for (int i = jj + 1 + (tid >> 4); i < D; i += 16)
+                for (int l = i + (((tid & 15) - (i - jj - 1)) & 15); l < D; l += 16)
+                    Wk[i * D + l] = fma(-R[jj * D + i], R[jj * D + l], Wk[i * D + l]);
         __syncthreads();
     }
-    // candidate pruning: lam_lo <= the smallest eigenvalue of P = R^T R.  Start: 1 / (a Gershgorin bound of
-    // the largest eigenvalue of P^{-1} = R^{-1} R^{-T}) -- valid, but loose by ~2x for a posterior draw at
-    // D = 64 -- then bisection towards min_i P_ii (an upper bound) by Cholesky tests: P - beta I positive
-    // definite <=> lambda_min(P) > beta.
+    // candidate pruning: lam_lo <= the smallest eigenvalue of P = R^T R, by Cholesky tests of P - beta I
+    // (positive definite <=> lambda_min(P) > beta) on [0, min_i P_ii]: each round tests three betas at
+    // once (quarter points), one barrier per column
     if (W.lam_lo) {
-        double *Ri = R + D * D;  // [D][D] upper triangular inverse
-        for (int c = threadIdx.x; c < D; c += blockDim.x) {
-            for (int i = D - 1; i >= 0; --i) {
-                double v = (i == c) ? 1.0 : 0.0;
-                for (int k = i + 1; k <= c; ++k) v = fma(-R[i * D + k], Ri[k * D + c], v);
-                Ri[i * D + c] = (i > c) ? 0.0 : v / R[i * D + i];
-            }
-        }
+        __shared__ double dmin;
+        if (tid == 0) dmin = 1e300;
         __syncthreads();
-        __shared__ double rowmax, dmin;
-        __shared__ int pd;
-        if (threadIdx.x == 0) {
-            rowmax = 0.0;
-            dmin = 1e300;
-        }
+        for (int i = tid; i < D; i += blockDim.x)
+            atomicMin(reinterpret_cast<unsigned long long *>(&dmin), (unsigned long long)__double_as_longlong(pget(i, i)));
         __syncthreads();
-        for (int i = threadIdx.x; i < D; i += blockDim.x) {
-            double rs = 0.0;
-            for (int k = 0; k < D; ++k) {
-                double v = 0.0;  // (R^{-1} R^{-T})_ik
-                for (int m = (i > k ? i : k); m < D; ++m) v = fma(Ri[i * D + m], Ri[k * D + m], v);
-                rs += fabs(v);
-            }
-            atomicMax(reinterpret_cast<unsigned long long *>(&rowmax), (unsigned long long)__double_as_longlong(rs));
-            const double pii = Pp[i * D - (i * (i - 1)) / 2];
-            atomicMin(reinterpret_cast<unsigned long long *>(&dmin), (unsigned long long)__double_as_longlong(pii));
-        }
-        __syncthreads();
-        double lo = (rowmax > 0.0) ? 1.0 / rowmax : 0.0, hi = dmin;
-        double *Cw = Ri;  // the inverse is no longer needed: Cholesky workspace of P - beta I
-        for (int it = 0; it < 8 && hi > lo; ++it) {
-            // right-looking Cholesky of P - beta I in LDS: a pivot, a row scaling and a trailing update per
-            // column, every step spread over the block (no long dependent chains)
-            const double beta = 0.5 * (lo + hi);
-            for (int k = threadIdx.x; k < D * D; k += blockDim.x) {
+        double lo = 0.0, hi = dmin;
+        for (int rd = 0; rd < kLamRounds && hi > lo; ++rd) {
+            double beta[3];
+#pragma unroll
+            for (int q = 0; q < 3; ++q) beta[q] = lo + (hi - lo) * (0.25 * (q + 1));
+            for (int k = tid; k < D * D; k += blockDim.x) {
                 const int a = k / D, b = k - a * D;
-                const int i0 = a < b ? a : b, i1 = a < b ? b : a;
-                const double v = Pp[i0 * D - (i0 * (i0 - 1)) / 2 + (i1 - i0)];
-                Cw[k] = (a == b) ? v - beta : 0.5 * v;
+                if (b < a) continue;
+                const double v = pget(a, b);
+#pragma unroll
+                for (int q = 0; q < 3; ++q) Wk[q * D * D + k] = (a == b) ? v - beta[q] : v;
             }
-            if (threadIdx.x == 0) pd = 1;
             __syncthreads();
-            for (int jj = 0; jj < D; ++jj) {
-                if (threadIdx.x == 0) {
-                    const double v = Cw[jj * D + jj];
-                    if (!(v > 0.0)) pd = 0;
-                    Cw[jj * D + jj] = (v > 0.0) ? sqrt(v) : 1.0;
+            int pd = 7;  // bit q: P - beta_q I still positive definite (block-uniform)
+            for (int jj = 0; jj < D && pd; ++jj) {
+                double r[3];
+#pragma unroll
+                for (int q = 0; q < 3; ++q) {
+                    const double v = Wk[q * D * D + jj * D + jj];
+                    if (!(v > 0.0)) pd &= ~(1 << q);
+                    r[q] = (v > 0.0) ? 1.0 / sqrt(v) : 0.0;
                 }
-                __syncthreads();
-                if (!pd) break;  // block-uniform (read after the barrier)
-                const double dj = Cw[jj * D + jj];
-                for (int i = jj + 1 + threadIdx.x; i < D; i += blockDim.x) Cw[jj * D + i] /= dj;
-                __syncthreads();
-                const int m = D - jj - 1;
-                for (int k = threadIdx.x; k < m * m; k += blockDim.x) {
-                    const int i = jj + 1 + k / m, l = jj + 1 + k % m;
-                    if (l >= i) Cw[i * D + l] = fma(-Cw[jj * D + i], Cw[jj * D + l], Cw[i * D + l]);
-                }
+                for (int i = jj + 1 + (tid >> 4); i < D; i += 16)
+                    for (int l = i + (((tid & 15) - (i - jj - 1)) & 15); l < D; l += 16) {
+#pragma unroll
+                        for (int q = 0; q < 3; ++q) {
+                            if (!(pd >> q & 1)) continue;
+                            double *C = Wk + q * D * D;
+                            C[i * D + l] = fma(-(C[jj * D + i] * r[q]), C[jj * D + l] * r[q], C[i * D + l]);
+                        }
+                    }
                 __syncthreads();
             }
-            if (pd) lo = beta;  // block-uniform
-            else hi = beta;
-            __syncthreads();
+            // pd is monotone in beta: the largest positive definite beta is the new lower end
+            const int top = (pd & 4) ? 3 : (pd & 2) ? 2 : (pd & 1) ? 1 : 0;
+            if (top > 0) lo = beta[top - 1];
+            if (top < 3) hi = beta[top];
         }
         // 1% for the fp32 factor and the fp32 contraction, and the Cholesky's own rounding
-        if (threadIdx.x == 0) W.lam_lo[s] = 0.99 * lo;
-        __syncthreads();
+        if (tid == 0) W.lam_lo[s] = 0.99 * lo;
     }
     float *An = W.wA + (int64_t)s * D * D;
     for (int k = threadIdx.x; k < D * D; k += blockDim.x) An[k] = (float)R[k];
@@ -663,7 +655,10 @@ hipError_t np8_launch_loglik_wide_mfma(const AssignArgs &A, int D, double *parti
 // being accumulated S += D^T D on v_mfma_f64_16x16x4_f64 (items = the k dimension: 4 per MFMA, 16 steps
 // per chunk, the 16x16 tiles ti <= tj of S), items of other slots masked to 0.  Sums stay in registers
 // while the slot does not change and are committed with fp64 atomics when it does.
-constexpr int kSuffChunks = 8;
+#ifndef NP8_SUFF_CHUNKS
+#define NP8_SUFF_CHUNKS 8
+#endif
+constexpr int kSuffChunks = NP8_SUFF_CHUNKS;
 
 template <int D>
 __global__ __launch_bounds__(256) void np8_suffstats_wide(ParamArgs P) {
@@ -699,7 +694,11 @@ __global__ __launch_bounds__(256) void np8_suffstats_wide(ParamArgs P) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int a = 16 * ti + g + 4 * r, b = 16 * tj + col;  // f64 MFMA layout
+#ifdef NP8_EXP_SUFF_NOATOMIC  // experiment (wrong sums): plain stores instead of atomics
+                    if (a <= b) dst[D + a * D - (a * (a - 1)) / 2 + (b - a)] = acc[q][r];
+#else
                     if (a <= b) unsafeAtomicAdd(dst + D + a * D - (a * (a - 1)) / 2 + (b - a), acc[q][r]);
+#endif
                 }
 #pragma unroll
         for (int t = 0; t < T; ++t) {
@@ -830,7 +829,15 @@ hipError_t np8_launch_wide_dist(const WideArgs &W, hipStream_t s) {
 }
 
 hipError_t np8_launch_wide_refresh(const WideArgs &W, hipStream_t s) {
-    hipLaunchKernelGGL(np8_wide_rows, dim3((unsigned)W.kcap), dim3(256), 2 * sizeof(double) * W.D * W.D, s, W);
+    const size_t lds = 4 * sizeof(double) * W.D * W.D;  // 128 KB at D = 64
+    static bool allowed = false;  // (set before the first launch, which is not inside a graph capture)
+    if (!allowed) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&np8_wide_rows),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)(4 * sizeof(double) * 64 * 64));
+        if (e != hipSuccess) return e;
+        allowed = true;
+    }
+    hipLaunchKernelGGL(np8_wide_rows, dim3((unsigned)W.kcap), dim3(256), lds, s, W);
     hipLaunchKernelGGL(np8_wide_clean, dim3((unsigned)((W.kcap + 255) / 256)), dim3(256), 0, s, W);
     return hipGetLastError();
 }

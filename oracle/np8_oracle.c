@@ -1138,11 +1138,13 @@ static int niw_draw_impl(const np8o_ctx *c, uint64_t i, uint32_t t, uint32_t str
     niw_outputs_from_F(D, F, Ppk);
     /* mu = mun + Ln B^{-T} z rskn */
     const double rskn = 1.0 / sqrt(kn);
-    double y[NP8O_DMAX];
-    for (int a = D - 1; a >= 0; --a) {
-        double s = z[a] * rskn;
-        for (int k = a + 1; k < D; ++k) s = fma(-B[k * D + a], y[k], s);
-        y[a] = s / B[a * D + a];
+    /* back substitution by columns: y_k = acc_k / B_kk for k = D-1, ..., 0, each leaving fma(-B_ka, y_k, acc_a)
+     * in the sums of a < k (acc_a from z_a rskn; the device runs it on one wave, np8_niw.hip) */
+    double y[NP8O_DMAX], acc[NP8O_DMAX];
+    for (int a = 0; a < D; ++a) acc[a] = z[a] * rskn;
+    for (int k = D - 1; k >= 0; --k) {
+        y[k] = acc[k] / B[k * D + k];
+        for (int a = 0; a < k; ++a) acc[a] = fma(-B[k * D + a], y[k], acc[a]);
     }
     for (int a = 0; a < D; ++a) {
         double s = 0.0;

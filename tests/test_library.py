@@ -36,13 +36,13 @@ def test_create_rejects_bad_configuration_without_crashing():
     mu0 = np.zeros(5)
     lam = np.eye(5)
     cfg = np8._Config()
-    cfg.D, cfg.M, cfg.alpha = 5, 3, 1.0  # D = 5 has no kernel instantiation
+    cfg.D, cfg.M, cfg.alpha = 5, 2, 1.0  # (D, M) = (5, 2) has no kernel instantiation
     cfg.mu0 = mu0.ctypes.data_as(C.POINTER(C.c_double))
     cfg.Lambda = lam.ctypes.data_as(C.POINTER(C.c_double))
     cfg.kappa, cfg.nu, cfg.kcap, cfg.device = 0.002, 4.0, 16, -1
     h = C.c_void_p()
     assert L.np8_create(C.byref(h), C.byref(cfg)) == np8.NP8_ERR_ARG
-    cfg.D = 2
+    cfg.D, cfg.M = 2, 3
     lam2 = -np.eye(2)  # not SPD
     cfg.Lambda = lam2.ctypes.data_as(C.POINTER(C.c_double))
     assert L.np8_create(C.byref(h), C.byref(cfg)) == np8.NP8_ERR_ARG
