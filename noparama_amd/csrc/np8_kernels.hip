@@ -513,8 +513,13 @@ __global__ __launch_bounds__(NP8_ASSIGN_BLOCK) __attribute__((amdgpu_waves_per_e
         if (s != zi) {
             atomicSub(delta + zi, 1);
             atomicAdd(delta + s, 1);
-            A.z[il] = s;
-            if (sorted) zs[p] = s;
+            // the item's addresses again (a rare path): two 64-bit addresses kept live through the draw were
+            // spilled to scratch for every item (19 of the 38 MB the C3 launch wrote)
+            int64_t pq = A.p0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+            asm volatile("" : "+v"(pq));
+            const int64_t lq = sorted ? (int64_t)__atomic_load_n(ids + pq, __ATOMIC_RELAXED) : position_to_local(A, pq);
+            A.z[key_item(lq)] = s;
+            if (sorted) zs[pq] = s;
         }
     } else {
         const int q = atomicAdd(A.nreq, 1);

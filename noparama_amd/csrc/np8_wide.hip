@@ -323,7 +323,10 @@ __global__ void np8_wide_clean(WideArgs W) {
 // ---- the sweep kernel -----------------------------------------------------------------------------
 // Dynamic LDS: two candidate-row stages of Wide<D>::ROW floats (33 KB at D = 64).
 template <int D, int M, int PRIOR>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void np8_assign_wide(AssignArgs A) {
+#ifndef NP8_WIDE_WAVES
+#define NP8_WIDE_WAVES 2
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NP8_WIDE_WAVES, NP8_WIDE_WAVES))) void np8_assign_wide(AssignArgs A) {
     using W = Wide<D>;
     constexpr int CS = W::CS, F = W::F;
     extern __shared__ __attribute__((aligned(16))) float stage[];
