@@ -183,6 +183,7 @@ __device__ __forceinline__ void row_glds(const float *__restrict__ wfrag, int sj
 
 // ---- table maintenance ---------------------------------------------------------------------------
 constexpr int kLamRounds = 5;  // eigenvalue-bound rounds of three concurrent Cholesky tests: 4^5 = 1024 steps
+constexpr double kLamRelWidth = 0.02;  // ... or fewer, once the bracket [lo, hi] is within 2% of hi
 
 // One block per slot (grid kcap): the slots flagged in wdirty get their factor and fp32 mean.
 // LDS: R [D][D] | three [D][D] workspaces.
@@ -234,10 +235,20 @@ __global__ __launch_bounds__(256) void np8_wide_rows(WideArgs W) {
             atomicMin(reinterpret_cast<unsigned long long *>(&dmin), (unsigned long long)__double_as_longlong(pget(i, i)));
         __syncthreads();
         double lo = 0.0, hi = dmin;
+        // warm start: the slot's bound from its last factorisation (the parameters of a cluster move a
+        // little per sweep) bracketed first; a stale one (a reused slot) only costs that round
+        const double prev = W.lam_lo[s] / 0.99;
+        const bool warm = prev > 0.0 && prev < hi;
         for (int rd = 0; rd < kLamRounds && hi > lo; ++rd) {
             double beta[3];
+            if (rd == 0 && warm) {
+                beta[0] = 0.93 * prev;
+                beta[1] = 0.98 * prev;
+                beta[2] = fmin(1.02 * prev, 0.5 * (prev + hi));
+            } else {
 #pragma unroll
-            for (int q = 0; q < 3; ++q) beta[q] = lo + (hi - lo) * (0.25 * (q + 1));
+                for (int q = 0; q < 3; ++q) beta[q] = lo + (hi - lo) * (0.25 * (q + 1));
+            }
             for (int k = tid; k < D * D; k += blockDim.x) {
                 const int a = k / D, b = k - a * D;
                 if (b < a) continue;
@@ -270,6 +281,7 @@ __global__ __launch_bounds__(256) void np8_wide_rows(WideArgs W) {
             const int top = (pd & 4) ? 3 : (pd & 2) ? 2 : (pd & 1) ? 1 : 0;
             if (top > 0) lo = beta[top - 1];
             if (top < 3) hi = beta[top];
+            if (hi - lo <= kLamRelWidth * hi) break;  // block-uniform
         }
         // 1% for the fp32 factor and the fp32 contraction, and the Cholesky's own rounding
         if (tid == 0) W.lam_lo[s] = 0.99 * lo;
