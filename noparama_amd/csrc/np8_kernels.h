@@ -129,7 +129,7 @@ struct AssignArgs {
     const float *wfrag;
     const float *wmu;          // natural fp32 means [kcap][D]
     const double *lam_lo;      // [kcap] precision eigenvalue lower bounds (np8_wide_rows)
-    const double *wdist;       // [K][kcap] squared distances between row means (np8_wide_dist); null: no pruning
+    const double *wdist;       // [K][kcap] distances between row means (np8_wide_dist); null: no pruning
 };
 
 // Wide-path tables (np8_wide.hip), maintained for the slots flagged in dirty.

@@ -308,8 +308,8 @@ __global__ __launch_bounds__(256) void np8_wide_rows(WideArgs W) {
     for (int a = threadIdx.x; a < D; a += blockDim.x) W.wmu[(int64_t)s * D + a] = (float)W.slot_mu[(int64_t)s * D + a];
 }
 
-// Candidate pruning (DESIGN.md "Wide path"): squared distances between the fp32 means of the dense rows,
-// in fp64, wdist[j0 * kcap + j].  One block per row j0 (a grid of kcap; rows >= K exit).
+// Candidate pruning (DESIGN.md "Wide path"): distances between the fp32 means of the dense rows, in fp64,
+// wdist[j0 * kcap + j].  One block per row j0 (a grid of kcap; rows >= K exit).
 __global__ __launch_bounds__(256) void np8_wide_dist(WideArgs W) {
     const int K = W.ctl->K, j0 = blockIdx.x;
     if (j0 >= K) return;
@@ -324,7 +324,7 @@ __global__ __launch_bounds__(256) void np8_wide_dist(WideArgs W) {
             const double dd = (double)mj[a] - (double)m0[a];
             d2 = fma(dd, dd, d2);
         }
-        W.wdist[(int64_t)j0 * W.kcap + j] = d2;
+        W.wdist[(int64_t)j0 * W.kcap + j] = sqrt(d2);  // the distance itself: no square root per lane and row
     }
 }
 
@@ -458,7 +458,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NP8_WIDE_WA
             bool need = false;
             if (wave_live && valid && sj != zi) {
                 const double base = e[F + kFieldC] + e[F + kFieldLogn];
-                const double gap = fmax(sqrt(A.wdist[(int64_t)jo * A.kcap + j]) - rown, 0.0);
+                const double gap = fmax(A.wdist[(int64_t)jo * A.kcap + j] - rown, 0.0);
                 const double far = 0.5 * A.lam_lo[sj] * gap * gap;
                 const double U = base - far - Tl;
                 need = !(U <= -kSkip - 2.0 - 1e-9 * (fabs(base) + fabs(Tl) + far));
