@@ -57,7 +57,7 @@ struct np8_ctx {
     std::vector<double> U, Uinv;
     double *d_U = nullptr, *d_Uinv = nullptr, *d_Psi0 = nullptr;
     int64_t *pend = nullptr;
-    // wide path (NP8_CONTRACT_F32_MFMA, D in {32, 64}): fp32 items in X/Xs, fp32 MFMA contraction
+    // wide path (NP8_CONTRACT_F32_MFMA, D in {32, 48, 64}): fp32 items in X/Xs, fp32 MFMA contraction
     int contraction = NP8_CONTRACT_F64;
     bool wide = false;
     float *wA = nullptr, *wfrag = nullptr, *wmu = nullptr;

@@ -823,6 +823,8 @@ __device__ void frame_to_vmu_d(const FinArgs &F, const double *frame, int64_t i,
 __device__ void frame_to_vmu(const FinArgs &F, const double *frame, int64_t i, int m, double *vmu) {
     if (F.D == 32)
         frame_to_vmu_d<32>(F, frame, i, m, vmu);
+    else if (F.D == 48)
+        frame_to_vmu_d<48>(F, frame, i, m, vmu);
     else
         frame_to_vmu_d<64>(F, frame, i, m, vmu);
 }

@@ -1,4 +1,4 @@
-// np8_wide.hip -- the wide path (DESIGN.md "Wide path"; BASELINE.json config C5): D in {32, 64}, items
+// np8_wide.hip -- the wide path (DESIGN.md "Wide path"; BASELINE.json config C5): D in {32, 48, 64}, items
 // held in fp32, cluster likelihoods through fp32 MFMA (v_mfma_f32_16x16x4_f32, exact k-ordered fmaf
 // chains), everything else (auxiliary draws, the categorical pick, counts) in fp64 as on the narrow path.
 //
@@ -656,6 +656,8 @@ hipError_t np8_launch_loglik_wide_mfma(const AssignArgs &A, int D, double *parti
     if (nb <= 0) return hipSuccess;
     if (D == 32)
         hipLaunchKernelGGL((np8_loglik_wide_mfma<32>), dim3((unsigned)nb), dim3(256), 0, s, A, partial);
+    else if (D == 48)
+        hipLaunchKernelGGL((np8_loglik_wide_mfma<48>), dim3((unsigned)nb), dim3(256), 0, s, A, partial);
     else if (D == 64)
         hipLaunchKernelGGL((np8_loglik_wide_mfma<64>), dim3((unsigned)nb), dim3(256), 0, s, A, partial);
     else
@@ -772,6 +774,8 @@ hipError_t np8_launch_suffstats_wide(const ParamArgs &P, hipStream_t s) {
     if (nb <= 0) return hipSuccess;
     if (P.D == 32)
         hipLaunchKernelGGL((np8_suffstats_wide<32>), dim3((unsigned)nb), dim3(256), 0, s, P);
+    else if (P.D == 48)
+        hipLaunchKernelGGL((np8_suffstats_wide<48>), dim3((unsigned)nb), dim3(256), 0, s, P);
     else if (P.D == 64)
         hipLaunchKernelGGL((np8_suffstats_wide<64>), dim3((unsigned)nb), dim3(256), 0, s, P);
     else
@@ -780,7 +784,7 @@ hipError_t np8_launch_suffstats_wide(const ParamArgs &P, hipStream_t s) {
 }
 
 // ---- dispatch ----------------------------------------------------------------------------------------
-#define NP8_WIDE_FOR_EACH(X) X(32, 3) X(64, 3)
+#define NP8_WIDE_FOR_EACH(X) X(32, 3) X(48, 3) X(64, 3)
 
 bool np8_wide_supported(int D, int M) {
 #define X(d, m) \
@@ -831,6 +835,8 @@ hipError_t np8_launch_loglik_wide(const LoglikArgs &L, const WideArgs &W, int D,
     if (nb <= 0) return hipSuccess;
     if (D == 32)
         hipLaunchKernelGGL((np8_loglik_wide<32>), dim3((unsigned)nb), dim3(256), 0, s, L, W);
+    else if (D == 48)
+        hipLaunchKernelGGL((np8_loglik_wide<48>), dim3((unsigned)nb), dim3(256), 0, s, L, W);
     else if (D == 64)
         hipLaunchKernelGGL((np8_loglik_wide<64>), dim3((unsigned)nb), dim3(256), 0, s, L, W);
     else

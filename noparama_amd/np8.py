@@ -76,7 +76,7 @@ class _Config(C.Structure):
 
 PARAM_UPDATE = {"frozen": 0, "mh_g0": 1, "niw_conjugate": 2}  # NP8_PARAM_* (include/np8.h)
 PRIOR = {"reference": 0, "niw": 1}  # NP8_PRIOR_*
-CONTRACTION = {"f64": 0, "f32": 1}  # NP8_CONTRACT_*: "f32" = the fp32 MFMA wide path (D in {32, 64})
+CONTRACTION = {"f64": 0, "f32": 1}  # NP8_CONTRACT_*: "f32" = the fp32 MFMA wide path (D in {32, 48, 64})
 
 
 class Stats(C.Structure):
@@ -201,7 +201,7 @@ class NealAlgorithm8:
     or beyond the free slots are deferred to the item's next update (lowest scan positions first).
     `prior`: "reference" (the reference's G0 as it draws) or "niw" (a proper Normal-Inverse-Wishart with
     kappa0 = kappa, nu0 = nu >= D + 1, Psi0 = Lambda).  `contraction`: "f64" (D <= 16) or "f32" (D in
-    {32, 64}: items in fp32, cluster likelihoods on the fp32 matrix cores; config C5).
+    {32, 48, 64}: items in fp32, cluster likelihoods on the fp32 matrix cores; config C5).
     `substeps`: the data-parallel sweep (chunk 0) as S synchronous sub-steps over a fixed hash partition of
     the items (DESIGN.md "Sub-steps"); 1 = one step against the sweep-start state.
     """

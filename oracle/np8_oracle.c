@@ -496,7 +496,7 @@ np8o_ctx *np8o_create(const np8o_config *cfg) {
         return NULL;
     if (cfg->prior == NP8O_PRIOR_NIW && !(cfg->nu >= cfg->D + 1.0 && cfg->nu < 1e12)) return NULL;
     if (cfg->contraction != NP8O_CONTRACT_F64 &&
-        !(cfg->contraction == NP8O_CONTRACT_F32 && (cfg->D == 32 || cfg->D == 64) &&
+        !(cfg->contraction == NP8O_CONTRACT_F32 && (cfg->D == 32 || cfg->D == 48 || cfg->D == 64) &&
           cfg->param_update != NP8O_PARAM_MH_G0))
         return NULL;
     if (cfg->req_max < 0 || cfg->req_max > NP8O_REQMAX) return NULL;

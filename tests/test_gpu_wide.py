@@ -1,4 +1,4 @@
-"""GPU parity of the wide path (DESIGN.md "Wide path"; config C5): D in {32, 64}, fp32 items, the
+"""GPU parity of the wide path (DESIGN.md "Wide path"; config C5): D in {32, 48, 64}, fp32 items, the
 cluster likelihoods contracted on the fp32 matrix cores (v_mfma_f32_32x32x2_f32).
 
 The oracle restates the contraction (NP8O_CONTRACT_F32: fmaf chains in k order, the accumulator
@@ -46,7 +46,7 @@ def assert_state(a, b):
     assert np.array_equal(sa["sigma"], sb["sigma"])
 
 
-@pytest.mark.parametrize("D", [32, 64])
+@pytest.mark.parametrize("D", [32, 48, 64])
 @pytest.mark.parametrize("prior", ["reference", "niw"])
 def test_wide_loglik_matrix_bit_exact(D, prior):
     X, _, _ = mixture(D, 1500, 8, D)
@@ -63,7 +63,7 @@ def test_wide_loglik_matrix_bit_exact(D, prior):
     np.testing.assert_allclose(lg[:, :K], ref[:, :K], rtol=F32_LL_RTOL)
 
 
-@pytest.mark.parametrize("D", [32, 64])
+@pytest.mark.parametrize("D", [32, 48, 64])
 @pytest.mark.parametrize("prior", ["reference", "niw"])
 def test_wide_sweeps_bit_exact(D, prior):
     """Warm start (the data's own clusters, unit covariances): the C5 benchmark's situation."""
@@ -138,7 +138,7 @@ def test_wide_graph_replay_bit_exact():
     assert_state(g, o)
 
 
-@pytest.mark.parametrize("D", [32, 64])
+@pytest.mark.parametrize("D", [32, 48, 64])
 def test_wide_niw_conjugate_chain(D):
     """niw_conjugate on the wide path: statistics on the fp64 matrix cores (np8_suffstats_wide), summed
     in another order than the oracle's item loop, so posterior parameters agree to ~1e-13 relative and
