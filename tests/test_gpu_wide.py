@@ -1,5 +1,5 @@
 """GPU parity of the wide path (DESIGN.md "Wide path"; config C5): D in {32, 48, 64}, fp32 items, the
-cluster likelihoods contracted on the fp32 matrix cores (v_mfma_f32_32x32x2_f32).
+cluster likelihoods contracted on the fp32 matrix cores (v_mfma_f32_16x16x4_f32, 16-row tiles of the triangular factor).
 
 The oracle restates the contraction (NP8O_CONTRACT_F32: fmaf chains in k order, the accumulator
 layout's fp64 summation order), so labels, counts, parameters and log-likelihoods are bit-exact.  The
