@@ -65,7 +65,7 @@ def parse():
     a.d = a.d if a.d is not None else (64 if c5 else 8)
     a.k = a.k if a.k is not None else (256 if c5 else 64)
     if a.traffic_json is None:
-        a.traffic_json = os.path.join(ROOT, "profiles", "traffic_r02h_c5.json" if c5 else "traffic_r02j.json")
+        a.traffic_json = os.path.join(ROOT, "profiles", "traffic_r02j_c5.json" if c5 else "traffic_r02j.json")
     return a
 
 
