@@ -34,6 +34,22 @@ FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X FP32 matrix peak (MI355X_MICROARCH.md: 1
 HBM_PEAK_GBS = 8000.0
 
 
+def binding_roof(exec_flops, abytes, ms, peak_tflops, kname):
+    """The roof that binds the kernel as it runs: its executed flops (device counters, after
+    exact pruning) against the compute peak, or its algorithmic bytes (item row + label per item) against
+    HBM -- whichever fraction is larger.  Without executed counts the HBM roof is reported."""
+    hbm_gbs = abytes / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
+    exec_tf = exec_flops / (ms * 1e-3) / 1e12 if (exec_flops is not None and ms > 0) else None
+    if exec_tf is not None and exec_tf / peak_tflops > hbm_gbs / HBM_PEAK_GBS:
+        return {"bound": "mfma", "achieved": exec_tf, "peak": peak_tflops, "unit": "TFLOP/s",
+                "frac": exec_tf / peak_tflops,
+                "note": f"kernel {kname}: executed flops (device counters, after exact pruning) / launch time"}
+    return {"bound": "hbm", "achieved": hbm_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": hbm_gbs / HBM_PEAK_GBS,
+            "algorithmic_bytes_per_launch": abytes,
+            "note": f"kernel {kname}: algorithmic bytes (item row + label per item) / launch time; the "
+                    "executed flops after exact pruning are a smaller fraction of the compute peak"}
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -235,20 +251,8 @@ def main():
         except Exception:
             traffic = None
 
-    # the binding roof of the kernel as it runs: the executed flops (device counters) against the compute
-    # peak, or the algorithmic bytes (X row + label per item) against HBM -- whichever fraction is larger
-    abytes = float(n_items) * (xbytes + 8)
-    hbm_gbs = abytes / (ms_assign * 1e-3) / 1e9 if ms_assign > 0 else 0.0
-    exec_tf = exec_flops / (ms_assign * 1e-3) / 1e12 if (exec_flops is not None and ms_assign > 0) else None
-    kname = "np8_assign_wide" if wide else "np8_assign"
-    if exec_tf is not None and exec_tf / peak > hbm_gbs / HBM_PEAK_GBS:
-        binding = {"bound": "mfma", "achieved": exec_tf, "peak": peak, "unit": "TFLOP/s", "frac": exec_tf / peak,
-                   "note": f"kernel {kname}: executed flops (device counters, after exact pruning) / launch time"}
-    else:
-        binding = {"bound": "hbm", "achieved": hbm_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                   "frac": hbm_gbs / HBM_PEAK_GBS, "algorithmic_bytes_per_launch": abytes,
-                   "note": f"kernel {kname}: algorithmic bytes (item row + label per item) / launch time; the "
-                           "executed flops after exact pruning are a smaller fraction of the compute peak"}
+    binding = binding_roof(exec_flops, float(n_items) * (xbytes + 8), ms_assign, peak,
+                           "np8_assign_wide" if wide else "np8_assign")
 
     if rank == 0:
         cpu = None
