@@ -172,10 +172,11 @@ def main():
             smp.sweep(n, sync=sync)
             return
         for _ in range(n):  # fallback transport: the exchange record through host memory
-            rec = torch.from_numpy(smp.step_local())
-            out = [torch.zeros_like(rec) for _ in range(world)]
-            dist.all_gather(out, rec)
-            smp.step_merge(np.concatenate([o.numpy() for o in out]), world)
+            for _ in range(smp.substeps):  # one record exchange per synchronous sub-step, then the sweep's end
+                rec = torch.from_numpy(smp.step_local())
+                out = [torch.zeros_like(rec) for _ in range(world)]
+                dist.all_gather(out, rec)
+                smp.step_merge(np.concatenate([o.numpy() for o in out]), world)
             if args.param_update == "frozen":
                 smp.end_sweep()
             else:  # the per-cluster statistics summed over ranks on the host transport
@@ -223,7 +224,10 @@ def main():
     n_launch = st1["n_timed_assign"] - st0["n_timed_assign"]
     ms_assign = (st1["ms_assign"] - st0["ms_assign"]) / max(n_launch, 1)
     Kc = Kfinal + smp.M
-    n_items = hi - lo
+    # items of one assign launch: with S sub-steps a sweep makes S launches over ~N/S items each, and the
+    # timed launch is one of them (per-launch bytes/flops, not per-sweep)
+    S = max(args.substeps, 1)
+    n_items = (hi - lo) / S
     # N (K+M) (D^2 + 2D + 4) for the fp64 table form (packed P: D(D+1)/2 multiply-adds
     # plus d = x - mu and the weight).  Wide path: the triangular factor form y = A (x - mu), |y|^2:
     # D subtractions + D(D+1)/2 multiply-adds + D squares-and-adds = D^2 + 4D per item and candidate
@@ -236,8 +240,8 @@ def main():
     xbytes = 4 * D if wide else 8 * D
     # executed work: quadratic forms the kernel evaluated (device counters), at their real cost
     # (isotropic rows: D subtractions + D multiply-adds + scale, weight = 3D + 3 flops)
-    nq = (sc1["n_quad"] - sc0["n_quad"]) / cnt_sweeps if cnt_sweeps else 0.0  # per sweep (= per launch)
-    nq_iso = (sc1["n_quad_iso"] - sc0["n_quad_iso"]) / cnt_sweeps if cnt_sweeps else 0.0
+    nq = (sc1["n_quad"] - sc0["n_quad"]) / cnt_sweeps / S if cnt_sweeps else 0.0  # per launch
+    nq_iso = (sc1["n_quad_iso"] - sc0["n_quad_iso"]) / cnt_sweeps / S if cnt_sweeps else 0.0
     if wide:  # item-row contractions on the matrix cores (pruned rows skipped), at the MACs of the 16-row tiles
         exec_flops = nq * 2 * sum(16 * (D - 16 * t) for t in range(D // 16)) if cnt_sweeps else None
     else:
@@ -309,9 +313,9 @@ def main():
                              "cost, over the timed launch time; the M auxiliary G0 draws per item (Philox, "
                              "Box-Muller, chi^2 logs) are not flops of this count"),
                     "quad_forms_per_item": nq / max(n_items, 1),
-                    "aux_exact_per_item": (sc1["aux_exact_lanes"] - sc0["aux_exact_lanes"]) / cnt_sweeps / max(n_items, 1),
+                    "aux_exact_per_item": (sc1["aux_exact_lanes"] - sc0["aux_exact_lanes"]) / cnt_sweeps / max(hi - lo, 1),
                     "aux_exact_wave_frac": (sc1["aux_exact_waves"] - sc0["aux_exact_waves"]) / cnt_sweeps
-                    / max(((n_items + 63) // 64) * smp.M, 1),
+                    / max(((hi - lo + 63) // 64) * smp.M, 1),
                     "aux_screen_violations": sc1["screen_violations"] - sc0["screen_violations"],
                     "iso_fraction": nq_iso / max(nq, 1),
                     "tflops": exec_flops / (ms_assign * 1e-3) / 1e12 if ms_assign > 0 else None,

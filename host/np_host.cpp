@@ -221,6 +221,8 @@ void NealAlgorithm8Hip::setData(const dataset_t &dataset) {
         for (int a = 0; a < D; ++a) X[(size_t)i * D + a] = (*dataset[i])[a];
     }
     check(np8_set_data(_ctx, X.data(), _N, D, 0, _N), "np8_set_data");
+    _tracked = nullptr;  // np8_set_data drops the device change log: the next patch reloads the whole state
+    _slot_id.clear();
 }
 
 void NealAlgorithm8Hip::initRandom(int K) { check(np8_init_random(_ctx, K), "np8_init_random"); }

@@ -1,12 +1,41 @@
 // results_selftest.cpp -- writes the output files of a small hand-built membertrix (no GPU needed);
 // tests/test_host_driver.py checks their format against the reference's (src/np_results.cpp).
+//
+// results_selftest --metrics <file>: the product's clustering_performance::calculate (the one that
+// writes results.score.txt, reference src/clustering_performance.cpp:38-82) over label pairs read
+// from <file> -- two lines per case, the ground truth then the result, whitespace-separated ints --
+// printing "purity rand_index adjusted_rand_index" per case at full precision.
+#include <cstdio>
+#include <fstream>
 #include <iostream>
+#include <sstream>
+#include <string>
 
 #include "np_results.h"
 
+static int metrics(const char *path) {
+    std::ifstream in(path);
+    if (!in) {
+        std::cerr << "results_selftest: cannot read " << path << std::endl;
+        return 2;
+    }
+    std::string lt, lr;
+    while (std::getline(in, lt) && std::getline(in, lr)) {
+        std::vector<int> a, b;
+        std::istringstream st(lt), sr(lr);
+        for (int v; st >> v;) a.push_back(v);
+        for (int v; sr >> v;) b.push_back(v);
+        clustering_performance cp;
+        cp.calculate(a, b);
+        std::printf("%.17g %.17g %.17g\n", cp.purity, cp.rand_index, cp.adjusted_rand_index);
+    }
+    return 0;
+}
+
 int main(int argc, char **argv) {
+    if (argc == 3 && std::string(argv[1]) == "--metrics") return metrics(argv[2]);
     if (argc < 2) {
-        std::cerr << "usage: results_selftest <workspace/>" << std::endl;
+        std::cerr << "usage: results_selftest <workspace/> | --metrics <file>" << std::endl;
         return 1;
     }
     membertrix m;

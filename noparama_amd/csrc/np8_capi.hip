@@ -89,6 +89,7 @@ struct np8_ctx {
     double caux = 0, rsk = 0, logam = 0;
     // data / state
     int64_t n_loc = 0, offset = 0, n_glob = 0;
+    uint64_t data_hash = 0;  // of the items as np8_set_data received them (checkpoints name their data)
     bool have_data = false, have_state = false;
     uint32_t epoch = 0;
     int32_t checks = 0;
@@ -192,6 +193,19 @@ int fail(np8_ctx *c, int code, const std::string &msg) {
     } while (0)
 
 int packed_index(int D, int a, int b) { return a * D - (a * (a - 1)) / 2 + (b - a); }
+
+// 64-bit FNV-1a over 8-byte words (checkpoint identity, not a security hash)
+uint64_t hash_words(uint64_t h, const void *p, size_t bytes) {
+    const unsigned char *b = static_cast<const unsigned char *>(p);
+    for (size_t i = 0; i < bytes; i += 8) {
+        uint64_t w = 0;
+        std::memcpy(&w, b + i, (bytes - i) < 8 ? (bytes - i) : 8);
+        h = (h ^ w) * 0x100000001b3ull;
+        h ^= h >> 29;
+    }
+    return h;
+}
+
 
 // LU with partial pivoting (what Eigen's MatrixXd::inverse()/determinant() use,
 // multivariatenormal.cpp:87,90).  Row-major.  Returns false when singular.
@@ -1409,6 +1423,7 @@ int np8_set_data(np8_ctx *c, const double *X, int64_t n, int32_t D, int64_t offs
     for (int64_t p = 0; p < n; ++p) c->sub_start[substep_of(c->seed, offset + p, (uint32_t)c->substeps) + 1] += 1;
     for (int k = 0; k < c->substeps; ++k) c->sub_start[(size_t)k + 1] += c->sub_start[(size_t)k];
     c->sub_next = 0;
+    c->data_hash = hash_words(0xcbf29ce484222325ull ^ (uint64_t)n, X, sizeof(double) * (size_t)n * D);
     c->track = 0;  // a change log needs a new baseline for the new items
     c->vis_tag.assign((size_t)n, 0u);
     c->vis_n.assign((size_t)n, 0u);
@@ -1608,11 +1623,22 @@ namespace {
 struct CkptHeader {
     char magic[8];
     int32_t D, M, kcap, substeps, prior, contraction, checks, have_best;
+    int32_t param_update, mh_steps, req_max, pad0;
+    int64_t chunk;
     int64_t n_loc, offset, n_glob, n_new, n_rejected, mh_accepted;
-    uint64_t seed;
+    uint64_t seed, hyper_hash, data_hash;
     uint32_t epoch, pad;
     double L, best[2];
 };
+
+// the chain's hyper-parameters: alpha, kappa, nu, mu0, Lambda (the base measure of either prior)
+uint64_t hyper_hash(const np8_ctx *c) {
+    uint64_t h = 0xcbf29ce484222325ull;
+    const double s[3] = {c->alpha, c->kappa, c->nu};
+    h = hash_words(h, s, sizeof(s));
+    h = hash_words(h, c->mu0.data(), sizeof(double) * c->mu0.size());
+    return hash_words(h, c->Lambda.data(), sizeof(double) * c->Lambda.size());
+}
 
 struct CkptPart {
     void *dev;
@@ -1653,7 +1679,13 @@ int np8_checkpoint(np8_ctx *c, void *out, int64_t bytes) {
     if (r) return r;
     CkptHeader H;
     std::memset(&H, 0, sizeof(H));
-    std::memcpy(H.magic, "NP8CKPT1", 8);
+    std::memcpy(H.magic, "NP8CKPT2", 8);
+    H.param_update = c->param_update;
+    H.mh_steps = c->mh_steps;
+    H.req_max = c->req_max;
+    H.chunk = c->chunk;
+    H.hyper_hash = hyper_hash(c);
+    H.data_hash = c->data_hash;
     H.D = c->D;
     H.M = c->M;
     H.kcap = c->kcap;
@@ -1690,10 +1722,13 @@ int np8_restore(np8_ctx *c, const void *in, int64_t bytes) {
         return fail(c, NP8_ERR_ARG, "np8_restore: size differs from this context's checkpoint");
     CkptHeader H;
     std::memcpy(&H, in, sizeof(H));
-    if (std::memcmp(H.magic, "NP8CKPT1", 8) != 0 || H.D != c->D || H.M != c->M || H.kcap != c->kcap ||
-        H.substeps != c->substeps || H.prior != c->prior || H.contraction != c->contraction || H.n_loc != c->n_loc ||
-        H.offset != c->offset || H.n_glob != c->n_glob || H.seed != c->seed)
-        return fail(c, NP8_ERR_ARG, "np8_restore: checkpoint of another configuration, seed or data shard");
+    if (std::memcmp(H.magic, "NP8CKPT2", 8) != 0 || H.D != c->D || H.M != c->M || H.kcap != c->kcap ||
+        H.substeps != c->substeps || H.prior != c->prior || H.contraction != c->contraction ||
+        H.param_update != c->param_update || H.mh_steps != c->mh_steps || H.req_max != c->req_max ||
+        H.chunk != c->chunk || H.hyper_hash != hyper_hash(c) || H.seed != c->seed)
+        return fail(c, NP8_ERR_ARG, "np8_restore: checkpoint of another configuration or seed");
+    if (H.n_loc != c->n_loc || H.offset != c->offset || H.n_glob != c->n_glob || H.data_hash != c->data_hash)
+        return fail(c, NP8_ERR_ARG, "np8_restore: checkpoint of other data or another data shard");
     drop_graph(c);
     HIPC(c, hipStreamSynchronize(c->stream));
     const unsigned char *p = static_cast<const unsigned char *>(in) + sizeof(H);
@@ -1877,6 +1912,8 @@ int np8_update_points(np8_ctx *c, const int64_t *ids, int64_t n) {
 int np8_end_sweep(np8_ctx *c) {
     if (!c) return NP8_ERR_ARG;
     if (!c->have_state) return fail(c, NP8_ERR_STATE, "np8_end_sweep: no state");
+    if (c->sub_next != 0)
+        return fail(c, NP8_ERR_STATE, "np8_end_sweep: the sweep's sub-steps are not all done (np8_step_local/np8_step_merge)");
     return end_sweep(c);
 }
 
@@ -2125,6 +2162,8 @@ int np8_end_sweep_stats(np8_ctx *c, const double *summed) {
     if (!c || !summed) return NP8_ERR_ARG;
     if (!c->have_state) return fail(c, NP8_ERR_STATE, "np8_end_sweep_stats: no state");
     if (c->param_update == NP8_PARAM_FROZEN) return fail(c, NP8_ERR_STATE, "np8_end_sweep_stats: frozen parameters");
+    if (c->sub_next != 0)
+        return fail(c, NP8_ERR_STATE, "np8_end_sweep_stats: the sweep's sub-steps are not all done");
     const size_t nacc = (size_t)c->kcap * (c->D + c->DP);
     HIPC(c, hipMemcpyAsync(c->acc, summed, sizeof(double) * nacc, hipMemcpyHostToDevice, c->stream));
     int r = end_sweep(c, true);

@@ -112,7 +112,10 @@ __device__ __forceinline__ double niw_aux_ll(const double *__restrict__ hyp, dou
 // fp32 on the transcendental units (v_log_f32, v_sqrt_f32, v_cos_f32/v_sin_f32 in revolutions,
 // v_rcp_f32); the margin covers those approximations with a factor of ten: |error of r cos, r sin| <=
 // 4e-3 (3.5e-4 from rounding u0 to fp32 near 1), relative 1e-4 elsewhere, chi_extra_err for chi_extra.
-// Returns +inf (no screen) near v = 0 (|v| < 1/4), where log|v| and ny/|v| are ill-conditioned.
+// |v| enters only through the interval [av_lo, av_hi], which contains it whenever the error of g0 is within
+// dg, so the bound stays valid for small |v|: ny/|v| and -D log|v| grow there, and the relative margin grows
+// with them (qlb and D |log av_lo| are in err).  Returns +inf (no screen) when av_lo < 0.02, which keeps the
+// interval away from 0; tests/test_gpu_screen.py drives many lanes into |v| in [0.02, 0.25] in count mode.
 template <int D>
 __device__ __forceinline__ float aux_screen_ub(const uint32_t (&w)[4], float chi_extra, float chi_extra_err, float ny,
                                                float nu, float rsk, float caux, float thr) {

@@ -264,6 +264,8 @@ class NealAlgorithm8:
         if X.ndim != 2 or X.shape[1] != self.D:
             raise ValueError("X must be [n, D]")
         self.N = X.shape[0]
+        # np8_set_data drops the device change log: the next patch() reloads the whole state
+        self._tracked, self._slot_id = None, {}
         self._check(lib().np8_set_data(self._h, _p(X), self.N, self.D, int(offset),
                                        int(self.N if n_global is None else n_global)))
 

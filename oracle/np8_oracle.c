@@ -1195,8 +1195,9 @@ static void wide_factor(np8o_ctx *c, int s) {
             R[j * D + i] = w / R[j * D + j];
         }
     }
-    float *A = c->wA + (size_t)s * D * D;
-    for (int k = 0; k < D * D; ++k) A[k] = (float)R[k];
+    float *At = c->wA + (size_t)s * D * D; /* transposed: At[b][a] = fp32(R[a][b]) */
+    for (int a = 0; a < D; ++a)
+        for (int b = 0; b < D; ++b) At[b * D + a] = (float)R[a * D + b];
     for (int a = 0; a < D; ++a) c->wmu[(size_t)s * D + a] = (float)c->slot_mu[(size_t)s * D + a];
 }
 
@@ -1206,13 +1207,16 @@ static void wide_factor(np8o_ctx *c, int s) {
  * r inner): the lane groups of the 16x16 accumulator layout; ll = c - q/2 in fp64. */
 static double wide_q(const np8o_ctx *c, const double *x, int sj) {
     const int D = c->D;
-    const float *A = c->wA + (size_t)sj * D * D, *mj = c->wmu + (size_t)sj * D;
+    const float *At = c->wA + (size_t)sj * D * D, *mj = c->wmu + (size_t)sj * D;
     float xt[NP8O_DMAX], y[NP8O_DMAX];
     for (int b = 0; b < D; ++b) xt[b] = (float)x[b] - mj[b];
-    for (int a = 0; a < D; ++a) {
-        float v = 0.0f;
-        for (int b = 0; b < D; ++b) v = fmaf(A[a * D + b], xt[b], v);
-        y[a] = v;
+    /* R is upper triangular: A[a][b] = 0 for b < a, and fmaf(0, t, v) = v, so each row's chain starts at
+     * b = a; the rows' chains run interleaved (b outer), each still in increasing b */
+    for (int a = 0; a < D; ++a) y[a] = 0.0f;
+    for (int b = 0; b < D; ++b) {
+        const float t = xt[b];
+        const float *col = At + (size_t)b * D;
+        for (int a = 0; a <= b; ++a) y[a] = fmaf(col[a], t, y[a]);
     }
     float s[4] = {0.0f, 0.0f, 0.0f, 0.0f};
     for (int g = 0; g < 4; ++g)

@@ -1,0 +1,99 @@
+"""GPU parity at the full benchmarked configurations (VERDICT r2 "Next round" #1).
+
+The bench's own workloads (`bench.workload`) are run through the HIP path and through the
+oracle's synchronous sweep (OpenMP, 16 threads on the GPU box) from the same state with the same seed:
+
+  * C3: N = 1e6, D = 8, K = 64, the warm state, 5 eager sweeps then one 20-sweep graph replay (the sweep
+    graph the bench times, with timing events on as in the bench), sorted layout, candidate pruning and the
+    radius gathering; labels, counts, K, the max-likelihood snapshot bit-exact, total log-likelihood 1e-11.
+  * C5: N = 1e6, D = 64, K = 256, the NIW prior, fp32 items and the fp32 MFMA contraction: 2 frozen sweeps
+    bit-exact (parameters too); 1 `niw_conjugate` sweep: labels and counts bit-exact, parameters within
+    DESIGN.md 7's 1e-10 (statistics summed in another order).
+
+Reference semantics: /root/reference/src/np_neal_algorithm8.cpp:49-167, np_mcmc.cpp:109-175.
+"""
+import argparse
+
+import numpy as np
+import pytest
+
+import bench
+import oracle as O
+from noparama_amd import NealAlgorithm8
+
+pytestmark = pytest.mark.gpu
+
+THREADS = 16
+
+
+def bench_workload(config, **over):
+    a = argparse.Namespace(n=1_000_000, d=64 if config == "C5" else 8, k=256 if config == "C5" else 64,
+                           seed=20261015, kcap=0, substeps=1, config=config)
+    for k, v in over.items():
+        setattr(a, k, v)
+    return a, bench.workload(a)
+
+
+def same(g, o, which=0, exact_params=True):
+    sg, so = g.state(which), o.state(which)
+    assert sg["K"] == so["K"], (sg["K"], so["K"])
+    diff = np.flatnonzero(sg["z"] != so["z"])
+    assert diff.size == 0, f"{diff.size} labels differ, first at {diff[:8]}"
+    assert np.array_equal(sg["counts"], so["counts"])
+    if exact_params:
+        assert np.array_equal(sg["mu"], so["mu"])
+        assert np.array_equal(sg["sigma"], so["sigma"])
+    else:
+        np.testing.assert_allclose(sg["mu"], so["mu"], rtol=1e-10, atol=1e-10)
+        np.testing.assert_allclose(sg["sigma"], so["sigma"], rtol=1e-10, atol=1e-12)
+    return sg
+
+
+@pytest.mark.timeout(300)
+def test_c3_full_size_warm_graph_bit_exact():
+    args, (X, z, mu, sig, opts) = bench_workload("C3")
+    g = NealAlgorithm8(8, seed=args.seed, device=0, **opts)
+    o = O.Chain(8, seed=args.seed, kcap=g.kcap, chunk=0)
+    O.set_threads(THREADS)
+    try:
+        g.set_timing(True)
+        for c in (g, o):
+            c.set_data(X)
+            c.set_state(z, mu, sig)
+        g.sweep(5)
+        o.sweep(5)
+        same(g, o)
+        g.sweep(20)  # one captured 20-sweep graph replay, as the bench times it
+        o.sweep(20)
+        st = same(g, o)
+        same(g, o, which=1)
+        assert g.stats()["epoch"] == o.epoch
+        np.testing.assert_allclose(g.total_loglik(), o.total_loglik(), rtol=1e-11)
+        np.testing.assert_allclose(g.stats()["best_loglik"], o.best_loglik(), rtol=1e-11)
+        print(f"C3 N=1e6 25 sweeps: K={st['K']} bit-exact")
+    finally:
+        O.set_threads(1)
+        g.close()
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("param_update,sweeps", [("frozen", 2), ("niw_conjugate", 1)])
+def test_c5_full_size_bit_exact(param_update, sweeps):
+    args, (X, z, mu, sig, opts) = bench_workload("C5")
+    kw = {k: v for k, v in opts.items()}
+    g = NealAlgorithm8(64, seed=args.seed, device=0, param_update=param_update, **kw)
+    o = O.Chain(64, seed=args.seed, param_update=param_update, **kw)
+    O.set_threads(THREADS)
+    try:
+        for c in (g, o):
+            c.set_data(X)
+            c.set_state(z, mu, sig)
+        for _ in range(sweeps):
+            g.sweep(1)
+            o.sweep(1)
+            st = same(g, o, exact_params=(param_update == "frozen"))
+        np.testing.assert_allclose(g.total_loglik(), o.total_loglik(), rtol=1e-10)
+        print(f"C5 N=1e6 D=64 {param_update} {sweeps} sweeps: K={st['K']} labels bit-exact")
+    finally:
+        O.set_threads(1)
+        g.close()

@@ -108,3 +108,22 @@ def test_single_item_updates_patch_membertrix():
             assert_coherent(trix, smp)
     finally:
         smp.close()
+
+
+def test_patch_after_new_data_reloads_membertrix():
+    """np8_set_data drops the device change log; the next update() must reload the whole state
+    into the membertrix (first contact) instead of failing on change tracking being off."""
+    X, _ = datasets.read_data(os.path.join(HERE, "golden", "twogaussians.data"))
+    smp = NealAlgorithm8(2, seed=31, kcap=256, device=0)
+    try:
+        smp.set_data(X)
+        smp.init_random(20)
+        trix = membertrix(X.shape[0])
+        smp.update(trix, np.arange(X.shape[0]))
+        assert_coherent(trix, smp)
+        smp.set_data(X[::-1].copy())  # new items
+        smp.init_random(10)
+        smp.update(trix, np.arange(X.shape[0]))
+        assert_coherent(trix, smp)
+    finally:
+        smp.close()

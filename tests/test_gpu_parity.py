@@ -266,6 +266,50 @@ def test_host_exchange_two_ranks_equals_one(req_max):
     del z, mu, sig
 
 
+@pytest.mark.parametrize("param_update", ["frozen", "mh_g0"])
+def test_host_exchange_substeps_equals_oracle(param_update):
+    """the host-exchange transport (MPI/gloo) with S = 4 sub-steps runs S record exchanges
+    (np8_step_local / np8_step_merge) per sweep and then ends the sweep; ending it earlier is an error.
+    Two ranks on one GPU against the oracle's single chain, bit-exact."""
+    X, _, mu, sig = datasets.mixture(6000, 8, 12, 0.8, 6.0, seed=19)
+    N, S = X.shape[0], 4
+    o = O.Chain(8, seed=55, kcap=512, substeps=S, param_update=param_update)
+    o.set_data(X)
+    o.init_random(12)
+    o.sweep(3)
+    ranks = [NealAlgorithm8(8, seed=55, kcap=512, device=0, substeps=S, param_update=param_update)
+             for _ in range(2)]
+    bounds = [(0, 2900), (2900, N)]
+    for r, c in enumerate(ranks):
+        c.comm_init(None, r, 2)
+        c.set_data(X[bounds[r][0]:bounds[r][1]], offset=bounds[r][0], n_global=N)
+        c.init_random(12)
+    for sweep in range(3):
+        for s in range(S):
+            recs = np.concatenate([c.step_local() for c in ranks])
+            for c in ranks:
+                c.step_merge(recs, 2)
+            if sweep == 0 and s == 0:
+                with pytest.raises(NP8Error):
+                    ranks[0].end_sweep()  # three sub-steps still to go
+        if param_update == "frozen":
+            for c in ranks:
+                c.end_sweep()
+        else:
+            st = sum(c.param_stats_local() for c in ranks)
+            for c in ranks:
+                c.end_sweep_stats(st)
+    so = o.state()
+    z2 = np.concatenate([c.state()["z"] for c in ranks])
+    assert np.array_equal(so["z"], z2)
+    for c in ranks:
+        st = c.state()
+        assert st["K"] == so["K"] and np.array_equal(st["counts"], so["counts"])
+        np.testing.assert_allclose(st["mu"], so["mu"], rtol=1e-13, atol=1e-13)
+    for c in ranks:
+        c.close()
+
+
 # ---- cluster-parameter update (mh_g0, UpdateClusters as intended) ------------------------------------
 # The statistics are fp64 sums whose order differs between the device (wave reduction + atomics) and
 # the oracle (item order); decisions u < exp(LL' - LL) can only differ when the two sides fall within

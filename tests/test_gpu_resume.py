@@ -44,16 +44,28 @@ def test_resumed_chain_equals_uninterrupted(param_update, substeps):
         b.close()
 
 
-def test_restore_rejects_other_configuration():
+@pytest.mark.parametrize("other", [dict(seed=2), dict(param_update="mh_g0"), dict(alpha=2.0), dict(kappa=0.01),
+                                   dict(req_max=64), dict(mh_steps=5), dict(chunk=100), "data"])
+def test_restore_rejects_other_configuration(other):
+    """a checkpoint names its configuration (parameter update, MH steps, req_max, chunk, the
+    hyper-parameters) and its data (a hash of the items np8_set_data received); restoring it into anything
+    else fails instead of silently continuing as another chain."""
     X = datasets.config_c3(N=5000)[0]
-    a = NealAlgorithm8(8, seed=1, kcap=512, device=0)
-    b = NealAlgorithm8(8, seed=2, kcap=512, device=0)
+    base = dict(seed=1, kcap=512, device=0)
+    a = NealAlgorithm8(8, **base)
+    b = NealAlgorithm8(8, **{**base, **(other if isinstance(other, dict) else {})})
     try:
         a.set_data(X)
         a.init_random(20)
-        b.set_data(X)
+        ck = a.checkpoint()
+        if other == "data":
+            X2 = X.copy()
+            X2[1234, 3] += 1e-9
+            b.set_data(X2)
+        else:
+            b.set_data(X)
         with pytest.raises(NP8Error):
-            b.restore(a.checkpoint())
+            b.restore(ck)
     finally:
         a.close()
         b.close()

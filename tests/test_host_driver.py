@@ -62,6 +62,53 @@ def test_results_files_in_reference_format(tmp_path):
         "Purity: 1\nRand Index: 1\nAdjusted Rand Index: 1\n")
 
 
+def test_product_metrics_match_sklearn_goldens(tmp_path):
+    """the product's clustering_performance::calculate (host/np_host.cpp, which writes
+    results.score.txt; reference src/clustering_performance.cpp:38-82 with int64 counts instead of its
+    int32 ones) against sklearn's adjusted_rand_score / rand_score and a numpy purity
+    (tests/golden/metrics.json), plus one case past the reference's int32 overflow (N = 200 000)."""
+    import json
+    import math
+
+    import numpy as np
+
+    exe = os.path.join(ROOT, "host", "build", "results_selftest")
+    cases = json.load(open(os.path.join(ROOT, "tests", "golden", "metrics.json")))
+    big = np.repeat([0, 1, 2, 3], 50_000)
+    big_res = big.copy()
+    big_res[::7] = (big_res[::7] + 1) % 4
+    p = tmp_path / "pairs.txt"
+    with open(p, "w") as f:
+        for c in cases:
+            f.write(" ".join(map(str, c["truth"])) + "\n" + " ".join(map(str, c["result"])) + "\n")
+        f.write(" ".join(map(str, big)) + "\n" + " ".join(map(str, big_res)) + "\n")
+    r = subprocess.run([exe, "--metrics", str(p)], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    rows = [list(map(float, ln.split())) for ln in r.stdout.strip().splitlines()]
+    assert len(rows) == len(cases) + 1
+    for c, (pur, ri, ari) in zip(cases, rows):
+        assert abs(pur - c["purity"]) <= 1e-12
+        assert abs(ri - c["rand_index"]) <= 1e-12
+        if math.isnan(ari):
+            # the reference's formula is 0/0 (both labellings one cluster, or both all singletons):
+            # clustering_performance.cpp:75 divides anyway (NaN); sklearn defines that case as 1.0
+            assert c["ari"] == 1.0 and (len(set(c["truth"])) in (1, len(c["truth"])))
+        else:
+            assert abs(ari - c["ari"]) <= 1e-12, (ari, c["ari"])
+    # the large case against the int64 formula computed here (sklearn's own formula, in Python ints)
+    F = np.zeros((4, 4), dtype=object)
+    np.add.at(F, (big, big_res), 1)
+    comb = lambda v: v * (v - 1) // 2  # noqa: E731
+    a = sum(comb(int(v)) for v in F.ravel())
+    b = sum(comb(int(v)) for v in F.sum(axis=1))
+    c_ = sum(comb(int(v)) for v in F.sum(axis=0))
+    S = comb(big.size)
+    exp_ari = (a - b * c_ / S) / ((b + c_) / 2 - b * c_ / S)
+    assert abs(rows[-1][0] - sum(F.max(axis=0)) / big.size) <= 1e-12
+    assert abs(rows[-1][1] - ((2 * a - b - c_) / S + 1)) <= 1e-12
+    assert abs(rows[-1][2] - exp_ari) <= 1e-12
+
+
 def test_f64_data_roundtrip(tmp_path):
     from noparama_amd import datasets
 
