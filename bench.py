@@ -32,6 +32,9 @@ sys.path.insert(0, ROOT)
 FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector (= FP64 matrix) peak, vendor spec
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X FP32 matrix peak (MI355X_MICROARCH.md: 155 measured)
 HBM_PEAK_GBS = 8000.0
+# committed rocprofv3 PMC summaries of the assign kernels (HBM bytes per launch, tools/prof*.sh)
+C3_TRAFFIC = "traffic_r02j.json"
+C5_TRAFFIC = "traffic_r02j_c5.json"
 
 
 def binding_roof(exec_flops, abytes, ms, peak_tflops, kname):
@@ -69,6 +72,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget (0 = skip)")
     ap.add_argument("--cold-sweeps", type=int, default=20,
                     help="cold leg: sweeps from the reference's initialisation (init_random(20)), 0 = skip")
+    ap.add_argument("--no-c5", dest="c5_sub", action="store_false",
+                    help="skip the C5 sub-record of the default (C3) run")
     ap.add_argument("--traffic-json", default=None,
                     help="HBM bytes per assign launch from the committed PMC profile of this config")
     ap.add_argument("--sampler", default="neal8", choices=["neal8", "jain_neal", "triadic"],
@@ -81,7 +86,7 @@ def parse():
     a.d = a.d if a.d is not None else (64 if c5 else 8)
     a.k = a.k if a.k is not None else (256 if c5 else 64)
     if a.traffic_json is None:
-        a.traffic_json = os.path.join(ROOT, "profiles", "traffic_r02j_c5.json" if c5 else "traffic_r02j.json")
+        a.traffic_json = os.path.join(ROOT, "profiles", C5_TRAFFIC if c5 else C3_TRAFFIC)
     return a
 
 
@@ -184,92 +189,20 @@ def main():
                 dist.all_reduce(st)
                 smp.end_sweep_stats(st.numpy())
 
-    # timing (event pairs around one assign launch per graph replay, plus the executed-work counters)
-    # is on from the start, so the timed region replays the graph warm-up captured; np8_prepare_sweeps
-    # captures and uploads the graph of the timed sweeps if the warm-up did not (warm-up < 20 sweeps)
-    smp.set_timing(True)
-    sweeps(args.warmup)  # includes np8_sync
-    if transport != "gloo":
-        smp.prepare_sweeps(args.steps)
-    torch.cuda.synchronize()
-    st0 = smp.stats()
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    sweeps(args.steps, sync=False)
-    smp.sync()
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    t1 = time.perf_counter()
-    dt = t1 - t0
-    if dist:
-        tt = torch.tensor([dt], dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt = float(tt.item())
-    st1 = smp.stats()
-    Kfinal = st1["K"]
-    # executed-work counters over separate (untimed) sweeps: they add scalar loads and atomics per wave
-    cnt_sweeps = 20 if transport != "gloo" else 0
-    if cnt_sweeps:
-        smp.set_timing(True, counters=True)
-        sc0 = smp.stats()
-        sweeps(cnt_sweeps)
-        sc1 = smp.stats()
-        smp.set_timing(True)
-
-    # roofline of the dominant kernel (np8_assign): algorithmic flops per launch / avg launch time
-    # every launch is timed when sweeps go one by one; one per 20-sweep graph replay otherwise
-    n_launch = st1["n_timed_assign"] - st0["n_timed_assign"]
-    ms_assign = (st1["ms_assign"] - st0["ms_assign"]) / max(n_launch, 1)
-    Kc = Kfinal + smp.M
-    # items of one assign launch: with S sub-steps a sweep makes S launches over ~N/S items each, and the
-    # timed launch is one of them (per-launch bytes/flops, not per-sweep)
-    S = max(args.substeps, 1)
-    n_items = (hi - lo) / S
-    # N (K+M) (D^2 + 2D + 4) for the fp64 table form (packed P: D(D+1)/2 multiply-adds
-    # plus d = x - mu and the weight).  Wide path: the triangular factor form y = A (x - mu), |y|^2:
-    # D subtractions + D(D+1)/2 multiply-adds + D squares-and-adds = D^2 + 4D per item and candidate
-    # (SURVEY.md's 2D^2 + 4D counts a full D x D contraction, which the kernel does not perform).
-    flops = float(n_items) * Kc * ((D * D + 4 * D) if wide else (D * D + 2 * D + 4))
-    # what the matrix cores execute on the wide path: 16-row tiles of the triangular A, 2 flops per MAC
-    mfma_flops = float(n_items) * Kc * 2 * sum(16 * (D - 16 * t) for t in range(D // 16)) if wide else None
-    achieved = flops / (ms_assign * 1e-3) / 1e12 if ms_assign > 0 else 0.0
-    peak = FP32_MFMA_PEAK_TFLOPS if wide else FP64_PEAK_TFLOPS
-    xbytes = 4 * D if wide else 8 * D
-    # executed work: quadratic forms the kernel evaluated (device counters), at their real cost
-    # (isotropic rows: D subtractions + D multiply-adds + scale, weight = 3D + 3 flops)
-    nq = (sc1["n_quad"] - sc0["n_quad"]) / cnt_sweeps / S if cnt_sweeps else 0.0  # per launch
-    nq_iso = (sc1["n_quad_iso"] - sc0["n_quad_iso"]) / cnt_sweeps / S if cnt_sweeps else 0.0
-    if wide:  # item-row contractions on the matrix cores (pruned rows skipped), at the MACs of the 16-row tiles
-        exec_flops = nq * 2 * sum(16 * (D - 16 * t) for t in range(D // 16)) if cnt_sweeps else None
-    else:
-        exec_flops = ((nq - nq_iso) * (D * D + 2 * D + 4) + nq_iso * (3 * D + 3)) if cnt_sweeps else None
-    traffic = traffic_src = None
-    if os.path.exists(args.traffic_json):
-        try:
-            tj = json.load(open(args.traffic_json))
-            traffic = tj.get("assign_bytes_per_launch")
-            traffic_src = f"{os.path.relpath(args.traffic_json, ROOT)} (rocprofv3 PMC pass, {tj.get('commit', 'commit n/a')})"
-        except Exception:
-            traffic = None
-
-    binding = binding_roof(exec_flops, float(n_items) * (xbytes + 8), ms_assign, peak,
-                           "np8_assign_wide" if wide else "np8_assign")
-
+    m = measure(smp, sweeps, args.steps, args.warmup, transport != "gloo", dist, torch, hi - lo, D, wide,
+                max(args.substeps, 1), args.traffic_json)
     if rank == 0:
         cpu = None
         if world == 1 and args.cpu_seconds > 0:
             cpu = cpu_baseline(X, z, mu, sig, D, args.seed, args.cpu_seconds, opts)
         out = {
             "metric": f"Gibbs sweeps/sec (Neal-8, N={N:.0e} D={D})".replace("+0", ""),
-            "value": args.steps / dt,
+            "value": args.steps / m["dt"],
             "unit": "sweeps/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": dt / args.steps * 1e3,
+            "ms_per_step": m["dt"] / args.steps * 1e3,
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
@@ -281,64 +214,163 @@ def main():
                             + {"frozen": "frozen cluster parameters",
                                "mh_g0": "mh_g0 cluster-parameter update (20 MH steps/cluster/sweep)",
                                "niw_conjugate": "niw_conjugate cluster-parameter update"}[args.param_update],
-                "N": N, "D": D, "K_final": Kfinal, "parallelism": f"data-sharded x{world}",
+                "N": N, "D": D, "K_final": m["K_final"], "parallelism": f"data-sharded x{world}",
                 "substeps": args.substeps,
                 "exchange": transport,
                 "param_update": args.param_update,
-                "params_ms_per_timed_sweep": ((st1["ms_params"] - st0["ms_params"])
-                                              / (st1["n_timed_params"] - st0["n_timed_params"]))
-                if st1["n_timed_params"] > st0["n_timed_params"] else None,
+                "params_ms_per_timed_sweep": m["params_ms"],
                 "sweep_graphs": os.environ.get("NP8_NO_GRAPH") is None,
             },
-            "roofline": {
-                **binding,
-                "traffic": traffic,
-                # the unpruned table form's flops over the launch time: an algorithmic-equivalent rate, not
-                # work the kernel performs (exact pruning skips almost every candidate row), so it can pass 1
-                "algorithmic_equivalent": {"achieved": achieved, "peak": peak, "unit": "TFLOP/s",
-                                           "frac": achieved / peak},
-                "assign_ms_per_launch": ms_assign,
-                # wide path: the matrix-core work of every row, as if none were pruned (the executed work
-                # is in "executed": item-row contractions counted on the device)
-                "mfma_unpruned_tflops": (mfma_flops / (ms_assign * 1e-3) / 1e12) if (wide and ms_assign > 0) else None,
-                "assign_launches_timed": n_launch,
-                "algorithmic_flops_per_launch": flops,
-                "traffic_source": traffic_src,
-                "executed": None if not cnt_sweeps else {
-                    "note": ("what np8_assign_wide executed: item-row contractions on the matrix cores after exact "
-                             "candidate pruning (device counters over 20 untimed sweeps), at the MACs of the 16-row "
-                             "tiles, over the timed launch time" if wide else
-                             "what np8_assign executed: quadratic forms after exact candidate pruning "
-                             "(device counters over 20 untimed sweeps after the timed ones), at their real "
-                             "cost, over the timed launch time; the M auxiliary G0 draws per item (Philox, "
-                             "Box-Muller, chi^2 logs) are not flops of this count"),
-                    "quad_forms_per_item": nq / max(n_items, 1),
-                    "aux_exact_per_item": (sc1["aux_exact_lanes"] - sc0["aux_exact_lanes"]) / cnt_sweeps / max(hi - lo, 1),
-                    "aux_exact_wave_frac": (sc1["aux_exact_waves"] - sc0["aux_exact_waves"]) / cnt_sweeps
-                    / max(((hi - lo + 63) // 64) * smp.M, 1),
-                    "aux_screen_violations": sc1["screen_violations"] - sc0["screen_violations"],
-                    "iso_fraction": nq_iso / max(nq, 1),
-                    "tflops": exec_flops / (ms_assign * 1e-3) / 1e12 if ms_assign > 0 else None,
-                    "frac_of_peak": exec_flops / (ms_assign * 1e-3) / 1e12 / peak if ms_assign > 0 else None,
-                },
-                "hbm_frac_algorithmic": (n_items * (xbytes + 8)) / (ms_assign * 1e-3) / 1e9 / HBM_PEAK_GBS
-                if ms_assign > 0 else None,
-            },
+            "roofline": m["roofline"],
             "cpu_baseline": cpu,
         }
         if world == 1 and not wide and args.cold_sweeps > 0:
-            out["cold_start"] = cold_start(args, X, D, opts, local_rank)
+            smp.close()
+            out["cold_start"] = cold_start(args, X, z, D, opts, local_rank, torch)
+        if world == 1 and not wide and args.c5_sub:
+            smp.close()
+            del X, z, mu, sig
+            out["c5"] = c5_record(args, local_rank, torch)
         print(json.dumps(out))
     if dist:
         dist.destroy_process_group()
 
 
-def cold_start(args, X, D, opts, device):
+def measure(smp, sweeps, steps, warmup, graphs, dist, torch, n_loc, D, wide, S, traffic_json):
+    """The timed region (barrier + synchronize on both sides, max over ranks) and the roofline of the
+    dominant kernel.  The assign launch time comes from a separate replay of one 20-sweep graph with every
+    assign bracketed by event nodes (NP8_TIMING_ALL_ASSIGNS; VERDICT r2: not a single sample); the timed
+    region itself carries one event pair per graph replay, reported beside it."""
+    # timing (event pairs around one assign launch per graph replay) is on from the start, so the timed
+    # region replays the graph warm-up captured; np8_prepare_sweeps captures and uploads the graph of the
+    # timed sweeps if the warm-up did not (warm-up < 20 sweeps)
+    smp.set_timing(True)
+    sweeps(warmup)  # includes np8_sync
+    if graphs:
+        smp.prepare_sweeps(steps)
+    torch.cuda.synchronize()
+    st0 = smp.stats()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    sweeps(steps, sync=False)
+    smp.sync()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if dist:
+        tt = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    st1 = smp.stats()
+    Kfinal = st1["K"]
+    n_in = st1["n_timed_assign"] - st0["n_timed_assign"]
+    ms_in = (st1["ms_assign"] - st0["ms_assign"]) / max(n_in, 1)
+    ms_assign, n_launch, src = ms_in, n_in, "timed region (one event pair per graph replay)"
+    if graphs:  # every assign of one 20-sweep replay (after the timed region, untimed for the headline)
+        smp.set_timing(True, all_assigns=True)
+        a0 = smp.stats()
+        sweeps(20)
+        a1 = smp.stats()
+        smp.set_timing(True)
+        if a1["n_timed_assign"] > a0["n_timed_assign"]:
+            n_launch = a1["n_timed_assign"] - a0["n_timed_assign"]
+            ms_assign = (a1["ms_assign"] - a0["ms_assign"]) / n_launch
+            src = "every assign launch of one 20-sweep graph replay after the timed region"
+    # executed-work counters over separate (untimed) sweeps: they add scalar loads and atomics per wave
+    cnt_sweeps = 20 if graphs else 0
+    if cnt_sweeps:
+        smp.set_timing(True, counters=True)
+        sc0 = smp.stats()
+        sweeps(cnt_sweeps)
+        sc1 = smp.stats()
+        smp.set_timing(True)
+    Kc = Kfinal + smp.M
+    # items of one assign launch: with S sub-steps a sweep makes S launches over ~N/S items each (ADVICE r2:
+    # per-launch bytes/flops, not per-sweep)
+    n_items = n_loc / S
+    # SURVEY.md 8(d): N (K+M) (D^2 + 2D + 4) for the fp64 table form (packed P: D(D+1)/2 multiply-adds
+    # plus d = x - mu and the weight).  Wide path: the triangular factor form y = A (x - mu), |y|^2:
+    # D subtractions + D(D+1)/2 multiply-adds + D squares-and-adds = D^2 + 4D per item and candidate
+    # (SURVEY.md's 2D^2 + 4D counts a full D x D contraction, which the kernel does not perform).
+    flops = float(n_items) * Kc * ((D * D + 4 * D) if wide else (D * D + 2 * D + 4))
+    # what the matrix cores execute on the wide path: 16-row tiles of the triangular A, 2 flops per MAC
+    mac_tiles = sum(16 * (D - 16 * t) for t in range(D // 16))
+    mfma_flops = float(n_items) * Kc * 2 * mac_tiles if wide else None
+    achieved = flops / (ms_assign * 1e-3) / 1e12 if ms_assign > 0 else 0.0
+    peak = FP32_MFMA_PEAK_TFLOPS if wide else FP64_PEAK_TFLOPS
+    xbytes = 4 * D if wide else 8 * D
+    # executed work: quadratic forms the kernel evaluated (device counters), at their real cost
+    # (isotropic rows: D subtractions + D multiply-adds + scale, weight = 3D + 3 flops)
+    nq = (sc1["n_quad"] - sc0["n_quad"]) / cnt_sweeps / S if cnt_sweeps else 0.0  # per launch
+    nq_iso = (sc1["n_quad_iso"] - sc0["n_quad_iso"]) / cnt_sweeps / S if cnt_sweeps else 0.0
+    if wide:  # item-row contractions on the matrix cores (pruned rows skipped), at the MACs of the 16-row tiles
+        exec_flops = nq * 2 * mac_tiles if cnt_sweeps else None
+    else:
+        exec_flops = ((nq - nq_iso) * (D * D + 2 * D + 4) + nq_iso * (3 * D + 3)) if cnt_sweeps else None
+    traffic = traffic_src = None
+    if traffic_json and os.path.exists(traffic_json):
+        try:
+            tj = json.load(open(traffic_json))
+            traffic = tj.get("assign_bytes_per_launch")
+            traffic_src = f"{os.path.relpath(traffic_json, ROOT)} (rocprofv3 PMC pass, {tj.get('commit', 'commit n/a')})"
+        except Exception:
+            traffic = None
+    abytes = float(n_items) * (xbytes + 8)
+    binding = binding_roof(exec_flops, abytes, ms_assign, peak, "np8_assign_wide" if wide else "np8_assign")
+    roof = {
+        **binding,
+        "traffic": traffic,
+        "traffic_over_algorithmic": (traffic / abytes) if traffic else None,
+        # the unpruned table form's flops over the launch time: an algorithmic-equivalent rate, not
+        # work the kernel performs (exact pruning skips almost every candidate row), so it can pass 1
+        "algorithmic_equivalent": {"achieved": achieved, "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak},
+        "assign_ms_per_launch": ms_assign,
+        "assign_ms_source": src,
+        "assign_launches_timed": n_launch,
+        "assign_ms_timed_region": ms_in,
+        "assign_launches_timed_region": n_in,
+        # wide path: the matrix-core work of every row, as if none were pruned
+        "mfma_unpruned_tflops": (mfma_flops / (ms_assign * 1e-3) / 1e12) if (wide and ms_assign > 0) else None,
+        "algorithmic_flops_per_launch": flops,
+        "traffic_source": traffic_src,
+        "executed": None if not cnt_sweeps else {
+            "note": ("what np8_assign_wide executed: item-row contractions on the matrix cores after exact "
+                     "candidate pruning (device counters over 20 untimed sweeps), at the MACs of the 16-row "
+                     "tiles, over the launch time" if wide else
+                     "what np8_assign executed: quadratic forms after exact candidate pruning "
+                     "(device counters over 20 untimed sweeps after the timed ones), at their real "
+                     "cost, over the launch time; the M auxiliary G0 draws per item (Philox, "
+                     "Box-Muller, chi^2 logs) are not flops of this count"),
+            "quad_forms_per_item": nq / max(n_items, 1),
+            "aux_exact_per_item": (sc1["aux_exact_lanes"] - sc0["aux_exact_lanes"]) / cnt_sweeps / max(n_loc, 1),
+            "aux_exact_wave_frac": (sc1["aux_exact_waves"] - sc0["aux_exact_waves"]) / cnt_sweeps
+            / max(((n_loc + 63) // 64) * smp.M, 1),
+            "aux_screen_violations": sc1["screen_violations"] - sc0["screen_violations"],
+            "iso_fraction": nq_iso / max(nq, 1),
+            "tflops": exec_flops / (ms_assign * 1e-3) / 1e12 if ms_assign > 0 else None,
+            "frac_of_peak": exec_flops / (ms_assign * 1e-3) / 1e12 / peak if ms_assign > 0 else None,
+        },
+        "hbm_frac_algorithmic": abytes / (ms_assign * 1e-3) / 1e9 / HBM_PEAK_GBS if ms_assign > 0 else None,
+    }
+    params_ms = ((st1["ms_params"] - st0["ms_params"]) / (st1["n_timed_params"] - st0["n_timed_params"])
+                 if st1["n_timed_params"] > st0["n_timed_params"] else None)
+    return {"dt": dt, "K_final": Kfinal, "roofline": roof, "params_ms": params_ms}
+
+
+def cold_start(args, X, labels, D, opts, device, torch):
     """The reference's flow from its initialisation (np_mcmc.cpp:49-92: K = 20 random G0 clusters, uniform
-    labels), the first sweeps of the chain: per sweep the time, K and the new-cluster requests accepted
-    and deferred.  Each sweep is synchronised (K is read back), so the rate includes one host round trip
-    per sweep."""
-    from noparama_amd import NealAlgorithm8
+    labels), on the same data:
+      * sweeps 0 .. cold_sweeps-1 one by one (K read back after each: one host round trip per sweep), with
+        the new-cluster requests accepted and deferred;
+      * "mixed": sweeps 50 .. 149 timed as the warm leg is (graph replay, no per-sweep sync), with the
+        assign kernel's roofline: the regime the reference's own start reaches (VERDICT r2 #6);
+      * "quality": at sweep 300, K and the purity / ARI of the max-likelihood and last labellings against
+        the generator's labels (noparama_amd.metrics = clustering_performance.cpp:38-82), for this sampler
+        and for the same chain in 16 synchronous sub-steps (VERDICT r2 #2)."""
+    from noparama_amd import NealAlgorithm8, metrics
 
     smp = NealAlgorithm8(D, seed=args.seed + 1, device=device, param_update=args.param_update, **opts)
     smp.set_data(X)
@@ -355,11 +387,67 @@ def cold_start(args, X, D, opts, device):
         dfr.append(s1["rejected_requests"] - s0["rejected_requests"])
         s0 = s1
     tot = sum(per) * 1e-3
+    out = {"sweeps": args.cold_sweeps, "value": args.cold_sweeps / tot, "unit": "sweeps/s",
+           "ms_per_sweep": [round(v, 3) for v in per], "K_per_sweep": Ks,
+           "new_clusters_per_sweep": acc, "deferred_requests_per_sweep": dfr,
+           "req_max": smp.req_max, "init": "init_random(20) (np_mcmc.cpp:49-92)"}
+    if args.cold_sweeps < 50:
+        smp.sweep(50 - args.cold_sweeps)
+    K50 = smp.K
+    m = measure(smp, lambda n, sync=True: smp.sweep(n, sync=sync), 100, 0, True, None, torch, X.shape[0], D,
+                False, 1, None)
+    out["mixed"] = {"sweeps": "50..149 (then 20 + 20 untimed for the launch times and counters)",
+                    "value": 100 / m["dt"], "unit": "sweeps/s", "ms_per_sweep": m["dt"] / 100 * 1e3,
+                    "K_at_50": K50, "K_final": m["K_final"], "roofline": m["roofline"]}
+    smp.sweep(300 - 190)
+    out["quality"] = {"sweeps": 300, "this_sampler": chain_quality(smp, labels),
+                      "substeps_16": None}
     smp.close()
-    return {"sweeps": args.cold_sweeps, "value": args.cold_sweeps / tot, "unit": "sweeps/s",
-            "ms_per_sweep": [round(v, 3) for v in per], "K_per_sweep": Ks,
-            "new_clusters_per_sweep": acc, "deferred_requests_per_sweep": dfr,
-            "req_max": smp.req_max, "init": "init_random(20) (np_mcmc.cpp:49-92)"}
+    s16 = NealAlgorithm8(D, seed=args.seed + 1, device=device, param_update=args.param_update, substeps=16,
+                         kcap=1024)
+    s16.set_data(X)
+    s16.init_random(20)
+    s16.sweep(300)
+    out["quality"]["substeps_16"] = chain_quality(s16, labels)
+    out["quality"]["note"] = ("S = 16 runs with kcap 1024 (the sub-step sort holds substeps x kcap <= 16384 bins); "
+                              "tolerance SURVEY.md 8(d): |d purity| <= 0.02, |d ARI| <= 0.05")
+    s16.close()
+    return out
+
+
+def chain_quality(smp, labels):
+    from noparama_amd import metrics
+
+    res = {}
+    for which, tag in ((1, "maxlik"), (0, "last")):
+        st = smp.state(which=which, params=False)
+        mm = metrics.similarity(labels, st["z"])
+        res[tag] = {"K": st["K"], "purity": mm["purity"], "rand_index": mm["rand_index"],
+                    "ari": mm["adjusted_rand_index"]}
+    return res
+
+
+def c5_record(args, device, torch):
+    """Config C5 (N = 1e6, D = 64, K = 256, NIW prior, fp32 MFMA contraction) timed inside the default run
+    (VERDICT r2 #7): frozen and niw_conjugate sweeps/s with the roofline of np8_assign_wide."""
+    import argparse as _ap
+
+    from noparama_amd import NealAlgorithm8
+
+    a = _ap.Namespace(**{**vars(args), "config": "C5", "d": 64, "k": 256, "substeps": 1})
+    X, z, mu, sig, opts = workload(a)
+    out = {"workload": "C5: N=1000000 D=64 K~256 M=3 mixture, warm state, NIW prior, fp32 items + fp32 MFMA "
+                       "contraction"}
+    for pu, steps in (("frozen", 40), ("niw_conjugate", 20)):
+        smp = NealAlgorithm8(64, seed=args.seed, device=device, param_update=pu, **opts)
+        smp.set_data(X)
+        smp.set_state(z, mu, sig)
+        m = measure(smp, lambda n, sync=True: smp.sweep(n, sync=sync), steps, 5, True, None, torch, X.shape[0],
+                    64, True, 1, os.path.join(ROOT, "profiles", C5_TRAFFIC) if pu == "frozen" else None)
+        out[pu] = {"value": steps / m["dt"], "unit": "sweeps/s", "steps": steps, "ms_per_step": m["dt"] / steps * 1e3,
+                   "K_final": m["K_final"], "params_ms_per_timed_sweep": m["params_ms"], "roofline": m["roofline"]}
+        smp.close()
+    return out
 
 
 def main_sm(args):

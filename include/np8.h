@@ -281,6 +281,8 @@ int np8_stats(np8_ctx *ctx, np8_stats_t *out);
  * Any non-zero value without the counter bit is the events alone. */
 #define NP8_TIMING_EVENTS 1
 #define NP8_TIMING_COUNTERS 2
+/* with NP8_TIMING_EVENTS: a replayed sweep graph times every assign launch (default: one per replay) */
+#define NP8_TIMING_ALL_ASSIGNS 4
 int np8_set_timing(np8_ctx *ctx, int32_t enable);
 /* Launch on this stream instead of the context's own (hipStream_t as void*). */
 int np8_set_stream(np8_ctx *ctx, void *stream);

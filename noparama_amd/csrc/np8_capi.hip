@@ -140,7 +140,7 @@ struct np8_ctx {
     ncclComm_t comm = nullptr;
     int rank = 0, world = 1;
     // timing: event pairs around launches; count_eval: the assign kernels' executed-work counters
-    bool timing = false, count_eval = false;
+    bool timing = false, count_eval = false, time_all = false;
     std::vector<Timer> timers;
     std::vector<hipEvent_t> event_pool;
     double ms[6] = {0, 0, 0, 0, 0, 0};  // assign, finalize, loglik, params, sm members, sm eval
@@ -1144,7 +1144,7 @@ int capture_graph(np8_ctx *c) {
         return NP8_OK;
     }
     c->capturing = true;
-    c->capture_timed_left = 1;
+    c->capture_timed_left = c->time_all ? (int)kGraphSweeps * c->substeps : 1;
     for (uint32_t i = 0; i < kGraphSweeps && !r; ++i) {
         r = population(c);
         if (!r) r = end_sweep(c);
@@ -1162,7 +1162,7 @@ int capture_graph(np8_ctx *c) {
         g = nullptr;
         c->graph_par = ch0 & 1;
         c->graph_phase = (int)(e0 % kGraphSweeps);
-        c->graph_timing = (c->timing ? 1 : 0) | (c->count_eval ? 2 : 0);
+        c->graph_timing = (c->timing ? 1 : 0) | (c->count_eval ? 2 : 0) | (c->time_all ? 4 : 0);
     } else {
         c->graph_timers.clear();
         c->graphs_off = true;
@@ -1176,7 +1176,7 @@ int capture_graph(np8_ctx *c) {
 // phase, check parity or timing setting).
 int ensure_graph(np8_ctx *c) {
     if (!c->graph || c->graph_par != (c->checks & 1) || c->graph_phase != (int)(c->epoch % kGraphSweeps) ||
-        c->graph_timing != ((c->timing ? 1 : 0) | (c->count_eval ? 2 : 0)))
+        c->graph_timing != ((c->timing ? 1 : 0) | (c->count_eval ? 2 : 0) | (c->time_all ? 4 : 0)))
         return capture_graph(c);
     return NP8_OK;
 }
@@ -2073,6 +2073,7 @@ int np8_set_timing(np8_ctx *c, int32_t enable) {
     if (!c) return NP8_ERR_ARG;
     c->timing = (enable & NP8_TIMING_EVENTS) != 0;
     c->count_eval = (enable & NP8_TIMING_COUNTERS) != 0;
+    c->time_all = c->timing && (enable & NP8_TIMING_ALL_ASSIGNS) != 0;
     return NP8_OK;
 }
 

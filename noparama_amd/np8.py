@@ -358,9 +358,10 @@ class NealAlgorithm8:
         self._check(lib().np8_total_loglik(self._h, C.byref(v)))
         return v.value
 
-    def set_timing(self, on=True, counters=False):
-        """on: device-event timing; counters: the assign kernel's executed-work counters (n_quad)."""
-        self._check(lib().np8_set_timing(self._h, (1 if on else 0) | (2 if counters else 0)))
+    def set_timing(self, on=True, counters=False, all_assigns=False):
+        """on: device-event timing; counters: the assign kernel's executed-work counters (n_quad);
+        all_assigns: a replayed sweep graph times every assign launch (default: one per replay)."""
+        self._check(lib().np8_set_timing(self._h, (1 if on else 0) | (2 if counters else 0) | (4 if all_assigns else 0)))
 
     # -- multi-rank ----------------------------------------------------------------------------
     def comm_init(self, uid, rank, world):

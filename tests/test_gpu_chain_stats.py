@@ -102,3 +102,37 @@ def test_one_step_sweep_deviation_is_recorded():
     print(f"one-step sweep: maxlik K {K:.2f} vs {g['K'].mean():.2f}, ARI {ari:.4f} vs {np.nanmean(g['ari']):.4f}")
     assert np.mean([r["maxlik"]["purity"] for r in runs]) > 0.99
     assert K > g["K"].mean()  # the documented direction of the deviation
+
+
+def scale_run(X, lab, seed, S, T=300):
+    from noparama_amd import NealAlgorithm8, metrics
+
+    s = NealAlgorithm8(X.shape[1], seed=seed, device=0, substeps=S, kcap=1024)
+    try:
+        s.set_data(X)
+        s.init_random(20)
+        s.sweep(T)
+        st = s.state(which=1, params=False)
+        m = metrics.similarity(lab, st["z"])
+        return m["purity"], m["adjusted_rand_index"], st["K"]
+    finally:
+        s.close()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("N,seeds", [(100_000, 4), (1_000_000, 2)])
+def test_one_step_sweep_matches_substeps_at_north_star_scale(N, seeds):
+    """the benchmarked sampler (one synchronous step per sweep, S = 1) against S = 16 on the C3
+    generator's data (64 components, D = 8) from the reference's initialisation (init_random(20),
+    np_mcmc.cpp:49-92), 300 sweeps: the max-likelihood labelling's purity and ARI against the generator's
+    labels within SURVEY.md 8(d)'s tolerances (|d mean purity| <= 0.02, |d mean ARI| <= 0.05).  Unlike
+    twogaussians (N = 200, where S = 1 over-splits), at this scale the synchronous step scores like the
+    sub-stepped one (tools/chain_quality.py: N = 1e6, 3 seeds: ARI 0.912 for S = 1, 0.911 for S = 8)."""
+    X, lab = datasets.config_c3(N=N)[:2]
+    res = {S: np.array([scale_run(X, lab, 500 + r, S) for r in range(seeds)]) for S in (1, 16)}
+    m1, m16 = res[1].mean(axis=0), res[16].mean(axis=0)
+    print(f"N={N}: S=1 purity {m1[0]:.4f} ARI {m1[1]:.4f} K {m1[2]:.1f}; "
+          f"S=16 purity {m16[0]:.4f} ARI {m16[1]:.4f} K {m16[2]:.1f}")
+    assert abs(m1[0] - m16[0]) <= 0.02
+    assert abs(m1[1] - m16[1]) <= 0.05
+    assert m1[0] > 0.95 and m1[1] > 0.8  # and both find the components

@@ -43,7 +43,8 @@ def test_screen_has_no_violations_near_v_zero(D, nu):
             assert sg["K"] == so["K"] and np.array_equal(sg["z"], so["z"])
         s1 = g.stats()
         assert s1["screen_violations"] - s0["screen_violations"] == 0
-        assert s1["new_clusters"] > 0  # auxiliaries were picked: the screened region mattered
+        if D <= 3:
+            assert s1["new_clusters"] > 0  # auxiliaries were picked: the screened region mattered
         # the regime is populated: a few percent of G0 draws have |v| < 1/4 (P(|D + nu g| < 1/4))
         from math import erf, sqrt
         p = 0.5 * (erf((0.25 - D) / nu / sqrt(2)) - erf((-0.25 - D) / nu / sqrt(2)))

@@ -20,7 +20,8 @@ from noparama_amd import NealAlgorithm8, datasets, metrics  # noqa: E402
 
 
 def run(X, lab, seed, S, T, every=10, alpha=1.0):
-    s = NealAlgorithm8(X.shape[1], seed=seed, device=0, substeps=S, alpha=alpha)
+    # the sort of the sub-step layout holds substeps * kcap <= 16384 bins (np8_create)
+    s = NealAlgorithm8(X.shape[1], seed=seed, device=0, substeps=S, alpha=alpha, kcap=min(2048, 16384 // S))
     try:
         s.set_data(X)
         s.init_random(20)
@@ -60,8 +61,8 @@ def main():
         res.setdefault("summary", {})[f"S={S}"] = summ
         print(f"N={a.n} S={S}: {json.dumps(summ)} "
               f"{np.mean([r['sweeps_per_s'] for r in rows]):.0f} sweeps/s", flush=True)
-    if a.out:
-        json.dump(res, open(a.out, "w"), indent=1)
+        if a.out:
+            json.dump(res, open(a.out, "w"), indent=1)
 
 
 if __name__ == "__main__":
