@@ -78,6 +78,12 @@ struct np8_ctx {
     bool gath_clear = false;   // the last prune zeroed the gathered radius buffer for this sweep
     int64_t assign_waves = 0;  // waves of the last assign launch (its radius records)
     double *plr2 = nullptr;    // per dense row: the squared radius its candidate list assumes
+    // two-kernel assign (np8_assign_fast, then np8_assign over the lanes it deferred): reference prior with a
+    // diagonal base-measure whitening; NP8_NO_FAST=1 switches it off (A/B runs)
+    int32_t *queue = nullptr;  // [64 * waves] deferred positions, by fast-kernel wave
+    int32_t *qcount = nullptr; // [waves] deferred lanes per wave
+    int32_t *qlist = nullptr;  // [waves] the waves that deferred lanes (ctl->qwaves)
+    bool diag_U = false, fast_off = false;
     // data-parallel sweep in `substeps` synchronous sub-steps (np8_config.substeps): sub-step s is the
     // contiguous range [sub_start[s], sub_start[s+1]) of the label-sorted layout (sorted by sub-step, slot)
     int substeps = 1;
@@ -423,7 +429,7 @@ void free_device(np8_ctx *c) {
                     c->sm_hist, c->sm_mem, c->sm_off, c->sm_live, c->sm_Xm, c->sm_ownm, c->sm_cross, c->sm_ctl,
                     c->sm_typ, c->sm_slist, c->sm_stheta, c->stage, c->evalc, c->z_base, c->cnt_base,
                     c->chg_slot, c->mu_base, c->sigma_base, c->chg_item, c->chg_count, c->chg_flags,
-                    c->inv_hist, c->inv_out};
+                    c->inv_hist, c->inv_out, c->queue, c->qcount, c->qlist};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     if (c->sm_first_host) (void)hipHostFree(c->sm_first_host);
@@ -753,6 +759,7 @@ AssignArgs assign_args(np8_ctx *c, int64_t p0, int64_t p1, const int64_t *order,
     A.wmu = c->wmu;
     A.lam_lo = c->lam_lo;
     A.wdist = nullptr;  // set by launch_assign on the wide path (after np8_wide_dist)
+    A.queue = A.queue_out = A.qcount = A.qlist = nullptr;
     return A;
 }
 
@@ -795,10 +802,20 @@ int launch_assign(np8_ctx *c, int64_t p0, int64_t p1, const int64_t *order, bool
             HIPC(c, np8_launch_wide_dist(wide_args(c), c->stream));
             A.wdist = c->wdist;
         }
-        HIPC(c, np8_launch_assign_wide(A, c->D, c->M, c->prior, c->stream));
+        HIPC(c, np8_launch_assign_wide(A, c->D, c->M, c->prior, c->diag_U, c->stream));
     }
-    else
+    else if (c->diag_U && !c->fast_off && c->prior == NP8_PRIOR_REFERENCE && A.sorted && !order && !use_perm) {
+        // the lean kernel for every lane, then the full one over the lanes it deferred (ctl->qn)
+        A.queue_out = c->queue;
+        A.qcount = c->qcount;
+        A.qlist = c->qlist;
+        HIPC(c, np8_launch_assign_fast(A, c->D, c->M, c->stream));
+        A.queue = c->queue;
+        A.queue_out = nullptr;
+        HIPC(c, np8_launch_assign_queue(A, c->D, c->M, c->stream));  // a small grid walking ctl->qwaves
+    } else {
         HIPC(c, np8_launch_assign(A, c->D, c->M, c->prior, c->stream));
+    }
     timer_end(c, t);
     return NP8_OK;
 }
@@ -1292,6 +1309,7 @@ int np8_create(np8_ctx **out, const np8_config *cfg) {
     c->graphs_off = std::getenv("NP8_NO_GRAPH") != nullptr;  // A/B switch for launch-by-launch sweeps
     c->prune_on = !c->wide && c->kcap <= kPruneMaxKcap && std::getenv("NP8_NO_PRUNE") == nullptr;
     c->wide_prune_off = std::getenv("NP8_NO_PRUNE") != nullptr;
+    c->fast_off = std::getenv("NP8_NO_FAST") != nullptr;
     c->rec_cap = c->req_max;  // grown to the item count by np8_set_data (one rank)
     c->rec_bytes = record_bytes(c->kcap, (int)c->rec_cap, c->D);
     int r = 0;
@@ -1314,8 +1332,12 @@ int np8_create(np8_ctx **out, const np8_config *cfg) {
     // hyp: mu0 | UinvT packed | caux | rsk | logam | nu | LT packed | NIW sum-log bound
     std::vector<double> hyp;
     hyp.insert(hyp.end(), c->mu0.begin(), c->mu0.end());
+    c->diag_U = true;
     for (int a = 0; a < D; ++a)
-        for (int b = a; b < D; ++b) hyp.push_back(c->UinvT[a * D + b]);
+        for (int b = a; b < D; ++b) {
+            hyp.push_back(c->UinvT[a * D + b]);
+            if (b != a && c->UinvT[a * D + b] != 0.0) c->diag_U = false;
+        }
     hyp.push_back(c->caux);
     hyp.push_back(c->rsk);
     hyp.push_back(c->logam);
@@ -1409,7 +1431,10 @@ int np8_set_data(np8_ctx *c, const double *X, int64_t n, int32_t D, int64_t offs
     int r = 0;
     const size_t nx = c->wide ? ((size_t)n * D + 1) / 2 : (size_t)n * D;  // wide path: fp32 items
     if ((r = dalloc(c, &c->X, nx)) || (r = dalloc(c, &c->z, (size_t)n)) ||
-        (r = dalloc(c, &c->z_best, (size_t)n)) || (r = dalloc(c, &c->wr2, (size_t)((n + 63) / 64))))
+        (r = dalloc(c, &c->z_best, (size_t)n)) || (r = dalloc(c, &c->wr2, (size_t)((n + 63) / 64))) ||
+        (r = dalloc(c, &c->queue, (size_t)(64 * ((n + 63) / 64) + 64))) ||
+        (r = dalloc(c, &c->qcount, (size_t)((n + 63) / 64 + 1))) ||
+        (r = dalloc(c, &c->qlist, (size_t)((n + 63) / 64 + 1))))
         return r;
     for (int b = 0; b < 2; ++b)
         if ((r = dalloc(c, &c->Xs[b], nx)) || (r = dalloc(c, &c->zs[b], (size_t)n)) ||

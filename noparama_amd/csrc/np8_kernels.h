@@ -35,6 +35,8 @@ struct Ctl {
                                        // not have skipped (the auxiliary screen's self-check; must stay 0)
     unsigned long long n_aux_exact[2]; // count_eval runs: (lane, auxiliary) pairs the screen did not skip,
                                        // and (wave, auxiliary) pairs in which at least one lane was not skipped
+    uint32_t qwaves;                   // np8_assign_fast waves with deferred lanes this step (AssignArgs::qlist)
+    uint32_t pad3;
 };
 
 // Executed work of np8_assign when AssignArgs::count_eval is set (timing mode): per wave, the cluster
@@ -130,6 +132,14 @@ struct AssignArgs {
     const float *wmu;          // natural fp32 means [kcap][D]
     const double *lam_lo;      // [kcap] precision eigenvalue lower bounds (np8_wide_rows)
     const double *wdist;       // [K][kcap] distances between row means (np8_wide_dist); null: no pruning
+    // two-kernel step (np8_assign_fast + np8_assign): positions the fast kernel deferred; non-null makes
+    // np8_assign run over them instead of [p0, p1)
+    // (one wave per workgroup: fast-kernel wave w writes its deferred positions to queue[64 w ..] and their
+    // number to qcount[w]; queue mode runs block w over them)
+    int32_t *queue;
+    int32_t *queue_out;        // np8_assign_fast: where deferred positions go
+    int32_t *qcount;           // [waves of the step]
+    int32_t *qlist;            // waves with deferred lanes (ctl->qwaves of them, cleared by np8_finalize)
 };
 
 // Wide-path tables (np8_wide.hip), maintained for the slots flagged in dirty.
@@ -350,7 +360,7 @@ struct SortArgs {
 
 bool np8_supported(int D, int M);
 bool np8_wide_supported(int D, int M);
-hipError_t np8_launch_assign_wide(const np8::AssignArgs &A, int D, int M, int prior, hipStream_t s);
+hipError_t np8_launch_assign_wide(const np8::AssignArgs &A, int D, int M, int prior, bool diag_u, hipStream_t s);
 // Wide-path pruning: the distance table of the current dense rows (after every table change).
 hipError_t np8_launch_wide_dist(const np8::WideArgs &W, hipStream_t s);
 hipError_t np8_launch_loglik_matrix_wide(const np8::AssignArgs &A, const np8::WideArgs &W, int D, int M, int prior,
@@ -364,6 +374,10 @@ hipError_t np8_launch_niw_post(const np8::NiwArgs &A, int nblocks, hipStream_t s
 hipError_t np8_launch_niw_aux_slots(const np8::NiwArgs &A, hipStream_t s);
 hipError_t np8_launch_resort(const SortArgs &S, hipStream_t s);
 hipError_t np8_launch_assign(const np8::AssignArgs &A, int D, int M, int prior, hipStream_t s);
+// np8_assign_fast (reference prior, isotropic Lambda, label-sorted layout): defers lanes into A.queue_out / ctl->qn
+hipError_t np8_launch_assign_fast(const np8::AssignArgs &A, int D, int M, hipStream_t s);
+// np8_assign_queue: the lanes np8_assign_fast deferred (A.queue, A.qcount, A.qlist, ctl->qwaves)
+hipError_t np8_launch_assign_queue(const np8::AssignArgs &A, int D, int M, hipStream_t s);
 // Pruning radii: the step's per-wave records (AssignArgs::wr2) into the gathered radii (r2 + kcap).
 hipError_t np8_launch_fold_r2(const np8::WaveR2 *wr2, int64_t n, double *r2, int kcap, hipStream_t s);
 // Debug invariants (np8_config / NP8_DEBUG_INVARIANTS): every label a live slot, the live slots' counts the

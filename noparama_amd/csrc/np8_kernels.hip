@@ -249,12 +249,13 @@ template <int D, int M, int PRIOR, bool COUNT>
 #ifndef NP8_ASSIGN_BLOCK
 #define NP8_ASSIGN_BLOCK 64  // one wave per workgroup (256: 2% slower at C3)
 #endif
-__global__ __launch_bounds__(NP8_ASSIGN_BLOCK) __attribute__((amdgpu_waves_per_eu(NP8_ASSIGN_WAVES))) void np8_assign(AssignArgs A) {
+#ifndef NP8_FAST_WAVES
+#define NP8_FAST_WAVES 4  // 109 VGPRs, no spills (5: 96 with spills, 2-6% slower at C3)
+#endif
+__device__ __forceinline__ void assign_item(const AssignArgs &A, const int64_t p, const int64_t qslot) {
     constexpr int DP = D * (D + 1) / 2;
     constexpr int CS = (D + DP + 5 + 1) & ~1;
     constexpr int F = D + DP;
-    const int64_t p = A.p0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= A.p1) return;
     const bool sorted = A.sorted != 0;  // label-sorted layout: X and zs indexed by position
     // (ternaries, not A.zs[cur]: a runtime index into the argument struct would move it to scratch)
     const int cur = sorted ? A.ctl->cur : 0;
@@ -489,14 +490,15 @@ __global__ __launch_bounds__(NP8_ASSIGN_BLOCK) __attribute__((amdgpu_waves_per_e
             d2 = fma(dd, dd, d2);
         }
         const int32_t t0 = __builtin_amdgcn_readfirstlane(ts);
-        const bool one = __ballot(1) == ~0ull && __ballot(ts != t0) == 0;  // full wave, one slot
+        // full wave, one slot (queue mode: the wave's record belongs to np8_assign_fast, lanes go one by one)
+        const bool one = !A.queue && __ballot(1) == ~0ull && __ballot(ts != t0) == 0;
         if (one) {
 #pragma unroll
             for (int o = 32; o > 0; o >>= 1) d2 = fmax(d2, __shfl_xor(d2, o));
         } else {
             atomicMax(reinterpret_cast<unsigned long long *>(A.r2 + A.kcap + ts), (unsigned long long)__double_as_longlong(d2));
         }
-        if ((threadIdx.x & 63) == (__ffsll((unsigned long long)__ballot(1)) - 1)) {  // the wave's record
+        if (!A.queue && (threadIdx.x & 63) == (__ffsll((unsigned long long)__ballot(1)) - 1)) {  // the wave's record
             WaveR2 w;
             w.d2 = one ? d2 : 0.0;
             w.slot = one ? t0 : -1;
@@ -518,8 +520,9 @@ __global__ __launch_bounds__(NP8_ASSIGN_BLOCK) __attribute__((amdgpu_waves_per_e
             atomicAdd(delta + s, 1);
             // the item's addresses again (a rare path): two 64-bit addresses kept live through the draw were
             // spilled to scratch for every item (19 of the 38 MB the C3 launch wrote)
-            int64_t pq = A.p0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+            int64_t pq = A.queue ? qslot : (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
             asm volatile("" : "+v"(pq));
+            pq = A.queue ? (int64_t)A.queue[pq] : A.p0 + pq;
             const int64_t lq = sorted ? (int64_t)__atomic_load_n(ids + pq, __ATOMIC_RELAXED) : position_to_local(A, pq);
             A.z[key_item(lq)] = s;
             if (sorted) zs[pq] = s;
@@ -547,6 +550,263 @@ __global__ __launch_bounds__(NP8_ASSIGN_BLOCK) __attribute__((amdgpu_waves_per_e
             }
         }
     }
+}
+
+// One lane per item of [p0, p1).
+template <int D, int M, int PRIOR, bool COUNT>
+__global__ __launch_bounds__(NP8_ASSIGN_BLOCK) __attribute__((amdgpu_waves_per_eu(NP8_ASSIGN_WAVES))) void np8_assign(AssignArgs A) {
+    const int64_t p = A.p0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p < A.p1) assign_item<D, M, PRIOR, COUNT>(A, p, -1);
+}
+
+// The lanes np8_assign_fast deferred: fast-kernel wave qlist[k] left qcount of them at queue[64 wave ..]; the
+// grid walks the listed waves (the deferred lanes of one fast wave share its rows).  Rarely has work, so it
+// takes the registers it wants (no spills) at fewer waves per SIMD.
+template <int D, int M, int PRIOR, bool COUNT>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void np8_assign_queue(AssignArgs A) {
+    static_assert(NP8_ASSIGN_BLOCK == 64, "np8_assign_fast's waves are its workgroups");
+    const int lane = threadIdx.x & 63;
+    const int nw = (int)A.ctl->qwaves;
+    for (int k = blockIdx.x; k < nw; k += gridDim.x) {
+        const int64_t wv = A.qlist[k];
+        const int cnt = A.qcount[wv];
+        if (lane < cnt) assign_item<D, M, PRIOR, COUNT>(A, (int64_t)A.queue[wv * 64 + lane], wv * 64 + lane);
+    }
+}
+
+// ---- experiment: per-wave phase timestamps of np8_assign_fast (built only with NP8_EXP_CLOCKS) -------
+#ifdef NP8_EXP_CLOCKS
+constexpr int64_t kClkWaves = 1 << 16;
+__device__ unsigned long long g_np8_clk[kClkWaves * 8];
+// every load issued so far has landed, then the 100 MHz real-time clock (10 ns)
+#define NP8_CLK(k)                                                                                     \
+    do {                                                                                               \
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");                                    \
+        const int64_t w_ = (p - A.p0) >> 6;                                                            \
+        if (!COUNT && (threadIdx.x & 63) == 0 && w_ < kClkWaves)                                       \
+            g_np8_clk[w_ * 8 + (k)] = __builtin_amdgcn_s_memrealtime();                                \
+    } while (0)
+extern "C" int np8_exp_clocks(unsigned long long *out, int64_t n) {
+    if (n > kClkWaves * 8) n = kClkWaves * 8;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_np8_clk), sizeof(unsigned long long) * n, 0, hipMemcpyDeviceToHost) ==
+                   hipSuccess ? 0 : -1;
+}
+#else
+#define NP8_CLK(k)
+#endif
+
+// ---- the data-parallel sweep's fast path -------------------------------------------------------------
+// np8_assign_fast<D,M>: the common case of np8_assign -- the reference prior with an isotropic Lambda (every
+// G0 draw, and so every row, isotropic; the base measure's whitening diagonal), the label-sorted layout --
+// with only the work almost every lane needs: the own row, the candidate list (or the table), the two
+// levels of the auxiliary screen, the move.  A lane the screen cannot clear (an auxiliary may come within
+// kSkip of the running maximum: 0.3% of (item, auxiliary) pairs at C3), or a wave meeting a row that is not
+// isotropic, is deferred: its position goes to a queue that np8_assign then runs in queue mode, from the
+// start, with the full code (exact auxiliary draws, new-cluster requests).  A deferred lane writes nothing
+// here, so every item's result is np8_assign's, bit for bit.  The lean kernel keeps its registers low
+// (no exact fp64 draws, no request payload): more waves per SIMD to hide the loads' latency.
+template <int D, int M, int PRIOR, bool COUNT>
+__global__ __launch_bounds__(NP8_ASSIGN_BLOCK) __attribute__((amdgpu_waves_per_eu(NP8_FAST_WAVES))) void np8_assign_fast(AssignArgs A) {
+    using H = HypView<D>;
+    constexpr int DP = D * (D + 1) / 2;
+    constexpr int CS = (D + DP + 5 + 1) & ~1;
+    constexpr int F = D + DP;
+    const int64_t p = A.p0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= A.p1) return;
+    NP8_CLK(0);
+    const int lane = threadIdx.x & 63;
+    const int cur = A.ctl->cur;
+    int32_t *__restrict__ zs = cur ? A.zs[1] : A.zs[0];
+    const int32_t *__restrict__ ids = cur ? A.ids[1] : A.ids[0];
+    const double *__restrict__ X = cur ? A.Xs[1] : A.Xs[0];
+    const double *__restrict__ cand = A.cand;
+    const double *__restrict__ hyp = A.hyp;
+    const int32_t zi = zs[p];
+    const int32_t il = ids[p];
+    const uint64_t ig = (uint64_t)(A.offset + il);
+    const uint32_t t = A.ctl->t_base + A.t;
+    double x[D];
+#pragma unroll
+    for (int a = 0; a < D; ++a) x[a] = X[(int64_t)a * A.n_loc + p];
+    const int K = A.ctl->K;
+    NP8_CLK(1);
+    const int32_t zf = __builtin_amdgcn_readfirstlane(zi);
+    const int32_t jo = (__ballot(zi != zf) == 0ull) ? A.dense_of[zf] : A.dense_of[zi];
+
+    bool defer = COUNT;  // counting runs: every lane takes np8_assign's counting instance
+    PickState st;
+    st.S = 1.0;
+    st.u = -1.0;
+    st.pick = jo;
+    st.T = 0.0;
+    double d2own = 0.0;  // |x - mu_own|^2: the own row's quadratic form and the list's radius check
+    int32_t pslot = zi;
+    if (!COUNT) {
+        uint64_t pend = __ballot(1);
+        while (pend) {  // one pass per distinct own row of the wave (one in the label-sorted layout)
+            const int32_t j = __builtin_amdgcn_readlane(jo, __ffsll((unsigned long long)pend) - 1);
+            const double *eo = cand + (int64_t)j * CS;
+            const double iso = eo[F + kFieldIso];
+            if (jo == j) {
+                if (iso > 0.0) {  // cand_ll's isotropic form, operation for operation
+                    double s2 = (x[0] - eo[0]) * (x[0] - eo[0]);
+#pragma unroll
+                    for (int a = 1; a < D; ++a) s2 = fma(x[a] - eo[a], x[a] - eo[a], s2);
+                    d2own = s2;
+                    st.T = fma(-0.5, s2 * iso, eo[F + kFieldC]) + eo[F + kFieldLogn1];
+                } else {
+                    defer = true;
+                }
+            }
+            pend &= ~__ballot(jo == j);
+        }
+    }
+    NP8_CLK(2);
+    const double zslot = (double)zi;
+    int ngroups = 0;
+    for (uint64_t pend = __ballot(1); pend && ngroups <= kMaxListGroups; ++ngroups)
+        pend &= ~__ballot(jo == __builtin_amdgcn_readlane(jo, __ffsll((unsigned long long)pend) - 1));
+    bool full = !defer;  // this lane walks the whole table
+    // one candidate row (wave-uniform): the isotropic likelihood, or the wave's lanes deferred
+    auto visit = [&](int j, bool own_skip) {
+        const double *e = cand + (int64_t)j * CS;
+        const double iso = e[F + kFieldIso];
+        if (!(iso > 0.0)) {
+            defer = true;
+            return;
+        }
+        double s2 = (x[0] - e[0]) * (x[0] - e[0]);
+#pragma unroll
+        for (int a = 1; a < D; ++a) s2 = fma(x[a] - e[a], x[a] - e[a], s2);
+        const double lw = fma(-0.5, s2 * iso, e[F + kFieldC]) + e[F + kFieldLogn];
+        if (own_skip && e[F + kFieldSlot] == zslot) return;
+        ensure_u(st, lw, A.seed, ig, t);
+        pick_step(st, lw, j);
+        pslot = (st.pick == j) ? (int32_t)e[F + kFieldSlot] : pslot;
+    };
+    if (!defer && A.use_lists && A.ctl->lists_ok && ngroups <= kMaxListGroups) {
+        uint64_t pend = __ballot(1);
+        while (pend) {
+            const int32_t j0 = __builtin_amdgcn_readlane(jo, __ffsll((unsigned long long)pend) - 1);
+            pend &= ~__ballot(jo == j0);
+            if (jo == j0 && !defer) {
+                full = !(d2own <= A.plr2[j0]);
+                if (!full) {
+                    const int32_t nl = A.plen[j0];
+                    const int32_t *__restrict__ lst = A.plist + (int64_t)j0 * A.ls;
+                    for (int q = 0; q < nl && !defer; ++q) visit(lst[q], false);
+                }
+            }
+        }
+    }
+    if (__ballot(full && !defer)) {  // wave-uniform row loop over the lanes that need it
+        for (int j = 0; j < K; ++j)
+            if (full && !defer) visit(j, true);
+    }
+    NP8_CLK(3);
+    // the auxiliaries: np8_assign's two-level screen, then the exact fp64 draw for the lanes it cannot clear;
+    // a lane that picks an auxiliary (a new-cluster request) is deferred
+    if (!defer) {
+        double ny;
+        {
+            const double *U = hyp + H::kUinvT;  // diagonal (launch condition): whiten() + norm_of() with zeros left out
+            double n2 = 0.0;
+#pragma unroll
+            for (int a = 0; a < D; ++a) {
+                const double y = U[a * D - (a * (a - 1)) / 2] * (x[a] - hyp[H::kMu0 + a]);
+                n2 = fma(y, y, n2);
+            }
+            ny = sqrt(n2);
+        }
+        const double logam = hyp[H::kLogam];
+        const float thr = (float)(st.T - kSkip - logam);  // T only grows: conservative for every m
+        const float nyf = (float)ny, nuf = (float)hyp[H::kNu], rskf = (float)hyp[H::kRsk], cauxf = (float)hyp[H::kCaux];
+        constexpr int Qa = (1 + ((((D - 1) & 1) || (D - 1) / 2 > 2) ? 1 : 0) + ((D - 1) / 2 > 4 ? ((D - 1) / 2 - 1) / 4 : 0));
+        constexpr bool has_call1 = Qa > 1;
+        uint32_t need = 0u;
+#pragma unroll 1
+        for (int m = 0; m < M; ++m) {
+            uint32_t w[4];
+            philox_call(A.seed, ig, t, kStreamAux, (uint32_t)(m * Qa), w);
+            if (!(aux_screen_ub<D>(w, 0.0f, 0.0f, nyf, nuf, rskf, cauxf, thr) <= thr)) need |= 1u << m;
+        }
+        NP8_CLK(4);
+#pragma unroll 1
+        for (int m = 0; m < M; ++m) {
+            bool skip = ((need >> m) & 1u) == 0u;
+            if (__ballot(!skip) == 0ull) continue;  // wave-uniform: the common case
+            uint32_t w0[4], w1[4] = {0u, 0u, 0u, 0u};
+            philox_call(A.seed, ig, t, kStreamAux, (uint32_t)(m * Qa), w0);
+            const bool l2 = has_call1 && !skip;
+            if (l2) {  // level 2: the chi^2 terms of call 1
+                philox_call(A.seed, ig, t, kStreamAux, (uint32_t)(m * Qa + 1), w1);
+                float e1;
+                const float c1 = aux_screen_chi1<D>(w1, e1);
+                skip = aux_screen_ub<D>(w0, c1, e1, nyf, nuf, rskf, cauxf, thr) <= thr;
+            }
+            if (!skip) {
+                double v, xpar, chi2;
+                aux_core_w<D>(A.seed, ig, t, m, hyp[H::kNu], v, xpar, chi2, w0, l2, w1);
+                const double lw = aux_loglik(ny, v, xpar, chi2, D, hyp[H::kRsk], hyp[H::kCaux]) + logam;
+                ensure_u(st, lw, A.seed, ig, t);
+                pick_step(st, lw, K + m);
+            }
+        }
+        defer = st.pick >= K;  // a new-cluster request: np8_assign builds its payload
+    }
+    NP8_CLK(5);
+    // deferred lanes: positions into this wave's slots of the queue (compacted, no atomics), their count
+    // for np8_assign's queue mode; nothing else is written for them
+    const uint64_t db = __ballot(defer);
+    if (db) {  // rare (requests, rows that are not isotropic): the wave lists itself for np8_assign's queue mode
+        const int64_t wv = (p - A.p0) >> 6;
+        if (defer) A.queue_out[wv * 64 + __popcll(db & ((1ull << lane) - 1ull))] = (int32_t)p;
+        if (lane == (__ffsll((unsigned long long)db) - 1)) {
+            A.qcount[wv] = __popcll(db);
+            A.qlist[atomicAdd(&A.ctl->qwaves, 1u)] = (int32_t)wv;
+        }
+    }
+    const int32_t snew = pslot;  // a lane that is not deferred picked an existing row
+    if (A.collect_r2) {  // np8_assign's radius collection, over the lanes not deferred
+        const int32_t tr = defer ? jo : st.pick;
+        const double *e = cand + (int64_t)tr * CS;
+        double d2 = 0.0;
+#pragma unroll
+        for (int a = 0; a < D; ++a) {
+            const double dd = x[a] - e[a];
+            d2 = fma(dd, dd, d2);
+        }
+        // the lanes not deferred share one slot (the label-sorted layout): one record for the wave; deferred
+        // lanes add theirs in np8_assign's queue mode
+        const uint64_t kept = __ballot(!defer);
+        const int32_t t0 = __shfl(snew, kept ? __ffsll((unsigned long long)kept) - 1 : 0);
+        const bool one = kept != 0ull && __ballot(!defer && snew != t0) == 0;
+        if (one) {
+            d2 = defer ? 0.0 : d2;
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) d2 = fmax(d2, __shfl_xor(d2, o));
+        } else if (!defer) {
+            atomicMax(reinterpret_cast<unsigned long long *>(A.r2 + A.kcap + snew), (unsigned long long)__double_as_longlong(d2));
+        }
+        if (lane == (__ffsll((unsigned long long)__ballot(1)) - 1)) {  // the wave's record
+            WaveR2 wr;
+            wr.d2 = one ? d2 : 0.0;
+            wr.slot = one ? t0 : -1;
+            wr.pad = 0;
+            A.wr2[(p - A.p0) >> 6] = wr;
+        }
+    }
+    const uint64_t mv = __ballot(!defer && snew != zi);
+    if (mv && lane == (__ffsll((unsigned long long)__ballot(1)) - 1))
+        atomicAdd(reinterpret_cast<unsigned long long *>(&A.ctl->moved), (unsigned long long)__popcll(mv));
+    if (!defer && snew != zi) {
+        int32_t *delta = reinterpret_cast<int32_t *>(A.rec + kRecHeaderBytes);
+        atomicSub(delta + zi, 1);
+        atomicAdd(delta + snew, 1);
+        A.z[il] = snew;
+        zs[p] = snew;
+    }
+    NP8_CLK(6);
 }
 
 // ---- label-sorted layout ------------------------------------------------------------------------------
@@ -1069,6 +1329,7 @@ __global__ __launch_bounds__(kFinThreads) void np8_finalize(FinArgs F) {
     }
     if (tid == 0) {
         F.ctl->K = nlive;
+        F.ctl->qwaves = 0;  // np8_assign_fast's deferred waves of this step are done
         F.ctl->cand_fresh = 1;
         F.ctl->n_pend = (F.prior == kPriorNiw) ? A : 0;
     }
@@ -1419,6 +1680,44 @@ bool np8_supported(int D, int M) {
     NP8_FOR_EACH_DM(X)
 #undef X
     return false;
+}
+
+hipError_t np8_launch_assign_fast(const AssignArgs &A, int D, int M, hipStream_t s) {
+    const int64_t n = A.p1 - A.p0;
+    if (n <= 0) return hipSuccess;
+    const dim3 grid((unsigned)((n + NP8_ASSIGN_BLOCK - 1) / NP8_ASSIGN_BLOCK)), block(NP8_ASSIGN_BLOCK);
+#define X(d, m)                                                                                          \
+    if (D == d && M == m) {                                                                              \
+        if (A.count_eval)                                                                                \
+            hipLaunchKernelGGL((np8_assign_fast<d, m, kPriorReference, true>), grid, block, 0, s, A);    \
+        else                                                                                             \
+            hipLaunchKernelGGL((np8_assign_fast<d, m, kPriorReference, false>), grid, block, 0, s, A);   \
+        return hipGetLastError();                                                                        \
+    }
+    NP8_FOR_EACH_DM(X)
+#undef X
+    return hipErrorInvalidValue;
+}
+
+hipError_t np8_launch_assign_queue(const AssignArgs &A, int D, int M, hipStream_t s) {
+    const int64_t n = A.p1 - A.p0;
+    if (n <= 0) return hipSuccess;
+    // walks the listed waves with a grid of at most kQueueBlocks (usually a few waves have work)
+    constexpr int64_t kQueueBlocks = 2048;
+    int64_t nb = (n + 63) / 64;
+    if (nb > kQueueBlocks) nb = kQueueBlocks;
+    const dim3 grid((unsigned)nb), block(64);
+#define X(d, m)                                                                                           \
+    if (D == d && M == m) {                                                                               \
+        if (A.count_eval)                                                                                 \
+            hipLaunchKernelGGL((np8_assign_queue<d, m, kPriorReference, true>), grid, block, 0, s, A);    \
+        else                                                                                              \
+            hipLaunchKernelGGL((np8_assign_queue<d, m, kPriorReference, false>), grid, block, 0, s, A);   \
+        return hipGetLastError();                                                                         \
+    }
+    NP8_FOR_EACH_DM(X)
+#undef X
+    return hipErrorInvalidValue;
 }
 
 hipError_t np8_launch_assign(const AssignArgs &A, int D, int M, int prior, hipStream_t s) {

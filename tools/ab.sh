@@ -3,7 +3,7 @@
 # for each variant library given (tools/build_variant.sh), one JSON line each into gpurun_out/ab/.
 set -o pipefail
 mkdir -p gpurun_out/ab
-ARGS=${AB_ARGS:-"--steps 200 --warmup 40 --cpu-seconds 0 --cold-sweeps 0"}
+ARGS=${AB_ARGS:-"--steps 200 --warmup 40 --cpu-seconds 0 --cold-sweeps 0 --no-c5"}
 timeout -k 10 200 python -u bench.py $ARGS > gpurun_out/ab/base.json 2> gpurun_out/ab/base.err || exit 1
 for v in "$@"; do
   NP8_LIB_OVERRIDE=$PWD/noparama_amd/lib/exp/$v.so timeout -k 10 200 python -u bench.py $ARGS \
