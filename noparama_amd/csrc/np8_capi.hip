@@ -80,6 +80,9 @@ struct np8_ctx {
     double *plr2 = nullptr;    // per dense row: the squared radius its candidate list assumes
     // two-kernel assign (np8_assign_fast, then np8_assign over the lanes it deferred): reference prior with a
     // diagonal base-measure whitening; NP8_NO_FAST=1 switches it off (A/B runs)
+    double *slot_logn1 = nullptr;  // [kcap] log(n - 1) per live slot (np8_finalize)
+    int32_t *plen_s = nullptr;     // [kcap] plen / plr2 by slot (np8_prune)
+    double *plr2_s = nullptr;
     int32_t *queue = nullptr;  // [64 * waves] deferred positions, by fast-kernel wave
     int32_t *qcount = nullptr; // [waves] deferred lanes per wave
     int32_t *qlist = nullptr;  // [waves] the waves that deferred lanes (ctl->qwaves)
@@ -429,7 +432,8 @@ void free_device(np8_ctx *c) {
                     c->sm_hist, c->sm_mem, c->sm_off, c->sm_live, c->sm_Xm, c->sm_ownm, c->sm_cross, c->sm_ctl,
                     c->sm_typ, c->sm_slist, c->sm_stheta, c->stage, c->evalc, c->z_base, c->cnt_base,
                     c->chg_slot, c->mu_base, c->sigma_base, c->chg_item, c->chg_count, c->chg_flags,
-                    c->inv_hist, c->inv_out, c->queue, c->qcount, c->qlist};
+                    c->inv_hist, c->inv_out, c->queue, c->qcount, c->qlist, c->slot_logn1, c->plen_s,
+                    c->plr2_s};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     if (c->sm_first_host) (void)hipHostFree(c->sm_first_host);
@@ -632,6 +636,7 @@ FinArgs fin_args(np8_ctx *c, const unsigned char *recs, int world) {
     F.slot_c = c->slot_c;
     F.slot_sigma = c->slot_sigma;
     F.slot_iso = c->slot_iso;
+    F.slot_logn1 = c->slot_logn1;
     F.gp_iso = c->gp_iso;
     F.cand = c->cand;
     F.dense_of = c->dense_of;
@@ -760,6 +765,12 @@ AssignArgs assign_args(np8_ctx *c, int64_t p0, int64_t p1, const int64_t *order,
     A.lam_lo = c->lam_lo;
     A.wdist = nullptr;  // set by launch_assign on the wide path (after np8_wide_dist)
     A.queue = A.queue_out = A.qcount = A.qlist = nullptr;
+    A.slot_mu = c->slot_mu;
+    A.slot_c = c->slot_c;
+    A.slot_iso = c->slot_iso;
+    A.slot_logn1 = c->slot_logn1;
+    A.plen_s = c->plen_s;
+    A.plr2_s = c->plr2_s;
     return A;
 }
 
@@ -770,6 +781,7 @@ int launch_finalize(np8_ctx *c, const unsigned char *recs, int world) {
     if (c->gather)  // the step's radius records (any order with finalize: both only raise the gathered radii)
         HIPC(c, np8_launch_fold_r2(c->wr2, c->assign_waves, c->r2, c->kcap, c->stream));
     HIPC(c, np8_launch_finalize(F, c->stream));
+    if (F.frame_payload && c->prior != NP8_PRIOR_NIW) HIPC(c, np8_launch_frame_slots(F, c->stream));
     if (c->prior == NP8_PRIOR_NIW) {  // the accepted auxiliaries' full parameters
         NiwArgs A = niw_args(c);
         A.recs = recs;
@@ -830,6 +842,8 @@ int launch_prune(np8_ctx *c, bool last) {
     P.plist = c->plist;
     P.plen = c->plen;
     P.plr2 = c->plr2;
+    P.plen_s = c->plen_s;
+    P.plr2_s = c->plr2_s;
     P.ls = c->kcap;
     P.D = c->D;
     P.kcap = c->kcap;
@@ -1320,6 +1334,8 @@ int np8_create(np8_ctx **out, const np8_config *cfg) {
         (r = dalloc(c, &c->mu_best, (size_t)kc * D)) || (r = dalloc(c, &c->sigma_best, (size_t)kc * D * D)) ||
         (r = dalloc(c, &c->cand, (size_t)kc * c->CS)) || (r = dalloc(c, &c->ctl, 1)) ||
         (r = dalloc(c, &c->dense_of, (size_t)kc)) || (r = dalloc(c, &c->slot_iso, (size_t)kc)) ||
+        (r = dalloc(c, &c->slot_logn1, (size_t)kc)) || (r = dalloc(c, &c->plen_s, (size_t)kc)) ||
+        (r = dalloc(c, &c->plr2_s, (size_t)kc)) ||
         (r = dalloc(c, &c->rec, (size_t)c->rec_bytes)) || (r = dalloc(c, &c->evalc, (size_t)4 * kEvalSlots)) ||
         (c->param_update != NP8_PARAM_FROZEN && (r = dalloc(c, &c->acc, (size_t)kc * (D + DP)))) ||
         (kc <= kPruneMaxKcap && ((r = dalloc(c, &c->r2, 2 * (size_t)kc)) || (r = dalloc(c, &c->plen, (size_t)kc)) ||
@@ -1368,6 +1384,7 @@ int np8_create(np8_ctx **out, const np8_config *cfg) {
         (c->prior == NP8_PRIOR_NIW &&
          ((r = dalloc(c, &c->d_U, (size_t)D * D)) || (r = dalloc(c, &c->d_Uinv, (size_t)D * D)) ||
           (r = dalloc(c, &c->d_Psi0, (size_t)D * D)) || (r = dalloc(c, &c->pend, (size_t)4 * kReqMax)))) ||
+        (c->wide && c->prior != NP8_PRIOR_NIW && (r = dalloc(c, &c->pend, (size_t)4 * kReqMax))) ||
         (c->wide && ((r = dalloc(c, &c->wA, (size_t)kc * D * D)) ||
                      (r = dalloc(c, &c->wfrag, (size_t)kc * (D * D + D))) ||  // >= the compact rows
                      (r = dalloc(c, &c->wmu, (size_t)kc * D)) || (r = dalloc(c, &c->lam_lo, (size_t)kc)) ||

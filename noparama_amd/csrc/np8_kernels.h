@@ -140,6 +140,10 @@ struct AssignArgs {
     int32_t *queue_out;        // np8_assign_fast: where deferred positions go
     int32_t *qcount;           // [waves of the step]
     int32_t *qlist;            // waves with deferred lanes (ctl->qwaves of them, cleared by np8_finalize)
+    // np8_assign_fast: the own row by slot, in one round of loads (no slot -> dense row -> row chain)
+    const double *slot_mu, *slot_c, *slot_iso, *slot_logn1;
+    const int32_t *plen_s;     // plen of the slot's dense row (np8_prune)
+    const double *plr2_s;      // plr2 of the slot's dense row
 };
 
 // Wide-path tables (np8_wide.hip), maintained for the slots flagged in dirty.
@@ -164,6 +168,8 @@ struct PruneArgs {
     double *r2;         // [2][kcap]: radii in use | gathered this sweep
     int32_t *plist, *plen;
     double *plr2;       // per dense row: the squared radius the list was built for
+    int32_t *plen_s;    // plen and plr2 again, indexed by the row's slot (np8_assign_fast)
+    double *plr2_s;
     int32_t ls, D, kcap;
     int32_t gathered;   // the sweep's last step of a gathering sweep: lists from the gathered radii, which
                         // then become the radii in use
@@ -180,6 +186,7 @@ struct FinArgs {
     int32_t *zs[2];  // sorted-layout labels (buffer ctl->cur), null when not in use
     int64_t n_loc, offset;
     double *slot_mu, *slot_P, *slot_c, *slot_sigma, *slot_iso;
+    double *slot_logn1;  // log(n - 1) of each live slot (the own-row weight), as its dense row holds it
     double *cand;
     int32_t *dense_of;
     Ctl *ctl;
@@ -376,6 +383,8 @@ hipError_t np8_launch_resort(const SortArgs &S, hipStream_t s);
 hipError_t np8_launch_assign(const np8::AssignArgs &A, int D, int M, int prior, hipStream_t s);
 // np8_assign_fast (reference prior, isotropic Lambda, label-sorted layout): defers lanes into A.queue_out / ctl->qn
 hipError_t np8_launch_assign_fast(const np8::AssignArgs &A, int D, int M, hipStream_t s);
+// wide path, reference prior: the slots np8_finalize accepted (ctl->n_pend, F.pend)
+hipError_t np8_launch_frame_slots(const np8::FinArgs &F, hipStream_t s);
 // np8_assign_queue: the lanes np8_assign_fast deferred (A.queue, A.qcount, A.qlist, ctl->qwaves)
 hipError_t np8_launch_assign_queue(const np8::AssignArgs &A, int D, int M, hipStream_t s);
 // Pruning radii: the step's per-wave records (AssignArgs::wr2) into the gathered radii (r2 + kcap).

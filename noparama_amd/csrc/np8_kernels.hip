@@ -615,10 +615,10 @@ __global__ __launch_bounds__(NP8_ASSIGN_BLOCK) __attribute__((amdgpu_waves_per_e
     if (p >= A.p1) return;
     NP8_CLK(0);
     const int lane = threadIdx.x & 63;
-    const int cur = A.ctl->cur;
-    int32_t *__restrict__ zs = cur ? A.zs[1] : A.zs[0];
-    const int32_t *__restrict__ ids = cur ? A.ids[1] : A.ids[0];
-    const double *__restrict__ X = cur ? A.Xs[1] : A.Xs[0];
+    // the label-sorted layout is always buffer 0 (np8_sort_copyback): no load in front of the item loads
+    int32_t *__restrict__ zs = A.zs[0];
+    const int32_t *__restrict__ ids = A.ids[0];
+    const double *__restrict__ X = A.Xs[0];
     const double *__restrict__ cand = A.cand;
     const double *__restrict__ hyp = A.hyp;
     const int32_t zi = zs[p];
@@ -630,37 +630,45 @@ __global__ __launch_bounds__(NP8_ASSIGN_BLOCK) __attribute__((amdgpu_waves_per_e
     for (int a = 0; a < D; ++a) x[a] = X[(int64_t)a * A.n_loc + p];
     const int K = A.ctl->K;
     NP8_CLK(1);
-    const int32_t zf = __builtin_amdgcn_readfirstlane(zi);
-    const int32_t jo = (__ballot(zi != zf) == 0ull) ? A.dense_of[zf] : A.dense_of[zi];
-
     bool defer = COUNT;  // counting runs: every lane takes np8_assign's counting instance
     PickState st;
     st.S = 1.0;
     st.u = -1.0;
-    st.pick = jo;
     st.T = 0.0;
     double d2own = 0.0;  // |x - mu_own|^2: the own row's quadratic form and the list's radius check
+    int32_t jo = 0, nlist = 0;
+    double r2list = 0.0;
     int32_t pslot = zi;
-    if (!COUNT) {
+    {
+        // one pass per distinct own slot of the wave (one in the label-sorted layout); everything about the
+        // own row is read by slot in one round of scalar loads: the parameters from the slot tables (the
+        // candidate rows copy them), log(n - 1), the dense row and its candidate list's length and radius
         uint64_t pend = __ballot(1);
-        while (pend) {  // one pass per distinct own row of the wave (one in the label-sorted layout)
-            const int32_t j = __builtin_amdgcn_readlane(jo, __ffsll((unsigned long long)pend) - 1);
-            const double *eo = cand + (int64_t)j * CS;
-            const double iso = eo[F + kFieldIso];
-            if (jo == j) {
+        while (pend) {
+            const int32_t s = __builtin_amdgcn_readlane(zi, __ffsll((unsigned long long)pend) - 1);
+            const double *mo = A.slot_mu + (int64_t)s * D;
+            const double iso = A.slot_iso[s], cs = A.slot_c[s], l1 = A.slot_logn1[s];
+            const int32_t js = A.dense_of[s], pl = A.plen_s[s];
+            const double pr = A.plr2_s[s];
+            if (zi == s) {
+                jo = js;
+                nlist = pl;
+                r2list = pr;
                 if (iso > 0.0) {  // cand_ll's isotropic form, operation for operation
-                    double s2 = (x[0] - eo[0]) * (x[0] - eo[0]);
+                    double s2 = (x[0] - mo[0]) * (x[0] - mo[0]);
 #pragma unroll
-                    for (int a = 1; a < D; ++a) s2 = fma(x[a] - eo[a], x[a] - eo[a], s2);
+                    for (int a = 1; a < D; ++a) s2 = fma(x[a] - mo[a], x[a] - mo[a], s2);
                     d2own = s2;
-                    st.T = fma(-0.5, s2 * iso, eo[F + kFieldC]) + eo[F + kFieldLogn1];
+                    st.T = fma(-0.5, s2 * iso, cs) + l1;
                 } else {
                     defer = true;
                 }
             }
-            pend &= ~__ballot(jo == j);
+            pend &= ~__ballot(zi == s);
         }
     }
+    if (COUNT) defer = true;
+    st.pick = jo;
     NP8_CLK(2);
     const double zslot = (double)zi;
     int ngroups = 0;
@@ -690,11 +698,10 @@ __global__ __launch_bounds__(NP8_ASSIGN_BLOCK) __attribute__((amdgpu_waves_per_e
             const int32_t j0 = __builtin_amdgcn_readlane(jo, __ffsll((unsigned long long)pend) - 1);
             pend &= ~__ballot(jo == j0);
             if (jo == j0 && !defer) {
-                full = !(d2own <= A.plr2[j0]);
+                full = !(d2own <= r2list);
                 if (!full) {
-                    const int32_t nl = A.plen[j0];
                     const int32_t *__restrict__ lst = A.plist + (int64_t)j0 * A.ls;
-                    for (int q = 0; q < nl && !defer; ++q) visit(lst[q], false);
+                    for (int q = 0; q < nlist && !defer; ++q) visit(lst[q], false);
                 }
             }
         }
@@ -850,7 +857,9 @@ __global__ __launch_bounds__(kSortThreads) void np8_sort_scatter(SortArgs S) {
     const int nb = S.kcap * S.nsub;
     int *lh = reinterpret_cast<int *>(smem);
     int *lbase = lh + nb;
-    const int src = S.ctl->cur, dst = src ^ 1;
+    // the current layout is always buffer 0 (kernels need not load which one): a rebuild from the item order
+    // writes it directly, a re-sort goes 0 -> 1 and np8_sort_copyback copies it back
+    const int src = 0, dst = S.force ? 0 : 1;
     const int32_t *z = S.force ? S.z : (src ? S.zs[1] : S.zs[0]);
     const int32_t *ids = S.force ? nullptr : (src ? S.ids[1] : S.ids[0]);
     const double *X = S.force ? S.X : (src ? S.Xs[1] : S.Xs[0]);
@@ -883,12 +892,25 @@ __global__ __launch_bounds__(kSortThreads) void np8_sort_scatter(SortArgs S) {
             for (int a = 0; a < S.D; ++a) Xo[(int64_t)a * S.n + q] = X[(int64_t)a * S.n + p];
         }
     }
-    // the last block to finish makes the new layout current (read by the next kernels)
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __threadfence();
-        if (atomicAdd(&S.ctl->done_blocks, 1u) == gridDim.x - 1) S.ctl->cur = dst;
-    }
+}
+
+// A re-sort's result (buffer 1) back into buffer 0, the current layout.  16-byte pieces, grid-stride.
+__global__ __launch_bounds__(256) void np8_sort_copyback(SortArgs S) {
+    if (!S.ctl->do_sort || S.force) return;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    auto copy = [&](const void *src, void *dst, int64_t bytes) {
+        const uint4 *s4 = reinterpret_cast<const uint4 *>(src);
+        uint4 *d4 = reinterpret_cast<uint4 *>(dst);
+        const int64_t n16 = bytes / 16;
+        for (int64_t i = i0; i < n16; i += stride) d4[i] = s4[i];
+        const unsigned char *sb = reinterpret_cast<const unsigned char *>(src);
+        unsigned char *db = reinterpret_cast<unsigned char *>(dst);
+        for (int64_t i = n16 * 16 + i0; i < bytes; i += stride) db[i] = sb[i];
+    };
+    copy(S.zs[1], S.zs[0], 4 * S.n);
+    copy(S.ids[1], S.ids[0], 4 * S.n);
+    copy(S.Xs[1], S.Xs[0], (int64_t)S.esz * S.D * S.n);
 }
 
 __global__ __launch_bounds__(1024) void np8_sort_scan(SortArgs S) {
@@ -994,7 +1016,8 @@ constexpr int kPruneBlocks = 32;  // np8_prune grid: 128 rows per pass
 // R2of(slot): the squared radius of the slot's items that will walk the list.
 template <int DT = 0, typename R2of>
 __device__ void prune_row(const double *__restrict__ cand, R2of R2of_slot, int32_t *__restrict__ plist,
-                          int32_t *__restrict__ plen, double *__restrict__ plr2, int ls, int Drt, int K, int k0) {
+                          int32_t *__restrict__ plen, double *__restrict__ plr2, int32_t *__restrict__ plen_s,
+                          double *__restrict__ plr2_s, int ls, int Drt, int K, int k0) {
     const int D = DT > 0 ? DT : Drt;
     const int DP = D * (D + 1) / 2, CS = cand_stride(D), F = D + DP;
     const int lane = threadIdx.x & 63;
@@ -1038,8 +1061,11 @@ __device__ void prune_row(const double *__restrict__ cand, R2of R2of_slot, int32
         count += __popcll(b);
     }
     if (lane == 0) {
+        const double r2l = prunable ? R2 : __longlong_as_double(0x7FF0000000000000ll);  // +inf: every row is listed
         plen[k0] = count;
-        plr2[k0] = prunable ? R2 : __longlong_as_double(0x7FF0000000000000ll);  // +inf: every row is listed
+        plr2[k0] = r2l;
+        plen_s[slot0] = count;
+        plr2_s[slot0] = r2l;
     }
 }
 
@@ -1194,6 +1220,20 @@ __global__ __launch_bounds__(kFinThreads) void np8_finalize(FinArgs F) {
     const int D = F.D, DP = D * (D + 1) / 2, CS = cand_stride(D);
     const int per = (kcap + kFinThreads - 1) / kFinThreads;
     const int s0 = min(kcap, tid * per), s1 = min(kcap, s0 + per);
+    // everything the common step (no request accepted) needs from global memory, loaded in one round:
+    // old counts (liveness changes), deltas, and the table entries of this thread's first kFinPre slots
+    constexpr int kFinPre = 2;
+    int cold[kFinPre];
+    double pc[kFinPre], piso[kFinPre];
+#pragma unroll
+    for (int q = 0; q < kFinPre; ++q) {
+        const int s = s0 + q;
+        const bool in = s < s1;
+        cold[q] = in ? F.cnt[s] : 0;
+        pc[q] = in ? F.slot_c[s] : 0.0;
+        piso[q] = in ? F.slot_iso[s] : 0.0;
+    }
+    const int cand_fresh = F.ctl->cand_fresh;
 
     if (tid == 0) {
         int n = 0;
@@ -1205,7 +1245,17 @@ __global__ __launch_bounds__(kFinThreads) void np8_finalize(FinArgs F) {
         s_flags[0] = n;
         s_flags[1] = 0;
     }
-    for (int s = s0; s < s1; ++s) {
+    // (slot s0 + q for q < kFinPre from the registers -- unrolled, static indices -- then any further ones)
+#pragma unroll
+    for (int q = 0; q < kFinPre; ++q) {
+        const int s = s0 + q;
+        if (s < s1) {
+            int c = cold[q];
+            for (int r = 0; r < F.world; ++r) c += rec_delta(F, r)[s];
+            cnt_s[s] = c;
+        }
+    }
+    for (int s = s0 + kFinPre; s < s1; ++s) {
         int c = F.cnt[s];
         for (int r = 0; r < F.world; ++r) c += rec_delta(F, r)[s];
         cnt_s[s] = c;
@@ -1269,16 +1319,14 @@ __global__ __launch_bounds__(kFinThreads) void np8_finalize(FinArgs F) {
         for (int q = tid; q < A; q += kFinThreads) {
             const Request r = *request_at(F, base, kidx[q]);
             const int s = freeslot[q];
-            if (F.prior == kPriorNiw) {  // built by np8_niw_aux_slots (O(D^3) per slot)
+            if (F.prior == kPriorNiw || F.frame_payload) {
+                // built by np8_niw_aux_slots (NIW: O(D^3) per slot) or np8_frame_slots (the wide path's (v, mu)
+                // from the item frame): registers this one workgroup cannot spare
                 int64_t *pe = F.pend + 4 * (int64_t)q;
                 pe[0] = reinterpret_cast<const unsigned char *>(request_vmu(F, base, kidx[q])) - F.recs;
                 pe[1] = r.i;
                 pe[2] = r.m;
                 pe[3] = s;
-            } else if (F.frame_payload) {  // wide path: (v, mu) from the item frame
-                double vmu[kMaxD + 1];
-                frame_to_vmu(F, request_vmu(F, base, kidx[q]), r.i, r.m, vmu);
-                write_new_slot(F, vmu, s);
             } else {
                 write_new_slot(F, request_vmu(F, base, kidx[q]), s);
             }
@@ -1295,30 +1343,48 @@ __global__ __launch_bounds__(kFinThreads) void np8_finalize(FinArgs F) {
     __syncthreads();
     // write counts back and rebuild the dense candidate table in ascending slot order
     int nl = 0, lchange = 0;
-    for (int s = s0; s < s1; ++s) {
+#pragma unroll
+    for (int q = 0; q < kFinPre; ++q) {
+        const int s = s0 + q;
+        if (s < s1) {
+            nl += (cnt_s[s] > 0);
+            lchange |= ((cnt_s[s] > 0) != (cold[q] > 0));  // a slot became live or empty
+        }
+    }
+    for (int s = s0 + kFinPre; s < s1; ++s) {
         nl += (cnt_s[s] > 0);
-        lchange |= ((cnt_s[s] > 0) != (F.cnt[s] > 0));  // a slot became live or empty
+        lchange |= ((cnt_s[s] > 0) != (F.cnt[s] > 0));
     }
     // the live rows keep their order and parameters unless a slot changed liveness, requests were
     // accepted or the state was uploaded: then mu/P' of every row are copied below
-    const bool copy_rows = __syncthreads_or(lchange | (A > 0 ? 1 : 0) | (F.ctl->cand_fresh ? 0 : 1)) != 0;
+    const bool copy_rows = __syncthreads_or(lchange | (A > 0 ? 1 : 0) | (cand_fresh ? 0 : 1)) != 0;
     int nlive;
     int k = block_excl_scan(nl, sh, &nlive);
-    for (int s = s0; s < s1; ++s) {
+    // slot s -> its dense row, counts and the row's scalar fields (the prefetched entries unless this step
+    // created slots, whose entries were written above)
+    auto write_slot = [&](int s, double cs, double iso) {
         const int c = cnt_s[s];
         F.cnt[s] = c;
         F.dense_of[s] = (c > 0) ? k : -1;
         if (c > 0) {
             double *e = F.cand + (int64_t)k * CS + D + DP;
-            e[kFieldC] = F.slot_c[s];
+            const double l1 = (c > 1) ? log_pos((double)(c - 1)) : kZeroLogWeight;
+            e[kFieldC] = cs;
             e[kFieldLogn] = log_pos((double)c);
-            e[kFieldLogn1] = (c > 1) ? log_pos((double)(c - 1)) : kZeroLogWeight;
+            e[kFieldLogn1] = l1;
+            F.slot_logn1[s] = l1;
             e[kFieldSlot] = (double)s;
-            e[kFieldIso] = F.slot_iso[s];
+            e[kFieldIso] = iso;
             live_s[k] = s;
             ++k;
         }
+    };
+#pragma unroll
+    for (int q = 0; q < kFinPre; ++q) {
+        const int s = s0 + q;
+        if (s < s1) write_slot(s, A == 0 ? pc[q] : F.slot_c[s], A == 0 ? piso[q] : F.slot_iso[s]);
     }
+    for (int s = s0 + kFinPre; s < s1; ++s) write_slot(s, F.slot_c[s], F.slot_iso[s]);
     __syncthreads();
     // mu and P' of every live row, all threads (not on the wide path: its kernels read the fp32 factor
     // rows of np8_wide_rows, and 4 MB of P' at D = 64 would keep this one workgroup busy for 0.3 ms)
@@ -1331,7 +1397,7 @@ __global__ __launch_bounds__(kFinThreads) void np8_finalize(FinArgs F) {
         F.ctl->K = nlive;
         F.ctl->qwaves = 0;  // np8_assign_fast's deferred waves of this step are done
         F.ctl->cand_fresh = 1;
-        F.ctl->n_pend = (F.prior == kPriorNiw) ? A : 0;
+        F.ctl->n_pend = (F.prior == kPriorNiw || F.frame_payload) ? A : 0;
     }
     // clear the local record for the next step (all reads of it are behind the barriers above)
     if (F.local_rec) {
@@ -1339,6 +1405,30 @@ __global__ __launch_bounds__(kFinThreads) void np8_finalize(FinArgs F) {
         for (int s = tid; s < kcap; s += kFinThreads) delta[s] = 0;
         if (tid == 0) reinterpret_cast<RecHeader *>(F.local_rec)->nreq = 0;
     }
+}
+
+// The wide path's new slots under the reference prior: (v, mu) of each accepted request from the item frame
+// its rank recorded, then the slot (what np8_finalize did in place before: 2.7 KB of scratch per lane there).
+// One thread per pending request (ctl->n_pend, listed by np8_finalize).
+__global__ __launch_bounds__(64) void np8_frame_slots(FinArgs F) {
+    const int n = F.ctl->n_pend;
+    for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < n; q += gridDim.x * blockDim.x) {
+        const int64_t *pe = F.pend + 4 * (int64_t)q;
+        const double *frame = reinterpret_cast<const double *>(F.recs + pe[0]);
+        double vmu[kMaxD + 1];
+        const int sl = (int)pe[3];
+        frame_to_vmu(F, frame, pe[1], (int)pe[2], vmu);
+        write_new_slot(F, vmu, sl);
+        // np8_finalize built the slot's dense row before its parameters existed: its scalars now
+        double *e = F.cand + (int64_t)F.dense_of[sl] * cand_stride(F.D) + F.D + F.D * (F.D + 1) / 2;
+        e[kFieldC] = F.slot_c[sl];
+        e[kFieldIso] = F.slot_iso[sl];
+    }
+}
+
+hipError_t np8_launch_frame_slots(const FinArgs &F, hipStream_t s) {
+    hipLaunchKernelGGL(np8_frame_slots, dim3(64), dim3(64), 0, s, F);
+    return hipGetLastError();
 }
 
 // ---- max likelihood --------------------------------------------------------------------------------
@@ -1952,6 +2042,7 @@ hipError_t np8_launch_resort(const SortArgs &S, hipStream_t s) {
     hipLaunchKernelGGL(np8_sort_hist, dim3(nb), dim3(kSortThreads), sizeof(int) * bins, s, S);
     hipLaunchKernelGGL(np8_sort_scan, dim3(1), dim3(1024), 0, s, S);
     hipLaunchKernelGGL(np8_sort_scatter, dim3(nb), dim3(kSortThreads), 2 * sizeof(int) * bins, s, S);
+    hipLaunchKernelGGL(np8_sort_copyback, dim3(1024), dim3(256), 0, s, S);
     return hipGetLastError();
 }
 
@@ -2040,7 +2131,7 @@ __global__ __launch_bounds__(256) void np8_prune(PruneArgs A) {
         for (int s = threadIdx.x; s < A.kcap; s += blockDim.x) A.r2[A.kcap + s] = 0.0;
     auto R2of = [&](int slot) { return src[slot]; };
     for (int k0 = blockIdx.x * 4 + (threadIdx.x >> 6); k0 < K; k0 += gridDim.x * 4)  // wave-uniform
-        prune_row<DT>(A.cand, R2of, A.plist, A.plen, A.plr2, A.ls, A.D, K, k0);
+        prune_row<DT>(A.cand, R2of, A.plist, A.plen, A.plr2, A.plen_s, A.plr2_s, A.ls, A.D, K, k0);
 }
 
 __global__ void np8_advance_epoch(Ctl *ctl, uint32_t n) { ctl->t_base += n; }
