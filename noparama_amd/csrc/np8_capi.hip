@@ -87,6 +87,12 @@ struct np8_ctx {
     int32_t *qcount = nullptr; // [waves] deferred lanes per wave
     int32_t *qlist = nullptr;  // [waves] the waves that deferred lanes (ctl->qwaves)
     bool diag_U = false, fast_off = false;
+    // fewer launches per step (np8_step_tail): the radius fold, finalize and the candidate lists in one launch
+    // (NP8_FUSE=1; off by default: 26.9 vs 23.1 us per sweep at N = 125k)
+    bool fuse_off = false;
+    bool queue_on = false;  // NP8_QUEUE=1: launch np8_assign_queue after the fast kernel even when no lane can defer
+    bool pruned_last = false;    // the sweep's last step built the lists (end_sweep's prune already done)
+
     // data-parallel sweep in `substeps` synchronous sub-steps (np8_config.substeps): sub-step s is the
     // contiguous range [sub_start[s], sub_start[s+1]) of the label-sorted layout (sorted by sub-step, slot)
     int substeps = 1;
@@ -109,6 +115,9 @@ struct np8_ctx {
     int32_t *z = nullptr, *z_best = nullptr;
     double *slot_mu = nullptr, *slot_P = nullptr, *slot_c = nullptr, *slot_sigma = nullptr, *slot_iso = nullptr;
     double gp_iso = 0.0;
+    // every row np8_assign_fast can meet is isotropic (the uploaded live slots, and every G0 draw: gp_iso > 0), so
+    // it defers no lane and np8_assign_queue is left out of the step (a restored checkpoint: unknown, false)
+    bool rows_iso = false;
     int32_t *cnt = nullptr, *cnt_best = nullptr;
     double *mu_best = nullptr, *sigma_best = nullptr;
     double *cand = nullptr;
@@ -532,6 +541,8 @@ int upload_slots(np8_ctx *c, const std::vector<SlotHost> &slots, const std::vect
                 is = is && ((a == b) ? slots[s].P[q] == slots[s].P[0] : slots[s].P[q] == 0.0);
         iso[s] = is ? slots[s].P[0] : 0.0;
     }
+    c->rows_iso = c->gp_iso > 0.0;
+    for (int s = 0; s < K; ++s) c->rows_iso = c->rows_iso && (cnt[s] == 0 || iso[s] > 0.0);
     HIPC(c, hipMemcpyAsync(c->slot_iso, iso.data(), sizeof(double) * iso.size(), hipMemcpyHostToDevice, c->stream));
     std::vector<int32_t> cn(c->kcap, 0);
     for (int s = 0; s < K; ++s) cn[s] = cnt[s];
@@ -774,10 +785,34 @@ AssignArgs assign_args(np8_ctx *c, int64_t p0, int64_t p1, const int64_t *order,
     return A;
 }
 
-int launch_finalize(np8_ctx *c, const unsigned char *recs, int world) {
+PruneArgs prune_args(np8_ctx *c, bool last);
+
+// prune: -1 none; 0 / 1 the candidate lists right after finalize, in the same launch (np8_step_tail), as
+// launch_prune(c, false / true) would build them -- the frozen reference-prior sweep, where nothing changes the
+// table between the two.
+int launch_finalize(np8_ctx *c, const unsigned char *recs, int world, int prune = -1) {
     Timer t;
     timer_begin(c, 1, t);
     FinArgs F = fin_args(c, recs, world);
+    const bool tail = !c->fuse_off && (prune >= 0 || c->gather) && !c->wide && c->prior == NP8_PRIOR_REFERENCE;
+    if (tail) {  // radius fold, finalize (+ lists) in one launch
+        TailArgs T;
+        std::memset(&T, 0, sizeof(T));
+        T.fold = c->gather ? 1 : 0;
+        T.fold_n = c->assign_waves;
+        T.fin = 1;
+        PruneArgs P;
+        std::memset(&P, 0, sizeof(P));
+        if (prune >= 0) {
+            P = prune_args(c, prune == 1);
+            T.prune = 1;
+        }
+        AssignArgs A = assign_args(c, 0, 0, nullptr, false);  // the radius records (wr2)
+        HIPC(c, np8_launch_step_tail(A, F, P, T, c->assign_waves, c->D, c->M, c->stream));
+        if (prune >= 0) c->lists_valid = true;
+        timer_end(c, t);
+        return NP8_OK;
+    }
     if (c->gather)  // the step's radius records (any order with finalize: both only raise the gathered radii)
         HIPC(c, np8_launch_fold_r2(c->wr2, c->assign_waves, c->r2, c->kcap, c->stream));
     HIPC(c, np8_launch_finalize(F, c->stream));
@@ -821,10 +856,13 @@ int launch_assign(np8_ctx *c, int64_t p0, int64_t p1, const int64_t *order, bool
         A.queue_out = c->queue;
         A.qcount = c->qcount;
         A.qlist = c->qlist;
+        A.no_queue = (c->rows_iso && !A.count_eval && !c->queue_on) ? 1 : 0;
         HIPC(c, np8_launch_assign_fast(A, c->D, c->M, c->stream));
-        A.queue = c->queue;
-        A.queue_out = nullptr;
-        HIPC(c, np8_launch_assign_queue(A, c->D, c->M, c->stream));  // a small grid walking ctl->qwaves
+        if (!A.no_queue) {
+            A.queue = c->queue;
+            A.queue_out = nullptr;
+            HIPC(c, np8_launch_assign_queue(A, c->D, c->M, c->stream));  // a small grid walking ctl->qwaves
+        }
     } else {
         HIPC(c, np8_launch_assign(A, c->D, c->M, c->prior, c->stream));
     }
@@ -834,7 +872,7 @@ int launch_assign(np8_ctx *c, int64_t p0, int64_t p1, const int64_t *order, bool
 
 // Candidate lists for the next sweep from the radii this sweep collected (after every change of
 // the table: finalize and the parameter update).
-int launch_prune(np8_ctx *c, bool last) {
+PruneArgs prune_args(np8_ctx *c, bool last) {
     PruneArgs P;
     P.cand = c->cand;
     P.ctl = c->ctl;
@@ -852,6 +890,11 @@ int launch_prune(np8_ctx *c, bool last) {
     // buffer would only raise radii: pruning stays exact)
     P.clear_next = (last && !P.gathered && c->r2_zero && (c->epoch + 1) % kGatherEvery == 0) ? 1 : 0;
     c->gath_clear = P.clear_next != 0;
+    return P;
+}
+
+int launch_prune(np8_ctx *c, bool last) {
+    PruneArgs P = prune_args(c, last);
     HIPC(c, np8_launch_prune(P, c->kcap, c->stream));
     c->lists_valid = true;
     return NP8_OK;
@@ -925,15 +968,24 @@ int step(np8_ctx *c, int64_t p0, int64_t p1, const int64_t *order, bool use_perm
     int r = launch_assign(c, p0, p1, order, use_perm);
     if (r) return r;
     if (c->world > 1 && !c->comm) return fail(c, NP8_ERR_STATE, "host-exchange mode: use np8_step_local/np8_step_merge");
+    // the lists right after finalize (np8_step_tail) when nothing changes the table in between: the next sub-step's
+    // (radii in use), or the sweep's when its parameters are frozen (end_sweep's prune)
+    const bool mid = sub >= 0 && sub + 1 < c->substeps;
+    const int fprune = (c->collecting && !c->fuse_off && !c->wide && c->prior == NP8_PRIOR_REFERENCE &&
+                        (mid || c->param_update == NP8_PARAM_FROZEN)) ? (mid ? 0 : 1) : -1;
     if (c->comm) {  // the exchange over RCCL (also with a one-rank communicator)
         HIPC(c, np8_launch_req_select(c->stage, c->stage_cap, c->rec, c->rec_cap, c->kcap, c->D, c->req_max, c->stream));
         NCCLC(c, ncclAllGather(c->rec, c->gath, (size_t)c->rec_bytes, ncclUint8, c->comm, c->stream));
-        r = launch_finalize(c, c->gath, c->world);
+        r = launch_finalize(c, c->gath, c->world, fprune);
     } else {
-        r = launch_finalize(c, c->rec, 1);
+        r = launch_finalize(c, c->rec, 1, fprune);
     }
     if (r) return r;
-    if (c->collecting && sub >= 0 && sub + 1 < c->substeps)
+    if (fprune >= 0) {
+        c->pruned_last = fprune == 1;
+        return NP8_OK;
+    }
+    if (c->collecting && mid)
         return launch_prune(c, false);  // lists for the next sub-step (the radii in use)
     // the table changed: lists are valid again after the next prune (end of sweep or of a sub-step)
     c->lists_valid = false;
@@ -1087,10 +1139,13 @@ int end_sweep(np8_ctx *c, bool stats_given = false) {
     int r0 = param_update(c, stats_given ? 2 : 0);
     if (r0) return r0;
     if (c->collecting) {  // after finalize and the parameter update: the table is final
-        r0 = launch_prune(c, true);
-        if (r0) return r0;
+        if (!c->pruned_last) {  // (unless the step's np8_step_tail built the lists already)
+            r0 = launch_prune(c, true);
+            if (r0) return r0;
+        }
         c->collecting = c->gather = false;
     }
+    c->pruned_last = false;
     if (c->debug_inv && (r0 = launch_invariants(c))) return r0;
     if (c->epoch % 5u == 0u) {  // np_mcmc.cpp:172-174
         int r = launch_total_loglik(c);
@@ -1324,6 +1379,8 @@ int np8_create(np8_ctx **out, const np8_config *cfg) {
     c->prune_on = !c->wide && c->kcap <= kPruneMaxKcap && std::getenv("NP8_NO_PRUNE") == nullptr;
     c->wide_prune_off = std::getenv("NP8_NO_PRUNE") != nullptr;
     c->fast_off = std::getenv("NP8_NO_FAST") != nullptr;
+    c->fuse_off = std::getenv("NP8_FUSE") == nullptr;  // opt-in: measured slower than separate launches
+    c->queue_on = std::getenv("NP8_QUEUE") != nullptr;
     c->rec_cap = c->req_max;  // grown to the item count by np8_set_data (one rank)
     c->rec_bytes = record_bytes(c->kcap, (int)c->rec_cap, c->D);
     int r = 0;
@@ -1778,6 +1835,7 @@ int np8_restore(np8_ctx *c, const void *in, int64_t bytes) {
         HIPC(c, hipMemcpy(q.dev, p, q.bytes, hipMemcpyHostToDevice));
         p += q.bytes;
     }
+    c->rows_iso = false;  // raw slot tables: isotropy unknown (np8_assign_queue stays in)
     c->sorted_valid = false;
     c->use_sorted = false;
     c->lists_valid = c->r2_zero = c->collecting = false;
@@ -1972,6 +2030,8 @@ int np8_sync(np8_ctx *c) {
         if (h.err & kErrCapacity) return fail(c, NP8_ERR_CAPACITY, "a device table is full");
         if (h.err & kErrInvariant)
             return fail(c, NP8_ERR_STATE, "a debug invariant failed (np8_check_invariants: labels, counts, K, table)");
+        if (h.err & kErrQueue)
+            return fail(c, NP8_ERR_STATE, "internal: np8_assign_fast deferred a lane with no queue launched");
     }
     return NP8_OK;
 }

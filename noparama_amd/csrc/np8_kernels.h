@@ -23,7 +23,7 @@ struct Ctl {
     int32_t cur;        // which label-sorted buffer is current
     int32_t do_sort;    // this re-sort pass runs (decided by np8_sort_scan)
     uint32_t done_blocks;
-    int32_t pad2;
+    uint32_t tail_done;   // np8_step_tail: workgroups finished (the last one runs the serial part, resets it)
     int64_t mh_accepted;  // accepted MH proposals (cumulative)
     uint32_t t_base;      // epoch = t_base + the launch's epoch offset (advanced on the device by
                           // replayed sweep graphs, np8_advance_epoch)
@@ -45,7 +45,7 @@ struct Ctl {
 // of the grid serialises the atomics in one L2 channel (4x the kernel time at C3).
 constexpr int kEvalSlots = 1024;
 
-enum : int32_t { kErrCapacity = 1, kErrSigma = 2, kErrInvariant = 4 };
+enum : int32_t { kErrCapacity = 1, kErrSigma = 2, kErrInvariant = 4, kErrQueue = 8 };
 
 // Exchange record of one rank for one synchronous step:
 //   RecHeader | int32 delta[kcap] | Request req[rec_cap] | double vmu[rec_cap][D+1]
@@ -144,6 +144,9 @@ struct AssignArgs {
     const double *slot_mu, *slot_c, *slot_iso, *slot_logn1;
     const int32_t *plen_s;     // plen of the slot's dense row (np8_prune)
     const double *plr2_s;      // plr2 of the slot's dense row
+    // np8_assign_fast: the host launches no np8_assign_queue after it (every live row isotropic, so no lane is
+    // deferred; a deferred lane would set kErrQueue)
+    int32_t no_queue, pad_nq;
 };
 
 // Wide-path tables (np8_wide.hip), maintained for the slots flagged in dirty.
@@ -298,6 +301,22 @@ struct NiwArgs {
     const int64_t *pend;
 };
 
+// np8_step_tail (the end of a synchronous step in one launch): which parts run.
+struct TailArgs {
+    int32_t queue;   // (unused: np8_assign_fast's deferred lanes keep np8_assign_queue -- measured slower here)
+    int32_t fold;    // the step's radius records (AssignArgs::wr2, fold_n of them) into the gathered radii
+    int32_t select;  // np8_req_select: staging record -> exchanged record (sharded step; no finalize then)
+    int32_t fin;     // np8_finalize (FinArgs)
+    int32_t prune;   // np8_prune after it (PruneArgs; the frozen reference-prior sweep)
+    int32_t pad;
+    int64_t fold_n;
+    int64_t lds_bytes;  // dynamic LDS of the launch (np8_finalize_lds_bytes; prune_block stages rows in it)
+    const unsigned char *stage;  // select: staging record, its request capacity, the exchanged record
+    int64_t stage_cap;
+    unsigned char *rec;
+    int64_t rec_cap;
+};
+
 struct LoglikArgs {
     const double *X;
     const int32_t *z;
@@ -409,6 +428,10 @@ hipError_t np8_launch_loglik_matrix(const np8::AssignArgs &A, int D, int M, int 
                                     double *out, hipStream_t s);
 size_t np8_finalize_lds_bytes(int kcap);
 hipError_t np8_launch_finalize(const np8::FinArgs &F, hipStream_t s);
+// np8_step_tail: grid sized for the deferred waves of a step of n_waves fast-kernel waves (T.queue) or the radius
+// records (T.fold), else one workgroup
+hipError_t np8_launch_step_tail(const np8::AssignArgs &A, const np8::FinArgs &F, const np8::PruneArgs &P,
+                                const np8::TailArgs &T, int64_t n_waves, int D, int M, hipStream_t s);
 hipError_t np8_launch_req_select(const unsigned char *stage, int64_t stage_cap, unsigned char *rec, int64_t rec_cap,
                                  int kcap, int D, int req_max, hipStream_t s);
 hipError_t np8_launch_loglik(const np8::LoglikArgs &A, int D, hipStream_t s);

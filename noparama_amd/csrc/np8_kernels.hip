@@ -712,9 +712,10 @@ __global__ __launch_bounds__(NP8_ASSIGN_BLOCK) __attribute__((amdgpu_waves_per_e
     }
     NP8_CLK(3);
     // the auxiliaries: np8_assign's two-level screen, then the exact fp64 draw for the lanes it cannot clear;
-    // a lane that picks an auxiliary (a new-cluster request) is deferred
+    // a lane that picks an auxiliary makes a new-cluster request (appended below)
+    bool req = false;
+    double ny = 0.0;
     if (!defer) {
-        double ny;
         {
             const double *U = hyp + H::kUinvT;  // diagonal (launch condition): whiten() + norm_of() with zeros left out
             double n2 = 0.0;
@@ -759,13 +760,17 @@ __global__ __launch_bounds__(NP8_ASSIGN_BLOCK) __attribute__((amdgpu_waves_per_e
                 pick_step(st, lw, K + m);
             }
         }
-        defer = st.pick >= K;  // a new-cluster request: np8_assign builds its payload
+        req = st.pick >= K;
     }
     NP8_CLK(5);
     // deferred lanes: positions into this wave's slots of the queue (compacted, no atomics), their count
     // for np8_assign's queue mode; nothing else is written for them
     const uint64_t db = __ballot(defer);
-    if (db) {  // rare (requests, rows that are not isotropic): the wave lists itself for np8_assign's queue mode
+    if (db) {  // rare (rows that are not isotropic): the wave lists itself for np8_assign's queue mode
+        if (A.no_queue) {  // the host left the queue kernel out (every row isotropic): must not happen
+            if (lane == (__ffsll((unsigned long long)db) - 1)) atomicOr(&A.ctl->err, kErrQueue);
+            return;
+        }
         const int64_t wv = (p - A.p0) >> 6;
         if (defer) A.queue_out[wv * 64 + __popcll(db & ((1ull << lane) - 1ull))] = (int32_t)p;
         if (lane == (__ffsll((unsigned long long)db) - 1)) {
@@ -773,9 +778,10 @@ __global__ __launch_bounds__(NP8_ASSIGN_BLOCK) __attribute__((amdgpu_waves_per_e
             A.qlist[atomicAdd(&A.ctl->qwaves, 1u)] = (int32_t)wv;
         }
     }
-    const int32_t snew = pslot;  // a lane that is not deferred picked an existing row
+    const int32_t snew = req ? zi : pslot;  // a lane not deferred picked an existing row or stays (request)
     if (A.collect_r2) {  // np8_assign's radius collection, over the lanes not deferred
-        const int32_t tr = defer ? jo : st.pick;
+        // (a requester counts for its old cluster, in case the request is rejected: np8_assign's rule)
+        const int32_t tr = (defer || req) ? jo : st.pick;
         const double *e = cand + (int64_t)tr * CS;
         double d2 = 0.0;
 #pragma unroll
@@ -812,6 +818,22 @@ __global__ __launch_bounds__(NP8_ASSIGN_BLOCK) __attribute__((amdgpu_waves_per_e
         atomicAdd(delta + snew, 1);
         A.z[il] = snew;
         zs[p] = snew;
+    }
+    if (req) {  // np8_assign's request with its payload, the auxiliary's (v, mu)
+        const int q = atomicAdd(A.nreq, 1);
+        if (q < A.req_cap) {  // always: the area holds every item of the step
+            Request r;
+            r.pos = (int64_t)ig;  // synchronous sweep: scan position = item index
+            r.i = (int64_t)ig;
+            r.m = st.pick - K;
+            r.zold = zi;
+            r.lpos = (int32_t)p;
+            r.pad = 0;
+            A.req[q] = r;
+            double y0[D];
+            whiten<D>(hyp, x, y0);
+            aux_params<D>(hyp, y0, ny, A.seed, ig, t, st.pick - K, A.vmu + (int64_t)q * (D + 1));
+        }
     }
     NP8_CLK(6);
 }
@@ -1163,11 +1185,10 @@ __device__ int64_t select_kth_pos(PosAt pos_at, int n, int k, int *hist /* 2048 
 // Several ranks: this rank's requests of the step (staging record, arrival order) -> the req_max of
 // lowest scan position in the exchanged record (the only ones np8_finalize can accept from this rank,
 // DESIGN.md "Finalize"); clears the staging count.  One workgroup; dynamic LDS: hist int[2048].
-__global__ __launch_bounds__(kFinThreads) void np8_req_select(const unsigned char *__restrict__ stage, int64_t stage_cap,
-                                                              unsigned char *__restrict__ rec, int64_t rec_cap, int kcap,
-                                                              int D, int req_max) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    int *hist = reinterpret_cast<int *>(smem);
+// (the body of np8_req_select, also run as the serial tail of np8_step_tail)
+__device__ void req_select_block(const unsigned char *__restrict__ stage, int64_t stage_cap,
+                                 unsigned char *__restrict__ rec, int64_t rec_cap, int kcap, int D, int req_max,
+                                 int *hist /* LDS int[2048] */) {
     __shared__ int sh[32];
     __shared__ int s_cnt;
     RecHeader *sh_hdr = reinterpret_cast<RecHeader *>(const_cast<unsigned char *>(stage));
@@ -1195,6 +1216,13 @@ __global__ __launch_bounds__(kFinThreads) void np8_req_select(const unsigned cha
     }
 }
 
+__global__ __launch_bounds__(kFinThreads) void np8_req_select(const unsigned char *__restrict__ stage, int64_t stage_cap,
+                                                              unsigned char *__restrict__ rec, int64_t rec_cap, int kcap,
+                                                              int D, int req_max) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    req_select_block(stage, stage_cap, rec, rec_cap, kcap, D, req_max, reinterpret_cast<int *>(smem));
+}
+
 namespace {
 __device__ int64_t request_pos(const FinArgs &F, const int *base, int q) { return request_at(F, base, q)->pos; }
 }  // namespace
@@ -1205,8 +1233,8 @@ __device__ int64_t request_pos(const FinArgs &F, const int *base, int q) { retur
 // with every requester still in its old slot; the A = min(req_max, free, requests) requests of lowest
 // scan position are accepted, in position order, into the lowest free slots in ascending order; each
 // accepted requester leaves its old slot; the others keep their cluster (deferred to their next update).
-__global__ __launch_bounds__(kFinThreads) void np8_finalize(FinArgs F) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+// (the body of np8_finalize, also run as the serial tail of np8_step_tail; smem: np8_finalize_lds_bytes)
+__device__ void finalize_block(const FinArgs &F, unsigned char *smem) {
     int64_t *keys = reinterpret_cast<int64_t *>(smem);
     int *kidx = reinterpret_cast<int *>(smem + sizeof(int64_t) * kReqMax);
     int *freeslot = kidx + kReqMax;
@@ -1406,6 +1434,157 @@ __global__ __launch_bounds__(kFinThreads) void np8_finalize(FinArgs F) {
         if (tid == 0) reinterpret_cast<RecHeader *>(F.local_rec)->nreq = 0;
     }
 }
+
+__global__ __launch_bounds__(kFinThreads) void np8_finalize(FinArgs F) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    finalize_block(F, smem);
+}
+
+// np8_prune's work for one workgroup of kFinThreads: every live row's list, after the radius buffers'
+// bookkeeping.  Runs after finalize_block in the same workgroup (the table it reads is behind a barrier).  The
+// rows' fields the bound needs are staged in LDS first (the finalize scratch, free by now; structure of arrays,
+// lane j reads row j's), so one wave per row walks them without a dependent global load per row; the
+// arithmetic is prune_row's, operation for operation.  Tables too large for the LDS take prune_row itself.
+template <int D>
+__device__ void prune_block(const PruneArgs &A, unsigned char *smem, size_t lds_bytes) {
+    constexpr int DP = D * (D + 1) / 2, CS = (D + DP + 5 + 1) & ~1, F = D + DP;
+    constexpr int RW = D + 5;  // mu[D] | c + log n | c + log(n - 1) | iso | R^2 | slot
+    __syncthreads();
+    const int K = A.ctl->K;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, nwb = kFinThreads / 64;
+    if (tid == 0) A.ctl->lists_ok = 1;
+    const double *src = A.r2 + (A.gathered ? A.kcap : 0);
+    auto R2of = [&](int slot) { return src[slot]; };
+    if ((size_t)K * RW * sizeof(double) > lds_bytes) {
+        for (int k0 = wid; k0 < K; k0 += nwb)  // wave-uniform
+            prune_row<D>(A.cand, R2of, A.plist, A.plen, A.plr2, A.plen_s, A.plr2_s, A.ls, A.D, K, k0);
+    } else {
+        double *st = reinterpret_cast<double *>(smem);
+        for (int idx = tid; idx < K * RW; idx += kFinThreads) {
+            const int r = idx / RW, f = idx - r * RW;
+            const double *e = A.cand + (int64_t)r * CS;
+            double v;
+            if (f < D)
+                v = e[f];
+            else if (f == D)
+                v = e[F + kFieldC] + e[F + kFieldLogn];
+            else if (f == D + 1)
+                v = e[F + kFieldC] + e[F + kFieldLogn1];
+            else if (f == D + 2)
+                v = e[F + kFieldIso];
+            else if (f == D + 3)
+                v = src[(int)e[F + kFieldSlot]];
+            else
+                v = e[F + kFieldSlot];
+            st[f * K + r] = v;
+        }
+        __syncthreads();
+        for (int k0 = wid; k0 < K; k0 += nwb) {  // wave-uniform: one row per wave
+            const int slot0 = (int)st[(D + 4) * K + k0];
+            const double R2 = st[(D + 3) * K + k0];
+            const double iso0 = st[(D + 2) * K + k0];
+            const double base0 = st[(D + 1) * K + k0];
+            const bool prunable = iso0 > 0.0 && R2 < 1e300 && base0 > -1e299;
+            const double R = sqrt(R2);
+            int count = 0;
+            for (int jb = 0; jb < K; jb += 64) {
+                const int j = jb + lane;
+                bool keep = j < K && j != k0;
+                if (keep && prunable) {
+                    const double isoj = st[(D + 2) * K + j];
+                    if (isoj > 0.0) {
+                        double dist2 = 0.0;
+#pragma unroll
+                        for (int a = 0; a < D; ++a) {
+                            const double dd = st[a * K + j] - st[a * K + k0];
+                            dist2 = fma(dd, dd, dist2);
+                        }
+                        const double delta = sqrt(dist2) - R;
+                        if (delta > 0.0) {
+                            const double wj = st[D * K + j];
+                            const double far = 0.5 * isoj * delta * delta, near = 0.5 * iso0 * R2;
+                            const double U = (wj - base0) - far + near;
+                            const double mag = fabs(wj) + fabs(base0) + far + near;
+                            keep = !(U <= -kSkip - 2.0 - 1e-9 * mag);
+                        }
+                    }
+                }
+                const uint64_t b = __ballot(keep);
+                if (keep) A.plist[(int64_t)k0 * A.ls + count + __popcll(b & ((1ull << lane) - 1ull))] = j;
+                count += __popcll(b);
+            }
+            if (lane == 0) {
+                const double r2l = prunable ? R2 : __longlong_as_double(0x7FF0000000000000ll);  // +inf: every row listed
+                A.plen[k0] = count;
+                A.plr2[k0] = r2l;
+                A.plen_s[slot0] = count;
+                A.plr2_s[slot0] = r2l;
+            }
+        }
+    }
+    __syncthreads();  // the radius buffers' bookkeeping after every read of src
+    if (A.gathered)
+        for (int s = tid; s < A.kcap; s += kFinThreads) A.r2[s] = A.r2[A.kcap + s];
+    if (A.clear_next)  // only the radii in use were read (not gathered)
+        for (int s = tid; s < A.kcap; s += kFinThreads) A.r2[A.kcap + s] = 0.0;
+}
+
+namespace {
+
+// The end of a synchronous step in one launch (DESIGN.md §5 "Fewer launches"): the lanes np8_assign_fast deferred
+// (np8_assign_queue's work, T.queue), the step's radius records folded into the gathered radii (np8_fold_r2,
+// T.fold), then -- in the one workgroup that finishes last (a release/acquire counter, no workgroup waits for
+// another) -- the request selection of a sharded step (np8_req_select, T.select) or np8_finalize (T.fin) followed
+// by the candidate lists (np8_prune, T.prune).  Each part does what its own kernel did, in the same order, so the
+// chain is unchanged; the separate kernels remain for the other step kinds.
+template <int D>
+__global__ __launch_bounds__(kFinThreads) void np8_step_tail(AssignArgs A, FinArgs F, PruneArgs P, TailArgs T) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    __shared__ int s_last;
+    const int lane = threadIdx.x & 63;
+    if (T.fold) {  // np8_fold_r2, one record per thread (both it and the queue's lanes only raise the radii)
+        unsigned long long *g = reinterpret_cast<unsigned long long *>(F.r2 + F.kcap);
+        const int64_t nf = (T.fold_n + 63) & ~63ll;  // whole waves (the shuffles below)
+        for (int64_t k = (int64_t)blockIdx.x * kFinThreads + threadIdx.x; k < nf; k += (int64_t)gridDim.x * kFinThreads) {
+            WaveR2 r;
+            r.slot = -1;
+            r.d2 = 0.0;
+            if (k < T.fold_n) r = A.wr2[k];
+            unsigned long long m = r.slot >= 0 ? (unsigned long long)__double_as_longlong(r.d2) : 0ull;
+            const int32_t s0 = __builtin_amdgcn_readfirstlane(r.slot);
+            if (__ballot(r.slot >= 0 && r.slot != s0) == 0ull) {  // the wave's records are one slot: one atomic
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) {
+                    const unsigned long long v = __shfl_xor(m, o);
+                    m = v > m ? v : m;
+                }
+                if (lane == 0 && s0 >= 0) atomicMax(g + s0, m);
+            } else if (r.slot >= 0) {
+                atomicMax(g + r.slot, m);
+            }
+        }
+    }
+    __syncthreads();  // this workgroup's records are folded
+    if (gridDim.x > 1) {  // the workgroup that finishes last runs the serial part
+        if (threadIdx.x == 0) {
+            __threadfence();  // release this workgroup's writes (labels, records, radii) at device scope
+            const unsigned prev = atomicAdd(&A.ctl->tail_done, 1u);
+            s_last = prev == gridDim.x - 1;
+            if (s_last) {
+                __threadfence();  // acquire the other workgroups' writes
+                A.ctl->tail_done = 0u;
+            }
+        }
+        __syncthreads();
+        if (!s_last) return;
+        __threadfence();
+    }
+    if (T.select) req_select_block(T.stage, T.stage_cap, T.rec, T.rec_cap, F.kcap, D, F.req_max, reinterpret_cast<int *>(smem));
+    if (T.fin) finalize_block(F, smem);
+    if (T.prune) prune_block<D>(P, smem, T.lds_bytes);
+}
+
+}  // namespace
 
 // The wide path's new slots under the reference prior: (v, mu) of each accepted request from the item frame
 // its rank recorded, then the slot (what np8_finalize did in place before: 2.7 KB of scratch per lane there).
@@ -2052,6 +2231,30 @@ size_t np8_finalize_lds_bytes(int kcap) {
 
 hipError_t np8_launch_finalize(const FinArgs &F, hipStream_t s) {
     hipLaunchKernelGGL(np8_finalize, dim3(1), dim3(kFinThreads), np8_finalize_lds_bytes(F.kcap), s, F);
+    return hipGetLastError();
+}
+
+hipError_t np8_launch_step_tail(const AssignArgs &A, const FinArgs &F, const PruneArgs &P, const TailArgs &T0,
+                                int64_t n_waves, int D, int M, hipStream_t s) {
+    (void)n_waves;
+    (void)M;
+    // the fold reads one record per thread; otherwise one workgroup
+    constexpr int64_t kTailBlocks = 256;
+    int64_t nb = T0.fold ? (T0.fold_n + kFinThreads - 1) / kFinThreads : 1;
+    nb = nb < 1 ? 1 : (nb > kTailBlocks ? kTailBlocks : nb);
+    TailArgs T = T0;
+    T.lds_bytes = (int64_t)np8_finalize_lds_bytes(F.kcap);
+    const size_t lds = (size_t)T.lds_bytes;
+    switch (D) {
+#define Y(d)                                                                                              \
+    case d:                                                                                               \
+        hipLaunchKernelGGL((np8_step_tail<d>), dim3((unsigned)nb), dim3(kFinThreads), lds, s, A, F, P, T); \
+        break;
+        Y(1) Y(2) Y(3) Y(4) Y(5) Y(6) Y(7) Y(8) Y(9) Y(10) Y(11) Y(12) Y(13) Y(14) Y(15) Y(16)
+#undef Y
+        default:
+            return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 

@@ -30,14 +30,21 @@ per_kernel = defaultdict(dict)
 for (k, c), v in agg.items():
     per_kernel[k][c] = {"launches": len(v), "mean": sum(v) / len(v)}
 out = {"source": src, "counters": per_kernel}
-assign = [k for k in per_kernel if "np8_assign" in k]
-assign.sort(key=lambda k: -per_kernel[k].get("SQ_WAVES", {}).get("launches", 0))
+# the assign step: np8_assign_fast + np8_assign_queue (C3, launched once each per step), np8_assign_wide (C5) or
+# np8_assign; counting instances (template flag true) run outside the timed sweeps and are left out
+assign = [k for k in per_kernel if "np8_assign" in k and "true>" not in k and "matrix" not in k]
+assign.sort(key=lambda k: -per_kernel[k].get("SQ_WAVES", per_kernel[k].get("FETCH_SIZE", {})).get("launches", 0))
 if assign:
     a = per_kernel[assign[0]]
-    fetch = a.get("FETCH_SIZE", {}).get("mean")
-    write = a.get("WRITE_SIZE", {}).get("mean", 0.0)
-    if fetch is not None:
+    nl = a.get("FETCH_SIZE", {}).get("launches")
+    step = [k for k in assign if per_kernel[k].get("FETCH_SIZE", {}).get("launches") == nl]
+    out["assign_step_kernels"] = step
+    fetch = sum(per_kernel[k].get("FETCH_SIZE", {}).get("mean", 0.0) for k in step)
+    write = sum(per_kernel[k].get("WRITE_SIZE", {}).get("mean", 0.0) for k in step)
+    if nl:
         out["assign_bytes_per_launch"] = (2.0 * fetch + write) * 1024.0
+        out["assign_fetch_bytes_per_launch"] = 2.0 * fetch * 1024.0
+        out["assign_write_bytes_per_launch"] = write * 1024.0
     if "SQ_INSTS_VALU" in a and "SQ_WAVES" in a:
         # SQ_INSTS_VALU counts wave-instructions; one item per lane, so this is also the VALU instruction
         # count of one item's lane
@@ -47,6 +54,8 @@ if assign:
         # waves in quad-cycles; GRBM_GUI_ACTIVE is summed over the 8 XCDs; 1024 SIMDs
         cyc = a["GRBM_GUI_ACTIVE"]["mean"] / 8.0
         out["assign_valu_issue_frac"] = 4.0 * a["SQ_ACTIVE_INST_VALU"]["mean"] / (1024.0 * cyc)
+    if "SQ_WAIT_ANY" in a and "SQ_WAVE_CYCLES" in a:
+        out["assign_wait_any_frac"] = a["SQ_WAIT_ANY"]["mean"] / a["SQ_WAVE_CYCLES"]["mean"]
 try:
     commit = subprocess.run(["git", "-C", ROOT, "rev-parse", "--short", "HEAD"], capture_output=True,
                             text=True).stdout.strip()
