@@ -349,6 +349,14 @@ def measure(smp, sweeps, steps, warmup, graphs, dist, torch, n_loc, D, wide, S, 
             "aux_exact_wave_frac": (sc1["aux_exact_waves"] - sc0["aux_exact_waves"]) / cnt_sweeps
             / max(((n_loc + 63) // 64) * smp.M, 1),
             "aux_screen_violations": sc1["screen_violations"] - sc0["screen_violations"],
+            # how the candidate walk went (DESIGN.md 4 "Candidate pruning"): lanes on the whole table, waves
+            # that paid the table loop for at least one lane, waves of more own rows than the list walk takes
+            "full_walk_lane_frac": (sc1["full_walk_lanes"] - sc0["full_walk_lanes"]) / cnt_sweeps / max(n_loc, 1),
+            "full_walk_wave_frac": (sc1["full_walk_waves"] - sc0["full_walk_waves"]) / cnt_sweeps
+            / max((n_loc + 63) // 64, 1),
+            "many_group_wave_frac": (sc1["many_group_waves"] - sc0["many_group_waves"]) / cnt_sweeps
+            / max((n_loc + 63) // 64, 1),
+            "list_entries_per_item": (sc1["list_entries"] - sc0["list_entries"]) / cnt_sweeps / max(n_loc, 1),
             "iso_fraction": nq_iso / max(nq, 1),
             "tflops": exec_flops / (ms_assign * 1e-3) / 1e12 if ms_assign > 0 else None,
             "frac_of_peak": exec_flops / (ms_assign * 1e-3) / 1e12 / peak if ms_assign > 0 else None,

@@ -132,6 +132,11 @@ typedef struct {
     /* NP8_TIMING_COUNTERS: (item, auxiliary) pairs the screen did not skip (the exact fp64 draw ran), and
      * (wave, auxiliary) pairs where at least one of the wave's 64 items needed it */
     int64_t aux_exact_lanes, aux_exact_waves;
+    /* NP8_TIMING_COUNTERS, how the candidate walk went: lanes that walked the whole table (no usable list, or
+     * outside the radius their list was built for) and waves with at least one such lane (the whole wave
+     * pays the table loop); waves of more own rows than the list walk takes (a stale layout); list entries
+     * walked by lanes */
+    int64_t full_walk_lanes, full_walk_waves, many_group_waves, list_entries;
 } np8_stats_t;
 
 /* Create / destroy.  Replaces NealAlgorithm8::NealAlgorithm8 (np_neal_algorithm8.cpp:17-34). */

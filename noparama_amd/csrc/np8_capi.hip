@@ -1393,7 +1393,7 @@ int np8_create(np8_ctx **out, const np8_config *cfg) {
         (r = dalloc(c, &c->dense_of, (size_t)kc)) || (r = dalloc(c, &c->slot_iso, (size_t)kc)) ||
         (r = dalloc(c, &c->slot_logn1, (size_t)kc)) || (r = dalloc(c, &c->plen_s, (size_t)kc)) ||
         (r = dalloc(c, &c->plr2_s, (size_t)kc)) ||
-        (r = dalloc(c, &c->rec, (size_t)c->rec_bytes)) || (r = dalloc(c, &c->evalc, (size_t)4 * kEvalSlots)) ||
+        (r = dalloc(c, &c->rec, (size_t)c->rec_bytes)) || (r = dalloc(c, &c->evalc, (size_t)8 * kEvalSlots)) ||
         (c->param_update != NP8_PARAM_FROZEN && (r = dalloc(c, &c->acc, (size_t)kc * (D + DP)))) ||
         (kc <= kPruneMaxKcap && ((r = dalloc(c, &c->r2, 2 * (size_t)kc)) || (r = dalloc(c, &c->plen, (size_t)kc)) ||
                                 (r = dalloc(c, &c->plr2, (size_t)kc)) ||
@@ -2159,13 +2159,17 @@ int np8_stats(np8_ctx *c, np8_stats_t *out) {
     out->mh_accepted = h.mh_accepted;
     out->screen_violations = (int64_t)h.n_screen_viol;
     {
-        std::vector<unsigned long long> ev((size_t)4 * kEvalSlots);
+        std::vector<unsigned long long> ev((size_t)8 * kEvalSlots);
         HIPC(c, hipMemcpy(ev.data(), c->evalc, sizeof(unsigned long long) * ev.size(), hipMemcpyDeviceToHost));
         for (int k = 0; k < kEvalSlots; ++k) {
             out->n_quad += (int64_t)ev[2 * k];
             out->n_quad_iso += (int64_t)ev[2 * k + 1];
             out->aux_exact_lanes += (int64_t)ev[2 * kEvalSlots + 2 * k];
             out->aux_exact_waves += (int64_t)ev[2 * kEvalSlots + 2 * k + 1];
+            out->full_walk_lanes += (int64_t)ev[4 * kEvalSlots + 2 * k];
+            out->full_walk_waves += (int64_t)ev[4 * kEvalSlots + 2 * k + 1];
+            out->many_group_waves += (int64_t)ev[6 * kEvalSlots + 2 * k];
+            out->list_entries += (int64_t)ev[6 * kEvalSlots + 2 * k + 1];
         }
     }
     return NP8_OK;

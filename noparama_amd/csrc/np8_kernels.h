@@ -41,7 +41,8 @@ struct Ctl {
 
 // Executed work of np8_assign when AssignArgs::count_eval is set (timing mode): per wave, the cluster
 // quadratic forms its items evaluated (own rows included) and how many took the isotropic form, added
-// to counter pair (wave id mod kEvalSlots) -- spread over many addresses: one counter pair for every wave
+// to counter pair (wave id mod kEvalSlots); regions 1-3 of evalc: exact auxiliaries (lanes, waves), full-table
+// walks (lanes, waves), many-row waves and list entries walked -- spread over many addresses: one counter pair for every wave
 // of the grid serialises the atomics in one L2 channel (4x the kernel time at C3).
 constexpr int kEvalSlots = 1024;
 
@@ -209,6 +210,52 @@ struct FinArgs {
     const double *hyp;
     int32_t *wdirty;
 };
+
+// Wave-aggregated atomics on a few hot addresses (count deltas, gathered radii): one atomic per distinct key
+// among the wave's `on` lanes instead of one per lane.  Same-address device-scope atomics serialise at the
+// memory side across the XCDs; in the regime the reference's start reaches (duplicate clusters, ~30% of the
+// items moving per sweep) per-lane atomics on ~140 counters cost the assign kernel more than its arithmetic.
+// Every active lane of the wave must call (ballots over the active lanes).
+__device__ __forceinline__ void wave_add_by_key(int32_t *base, int32_t key, int32_t v, bool on) {
+    const int lane = threadIdx.x & 63;
+    uint64_t pend = __ballot(on);
+    while (pend) {
+        const int l = __ffsll((unsigned long long)pend) - 1;
+        const int32_t k = __builtin_amdgcn_readlane(key, l);
+        const uint64_t m = __ballot(on && key == k);
+        if (lane == l) atomicAdd(base + k, v * (int32_t)__popcll(m));
+        pend &= ~m;
+    }
+}
+
+// A slot of a shared append area for each lane with `on` (one atomicAdd per wave); -1 for the others.
+__device__ __forceinline__ int wave_append(int32_t *count, bool on) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t m = __ballot(on);
+    if (m == 0ull) return -1;
+    const int l = __ffsll((unsigned long long)m) - 1;
+    int base = 0;
+    if (lane == l) base = atomicAdd(count, (int32_t)__popcll(m));
+    base = __shfl(base, l);
+    return on ? base + (int)__popcll(m & ((1ull << lane) - 1ull)) : -1;
+}
+
+// max of non-negative doubles (as their bit patterns) per distinct key, one atomicMax per key
+__device__ __forceinline__ void wave_max_by_key(unsigned long long *base, int32_t key, double v, bool on) {
+    const int lane = threadIdx.x & 63;
+    uint64_t pend = __ballot(on);
+    while (pend) {
+        const int l = __ffsll((unsigned long long)pend) - 1;
+        const int32_t k = __builtin_amdgcn_readlane(key, l);
+        const bool in = on && key == k;
+        const uint64_t m = __ballot(in);
+        double r = in ? v : 0.0;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) r = fmax(r, __shfl_xor(r, o));
+        if (lane == l) atomicMax(base + k, (unsigned long long)__double_as_longlong(r));
+        pend &= ~m;
+    }
+}
 
 // Auxiliary draw m of (item i, epoch t) -> a slot: the G0 draw of normalinvwishart.h:44-64 in the
 // factored form (DESIGN.md "G0").

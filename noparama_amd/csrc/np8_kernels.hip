@@ -303,7 +303,7 @@ __device__ __forceinline__ void assign_item(const AssignArgs &A, const int64_t p
     // left out are those every such lane's pick_step skips anyway, and the order is ascending as in the
     // full walk.  Lists hold for every item of the row, whatever its wave (np8_prune: the radius covers
     // each item the last sweep left in the row).
-    int32_t nq_lane = 0, niso_lane = 0;  // COUNT: quadratic forms this lane evaluated
+    int32_t nq_lane = 0, niso_lane = 0, nlist_lane = 0;  // COUNT: quadratic forms this lane evaluated, list entries
     int32_t pslot = zi;                  // slot of the picked row (no reload of the row at the end)
     // (a wave of many own rows -- a stale layout, a cold start -- walks the table once instead)
     int ngroups = 0;
@@ -342,11 +342,28 @@ __device__ __forceinline__ void assign_item(const AssignArgs &A, const int64_t p
                         pslot = (st.pick == j) ? (int32_t)e[F + kFieldSlot] : pslot;
                         if constexpr (COUNT) {
                             nq_lane += 1;
+                            nlist_lane += 1;
                             niso_lane += (e[F + kFieldIso] > 0.0) ? 1 : 0;
                         }
                     }
                 }
             }
+        }
+    }
+    if constexpr (COUNT) {  // how the walk went (lanes on the whole table, waves paying the table loop)
+        const uint64_t fb = __ballot(full);
+        const int64_t nl_w = [&] {
+            int64_t t = 0;
+            for (uint64_t act = __ballot(1); act; act &= act - 1ull) t += __builtin_amdgcn_readlane(nlist_lane, __ffsll((unsigned long long)act) - 1);
+            return t;
+        }();
+        if ((threadIdx.x & 63) == (__ffsll((unsigned long long)__ballot(1)) - 1)) {
+            const int64_t w = (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) % kEvalSlots;
+            unsigned long long *ec = A.evalc + 4 * kEvalSlots + 2 * w;
+            atomicAdd(ec, (unsigned long long)__popcll(fb));
+            atomicAdd(ec + 1, fb ? 1ull : 0ull);
+            atomicAdd(ec + 2 * kEvalSlots, (ngroups > kMaxListGroups) ? 1ull : 0ull);
+            atomicAdd(ec + 2 * kEvalSlots + 1, (unsigned long long)nl_w);
         }
     }
     if (full) {  // wave-uniform row loop (scalar loads) over the lanes that need it
@@ -496,7 +513,7 @@ __device__ __forceinline__ void assign_item(const AssignArgs &A, const int64_t p
 #pragma unroll
             for (int o = 32; o > 0; o >>= 1) d2 = fmax(d2, __shfl_xor(d2, o));
         } else {
-            atomicMax(reinterpret_cast<unsigned long long *>(A.r2 + A.kcap + ts), (unsigned long long)__double_as_longlong(d2));
+            wave_max_by_key(reinterpret_cast<unsigned long long *>(A.r2 + A.kcap), ts, d2, true);
         }
         if (!A.queue && (threadIdx.x & 63) == (__ffsll((unsigned long long)__ballot(1)) - 1)) {  // the wave's record
             WaveR2 w;
@@ -513,11 +530,13 @@ __device__ __forceinline__ void assign_item(const AssignArgs &A, const int64_t p
 #endif
     if (mv && (threadIdx.x & 63) == (__ffsll((unsigned long long)__ballot(1)) - 1))
         atomicAdd(reinterpret_cast<unsigned long long *>(&A.ctl->moved), (unsigned long long)__popcll(mv));
+    const bool mover = st.pick < K && snew != zi;
+    wave_add_by_key(delta, zi, -1, mover);
+    wave_add_by_key(delta, snew, 1, mover);
+    const int qreq = wave_append(A.nreq, st.pick >= K);  // (requests are accepted by scan position, not arrival)
     if (st.pick < K) {
         const int32_t s = snew;
         if (s != zi) {
-            atomicSub(delta + zi, 1);
-            atomicAdd(delta + s, 1);
             // the item's addresses again (a rare path): two 64-bit addresses kept live through the draw were
             // spilled to scratch for every item (19 of the 38 MB the C3 launch wrote)
             int64_t pq = A.queue ? qslot : (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -528,7 +547,7 @@ __device__ __forceinline__ void assign_item(const AssignArgs &A, const int64_t p
             if (sorted) zs[pq] = s;
         }
     } else {
-        const int q = atomicAdd(A.nreq, 1);
+        const int q = qreq;
         if (q < A.req_cap) {  // always: the area holds every item of the step
             Request r;
             r.pos = sorted ? (int64_t)ig : A.offset + p;  // synchronous sweep: scan position = item index
@@ -596,6 +615,13 @@ extern "C" int np8_exp_clocks(unsigned long long *out, int64_t n) {
 #endif
 
 // ---- the data-parallel sweep's fast path -------------------------------------------------------------
+// lane l's double (l wave-uniform), as two readlanes: an SGPR pair for the rest of the wave
+__device__ __forceinline__ double readlane_d(double v, int l) {
+    const int64_t b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)(b & 0xFFFFFFFFll), l), hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+    return __longlong_as_double(((int64_t)hi << 32) | (uint32_t)lo);
+}
+
 // np8_assign_fast<D,M>: the common case of np8_assign -- the reference prior with an isotropic Lambda (every
 // G0 draw, and so every row, isotropic; the base measure's whitening diagonal), the label-sorted layout --
 // with only the work almost every lane needs: the own row, the candidate list (or the table), the two
@@ -675,41 +701,74 @@ __global__ __launch_bounds__(NP8_ASSIGN_BLOCK) __attribute__((amdgpu_waves_per_e
     for (uint64_t pend = __ballot(1); pend && ngroups <= kMaxListGroups; ++ngroups)
         pend &= ~__ballot(jo == __builtin_amdgcn_readlane(jo, __ffsll((unsigned long long)pend) - 1));
     bool full = !defer;  // this lane walks the whole table
-    // one candidate row (wave-uniform): the isotropic likelihood, or the wave's lanes deferred
-    auto visit = [&](int j, bool own_skip) {
-        const double *e = cand + (int64_t)j * CS;
-        const double iso = e[F + kFieldIso];
-        if (!(iso > 0.0)) {
-            defer = true;
-            return;
-        }
-        double s2 = (x[0] - e[0]) * (x[0] - e[0]);
+    // rows row_of(0 .. n-1) (wave-uniform), for the lanes with `mine`: a wave's worth of rows per round of loads
+    // (lane q: row q's fields, the wave's active lanes are 0 .. nact - 1 -- the last wave of the range is
+    // partial), then broadcast row by row: no dependent load per row (the mixed regime walks ~9 rows per item,
+    // a stale wave the whole table).  A row that is not isotropic defers the lane (np8_assign takes it).
+    auto walk = [&](auto row_of, int n, bool mine, bool own_skip) {
+        const int nact = __popcll(__ballot(1));
+        for (int qb = 0; qb < n; qb += nact) {
+            const int q = qb + lane;
+            int32_t jq = 0;
+            double fm[D], fiso = 0.0, fc = 0.0, fl = 0.0, fsl = 0.0;
 #pragma unroll
-        for (int a = 1; a < D; ++a) s2 = fma(x[a] - e[a], x[a] - e[a], s2);
-        const double lw = fma(-0.5, s2 * iso, e[F + kFieldC]) + e[F + kFieldLogn];
-        if (own_skip && e[F + kFieldSlot] == zslot) return;
-        ensure_u(st, lw, A.seed, ig, t);
-        pick_step(st, lw, j);
-        pslot = (st.pick == j) ? (int32_t)e[F + kFieldSlot] : pslot;
-    };
-    if (!defer && A.use_lists && A.ctl->lists_ok && ngroups <= kMaxListGroups) {
-        uint64_t pend = __ballot(1);
-        while (pend) {
-            const int32_t j0 = __builtin_amdgcn_readlane(jo, __ffsll((unsigned long long)pend) - 1);
-            pend &= ~__ballot(jo == j0);
-            if (jo == j0 && !defer) {
-                full = !(d2own <= r2list);
-                if (!full) {
-                    const int32_t *__restrict__ lst = A.plist + (int64_t)j0 * A.ls;
-                    for (int q = 0; q < nlist && !defer; ++q) visit(lst[q], false);
+            for (int a = 0; a < D; ++a) fm[a] = 0.0;
+            if (q < n) {
+                jq = row_of(q);
+                const double *e = cand + (int64_t)jq * CS;
+#pragma unroll
+                for (int a = 0; a < D; ++a) fm[a] = e[a];
+                fiso = e[F + kFieldIso];
+                fc = e[F + kFieldC];
+                fl = e[F + kFieldLogn];
+                fsl = e[F + kFieldSlot];
+            }
+            const int nb = min(nact, n - qb);
+            for (int k = 0; k < nb; ++k) {  // wave-uniform: the rows in order (ascending)
+                const double iso = readlane_d(fiso, k);
+                if (mine && !defer) {
+                    if (!(iso > 0.0)) {
+                        defer = true;
+                    } else {
+                        const double m0 = readlane_d(fm[0], k);
+                        double s2 = (x[0] - m0) * (x[0] - m0);
+#pragma unroll
+                        for (int a = 1; a < D; ++a) {
+                            const double ma = readlane_d(fm[a], k);
+                            s2 = fma(x[a] - ma, x[a] - ma, s2);
+                        }
+                        const double lw = fma(-0.5, s2 * iso, readlane_d(fc, k)) + readlane_d(fl, k);
+                        const double sl = readlane_d(fsl, k);
+                        if (!(own_skip && sl == zslot)) {
+                            const int j = __builtin_amdgcn_readlane(jq, k);
+                            ensure_u(st, lw, A.seed, ig, t);
+                            pick_step(st, lw, j);
+                            pslot = (st.pick == j) ? (int32_t)sl : pslot;
+                        }
+                    }
                 }
             }
         }
+    };
+    if (A.use_lists && A.ctl->lists_ok && ngroups <= kMaxListGroups) {  // wave-uniform
+        uint64_t pend = __ballot(1);
+        while (pend) {
+            const int lead = __ffsll((unsigned long long)pend) - 1;
+            const int32_t j0 = __builtin_amdgcn_readlane(jo, lead);
+            const int32_t nl0 = __builtin_amdgcn_readlane(nlist, lead);
+            const bool grp = jo == j0;
+            pend &= ~__ballot(grp);
+            bool mine = false;  // this lane walks the group's list
+            if (grp && !defer) {
+                full = !(d2own <= r2list);
+                mine = !full;
+            }
+            if (__ballot(mine) == 0ull) continue;
+            walk([&](int q) { return A.plist[(int64_t)j0 * A.ls + q]; }, nl0, mine, false);
+        }
     }
-    if (__ballot(full && !defer)) {  // wave-uniform row loop over the lanes that need it
-        for (int j = 0; j < K; ++j)
-            if (full && !defer) visit(j, true);
-    }
+    if (__ballot(full && !defer))  // wave-uniform row loop over the lanes that need it
+        walk([](int q) { return q; }, K, full && !defer, true);
     NP8_CLK(3);
     // the auxiliaries: np8_assign's two-level screen, then the exact fp64 draw for the lanes it cannot clear;
     // a lane that picks an auxiliary makes a new-cluster request (appended below)
@@ -798,8 +857,8 @@ __global__ __launch_bounds__(NP8_ASSIGN_BLOCK) __attribute__((amdgpu_waves_per_e
             d2 = defer ? 0.0 : d2;
 #pragma unroll
             for (int o = 32; o > 0; o >>= 1) d2 = fmax(d2, __shfl_xor(d2, o));
-        } else if (!defer) {
-            atomicMax(reinterpret_cast<unsigned long long *>(A.r2 + A.kcap + snew), (unsigned long long)__double_as_longlong(d2));
+        } else {
+            wave_max_by_key(reinterpret_cast<unsigned long long *>(A.r2 + A.kcap), snew, d2, !defer);
         }
         if (lane == (__ffsll((unsigned long long)__ballot(1)) - 1)) {  // the wave's record
             WaveR2 wr;
@@ -812,15 +871,19 @@ __global__ __launch_bounds__(NP8_ASSIGN_BLOCK) __attribute__((amdgpu_waves_per_e
     const uint64_t mv = __ballot(!defer && snew != zi);
     if (mv && lane == (__ffsll((unsigned long long)__ballot(1)) - 1))
         atomicAdd(reinterpret_cast<unsigned long long *>(&A.ctl->moved), (unsigned long long)__popcll(mv));
-    if (!defer && snew != zi) {
+    {
         int32_t *delta = reinterpret_cast<int32_t *>(A.rec + kRecHeaderBytes);
-        atomicSub(delta + zi, 1);
-        atomicAdd(delta + snew, 1);
+        const bool mover = !defer && snew != zi;
+        wave_add_by_key(delta, zi, -1, mover);
+        wave_add_by_key(delta, snew, 1, mover);
+    }
+    if (!defer && snew != zi) {
         A.z[il] = snew;
         zs[p] = snew;
     }
+    const int qreq = wave_append(A.nreq, req);  // (requests are accepted by scan position, not arrival)
     if (req) {  // np8_assign's request with its payload, the auxiliary's (v, mu)
-        const int q = atomicAdd(A.nreq, 1);
+        const int q = qreq;
         if (q < A.req_cap) {  // always: the area holds every item of the step
             Request r;
             r.pos = (int64_t)ig;  // synchronous sweep: scan position = item index

@@ -542,15 +542,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NP8_WIDE_WA
     const uint64_t mv = __ballot(snew != zi);
     if (mv && lane == (__ffsll((unsigned long long)__ballot(1)) - 1))
         atomicAdd(reinterpret_cast<unsigned long long *>(&A.ctl->moved), (unsigned long long)__popcll(mv));
+    const bool mover = st.pick < K && snew != zi;
+    wave_add_by_key(delta, zi, -1, mover);
+    wave_add_by_key(delta, snew, 1, mover);
+    const int qreq = wave_append(A.nreq, st.pick >= K);  // (requests are accepted by scan position, not arrival)
     if (st.pick < K) {
         if (snew != zi) {
-            atomicSub(delta + zi, 1);
-            atomicAdd(delta + snew, 1);
             A.z[il] = snew;
             if (sorted) zs[pc] = snew;
         }
     } else {
-        const int q = atomicAdd(A.nreq, 1);
+        const int q = qreq;
         if (q < A.req_cap) {  // always: the area holds every item of the step
             Request r;
             r.pos = sorted ? (int64_t)ig : A.offset + p;

@@ -106,6 +106,10 @@ class Stats(C.Structure):
         ("screen_violations", C.c_int64),
         ("aux_exact_lanes", C.c_int64),
         ("aux_exact_waves", C.c_int64),
+        ("full_walk_lanes", C.c_int64),
+        ("full_walk_waves", C.c_int64),
+        ("many_group_waves", C.c_int64),
+        ("list_entries", C.c_int64),
     ]
 
 

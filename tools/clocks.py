@@ -15,11 +15,16 @@ from noparama_amd import NealAlgorithm8, datasets  # noqa: E402
 from noparama_amd import np8 as _np8  # noqa: E402
 
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000
+mode = sys.argv[2] if len(sys.argv) > 2 else "warm"  # warm: the C3 state; mixed: sweep 60 after init_random(20)
 X, z, mu, sig = datasets.config_c3(N=N)
 s = NealAlgorithm8(8, seed=20261015, device=0)
 s.set_data(X)
-s.set_state(z, mu, sig)
-s.sweep(25)
+if mode == "mixed":
+    s.init_random(20)
+    s.sweep(61)
+else:
+    s.set_state(z, mu, sig)
+    s.sweep(25)
 nw = (N + 63) // 64
 buf = np.zeros(nw * 8, dtype=np.uint64)
 lib = _np8.lib()
@@ -32,7 +37,7 @@ T = T[ok]
 t0 = T[:, 0].min()
 ph = np.diff(T, axis=1)
 names = ["loads x/zs/ids", "own row", "lists/table", "ny + screen L1", "aux L2/exact", "pick end/writes"]
-out = {"N": N, "waves": int(ok.sum()), "launch_span_us": (T[:, 6].max() - t0) / 1e3,
+out = {"N": N, "mode": mode, "K": s.K, "waves": int(ok.sum()), "launch_span_us": (T[:, 6].max() - t0) / 1e3,
        "wave_latency_us_mean": float((T[:, 6] - T[:, 0]).mean() / 1e3),
        "phase_us_mean": {n: float(ph[:, k].mean() / 1e3) for k, n in enumerate(names)},
        "phase_us_p90": {n: float(np.percentile(ph[:, k], 90) / 1e3) for k, n in enumerate(names)},
