@@ -363,6 +363,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NP8_WIDE_WA
 
     // the item's frame for the auxiliaries: only |U^T (x - mu0)| is needed
     double rown = 0.0;  // |x - muf_own|
+    double x2 = 0.0;    // |x|^2 (the exact distance screen)
     double ny;
     if constexpr (DIAGU) {
         const double *U = hyp + D;
@@ -375,6 +376,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NP8_WIDE_WA
             n2 = fma(y, y, n2);
             const double dd = (double)xa - (double)mo[a];
             d2 = fma(dd, dd, d2);
+            x2 = fma((double)xa, (double)xa, x2);
         }
         ny = sqrt(n2);
         if (A.wdist) rown = sqrt(d2);
@@ -383,6 +385,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NP8_WIDE_WA
 #pragma unroll
         for (int a = 0; a < D; ++a) xf[a] = X[(int64_t)a * n + xr];
         ny = wide_whiten_norm<D>(hyp, xf);
+#pragma unroll
+        for (int a = 0; a < D; ++a) x2 = fma((double)xf[a], (double)xf[a], x2);
         if (A.wdist) {  // the item's distance to its own row's fp32 mean (candidate pruning)
             const float *mo = A.wmu + (int64_t)zi * D;
             double d2 = 0.0;
@@ -454,10 +458,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NP8_WIDE_WA
     // (and a relative margin) for every lane is one its pick_step would skip -- results unchanged.
     // kMaskWords: up to 64 * 8 = 512 rows (kcap of the wide path).
     constexpr int kMaskWords = 8;
-    __shared__ unsigned long long rmask[kMaskWords];
+    __shared__ unsigned long long rmask[kMaskWords], rmask2[kMaskWords];
     const bool prune = A.wdist != nullptr && K <= 64 * kMaskWords;
     if (prune) {
-        if (threadIdx.x < kMaskWords) rmask[threadIdx.x] = 0ull;
+        if (threadIdx.x < kMaskWords) rmask[threadIdx.x] = rmask2[threadIdx.x] = 0ull;
         __syncthreads();
         // per distinct own row of the wave (one in the label-sorted layout): the group's largest radius and
         // smallest running maximum bound every lane of the group at once (U grows with |x - mu_own| and falls
@@ -495,16 +499,108 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NP8_WIDE_WA
         }
         __syncthreads();
     }
-    // the next row to evaluate at or after j (block-uniform)
-    auto next_row = [&](int j) -> int {
-        if (!prune) return j;
+    // the next row at or after j in mask m (block-uniform)
+    auto next_in = [&](const unsigned long long *m, int j) -> int {
         while (j < K) {
-            const unsigned long long w = rmask[j >> 6] >> (j & 63);
+            const unsigned long long w = m[j >> 6] >> (j & 63);
             if (w) return j + __ffsll(w) - 1;
             j = (j | 63) + 1;
         }
         return K;
     };
+    // The exact-distance screen of the rows the mask kept (DESIGN.md §5 "Wide-path pruning"): per item and row,
+    // lw_j(x) <= c_j + log n_j - lam_j |x - muf_j|^2 / 2 with the distance itself, |x|^2 + |muf_j|^2 - 2 x.muf_j,
+    // the dot products of 16 rows and the wave's 64 items on the matrix cores (D/4 MFMAs per item tile and 16
+    // rows, against 2.5 D^2/16... for a contraction), lowered by a rigorous margin for their fp32 rounding
+    // (|error| <= 64 u sum |x_a mu_a| <= 4e-6 (|x|^2 + |muf|^2)); the triangle inequality of the mask loses
+    // most of it at D = 64 (x - mu_own is nearly orthogonal to mu_j - mu_own).  A row survives when a lane of
+    // the block may not skip it; results are unchanged.
+    if (prune) {
+        if (wave_live) {
+            using W2 = Wide<D>;
+            const double Tl = valid ? st.T : 1e300;
+            double Ti[4], x2i[4];
+            int32_t zit[4];
+#pragma unroll
+            for (int nt = 0; nt < 4; ++nt) {
+                Ti[nt] = __shfl(Tl, 16 * nt + col);
+                x2i[nt] = __shfl(x2, 16 * nt + col);
+                zit[nt] = __shfl(zi, 16 * nt + col);
+            }
+            int j = next_in(rmask, 0);
+            while (j < K) {  // block-uniform: 16 kept rows at a time
+                int myrow = K, orow[4] = {K, K, K, K};
+                int jj = j;
+#pragma unroll 1
+                for (int c = 0; c < 16; ++c) {
+                    myrow = (col == c) ? jj : myrow;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) orow[r] = (4 * g + r == c) ? jj : orow[r];
+                    if (jj < K) jj = next_in(rmask, jj + 1);
+                }
+                j = jj;
+                // A operand: lane (g, col) holds muf[4 s + g] of row myrow (the transposed mean of its fragment row)
+                float am[W2::S];
+                double m2p = 0.0;
+                if (myrow < K) {
+                    const int sj = (int)cand[(int64_t)myrow * CS + F + kFieldSlot];
+                    const float *mt = A.wfrag + (int64_t)sj * W2::ROW + W2::NCH * 256 + g * W2::S;
+#pragma unroll
+                    for (int s = 0; s < W2::S; ++s) {
+                        am[s] = mt[s];
+                        m2p = fma((double)am[s], (double)am[s], m2p);
+                    }
+                } else {
+#pragma unroll
+                    for (int s = 0; s < W2::S; ++s) am[s] = 0.0f;
+                }
+                double m2 = m2p + __shfl_xor(m2p, 16);
+                m2 += __shfl_xor(m2, 32);  // |muf|^2 of row myrow, on the four lanes of column col
+                typedef float f32x4 __attribute__((ext_vector_type(4)));
+                f32x4 acc[4];
+#pragma unroll
+                for (int nt = 0; nt < 4; ++nt) acc[nt] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+                for (int s = 0; s < W2::S; ++s)
+#pragma unroll
+                    for (int nt = 0; nt < 4; ++nt) acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(am[s], xb[nt][s], acc[nt], 0, 0, 0);
+                // output (nt, r) of lane (g, col): row orow[r] (= 4 g + r of the 16), item 16 nt + col
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int jr = orow[r];
+                    const double m2r = __shfl(m2, 4 * g + r);
+                    bool nr = false;
+                    if (jr < K) {
+                        const double *e = cand + (int64_t)jr * CS;
+                        const int32_t sjr = (int32_t)e[F + kFieldSlot];
+                        const double base = e[F + kFieldC] + e[F + kFieldLogn];
+                        const double lam = A.lam_lo[sjr];
+#pragma unroll
+                        for (int nt = 0; nt < 4; ++nt) {
+                            if (sjr != zit[nt] && Ti[nt] < 1e299) {
+                                const double sq = x2i[nt] + m2r;
+                                const double d2 = fmax(fma(-2.0, (double)acc[nt][r], sq) - 1e-5 * sq, 0.0);
+                                const double far = 0.5 * lam * d2;
+                                const double U = base - far - Ti[nt];
+                                nr = nr || !(U <= -kSkip - 2.0 - 1e-9 * (fabs(base) + fabs(Ti[nt]) + far));
+                            }
+                        }
+                    }
+                    const uint64_t b = __ballot(nr);
+                    // rows 4 g' + r: lanes 16 g' .. 16 g' + 15
+#pragma unroll
+                    for (int gg = 0; gg < 4; ++gg) {
+                        const int row = __builtin_amdgcn_readlane(jr, 16 * gg);
+                        if (lane == 0 && ((b >> (16 * gg)) & 0xFFFFull) != 0ull && row < K)
+                            atomicOr(&rmask2[row >> 6], 1ull << (row & 63));
+                    }
+                }
+            }
+        }
+        __syncthreads();
+    }
+    // the next row to evaluate at or after j (block-uniform)
+    auto next_row = [&](int j) -> int { return prune ? next_in(rmask2, j) : j; };
 
     // the evaluated candidates in ascending order, block-uniform: the next one is copied into the other
     // stage while the MFMAs of this one run; one barrier per row
