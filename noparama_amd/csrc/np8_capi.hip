@@ -175,6 +175,8 @@ struct np8_ctx {
     int32_t sm_batch = 1024;
     int32_t sm_K = 0;
     bool sm_all_iso = false;
+    double *sm_mb = nullptr;  // triadic merge bound: [kcap][4] member sums per live row (np8_tri_bound)
+    bool sm_mb_on = false, tri_bound_off = false;
     // membership change log (np8_track_changes / np8_changes): the baseline state and the output staging
     int track = 0;
     int32_t *z_base = nullptr, *cnt_base = nullptr, *chg_slot = nullptr;
@@ -442,7 +444,7 @@ void free_device(np8_ctx *c) {
                     c->sm_typ, c->sm_slist, c->sm_stheta, c->stage, c->evalc, c->z_base, c->cnt_base,
                     c->chg_slot, c->mu_base, c->sigma_base, c->chg_item, c->chg_count, c->chg_flags,
                     c->inv_hist, c->inv_out, c->queue, c->qcount, c->qlist, c->slot_logn1, c->plen_s,
-                    c->plr2_s};
+                    c->plr2_s, c->sm_mb};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     if (c->sm_first_host) (void)hipHostFree(c->sm_first_host);
@@ -455,6 +457,7 @@ void free_device(np8_ctx *c) {
     c->sm_first_host = nullptr;
     c->sm_n = -1;
     c->sm_cross_cap = 0;
+    c->sm_mb = nullptr;
     for (int b = 0; b < 2; ++b) {
         c->Xs[b] = nullptr;
         c->zs[b] = c->ids[b] = nullptr;
@@ -1379,6 +1382,10 @@ int np8_create(np8_ctx **out, const np8_config *cfg) {
     c->prune_on = !c->wide && c->kcap <= kPruneMaxKcap && std::getenv("NP8_NO_PRUNE") == nullptr;
     c->wide_prune_off = std::getenv("NP8_NO_PRUNE") != nullptr;
     c->fast_off = std::getenv("NP8_NO_FAST") != nullptr;
+    {  // NP8_TRI_BOUND=0: every triadic merge walks (A/B of the merge bound)
+        const char *tb = std::getenv("NP8_TRI_BOUND");
+        c->tri_bound_off = tb != nullptr && tb[0] == '0';
+    }
     c->fuse_off = std::getenv("NP8_FUSE") == nullptr;  // opt-in: measured slower than separate launches
     c->queue_on = std::getenv("NP8_QUEUE") != nullptr;
     c->rec_cap = c->req_max;  // grown to the item count by np8_set_data (one rank)
@@ -2341,6 +2348,7 @@ static SmArgs sm_args(np8_ctx *c) {
     A.sc = c->sm_ctl;
     A.typ = c->sm_typ;
     A.iso_walk = (c->sm_all_iso && c->gp_iso > 0.0) ? 1 : 0;
+    A.mb = c->sm_mb_on ? c->sm_mb : nullptr;
     return A;
 }
 
@@ -2354,7 +2362,8 @@ static int sm_buffers(np8_ctx *c) {
         (r = dalloc(c, &c->sm_off, (size_t)c->kcap + 1)) || (r = dalloc(c, &c->sm_live, (size_t)c->kcap)) ||
         (r = dalloc(c, &c->sm_ownm, (size_t)c->n_loc)) || (r = dalloc(c, &c->sm_Xm, (size_t)c->n_loc * c->D)) ||
         (r = dalloc(c, &c->sm_typ, (size_t)kSmBatchMax)) || (r = dalloc(c, &c->sm_slist, (size_t)kSmBatchMax)) ||
-        (r = dalloc(c, &c->sm_stheta, (size_t)kSmBatchMax * (c->D + 1))))
+        (r = dalloc(c, &c->sm_stheta, (size_t)kSmBatchMax * (c->D + 1))) ||
+        (!c->sm_mb && (r = dalloc(c, &c->sm_mb, (size_t)4 * c->kcap))))
         return r;
     if (!c->sm_ctl) {
         if ((r = dalloc(c, &c->sm_ctl, 1))) return r;
@@ -2365,7 +2374,7 @@ static int sm_buffers(np8_ctx *c) {
 }
 
 // The state the attempts of a batch see: dense table, live count, member lists, own and cross.
-static int sm_rebuild(np8_ctx *c) {
+static int sm_rebuild(np8_ctx *c, bool triadic) {
     int r = rebuild(c);
     if (r) return r;
     Ctl h;
@@ -2379,6 +2388,8 @@ static int sm_rebuild(np8_ctx *c) {
     Timer t;
     timer_begin(c, 4, t);
     HIPC(c, np8_launch_sm_members(sm_args(c), c->stream));
+    c->sm_mb_on = triadic && !c->tri_bound_off;
+    if (c->sm_mb_on) HIPC(c, np8_launch_tri_bound(sm_args(c), c->stream));  // the triadic merge bound's sums
     timer_end(c, t);
     int32_t all_iso = 0;  // every live slot isotropic: the triadic walk's fast form applies
     HIPC(c, hipMemcpyAsync(&all_iso, &c->sm_ctl->all_iso, sizeof(all_iso), hipMemcpyDeviceToHost, c->stream));
@@ -2405,7 +2416,7 @@ static int split_merge_sweeps(np8_ctx *c, int32_t n_sweeps, bool triadic) {
         c->use_sorted = false;
         c->sorted_valid = false;
         c->lists_valid = c->r2_zero = c->collecting = false;
-        if ((r = sm_rebuild(c))) return r;
+        if ((r = sm_rebuild(c, triadic))) return r;
         int64_t a = 0;
         while (a < N) {
             const int32_t nb = (int32_t)std::min<int64_t>(c->sm_batch, N - a);
@@ -2427,7 +2438,7 @@ static int split_merge_sweeps(np8_ctx *c, int32_t n_sweeps, bool triadic) {
             }
             FinArgs F = fin_args(c, c->rec, 1);
             HIPC(c, triadic ? np8_launch_tri_apply(A, F, first, c->stream) : np8_launch_sm_apply(A, F, first, c->stream));
-            if ((r = sm_rebuild(c))) return r;
+            if ((r = sm_rebuild(c, triadic))) return r;
             c->sm_batch = (int32_t)std::max<int64_t>(kSmBatchMin, std::min<int64_t>(kSmBatchMax, 2 * (first - a + 1)));
             a = first + 1;
         }

@@ -325,6 +325,7 @@ struct SmArgs {
     int64_t a0;
     int32_t nb;
     int32_t iso_walk;   // triadic: every target isotropic (all live slots and G0), the walk's fast form
+    double *mb;         // triadic: [K][4] per live row, the merge bound's member sums (np8_tri_bound); null: off
 };
 
 // NIW prior kernels (np8_niw.hip): posterior / prior draws per slot and picked auxiliaries -> slots.
@@ -492,5 +493,6 @@ hipError_t np8_launch_prune(const np8::PruneArgs &A, int kcap, hipStream_t s);
 hipError_t np8_launch_sm_members(const np8::SmArgs &A, hipStream_t s);
 hipError_t np8_launch_sm_eval(const np8::SmArgs &A, hipStream_t s);
 hipError_t np8_launch_sm_apply(const np8::SmArgs &A, const np8::FinArgs &F, int64_t a, hipStream_t s);
+hipError_t np8_launch_tri_bound(const np8::SmArgs &A, hipStream_t s);
 hipError_t np8_launch_tri_eval(const np8::SmArgs &A, hipStream_t s);
 hipError_t np8_launch_tri_apply(const np8::SmArgs &A, const np8::FinArgs &F, int64_t a, hipStream_t s);

@@ -244,6 +244,69 @@ __global__ __launch_bounds__(kSmThreads) void np8_sm_cross(SmArgs A) {
     }
 }
 
+// Triadic merge bound (DESIGN.md 2e "Merge bound"), per state: for live row r, over its members x,
+//   mb[r][0] = sum max_k ll_k(x)          (every live slot k),   mb[r][1] = sum |max_k ll_k(x)|,
+//   mb[r][2] = sum max_{k != own} ll_k(x) (every other slot),    mb[r][3] = sum |...|,
+// with ll_k = sm_ll, the walk's own likelihood bit for bit.  A triadic merge moves every member of its
+// three sources onto two of them, so its after-move sum is at most mb[r0][0] + mb[r1][0] + mb[r2][2].
+// Block (row r, member chunk): the live slots staged in LDS 64 at a time; one atomic per block and sum
+// (the order of these sums only enters the bound through its error margin).
+constexpr int kBoundTile = 64, kBoundChunks = 16;
+template <int D>
+__global__ __launch_bounds__(kSmThreads) void np8_tri_bound(SmArgs A) {
+    constexpr int DP = D * (D + 1) / 2, W = D + DP + 2;
+    __shared__ double th[kBoundTile][W];
+    __shared__ double red[kSmThreads];
+    const int r = blockIdx.x;
+    const int sr = A.live[r];
+    const int b = A.off[sr], n = A.off[sr + 1] - b;
+    const int per = (n + kBoundChunks - 1) / kBoundChunks;
+    const int p0 = min(n, (int)blockIdx.y * per), p1 = min(n, p0 + per);
+    double s_all = 0.0, a_all = 0.0, s_ex = 0.0, a_ex = 0.0;
+    for (int pb = p0; pb < p1; pb += kSmThreads) {  // block-uniform
+        const int p = pb + threadIdx.x;
+        const bool valid = p < p1;
+        double x[D];
+#pragma unroll
+        for (int a = 0; a < D; ++a) x[a] = 0.0;
+        if (valid) load_xm<D>(A, b + p, x);
+        double mall = -__builtin_huge_val(), mex = -__builtin_huge_val();
+        for (int k0 = 0; k0 < A.K; k0 += kBoundTile) {
+            const int nk = min(kBoundTile, A.K - k0);
+            __syncthreads();
+            for (int e = threadIdx.x; e < nk * W; e += kSmThreads) {
+                const int kk = e / W, f = e - kk * W;
+                const int s = A.live[k0 + kk];
+                th[kk][f] = (f < D) ? A.slot_mu[(int64_t)s * D + f]
+                                    : (f < D + DP ? A.slot_P[(int64_t)s * DP + (f - D)]
+                                                  : (f == D + DP ? A.slot_c[s] : A.slot_iso[s]));
+            }
+            __syncthreads();
+            if (valid) {
+                for (int kk = 0; kk < nk; ++kk) {
+                    __asm__ __volatile__("" ::: "memory");  // parameters stay in LDS
+                    const double l = sm_ll<D>(x, &th[kk][0], &th[kk][D], th[kk][D + DP], th[kk][D + DP + 1]);
+                    mall = fmax(mall, l);
+                    mex = (k0 + kk == r) ? mex : fmax(mex, l);
+                }
+            }
+        }
+        if (valid) {
+            s_all += mall;
+            a_all += fabs(mall);
+            s_ex += mex;
+            a_ex += fabs(mex);
+        }
+    }
+    const double v0 = tree256(red, s_all), v1 = tree256(red, a_all), v2 = tree256(red, s_ex), v3 = tree256(red, a_ex);
+    if (threadIdx.x == 0 && p1 > p0) {
+        atomicAdd(&A.mb[4 * r + 0], v0);
+        atomicAdd(&A.mb[4 * r + 1], v1);
+        atomicAdd(&A.mb[4 * r + 2], v2);
+        atomicAdd(&A.mb[4 * r + 3], v3);
+    }
+}
+
 // ---- attempts ----------------------------------------------------------------------------------------------
 // Outcome codes as np8o_sm_sweep: 0 skipped, 1 split rejected, 2 merge rejected, 3 split accepted,
 // 4 merge accepted, 5 split rejected for want of a free slot; kPending: a split not evaluated (its
@@ -576,6 +639,30 @@ __device__ __forceinline__ bool tri_dyadic_merge_accept(const SmArgs &A, const T
     return sm_accept(x, uniform(A.seed, (uint64_t)a, A.t, kStreamSmAccept, 0));
 }
 
+// Triadic merge 3 -> 2 rejected without its walk (DESIGN.md 2e "Merge bound"): the walk's acceptance
+// exponent x = rP + rR + (after - before) is at most
+//   rP  <= -(log alpha + sum_i lgamma(n_i) - lgamma(n - 1))   (sum_q lgamma(N_q) over N_0 + N_1 = n, N_q >= 1,
+//                                                              is largest at (1, n - 1): lgamma is convex)
+//   after <= mb[r0][0] + mb[r1][0] + mb[r2][2]                  (np8_tri_bound; targets are slots 0 and 1)
+// plus a margin for the different summation orders (n u sum|terms| <= 1.2e-10 sum|terms| at n <= 2^20,
+// lgamma_int's 2e-15).  When that bound is below log u by 1e-6, exp_le0(x) < u: the walk would reject.
+__device__ __forceinline__ bool tri_merge_bound_rejects(const SmArgs &A, const Tri &T, int64_t a) {
+    const int r0 = A.dense[T.cl[0]], r1 = A.dense[T.cl[1]], r2 = A.dense[T.cl[2]];
+    const int n0 = A.off[T.cl[0] + 1] - A.off[T.cl[0]], n1 = A.off[T.cl[1] + 1] - A.off[T.cl[1]],
+              n2 = A.off[T.cl[2] + 1] - A.off[T.cl[2]];
+    const double g0 = lgamma_int(n0), g1 = lgamma_int(n1), g2 = lgamma_int(n2);
+    const double gn = lgamma_int((int64_t)n0 + n1 + n2 - 1);
+    const double rp = -(A.log_alpha + ((g0 + g1) + g2) - gn);
+    const double before = (tri_own(A, T.cl[0]) + tri_own(A, T.cl[1])) + tri_own(A, T.cl[2]);
+    const double after = (A.mb[4 * r0] + A.mb[4 * r1]) + A.mb[4 * r2 + 2];
+    const double mag = A.mb[4 * r0 + 1] + A.mb[4 * r1 + 1] + A.mb[4 * r2 + 3] + fabs(before) + fabs(A.log_alpha) + g0 +
+                       g1 + g2 + gn + fabs(A.lrr[2]);
+    const double xub = ((rp + A.lrr[2]) + (after - before)) + (1e-9 * mag + 1e-6);
+    if (!(xub < 0.0)) return false;
+    const double u = uniform(A.seed, (uint64_t)a, A.t, kStreamSmAccept, 0);
+    return xub < log_pos(u) - 1e-6;
+}
+
 template <int D>
 __global__ __launch_bounds__(kSmThreads) void np8_tri_classify(SmArgs A) {
     const int q = blockIdx.x * kSmThreads + threadIdx.x;
@@ -588,6 +675,8 @@ __global__ __launch_bounds__(kSmThreads) void np8_tri_classify(SmArgs A) {
     } else if (T.kind == 0) {
         out = tri_dyadic_merge_accept(A, T, a) ? 2 : 1;
         if (out == 2) atomicMin(reinterpret_cast<unsigned long long *>(&A.sc->first), (unsigned long long)a);
+    } else if (T.kind == 2 && A.mb && tri_merge_bound_rejects(A, T, a)) {
+        out = 5;  // what the walk returns for a rejected triadic merge (1 + 2 kind)
     } else {
         out = kPending;
         const int e = atomicAdd(&A.sc->nsplit, 1);
@@ -912,6 +1001,20 @@ hipError_t np8_launch_sm_apply(const SmArgs &A, const FinArgs &F, int64_t a, hip
     if (A.D == d) {                                                             \
         hipLaunchKernelGGL(np8_sm_apply<d>, dim3(1), dim3(64), 0, s, A, F, a);  \
         return hipGetLastError();                                               \
+    }
+    NP8_SM_FOR_EACH_D(X)
+#undef X
+    return hipErrorInvalidValue;
+}
+
+hipError_t np8_launch_tri_bound(const SmArgs &A, hipStream_t s) {
+    if (A.N <= 0 || A.K <= 0 || !A.mb) return hipSuccess;
+    hipError_t e = hipMemsetAsync(A.mb, 0, sizeof(double) * 4 * (size_t)A.K, s);
+    if (e != hipSuccess) return e;
+#define X(d)                                                                                                  \
+    if (A.D == d) {                                                                                           \
+        hipLaunchKernelGGL(np8_tri_bound<d>, dim3((unsigned)A.K, kBoundChunks), dim3(kSmThreads), 0, s, A); \
+        return hipGetLastError();                                                                             \
     }
     NP8_SM_FOR_EACH_D(X)
 #undef X

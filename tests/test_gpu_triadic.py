@@ -109,3 +109,24 @@ def test_kcap_saturation_parity():
         g.sweep(1)
         o.tri_sweep(1)
         assert_same(g, o)
+
+
+def test_merge_bound_warm_state_parity(monkeypatch):
+    """Well-separated warm state (C3's shape, smaller): the triadic merges are rejected by the merge bound
+    (np8_tri_bound / tri_merge_bound_rejects) without their walk.  Same chain as the oracle and as the
+    device with the bound off (NP8_TRI_BOUND=0), bit for bit, outcome counts included."""
+    N, D, K = 6000, 8, 8
+    X, z, mu, sig = datasets.mixture(N, D, K, 0.8, 20.0, seed=5)
+    g, o = pair(D, seed=17, kcap=64)
+    monkeypatch.setenv("NP8_TRI_BOUND", "0")
+    g_off = TriadicAlgorithm(D, seed=17, kcap=64, device=0)
+    monkeypatch.delenv("NP8_TRI_BOUND")
+    for c in (g, o, g_off):
+        c.set_data(X)
+        c.set_state(z, mu, sig)
+    g.sweep(2)
+    g_off.sweep(2)
+    o.tri_sweep(2)
+    assert_same(g, o)
+    assert_same(g_off, o)
+    assert o.tri_stats[5] > 500  # triadic merges rejected: the bound's case
