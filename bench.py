@@ -68,6 +68,9 @@ def parse():
                          "(the multi-GPU code path, collectives captured in the sweep graph)")
     ap.add_argument("--substeps", type=int, default=1,
                     help="the data-parallel sweep as S synchronous sub-steps (np8_config.substeps)")
+    ap.add_argument("--weak", action="store_true",
+                    help="weak scaling: --n items PER RANK (total n x ranks); value = whole-job item updates/s / n, "
+                         "i.e. sweeps/s of an n-item data set (C4 as written is strong: total n fixed)")
     ap.add_argument("--config", default="C3", help="config tag for the JSON line (BASELINE.json configs)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget (0 = skip)")
     ap.add_argument("--cold-sweeps", type=int, default=20,
@@ -131,6 +134,9 @@ def main():
 
     from noparama_amd import NealAlgorithm8, comm_unique_id
 
+    n_rank = args.n
+    if args.weak:  # every rank keeps n items: the data set grows with the ranks
+        args.n = n_rank * world
     N, D, K = args.n, args.d, args.k
     X, z, mu, sig, opts = workload(args)
     wide = opts.get("contraction") == "f32"
@@ -196,15 +202,15 @@ def main():
         if world == 1 and args.cpu_seconds > 0:
             cpu = cpu_baseline(X, z, mu, sig, D, args.seed, args.cpu_seconds, opts)
         out = {
-            "metric": f"Gibbs sweeps/sec (Neal-8, N={N:.0e} D={D})".replace("+0", ""),
-            "value": args.steps / m["dt"],
+            "metric": f"Gibbs sweeps/sec (Neal-8, N={(n_rank if args.weak else N):.0e} D={D})".replace("+0", ""),
+            "value": args.steps / m["dt"] * (N / n_rank if args.weak else 1.0),
             "unit": "sweeps/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": m["dt"] / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "strong",
+            "scaling": "weak" if args.weak else "strong",
             "vs_baseline": None,
             "dtype": "f32-mfma contraction, f64 draws" if wide else "f64",
             "data": "synthetic",
@@ -217,6 +223,8 @@ def main():
                 "N": N, "D": D, "K_final": m["K_final"], "parallelism": f"data-sharded x{world}",
                 "substeps": args.substeps,
                 "exchange": transport,
+                "weak": ({"items_per_rank": n_rank, "items_total": N, "data_sweeps_per_s": args.steps / m["dt"],
+                          "value": "whole-job item updates per second / items_per_rank"} if args.weak else None),
                 "param_update": args.param_update,
                 "params_ms_per_timed_sweep": m["params_ms"],
                 "sweep_graphs": os.environ.get("NP8_NO_GRAPH") is None,

@@ -177,6 +177,10 @@ struct np8_ctx {
     bool sm_all_iso = false;
     double *sm_mb = nullptr;  // triadic merge bound: [kcap][4] member sums per live row (np8_tri_bound)
     bool sm_mb_on = false, tri_bound_off = false;
+    // NP8_FINPRUNE=1: finalize and the lists in one launch (np8_fin_prune), opt-in: measured slower (125k items:
+    // 26.6 vs 21.1 us per sweep; 1e6: 51.7 vs 46.1) -- the agent-scope release/acquire between its workgroups
+    // (L2 writeback and invalidate across the XCDs) costs more than the dependent dispatch it saves
+    bool fp_off = true;
     // membership change log (np8_track_changes / np8_changes): the baseline state and the output staging
     int track = 0;
     int32_t *z_base = nullptr, *cnt_base = nullptr, *chg_slot = nullptr;
@@ -818,6 +822,14 @@ int launch_finalize(np8_ctx *c, const unsigned char *recs, int world, int prune 
     }
     if (c->gather)  // the step's radius records (any order with finalize: both only raise the gathered radii)
         HIPC(c, np8_launch_fold_r2(c->wr2, c->assign_waves, c->r2, c->kcap, c->stream));
+    if (prune >= 0 && !c->fp_off && !c->wide && c->prior == NP8_PRIOR_REFERENCE) {
+        // finalize and the lists in one launch, the lists still one per wave over several workgroups
+        PruneArgs P = prune_args(c, prune == 1);
+        HIPC(c, np8_launch_fin_prune(F, P, c->stream));
+        c->lists_valid = true;
+        timer_end(c, t);
+        return NP8_OK;
+    }
     HIPC(c, np8_launch_finalize(F, c->stream));
     if (F.frame_payload && c->prior != NP8_PRIOR_NIW) HIPC(c, np8_launch_frame_slots(F, c->stream));
     if (c->prior == NP8_PRIOR_NIW) {  // the accepted auxiliaries' full parameters
@@ -974,7 +986,7 @@ int step(np8_ctx *c, int64_t p0, int64_t p1, const int64_t *order, bool use_perm
     // the lists right after finalize (np8_step_tail) when nothing changes the table in between: the next sub-step's
     // (radii in use), or the sweep's when its parameters are frozen (end_sweep's prune)
     const bool mid = sub >= 0 && sub + 1 < c->substeps;
-    const int fprune = (c->collecting && !c->fuse_off && !c->wide && c->prior == NP8_PRIOR_REFERENCE &&
+    const int fprune = (c->collecting && (!c->fuse_off || !c->fp_off) && !c->wide && c->prior == NP8_PRIOR_REFERENCE &&
                         (mid || c->param_update == NP8_PARAM_FROZEN)) ? (mid ? 0 : 1) : -1;
     if (c->comm) {  // the exchange over RCCL (also with a one-rank communicator)
         HIPC(c, np8_launch_req_select(c->stage, c->stage_cap, c->rec, c->rec_cap, c->kcap, c->D, c->req_max, c->stream));
@@ -1385,6 +1397,10 @@ int np8_create(np8_ctx **out, const np8_config *cfg) {
     {  // NP8_TRI_BOUND=0: every triadic merge walks (A/B of the merge bound)
         const char *tb = std::getenv("NP8_TRI_BOUND");
         c->tri_bound_off = tb != nullptr && tb[0] == '0';
+    }
+    {
+        const char *fp = std::getenv("NP8_FINPRUNE");
+        c->fp_off = !(fp != nullptr && fp[0] == '1');
     }
     c->fuse_off = std::getenv("NP8_FUSE") == nullptr;  // opt-in: measured slower than separate launches
     c->queue_on = std::getenv("NP8_QUEUE") != nullptr;
@@ -2039,6 +2055,8 @@ int np8_sync(np8_ctx *c) {
             return fail(c, NP8_ERR_STATE, "a debug invariant failed (np8_check_invariants: labels, counts, K, table)");
         if (h.err & kErrQueue)
             return fail(c, NP8_ERR_STATE, "internal: np8_assign_fast deferred a lane with no queue launched");
+        if (h.err & kErrSpin)
+            return fail(c, NP8_ERR_STATE, "internal: np8_fin_prune's list workgroups timed out waiting for finalize");
     }
     return NP8_OK;
 }

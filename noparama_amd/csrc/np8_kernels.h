@@ -37,6 +37,8 @@ struct Ctl {
                                        // and (wave, auxiliary) pairs in which at least one lane was not skipped
     uint32_t qwaves;                   // np8_assign_fast waves with deferred lanes this step (AssignArgs::qlist)
     uint32_t pad3;
+    uint32_t fin_flag;    // np8_fin_prune: finalize done (set by workgroup 0, reset by the last list workgroup)
+    uint32_t prune_exit;  // np8_fin_prune: list workgroups finished
 };
 
 // Executed work of np8_assign when AssignArgs::count_eval is set (timing mode): per wave, the cluster
@@ -46,7 +48,7 @@ struct Ctl {
 // of the grid serialises the atomics in one L2 channel (4x the kernel time at C3).
 constexpr int kEvalSlots = 1024;
 
-enum : int32_t { kErrCapacity = 1, kErrSigma = 2, kErrInvariant = 4, kErrQueue = 8 };
+enum : int32_t { kErrCapacity = 1, kErrSigma = 2, kErrInvariant = 4, kErrQueue = 8, kErrSpin = 16 };
 
 // Exchange record of one rank for one synchronous step:
 //   RecHeader | int32 delta[kcap] | Request req[rec_cap] | double vmu[rec_cap][D+1]
@@ -490,6 +492,7 @@ hipError_t np8_launch_suffstats_wide(const np8::ParamArgs &P, hipStream_t s);
 hipError_t np8_launch_mh_g0(const np8::ParamArgs &A, hipStream_t s);
 hipError_t np8_launch_advance_epoch(np8::Ctl *ctl, uint32_t n, hipStream_t s);
 hipError_t np8_launch_prune(const np8::PruneArgs &A, int kcap, hipStream_t s);
+hipError_t np8_launch_fin_prune(const np8::FinArgs &F, const np8::PruneArgs &P, hipStream_t s);
 hipError_t np8_launch_sm_members(const np8::SmArgs &A, hipStream_t s);
 hipError_t np8_launch_sm_eval(const np8::SmArgs &A, hipStream_t s);
 hipError_t np8_launch_sm_apply(const np8::SmArgs &A, const np8::FinArgs &F, int64_t a, hipStream_t s);

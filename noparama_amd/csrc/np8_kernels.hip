@@ -1647,6 +1647,64 @@ __global__ __launch_bounds__(kFinThreads) void np8_step_tail(AssignArgs A, FinAr
     if (T.prune) prune_block<D>(P, smem, T.lds_bytes);
 }
 
+// Finalize and the candidate lists in one launch with the lists still built in parallel (DESIGN.md §5 "Fewer
+// launches"): workgroup 0 runs np8_finalize's body, then releases a flag (agent scope); workgroups 1 .. nP wait
+// for it (bounded spin: a workgroup that gives up sets kErrSpin and builds nothing) and build one list per wave,
+// prune_row's arithmetic, as np8_prune's workgroups do.  Every workgroup is resident at once (nP <= 8 on 256
+// CUs; workgroup 0 is dispatched first), so the wait always ends.  The last prune workgroup to finish resets the
+// flag and the exit counter for the next launch.  Saves one dependent kernel dispatch per sweep.
+constexpr int kFpPruneBlocks = 8;
+template <int DT>
+__global__ __launch_bounds__(kFinThreads) void np8_fin_prune(FinArgs F, PruneArgs P, int nP) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    __shared__ int s_ok;
+    if (blockIdx.x == 0) {
+        finalize_block(F, smem);
+        __syncthreads();
+        // np8_prune's first-workgroup duties: the radius buffers (the lists read the other half of r2) and lists_ok
+        if (P.gathered)
+            for (int s = threadIdx.x; s < P.kcap; s += kFinThreads) P.r2[s] = P.r2[P.kcap + s];
+        if (P.clear_next)
+            for (int s = threadIdx.x; s < P.kcap; s += kFinThreads) P.r2[P.kcap + s] = 0.0;
+        if (threadIdx.x == 0) {
+            P.ctl->lists_ok = 1;
+            __threadfence();
+            __hip_atomic_store(&F.ctl->fin_flag, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        return;
+    }
+    if (threadIdx.x == 0) {
+        int ok = 0;
+        for (int it = 0; it < (1 << 22); ++it) {
+            if (__hip_atomic_load(&F.ctl->fin_flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
+                ok = 1;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+        if (!ok) atomicOr(&F.ctl->err, kErrSpin);
+        s_ok = ok;
+    }
+    __syncthreads();
+    __threadfence();  // every wave: acquire what workgroup 0 wrote (the table, K)
+    if (s_ok) {
+        const int K = __hip_atomic_load(&P.ctl->K, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const double *src = P.r2 + (P.gathered ? P.kcap : 0);
+        auto R2of = [&](int slot) { return src[slot]; };
+        constexpr int kWaves = kFinThreads / 64;
+        for (int k0 = ((int)blockIdx.x - 1) * kWaves + ((int)threadIdx.x >> 6); k0 < K; k0 += nP * kWaves)  // wave-uniform
+            prune_row<DT>(P.cand, R2of, P.plist, P.plen, P.plr2, P.plen_s, P.plr2_s, P.ls, P.D, K, k0);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();
+        if (atomicAdd(&F.ctl->prune_exit, 1u) == (unsigned)nP - 1u) {  // the last one: reset for the next launch
+            atomicExch(&F.ctl->prune_exit, 0u);
+            atomicExch(&F.ctl->fin_flag, 0u);
+        }
+    }
+}
+
 }  // namespace
 
 // The wide path's new slots under the reference prior: (v, mu) of each accepted request from the item frame
@@ -2312,6 +2370,23 @@ hipError_t np8_launch_step_tail(const AssignArgs &A, const FinArgs &F, const Pru
 #define Y(d)                                                                                              \
     case d:                                                                                               \
         hipLaunchKernelGGL((np8_step_tail<d>), dim3((unsigned)nb), dim3(kFinThreads), lds, s, A, F, P, T); \
+        break;
+        Y(1) Y(2) Y(3) Y(4) Y(5) Y(6) Y(7) Y(8) Y(9) Y(10) Y(11) Y(12) Y(13) Y(14) Y(15) Y(16)
+#undef Y
+        default:
+            return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t np8_launch_fin_prune(const FinArgs &F, const PruneArgs &P, hipStream_t s) {
+    int nP = (F.kcap + kFinThreads / 64 - 1) / (kFinThreads / 64);
+    nP = nP < 1 ? 1 : (nP > kFpPruneBlocks ? kFpPruneBlocks : nP);
+    const size_t lds = np8_finalize_lds_bytes(F.kcap);
+    switch (F.D) {
+#define Y(d)                                                                                                 \
+    case d:                                                                                                  \
+        hipLaunchKernelGGL((np8_fin_prune<d>), dim3((unsigned)(1 + nP)), dim3(kFinThreads), lds, s, F, P, nP); \
         break;
         Y(1) Y(2) Y(3) Y(4) Y(5) Y(6) Y(7) Y(8) Y(9) Y(10) Y(11) Y(12) Y(13) Y(14) Y(15) Y(16)
 #undef Y
