@@ -249,8 +249,11 @@ template <int D, int M, int PRIOR, bool COUNT>
 #ifndef NP8_ASSIGN_BLOCK
 #define NP8_ASSIGN_BLOCK 64  // one wave per workgroup (256: 2% slower at C3)
 #endif
+#ifndef NP8_WALK_LDS
+#define NP8_WALK_LDS 1  // np8_assign_fast's candidate walk broadcasts rows through LDS (0: v_readlane)
+#endif
 #ifndef NP8_FAST_WAVES
-#define NP8_FAST_WAVES 4  // 109 VGPRs, no spills (5: 96 with spills, 2-6% slower at C3)
+#define NP8_FAST_WAVES 4  // 127 VGPRs, 30 dwords spilled on the rare paths (62 KB written per C3 launch); 5: 2-6% slower
 #endif
 __device__ __forceinline__ void assign_item(const AssignArgs &A, const int64_t p, const int64_t qslot) {
     constexpr int DP = D * (D + 1) / 2;
@@ -705,6 +708,18 @@ __global__ __launch_bounds__(NP8_ASSIGN_BLOCK) __attribute__((amdgpu_waves_per_e
     // (lane q: row q's fields, the wave's active lanes are 0 .. nact - 1 -- the last wave of the range is
     // partial), then broadcast row by row: no dependent load per row (the mixed regime walks ~9 rows per item,
     // a stale wave the whole table).  A row that is not isotropic defers the lane (np8_assign takes it).
+#if NP8_WALK_LDS
+    // the round's rows staged in LDS ([field][row], one-wave workgroups) and read back at a wave-uniform address
+    // (a broadcast on the LDS pipe) instead of 2 v_readlane per double on the VALU
+    static_assert(NP8_ASSIGN_BLOCK == 64, "the walk's LDS rows are per wave");
+    __shared__ double s_row[D + 4][64];
+    __shared__ int32_t s_j[64];
+#define NP8_ROWF(v, f, k) s_row[f][k]
+#define NP8_ROWJ(k) s_j[k]
+#else
+#define NP8_ROWF(v, f, k) readlane_d(v, k)
+#define NP8_ROWJ(k) __builtin_amdgcn_readlane(jq, k)
+#endif
     auto walk = [&](auto row_of, int n, bool mine, bool own_skip) {
         const int nact = __popcll(__ballot(1));
         for (int qb = 0; qb < n; qb += nact) {
@@ -723,24 +738,35 @@ __global__ __launch_bounds__(NP8_ASSIGN_BLOCK) __attribute__((amdgpu_waves_per_e
                 fl = e[F + kFieldLogn];
                 fsl = e[F + kFieldSlot];
             }
+#if NP8_WALK_LDS
+            __syncthreads();  // (one wave) the previous round's reads are done
+#pragma unroll
+            for (int a = 0; a < D; ++a) s_row[a][lane] = fm[a];
+            s_row[D][lane] = fiso;
+            s_row[D + 1][lane] = fc;
+            s_row[D + 2][lane] = fl;
+            s_row[D + 3][lane] = fsl;
+            s_j[lane] = jq;
+            __syncthreads();
+#endif
             const int nb = min(nact, n - qb);
             for (int k = 0; k < nb; ++k) {  // wave-uniform: the rows in order (ascending)
-                const double iso = readlane_d(fiso, k);
+                const double iso = NP8_ROWF(fiso, D, k);
                 if (mine && !defer) {
                     if (!(iso > 0.0)) {
                         defer = true;
                     } else {
-                        const double m0 = readlane_d(fm[0], k);
+                        const double m0 = NP8_ROWF(fm[0], 0, k);
                         double s2 = (x[0] - m0) * (x[0] - m0);
 #pragma unroll
                         for (int a = 1; a < D; ++a) {
-                            const double ma = readlane_d(fm[a], k);
+                            const double ma = NP8_ROWF(fm[a], a, k);
                             s2 = fma(x[a] - ma, x[a] - ma, s2);
                         }
-                        const double lw = fma(-0.5, s2 * iso, readlane_d(fc, k)) + readlane_d(fl, k);
-                        const double sl = readlane_d(fsl, k);
+                        const double lw = fma(-0.5, s2 * iso, NP8_ROWF(fc, D + 1, k)) + NP8_ROWF(fl, D + 2, k);
+                        const double sl = NP8_ROWF(fsl, D + 3, k);
                         if (!(own_skip && sl == zslot)) {
-                            const int j = __builtin_amdgcn_readlane(jq, k);
+                            const int j = NP8_ROWJ(k);
                             ensure_u(st, lw, A.seed, ig, t);
                             pick_step(st, lw, j);
                             pslot = (st.pick == j) ? (int32_t)sl : pslot;
@@ -769,6 +795,8 @@ __global__ __launch_bounds__(NP8_ASSIGN_BLOCK) __attribute__((amdgpu_waves_per_e
     }
     if (__ballot(full && !defer))  // wave-uniform row loop over the lanes that need it
         walk([](int q) { return q; }, K, full && !defer, true);
+#undef NP8_ROWF
+#undef NP8_ROWJ
     NP8_CLK(3);
     // the auxiliaries: np8_assign's two-level screen, then the exact fp64 draw for the lanes it cannot clear;
     // a lane that picks an auxiliary makes a new-cluster request (appended below)

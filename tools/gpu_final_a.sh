@@ -1,11 +1,10 @@
 #!/bin/bash
-# One GPU call: the -m gpu suite, the default bench line, the C3 profile (tools/prof.sh) and the C5 profile
+# One GPU call: the default bench line, the C3 profile (tools/prof.sh) and the C5 profile
 # (tools/prof_c5.sh) at the current build.  Each GPU step under its own limit, chained.
 set -o pipefail
 export TMPDIR=/tmp
 OUT=${OUT:-gpurun_out/fa}
 mkdir -p $OUT
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $OUT/gpu_tests.log 2>&1 &&
 timeout -k 10 300 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err &&
 bash tools/prof.sh $OUT/prof &&
 bash tools/prof_c5.sh $OUT/prof_c5 &&
