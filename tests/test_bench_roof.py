@@ -23,3 +23,12 @@ def test_no_counters_reports_hbm():
     r = bench.binding_roof(None, 1e6, 0.01, 78.6, "np8_assign")
     assert r["bound"] == "hbm" and r["frac"] > 0
     assert bench.binding_roof(None, 1e6, 0.0, 78.6, "np8_assign")["achieved"] == 0.0
+
+
+def test_weak_scaling_flag(monkeypatch):
+    """--weak keeps --n items per rank (bench.py main multiplies by the ranks); the default is C4's strong scaling."""
+    monkeypatch.setattr("sys.argv", ["bench.py", "--gpus", "2", "--weak", "--n", "1000"])
+    a = bench.parse()
+    assert a.weak and a.n == 1000 and a.gpus == 2
+    monkeypatch.setattr("sys.argv", ["bench.py"])
+    assert not bench.parse().weak
