@@ -793,6 +793,7 @@ AssignArgs assign_args(np8_ctx *c, int64_t p0, int64_t p1, const int64_t *order,
 }
 
 PruneArgs prune_args(np8_ctx *c, bool last);
+int launch_prune(np8_ctx *c, bool last);
 
 // prune: -1 none; 0 / 1 the candidate lists right after finalize, in the same launch (np8_step_tail), as
 // launch_prune(c, false / true) would build them -- the frozen reference-prior sweep, where nothing changes the
@@ -801,11 +802,14 @@ int launch_finalize(np8_ctx *c, const unsigned char *recs, int world, int prune 
     Timer t;
     timer_begin(c, 1, t);
     FinArgs F = fin_args(c, recs, world);
-    const bool tail = !c->fuse_off && (prune >= 0 || c->gather) && !c->wide && c->prior == NP8_PRIOR_REFERENCE;
+    // the one-workgroup tail (finalize + lists) on the sweeps that do not gather radii: a gathering sweep's fold
+    // needs every assign record, i.e. a multi-workgroup launch whose last workgroup would run the serial part
+    // behind agent-scope fences (their L2 writeback costs more than the dispatch it saves, §5)
+    const bool tail = !c->fuse_off && prune >= 0 && !c->gather && !c->wide && c->prior == NP8_PRIOR_REFERENCE;
     if (tail) {  // radius fold, finalize (+ lists) in one launch
         TailArgs T;
         std::memset(&T, 0, sizeof(T));
-        T.fold = c->gather ? 1 : 0;
+        T.fold = 0;
         T.fold_n = c->assign_waves;
         T.fin = 1;
         PruneArgs P;
@@ -840,6 +844,10 @@ int launch_finalize(np8_ctx *c, const unsigned char *recs, int world, int prune 
     }
     int r = refresh_wide(c, false);  // the slots created here
     if (r) return r;
+    if (prune >= 0) {  // the lists the caller asked for (a gathering sweep, or the tail switched off)
+        r = launch_prune(c, prune == 1);
+        if (r) return r;
+    }
     timer_end(c, t);
     return NP8_OK;
 }

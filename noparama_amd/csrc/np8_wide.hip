@@ -174,7 +174,10 @@ __device__ __forceinline__ void row_glds(const float *__restrict__ wfrag, int sj
 
 // ---- table maintenance ---------------------------------------------------------------------------
 constexpr int kLamRounds = 5;  // eigenvalue-bound rounds of three concurrent Cholesky tests: 4^5 = 1024 steps
-constexpr double kLamRelWidth = 0.02;  // ... or fewer, once the bracket [lo, hi] is within 2% of hi
+#ifndef NP8_LAM_REL_WIDTH
+#define NP8_LAM_REL_WIDTH 0.02
+#endif
+constexpr double kLamRelWidth = NP8_LAM_REL_WIDTH;  // ... or fewer, once the bracket [lo, hi] is within 2% of hi
 
 // One block per slot (grid kcap): the slots flagged in wdirty get their factor and fp32 mean.
 // LDS: R [D][D] | three [D][D] workspaces.
