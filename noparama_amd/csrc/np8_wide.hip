@@ -175,9 +175,9 @@ __device__ __forceinline__ void row_glds(const float *__restrict__ wfrag, int sj
 // ---- table maintenance ---------------------------------------------------------------------------
 constexpr int kLamRounds = 5;  // eigenvalue-bound rounds of three concurrent Cholesky tests: 4^5 = 1024 steps
 #ifndef NP8_LAM_REL_WIDTH
-#define NP8_LAM_REL_WIDTH 0.02
+#define NP8_LAM_REL_WIDTH 0.05  // 2%: C5 niw_conjugate 638 vs 675 sweeps/s, the bound 3% looser at most, contractions unchanged
 #endif
-constexpr double kLamRelWidth = NP8_LAM_REL_WIDTH;  // ... or fewer, once the bracket [lo, hi] is within 2% of hi
+constexpr double kLamRelWidth = NP8_LAM_REL_WIDTH;  // ... or fewer, once the bracket [lo, hi] is within 5% of hi
 
 // One block per slot (grid kcap): the slots flagged in wdirty get their factor and fp32 mean.
 // LDS: R [D][D] | three [D][D] workspaces.
