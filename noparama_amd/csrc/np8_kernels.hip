@@ -1342,23 +1342,26 @@ __device__ void finalize_block(const FinArgs &F, unsigned char *smem) {
     // everything the common step (no request accepted) needs from global memory, loaded in one round:
     // old counts (liveness changes), deltas, and the table entries of this thread's first kFinPre slots
     constexpr int kFinPre = 2;
-    int cold[kFinPre];
+    int cold[kFinPre], d0[kFinPre];
     double pc[kFinPre], piso[kFinPre];
+    const int32_t *delta0 = rec_delta(F, 0);
 #pragma unroll
     for (int q = 0; q < kFinPre; ++q) {
         const int s = s0 + q;
         const bool in = s < s1;
         cold[q] = in ? F.cnt[s] : 0;
+        d0[q] = in ? delta0[s] : 0;  // rank 0's delta in the same round of loads (the single-rank step: all of them)
         pc[q] = in ? F.slot_c[s] : 0.0;
         piso[q] = in ? F.slot_iso[s] : 0.0;
     }
     const int cand_fresh = F.ctl->cand_fresh;
+    const int nreq0 = rec_header(F, 0)->nreq;  // (same round: every thread, one address)
 
     if (tid == 0) {
         int n = 0;
         for (int r = 0; r < F.world; ++r) {
             base[r] = n;
-            n += min(rec_header(F, r)->nreq, F.rec_cap);
+            n += min(r == 0 ? nreq0 : rec_header(F, r)->nreq, F.rec_cap);
         }
         base[F.world] = n;
         s_flags[0] = n;
@@ -1369,8 +1372,8 @@ __device__ void finalize_block(const FinArgs &F, unsigned char *smem) {
     for (int q = 0; q < kFinPre; ++q) {
         const int s = s0 + q;
         if (s < s1) {
-            int c = cold[q];
-            for (int r = 0; r < F.world; ++r) c += rec_delta(F, r)[s];
+            int c = cold[q] + d0[q];
+            for (int r = 1; r < F.world; ++r) c += rec_delta(F, r)[s];
             cnt_s[s] = c;
         }
     }
