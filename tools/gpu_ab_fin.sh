@@ -1,9 +1,9 @@
 #!/bin/bash
-# One GPU call: the -m gpu suite with finalize's record loads batched into its first round
+# One GPU call: the -m gpu suite with the lists' first candidate block preloaded (prune_row)
 # (noparama_amd/lib/exp/fin.so), then A/B against the current build at N = 125k and 1e6 (twice each).
 set -o pipefail
 export TMPDIR=/tmp
-OUT=${OUT:-gpurun_out/fin}
+OUT=${OUT:-gpurun_out/prn}
 mkdir -p $OUT
 L=noparama_amd/lib/exp/fin.so
 A="--steps 300 --warmup 40 --cpu-seconds 0 --cold-sweeps 0 --no-c5"
