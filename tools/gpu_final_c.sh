@@ -2,7 +2,7 @@
 # The round-end check on the final build: the -m gpu suite, smoke(), the default bench line and C5 niw_conjugate.
 set -o pipefail
 export TMPDIR=/tmp
-OUT=${OUT:-gpurun_out/fc}
+OUT=${OUT:-gpurun_out/fc2}
 mkdir -p $OUT
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $OUT/gpu_tests.log 2>&1 &&
 timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 &&
