@@ -137,6 +137,10 @@ typedef struct {
      * pays the table loop); waves of more own rows than the list walk takes (a stale layout); list entries
      * walked by lanes */
     int64_t full_walk_lanes, full_walk_waves, many_group_waves, list_entries;
+    /* how the per-sweep bookkeeping ran (DESIGN.md §5 "Fewer launches per sweep"): max-likelihood checks folded
+     * into the data-parallel step (cumulative), candidate-list rebuilds by the conditional step tail (steps whose
+     * counts moved beyond the lists' slack), and steps that kept the lists of the last build */
+    int64_t folded_checks, tail_list_builds, tail_steps;
 } np8_stats_t;
 
 /* Create / destroy.  Replaces NealAlgorithm8::NealAlgorithm8 (np_neal_algorithm8.cpp:17-34). */

@@ -92,6 +92,30 @@ struct np8_ctx {
     bool fuse_off = false;
     bool queue_on = false;  // NP8_QUEUE=1: launch np8_assign_queue after the fast kernel even when no lane can defer
     bool pruned_last = false;    // the sweep's last step built the lists (end_sweep's prune already done)
+    // conditional candidate lists (np8_step_tail, TailArgs::prune = 2): the lists of the last build are kept while
+    // the counts stay within kListSlack of it; NP8_LISTS_ALWAYS=1 rebuilds them every step (A/B runs)
+    double *lb = nullptr;        // [2][kcap] log n | log(n - 1) per slot at the last list build
+    bool tailcond_off = false;
+    // folded max-likelihood check (DESIGN.md "Max likelihood"): on check sweeps np8_assign_fast sums the items'
+    // log-likelihoods per wave (llpart), finalize (or np8_req_select, per rank) reduces them and decides the
+    // snapshot, which the next np8_assign_fast copies (snap_lazy: such a copy may be pending on the device, flushed
+    // by np8_snapshot_flush before anything else touches the labels); NP8_NO_LLFOLD=1: the separate kernels
+    double *llpart = nullptr;    // [waves]
+    bool llfold_off = false;
+    bool step_ll = false;        // the running step folds the check in
+    bool step_snap = false;      // the running step's assign consumes a pending snapshot
+    bool sweep_ll = false;       // this sweep's check was folded into its step
+    bool snap_lazy = false;
+    int64_t n_folded = 0, n_tail_cond = 0;  // (np8_stats; replays of a captured graph add the graph's counts)
+    int64_t cap_folded = 0, cap_tail = 0, graph_folded = 0, graph_tail = 0;
+    bool host_exch_step = false; // np8_step_local's assign: the host exchange keeps the separate check kernels
+    // re-sorts outside the sweep graphs: the graphs carry no periodic re-sort check; before a replay the host looks at
+    // ctl->moved as the last finalize mirrored it (host-mapped, one replay behind) and re-sorts when more than n/32
+    // items moved (the layout changes no result).  NP8_SORT_IN_GRAPH=1: the check every resort_every-th sweep inside
+    int64_t *moved_host = nullptr, *moved_dev = nullptr;
+    bool sort_in_graph = false;
+    uint32_t fin_advance = 0;    // the next finalize advances ctl->t_base (a captured graph's last step)
+    bool fin_advanced = false;
 
     // data-parallel sweep in `substeps` synchronous sub-steps (np8_config.substeps): sub-step s is the
     // contiguous range [sub_start[s], sub_start[s+1]) of the label-sorted layout (sorted by sub-step, slot)
@@ -154,6 +178,7 @@ struct np8_ctx {
     int graph_timing = 0;
     bool capturing = false, graphs_off = false;
     std::vector<Timer> graph_timers;
+    bool graph_snap0 = false, graph_snap1 = false;  // snap_lazy when the graph's sweeps start and end
     // multi-GPU
     ncclComm_t comm = nullptr;
     int rank = 0, world = 1;
@@ -448,10 +473,12 @@ void free_device(np8_ctx *c) {
                     c->sm_typ, c->sm_slist, c->sm_stheta, c->stage, c->evalc, c->z_base, c->cnt_base,
                     c->chg_slot, c->mu_base, c->sigma_base, c->chg_item, c->chg_count, c->chg_flags,
                     c->inv_hist, c->inv_out, c->queue, c->qcount, c->qlist, c->slot_logn1, c->plen_s,
-                    c->plr2_s, c->sm_mb};
+                    c->plr2_s, c->sm_mb, c->lb, c->llpart};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     if (c->sm_first_host) (void)hipHostFree(c->sm_first_host);
+    if (c->moved_host) (void)hipHostFree(c->moved_host);
+    c->moved_host = c->moved_dev = nullptr;
     c->sm_hist = c->sm_mem = c->sm_off = c->sm_live = nullptr;
     c->sm_Xm = c->sm_ownm = c->sm_cross = nullptr;
     c->sm_slist = nullptr;
@@ -468,6 +495,7 @@ void free_device(np8_ctx *c) {
     }
     c->s_hist = c->s_cursor = c->s_off = nullptr;
     c->slot_iso = nullptr;
+    c->lb = c->llpart = nullptr;
     c->acc = nullptr;
     c->r2 = nullptr;
     c->wr2 = nullptr;
@@ -676,6 +704,19 @@ FinArgs fin_args(np8_ctx *c, const unsigned char *recs, int world) {
     F.pad3 = 0;
     F.hyp = c->hyp;
     F.wdirty = c->wdirty;
+    F.ll_on = c->step_ll ? 1 : 0;
+    F.ll_rec = c->comm ? 1 : 0;
+    F.llpart = c->llpart;
+    F.ll_n = c->assign_waves;
+    F.snap_clear = c->step_snap ? 1 : 0;
+    F.par = c->checks & 1;
+    F.best = c->ctl->best;
+    F.have_best = &c->ctl->have_best;
+    F.lb = c->lb;
+    F.moved_mirror = c->moved_dev;
+    F.advance = c->fin_advance;
+    if (c->fin_advance) c->fin_advanced = true;
+    c->fin_advance = 0;
     return F;
 }
 
@@ -789,11 +830,49 @@ AssignArgs assign_args(np8_ctx *c, int64_t p0, int64_t p1, const int64_t *order,
     A.slot_logn1 = c->slot_logn1;
     A.plen_s = c->plen_s;
     A.plr2_s = c->plr2_s;
+    A.llpart = c->llpart;
+    A.gp0 = c->Gp[0];
+    A.z_best = c->z_best;
+    A.cnt_best = c->cnt_best;
+    A.mu_best = c->mu_best;
+    A.sigma_best = c->sigma_best;
+    A.cnt = c->cnt;
+    A.slot_sigma = c->slot_sigma;
     return A;
 }
 
 PruneArgs prune_args(np8_ctx *c, bool last);
 int launch_prune(np8_ctx *c, bool last);
+
+SnapArgs snap_args(np8_ctx *c) {
+    SnapArgs S;
+    S.L = &c->ctl->L;
+    S.best = c->ctl->best;
+    S.have_best = &c->ctl->have_best;
+    S.par = c->checks & 1;
+    S.z = c->z;
+    S.cnt = c->cnt;
+    S.z_best = c->z_best;
+    S.cnt_best = c->cnt_best;
+    S.slot_mu = c->slot_mu;
+    S.slot_sigma = c->slot_sigma;
+    S.mu_best = c->mu_best;
+    S.sigma_best = c->sigma_best;
+    S.n_loc = c->n_loc;
+    S.kcap = c->kcap;
+    S.D = c->D;
+    return S;
+}
+
+// A snapshot the folded check may have left for the next np8_assign_fast: copied now, before anything else reads
+// or changes the labelling (every entry point but the data-parallel sweep's own continuation).
+int flush_snapshot(np8_ctx *c) {
+    if (!c->snap_lazy) return NP8_OK;
+    c->snap_lazy = false;
+    HIPC(c, np8_launch_snapshot_flush(snap_args(c), c->ctl, c->stream));
+    HIPC(c, hipMemsetAsync(&c->ctl->snap_pend, 0, sizeof(int32_t), c->stream));
+    return NP8_OK;
+}
 
 // prune: -1 none; 0 / 1 the candidate lists right after finalize, in the same launch (np8_step_tail), as
 // launch_prune(c, false / true) would build them -- the frozen reference-prior sweep, where nothing changes the
@@ -805,8 +884,13 @@ int launch_finalize(np8_ctx *c, const unsigned char *recs, int world, int prune 
     // the one-workgroup tail (finalize + lists) on the sweeps that do not gather radii: a gathering sweep's fold
     // needs every assign record, i.e. a multi-workgroup launch whose last workgroup would run the serial part
     // behind agent-scope fences (their L2 writeback costs more than the dispatch it saves, §5)
-    const bool tail = !c->fuse_off && prune >= 0 && !c->gather && !c->wide && c->prior == NP8_PRIOR_REFERENCE;
-    if (tail) {  // radius fold, finalize (+ lists) in one launch
+    // the conditional form (the default): the lists of the last build stay when finalize finds every count within
+    // kListSlack of it -- the frozen reference-prior sweep's step with valid lists; a rebuild then costs the one
+    // workgroup what np8_prune does in parallel, so steps after which the lists are stale anyway keep np8_prune
+    const bool cond = !c->tailcond_off && prune >= 0 && !c->gather && !c->wide && c->prior == NP8_PRIOR_REFERENCE &&
+                      c->param_update == NP8_PARAM_FROZEN && c->lists_valid;
+    const bool tail = cond || (!c->fuse_off && prune >= 0 && !c->gather && !c->wide && c->prior == NP8_PRIOR_REFERENCE);
+    if (tail) {  // finalize (+ lists) in one launch
         TailArgs T;
         std::memset(&T, 0, sizeof(T));
         T.fold = 0;
@@ -816,7 +900,9 @@ int launch_finalize(np8_ctx *c, const unsigned char *recs, int world, int prune 
         std::memset(&P, 0, sizeof(P));
         if (prune >= 0) {
             P = prune_args(c, prune == 1);
-            T.prune = 1;
+            T.prune = cond ? 2 : 1;
+            F.slack_test = cond ? 1 : 0;
+            if (cond) (c->capturing ? c->cap_tail : c->n_tail_cond) += 1;
         }
         AssignArgs A = assign_args(c, 0, 0, nullptr, false);  // the radius records (wr2)
         HIPC(c, np8_launch_step_tail(A, F, P, T, c->assign_waves, c->D, c->M, c->stream));
@@ -867,6 +953,22 @@ int launch_assign(np8_ctx *c, int64_t p0, int64_t p1, const int64_t *order, bool
     A.collect_r2 = c->gather ? 1 : 0;
     A.use_lists = (c->collecting && c->lists_valid) ? 1 : 0;
     c->assign_waves = (p1 - p0 + 63) / 64;
+    // the fast kernel over the whole sweep, every row isotropic: it can fold the max-likelihood check in (frozen
+    // parameters: the labels after the step are what the check scores) and take a pending snapshot along
+    const bool fast = !c->wide && c->diag_U && !c->fast_off && c->prior == NP8_PRIOR_REFERENCE && A.sorted && !order &&
+                      !use_perm;
+    const bool whole = fast && c->substeps == 1 && p0 == 0 && p1 == c->n_loc && c->rows_iso && !A.count_eval &&
+                       !c->queue_on && (c->world == 1 || c->comm) && !c->host_exch_step;
+    c->step_ll = whole && !c->llfold_off && c->param_update == NP8_PARAM_FROZEN && c->gp_iso > 0.0 &&
+                 c->epoch % 5u == 0u && c->llpart;
+    if (c->snap_lazy && (!whole || c->step_ll)) {  // (a check sweep never follows a check sweep)
+        int r = flush_snapshot(c);
+        if (r) return r;
+    }
+    c->step_snap = c->snap_lazy;  // consumed by this step's assign, cleared by its finalize
+    c->snap_lazy = false;
+    A.ll_on = c->step_ll ? 1 : 0;
+    A.snap_on = c->step_snap ? 1 : 0;
     if (c->wide) {
         if (c->wdist && !c->wide_prune_off) {  // distances between the current rows' means (pruning)
             HIPC(c, np8_launch_wide_dist(wide_args(c), c->stream));
@@ -908,6 +1010,7 @@ PruneArgs prune_args(np8_ctx *c, bool last) {
     P.ls = c->kcap;
     P.D = c->D;
     P.kcap = c->kcap;
+    P.lb = c->lb;
     P.gathered = (last && c->gather) ? 1 : 0;
     // the next sweep gathers: clear its buffer here instead of with a memset node at its start (a stale
     // buffer would only raise radii: pruning stays exact)
@@ -926,9 +1029,7 @@ int launch_prune(np8_ctx *c, bool last) {
 // Label-sorted layout for the synchronous sweep: rebuilt from the item-order arrays when stale
 // (after a state upload or a chunked / per-item step), refreshed from itself every resort_every
 // sweeps so that items that moved cluster rejoin their group.
-int prepare_sorted(np8_ctx *c) {
-    const bool stale = !c->sorted_valid;
-    if (!stale && c->epoch % c->resort_every != 0) return NP8_OK;
+int launch_resort(np8_ctx *c, bool stale) {
     SortArgs S;
     S.X = c->X;
     S.z = c->z;
@@ -954,6 +1055,16 @@ int prepare_sorted(np8_ctx *c) {
     c->sorted_valid = true;
     return NP8_OK;
 }
+
+int prepare_sorted(np8_ctx *c) {
+    const bool stale = !c->sorted_valid;
+    if (!stale && c->epoch % c->resort_every != 0) return NP8_OK;
+    if (!stale && c->capturing && !c->sort_in_graph) return NP8_OK;  // (np8_sweep re-sorts between replays)
+    return launch_resort(c, stale);
+}
+
+// np8_sweep before a graph replay: the device's own check (> n/32 items moved since the last sort)
+int prepare_sorted_now(np8_ctx *c) { return launch_resort(c, !c->sorted_valid); }
 
 // One synchronous step over local positions [p0,p1): assign, exchange, finalize.  A whole-sweep
 // step (no order, no permutation) runs on the label-sorted layout.
@@ -994,15 +1105,19 @@ int step(np8_ctx *c, int64_t p0, int64_t p1, const int64_t *order, bool use_perm
     // the lists right after finalize (np8_step_tail) when nothing changes the table in between: the next sub-step's
     // (radii in use), or the sweep's when its parameters are frozen (end_sweep's prune)
     const bool mid = sub >= 0 && sub + 1 < c->substeps;
-    const int fprune = (c->collecting && (!c->fuse_off || !c->fp_off) && !c->wide && c->prior == NP8_PRIOR_REFERENCE &&
+    const int fprune = (c->collecting && (!c->fuse_off || !c->fp_off || !c->tailcond_off) && !c->wide &&
+                        c->prior == NP8_PRIOR_REFERENCE &&
                         (mid || c->param_update == NP8_PARAM_FROZEN)) ? (mid ? 0 : 1) : -1;
     if (c->comm) {  // the exchange over RCCL (also with a one-rank communicator)
-        HIPC(c, np8_launch_req_select(c->stage, c->stage_cap, c->rec, c->rec_cap, c->kcap, c->D, c->req_max, c->stream));
+        HIPC(c, np8_launch_req_select(c->stage, c->stage_cap, c->rec, c->rec_cap, c->kcap, c->D, c->req_max,
+                                      c->step_ll ? c->llpart : nullptr, c->assign_waves, c->stream));
         NCCLC(c, ncclAllGather(c->rec, c->gath, (size_t)c->rec_bytes, ncclUint8, c->comm, c->stream));
         r = launch_finalize(c, c->gath, c->world, fprune);
     } else {
         r = launch_finalize(c, c->rec, 1, fprune);
     }
+    c->sweep_ll = c->sweep_ll || c->step_ll;
+    c->step_ll = c->step_snap = false;
     if (r) return r;
     if (fprune >= 0) {
         c->pruned_last = fprune == 1;
@@ -1171,27 +1286,19 @@ int end_sweep(np8_ctx *c, bool stats_given = false) {
     c->pruned_last = false;
     if (c->debug_inv && (r0 = launch_invariants(c))) return r0;
     if (c->epoch % 5u == 0u) {  // np_mcmc.cpp:172-174
-        int r = launch_total_loglik(c);
-        if (r) return r;
-        SnapArgs S;
-        S.L = &c->ctl->L;
-        S.best = c->ctl->best;
-        S.have_best = &c->ctl->have_best;
-        S.par = c->checks & 1;
-        S.z = c->z;
-        S.cnt = c->cnt;
-        S.z_best = c->z_best;
-        S.cnt_best = c->cnt_best;
-        S.slot_mu = c->slot_mu;
-        S.slot_sigma = c->slot_sigma;
-        S.mu_best = c->mu_best;
-        S.sigma_best = c->sigma_best;
-        S.n_loc = c->n_loc;
-        S.kcap = c->kcap;
-        S.D = c->D;
-        HIPC(c, np8_launch_snapshot(S, c->stream));
+        if (c->sweep_ll) {  // folded into the step: decided by its finalize, copied by the next np8_assign_fast
+            c->snap_lazy = true;
+            (c->capturing ? c->cap_folded : c->n_folded) += 1;
+        } else {
+            int r = flush_snapshot(c);
+            if (r) return r;
+            r = launch_total_loglik(c);
+            if (r) return r;
+            HIPC(c, np8_launch_snapshot(snap_args(c), c->stream));
+        }
         c->checks += 1;
     }
+    c->sweep_ll = false;
     c->epoch += 1;
     return NP8_OK;
 }
@@ -1254,11 +1361,24 @@ int capture_graph(np8_ctx *c) {
     }
     c->capturing = true;
     c->capture_timed_left = c->time_all ? (int)kGraphSweeps * c->substeps : 1;
+    const bool snap0 = c->snap_lazy;
+    c->cap_folded = c->cap_tail = 0;
+    // the epoch advance in the last step's finalize when nothing after it reads t_base (frozen reference-prior sweep
+    // of one step); otherwise np8_advance_epoch ends the graph
+    const bool adv_fin = c->substeps == 1 && c->param_update == NP8_PARAM_FROZEN && !c->wide &&
+                         c->prior == NP8_PRIOR_REFERENCE;
+    c->fin_advanced = false;
     for (uint32_t i = 0; i < kGraphSweeps && !r; ++i) {
+        if (adv_fin && i + 1 == kGraphSweeps) c->fin_advance = kGraphSweeps;
         r = population(c);
         if (!r) r = end_sweep(c);
     }
-    if (!r && np8_launch_advance_epoch(c->ctl, kGraphSweeps, c->stream) != hipSuccess) r = NP8_ERR_HIP;
+    c->fin_advance = 0;
+    const bool snap1 = c->snap_lazy;
+    c->snap_lazy = snap0;
+    if (!r && !c->fin_advanced && np8_launch_advance_epoch(c->ctl, kGraphSweeps, c->stream) != hipSuccess)
+        r = NP8_ERR_HIP;
+    c->fin_advanced = false;
     hipGraph_t g = nullptr;
     const hipError_t ee = hipStreamEndCapture(c->stream, &g);
     c->capturing = false;
@@ -1271,6 +1391,10 @@ int capture_graph(np8_ctx *c) {
         g = nullptr;
         c->graph_par = ch0 & 1;
         c->graph_phase = (int)(e0 % kGraphSweeps);
+        c->graph_snap0 = snap0;
+        c->graph_snap1 = snap1;
+        c->graph_folded = c->cap_folded;
+        c->graph_tail = c->cap_tail;
         c->graph_timing = (c->timing ? 1 : 0) | (c->count_eval ? 2 : 0) | (c->time_all ? 4 : 0);
     } else {
         c->graph_timers.clear();
@@ -1285,6 +1409,7 @@ int capture_graph(np8_ctx *c) {
 // phase, check parity or timing setting).
 int ensure_graph(np8_ctx *c) {
     if (!c->graph || c->graph_par != (c->checks & 1) || c->graph_phase != (int)(c->epoch % kGraphSweeps) ||
+        c->graph_snap0 != c->snap_lazy ||
         c->graph_timing != ((c->timing ? 1 : 0) | (c->count_eval ? 2 : 0) | (c->time_all ? 4 : 0)))
         return capture_graph(c);
     return NP8_OK;
@@ -1306,6 +1431,9 @@ int run_graph(np8_ctx *c) {
     }
     HIPC(c, hipGraphLaunch(c->graph, c->stream));
     for (const Timer &t : sampled) c->timers.push_back(t);
+    c->snap_lazy = c->graph_snap1;
+    c->n_folded += c->graph_folded;
+    c->n_tail_cond += c->graph_tail;
     c->epoch += kGraphSweeps;
     c->checks += (int32_t)(kGraphSweeps / 5);
     c->t_base += kGraphSweeps;
@@ -1412,6 +1540,19 @@ int np8_create(np8_ctx **out, const np8_config *cfg) {
     }
     c->fuse_off = std::getenv("NP8_FUSE") == nullptr;  // opt-in: measured slower than separate launches
     c->queue_on = std::getenv("NP8_QUEUE") != nullptr;
+    c->tailcond_off = std::getenv("NP8_LISTS_ALWAYS") != nullptr;
+    c->sort_in_graph = std::getenv("NP8_SORT_IN_GRAPH") != nullptr;
+    if (!c->sort_in_graph) {  // host-mapped mirror of ctl->moved (written by every finalize)
+        if (hipHostMalloc((void **)&c->moved_host, sizeof(int64_t), hipHostMallocMapped) != hipSuccess ||
+            hipHostGetDevicePointer((void **)&c->moved_dev, c->moved_host, 0) != hipSuccess) {
+            if (c->moved_host) (void)hipHostFree(c->moved_host);
+            c->moved_host = c->moved_dev = nullptr;
+            c->sort_in_graph = true;
+        } else {
+            *c->moved_host = 0;
+        }
+    }
+    c->llfold_off = std::getenv("NP8_NO_LLFOLD") != nullptr;
     c->rec_cap = c->req_max;  // grown to the item count by np8_set_data (one rank)
     c->rec_bytes = record_bytes(c->kcap, (int)c->rec_cap, c->D);
     int r = 0;
@@ -1427,6 +1568,7 @@ int np8_create(np8_ctx **out, const np8_config *cfg) {
         (r = dalloc(c, &c->rec, (size_t)c->rec_bytes)) || (r = dalloc(c, &c->evalc, (size_t)8 * kEvalSlots)) ||
         (c->param_update != NP8_PARAM_FROZEN && (r = dalloc(c, &c->acc, (size_t)kc * (D + DP)))) ||
         (kc <= kPruneMaxKcap && ((r = dalloc(c, &c->r2, 2 * (size_t)kc)) || (r = dalloc(c, &c->plen, (size_t)kc)) ||
+                                 (r = dalloc(c, &c->lb, 2 * (size_t)kc)) ||
                                 (r = dalloc(c, &c->plr2, (size_t)kc)) ||
                                  (r = dalloc(c, &c->plist, (size_t)kc * kc))))) {
         free_device(c);
@@ -1530,6 +1672,7 @@ int np8_set_data(np8_ctx *c, const double *X, int64_t n, int32_t D, int64_t offs
         return fail(c, NP8_ERR_ARG, "np8_set_data: shard outside [0, n_global) or n_global >= 2^31");
     drop_graph(c);
     c->lists_valid = c->r2_zero = c->collecting = false;
+    c->snap_lazy = false;  // (no state any more)
     c->n_loc = n;
     c->offset = offset;
     c->n_glob = n_global;
@@ -1537,6 +1680,7 @@ int np8_set_data(np8_ctx *c, const double *X, int64_t n, int32_t D, int64_t offs
     const size_t nx = c->wide ? ((size_t)n * D + 1) / 2 : (size_t)n * D;  // wide path: fp32 items
     if ((r = dalloc(c, &c->X, nx)) || (r = dalloc(c, &c->z, (size_t)n)) ||
         (r = dalloc(c, &c->z_best, (size_t)n)) || (r = dalloc(c, &c->wr2, (size_t)((n + 63) / 64))) ||
+        (r = dalloc(c, &c->llpart, (size_t)((n + 63) / 64))) ||
         (r = dalloc(c, &c->queue, (size_t)(64 * ((n + 63) / 64) + 64))) ||
         (r = dalloc(c, &c->qcount, (size_t)((n + 63) / 64 + 1))) ||
         (r = dalloc(c, &c->qlist, (size_t)((n + 63) / 64 + 1))))
@@ -1597,6 +1741,7 @@ static int set_state_common(np8_ctx *c, const std::vector<SlotHost> &slots, cons
         HIPC(c, e);
     }
     HIPC(c, hipMemcpyAsync(c->z, zloc.data(), sizeof(int32_t) * zloc.size(), hipMemcpyHostToDevice, c->stream));
+    c->snap_lazy = false;  // the snapshot restarts with the state (reset_ctl)
     c->sorted_valid = false;
     c->use_sorted = false;
     c->lists_valid = c->r2_zero = c->collecting = false;
@@ -1711,6 +1856,12 @@ int np8_sweep(np8_ctx *c, int32_t n_sweeps) {
             int r = ensure_graph(c);
             if (r) return r;
             if (c->graph) {
+                if (!c->sort_in_graph && c->moved_host && (*(volatile int64_t *)c->moved_host) * 32 > c->n_loc) {
+                    // the layout went stale (as of a replay ago): re-sort before this one (the device re-checks)
+                    int r = prepare_sorted_now(c);
+                    if (r) return r;
+                    *(volatile int64_t *)c->moved_host = 0;  // (until a finalize reports again)
+                }
                 int r = run_graph(c);
                 if (r) return r;
                 s += (int)kGraphSweeps - 1;
@@ -1804,8 +1955,10 @@ int np8_checkpoint(np8_ctx *c, void *out, int64_t bytes) {
     if (!c || !out) return NP8_ERR_ARG;
     if (!c->have_state) return fail(c, NP8_ERR_STATE, "np8_checkpoint: no state");
     if (bytes < np8_checkpoint_bytes(c)) return fail(c, NP8_ERR_ARG, "np8_checkpoint: buffer too small");
+    int r = flush_snapshot(c);
+    if (r) return r;
     Ctl h;
-    int r = read_ctl(c, &h);
+    r = read_ctl(c, &h);
     if (r) return r;
     CkptHeader H;
     std::memset(&H, 0, sizeof(H));
@@ -1867,6 +2020,7 @@ int np8_restore(np8_ctx *c, const void *in, int64_t bytes) {
         p += q.bytes;
     }
     c->rows_iso = false;  // raw slot tables: isotropy unknown (np8_assign_queue stays in)
+    c->snap_lazy = false;  // the snapshot buffers are the checkpoint's
     c->sorted_valid = false;
     c->use_sorted = false;
     c->lists_valid = c->r2_zero = c->collecting = false;
@@ -1930,6 +2084,7 @@ int np8_changes(np8_ctx *c, int64_t item_cap, int64_t *item, int32_t *slot, int3
     std::memset(out, 0, sizeof(*out));
     if (!c->track) return fail(c, NP8_ERR_STATE, "np8_changes: change tracking is off (np8_track_changes)");
     if (!c->have_state) return fail(c, NP8_ERR_STATE, "np8_changes: no state");
+    if (int r = flush_snapshot(c)) return r;
     if (item_cap < 0 || (item_cap > 0 && (!item || !slot)) || !created || !removed || !updated)
         return fail(c, NP8_ERR_ARG, "np8_changes: bad arguments");
     const int D = c->D, kc = c->kcap;
@@ -2012,6 +2167,7 @@ int np8_update_points(np8_ctx *c, const int64_t *ids, int64_t n) {
     if (!c->have_state) return fail(c, NP8_ERR_STATE, "np8_update_points: no state");
     if (c->world > 1) return fail(c, NP8_ERR_ARG, "np8_update_points: single-rank only");
     if (n <= 0) return NP8_OK;
+    if (int r = flush_snapshot(c)) return r;
     for (int64_t k = 0; k < n; ++k)
         if (ids[k] < 0 || ids[k] >= c->n_loc) return fail(c, NP8_ERR_RANGE, "np8_update_points: id out of range");
     if (n > c->order_cap) {
@@ -2072,8 +2228,10 @@ int np8_sync(np8_ctx *c) {
 int np8_get_state(np8_ctx *c, int32_t which, int32_t *z, int32_t *K, double *mu, double *Sigma, int64_t *counts) {
     if (!c) return NP8_ERR_ARG;
     if (!c->have_state) return fail(c, NP8_ERR_STATE, "np8_get_state: no state");
+    int r = flush_snapshot(c);
+    if (r) return r;
     Ctl h;
-    int r = read_ctl(c, &h);
+    r = read_ctl(c, &h);
     if (r) return r;
     if (which == 1 && !h.have_best) return fail(c, NP8_ERR_STATE, "np8_get_state: no max-likelihood snapshot yet");
     const int D = c->D, kc = c->kcap;
@@ -2191,6 +2349,9 @@ int np8_stats(np8_ctx *c, np8_stats_t *out) {
     out->n_timed_sm_eval = c->n_timed[5];
     out->mh_accepted = h.mh_accepted;
     out->screen_violations = (int64_t)h.n_screen_viol;
+    out->folded_checks = c->n_folded;
+    out->tail_list_builds = (int64_t)h.list_builds;
+    out->tail_steps = c->n_tail_cond;
     {
         std::vector<unsigned long long> ev((size_t)8 * kEvalSlots);
         HIPC(c, hipMemcpy(ev.data(), c->evalc, sizeof(unsigned long long) * ev.size(), hipMemcpyDeviceToHost));
@@ -2272,10 +2433,13 @@ int np8_step_local(np8_ctx *c, void *record_out) {
     }
     c->collecting = false;  // no pruning on the host-exchange path
     c->lists_valid = c->r2_zero = false;
+    c->host_exch_step = true;
     int r = launch_assign(c, p0, p1, nullptr, false);
+    c->host_exch_step = false;
     if (r) return r;
     if (c->stage)
-        HIPC(c, np8_launch_req_select(c->stage, c->stage_cap, c->rec, c->rec_cap, c->kcap, c->D, c->req_max, c->stream));
+        HIPC(c, np8_launch_req_select(c->stage, c->stage_cap, c->rec, c->rec_cap, c->kcap, c->D, c->req_max, nullptr, 0,
+                                      c->stream));
     HIPC(c, hipMemcpyAsync(record_out, c->rec, (size_t)c->rec_bytes, hipMemcpyDeviceToHost, c->stream));
     HIPC(c, hipStreamSynchronize(c->stream));
     return NP8_OK;
@@ -2434,7 +2598,9 @@ static int split_merge_sweeps(np8_ctx *c, int32_t n_sweeps, bool triadic) {
     if (c->wide || c->prior != NP8_PRIOR_REFERENCE)
         return fail(c, NP8_ERR_ARG, std::string(who) + ": needs the reference prior and the fp64 contraction");
     if (c->n_loc > INT32_MAX) return fail(c, NP8_ERR_ARG, std::string(who) + ": at most 2^31-1 items");
-    int r = sm_buffers(c);
+    int r = flush_snapshot(c);
+    if (r) return r;
+    r = sm_buffers(c);
     if (r) return r;
     const int64_t N = c->n_loc;
     for (int s = 0; s < n_sweeps; ++s) {

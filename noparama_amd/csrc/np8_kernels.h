@@ -39,7 +39,16 @@ struct Ctl {
     uint32_t pad3;
     uint32_t fin_flag;    // np8_fin_prune: finalize done (set by workgroup 0, reset by the last list workgroup)
     uint32_t prune_exit;  // np8_fin_prune: list workgroups finished
+    // folded max-likelihood check (DESIGN.md "Max likelihood"): the check sweep's finalize found an improvement;
+    // the next np8_assign_fast copies the labelling into the snapshot buffers (or np8_snapshot_flush does)
+    int32_t snap_pend;
+    uint32_t list_builds;  // candidate-list builds by the conditional step tail (diagnostics)
 };
+
+// Candidate lists are built with kListSlack nats of extra margin, so a list stays exact while no live slot's
+// log n or log(n - 1) moves by more than kListSlack / 2 from its value at the build (np8_step_tail's
+// conditional rebuild, DESIGN.md "Candidate pruning").
+constexpr double kListSlack = 2.0;
 
 // Executed work of np8_assign when AssignArgs::count_eval is set (timing mode): per wave, the cluster
 // quadratic forms its items evaluated (own rows included) and how many took the isotropic form, added
@@ -60,7 +69,8 @@ enum : int32_t { kErrCapacity = 1, kErrSigma = 2, kErrInvariant = 4, kErrQueue =
 // can accept from it (DESIGN.md "Finalize").
 struct RecHeader {
     int32_t nreq;
-    int32_t pad[3];
+    int32_t pad;
+    double L_local;  // folded max-likelihood check: this rank's sum of log-likelihoods (np8_req_select)
 };
 constexpr int kRecHeaderBytes = 16;
 
@@ -71,6 +81,7 @@ struct Request {
     int32_t zold;  // slot the item leaves
     int32_t lpos;  // position in the owner's label-sorted layout (-1: none)
     int32_t pad;
+    double dll;    // folded max-likelihood check: ll under the new slot - ll under zold (added if accepted)
 };
 
 // Item keys (DESIGN.md "Randomness"): the Philox item counter of every per-item draw is
@@ -150,6 +161,17 @@ struct AssignArgs {
     // np8_assign_fast: the host launches no np8_assign_queue after it (every live row isotropic, so no lane is
     // deferred; a deferred lane would set kErrQueue)
     int32_t no_queue, pad_nq;
+    // np8_assign_fast, folded max-likelihood check (frozen parameters): ll_on = this sweep is a check sweep: each
+    // wave stores the sum of its items' log-likelihoods under their new label in llpart[wave] (a requester counts
+    // under its old slot; its Request carries the difference); snap_on = a snapshot may be pending
+    // (ctl->snap_pend): copy the labelling as it stands before this sweep into the snapshot buffers
+    double *llpart = nullptr;
+    int32_t ll_on = 0, snap_on = 0;
+    double gp0 = 0.0;  // Gp[0]: a new slot's isotropic precision is gp0 / v^2 (np8_finalize's write_new_slot)
+    int32_t *z_best = nullptr, *cnt_best = nullptr;
+    double *mu_best = nullptr, *sigma_best = nullptr;
+    const int32_t *cnt = nullptr;
+    const double *slot_sigma = nullptr;
 };
 
 // Wide-path tables (np8_wide.hip), maintained for the slots flagged in dirty.
@@ -180,6 +202,7 @@ struct PruneArgs {
     int32_t gathered;   // the sweep's last step of a gathering sweep: lists from the gathered radii, which
                         // then become the radii in use
     int32_t clear_next; // (not gathered) zero the gathered buffer for the next sweep, which gathers
+    double *lb = nullptr;  // [2][kcap]: log n | log(n - 1) of each listed row's slot at the build (kListSlack test)
 };
 
 struct FinArgs {
@@ -211,6 +234,20 @@ struct FinArgs {
     int32_t frame_payload, pad3;
     const double *hyp;
     int32_t *wdirty;
+    // folded max-likelihood check (AssignArgs::ll_on): L = sum of the per-wave partials (one rank, ll_rec = 0) or of
+    // the records' L_local (rank order, ll_rec = 1), plus the accepted requests' dll; snapshot decision on best[par]
+    const double *llpart = nullptr;
+    int64_t ll_n = 0;
+    int32_t ll_on = 0, ll_rec = 0;
+    int32_t snap_clear = 0, par = 0;  // snap_clear: the step's assign consumed ctl->snap_pend
+    double *best = nullptr;
+    int32_t *have_best = nullptr;
+    // conditional candidate lists (np8_step_tail, TailArgs::prune == 2): the lists of the last build stay exact while
+    // every live slot's log n and log(n - 1) are within kListSlack / 2 of lb (PruneArgs::lb) and no slot changed
+    const double *lb = nullptr;
+    int32_t slack_test = 0;
+    uint32_t advance = 0;               // ctl->t_base += advance at the end (a captured graph's last step)
+    int64_t *moved_mirror = nullptr;    // host-mapped copy of ctl->moved (the host's re-sort decision), or null
 };
 
 // Wave-aggregated atomics on a few hot addresses (count deltas, gathered radii): one atomic per distinct key
@@ -357,7 +394,8 @@ struct TailArgs {
     int32_t fold;    // the step's radius records (AssignArgs::wr2, fold_n of them) into the gathered radii
     int32_t select;  // np8_req_select: staging record -> exchanged record (sharded step; no finalize then)
     int32_t fin;     // np8_finalize (FinArgs)
-    int32_t prune;   // np8_prune after it (PruneArgs; the frozen reference-prior sweep)
+    int32_t prune;   // np8_prune after it (PruneArgs; the frozen reference-prior sweep): 1 always, 2 only when
+                     // finalize finds the last lists stale (FinArgs::slack_test)
     int32_t pad;
     int64_t fold_n;
     int64_t lds_bytes;  // dynamic LDS of the launch (np8_finalize_lds_bytes; prune_block stages rows in it)
@@ -483,7 +521,9 @@ hipError_t np8_launch_finalize(const np8::FinArgs &F, hipStream_t s);
 hipError_t np8_launch_step_tail(const np8::AssignArgs &A, const np8::FinArgs &F, const np8::PruneArgs &P,
                                 const np8::TailArgs &T, int64_t n_waves, int D, int M, hipStream_t s);
 hipError_t np8_launch_req_select(const unsigned char *stage, int64_t stage_cap, unsigned char *rec, int64_t rec_cap,
-                                 int kcap, int D, int req_max, hipStream_t s);
+                                 int kcap, int D, int req_max, const double *llpart, int64_t ll_n, hipStream_t s);
+// A snapshot the folded max-likelihood check left pending (ctl->snap_pend): copy it now and clear the flag.
+hipError_t np8_launch_snapshot_flush(const np8::SnapArgs &A, np8::Ctl *ctl, hipStream_t s);
 hipError_t np8_launch_loglik(const np8::LoglikArgs &A, int D, hipStream_t s);
 hipError_t np8_launch_loglik_reduce(const double *partial, int64_t nb, double *out, double *out2, hipStream_t s);
 hipError_t np8_launch_snapshot(const np8::SnapArgs &A, hipStream_t s);

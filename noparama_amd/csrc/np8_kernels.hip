@@ -118,7 +118,7 @@ __device__ __forceinline__ double niw_aux_ll(const double *__restrict__ hyp, dou
 // interval away from 0; tests/test_gpu_screen.py drives many lanes into |v| in [0.02, 0.25] in count mode.
 template <int D>
 __device__ __forceinline__ float aux_screen_ub(const uint32_t (&w)[4], float chi_extra, float chi_extra_err, float ny,
-                                               float nu, float rsk, float caux, float thr) {
+                                               float nu, float rsk, float caux, float thr, bool with_thr = true) {
     constexpr float kLn2 = 0.693147180559945f;
     constexpr int k = (D - 1) / 2;
     const float u0 = fmaf((float)w[0], 0x1.0p-32f, 0x1.0p-33f);
@@ -146,7 +146,9 @@ __device__ __forceinline__ float aux_screen_ub(const uint32_t (&w)[4], float chi
     const float rsk2 = rsk * rsk;
     const float qlb = fmaf(amin, amin, rsk2 * fmaxf(chi - chi_extra_err, 0.0f));
     const float ub_ll = fmaf(-0.5f, qlb, caux - (float)D * lnv);
-    const float err = 1.0f + 1e-4f * (qlb + fabsf(caux) + (float)D * fabsf(lnv) + fabsf(thr));
+    // with_thr = false: the margin without the threshold's own term, which the caller adds once thr is known
+    // (np8_assign_fast screens before its own row is loaded: ub + 1e-4 |thr| <= thr)
+    const float err = 1.0f + 1e-4f * (qlb + fabsf(caux) + (float)D * fabsf(lnv) + (with_thr ? fabsf(thr) : 0.0f));
     return (av_lo >= 0.02f) ? ub_ll + err : __builtin_inff();
 }
 
@@ -559,6 +561,7 @@ __device__ __forceinline__ void assign_item(const AssignArgs &A, const int64_t p
             r.zold = zi;
             r.lpos = sorted ? (int32_t)p : -1;
             r.pad = 0;
+            r.dll = 0.0;
             A.req[q] = r;
             double *vmu = A.vmu + (int64_t)q * (D + 1);
             double y0[D];  // the item's frame again (not kept live through the draw: registers)
@@ -634,7 +637,11 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
 // start, with the full code (exact auxiliary draws, new-cluster requests).  A deferred lane writes nothing
 // here, so every item's result is np8_assign's, bit for bit.  The lean kernel keeps its registers low
 // (no exact fp64 draws, no request payload): more waves per SIMD to hide the loads' latency.
-template <int D, int M, int PRIOR, bool COUNT>
+// LL: a max-likelihood check sweep with the sum folded in (AssignArgs::ll_on): each wave also stores the sum of its
+// items' log-likelihoods under their new labels -- the values np8_loglik would compute after the step, operation for
+// operation (the walk's quadratic forms are the table form's isotropic one) -- in a separate instance, so that the
+// other sweeps carry none of its registers.
+template <int D, int M, int PRIOR, bool COUNT, bool LL>
 __global__ __launch_bounds__(NP8_ASSIGN_BLOCK) __attribute__((amdgpu_waves_per_eu(NP8_FAST_WAVES))) void np8_assign_fast(AssignArgs A) {
     using H = HypView<D>;
     constexpr int DP = D * (D + 1) / 2;
@@ -658,6 +665,34 @@ __global__ __launch_bounds__(NP8_ASSIGN_BLOCK) __attribute__((amdgpu_waves_per_e
 #pragma unroll
     for (int a = 0; a < D; ++a) x[a] = X[(int64_t)a * A.n_loc + p];
     const int K = A.ctl->K;
+    const int lists_ok = A.ctl->lists_ok;  // (the same round of scalar loads)
+    // a max-likelihood snapshot the last check left pending: the labelling before this step is the one it keeps
+    const int snap = (!LL && A.snap_on) ? A.ctl->snap_pend : 0;
+    if (snap) A.z_best[il] = zi;
+    // level 1 of the auxiliary screen while the own row's loads are in flight: each auxiliary's bound from its
+    // Philox call 0, without the threshold (the running maximum), which is compared below
+    double ny = 0.0;
+    {
+        const double *U = hyp + H::kUinvT;  // diagonal (launch condition): whiten() + norm_of() with zeros left out
+        double n2 = 0.0;
+#pragma unroll
+        for (int a = 0; a < D; ++a) {
+            const double y = U[a * D - (a * (a - 1)) / 2] * (x[a] - hyp[H::kMu0 + a]);
+            n2 = fma(y, y, n2);
+        }
+        ny = sqrt(n2);
+    }
+    constexpr int Qa = (1 + ((((D - 1) & 1) || (D - 1) / 2 > 2) ? 1 : 0) + ((D - 1) / 2 > 4 ? ((D - 1) / 2 - 1) / 4 : 0));
+    float ub1[M];
+    if (!COUNT) {
+        const float nyf = (float)ny, nuf = (float)hyp[H::kNu], rskf = (float)hyp[H::kRsk], cauxf = (float)hyp[H::kCaux];
+#pragma unroll
+        for (int m = 0; m < M; ++m) {
+            uint32_t w[4];
+            philox_call(A.seed, ig, t, kStreamAux, (uint32_t)(m * Qa), w);
+            ub1[m] = aux_screen_ub<D>(w, 0.0f, 0.0f, nyf, nuf, rskf, cauxf, 0.0f, false);
+        }
+    }
     NP8_CLK(1);
     bool defer = COUNT;  // counting runs: every lane takes np8_assign's counting instance
     PickState st;
@@ -665,6 +700,7 @@ __global__ __launch_bounds__(NP8_ASSIGN_BLOCK) __attribute__((amdgpu_waves_per_e
     st.u = -1.0;
     st.T = 0.0;
     double d2own = 0.0;  // |x - mu_own|^2: the own row's quadratic form and the list's radius check
+    double ll_own = 0.0, llp = 0.0;  // (LL) ll under the own row and under the row picked so far
     int32_t jo = 0, nlist = 0;
     double r2list = 0.0;
     int32_t pslot = zi;
@@ -688,7 +724,8 @@ __global__ __launch_bounds__(NP8_ASSIGN_BLOCK) __attribute__((amdgpu_waves_per_e
 #pragma unroll
                     for (int a = 1; a < D; ++a) s2 = fma(x[a] - mo[a], x[a] - mo[a], s2);
                     d2own = s2;
-                    st.T = fma(-0.5, s2 * iso, cs) + l1;
+                    ll_own = fma(-0.5, s2 * iso, cs);
+                    st.T = ll_own + l1;
                 } else {
                     defer = true;
                 }
@@ -698,6 +735,7 @@ __global__ __launch_bounds__(NP8_ASSIGN_BLOCK) __attribute__((amdgpu_waves_per_e
     }
     if (COUNT) defer = true;
     st.pick = jo;
+    llp = ll_own;
     NP8_CLK(2);
     const double zslot = (double)zi;
     int ngroups = 0;
@@ -763,20 +801,22 @@ __global__ __launch_bounds__(NP8_ASSIGN_BLOCK) __attribute__((amdgpu_waves_per_e
                             const double ma = NP8_ROWF(fm[a], a, k);
                             s2 = fma(x[a] - ma, x[a] - ma, s2);
                         }
-                        const double lw = fma(-0.5, s2 * iso, NP8_ROWF(fc, D + 1, k)) + NP8_ROWF(fl, D + 2, k);
+                        const double llj = fma(-0.5, s2 * iso, NP8_ROWF(fc, D + 1, k));
+                        const double lw = llj + NP8_ROWF(fl, D + 2, k);
                         const double sl = NP8_ROWF(fsl, D + 3, k);
                         if (!(own_skip && sl == zslot)) {
                             const int j = NP8_ROWJ(k);
                             ensure_u(st, lw, A.seed, ig, t);
                             pick_step(st, lw, j);
                             pslot = (st.pick == j) ? (int32_t)sl : pslot;
+                            if (LL) llp = (st.pick == j) ? llj : llp;
                         }
                     }
                 }
             }
         }
     };
-    if (A.use_lists && A.ctl->lists_ok && ngroups <= kMaxListGroups) {  // wave-uniform
+    if (A.use_lists && lists_ok && ngroups <= kMaxListGroups) {  // wave-uniform
         uint64_t pend = __ballot(1);
         while (pend) {
             const int lead = __ffsll((unsigned long long)pend) - 1;
@@ -801,30 +841,16 @@ __global__ __launch_bounds__(NP8_ASSIGN_BLOCK) __attribute__((amdgpu_waves_per_e
     // the auxiliaries: np8_assign's two-level screen, then the exact fp64 draw for the lanes it cannot clear;
     // a lane that picks an auxiliary makes a new-cluster request (appended below)
     bool req = false;
-    double ny = 0.0;
     if (!defer) {
-        {
-            const double *U = hyp + H::kUinvT;  // diagonal (launch condition): whiten() + norm_of() with zeros left out
-            double n2 = 0.0;
-#pragma unroll
-            for (int a = 0; a < D; ++a) {
-                const double y = U[a * D - (a * (a - 1)) / 2] * (x[a] - hyp[H::kMu0 + a]);
-                n2 = fma(y, y, n2);
-            }
-            ny = sqrt(n2);
-        }
         const double logam = hyp[H::kLogam];
         const float thr = (float)(st.T - kSkip - logam);  // T only grows: conservative for every m
         const float nyf = (float)ny, nuf = (float)hyp[H::kNu], rskf = (float)hyp[H::kRsk], cauxf = (float)hyp[H::kCaux];
-        constexpr int Qa = (1 + ((((D - 1) & 1) || (D - 1) / 2 > 2) ? 1 : 0) + ((D - 1) / 2 > 4 ? ((D - 1) / 2 - 1) / 4 : 0));
         constexpr bool has_call1 = Qa > 1;
         uint32_t need = 0u;
-#pragma unroll 1
-        for (int m = 0; m < M; ++m) {
-            uint32_t w[4];
-            philox_call(A.seed, ig, t, kStreamAux, (uint32_t)(m * Qa), w);
-            if (!(aux_screen_ub<D>(w, 0.0f, 0.0f, nyf, nuf, rskf, cauxf, thr) <= thr)) need |= 1u << m;
-        }
+        const float thr_err = 1e-4f * fabsf(thr);
+#pragma unroll
+        for (int m = 0; m < M; ++m)
+            if (!(ub1[m] + thr_err <= thr)) need |= 1u << m;
         NP8_CLK(4);
 #pragma unroll 1
         for (int m = 0; m < M; ++m) {
@@ -909,10 +935,27 @@ __global__ __launch_bounds__(NP8_ASSIGN_BLOCK) __attribute__((amdgpu_waves_per_e
         A.z[il] = snew;
         zs[p] = snew;
     }
+    if constexpr (LL) {  // the wave's sum, in a fixed order (a requester counts under its old slot)
+        double v = req ? ll_own : llp;
+        const uint64_t act = __ballot(1);
+        if (act == ~0ull) {
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) v = v + __shfl_xor(v, o);
+        } else {  // the range's last, partial wave: lane order
+            double s = 0.0;
+            for (uint64_t m = act; m; m &= m - 1ull) s = s + readlane_d(v, __ffsll((unsigned long long)m) - 1);
+            v = s;
+        }
+        if (lane == __ffsll((unsigned long long)act) - 1) A.llpart[(p - A.p0) >> 6] = v;
+    }
     const int qreq = wave_append(A.nreq, req);  // (requests are accepted by scan position, not arrival)
     if (req) {  // np8_assign's request with its payload, the auxiliary's (v, mu)
         const int q = qreq;
         if (q < A.req_cap) {  // always: the area holds every item of the step
+            double *vm = A.vmu + (int64_t)q * (D + 1);
+            double y0[D];
+            whiten<D>(hyp, x, y0);
+            aux_params<D>(hyp, y0, ny, A.seed, ig, t, st.pick - K, vm);
             Request r;
             r.pos = (int64_t)ig;  // synchronous sweep: scan position = item index
             r.i = (int64_t)ig;
@@ -920,11 +963,23 @@ __global__ __launch_bounds__(NP8_ASSIGN_BLOCK) __attribute__((amdgpu_waves_per_e
             r.zold = zi;
             r.lpos = (int32_t)p;
             r.pad = 0;
+            r.dll = 0.0;
+            if (LL) {  // ll under the slot np8_finalize would build from (v, mu) (write_new_slot), as np8_loglik evaluates it
+                const double v = vm[0], v2 = v * v;
+                const double iso_n = A.gp0 / v2, c_n = fma(-(double)D, log_pos(fabs(v)), hyp[H::kCaux]);
+                double s2 = (x[0] - vm[1]) * (x[0] - vm[1]);
+#pragma unroll
+                for (int a = 1; a < D; ++a) s2 = fma(x[a] - vm[1 + a], x[a] - vm[1 + a], s2);
+                r.dll = fma(-0.5, s2 * iso_n, c_n) - ll_own;
+            }
             A.req[q] = r;
-            double y0[D];
-            whiten<D>(hyp, x, y0);
-            aux_params<D>(hyp, y0, ny, A.seed, ig, t, st.pick - K, A.vmu + (int64_t)q * (D + 1));
         }
+    }
+    if (snap) {  // the rest of the pending snapshot: counts and parameters as the check's finalize left them
+        const int64_t g = p - A.p0, ng = A.p1 - A.p0;
+        for (int64_t k = g; k < A.kcap; k += ng) A.cnt_best[k] = A.cnt[k];
+        for (int64_t k = g; k < (int64_t)A.kcap * D; k += ng) A.mu_best[k] = A.slot_mu[k];
+        for (int64_t k = g; k < (int64_t)A.kcap * D * D; k += ng) A.sigma_best[k] = A.slot_sigma[k];
     }
     NP8_CLK(6);
 }
@@ -1111,6 +1166,49 @@ __device__ int block_excl_scan(int v, int *sh /* >= 16 ints */, int *total) {
     return r;
 }
 
+// Sum over the block in a fixed order (butterfly within each wave, then the waves in order); every thread
+// returns the same value.
+__device__ double block_sum_d(double v, double *sh /* >= 16 doubles */) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = v + __shfl_xor(v, o);
+    __syncthreads();
+    if (lane == 0) sh[wid] = v;
+    __syncthreads();
+    double t = sh[0];
+    for (int w = 1; w < nw; ++w) t = t + sh[w];
+    __syncthreads();
+    return t;
+}
+
+// Two sums at once (one set of barriers), each in block_sum_d's order.
+__device__ double2 block_sum2_d(double a, double b, double2 *sh /* >= 16 */) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        a = a + __shfl_xor(a, o);
+        b = b + __shfl_xor(b, o);
+    }
+    __syncthreads();
+    if (lane == 0) sh[wid] = make_double2(a, b);
+    __syncthreads();
+    double2 t = sh[0];
+    for (int w = 1; w < nw; ++w) {
+        t.x = t.x + sh[w].x;
+        t.y = t.y + sh[w].y;
+    }
+    __syncthreads();
+    return t;
+}
+
+// The folded max-likelihood check's per-rank sum: the assign's per-wave partials, thread-strided then block_sum_d
+// (np8_finalize for one rank, np8_req_select for the exchanged record: the same order).
+__device__ double partials_sum(const double *__restrict__ part, int64_t n, double *sh) {
+    double v = 0.0;
+    for (int64_t k = threadIdx.x; k < n; k += blockDim.x) v = v + part[k];
+    return block_sum_d(v, sh);
+}
+
 }  // namespace
 
 // ---- candidate pruning ------------------------------------------------------------------------------
@@ -1130,7 +1228,7 @@ constexpr int kPruneBlocks = 32;  // np8_prune grid: 128 rows per pass
 template <int DT = 0, typename R2of>
 __device__ void prune_row(const double *__restrict__ cand, R2of R2of_slot, int32_t *__restrict__ plist,
                           int32_t *__restrict__ plen, double *__restrict__ plr2, int32_t *__restrict__ plen_s,
-                          double *__restrict__ plr2_s, int ls, int Drt, int K, int k0) {
+                          double *__restrict__ plr2_s, int ls, int Drt, int K, int k0, double *__restrict__ lb, int kcap) {
     const int D = DT > 0 ? DT : Drt;
     const int DP = D * (D + 1) / 2, CS = cand_stride(D), F = D + DP;
     const int lane = threadIdx.x & 63;
@@ -1165,7 +1263,7 @@ __device__ void prune_row(const double *__restrict__ cand, R2of R2of_slot, int32
                     const double far = 0.5 * isoj * delta * delta, near = 0.5 * iso0 * R2;
                     const double U = (wj - base0) - far + near;
                     const double mag = fabs(wj) + fabs(base0) + far + near;
-                    keep = !(U <= -kSkip - 2.0 - 1e-9 * mag);
+                    keep = !(U <= -kSkip - 2.0 - kListSlack - 1e-9 * mag);
                 }
             }
         }
@@ -1179,6 +1277,10 @@ __device__ void prune_row(const double *__restrict__ cand, R2of R2of_slot, int32
         plr2[k0] = r2l;
         plen_s[slot0] = count;
         plr2_s[slot0] = r2l;
+        if (lb) {  // the counts' logs this list is exact for (within kListSlack / 2)
+            lb[slot0] = e0[F + kFieldLogn];
+            lb[kcap + slot0] = e0[F + kFieldLogn1];
+        }
     }
 }
 
@@ -1279,9 +1381,12 @@ __device__ int64_t select_kth_pos(PosAt pos_at, int n, int k, int *hist /* 2048 
 // (the body of np8_req_select, also run as the serial tail of np8_step_tail)
 __device__ void req_select_block(const unsigned char *__restrict__ stage, int64_t stage_cap,
                                  unsigned char *__restrict__ rec, int64_t rec_cap, int kcap, int D, int req_max,
-                                 int *hist /* LDS int[2048] */) {
+                                 const double *__restrict__ llpart, int64_t ll_n, int *hist /* LDS int[2048] */) {
     __shared__ int sh[32];
     __shared__ int s_cnt;
+    __shared__ double shd[16];
+    // folded max-likelihood check: this rank's sum travels in the exchanged record's header
+    const double Lloc = llpart ? partials_sum(llpart, ll_n, shd) : 0.0;
     RecHeader *sh_hdr = reinterpret_cast<RecHeader *>(const_cast<unsigned char *>(stage));
     const Request *sreq = reinterpret_cast<const Request *>(stage + kRecHeaderBytes + 4ll * kcap);
     const double *svmu = reinterpret_cast<const double *>(stage + record_vmu_offset(kcap, (int)stage_cap));
@@ -1303,15 +1408,17 @@ __device__ void req_select_block(const unsigned char *__restrict__ stage, int64_
     __syncthreads();
     if (threadIdx.x == 0) {
         reinterpret_cast<RecHeader *>(rec)->nreq = k;
+        if (llpart) reinterpret_cast<RecHeader *>(rec)->L_local = Lloc;
         sh_hdr->nreq = 0;
     }
 }
 
 __global__ __launch_bounds__(kFinThreads) void np8_req_select(const unsigned char *__restrict__ stage, int64_t stage_cap,
                                                               unsigned char *__restrict__ rec, int64_t rec_cap, int kcap,
-                                                              int D, int req_max) {
+                                                              int D, int req_max, const double *__restrict__ llpart,
+                                                              int64_t ll_n) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    req_select_block(stage, stage_cap, rec, rec_cap, kcap, D, req_max, reinterpret_cast<int *>(smem));
+    req_select_block(stage, stage_cap, rec, rec_cap, kcap, D, req_max, llpart, ll_n, reinterpret_cast<int *>(smem));
 }
 
 namespace {
@@ -1325,7 +1432,10 @@ __device__ int64_t request_pos(const FinArgs &F, const int *base, int q) { retur
 // scan position are accepted, in position order, into the lowest free slots in ascending order; each
 // accepted requester leaves its old slot; the others keep their cluster (deferred to their next update).
 // (the body of np8_finalize, also run as the serial tail of np8_step_tail; smem: np8_finalize_lds_bytes)
-__device__ void finalize_block(const FinArgs &F, unsigned char *smem) {
+// Returns (block-uniform) whether the candidate lists of the last build may be stale after this step: a slot changed
+// liveness, requests were accepted, the rows were re-copied, or (slack_test) a live slot's log n or log(n - 1) moved
+// more than kListSlack / 2 from the build's values.
+__device__ int finalize_block(const FinArgs &F, unsigned char *smem) {
     int64_t *keys = reinterpret_cast<int64_t *>(smem);
     int *kidx = reinterpret_cast<int *>(smem + sizeof(int64_t) * kReqMax);
     int *freeslot = kidx + kReqMax;
@@ -1343,7 +1453,7 @@ __device__ void finalize_block(const FinArgs &F, unsigned char *smem) {
     // old counts (liveness changes), deltas, and the table entries of this thread's first kFinPre slots
     constexpr int kFinPre = 2;
     int cold[kFinPre], d0[kFinPre];
-    double pc[kFinPre], piso[kFinPre];
+    double pc[kFinPre], piso[kFinPre], plb0[kFinPre], plb1[kFinPre];
     const int32_t *delta0 = rec_delta(F, 0);
 #pragma unroll
     for (int q = 0; q < kFinPre; ++q) {
@@ -1353,9 +1463,25 @@ __device__ void finalize_block(const FinArgs &F, unsigned char *smem) {
         d0[q] = in ? delta0[s] : 0;  // rank 0's delta in the same round of loads (the single-rank step: all of them)
         pc[q] = in ? F.slot_c[s] : 0.0;
         piso[q] = in ? F.slot_iso[s] : 0.0;
+        plb0[q] = (in && F.slack_test) ? F.lb[s] : 0.0;
+        plb1[q] = (in && F.slack_test) ? F.lb[kcap + s] : 0.0;
     }
     const int cand_fresh = F.ctl->cand_fresh;
     const int nreq0 = rec_header(F, 0)->nreq;  // (same round: every thread, one address)
+    // the folded check's partials (one rank), eight independent loads per round, summed in partials_sum's order
+    double llv = 0.0;
+    if (F.ll_on && !F.ll_rec) {
+        for (int64_t b = tid; b < F.ll_n; b += 8 * kFinThreads) {
+            double v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int64_t k = b + (int64_t)u * kFinThreads;
+                v[u] = k < F.ll_n ? F.llpart[k] : 0.0;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) llv = llv + v[u];
+        }
+    }
 
     if (tid == 0) {
         int n = 0;
@@ -1453,6 +1579,7 @@ __device__ void finalize_block(const FinArgs &F, unsigned char *smem) {
                 write_new_slot(F, request_vmu(F, base, kidx[q]), s);
             }
             if (F.wdirty) F.wdirty[s] = 1;
+            if (F.ll_on) reinterpret_cast<double *>(keys)[q] = r.dll;  // (keys are sorted: no longer needed)
             cnt_s[s] = 1;
             atomicSub(&cnt_s[r.zold], 1);  // a live slot (the requester is in it), never one of the free ones
             const int64_t item = key_item(r.i);
@@ -1484,15 +1611,18 @@ __device__ void finalize_block(const FinArgs &F, unsigned char *smem) {
     int k = block_excl_scan(nl, sh, &nlive);
     // slot s -> its dense row, counts and the row's scalar fields (the prefetched entries unless this step
     // created slots, whose entries were written above)
-    auto write_slot = [&](int s, double cs, double iso) {
+    int viol = 0;
+    auto write_slot = [&](int s, double cs, double iso, double lb0, double lb1) {
         const int c = cnt_s[s];
         F.cnt[s] = c;
         F.dense_of[s] = (c > 0) ? k : -1;
         if (c > 0) {
             double *e = F.cand + (int64_t)k * CS + D + DP;
             const double l1 = (c > 1) ? log_pos((double)(c - 1)) : kZeroLogWeight;
+            const double l0 = log_pos((double)c);
+            if (F.slack_test && !(fabs(l0 - lb0) <= 0.5 * kListSlack && fabs(l1 - lb1) <= 0.5 * kListSlack)) viol = 1;
             e[kFieldC] = cs;
-            e[kFieldLogn] = log_pos((double)c);
+            e[kFieldLogn] = l0;
             e[kFieldLogn1] = l1;
             F.slot_logn1[s] = l1;
             e[kFieldSlot] = (double)s;
@@ -1504,10 +1634,11 @@ __device__ void finalize_block(const FinArgs &F, unsigned char *smem) {
 #pragma unroll
     for (int q = 0; q < kFinPre; ++q) {
         const int s = s0 + q;
-        if (s < s1) write_slot(s, A == 0 ? pc[q] : F.slot_c[s], A == 0 ? piso[q] : F.slot_iso[s]);
+        if (s < s1) write_slot(s, A == 0 ? pc[q] : F.slot_c[s], A == 0 ? piso[q] : F.slot_iso[s], plb0[q], plb1[q]);
     }
-    for (int s = s0 + kFinPre; s < s1; ++s) write_slot(s, F.slot_c[s], F.slot_iso[s]);
-    __syncthreads();
+    for (int s = s0 + kFinPre; s < s1; ++s)
+        write_slot(s, F.slot_c[s], F.slot_iso[s], F.slack_test ? F.lb[s] : 0.0, F.slack_test ? F.lb[kcap + s] : 0.0);
+    const int stale = __syncthreads_or(viol) != 0 || copy_rows;
     // mu and P' of every live row, all threads (not on the wide path: its kernels read the fp32 factor
     // rows of np8_wide_rows, and 4 MB of P' at D = 64 would keep this one workgroup busy for 0.3 ms)
     const int W = D + DP;
@@ -1521,17 +1652,48 @@ __device__ void finalize_block(const FinArgs &F, unsigned char *smem) {
         F.ctl->cand_fresh = 1;
         F.ctl->n_pend = (F.prior == kPriorNiw || F.frame_payload) ? A : 0;
     }
+    // folded max-likelihood check (np_mcmc.cpp:172-174, 187-203): L = the ranks' sums of the assign's per-item
+    // log-likelihoods (requesters under their old slot) + the accepted requests' dll, in position order; the
+    // labelling is snapshotted on improvement by the next np8_assign_fast (ctl->snap_pend)
+    if (F.ll_on) {
+        __shared__ double2 shd2[16];
+        double v = 0.0;
+        for (int q = tid; q < A; q += kFinThreads) v = v + reinterpret_cast<const double *>(keys)[q];
+        const double2 sums = block_sum2_d(llv, v, shd2);
+        double S1 = sums.x;
+        if (F.ll_rec) {
+            S1 = rec_header(F, 0)->L_local;
+            for (int r = 1; r < F.world; ++r) S1 = S1 + rec_header(F, r)->L_local;
+        }
+        const double L = S1 + sums.y;
+        if (tid == 0) {
+            F.ctl->L = L;
+            F.ctl->L_local = F.ll_rec ? reinterpret_cast<const RecHeader *>(F.local_rec)->L_local : S1;
+            const double b = F.best[F.par];
+            const bool better = L > b;
+            F.best[F.par ^ 1] = better ? L : b;
+            if (better) *F.have_best = 1;
+            F.ctl->snap_pend = better ? 1 : 0;
+        }
+    } else if (F.snap_clear && tid == 0) {
+        F.ctl->snap_pend = 0;
+    }
     // clear the local record for the next step (all reads of it are behind the barriers above)
     if (F.local_rec) {
         int32_t *delta = reinterpret_cast<int32_t *>(F.local_rec + kRecHeaderBytes);
         for (int s = tid; s < kcap; s += kFinThreads) delta[s] = 0;
         if (tid == 0) reinterpret_cast<RecHeader *>(F.local_rec)->nreq = 0;
     }
+    if (tid == 0) {
+        if (F.moved_mirror) *F.moved_mirror = F.ctl->moved;  // (host-mapped: the host's lagged re-sort decision)
+        if (F.advance) F.ctl->t_base += F.advance;  // nothing after this step reads t_base before the next replay
+    }
+    return stale;
 }
 
 __global__ __launch_bounds__(kFinThreads) void np8_finalize(FinArgs F) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    finalize_block(F, smem);
+    (void)finalize_block(F, smem);
 }
 
 // np8_prune's work for one workgroup of kFinThreads: every live row's list, after the radius buffers'
@@ -1542,7 +1704,7 @@ __global__ __launch_bounds__(kFinThreads) void np8_finalize(FinArgs F) {
 template <int D>
 __device__ void prune_block(const PruneArgs &A, unsigned char *smem, size_t lds_bytes) {
     constexpr int DP = D * (D + 1) / 2, CS = (D + DP + 5 + 1) & ~1, F = D + DP;
-    constexpr int RW = D + 5;  // mu[D] | c + log n | c + log(n - 1) | iso | R^2 | slot
+    constexpr int RW = D + 7;  // mu[D] | c + log n | c + log(n - 1) | iso | R^2 | slot | log n | log(n - 1)
     __syncthreads();
     const int K = A.ctl->K;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, nwb = kFinThreads / 64;
@@ -1551,7 +1713,7 @@ __device__ void prune_block(const PruneArgs &A, unsigned char *smem, size_t lds_
     auto R2of = [&](int slot) { return src[slot]; };
     if ((size_t)K * RW * sizeof(double) > lds_bytes) {
         for (int k0 = wid; k0 < K; k0 += nwb)  // wave-uniform
-            prune_row<D>(A.cand, R2of, A.plist, A.plen, A.plr2, A.plen_s, A.plr2_s, A.ls, A.D, K, k0);
+            prune_row<D>(A.cand, R2of, A.plist, A.plen, A.plr2, A.plen_s, A.plr2_s, A.ls, A.D, K, k0, A.lb, A.kcap);
     } else {
         double *st = reinterpret_cast<double *>(smem);
         for (int idx = tid; idx < K * RW; idx += kFinThreads) {
@@ -1568,8 +1730,12 @@ __device__ void prune_block(const PruneArgs &A, unsigned char *smem, size_t lds_
                 v = e[F + kFieldIso];
             else if (f == D + 3)
                 v = src[(int)e[F + kFieldSlot]];
-            else
+            else if (f == D + 4)
                 v = e[F + kFieldSlot];
+            else if (f == D + 5)
+                v = e[F + kFieldLogn];
+            else
+                v = e[F + kFieldLogn1];
             st[f * K + r] = v;
         }
         __syncthreads();
@@ -1599,7 +1765,7 @@ __device__ void prune_block(const PruneArgs &A, unsigned char *smem, size_t lds_
                             const double far = 0.5 * isoj * delta * delta, near = 0.5 * iso0 * R2;
                             const double U = (wj - base0) - far + near;
                             const double mag = fabs(wj) + fabs(base0) + far + near;
-                            keep = !(U <= -kSkip - 2.0 - 1e-9 * mag);
+                            keep = !(U <= -kSkip - 2.0 - kListSlack - 1e-9 * mag);
                         }
                     }
                 }
@@ -1613,6 +1779,10 @@ __device__ void prune_block(const PruneArgs &A, unsigned char *smem, size_t lds_
                 A.plr2[k0] = r2l;
                 A.plen_s[slot0] = count;
                 A.plr2_s[slot0] = r2l;
+                if (A.lb) {
+                    A.lb[slot0] = st[(D + 5) * K + k0];
+                    A.lb[A.kcap + slot0] = st[(D + 6) * K + k0];
+                }
             }
         }
     }
@@ -1673,9 +1843,18 @@ __global__ __launch_bounds__(kFinThreads) void np8_step_tail(AssignArgs A, FinAr
         if (!s_last) return;
         __threadfence();
     }
-    if (T.select) req_select_block(T.stage, T.stage_cap, T.rec, T.rec_cap, F.kcap, D, F.req_max, reinterpret_cast<int *>(smem));
-    if (T.fin) finalize_block(F, smem);
-    if (T.prune) prune_block<D>(P, smem, T.lds_bytes);
+    if (T.select)
+        req_select_block(T.stage, T.stage_cap, T.rec, T.rec_cap, F.kcap, D, F.req_max, nullptr, 0,
+                         reinterpret_cast<int *>(smem));
+    int stale = 1;
+    if (T.fin) stale = finalize_block(F, smem);
+    if (T.prune == 1 || (T.prune == 2 && stale)) {
+        prune_block<D>(P, smem, T.lds_bytes);
+        if (T.prune == 2 && threadIdx.x == 0) P.ctl->list_builds += 1u;
+    } else if (T.prune == 2) {  // the lists stay: only the radius buffers' bookkeeping (never a gathering step here)
+        if (P.clear_next)
+            for (int s = threadIdx.x; s < P.kcap; s += kFinThreads) P.r2[P.kcap + s] = 0.0;
+    }
 }
 
 // Finalize and the candidate lists in one launch with the lists still built in parallel (DESIGN.md §5 "Fewer
@@ -1724,7 +1903,7 @@ __global__ __launch_bounds__(kFinThreads) void np8_fin_prune(FinArgs F, PruneArg
         auto R2of = [&](int slot) { return src[slot]; };
         constexpr int kWaves = kFinThreads / 64;
         for (int k0 = ((int)blockIdx.x - 1) * kWaves + ((int)threadIdx.x >> 6); k0 < K; k0 += nP * kWaves)  // wave-uniform
-            prune_row<DT>(P.cand, R2of, P.plist, P.plen, P.plr2, P.plen_s, P.plr2_s, P.ls, P.D, K, k0);
+            prune_row<DT>(P.cand, R2of, P.plist, P.plen, P.plr2, P.plen_s, P.plr2_s, P.ls, P.D, K, k0, P.lb, P.kcap);
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -1820,6 +1999,18 @@ __global__ __launch_bounds__(256) void np8_snapshot(SnapArgs A) {
     for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < nm; k += stride) A.mu_best[k] = A.slot_mu[k];
     for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < ns; k += stride)
         A.sigma_best[k] = A.slot_sigma[k];
+}
+
+// A snapshot the folded check left pending (ctl->snap_pend, consumed otherwise by the next np8_assign_fast): the
+// labelling, counts and parameters as they stand; the host clears the flag behind this launch.
+__global__ __launch_bounds__(256) void np8_snapshot_flush(SnapArgs A, const Ctl *__restrict__ ctl) {
+    if (!ctl->snap_pend) return;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x, g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (int64_t i = g; i < A.n_loc; i += stride) A.z_best[i] = A.z[i];
+    for (int64_t k = g; k < A.kcap; k += stride) A.cnt_best[k] = A.cnt[k];
+    const int64_t nm = (int64_t)A.kcap * A.D, ns = (int64_t)A.kcap * A.D * A.D;
+    for (int64_t k = g; k < nm; k += stride) A.mu_best[k] = A.slot_mu[k];
+    for (int64_t k = g; k < ns; k += stride) A.sigma_best[k] = A.slot_sigma[k];
 }
 
 // ---- cluster-parameter update (mh_g0) ------------------------------------------------------------------
@@ -2110,9 +2301,11 @@ hipError_t np8_launch_assign_fast(const AssignArgs &A, int D, int M, hipStream_t
 #define X(d, m)                                                                                          \
     if (D == d && M == m) {                                                                              \
         if (A.count_eval)                                                                                \
-            hipLaunchKernelGGL((np8_assign_fast<d, m, kPriorReference, true>), grid, block, 0, s, A);    \
+            hipLaunchKernelGGL((np8_assign_fast<d, m, kPriorReference, true, false>), grid, block, 0, s, A); \
+        else if (A.ll_on)                                                                                \
+            hipLaunchKernelGGL((np8_assign_fast<d, m, kPriorReference, false, true>), grid, block, 0, s, A); \
         else                                                                                             \
-            hipLaunchKernelGGL((np8_assign_fast<d, m, kPriorReference, false>), grid, block, 0, s, A);   \
+            hipLaunchKernelGGL((np8_assign_fast<d, m, kPriorReference, false, false>), grid, block, 0, s, A); \
         return hipGetLastError();                                                                        \
     }
     NP8_FOR_EACH_DM(X)
@@ -2428,9 +2621,9 @@ hipError_t np8_launch_fin_prune(const FinArgs &F, const PruneArgs &P, hipStream_
 }
 
 hipError_t np8_launch_req_select(const unsigned char *stage, int64_t stage_cap, unsigned char *rec, int64_t rec_cap,
-                                 int kcap, int D, int req_max, hipStream_t s) {
+                                 int kcap, int D, int req_max, const double *llpart, int64_t ll_n, hipStream_t s) {
     hipLaunchKernelGGL(np8_req_select, dim3(1), dim3(kFinThreads), sizeof(int) * 2048, s, stage, stage_cap, rec, rec_cap,
-                       kcap, D, req_max);
+                       kcap, D, req_max, llpart, ll_n);
     return hipGetLastError();
 }
 
@@ -2503,7 +2696,7 @@ __global__ __launch_bounds__(256) void np8_prune(PruneArgs A) {
         for (int s = threadIdx.x; s < A.kcap; s += blockDim.x) A.r2[A.kcap + s] = 0.0;
     auto R2of = [&](int slot) { return src[slot]; };
     for (int k0 = blockIdx.x * 4 + (threadIdx.x >> 6); k0 < K; k0 += gridDim.x * 4)  // wave-uniform
-        prune_row<DT>(A.cand, R2of, A.plist, A.plen, A.plr2, A.plen_s, A.plr2_s, A.ls, A.D, K, k0);
+        prune_row<DT>(A.cand, R2of, A.plist, A.plen, A.plr2, A.plen_s, A.plr2_s, A.ls, A.D, K, k0, A.lb, A.kcap);
 }
 
 __global__ void np8_advance_epoch(Ctl *ctl, uint32_t n) { ctl->t_base += n; }
@@ -2526,6 +2719,15 @@ hipError_t np8_launch_prune(const PruneArgs &A, int kcap, hipStream_t s) {
 
 hipError_t np8_launch_advance_epoch(Ctl *ctl, uint32_t n, hipStream_t s) {
     hipLaunchKernelGGL(np8_advance_epoch, dim3(1), dim3(1), 0, s, ctl, n);
+    return hipGetLastError();
+}
+
+hipError_t np8_launch_snapshot_flush(const SnapArgs &A, Ctl *ctl, hipStream_t s) {
+    int64_t n = A.n_loc > (int64_t)A.kcap * A.D * A.D ? A.n_loc : (int64_t)A.kcap * A.D * A.D;
+    int64_t nb = (n + 255) / 256;
+    if (nb > 2048) nb = 2048;
+    if (nb < 1) nb = 1;
+    hipLaunchKernelGGL(np8_snapshot_flush, dim3((unsigned)nb), dim3(256), 0, s, A, ctl);
     return hipGetLastError();
 }
 

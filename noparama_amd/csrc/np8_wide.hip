@@ -660,6 +660,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NP8_WIDE_WA
             r.zold = zi;
             r.lpos = sorted ? (int32_t)pc : -1;
             r.pad = 0;
+            r.dll = 0.0;
             A.req[q] = r;
             double *vmu = A.vmu + (int64_t)q * (D + 1);
             wide_frame_payload<D>(hyp, X, n, xr, vmu);

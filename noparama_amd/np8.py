@@ -110,6 +110,9 @@ class Stats(C.Structure):
         ("full_walk_waves", C.c_int64),
         ("many_group_waves", C.c_int64),
         ("list_entries", C.c_int64),
+        ("folded_checks", C.c_int64),
+        ("tail_list_builds", C.c_int64),
+        ("tail_steps", C.c_int64),
     ]
 
 

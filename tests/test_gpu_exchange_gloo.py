@@ -2,7 +2,8 @@
 device, so what runs here is the host-exchange transport -- the same per-step records moved over gloo
 (np8_step_local / np8_step_merge).  (The RCCL code path itself runs in tests/test_gpu_rccl_one_rank.py with
 a one-rank communicator; the driver's scaling runs use one GPU per rank.)  The sharded result must equal
-the single-rank sweep bit for bit."""
+the single-rank sweep bit for bit -- at N = 8000 from a poor start, and at the C3 workload itself (N = 1e6, D = 8,
+K = 64, warm state; the contiguous shards of C4) as 2 and 4 ranks."""
 import os
 import socket
 
@@ -12,6 +13,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 N, D, SWEEPS, SEED = 8000, 8, 6, 2024
+NC3, SWEEPS_C3 = 1_000_000, 12
 
 
 def _port():
@@ -22,15 +24,22 @@ def _port():
     return p
 
 
-def _data():
+def _data(kind="small"):
     from noparama_amd import datasets
 
+    if kind == "c3":  # the north-star workload: C3 data, its warm state (bench.py), 2% of the labels scrambled
+        X, z, mu, sig = datasets.config_c3(N=NC3)
+        z = z.astype(np.int32)
+        rng = np.random.default_rng(3)
+        idx = rng.choice(NC3, NC3 // 50, replace=False)
+        z[idx] = rng.integers(0, mu.shape[0], size=idx.size)
+        return X, z, mu, sig
     X, _, mu, sig = datasets.mixture(N, D, 10, 0.8, 8.0, seed=5)
     zr = np.random.default_rng(1).integers(0, 10, size=N).astype(np.int32)  # a poor start: many moves
     return X, zr, mu, sig
 
 
-def _rank(rank, world, port, outdir):
+def _rank(rank, world, port, outdir, kind="small"):
     import torch
     import torch.distributed as dist
 
@@ -38,8 +47,9 @@ def _rank(rank, world, port, outdir):
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    X, zr, mu, sig = _data()
-    lo, hi = (N * rank) // world, (N * (rank + 1)) // world
+    X, zr, mu, sig = _data(kind)
+    n, sweeps = X.shape[0], (SWEEPS_C3 if kind == "c3" else SWEEPS)
+    lo, hi = (n * rank) // world, (n * (rank + 1)) // world
     uid = [comm_unique_id() if rank == 0 else None]
     dist.broadcast_object_list(uid, src=0)
     smp = NealAlgorithm8(D, seed=SEED, device=0)
@@ -52,17 +62,17 @@ def _rank(rank, world, port, outdir):
     dist.all_gather_object(flags, ok)
     if all(flags):
         transport = "rccl"
-        smp.set_data(X[lo:hi], offset=lo, n_global=N)
+        smp.set_data(X[lo:hi], offset=lo, n_global=n)
         smp.set_state(zr[lo:hi], mu, sig)
-        smp.sweep(SWEEPS)
+        smp.sweep(sweeps)
     else:
         transport = "gloo"
         smp.close()
         smp = NealAlgorithm8(D, seed=SEED, device=0)
         smp.comm_init(None, rank, world)
-        smp.set_data(X[lo:hi], offset=lo, n_global=N)
+        smp.set_data(X[lo:hi], offset=lo, n_global=n)
         smp.set_state(zr[lo:hi], mu, sig, counts=np.bincount(zr, minlength=mu.shape[0]))
-        for _ in range(SWEEPS):
+        for _ in range(sweeps):
             rec = torch.from_numpy(smp.step_local())
             out = [torch.zeros_like(rec) for _ in range(world)]
             dist.all_gather(out, rec)
@@ -94,3 +104,25 @@ def test_two_rank_processes_equal_single_rank(tmp_path):
     for r in range(2):
         assert np.array_equal(np.load(tmp_path / f"c{r}.npy"), ref["counts"])
     print("transport:", open(tmp_path / "transport0").read())
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_c3_workload_sharded_equals_single_rank(tmp_path, world):
+    """C4's sharding of the C3 workload (N = 1e6, the warm state with 2% of the labels scrambled so that items move,
+    contiguous shards) on 2 and 4 ranks: labels and counts after 12 sweeps equal one rank's bit for bit."""
+    import torch.multiprocessing as mp
+
+    from noparama_amd import NealAlgorithm8
+
+    X, z, mu, sig = _data("c3")
+    one = NealAlgorithm8(D, seed=SEED, device=0)
+    one.set_data(X)
+    one.set_state(z, mu, sig)
+    one.sweep(SWEEPS_C3)
+    ref = one.state()
+    one.close()
+    mp.spawn(_rank, args=(world, _port(), str(tmp_path), "c3"), nprocs=world, join=True)
+    zz = np.concatenate([np.load(tmp_path / f"z{r}.npy") for r in range(world)])
+    assert np.array_equal(zz, ref["z"])
+    for r in range(world):
+        assert np.array_equal(np.load(tmp_path / f"c{r}.npy"), ref["counts"])
