@@ -507,6 +507,8 @@ const membertrix &MCMC::getMaxLikelihoodMatrix() {
 }
 
 // ---- clustering_performance -----------------------------------------------------------------------
+// (NaN where the reference returns early and leaves an index unset, clustering_performance.cpp:70-73: this
+// mirror's convention for that early return, not a value the reference computes)
 void clustering_performance::calculate(const std::vector<int> &A, const std::vector<int> &B) {
     purity = rand_index = adjusted_rand_index = std::numeric_limits<double>::quiet_NaN();
     if (A.empty() || A.size() != B.size()) return;

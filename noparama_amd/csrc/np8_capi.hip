@@ -100,7 +100,7 @@ struct np8_ctx {
     // log-likelihoods per wave (llpart), finalize (or np8_req_select, per rank) reduces them and decides the
     // snapshot, which the next np8_assign_fast copies (snap_lazy: such a copy may be pending on the device, flushed
     // by np8_snapshot_flush before anything else touches the labels); NP8_NO_LLFOLD=1: the separate kernels
-    double *llpart = nullptr;    // [waves]
+    Fx *llpart = nullptr;        // [waves]
     bool llfold_off = false;
     bool step_ll = false;        // the running step folds the check in
     bool step_snap = false;      // the running step's assign consumes a pending snapshot
@@ -116,6 +116,8 @@ struct np8_ctx {
     bool sort_in_graph = false;
     uint32_t fin_advance = 0;    // the next finalize advances ctl->t_base (a captured graph's last step)
     bool fin_advanced = false;
+    bool capture_sort_outside = false;  // the graph being captured leaves the re-sort to np8_sweep (and mirrors moved)
+    bool graph_sort_outside = false;    // ... the graph in hand does
 
     // data-parallel sweep in `substeps` synchronous sub-steps (np8_config.substeps): sub-step s is the
     // contiguous range [sub_start[s], sub_start[s+1]) of the label-sorted layout (sorted by sub-step, slot)
@@ -495,7 +497,8 @@ void free_device(np8_ctx *c) {
     }
     c->s_hist = c->s_cursor = c->s_off = nullptr;
     c->slot_iso = nullptr;
-    c->lb = c->llpart = nullptr;
+    c->lb = nullptr;
+    c->llpart = nullptr;
     c->acc = nullptr;
     c->r2 = nullptr;
     c->wr2 = nullptr;
@@ -713,7 +716,7 @@ FinArgs fin_args(np8_ctx *c, const unsigned char *recs, int world) {
     F.best = c->ctl->best;
     F.have_best = &c->ctl->have_best;
     F.lb = c->lb;
-    F.moved_mirror = c->moved_dev;
+    F.moved_mirror = (c->fin_advance && c->capture_sort_outside) ? c->moved_dev : nullptr;
     F.advance = c->fin_advance;
     if (c->fin_advance) c->fin_advanced = true;
     c->fin_advance = 0;
@@ -1059,7 +1062,7 @@ int launch_resort(np8_ctx *c, bool stale) {
 int prepare_sorted(np8_ctx *c) {
     const bool stale = !c->sorted_valid;
     if (!stale && c->epoch % c->resort_every != 0) return NP8_OK;
-    if (!stale && c->capturing && !c->sort_in_graph) return NP8_OK;  // (np8_sweep re-sorts between replays)
+    if (!stale && c->capturing && c->capture_sort_outside) return NP8_OK;  // (np8_sweep re-sorts between replays)
     return launch_resort(c, stale);
 }
 
@@ -1368,6 +1371,8 @@ int capture_graph(np8_ctx *c) {
     const bool adv_fin = c->substeps == 1 && c->param_update == NP8_PARAM_FROZEN && !c->wide &&
                          c->prior == NP8_PRIOR_REFERENCE;
     c->fin_advanced = false;
+    // the re-sort check leaves the graph when its last finalize mirrors ctl->moved for the host (np8_sweep)
+    c->capture_sort_outside = adv_fin && !c->sort_in_graph && c->moved_dev != nullptr;
     for (uint32_t i = 0; i < kGraphSweeps && !r; ++i) {
         if (adv_fin && i + 1 == kGraphSweeps) c->fin_advance = kGraphSweeps;
         r = population(c);
@@ -1393,6 +1398,7 @@ int capture_graph(np8_ctx *c) {
         c->graph_phase = (int)(e0 % kGraphSweeps);
         c->graph_snap0 = snap0;
         c->graph_snap1 = snap1;
+        c->graph_sort_outside = c->capture_sort_outside;
         c->graph_folded = c->cap_folded;
         c->graph_tail = c->cap_tail;
         c->graph_timing = (c->timing ? 1 : 0) | (c->count_eval ? 2 : 0) | (c->time_all ? 4 : 0);
@@ -1605,6 +1611,7 @@ int np8_create(np8_ctx **out, const np8_config *cfg) {
         }
         hyp.push_back(smax);
     }
+    for (int a = 0; a < D; ++a) hyp.push_back(c->UinvT[a * D + a]);  // the whitening diagonal, contiguous (kUdiag)
     std::vector<double> gp;
     for (int a = 0; a < D; ++a)
         for (int b = a; b < D; ++b) gp.push_back(c->Gp[a * D + b]);
@@ -1856,7 +1863,7 @@ int np8_sweep(np8_ctx *c, int32_t n_sweeps) {
             int r = ensure_graph(c);
             if (r) return r;
             if (c->graph) {
-                if (!c->sort_in_graph && c->moved_host && (*(volatile int64_t *)c->moved_host) * 32 > c->n_loc) {
+                if (c->graph_sort_outside && (*(volatile int64_t *)c->moved_host) * 32 > c->n_loc) {
                     // the layout went stale (as of a replay ago): re-sort before this one (the device re-checks)
                     int r = prepare_sorted_now(c);
                     if (r) return r;

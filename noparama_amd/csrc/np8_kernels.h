@@ -20,7 +20,7 @@ struct Ctl {
     double L_local;     // this rank's part
     double best[2];     // best L, double-buffered by check parity
     int64_t moved;      // items that changed cluster since the last re-sort (local)
-    int32_t cur;        // which label-sorted buffer is current
+    int32_t cur_unused; // (was: which label-sorted buffer is current; the layout is always buffer 0 now)
     int32_t do_sort;    // this re-sort pass runs (decided by np8_sort_scan)
     uint32_t done_blocks;
     uint32_t tail_done;   // np8_step_tail: workgroups finished (the last one runs the serial part, resets it)
@@ -50,6 +50,59 @@ struct Ctl {
 // conditional rebuild, DESIGN.md "Candidate pruning").
 constexpr double kListSlack = 2.0;
 
+// Exact sums of log-likelihoods (the folded max-likelihood check): x * 2^64 as a 128-bit two's-complement integer
+// (lo, hi), exact for every double with 2^-11 <= |x| < 2^62 (below, truncated toward zero).  Integer addition is
+// associative, so the sum is the same in any order -- whatever the label-sorted layout put into which wave, however
+// many ranks the items are spread over.
+struct Fx {
+    uint64_t lo;
+    int64_t hi;
+};
+
+NP8_HD Fx fx_add(Fx a, Fx b) {
+    Fx r;
+    r.lo = a.lo + b.lo;
+    r.hi = (int64_t)((uint64_t)a.hi + (uint64_t)b.hi + (r.lo < a.lo ? 1ull : 0ull));
+    return r;
+}
+
+NP8_HD Fx fx_neg(Fx a) {
+    Fx r;
+    r.lo = ~a.lo + 1ull;
+    r.hi = (int64_t)(~(uint64_t)a.hi + (r.lo == 0ull ? 1ull : 0ull));
+    return r;
+}
+
+NP8_HD Fx fx_of(double x) {
+    union {
+        double d;
+        uint64_t u;
+    } v;
+    v.d = x;
+    const int ex = (int)((v.u >> 52) & 0x7FF);
+    Fx r;
+    r.lo = 0ull;
+    r.hi = 0;
+    if (ex == 0 || ex == 0x7FF) return r;  // zero, subnormal (never an item's ll), inf / nan (never)
+    const uint64_t m = (v.u & 0xFFFFFFFFFFFFFull) | 0x10000000000000ull;
+    int sh = ex - 1075 + 64;  // x * 2^64 = m * 2^sh
+    if (sh > 74) sh = 74;     // |x| >= 2^63: saturates (never an item's ll)
+    if (sh >= 64) {
+        r.hi = (int64_t)(m << (sh - 64));
+    } else if (sh > 0) {
+        r.lo = m << sh;
+        r.hi = (int64_t)(m >> (64 - sh));
+    } else if (sh == 0) {
+        r.lo = m;
+    } else if (sh > -64) {
+        r.lo = m >> (-sh);
+    }
+    return (v.u >> 63) ? fx_neg(r) : r;
+}
+
+// The sum as a double: hi exactly (|hi| < 2^53), lo rounded, one fma -- a fixed function of the integer.
+NP8_HD double fx_to_double(Fx a) { return fma((double)a.hi, 0x1.0p64, (double)a.lo) * 0x1.0p-64; }
+
 // Executed work of np8_assign when AssignArgs::count_eval is set (timing mode): per wave, the cluster
 // quadratic forms its items evaluated (own rows included) and how many took the isotropic form, added
 // to counter pair (wave id mod kEvalSlots); regions 1-3 of evalc: exact auxiliaries (lanes, waves), full-table
@@ -69,10 +122,10 @@ enum : int32_t { kErrCapacity = 1, kErrSigma = 2, kErrInvariant = 4, kErrQueue =
 // can accept from it (DESIGN.md "Finalize").
 struct RecHeader {
     int32_t nreq;
-    int32_t pad;
-    double L_local;  // folded max-likelihood check: this rank's sum of log-likelihoods (np8_req_select)
+    int32_t pad[3];
+    Fx L_local;  // folded max-likelihood check: this rank's exact sum of log-likelihoods (np8_req_select)
 };
-constexpr int kRecHeaderBytes = 16;
+constexpr int kRecHeaderBytes = 32;
 
 struct Request {
     int64_t pos;   // global scan position (orders requests across ranks)
@@ -81,7 +134,7 @@ struct Request {
     int32_t zold;  // slot the item leaves
     int32_t lpos;  // position in the owner's label-sorted layout (-1: none)
     int32_t pad;
-    double dll;    // folded max-likelihood check: ll under the new slot - ll under zold (added if accepted)
+    Fx dll;        // folded max-likelihood check: ll under the new slot - ll under zold, exact (added if accepted)
 };
 
 // Item keys (DESIGN.md "Randomness"): the Philox item counter of every per-item draw is
@@ -110,7 +163,7 @@ struct WaveR2 {
 struct AssignArgs {
     const double *X;   // [D][n_loc] (structure of arrays), item order
     int32_t *z;        // [n_loc] slot ids, item order
-    int32_t sorted;    // run on the label-sorted layout (buffer ctl->cur of Xs/zs/ids)
+    int32_t sorted;    // run on the label-sorted layout (buffer 0 of Xs/zs/ids)
     const double *Xs[2];
     int32_t *zs[2];
     const int32_t *ids[2];  // position -> local item index
@@ -165,7 +218,7 @@ struct AssignArgs {
     // wave stores the sum of its items' log-likelihoods under their new label in llpart[wave] (a requester counts
     // under its old slot; its Request carries the difference); snap_on = a snapshot may be pending
     // (ctl->snap_pend): copy the labelling as it stands before this sweep into the snapshot buffers
-    double *llpart = nullptr;
+    Fx *llpart = nullptr;
     int32_t ll_on = 0, snap_on = 0;
     double gp0 = 0.0;  // Gp[0]: a new slot's isotropic precision is gp0 / v^2 (np8_finalize's write_new_slot)
     int32_t *z_best = nullptr, *cnt_best = nullptr;
@@ -212,7 +265,7 @@ struct FinArgs {
     int32_t world, rec_cap, kcap, D, M;
     int32_t *cnt;
     int32_t *z;
-    int32_t *zs[2];  // sorted-layout labels (buffer ctl->cur), null when not in use
+    int32_t *zs[2];  // sorted-layout labels (buffer 0 is the layout), null when not in use
     int64_t n_loc, offset;
     double *slot_mu, *slot_P, *slot_c, *slot_sigma, *slot_iso;
     double *slot_logn1;  // log(n - 1) of each live slot (the own-row weight), as its dense row holds it
@@ -236,7 +289,7 @@ struct FinArgs {
     int32_t *wdirty;
     // folded max-likelihood check (AssignArgs::ll_on): L = sum of the per-wave partials (one rank, ll_rec = 0) or of
     // the records' L_local (rank order, ll_rec = 1), plus the accepted requests' dll; snapshot decision on best[par]
-    const double *llpart = nullptr;
+    const Fx *llpart = nullptr;
     int64_t ll_n = 0;
     int32_t ll_on = 0, ll_rec = 0;
     int32_t snap_clear = 0, par = 0;  // snap_clear: the step's assign consumed ctl->snap_pend
@@ -419,7 +472,7 @@ struct LoglikArgs {
 struct ParamArgs {
     const double *X;  // item-order layout [D][n_loc]
     const int32_t *z;
-    const double *Xs[2];  // label-sorted layout (buffer ctl->cur) when sorted != 0
+    const double *Xs[2];  // label-sorted layout (buffer 0) when sorted != 0
     const int32_t *zs[2];
     int32_t sorted;
     int64_t n_loc;
@@ -453,9 +506,9 @@ struct SnapArgs {
 }  // namespace np8
 
 // Label-sorted layout (items grouped by cluster so that a wave shares its candidate set).
-// force: rebuild from the item-order arrays (X, z); otherwise re-sort buffer ctl->cur into
-// ctl->cur ^ 1 when more than n/32 items moved since the last sort.  The last scatter block flips
-// ctl->cur.
+// force: rebuild from the item-order arrays (X, z); otherwise re-sort buffer 0 when more than n/32 items moved
+// since the last sort.  The scatter writes buffer 1, np8_sort_copyback copies it back: the layout is always
+// buffer 0.
 struct SortArgs {
     const double *X;  // item-order layout [D][n]
     const int32_t *z;
@@ -521,7 +574,7 @@ hipError_t np8_launch_finalize(const np8::FinArgs &F, hipStream_t s);
 hipError_t np8_launch_step_tail(const np8::AssignArgs &A, const np8::FinArgs &F, const np8::PruneArgs &P,
                                 const np8::TailArgs &T, int64_t n_waves, int D, int M, hipStream_t s);
 hipError_t np8_launch_req_select(const unsigned char *stage, int64_t stage_cap, unsigned char *rec, int64_t rec_cap,
-                                 int kcap, int D, int req_max, const double *llpart, int64_t ll_n, hipStream_t s);
+                                 int kcap, int D, int req_max, const np8::Fx *llpart, int64_t ll_n, hipStream_t s);
 // A snapshot the folded max-likelihood check left pending (ctl->snap_pend): copy it now and clear the flag.
 hipError_t np8_launch_snapshot_flush(const np8::SnapArgs &A, np8::Ctl *ctl, hipStream_t s);
 hipError_t np8_launch_loglik(const np8::LoglikArgs &A, int D, hipStream_t s);

@@ -32,6 +32,7 @@ struct HypView {
     static constexpr int kNu = kCaux + 3;
     static constexpr int kLT = kCaux + 4;
     static constexpr int kSmax = kLT + DP;  // NIW screen: bound of the D-1 further log chi^2 draws
+    static constexpr int kUdiag = kSmax + 1;  // the diagonal of UinvT again, contiguous (one scalar load round)
 };
 
 // ll = c - q/2 with q = d' P d.  Isotropic entries (iso > 0, a wave-uniform branch): q = iso * |d|^2;
@@ -263,7 +264,7 @@ __device__ __forceinline__ void assign_item(const AssignArgs &A, const int64_t p
     constexpr int F = D + DP;
     const bool sorted = A.sorted != 0;  // label-sorted layout: X and zs indexed by position
     // (ternaries, not A.zs[cur]: a runtime index into the argument struct would move it to scratch)
-    const int cur = sorted ? A.ctl->cur : 0;
+    constexpr int cur = 0;  // the label-sorted layout is always buffer 0 (buffer 1: the re-sort's scratch)
     int32_t *__restrict__ zs = cur ? A.zs[1] : A.zs[0];
     const int32_t *__restrict__ ids = cur ? A.ids[1] : A.ids[0];
     const int64_t lk = sorted ? (int64_t)ids[p] : position_to_local(A, p);
@@ -561,7 +562,8 @@ __device__ __forceinline__ void assign_item(const AssignArgs &A, const int64_t p
             r.zold = zi;
             r.lpos = sorted ? (int32_t)p : -1;
             r.pad = 0;
-            r.dll = 0.0;
+            r.dll.lo = 0ull;
+            r.dll.hi = 0;
             A.req[q] = r;
             double *vmu = A.vmu + (int64_t)q * (D + 1);
             double y0[D];  // the item's frame again (not kept live through the draw: registers)
@@ -628,15 +630,35 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
     return __longlong_as_double(((int64_t)hi << 32) | (uint32_t)lo);
 }
 
+// Fx through a lane shuffle / readlane (four 32-bit pieces)
+__device__ __forceinline__ Fx fx_shfl_xor(Fx a, int o) {
+    const uint32_t l0 = (uint32_t)__shfl_xor((int)(uint32_t)a.lo, o), l1 = (uint32_t)__shfl_xor((int)(uint32_t)(a.lo >> 32), o);
+    const uint32_t h0 = (uint32_t)__shfl_xor((int)(uint32_t)(uint64_t)a.hi, o),
+                   h1 = (uint32_t)__shfl_xor((int)(uint32_t)((uint64_t)a.hi >> 32), o);
+    Fx r;
+    r.lo = ((uint64_t)l1 << 32) | l0;
+    r.hi = (int64_t)(((uint64_t)h1 << 32) | h0);
+    return r;
+}
+
+__device__ __forceinline__ Fx fx_readlane(Fx a, int l) {
+    Fx r;
+    r.lo = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(a.lo >> 32), l) << 32) |
+           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)a.lo, l);
+    r.hi = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)a.hi >> 32), l) << 32) |
+                     (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(uint64_t)a.hi, l));
+    return r;
+}
+
 // np8_assign_fast<D,M>: the common case of np8_assign -- the reference prior with an isotropic Lambda (every
 // G0 draw, and so every row, isotropic; the base measure's whitening diagonal), the label-sorted layout --
 // with only the work almost every lane needs: the own row, the candidate list (or the table), the two
-// levels of the auxiliary screen, the move.  A lane the screen cannot clear (an auxiliary may come within
-// kSkip of the running maximum: 0.3% of (item, auxiliary) pairs at C3), or a wave meeting a row that is not
-// isotropic, is deferred: its position goes to a queue that np8_assign then runs in queue mode, from the
-// start, with the full code (exact auxiliary draws, new-cluster requests).  A deferred lane writes nothing
-// here, so every item's result is np8_assign's, bit for bit.  The lean kernel keeps its registers low
-// (no exact fp64 draws, no request payload): more waves per SIMD to hide the loads' latency.
+// levels of the auxiliary screen, the exact fp64 draw for the auxiliaries the screen cannot clear (an auxiliary
+// may come within kSkip of the running maximum: 0.3% of (item, auxiliary) pairs at C3), the move and the
+// new-cluster request with its payload.  Only a lane whose own row or a walked row is not isotropic is deferred:
+// its position goes to a queue that np8_assign then runs in queue mode, from the start, with the full code.  A
+// deferred lane writes nothing here, so every item's result is np8_assign's, bit for bit; when every live row is
+// isotropic the host leaves the queue launch out (AssignArgs::no_queue; a deferred lane would set kErrQueue).
 // LL: a max-likelihood check sweep with the sum folded in (AssignArgs::ll_on): each wave also stores the sum of its
 // items' log-likelihoods under their new labels -- the values np8_loglik would compute after the step, operation for
 // operation (the walk's quadratic forms are the table form's isotropic one) -- in a separate instance, so that the
@@ -669,15 +691,39 @@ __global__ __launch_bounds__(NP8_ASSIGN_BLOCK) __attribute__((amdgpu_waves_per_e
     // a max-likelihood snapshot the last check left pending: the labelling before this step is the one it keeps
     const int snap = (!LL && A.snap_on) ? A.ctl->snap_pend : 0;
     if (snap) A.z_best[il] = zi;
+    NP8_CLK(1);
+    bool defer = COUNT;  // counting runs: every lane takes np8_assign's counting instance
+    PickState st;
+    st.S = 1.0;
+    st.u = -1.0;
+    st.T = 0.0;
+    double d2own = 0.0;  // |x - mu_own|^2: the own row's quadratic form and the list's radius check
+    double ll_own = 0.0, llp = 0.0;  // (LL) ll under the own row and under the row picked so far
+    int32_t jo = 0, nlist = 0;
+    double r2list = 0.0;
+    int32_t pslot = zi;
+    // the wave's first own slot (usually its only one in the label-sorted layout): its row's scalars are requested
+    // first, so that the auxiliaries' level-1 screen below runs while they are in flight
+    // (read-only in this kernel: restrict lets the wave-uniform reads go through the scalar cache)
+    const double *__restrict__ slot_mu = A.slot_mu, *__restrict__ slot_iso = A.slot_iso, *__restrict__ slot_c = A.slot_c,
+                               *__restrict__ slot_logn1 = A.slot_logn1, *__restrict__ plr2_s = A.plr2_s;
+    const int32_t *__restrict__ dense_of = A.dense_of, *__restrict__ plen_s = A.plen_s;
+    const int32_t s_1 = __builtin_amdgcn_readfirstlane(zi);
+    double mo_1[D];
+#pragma unroll
+    for (int a = 0; a < D; ++a) mo_1[a] = slot_mu[(int64_t)s_1 * D + a];
+    const double iso_1 = slot_iso[s_1], cs_1 = slot_c[s_1], l1_1 = slot_logn1[s_1];
+    const int32_t js_1 = dense_of[s_1], pl_1 = plen_s[s_1];
+    const double pr_1 = plr2_s[s_1];
     // level 1 of the auxiliary screen while the own row's loads are in flight: each auxiliary's bound from its
     // Philox call 0, without the threshold (the running maximum), which is compared below
     double ny = 0.0;
     {
-        const double *U = hyp + H::kUinvT;  // diagonal (launch condition): whiten() + norm_of() with zeros left out
+        const double *U = hyp + H::kUdiag;  // diagonal (launch condition): whiten() + norm_of() with zeros left out
         double n2 = 0.0;
 #pragma unroll
         for (int a = 0; a < D; ++a) {
-            const double y = U[a * D - (a * (a - 1)) / 2] * (x[a] - hyp[H::kMu0 + a]);
+            const double y = U[a] * (x[a] - hyp[H::kMu0 + a]);
             n2 = fma(y, y, n2);
         }
         ny = sqrt(n2);
@@ -691,30 +737,15 @@ __global__ __launch_bounds__(NP8_ASSIGN_BLOCK) __attribute__((amdgpu_waves_per_e
             uint32_t w[4];
             philox_call(A.seed, ig, t, kStreamAux, (uint32_t)(m * Qa), w);
             ub1[m] = aux_screen_ub<D>(w, 0.0f, 0.0f, nyf, nuf, rskf, cauxf, 0.0f, false);
+            asm volatile("" ::"v"(ub1[m]));  // computed here, while the own row's loads are in flight (not sunk)
         }
     }
-    NP8_CLK(1);
-    bool defer = COUNT;  // counting runs: every lane takes np8_assign's counting instance
-    PickState st;
-    st.S = 1.0;
-    st.u = -1.0;
-    st.T = 0.0;
-    double d2own = 0.0;  // |x - mu_own|^2: the own row's quadratic form and the list's radius check
-    double ll_own = 0.0, llp = 0.0;  // (LL) ll under the own row and under the row picked so far
-    int32_t jo = 0, nlist = 0;
-    double r2list = 0.0;
-    int32_t pslot = zi;
     {
         // one pass per distinct own slot of the wave (one in the label-sorted layout); everything about the
         // own row is read by slot in one round of scalar loads: the parameters from the slot tables (the
         // candidate rows copy them), log(n - 1), the dense row and its candidate list's length and radius
-        uint64_t pend = __ballot(1);
-        while (pend) {
-            const int32_t s = __builtin_amdgcn_readlane(zi, __ffsll((unsigned long long)pend) - 1);
-            const double *mo = A.slot_mu + (int64_t)s * D;
-            const double iso = A.slot_iso[s], cs = A.slot_c[s], l1 = A.slot_logn1[s];
-            const int32_t js = A.dense_of[s], pl = A.plen_s[s];
-            const double pr = A.plr2_s[s];
+        auto own = [&](int32_t s, const double (&mo)[D], double iso, double cs, double l1, int32_t js, int32_t pl,
+                       double pr) {
             if (zi == s) {
                 jo = js;
                 nlist = pl;
@@ -730,6 +761,15 @@ __global__ __launch_bounds__(NP8_ASSIGN_BLOCK) __attribute__((amdgpu_waves_per_e
                     defer = true;
                 }
             }
+        };
+        own(s_1, mo_1, iso_1, cs_1, l1_1, js_1, pl_1, pr_1);  // the first group, from the loads issued above
+        uint64_t pend = __ballot(zi != s_1);
+        while (pend) {  // (waves of several own slots: a stale layout, the range's edges)
+            const int32_t s = __builtin_amdgcn_readlane(zi, __ffsll((unsigned long long)pend) - 1);
+            double mo[D];
+#pragma unroll
+            for (int a = 0; a < D; ++a) mo[a] = slot_mu[(int64_t)s * D + a];
+            own(s, mo, slot_iso[s], slot_c[s], slot_logn1[s], dense_of[s], plen_s[s], plr2_s[s]);
             pend &= ~__ballot(zi == s);
         }
     }
@@ -935,15 +975,15 @@ __global__ __launch_bounds__(NP8_ASSIGN_BLOCK) __attribute__((amdgpu_waves_per_e
         A.z[il] = snew;
         zs[p] = snew;
     }
-    if constexpr (LL) {  // the wave's sum, in a fixed order (a requester counts under its old slot)
-        double v = req ? ll_own : llp;
+    if constexpr (LL) {  // the wave's exact sum (a requester counts under its old slot)
+        Fx v = fx_of(req ? ll_own : llp);
         const uint64_t act = __ballot(1);
         if (act == ~0ull) {
 #pragma unroll
-            for (int o = 32; o > 0; o >>= 1) v = v + __shfl_xor(v, o);
-        } else {  // the range's last, partial wave: lane order
-            double s = 0.0;
-            for (uint64_t m = act; m; m &= m - 1ull) s = s + readlane_d(v, __ffsll((unsigned long long)m) - 1);
+            for (int o = 32; o > 0; o >>= 1) v = fx_add(v, fx_shfl_xor(v, o));
+        } else {  // the range's last, partial wave
+            Fx s = {0ull, 0};
+            for (uint64_t m = act; m; m &= m - 1ull) s = fx_add(s, fx_readlane(v, __ffsll((unsigned long long)m) - 1));
             v = s;
         }
         if (lane == __ffsll((unsigned long long)act) - 1) A.llpart[(p - A.p0) >> 6] = v;
@@ -963,14 +1003,15 @@ __global__ __launch_bounds__(NP8_ASSIGN_BLOCK) __attribute__((amdgpu_waves_per_e
             r.zold = zi;
             r.lpos = (int32_t)p;
             r.pad = 0;
-            r.dll = 0.0;
+            r.dll.lo = 0ull;
+            r.dll.hi = 0;
             if (LL) {  // ll under the slot np8_finalize would build from (v, mu) (write_new_slot), as np8_loglik evaluates it
                 const double v = vm[0], v2 = v * v;
                 const double iso_n = A.gp0 / v2, c_n = fma(-(double)D, log_pos(fabs(v)), hyp[H::kCaux]);
                 double s2 = (x[0] - vm[1]) * (x[0] - vm[1]);
 #pragma unroll
                 for (int a = 1; a < D; ++a) s2 = fma(x[a] - vm[1 + a], x[a] - vm[1 + a], s2);
-                r.dll = fma(-0.5, s2 * iso_n, c_n) - ll_own;
+                r.dll = fx_add(fx_of(fma(-0.5, s2 * iso_n, c_n)), fx_neg(fx_of(ll_own)));
             }
             A.req[q] = r;
         }
@@ -1006,8 +1047,8 @@ __global__ __launch_bounds__(kSortThreads) void np8_sort_hist(SortArgs S) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     int *lh = reinterpret_cast<int *>(smem);
     const int nb = S.kcap * S.nsub;
-    const int32_t *z = S.force ? S.z : (S.ctl->cur ? S.zs[1] : S.zs[0]);
-    const int32_t *ids = S.force ? nullptr : (S.ctl->cur ? S.ids[1] : S.ids[0]);
+    const int32_t *z = S.force ? S.z : S.zs[0];
+    const int32_t *ids = S.force ? nullptr : S.ids[0];
     for (int s = threadIdx.x; s < nb; s += kSortThreads) lh[s] = 0;
     __syncthreads();
     for (int k = 0; k < kSortItems; ++k) {
@@ -1181,32 +1222,33 @@ __device__ double block_sum_d(double v, double *sh /* >= 16 doubles */) {
     return t;
 }
 
-// Two sums at once (one set of barriers), each in block_sum_d's order.
-__device__ double2 block_sum2_d(double a, double b, double2 *sh /* >= 16 */) {
+// Exact block sum of Fx values (every thread returns it).
+__device__ Fx block_sum_fx(Fx v, Fx *sh /* >= 16 */) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
-        a = a + __shfl_xor(a, o);
-        b = b + __shfl_xor(b, o);
+        const uint32_t l0 = (uint32_t)__shfl_xor((int)(uint32_t)v.lo, o), l1 = (uint32_t)__shfl_xor((int)(uint32_t)(v.lo >> 32), o);
+        const uint32_t h0 = (uint32_t)__shfl_xor((int)(uint32_t)(uint64_t)v.hi, o),
+                       h1 = (uint32_t)__shfl_xor((int)(uint32_t)((uint64_t)v.hi >> 32), o);
+        Fx w;
+        w.lo = ((uint64_t)l1 << 32) | l0;
+        w.hi = (int64_t)(((uint64_t)h1 << 32) | h0);
+        v = fx_add(v, w);
     }
     __syncthreads();
-    if (lane == 0) sh[wid] = make_double2(a, b);
+    if (lane == 0) sh[wid] = v;
     __syncthreads();
-    double2 t = sh[0];
-    for (int w = 1; w < nw; ++w) {
-        t.x = t.x + sh[w].x;
-        t.y = t.y + sh[w].y;
-    }
+    Fx t = sh[0];
+    for (int w = 1; w < nw; ++w) t = fx_add(t, sh[w]);
     __syncthreads();
     return t;
 }
 
-// The folded max-likelihood check's per-rank sum: the assign's per-wave partials, thread-strided then block_sum_d
-// (np8_finalize for one rank, np8_req_select for the exchanged record: the same order).
-__device__ double partials_sum(const double *__restrict__ part, int64_t n, double *sh) {
-    double v = 0.0;
-    for (int64_t k = threadIdx.x; k < n; k += blockDim.x) v = v + part[k];
-    return block_sum_d(v, sh);
+// The folded max-likelihood check's per-rank sum of the assign's per-wave partials (exact).
+__device__ Fx partials_sum(const Fx *__restrict__ part, int64_t n, Fx *sh) {
+    Fx v = {0ull, 0};
+    for (int64_t k = threadIdx.x; k < n; k += blockDim.x) v = fx_add(v, part[k]);
+    return block_sum_fx(v, sh);
 }
 
 }  // namespace
@@ -1381,12 +1423,13 @@ __device__ int64_t select_kth_pos(PosAt pos_at, int n, int k, int *hist /* 2048 
 // (the body of np8_req_select, also run as the serial tail of np8_step_tail)
 __device__ void req_select_block(const unsigned char *__restrict__ stage, int64_t stage_cap,
                                  unsigned char *__restrict__ rec, int64_t rec_cap, int kcap, int D, int req_max,
-                                 const double *__restrict__ llpart, int64_t ll_n, int *hist /* LDS int[2048] */) {
+                                 const Fx *__restrict__ llpart, int64_t ll_n, int *hist /* LDS int[2048] */) {
     __shared__ int sh[32];
     __shared__ int s_cnt;
-    __shared__ double shd[16];
-    // folded max-likelihood check: this rank's sum travels in the exchanged record's header
-    const double Lloc = llpart ? partials_sum(llpart, ll_n, shd) : 0.0;
+    __shared__ Fx shfx[16];
+    // folded max-likelihood check: this rank's exact sum travels in the exchanged record's header
+    Fx Lloc = {0ull, 0};
+    if (llpart) Lloc = partials_sum(llpart, ll_n, shfx);
     RecHeader *sh_hdr = reinterpret_cast<RecHeader *>(const_cast<unsigned char *>(stage));
     const Request *sreq = reinterpret_cast<const Request *>(stage + kRecHeaderBytes + 4ll * kcap);
     const double *svmu = reinterpret_cast<const double *>(stage + record_vmu_offset(kcap, (int)stage_cap));
@@ -1415,7 +1458,7 @@ __device__ void req_select_block(const unsigned char *__restrict__ stage, int64_
 
 __global__ __launch_bounds__(kFinThreads) void np8_req_select(const unsigned char *__restrict__ stage, int64_t stage_cap,
                                                               unsigned char *__restrict__ rec, int64_t rec_cap, int kcap,
-                                                              int D, int req_max, const double *__restrict__ llpart,
+                                                              int D, int req_max, const Fx *__restrict__ llpart,
                                                               int64_t ll_n) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     req_select_block(stage, stage_cap, rec, rec_cap, kcap, D, req_max, llpart, ll_n, reinterpret_cast<int *>(smem));
@@ -1452,7 +1495,7 @@ __device__ int finalize_block(const FinArgs &F, unsigned char *smem) {
     // everything the common step (no request accepted) needs from global memory, loaded in one round:
     // old counts (liveness changes), deltas, and the table entries of this thread's first kFinPre slots
     constexpr int kFinPre = 2;
-    int cold[kFinPre], d0[kFinPre];
+    int cold[kFinPre], d0[kFinPre], dof[kFinPre];
     double pc[kFinPre], piso[kFinPre], plb0[kFinPre], plb1[kFinPre];
     const int32_t *delta0 = rec_delta(F, 0);
 #pragma unroll
@@ -1461,6 +1504,7 @@ __device__ int finalize_block(const FinArgs &F, unsigned char *smem) {
         const bool in = s < s1;
         cold[q] = in ? F.cnt[s] : 0;
         d0[q] = in ? delta0[s] : 0;  // rank 0's delta in the same round of loads (the single-rank step: all of them)
+        dof[q] = in ? F.dense_of[s] : -1;
         pc[q] = in ? F.slot_c[s] : 0.0;
         piso[q] = in ? F.slot_iso[s] : 0.0;
         plb0[q] = (in && F.slack_test) ? F.lb[s] : 0.0;
@@ -1468,21 +1512,103 @@ __device__ int finalize_block(const FinArgs &F, unsigned char *smem) {
     }
     const int cand_fresh = F.ctl->cand_fresh;
     const int nreq0 = rec_header(F, 0)->nreq;  // (same round: every thread, one address)
-    // the folded check's partials (one rank), eight independent loads per round, summed in partials_sum's order
-    double llv = 0.0;
+    int nreq_all = min(nreq0, F.rec_cap);
+    for (int r = 1; r < F.world; ++r) nreq_all += min(rec_header(F, r)->nreq, F.rec_cap);
+    // the folded check's partials (one rank), eight independent loads per round
+    Fx llv = {0ull, 0};
     if (F.ll_on && !F.ll_rec) {
+        const uint64_t *pp = reinterpret_cast<const uint64_t *>(F.llpart);
         for (int64_t b = tid; b < F.ll_n; b += 8 * kFinThreads) {
-            double v[8];
+            uint64_t vl[8], vh[8];
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
                 const int64_t k = b + (int64_t)u * kFinThreads;
-                v[u] = k < F.ll_n ? F.llpart[k] : 0.0;
+                const bool in = k < F.ll_n;
+                vl[u] = in ? pp[2 * k] : 0ull;
+                vh[u] = in ? pp[2 * k + 1] : 0ull;
             }
 #pragma unroll
-            for (int u = 0; u < 8; ++u) llv = llv + v[u];
+            for (int u = 0; u < 8; ++u) {
+                Fx w;
+                w.lo = vl[u];
+                w.hi = (int64_t)vh[u];
+                llv = fx_add(llv, w);
+            }
         }
     }
 
+    // The steady step (no request, no slot changing liveness, rows current): the dense table keeps its rows, so only
+    // the slots whose count moved get their count and logs rewritten (rows from the prefetched dense_of) -- no scan,
+    // no table rebuild: one round of loads and a barrier or two.  Everything else takes the general path below.
+    {
+        int cnew[kFinPre], lch = 0;
+#pragma unroll
+        for (int q = 0; q < kFinPre; ++q) {
+            const int s = s0 + q;
+            int c = cold[q] + d0[q];
+            if (s < s1)
+                for (int r = 1; r < F.world; ++r) c += rec_delta(F, r)[s];
+            cnew[q] = c;
+            lch |= (s < s1) && ((c > 0) != (cold[q] > 0));
+        }
+        const int any_lch = __syncthreads_or(lch);
+        if (!any_lch && nreq_all == 0 && cand_fresh && per <= kFinPre && !F.frame_payload) {  // block-uniform
+            int viol = 0;
+#pragma unroll
+            for (int q = 0; q < kFinPre; ++q) {
+                const int s = s0 + q;
+                if (s < s1 && cnew[q] != cold[q]) {  // a live slot whose count moved (a dead one stays dead)
+                    const int c = cnew[q];
+                    F.cnt[s] = c;
+                    const double l0 = log_pos((double)c), l1 = (c > 1) ? log_pos((double)(c - 1)) : kZeroLogWeight;
+                    if (F.slack_test && !(fabs(l0 - plb0[q]) <= 0.5 * kListSlack && fabs(l1 - plb1[q]) <= 0.5 * kListSlack))
+                        viol = 1;
+                    double *e = F.cand + (int64_t)dof[q] * CS + D + DP;
+                    e[kFieldLogn] = l0;
+                    e[kFieldLogn1] = l1;
+                    F.slot_logn1[s] = l1;
+                }
+            }
+            const int stale_f = __syncthreads_or(viol);  // (unchanged slots passed the test at the last step)
+            if (F.ll_on) {
+                __shared__ Fx shfx_f[16];
+                Fx S = block_sum_fx(llv, shfx_f);
+                Fx Sloc = S;
+                if (F.ll_rec)
+                    for (int r = 0; r < F.world; ++r) S = fx_add(S, rec_header(F, r)->L_local);
+                const double L = fx_to_double(S);
+                if (tid == 0) {
+                    F.ctl->L = L;
+                    F.ctl->L_local = fx_to_double(F.ll_rec ? reinterpret_cast<const RecHeader *>(F.local_rec)->L_local : Sloc);
+                    const double b = F.best[F.par];
+                    const bool better = L > b;
+                    F.best[F.par ^ 1] = better ? L : b;
+                    if (better) *F.have_best = 1;
+                    F.ctl->snap_pend = better ? 1 : 0;
+                }
+            } else if (F.snap_clear && tid == 0) {
+                F.ctl->snap_pend = 0;
+            }
+            if (F.local_rec) {  // the local record's deltas (sparse when it is the record just read)
+                int32_t *delta = reinterpret_cast<int32_t *>(F.local_rec + kRecHeaderBytes);
+                if (F.local_rec == F.recs) {
+#pragma unroll
+                    for (int q = 0; q < kFinPre; ++q)
+                        if (s0 + q < s1 && d0[q] != 0) delta[s0 + q] = 0;
+                } else {
+                    for (int s = tid; s < kcap; s += kFinThreads) delta[s] = 0;
+                    if (tid == 0) reinterpret_cast<RecHeader *>(F.local_rec)->nreq = 0;
+                }
+            }
+            if (tid == 0) {
+                F.ctl->qwaves = 0;
+                if (F.prior == kPriorNiw) F.ctl->n_pend = 0;
+                if (F.moved_mirror) *F.moved_mirror = F.ctl->moved;
+                if (F.advance) F.ctl->t_base += F.advance;
+            }
+            return stale_f;
+        }
+    }
     if (tid == 0) {
         int n = 0;
         for (int r = 0; r < F.world; ++r) {
@@ -1579,13 +1705,13 @@ __device__ int finalize_block(const FinArgs &F, unsigned char *smem) {
                 write_new_slot(F, request_vmu(F, base, kidx[q]), s);
             }
             if (F.wdirty) F.wdirty[s] = 1;
-            if (F.ll_on) reinterpret_cast<double *>(keys)[q] = r.dll;  // (keys are sorted: no longer needed)
+            if (F.ll_on) llv = fx_add(llv, r.dll);  // (exact: any order)
             cnt_s[s] = 1;
             atomicSub(&cnt_s[r.zold], 1);  // a live slot (the requester is in it), never one of the free ones
             const int64_t item = key_item(r.i);
             if (item >= F.offset && item < F.offset + F.n_loc) {
                 F.z[item - F.offset] = s;
-                if (F.zs[0] && r.lpos >= 0) (F.ctl->cur ? F.zs[1] : F.zs[0])[r.lpos] = s;
+                if (F.zs[0] && r.lpos >= 0) F.zs[0][r.lpos] = s;
             }
         }
     }
@@ -1656,19 +1782,15 @@ __device__ int finalize_block(const FinArgs &F, unsigned char *smem) {
     // log-likelihoods (requesters under their old slot) + the accepted requests' dll, in position order; the
     // labelling is snapshotted on improvement by the next np8_assign_fast (ctl->snap_pend)
     if (F.ll_on) {
-        __shared__ double2 shd2[16];
-        double v = 0.0;
-        for (int q = tid; q < A; q += kFinThreads) v = v + reinterpret_cast<const double *>(keys)[q];
-        const double2 sums = block_sum2_d(llv, v, shd2);
-        double S1 = sums.x;
-        if (F.ll_rec) {
-            S1 = rec_header(F, 0)->L_local;
-            for (int r = 1; r < F.world; ++r) S1 = S1 + rec_header(F, r)->L_local;
-        }
-        const double L = S1 + sums.y;
+        __shared__ Fx shfx[16];
+        Fx S = block_sum_fx(llv, shfx);  // (one rank: partials + accepted requests' dll; sharded: the dll only)
+        Fx Sloc = S;
+        if (F.ll_rec)
+            for (int r = 0; r < F.world; ++r) S = fx_add(S, rec_header(F, r)->L_local);
+        const double L = fx_to_double(S);
         if (tid == 0) {
             F.ctl->L = L;
-            F.ctl->L_local = F.ll_rec ? reinterpret_cast<const RecHeader *>(F.local_rec)->L_local : S1;
+            F.ctl->L_local = fx_to_double(F.ll_rec ? reinterpret_cast<const RecHeader *>(F.local_rec)->L_local : Sloc);
             const double b = F.best[F.par];
             const bool better = L > b;
             F.best[F.par ^ 1] = better ? L : b;
@@ -1892,7 +2014,10 @@ __global__ __launch_bounds__(kFinThreads) void np8_fin_prune(FinArgs F, PruneArg
             }
             __builtin_amdgcn_s_sleep(2);
         }
-        if (!ok) atomicOr(&F.ctl->err, kErrSpin);
+        if (!ok) {  // the lists this workgroup owes are not built: the assign must walk the whole table
+            atomicOr(&F.ctl->err, kErrSpin);
+            __hip_atomic_store(&P.ctl->lists_ok, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
         s_ok = ok;
     }
     __syncthreads();
@@ -2054,7 +2179,7 @@ __global__ __launch_bounds__(64) void np8_suffstats(ParamArgs A) {
     __shared__ double T[W][65];
     const int lane = threadIdx.x;
     const bool sorted = A.sorted != 0;
-    const int cur = sorted ? A.ctl->cur : 0;
+    constexpr int cur = 0;  // the label-sorted layout is always buffer 0 (buffer 1: the re-sort's scratch)
     const double *__restrict__ X = sorted ? (cur ? A.Xs[1] : A.Xs[0]) : A.X;
     const int32_t *__restrict__ z = sorted ? (cur ? A.zs[1] : A.zs[0]) : A.z;
     const int64_t n = A.n_loc;
@@ -2621,7 +2746,7 @@ hipError_t np8_launch_fin_prune(const FinArgs &F, const PruneArgs &P, hipStream_
 }
 
 hipError_t np8_launch_req_select(const unsigned char *stage, int64_t stage_cap, unsigned char *rec, int64_t rec_cap,
-                                 int kcap, int D, int req_max, const double *llpart, int64_t ll_n, hipStream_t s) {
+                                 int kcap, int D, int req_max, const Fx *llpart, int64_t ll_n, hipStream_t s) {
     hipLaunchKernelGGL(np8_req_select, dim3(1), dim3(kFinThreads), sizeof(int) * 2048, s, stage, stage_cap, rec, rec_cap,
                        kcap, D, req_max, llpart, ll_n);
     return hipGetLastError();

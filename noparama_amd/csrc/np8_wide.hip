@@ -345,7 +345,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NP8_WIDE_WA
     const int64_t p = pw + lane;
     const bool valid = p < A.p1;
     const bool sorted = A.sorted != 0;
-    const int cur = sorted ? A.ctl->cur : 0;
+    constexpr int cur = 0;  // the label-sorted layout is always buffer 0 (buffer 1: the re-sort's scratch)
     int32_t *__restrict__ zs = cur ? A.zs[1] : A.zs[0];
     const int32_t *__restrict__ ids = cur ? A.ids[1] : A.ids[0];
     const float *__restrict__ X = reinterpret_cast<const float *>(sorted ? (cur ? A.Xs[1] : A.Xs[0]) : A.X);
@@ -660,7 +660,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NP8_WIDE_WA
             r.zold = zi;
             r.lpos = sorted ? (int32_t)pc : -1;
             r.pad = 0;
-            r.dll = 0.0;
+            r.dll.lo = 0ull;
+            r.dll.hi = 0;
             A.req[q] = r;
             double *vmu = A.vmu + (int64_t)q * (D + 1);
             wide_frame_payload<D>(hyp, X, n, xr, vmu);
@@ -747,7 +748,7 @@ __global__ __launch_bounds__(256) void np8_loglik_wide_mfma(AssignArgs A, double
     const int64_t p = pw + lane;
     const bool valid = p < A.n_loc;
     const bool sorted = A.sorted != 0;
-    const int cur = sorted ? A.ctl->cur : 0;
+    constexpr int cur = 0;  // the label-sorted layout is always buffer 0 (buffer 1: the re-sort's scratch)
     const int32_t *__restrict__ zs = cur ? A.zs[1] : A.zs[0];
     const float *__restrict__ X = reinterpret_cast<const float *>(sorted ? (cur ? A.Xs[1] : A.Xs[0]) : A.X);
     const int64_t n = A.n_loc;
@@ -814,7 +815,7 @@ __global__ __launch_bounds__(256) void np8_suffstats_wide(ParamArgs P) {
     __shared__ float tile[4][D][65];  // per wave: [dim][item] (+1 pad: conflict-free column reads)
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, g = lane >> 4, col = lane & 15;
     const bool sorted = P.sorted != 0;
-    const int cur = sorted ? P.ctl->cur : 0;
+    constexpr int cur = 0;  // the label-sorted layout is always buffer 0 (buffer 1: the re-sort's scratch)
     const float *__restrict__ X = reinterpret_cast<const float *>(sorted ? (cur ? P.Xs[1] : P.Xs[0]) : P.X);
     const int32_t *__restrict__ z = sorted ? (cur ? P.zs[1] : P.zs[0]) : P.z;
     const int64_t n = P.n_loc;

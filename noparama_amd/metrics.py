@@ -2,8 +2,10 @@
 (src/clustering_performance.cpp:14-82) -- contingency matrix with the ground truth as rows
 (calculateContingencyMatrix :14-36), purity (:52), Rand index (:65) and adjusted Rand index (:75) --
 in int64 counts instead of the reference's int32 (which overflow past a few hundred items).
-Same arithmetic as the C++ mirror (host/np_host.cpp clustering_performance::calculate): a 0/0 ARI is NaN,
-as the reference's division gives.
+Same arithmetic as the C++ mirror (host/np_host.cpp clustering_performance::calculate).  Where the reference returns
+early and leaves the index unset (clustering_performance.cpp:70-73, and S == 0), both mirrors report NaN: that is
+their own convention for the reference's early return, not a value the reference computes (no reference fixture
+pins it).
 """
 from __future__ import annotations
 
