@@ -35,6 +35,7 @@ HBM_PEAK_GBS = 8000.0
 # committed rocprofv3 PMC summaries of the assign kernels (HBM bytes per launch, tools/prof*.sh)
 C3_TRAFFIC = "traffic_r03e.json"
 C5_TRAFFIC = "traffic_r03e_c5.json"
+MIXED_TRAFFIC = "traffic_r04_mixed.json"  # PMC pass of the mixed regime (tools/prof_mixed.sh, tools/summarize_profile.py)
 
 
 def binding_roof(exec_flops, abytes, ms, peak_tflops, kname):
@@ -215,7 +216,8 @@ def main():
             "dtype": "f32-mfma contraction, f64 draws" if wide else "f64",
             "data": "synthetic",
             "config": {
-                "workload": f"{args.config}: N={N} D={D} K~{K} M=3 mixture, warm state, "
+                "workload": f"{args.config}: N={N} D={D} K~{K} M=3 mixture, warm state (theta = the generating "
+                            "parameters, z = the ground truth), "
                             + ("NIW prior, fp32 items + fp32 MFMA contraction, " if wide else "")
                             + {"frozen": "frozen cluster parameters",
                                "mh_g0": "mh_g0 cluster-parameter update (20 MH steps/cluster/sweep)",
@@ -365,6 +367,7 @@ def measure(smp, sweeps, steps, warmup, graphs, dist, torch, n_loc, D, wide, S, 
             "many_group_wave_frac": (sc1["many_group_waves"] - sc0["many_group_waves"]) / cnt_sweeps
             / max((n_loc + 63) // 64, 1),
             "list_entries_per_item": (sc1["list_entries"] - sc0["list_entries"]) / cnt_sweeps / max(n_loc, 1),
+            "pick_evals_per_item": (sc1["pick_evals"] - sc0["pick_evals"]) / cnt_sweeps / max(n_loc, 1),
             "iso_fraction": nq_iso / max(nq, 1),
             "tflops": exec_flops / (ms_assign * 1e-3) / 1e12 if ms_assign > 0 else None,
             "frac_of_peak": exec_flops / (ms_assign * 1e-3) / 1e12 / peak if ms_assign > 0 else None,
@@ -411,7 +414,7 @@ def cold_start(args, X, labels, D, opts, device, torch):
         smp.sweep(50 - args.cold_sweeps)
     K50 = smp.K
     m = measure(smp, lambda n, sync=True: smp.sweep(n, sync=sync), 100, 0, True, None, torch, X.shape[0], D,
-                False, 1, None)
+                False, 1, os.path.join(ROOT, "profiles", MIXED_TRAFFIC))
     out["mixed"] = {"sweeps": "50..149 (then 20 + 20 untimed for the launch times and counters)",
                     "value": 100 / m["dt"], "unit": "sweeps/s", "ms_per_sweep": m["dt"] / 100 * 1e3,
                     "K_at_50": K50, "K_final": m["K_final"], "roofline": m["roofline"]}
@@ -452,8 +455,8 @@ def c5_record(args, device, torch):
 
     a = _ap.Namespace(**{**vars(args), "config": "C5", "d": 64, "k": 256, "substeps": 1})
     X, z, mu, sig, opts = workload(a)
-    out = {"workload": "C5: N=1000000 D=64 K~256 M=3 mixture, warm state, NIW prior, fp32 items + fp32 MFMA "
-                       "contraction"}
+    out = {"workload": "C5: N=1000000 D=64 K~256 M=3 mixture, warm state (theta = the generating parameters, "
+                       "z = the ground truth), NIW prior, fp32 items + fp32 MFMA contraction"}
     for pu, steps in (("frozen", 40), ("niw_conjugate", 20)):
         smp = NealAlgorithm8(64, seed=args.seed, device=device, param_update=pu, **opts)
         smp.set_data(X)
@@ -521,7 +524,8 @@ def main_sm(args):
         "dtype": "f64",
         "data": "synthetic",
         "config": {
-            "workload": f"{args.config}: N={N} D={D} K~{K} mixture, warm state, {name} split-merge "
+            "workload": f"{args.config}: N={N} D={D} K~{K} mixture, warm state (theta = the generating parameters, "
+                        f"z = the ground truth), {name} split-merge "
                         f"(sams_prior, reference rules), {args.param_update} cluster parameters",
             "N": N, "D": D, "K_final": Kf, "attempt_outcomes": d,
             "state_rebuilds": nm, "attempt_batches": ne,

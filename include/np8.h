@@ -141,6 +141,9 @@ typedef struct {
      * into the data-parallel step (cumulative), candidate-list rebuilds by the conditional step tail (steps whose
      * counts moved beyond the lists' slack), and steps that kept the lists of the last build */
     int64_t folded_checks, tail_list_builds, tail_steps;
+    /* NP8_TIMING_COUNTERS: walked candidate rows within kSkip (80 nats) of the running maximum, i.e. that pay the
+     * pick's exp and division (cumulative) */
+    int64_t pick_evals;
 } np8_stats_t;
 
 /* Create / destroy.  Replaces NealAlgorithm8::NealAlgorithm8 (np_neal_algorithm8.cpp:17-34). */

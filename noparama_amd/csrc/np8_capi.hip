@@ -64,6 +64,10 @@ struct np8_ctx {
     int32_t *wdirty = nullptr;
     double *lam_lo = nullptr, *wdist = nullptr;  // wide-path candidate pruning (np8_wide_dist)
     double *acc = nullptr;  // [kcap][D + DP] parameter-update statistics
+    // wide path, one rank, niw_conjugate: np8_suffstats_wide's run records (reduced by np8_niw_post, no atomics)
+    double *part = nullptr;
+    int32_t *part_slot = nullptr;
+    int64_t part_waves = 0;
     // candidate pruning (np8_prune): per-slot radii and per-row candidate lists
     double *r2 = nullptr;
     WaveR2 *wr2 = nullptr;  // per-wave radius records of the sweep's assign (ceil(n_loc / 64))
@@ -475,7 +479,7 @@ void free_device(np8_ctx *c) {
                     c->sm_typ, c->sm_slist, c->sm_stheta, c->stage, c->evalc, c->z_base, c->cnt_base,
                     c->chg_slot, c->mu_base, c->sigma_base, c->chg_item, c->chg_count, c->chg_flags,
                     c->inv_hist, c->inv_out, c->queue, c->qcount, c->qlist, c->slot_logn1, c->plen_s,
-                    c->plr2_s, c->sm_mb, c->lb, c->llpart};
+                    c->plr2_s, c->sm_mb, c->lb, c->llpart, c->part, c->part_slot};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     if (c->sm_first_host) (void)hipHostFree(c->sm_first_host);
@@ -499,6 +503,8 @@ void free_device(np8_ctx *c) {
     c->slot_iso = nullptr;
     c->lb = nullptr;
     c->llpart = nullptr;
+    c->part = nullptr;
+    c->part_slot = nullptr;
     c->acc = nullptr;
     c->r2 = nullptr;
     c->wr2 = nullptr;
@@ -1246,6 +1252,13 @@ int param_update(np8_ctx *c, int stats_mode = 0) {
     const size_t nacc = (size_t)c->kcap * (c->D + c->DP);
     // acc is all zero here: allocated zeroed, and np8_mh_g0 clears every row it reads (the only
     // rows np8_suffstats adds to are those of live slots)
+    // one rank on the wide path: run records instead of atomics (the ranks' transports sum acc otherwise)
+    const bool recs = c->wide && c->part && stats_mode == 0 && c->world == 1 && !c->comm &&
+                      c->param_update == NP8_PARAM_NIW_CONJUGATE;
+    if (recs) {
+        A.part = c->part;
+        A.part_slot = c->part_slot;
+    }
     if (stats_mode != 2) {
         if (c->wide)
             HIPC(c, np8_launch_suffstats_wide(A, c->stream));
@@ -1258,8 +1271,15 @@ int param_update(np8_ctx *c, int stats_mode = 0) {
     }
     if (stats_mode == 0 && c->comm)
         NCCLC(c, ncclAllReduce(c->acc, c->acc, nacc, ncclFloat64, ncclSum, c->comm, c->stream));
-    if (c->param_update == NP8_PARAM_NIW_CONJUGATE)
-        HIPC(c, np8_launch_niw_post(niw_args(c), c->kcap, c->stream));
+    if (c->param_update == NP8_PARAM_NIW_CONJUGATE) {
+        NiwArgs N = niw_args(c);
+        if (recs) {
+            N.part = c->part;
+            N.part_slot = c->part_slot;
+            N.n_rec = c->part_waves * kSuffRuns;
+        }
+        HIPC(c, np8_launch_niw_post(N, c->kcap, c->stream));
+    }
     else
         HIPC(c, np8_launch_mh_g0(A, c->stream));
     int r = refresh_wide(c, true);  // every live slot's parameters changed
@@ -1571,7 +1591,7 @@ int np8_create(np8_ctx **out, const np8_config *cfg) {
         (r = dalloc(c, &c->dense_of, (size_t)kc)) || (r = dalloc(c, &c->slot_iso, (size_t)kc)) ||
         (r = dalloc(c, &c->slot_logn1, (size_t)kc)) || (r = dalloc(c, &c->plen_s, (size_t)kc)) ||
         (r = dalloc(c, &c->plr2_s, (size_t)kc)) ||
-        (r = dalloc(c, &c->rec, (size_t)c->rec_bytes)) || (r = dalloc(c, &c->evalc, (size_t)8 * kEvalSlots)) ||
+        (r = dalloc(c, &c->rec, (size_t)c->rec_bytes)) || (r = dalloc(c, &c->evalc, (size_t)10 * kEvalSlots)) ||
         (c->param_update != NP8_PARAM_FROZEN && (r = dalloc(c, &c->acc, (size_t)kc * (D + DP)))) ||
         (kc <= kPruneMaxKcap && ((r = dalloc(c, &c->r2, 2 * (size_t)kc)) || (r = dalloc(c, &c->plen, (size_t)kc)) ||
                                  (r = dalloc(c, &c->lb, 2 * (size_t)kc)) ||
@@ -1683,11 +1703,15 @@ int np8_set_data(np8_ctx *c, const double *X, int64_t n, int32_t D, int64_t offs
     c->n_loc = n;
     c->offset = offset;
     c->n_glob = n_global;
+    c->part_waves = c->wide ? np8_suffstats_wide_waves(n) : 0;
     int r = 0;
     const size_t nx = c->wide ? ((size_t)n * D + 1) / 2 : (size_t)n * D;  // wide path: fp32 items
     if ((r = dalloc(c, &c->X, nx)) || (r = dalloc(c, &c->z, (size_t)n)) ||
         (r = dalloc(c, &c->z_best, (size_t)n)) || (r = dalloc(c, &c->wr2, (size_t)((n + 63) / 64))) ||
         (r = dalloc(c, &c->llpart, (size_t)((n + 63) / 64))) ||
+        (c->wide && c->param_update == NP8_PARAM_NIW_CONJUGATE &&
+         ((r = dalloc(c, &c->part, (size_t)(np8_suffstats_wide_waves(n) * kSuffRuns * np8_suffstats_wide_record(D)))) ||
+          (r = dalloc(c, &c->part_slot, (size_t)(np8_suffstats_wide_waves(n) * kSuffRuns))))) ||
         (r = dalloc(c, &c->queue, (size_t)(64 * ((n + 63) / 64) + 64))) ||
         (r = dalloc(c, &c->qcount, (size_t)((n + 63) / 64 + 1))) ||
         (r = dalloc(c, &c->qlist, (size_t)((n + 63) / 64 + 1))))
@@ -2360,7 +2384,7 @@ int np8_stats(np8_ctx *c, np8_stats_t *out) {
     out->tail_list_builds = (int64_t)h.list_builds;
     out->tail_steps = c->n_tail_cond;
     {
-        std::vector<unsigned long long> ev((size_t)8 * kEvalSlots);
+        std::vector<unsigned long long> ev((size_t)10 * kEvalSlots);
         HIPC(c, hipMemcpy(ev.data(), c->evalc, sizeof(unsigned long long) * ev.size(), hipMemcpyDeviceToHost));
         for (int k = 0; k < kEvalSlots; ++k) {
             out->n_quad += (int64_t)ev[2 * k];
@@ -2371,6 +2395,7 @@ int np8_stats(np8_ctx *c, np8_stats_t *out) {
             out->full_walk_waves += (int64_t)ev[4 * kEvalSlots + 2 * k + 1];
             out->many_group_waves += (int64_t)ev[6 * kEvalSlots + 2 * k];
             out->list_entries += (int64_t)ev[6 * kEvalSlots + 2 * k + 1];
+            out->pick_evals += (int64_t)ev[8 * kEvalSlots + 2 * k];
         }
     }
     return NP8_OK;

@@ -439,6 +439,10 @@ struct NiwArgs {
     const int32_t *init_map;
     const unsigned char *recs;  // np8_niw_aux_slots: the records np8_finalize read
     const int64_t *pend;
+    // np8_niw_post: the run records of np8_suffstats_wide (ParamArgs::part), n_rec headers; null: acc only
+    const double *part = nullptr;
+    const int32_t *part_slot = nullptr;
+    int64_t n_rec = 0;
 };
 
 // np8_step_tail (the end of a synchronous step in one launch): which parts run.
@@ -488,7 +492,14 @@ struct ParamArgs {
     uint64_t seed;
     uint32_t t;  // epoch offset: epoch = ctl->t_base + t
     double *r2;  // pruning radii: +inf for every slot whose parameters change
+    // wide path, one rank (np8_suffstats_wide): each wave stores the sums of its first kSuffRuns slot runs as run
+    // records (raw MFMA accumulator layout, no atomics; np8_niw_post reduces a slot's records in record order) and
+    // only further runs (an unsorted layout) go to acc by atomics.  Null: every run to acc (ranks sum acc).
+    double *part = nullptr;
+    int32_t *part_slot = nullptr;  // [waves * kSuffRuns]: the run's slot, -1 unused
 };
+
+constexpr int kSuffRuns = 4;  // run records per wave of np8_suffstats_wide
 
 struct SnapArgs {
     const double *L;
@@ -582,6 +593,8 @@ hipError_t np8_launch_loglik_reduce(const double *partial, int64_t nb, double *o
 hipError_t np8_launch_snapshot(const np8::SnapArgs &A, hipStream_t s);
 hipError_t np8_launch_suffstats(const np8::ParamArgs &A, hipStream_t s);
 hipError_t np8_launch_suffstats_wide(const np8::ParamArgs &P, hipStream_t s);
+int64_t np8_suffstats_wide_waves(int64_t n);   // waves of one np8_suffstats_wide launch
+int64_t np8_suffstats_wide_record(int D);      // doubles of one run record
 hipError_t np8_launch_mh_g0(const np8::ParamArgs &A, hipStream_t s);
 hipError_t np8_launch_advance_epoch(np8::Ctl *ctl, uint32_t n, hipStream_t s);
 hipError_t np8_launch_prune(const np8::PruneArgs &A, int kcap, hipStream_t s);

@@ -310,6 +310,7 @@ __device__ __forceinline__ void assign_item(const AssignArgs &A, const int64_t p
     // full walk.  Lists hold for every item of the row, whatever its wave (np8_prune: the radius covers
     // each item the last sweep left in the row).
     int32_t nq_lane = 0, niso_lane = 0, nlist_lane = 0;  // COUNT: quadratic forms this lane evaluated, list entries
+    int32_t npick_lane = 0;  // COUNT: walked rows within kSkip of the running maximum (pick_step's exp and division)
     int32_t pslot = zi;                  // slot of the picked row (no reload of the row at the end)
     // (a wave of many own rows -- a stale layout, a cold start -- walks the table once instead)
     int ngroups = 0;
@@ -343,6 +344,7 @@ __device__ __forceinline__ void assign_item(const AssignArgs &A, const int64_t p
                         const int j = lst[q];  // uniform across the group: scalar loads
                         const double *e = cand + (int64_t)j * CS;
                         const double lw = cand_ll<D>(e, x) + e[F + kFieldLogn];
+                        if constexpr (COUNT) npick_lane += (lw - st.T > -kSkip) ? 1 : 0;
                         ensure_u(st, lw, A.seed, ig, t);
                         pick_step(st, lw, j);
                         pslot = (st.pick == j) ? (int32_t)e[F + kFieldSlot] : pslot;
@@ -377,6 +379,7 @@ __device__ __forceinline__ void assign_item(const AssignArgs &A, const int64_t p
             const double *e = cand + (int64_t)j * CS;
             const double lw = cand_ll<D>(e, x) + e[F + kFieldLogn];
             if (e[F + kFieldSlot] != zslot) {
+                if constexpr (COUNT) npick_lane += (lw - st.T > -kSkip) ? 1 : 0;
                 ensure_u(st, lw, A.seed, ig, t);
                 pick_step(st, lw, j);
                 pslot = (st.pick == j) ? (int32_t)e[F + kFieldSlot] : pslot;
@@ -390,17 +393,19 @@ __device__ __forceinline__ void assign_item(const AssignArgs &A, const int64_t p
     if constexpr (COUNT) {  // the quadratic forms this wave executed (own row + walked rows)
         nq_lane += 1;
         niso_lane += (cand[(int64_t)jo * CS + F + kFieldIso] > 0.0) ? 1 : 0;
-        int64_t nq = 0, niso = 0;
+        int64_t nq = 0, niso = 0, npk = 0;
         const uint64_t lanes = __ballot(1);
         for (uint64_t act = lanes; act; act &= act - 1ull) {  // sums over the active lanes
             const int l = __ffsll((unsigned long long)act) - 1;
             nq += __builtin_amdgcn_readlane(nq_lane, l);
             niso += __builtin_amdgcn_readlane(niso_lane, l);
+            npk += __builtin_amdgcn_readlane(npick_lane, l);
         }
         if ((threadIdx.x & 63) == (__ffsll((unsigned long long)lanes) - 1)) {
             unsigned long long *ec = A.evalc + 2 * ((blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) % kEvalSlots);
             atomicAdd(ec, (unsigned long long)nq);
             atomicAdd(ec + 1, (unsigned long long)niso);
+            atomicAdd(ec + 8 * kEvalSlots, (unsigned long long)npk);
         }
     }
     double ny;
@@ -624,7 +629,7 @@ extern "C" int np8_exp_clocks(unsigned long long *out, int64_t n) {
 
 // ---- the data-parallel sweep's fast path -------------------------------------------------------------
 // lane l's double (l wave-uniform), as two readlanes: an SGPR pair for the rest of the wave
-__device__ __forceinline__ double readlane_d(double v, int l) {
+[[maybe_unused]] __device__ __forceinline__ double readlane_d(double v, int l) {
     const int64_t b = __double_as_longlong(v);
     const int lo = __builtin_amdgcn_readlane((int)(b & 0xFFFFFFFFll), l), hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
     return __longlong_as_double(((int64_t)hi << 32) | (uint32_t)lo);
@@ -1205,21 +1210,6 @@ __device__ int block_excl_scan(int v, int *sh /* >= 16 ints */, int *total) {
     *total = sh[16];
     __syncthreads();
     return r;
-}
-
-// Sum over the block in a fixed order (butterfly within each wave, then the waves in order); every thread
-// returns the same value.
-__device__ double block_sum_d(double v, double *sh /* >= 16 doubles */) {
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = v + __shfl_xor(v, o);
-    __syncthreads();
-    if (lane == 0) sh[wid] = v;
-    __syncthreads();
-    double t = sh[0];
-    for (int w = 1; w < nw; ++w) t = t + sh[w];
-    __syncthreads();
-    return t;
 }
 
 // Exact block sum of Fx values (every thread returns it).

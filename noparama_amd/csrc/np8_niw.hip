@@ -109,6 +109,210 @@ __device__ void write_sigma(int D, int LD, const double *B, const double *Rhs, b
     }
 }
 
+// Sigma = T^T T in 2 x 2 blocks per thread (half the LDS reads), each element one k-ordered chain (write_sigma's
+// second half, for a T already formed).
+__device__ void sigma_from_t(int D, int LD, const double *T, double *Sigma) {
+    const int H = (D + 1) / 2;
+    for (int e = threadIdx.x; e < 16 * H; e += blockDim.x) {
+      for (int bb = e & 15; bb < H; bb += 16) {
+        const int a = 2 * (e >> 4), b = 2 * bb;
+        const bool a1 = a + 1 < D, b1 = b + 1 < D;
+        double s00 = 0.0, s01 = 0.0, s10 = 0.0, s11 = 0.0;
+        #pragma unroll 4
+        for (int k = 0; k < D; ++k) {
+            const double ta0 = T[k * LD + a], ta1 = a1 ? T[k * LD + a + 1] : 0.0;
+            const double tb0 = T[k * LD + b], tb1 = b1 ? T[k * LD + b + 1] : 0.0;
+            s00 = fma(ta0, tb0, s00);
+            s01 = fma(ta0, tb1, s01);
+            s10 = fma(ta1, tb0, s10);
+            s11 = fma(ta1, tb1, s11);
+        }
+        Sigma[a * D + b] = s00;
+        if (b1) Sigma[a * D + b + 1] = s01;
+        if (a1) Sigma[(a + 1) * D + b] = s10;
+        if (a1 && b1) Sigma[(a + 1) * D + b + 1] = s11;
+      }
+    }
+}
+
+constexpr int kPanelN = 16;
+
+// Panel of 16 columns c0 .. c0 + 15 of the lower Cholesky factor of the symmetric matrix in L's lower triangle, on
+// one wave (lane = row r, its 16 panel entries in registers): per column j the pivot, the scaled column, and the
+// updates of the panel's later columns -- element (r, c) receives fma(-L_rj, L_cj, .) for j ascending, then the
+// division by its pivot.  *skip != 0 if a pivot is not positive.
+__device__ __forceinline__ void lower_panel_factor(double *L, int LD, int D, int c0, int *skip) {
+    const int lane = threadIdx.x & 63;
+    double w[kPanelN];
+#pragma unroll
+    for (int i = 0; i < kPanelN; ++i) w[i] = (lane < D && c0 + i < D) ? L[lane * LD + c0 + i] : 0.0;
+    int sk = 0;
+#pragma unroll
+    for (int j = 0; j < kPanelN; ++j) {
+        const int jj = c0 + j;
+        if (jj >= D) break;  // (a last panel narrower than 16: D not a multiple of 16)
+        const double v = __shfl(w[j], jj);  // the pivot L[jj][jj]
+        const bool ok = v > 0.0;
+        if (!ok) sk = 1;
+        const double dj = ok ? sqrt(v) : 1e-300;
+        if (lane == jj) w[j] = dj;
+        if (lane > jj) w[j] = w[j] / dj;  // column jj of L
+#pragma unroll
+        for (int i = j + 1; i < kPanelN; ++i) {
+            if (c0 + i >= D) break;
+            const double lcj = __shfl(w[j], c0 + i);  // L[c][jj], c = c0 + i
+            if (lane >= c0 + i) w[i] = fma(-w[j], lcj, w[i]);
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < kPanelN; ++i)
+        if (lane < D && c0 + i < D && lane >= c0 + i) L[lane * LD + c0 + i] = w[i];
+    if (lane == 0) *skip = sk;
+}
+
+// The panel's 16 updates to element (r, c), r >= c >= c0 + 16, in ascending column order; all threads.
+__device__ __forceinline__ void lower_panel_trailing(double *L, int LD, int D, int c0) {
+    const int cols = D - (c0 + kPanelN);
+    for (int e = threadIdx.x; e < cols * D; e += blockDim.x) {
+        const int c = c0 + kPanelN + e / D, r = e - (e / D) * D;
+        if (r < c) continue;
+        double acc = L[r * LD + c];
+#pragma unroll
+        for (int j = 0; j < kPanelN; ++j) acc = fma(-L[r * LD + c0 + j], L[c * LD + c0 + j], acc);  // (c0 + 16 <= c < D)
+        L[r * LD + c] = acc;
+    }
+}
+
+// Forward substitution panel (rows c0 .. c0 + 15) of X = G^{-1} X0 (G lower) on one wave (lane = column j, the 16
+// rows in registers): row k divided by G_kk (inv: the lower inverse, columns j <= k only and 1 / G_kk on the
+// diagonal), then the panel's later rows updated, fma(-G_rk, X_kj, .).
+__device__ __forceinline__ void forward_panel(double *X, const double *G, int LD, int D, int c0, bool inv) {
+    const int lane = threadIdx.x & 63;
+    double w[kPanelN];
+#pragma unroll
+    for (int i = 0; i < kPanelN; ++i) w[i] = (lane < D && c0 + i < D) ? X[(c0 + i) * LD + lane] : 0.0;
+#pragma unroll
+    for (int i = 0; i < kPanelN; ++i) {
+        const int k = c0 + i;
+        if (k >= D) break;
+        const double gkk = G[k * LD + k];
+        const bool col = lane < D && (!inv || lane <= k);
+        if (col) w[i] = (inv && lane == k) ? 1.0 / gkk : w[i] / gkk;
+#pragma unroll
+        for (int i2 = i + 1; i2 < kPanelN; ++i2)
+            if (col && c0 + i2 < D) w[i2] = fma(-G[(c0 + i2) * LD + k], w[i], w[i2]);
+    }
+#pragma unroll
+    for (int i = 0; i < kPanelN; ++i)
+        if (lane < D && c0 + i < D && (!inv || lane <= c0 + i)) X[(c0 + i) * LD + lane] = w[i];
+}
+
+// The panel's updates to rows r >= c0 + 16, fma(-G_rk, X_kj, .) for k = c0 .. c0 + 15 ascending (inv: k >= j only);
+// all threads.
+__device__ __forceinline__ void forward_trailing(double *X, const double *G, int LD, int D, int c0, bool inv) {
+    const int rows = D - (c0 + kPanelN);
+    for (int e = threadIdx.x; e < rows * D; e += blockDim.x) {
+        const int r = c0 + kPanelN + e / D, j = e - (e / D) * D;
+        if (inv && j > c0 + kPanelN - 1) continue;  // (columns right of the panel get nothing from it)
+        double acc = X[r * LD + j];
+#pragma unroll
+        for (int i = 0; i < kPanelN; ++i) {
+            const int k = c0 + i;
+            if (!inv || k >= j) acc = fma(-G[r * LD + k], X[k * LD + j], acc);
+        }
+        X[r * LD + j] = acc;
+    }
+}
+
+__device__ __forceinline__ bool init_ok_records(const NiwArgs &A) { return A.init_k <= 0 && A.part_slot != nullptr; }
+
+// Slot s's statistics from np8_suffstats_wide's run records (ParamArgs::part): the matching records are listed in
+// record order (each thread scans a contiguous range of headers, an exclusive scan places its matches), then every
+// thread sums its raw accumulator elements over the list in that order -- a fixed order, no atomics -- and adds
+// them to what the atomic fallback left in acc.  S lands in L's lower triangle (element (b, a) = S_ab, a <= b), s1
+// in s1.  Scratch: an int list of cap entries (Li's storage, unused until the factor exists).
+__device__ void reduce_run_records(const NiwArgs &A, int s, const double *acc, double *L, int LD, double *s1, int *list,
+                                   int cap) {
+    const int D = A.D, T = D / 16, NT = T * (T + 1) / 2, RS = NT * 4 * 64 + T * 16;
+    const int tid = threadIdx.x, nt = blockDim.x, lane = tid & 63, wv = tid >> 6, nw = nt >> 6;
+    __shared__ int woff[17];
+    const int64_t per = (A.n_rec + nt - 1) / nt, h0 = (int64_t)tid * per, h1 = min(A.n_rec, h0 + per);
+    int c = 0;
+    for (int64_t h = h0; h < h1; ++h) c += (A.part_slot[h] == s);
+    int inc = c;  // block exclusive scan of the counts (thread order = record order)
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int v = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += v;
+    }
+    if (lane == 63) woff[wv] = inc;
+    __syncthreads();
+    if (tid == 0) {
+        int t = 0;
+        for (int w = 0; w < nw; ++w) {
+            const int x = woff[w];
+            woff[w] = t;
+            t += x;
+        }
+        woff[16] = t;
+    }
+    __syncthreads();
+    int o = woff[wv] + inc - c;
+    const int nm = woff[16];
+    if (nm <= cap)
+        for (int64_t h = h0; h < h1; ++h)
+            if (A.part_slot[h] == s) list[o++] = (int)h;
+    __syncthreads();
+    // this thread's elements e = tid + k nt (RS <= kRecE nt for D <= 64), two records per round of loads
+    constexpr int kRecE = 12;
+    double v[kRecE];
+#pragma unroll
+    for (int k = 0; k < kRecE; ++k) v[k] = 0.0;
+    if (nm <= cap) {
+        for (int m = 0; m < nm; m += 2) {
+            const int64_t r0 = (int64_t)list[m] * RS, r1 = (m + 1 < nm) ? (int64_t)list[m + 1] * RS : -1;
+            double a0[kRecE], a1[kRecE];
+#pragma unroll
+            for (int k = 0; k < kRecE; ++k) {
+                const int e = tid + k * nt;
+                a0[k] = (e < RS) ? A.part[r0 + e] : 0.0;
+                a1[k] = (e < RS && r1 >= 0) ? A.part[r1 + e] : 0.0;
+            }
+#pragma unroll
+            for (int k = 0; k < kRecE; ++k) {
+                v[k] = v[k] + a0[k];
+                if (r1 >= 0) v[k] = v[k] + a1[k];
+            }
+        }
+    } else {  // (more records than the scratch holds: every header in order)
+        for (int64_t h = 0; h < A.n_rec; ++h)
+            if (A.part_slot[h] == s)
+#pragma unroll
+                for (int k = 0; k < kRecE; ++k)
+                    if (tid + k * nt < RS) v[k] = v[k] + A.part[h * RS + tid + k * nt];
+    }
+#pragma unroll
+    for (int k = 0; k < kRecE; ++k) {
+        const int e = tid + k * nt;
+        if (e >= RS) continue;
+        const double vk = v[k];
+        if (e < NT * 256) {  // raw accumulator element (tile q, row group r, lane ln) -> (a, b)
+            const int q = e >> 8, r = (e >> 6) & 3, ln = e & 63;
+            int ti = 0, qq = q;
+            while (qq >= T - ti) {
+                qq -= T - ti;
+                ++ti;
+            }
+            const int tj = ti + qq;
+            const int a = 16 * ti + (ln >> 4) + 4 * r, b = 16 * tj + (ln & 15);
+            if (a <= b) L[b * LD + a] = acc[D + pix(D, a, b)] + vk;
+        } else {
+            const int kk = e - NT * 256, dim = 16 * (kk >> 4) + (kk & 15);
+            s1[dim] = acc[dim] + vk;
+        }
+    }
+}
+
 // Scalars of slot s and of its candidate row (when it has one): c, isotropy, pruning radius unknown.
 __device__ __forceinline__ void write_row_scalars(const NiwArgs &A, int s, int row, double c, double iso) {
     A.slot_c[s] = c;
@@ -169,64 +373,30 @@ __global__ __launch_bounds__(kNiwThreads) void np8_niw_post(NiwArgs A) {
 #endif
     NIW_T(0)
     zero_block(L, 3 * D * LD);  // L, Li, B: upper triangles stay 0
+    const bool recs = A.part != nullptr && n > 0 && init_ok_records(A);
+    if (recs) {  // the statistics from np8_suffstats_wide's run records: S into L's lower triangle, s1
+        __syncthreads();
+        reduce_run_records(A, s, acc, L, LD, s1, reinterpret_cast<int *>(Li), (int)(D * LD * 2));
+        __syncthreads();
+    }
     for (int a = tid; a < D; a += blockDim.x) {
         anc[a] = (n > 0) ? A.slot_mu[(int64_t)s * D + a] : 0.0;
-        s1[a] = (n > 0) ? acc[a] : 0.0;
+        if (!recs) s1[a] = (n > 0) ? acc[a] : 0.0;
         xb[a] = (n > 0) ? anc[a] + s1[a] / nd : A.mu0[a];
         dm[a] = xb[a] - A.mu0[a];
         mun[a] = fma(k0, A.mu0[a], nd * xb[a]) / kn;
     }
     if (tid == 0) bad = 0;
     __syncthreads();
-    // Psin's lower triangle formed in LDS by all threads (the statistics and Psi0 come from HBM once),
-    // then the left-looking Cholesky in place: the diagonal of column j, then its rows below -- the
-    // operations of the oracle's loop, in its order
+    // Psin's lower triangle formed in LDS by all threads (the statistics and Psi0 come from HBM once); the
+    // Bartlett draws (they need nothing of Psin) in the same phase
     for (int e = tid; e < D * D; e += blockDim.x) {
         const int r = e / D, j = e - r * D;
         if (j > r) continue;
-        const double sc = (n > 0) ? S[pix(D, j, r)] - (s1[r] * s1[j]) / nd : 0.0;
+        const double Srj = recs ? L[r * LD + j] : S[pix(D, j, r)];
+        const double sc = (n > 0) ? Srj - (s1[r] * s1[j]) / nd : 0.0;
         L[r * LD + j] = fma(kf, dm[r] * dm[j], A.Psi0[r * D + j] + sc);
     }
-    __syncthreads();
-    NIW_T(1)
-    // right-looking: per column the pivot and the scaled column, then the trailing update.  Element (r, c)
-    // receives fma(-L_rk, L_ck, .) for k = 0, 1, ... in order, then the division by its pivot: the
-    // operations of the oracle's left-looking loop, in its order.  (The pivot is read by every thread
-    // and written back after the barrier.)
-    for (int j = 0; j < D; ++j) {
-        const double v = L[j * LD + j];  // fully updated (behind the barrier)
-        if (!(v > 0.0)) {                // block-uniform
-            if (tid == 0) bad = 1;
-            break;
-        }
-        const double dj = sqrt(v);
-        for (int r = j + 1 + tid; r < D; r += blockDim.x) L[r * LD + j] = L[r * LD + j] / dj;
-        __syncthreads();
-        if (tid == 0) L[j * LD + j] = dj;
-        for (int r = j + 1 + (tid >> 4); r < D; r += 16)  // 16 x 16 threads over (r, c), no index division
-            for (int c = j + 1 + (tid & 15); c <= r; c += 16) L[r * LD + c] = fma(-L[r * LD + j], L[c * LD + j], L[r * LD + c]);
-        __syncthreads();
-    }
-    __syncthreads();
-    NIW_T(2)
-    if (bad) {  // block-uniform: not numerically positive definite, the slot keeps its parameters
-        if (n > 0)
-            for (int w = tid; w < W; w += blockDim.x) A.acc[(int64_t)s * W + w] = 0.0;
-        return;
-    }
-    // Li = L^{-1} (lower), right-looking over rows: row k is final once its sums are divided by L_kk, then
-    // it updates every later row -- element (r, j) receives fma(-L_rk, Li_kj, .) for k = j, ..., r - 1 in
-    // order from 0, as the oracle's column loop does
-    for (int k = 0; k < D; ++k) {
-        const double lkk = L[k * LD + k];
-        for (int j = tid; j <= k; j += blockDim.x) Li[k * LD + j] = (j == k) ? 1.0 / lkk : Li[k * LD + j] / lkk;
-        __syncthreads();
-        for (int r = k + 1 + (tid >> 4); r < D; r += 16)  // rows r > k, columns j <= k
-            for (int j = tid & 15; j <= k; j += 16) Li[r * LD + j] = fma(-L[r * LD + k], Li[k * LD + j], Li[r * LD + j]);
-        __syncthreads();
-    }
-    NIW_SYNC()
-    NIW_T(3)
     for (int a = tid; a < D; a += blockDim.x) {  // Bartlett diagonal
         const double g = chi2_mt(A.seed, i, t, stream, kNiwGammaCalls * (uint32_t)a, nun - a);
         gv[a] = g;
@@ -240,12 +410,89 @@ __global__ __launch_bounds__(kNiwThreads) void np8_niw_post(NiwArgs A) {
     for (int j = tid; j < D; j += blockDim.x)
         z[j] = normal_at(A.seed, i, t, stream, kNiwNormalCall0, (uint32_t)(D * (D - 1) / 2 + j));
     __syncthreads();
-    NIW_T(4)
+    NIW_T(1)
+    const int lane = tid & 63, wv = tid >> 6;
+    (void)lane;
+    // Cholesky of Psin, blocked right-looking (panels of 16 columns: the panel factored by wave 0 in registers, the
+    // rows below updated by every thread): element (r, c) receives fma(-L_rk, L_ck, .) for k = 0, 1, ... in order,
+    // then the division by its pivot -- the operations of the oracle's left-looking loop, in its order, with two
+    // barriers per panel (round 3: two per column).  Wave 1 meanwhile: y = B^{-T} z / sqrt(kn) (B, z drawn above).
+    __shared__ int skip_s, fail_s;
+    for (int p = 0; p * kPanelN < D; ++p) {
+        const int c0 = p * kPanelN;
+        if (wv == 0) {
+            lower_panel_factor(L, LD, D, c0, &skip_s);
+        } else if (wv == 1 && p == 0) {
+            const int ln = tid & 63;
+            const double rskn = 1.0 / sqrt(kn);
+            double v = (ln < D) ? z[ln] * rskn : 0.0;
+            for (int k = D - 1; k >= 0; --k) {
+                const double yk = __shfl(v, k) / B[k * LD + k];
+                if (ln == k) y[k] = yk;
+                if (ln < k) v = fma(-B[k * LD + ln], yk, v);
+            }
+        }
+        __syncthreads();
+        if (skip_s) {  // block-uniform: not numerically positive definite
+            if (tid == 0) bad = 1;
+            break;
+        }
+        lower_panel_trailing(L, LD, D, c0);
+        __syncthreads();
+    }
+    (void)fail_s;
+    __syncthreads();
+    NIW_T(2)
+    if (bad) {  // block-uniform: not numerically positive definite, the slot keeps its parameters
+        if (n > 0)
+            for (int w = tid; w < W; w += blockDim.x) A.acc[(int64_t)s * W + w] = 0.0;
+        return;
+    }
+    // Li = L^{-1} and T = B^{-1} L^T (into F's storage; F is formed after Sigma) as blocked forward substitutions:
+    // row k final once divided by its diagonal, then it updates every later row -- element (r, j) receives
+    // fma(-L_rk, Li_kj, .) for k = j, ..., r - 1 (T: fma(-B_ak, T_kj, .) for k = 0, ..., a - 1) in order, as the
+    // oracle's loops do; the two panels side by side (waves 0 and 1), the trailing rows by every thread.  Wave 2: the
+    // new mean mun + L y.
+    double *T = F;
+    for (int e = tid; e < D * D; e += blockDim.x) {
+        const int a = e / D, j = e - a * D;
+        T[a * LD + j] = L[j * LD + a];
+    }
+    __syncthreads();
+    for (int p = 0; p * kPanelN < D; ++p) {
+        const int c0 = p * kPanelN;
+        if (wv == 0) {
+            forward_panel(Li, L, LD, D, c0, true);
+        } else if (wv == 1) {
+            forward_panel(T, B, LD, D, c0, false);
+        } else if (wv == 2 && p == 0) {
+            for (int a = tid - 128; a < D; a += 64) {
+                double v = 0.0;
+#pragma unroll 8
+                for (int k = 0; k <= a; ++k) v = fma(L[a * LD + k], y[k], v);
+                mun[a] = mun[a] + v;  // (mun no longer needed: the new mean in its place)
+            }
+        }
+        __syncthreads();
+        forward_trailing(Li, L, LD, D, c0, true);
+        forward_trailing(T, B, LD, D, c0, false);
+        __syncthreads();
+    }
+    __syncthreads();
+    NIW_T(3)
+    const int row = A.write_cand ? A.dense_of[s] : -1;
+    for (int a = tid; a < D; a += blockDim.x) {
+        A.slot_mu[(int64_t)s * D + a] = mun[a];
+        if (row >= 0) A.cand[(int64_t)row * cand_stride(D) + a] = mun[a];
+    }
     if (tid == 0) {
         LogAcc la;
         for (int a = 0; a < D; ++a) la.add(gv[a], a, D - 1);
         sh[0] = la.sumlog;
     }
+    sigma_from_t(D, LD, F, A.slot_sigma + (int64_t)s * D * D);  // Sigma = T^T T (T in F's storage)
+    __syncthreads();
+    NIW_T(4)
     for (int e = tid; e < D * D; e += blockDim.x) {  // F = Li^T B
         const int a = e / D, b = e - a * D;
         double v = 0.0;
@@ -255,32 +502,10 @@ __global__ __launch_bounds__(kNiwThreads) void np8_niw_post(NiwArgs A) {
     }
     __syncthreads();
     NIW_T(5)
-    const int row = A.write_cand ? A.dense_of[s] : -1;
     const double iso = write_pprime(D, LD, F, A.slot_P + (int64_t)s * (D * (D + 1) / 2),
                                     row >= 0 ? A.cand + (int64_t)row * cand_stride(D) + D : nullptr);
     NIW_T(6)
-    if (tid < 64) {  // y = B^{-T} z / sqrt(kn): one wave, lane a holds y_a's sum; column k leaves it as k falls
-        const double rskn = 1.0 / sqrt(kn);
-        double v = (tid < D) ? z[tid] * rskn : 0.0;
-        for (int k = D - 1; k >= 0; --k) {
-            const double yk = __shfl(v, k) / B[k * LD + k];
-            if (tid == k) y[k] = yk;
-            if (tid < k) v = fma(-B[k * LD + tid], yk, v);
-        }
-    }
-    __syncthreads();
-    for (int a = tid; a < D; a += blockDim.x) {
-        double v = 0.0;
-        #pragma unroll 8
-        for (int k = 0; k <= a; ++k) v = fma(L[a * LD + k], y[k], v);
-        const double m = mun[a] + v;
-        A.slot_mu[(int64_t)s * D + a] = m;
-        if (row >= 0) A.cand[(int64_t)row * cand_stride(D) + a] = m;
-    }
-    NIW_SYNC()
     NIW_T(7)
-    write_sigma(D, LD, B, L, true, F, A.slot_sigma + (int64_t)s * D * D);  // T = B^{-1} L^T
-    NIW_SYNC()
     NIW_T(8)
 #ifdef NP8_EXP_NIW_TIMING
     if (tid == 0 && s < 2 && (t % 16) == 0)

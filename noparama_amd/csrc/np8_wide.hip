@@ -179,62 +179,136 @@ constexpr int kLamRounds = 5;  // eigenvalue-bound rounds of three concurrent Ch
 #endif
 constexpr double kLamRelWidth = NP8_LAM_REL_WIDTH;  // ... or fewer, once the bracket [lo, hi] is within 5% of hi
 
-// One block per slot (grid kcap): the slots flagged in wdirty get their factor and fp32 mean.
-// LDS: R [D][D] | three [D][D] workspaces.
+// One block of four waves per slot (grid kcap): the slots flagged in wdirty get their factor, its eigenvalue bound
+// and their fp32 mean.  The factor and the eigenvalue bound's Cholesky tests run blocked, right-looking, 16 columns
+// per panel: one wave factors a panel with its 16 rows in registers (lane = column, pivots and row entries by
+// readlane), then all 256 threads apply the panel's 16 updates to the rows below, each element's fma chain in
+// ascending column order -- the operations of the unblocked form (and of the oracle) in their order, with two
+// workgroup barriers per panel instead of two per column.  Waves 0..3 factor panels of four matrices at once: P
+// (wave 0) and P - beta_q I for the three betas of an eigenvalue round (waves 1-3).
+// LDS: four [D][D + 1] double matrices (133 KB at D = 64): the factor's work matrix (R in place), three tests.
+constexpr int kPanel = 16;
+
+// Panel p of matrix M (rows c0 .. c0 + 15, columns c0 .. D - 1) on one wave, lane = column.  Factor form (test =
+// false): row jj of R = row jj / sqrt(pivot); a non-positive pivot is replaced by 1e-300 and its column skips every
+// update (np8_wide_rows' error path), bit q of *skip.  Test form: the row is kept unscaled, rk[j] = 1 / sqrt(pivot)
+// scales both factors of each update; a non-positive pivot ends the test (*fail).
+__device__ __forceinline__ void panel_factor(double *M, int LD, int D, int c0, bool test, double *rk, int *skip,
+                                             int *fail) {
+    const int lane = threadIdx.x & 63;
+    double w[kPanel];
+#pragma unroll
+    for (int i = 0; i < kPanel; ++i) w[i] = (lane < D) ? M[(c0 + i) * LD + lane] : 0.0;
+    int sk = 0, fl = 0;
+#pragma unroll
+    for (int j = 0; j < kPanel; ++j) {
+        const int jj = c0 + j;
+        const double v = __shfl(w[j], jj);  // the pivot (row jj, column jj: lane jj)
+        if (test) {
+            if (!(v > 0.0) || fl) {
+                fl = 1;
+                continue;
+            }
+            const double r = 1.0 / sqrt(v);
+            if (lane == 0) rk[j] = r;
+            const double rowj = w[j] * r;  // C[jj][l] r
+#pragma unroll
+            for (int i = j + 1; i < kPanel; ++i) {
+                const double ci = __shfl(w[j], c0 + i) * r;  // C[jj][ii] r
+                if (lane >= c0 + i) w[i] = fma(-ci, rowj, w[i]);
+            }
+        } else {
+            const bool ok = v > 0.0;
+            const double dj = ok ? sqrt(v) : 1e-300;
+            if (!ok) sk |= 1 << j;
+            if (lane == jj) w[j] = dj;
+            if (lane > jj) w[j] = ok ? w[j] / dj : 0.0;  // row jj of R (zero after a failed pivot)
+            if (ok) {
+#pragma unroll
+                for (int i = j + 1; i < kPanel; ++i) {
+                    const double rji = __shfl(w[j], c0 + i);  // R[jj][ii]
+                    if (lane >= c0 + i) w[i] = fma(-rji, w[j], w[i]);
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < kPanel; ++i)
+        if (lane < D && lane >= c0 + i) M[(c0 + i) * LD + lane] = w[i];
+    if (lane == 0) {
+        *skip = sk;
+        *fail = fl;
+    }
+}
+
+// The panel's 16 updates to element (ii, l), ii >= c0 + 16, l >= ii, in ascending column order; all threads.
+__device__ __forceinline__ void panel_trailing(double *M, int LD, int D, int c0, bool test, const double *rk, int skip) {
+    const int rows = D - (c0 + kPanel);
+    for (int e = threadIdx.x; e < rows * D; e += blockDim.x) {
+        const int ii = c0 + kPanel + e / D, l = e - (e / D) * D;
+        if (l < ii) continue;
+        double acc = M[ii * LD + l];
+#pragma unroll
+        for (int j = 0; j < kPanel; ++j) {
+            const int k = c0 + j;
+            if (test)
+                acc = fma(-(M[k * LD + ii] * rk[j]), M[k * LD + l] * rk[j], acc);
+            else if (!((skip >> j) & 1))
+                acc = fma(-M[k * LD + ii], M[k * LD + l], acc);
+        }
+        M[ii * LD + l] = acc;
+    }
+}
+
+#ifdef NP8_EXP_WIDE_TIMING  // experiment: phase cycle counts of np8_wide_rows, blocks 0 and 1, printed
+#define WR_T(k) \
+    if (threadIdx.x == 0 && (k) < 16) tph[k] = (long long)__builtin_amdgcn_s_memtime();
+#else
+#define WR_T(k)
+#endif
 __global__ __launch_bounds__(256) void np8_wide_rows(WideArgs W) {
+#ifdef NP8_EXP_WIDE_TIMING
+    long long tph[16];
+    for (int k = 0; k < 16; ++k) tph[k] = 0;
+    int nrd = 0;
+#endif
+    WR_T(0)
     const int s = blockIdx.x;
-    if (!W.dirty[s] || W.cnt[s] <= 0) return;
-    const int D = W.D, DP = D * (D + 1) / 2, tid = threadIdx.x;
-    extern __shared__ __attribute__((aligned(16))) double R[];
-    double *Wk = R + D * D;
-    const double *Pp = W.slot_P + (int64_t)s * DP;
+    if (!W.dirty[s] || W.cnt[s] <= 0) return;  // block-uniform
+    const int D = W.D, LD = D + 1, tid = threadIdx.x, wv = tid >> 6;
+    extern __shared__ __attribute__((aligned(16))) double smr[];
+    double *Wk = smr, *C0 = Wk + D * LD;  // C0 + q * D * LD: test matrix q; R = the upper triangle of Wk at the end
+    const double *Pp = W.slot_P + (int64_t)s * (D * (D + 1) / 2);
     auto pget = [&](int a, int b) {  // sym(P) upper element, a <= b (the packed P' doubles off-diagonals)
         const double v = Pp[a * D - (a * (a - 1)) / 2 + (b - a)];
         return (a == b) ? v : 0.5 * v;
     };
+    __shared__ double dmin;
+    __shared__ double rk_s[4][kPanel];
+    __shared__ int skip_s[4], fail_s[4];
+    if (tid == 0) dmin = 1e300;
+    __syncthreads();
     for (int k = tid; k < D * D; k += blockDim.x) {
         const int a = k / D, b = k - a * D;
-        R[k] = 0.0;
-        Wk[k] = (b >= a) ? pget(a, b) : 0.0;
+        const double v = (b >= a) ? pget(a, b) : 0.0;
+        Wk[a * LD + b] = v;
+        if (a == b && W.lam_lo) atomicMin(reinterpret_cast<unsigned long long *>(&dmin), (unsigned long long)__double_as_longlong(v));
     }
     __syncthreads();
-    // R = chol_upper(P), right-looking: per column the pivot and the scaled row, then the trailing update.
-    // Element (i, l) receives its updates k = 0, 1, ... in order, each fma(-R_ki, R_kl, .), then the
-    // division by its pivot: the operations of the oracle's row-by-row form (np8o wide factor), in its order.
-    for (int jj = 0; jj < D; ++jj) {
-        const double v = Wk[jj * D + jj];  // fully updated (behind the barrier)
-        const bool ok = v > 0.0;           // block-uniform
-        const double dj = ok ? sqrt(v) : 1e-300;
-        if (tid == 0) {
-            R[jj * D + jj] = dj;
-            if (!ok) atomicOr(&W.ctl->err, kErrSigma);
-        }
-        if (ok)
-            for (int i = jj + 1 + tid; i < D; i += blockDim.x) R[jj * D + i] = Wk[jj * D + i] / dj;
-        __syncthreads();
-        if (ok)  // 16 x 16 threads over (i, l), l >= i (no index division)
-            for (int i = jj + 1 + (tid >> 4); i < D; i += 16)
-                for (int l = i + (((tid & 15) - (i - jj - 1)) & 15); l < D; l += 16)
-                    Wk[i * D + l] = fma(-R[jj * D + i], R[jj * D + l], Wk[i * D + l]);
-        __syncthreads();
-    }
-    // candidate pruning: lam_lo <= the smallest eigenvalue of P = R^T R, by Cholesky tests of P - beta I
-    // (positive definite <=> lambda_min(P) > beta) on [0, min_i P_ii]: each round tests three betas at
-    // once (quarter points), one barrier per column
-    if (W.lam_lo) {
-        __shared__ double dmin;
-        if (tid == 0) dmin = 1e300;
-        __syncthreads();
-        for (int i = tid; i < D; i += blockDim.x)
-            atomicMin(reinterpret_cast<unsigned long long *>(&dmin), (unsigned long long)__double_as_longlong(pget(i, i)));
-        __syncthreads();
-        double lo = 0.0, hi = dmin;
-        // warm start: the slot's bound from its last factorisation (the parameters of a cluster move a
-        // little per sweep) bracketed first; a stale one (a reused slot) only costs that round
-        const double prev = W.lam_lo[s] / 0.99;
-        const bool warm = prev > 0.0 && prev < hi;
-        for (int rd = 0; rd < kLamRounds && hi > lo; ++rd) {
-            double beta[3];
+    // candidate pruning: lam_lo <= the smallest eigenvalue of P, by Cholesky tests of P - beta I (positive definite
+    // <=> lambda_min(P) > beta) on [0, min_i P_ii]: each round tests three betas at once (quarter points; the first
+    // round brackets the slot's last bound); the first round runs beside the factor
+    const bool lam = W.lam_lo != nullptr;
+    double lo = 0.0, hi = lam ? dmin : 0.0;
+    const double prev = lam ? W.lam_lo[s] / 0.99 : 0.0;
+    const bool warm = prev > 0.0 && prev < hi;
+    bool factor = true;  // the first pass also factors P
+    int err = 0;
+    WR_T(1)
+    for (int rd = 0; rd < (lam ? kLamRounds : 1); ++rd) {  // block-uniform
+        const bool tests = lam && hi > lo;
+        double beta[3] = {0.0, 0.0, 0.0};
+        if (tests) {
             if (rd == 0 && warm) {
                 beta[0] = 0.93 * prev;
                 beta[1] = 0.98 * prev;
@@ -243,45 +317,55 @@ __global__ __launch_bounds__(256) void np8_wide_rows(WideArgs W) {
 #pragma unroll
                 for (int q = 0; q < 3; ++q) beta[q] = lo + (hi - lo) * (0.25 * (q + 1));
             }
-            for (int k = tid; k < D * D; k += blockDim.x) {
-                const int a = k / D, b = k - a * D;
-                if (b < a) continue;
-                const double v = pget(a, b);
-#pragma unroll
-                for (int q = 0; q < 3; ++q) Wk[q * D * D + k] = (a == b) ? v - beta[q] : v;
+            for (int k = tid; k < 3 * D * D; k += blockDim.x) {
+                const int q = k / (D * D), kk = k - q * D * D, a = kk / D, b = kk - a * D;
+                if (b >= a) C0[q * D * LD + a * LD + b] = (a == b) ? pget(a, a) - beta[q] : pget(a, b);
+            }
+            if (tid < 4) fail_s[tid] = 0;
+            __syncthreads();
+        }
+        if (!factor && !tests) break;
+        for (int p = 0; p < D / kPanel; ++p) {
+            const int c0 = p * kPanel;
+            // panel steps: wave 0 the factor (first pass), wave q + 1 test q (a failed test stops)
+            if (wv == 0 && factor) {
+                panel_factor(Wk, LD, D, c0, false, nullptr, &skip_s[0], &fail_s[3]);
+            } else if (wv > 0 && tests && !fail_s[wv - 1]) {
+                int dummy;
+                panel_factor(C0 + (wv - 1) * D * LD, LD, D, c0, true, rk_s[wv], &dummy, &fail_s[wv - 1]);
             }
             __syncthreads();
-            int pd = 7;  // bit q: P - beta_q I still positive definite (block-uniform)
-            for (int jj = 0; jj < D && pd; ++jj) {
-                double r[3];
-#pragma unroll
-                for (int q = 0; q < 3; ++q) {
-                    const double v = Wk[q * D * D + jj * D + jj];
-                    if (!(v > 0.0)) pd &= ~(1 << q);
-                    r[q] = (v > 0.0) ? 1.0 / sqrt(v) : 0.0;
-                }
-                for (int i = jj + 1 + (tid >> 4); i < D; i += 16)
-                    for (int l = i + (((tid & 15) - (i - jj - 1)) & 15); l < D; l += 16) {
-#pragma unroll
-                        for (int q = 0; q < 3; ++q) {
-                            if (!(pd >> q & 1)) continue;
-                            double *C = Wk + q * D * D;
-                            C[i * D + l] = fma(-(C[jj * D + i] * r[q]), C[jj * D + l] * r[q], C[i * D + l]);
-                        }
-                    }
-                __syncthreads();
+            if (factor) {
+                err |= skip_s[0];
+                panel_trailing(Wk, LD, D, c0, false, nullptr, skip_s[0]);
             }
-            // pd is monotone in beta: the largest positive definite beta is the new lower end
-            const int top = (pd & 4) ? 3 : (pd & 2) ? 2 : (pd & 1) ? 1 : 0;
-            if (top > 0) lo = beta[top - 1];
-            if (top < 3) hi = beta[top];
-            if (hi - lo <= kLamRelWidth * hi) break;  // block-uniform
+            if (tests)
+                for (int q = 0; q < 3; ++q)
+                    if (!fail_s[q]) panel_trailing(C0 + q * D * LD, LD, D, c0, true, rk_s[q + 1], 0);
+            __syncthreads();
         }
-        // 1% for the fp32 factor and the fp32 contraction, and the Cholesky's own rounding
-        if (tid == 0) W.lam_lo[s] = 0.99 * lo;
+        if (factor && err && tid == 0) atomicOr(&W.ctl->err, kErrSigma);
+        factor = false;
+#ifdef NP8_EXP_WIDE_TIMING
+        ++nrd;
+        WR_T(1 + nrd)
+#endif
+        if (!tests) break;
+        // positive definiteness is monotone in beta: the largest positive definite beta is the new lower end
+        const int pd = (!fail_s[0]) | ((!fail_s[1]) << 1) | ((!fail_s[2]) << 2);
+        const int top = (pd & 4) ? 3 : (pd & 2) ? 2 : (pd & 1) ? 1 : 0;
+        if (top > 0) lo = beta[top - 1];
+        if (top < 3) hi = beta[top];
+        __syncthreads();  // (fail_s read by every thread before the next round resets it)
+        if (hi - lo <= kLamRelWidth * hi) break;  // block-uniform
     }
+    // 1% for the fp32 factor and the fp32 contraction, and the Cholesky's own rounding
+    if (lam && tid == 0) W.lam_lo[s] = 0.99 * lo;
     float *An = W.wA + (int64_t)s * D * D;
-    for (int k = threadIdx.x; k < D * D; k += blockDim.x) An[k] = (float)R[k];
+    for (int k = threadIdx.x; k < D * D; k += blockDim.x) {
+        const int a = k / D, b = k - a * D;
+        An[k] = (b >= a) ? (float)Wk[a * LD + b] : 0.0f;
+    }
     // fragment chunks (mt, s4), s4 >= mt, in compact order; in chunk c = chunk(mt, s4) lane l's float4
     // element e (k-step ks = 4 s4 + e) holds A[16 mt + (l & 15)][4 ks + (l >> 4)]; then muf transposed:
     // [g][s] = muf[4 s + g]
@@ -293,13 +377,21 @@ __global__ __launch_bounds__(256) void np8_wide_rows(WideArgs W) {
         while (c >= (mt + 1) * S4 - (mt * (mt + 1)) / 2) ++mt;  // chunk -> (mt, s4)
         const int s4 = mt + (c - (mt * S4 - (mt * (mt - 1)) / 2));
         const int ks = 4 * s4 + e;
-        Af[k] = (float)R[(16 * mt + (l & 15)) * D + 4 * ks + (l >> 4)];
+        const int ra = 16 * mt + (l & 15), rb = 4 * ks + (l >> 4);
+        Af[k] = (rb >= ra) ? (float)Wk[ra * LD + rb] : 0.0f;
     }
     for (int k = threadIdx.x; k < D; k += blockDim.x) {
         const int g = k / S, st = k - g * S;
         Af[NCH * 256 + k] = (float)W.slot_mu[(int64_t)s * D + 4 * st + g];
     }
     for (int a = threadIdx.x; a < D; a += blockDim.x) W.wmu[(int64_t)s * D + a] = (float)W.slot_mu[(int64_t)s * D + a];
+#ifdef NP8_EXP_WIDE_TIMING
+    WR_T(15)
+    if (tid == 0 && s < 3)
+        printf("wide_rows s=%d rounds %d load %lld r1 %lld r2 %lld r3 %lld r4 %lld r5 %lld out %lld total %lld\n", s, nrd,
+               tph[1] - tph[0], tph[2] - tph[1], nrd > 1 ? tph[3] - tph[2] : 0, nrd > 2 ? tph[4] - tph[3] : 0,
+               nrd > 3 ? tph[5] - tph[4] : 0, nrd > 4 ? tph[6] - tph[5] : 0, tph[15] - tph[1 + nrd], tph[15] - tph[0]);
+#endif
 }
 
 // Candidate pruning (DESIGN.md "Wide path"): distances between the fp32 means of the dense rows, in fp64,
@@ -819,8 +911,16 @@ __global__ __launch_bounds__(256) void np8_suffstats_wide(ParamArgs P) {
     const float *__restrict__ X = reinterpret_cast<const float *>(sorted ? (cur ? P.Xs[1] : P.Xs[0]) : P.X);
     const int32_t *__restrict__ z = sorted ? (cur ? P.zs[1] : P.zs[0]) : P.z;
     const int64_t n = P.n_loc;
-    const int64_t base = ((int64_t)blockIdx.x * 4 + wv) * (64 * kSuffChunks);
-    if (base >= n) return;  // wave-uniform; no block barrier below
+    const int64_t wid = (int64_t)blockIdx.x * 4 + wv;
+    const int64_t base = wid * (64 * kSuffChunks);
+    int nrun = 0;  // run records this wave wrote
+    auto close_records = [&]() {  // the unused run records of this wave
+        if (P.part && lane < kSuffRuns && lane >= nrun) P.part_slot[wid * kSuffRuns + lane] = -1;
+    };
+    if (base >= n) {  // wave-uniform; no block barrier below
+        close_records();
+        return;
+    }
     float(*tl)[65] = tile[wv];
     f64x4 acc[NT];
     double s1[T];
@@ -833,6 +933,24 @@ __global__ __launch_bounds__(256) void np8_suffstats_wide(ParamArgs P) {
         for (int t = 0; t < T; ++t) s1[t] = 0.0;
     };
     auto commit = [&]() {
+        if (P.part && nrun < kSuffRuns) {  // a run record: the raw accumulators, then s1 (dims 16 t + col)
+            constexpr int RS = NT * 4 * 64 + T * 16;
+            double *rec = P.part + (wid * kSuffRuns + nrun) * RS;
+#pragma unroll
+            for (int q = 0; q < NT; ++q)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) rec[(q * 4 + r) * 64 + lane] = acc[q][r];
+#pragma unroll
+            for (int t = 0; t < T; ++t) {
+                double v = s1[t];
+                v += __shfl_xor(v, 16);
+                v += __shfl_xor(v, 32);
+                if (g == 0) rec[NT * 4 * 64 + t * 16 + col] = v;
+            }
+            if (lane == 0) P.part_slot[wid * kSuffRuns + nrun] = cs;
+            ++nrun;
+            return;
+        }
         double *dst = P.acc + (int64_t)cs * W;
         int q = 0;
 #pragma unroll
@@ -857,15 +975,28 @@ __global__ __launch_bounds__(256) void np8_suffstats_wide(ParamArgs P) {
         }
     };
     reset();
+    // software-pipelined: chunk c + 1's item rows and labels are in flight (registers) while chunk c (LDS) is
+    // contracted -- one round of 64 loads per chunk instead of eight dependent rounds
+    float xn[D];
+    int32_t zn;
+    auto fetch = [&](int c) {
+        const int64_t p = base + 64 * c + lane;
+        const bool valid = p < n && base + 64 * c < n;
+        zn = valid ? z[p] : -1;
+#pragma unroll
+        for (int a = 0; a < D; ++a) xn[a] = valid ? X[(int64_t)a * n + p] : 0.0f;
+    };
+    fetch(0);
     for (int c = 0; c < kSuffChunks; ++c) {
         const int64_t p0 = base + 64 * c;
         if (p0 >= n) break;
         const int64_t p = p0 + lane;
         const bool valid = p < n;
-        const int32_t zl = valid ? z[p] : -1;
-#pragma unroll 8
-        for (int a = 0; a < D; ++a) tl[a][lane] = valid ? X[(int64_t)a * n + p] : 0.0f;
+        const int32_t zl = zn;
+#pragma unroll
+        for (int a = 0; a < D; ++a) tl[a][lane] = xn[a];
         __builtin_amdgcn_wave_barrier();
+        if (c + 1 < kSuffChunks) fetch(c + 1);
         uint64_t pend = __ballot(valid);
         while (pend) {
             const int32_t sl = __shfl(zl, __ffsll((unsigned long long)pend) - 1);
@@ -897,6 +1028,14 @@ __global__ __launch_bounds__(256) void np8_suffstats_wide(ParamArgs P) {
         __builtin_amdgcn_wave_barrier();
     }
     if (cs >= 0) commit();
+    close_records();
+}
+
+// Waves of an np8_suffstats_wide launch over n items, and the doubles of one run record at D (ParamArgs::part).
+int64_t np8_suffstats_wide_waves(int64_t n) { return 4 * ((n + 4 * 64 * kSuffChunks - 1) / (4 * 64 * kSuffChunks)); }
+int64_t np8_suffstats_wide_record(int D) {
+    const int T = D / 16;
+    return (int64_t)(T * (T + 1) / 2) * 4 * 64 + T * 16;
 }
 
 hipError_t np8_launch_suffstats_wide(const ParamArgs &P, hipStream_t s) {
@@ -985,11 +1124,11 @@ hipError_t np8_launch_wide_dist(const WideArgs &W, hipStream_t s) {
 }
 
 hipError_t np8_launch_wide_refresh(const WideArgs &W, hipStream_t s) {
-    const size_t lds = 4 * sizeof(double) * W.D * W.D;  // 128 KB at D = 64
+    const size_t lds = 4 * sizeof(double) * W.D * (W.D + 1);  // 133 KB at D = 64
     static bool allowed = false;  // (set before the first launch, which is not inside a graph capture)
     if (!allowed) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&np8_wide_rows),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)(4 * sizeof(double) * 64 * 64));
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)(4 * sizeof(double) * 64 * 65));
         if (e != hipSuccess) return e;
         allowed = true;
     }

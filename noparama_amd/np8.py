@@ -113,6 +113,7 @@ class Stats(C.Structure):
         ("folded_checks", C.c_int64),
         ("tail_list_builds", C.c_int64),
         ("tail_steps", C.c_int64),
+        ("pick_evals", C.c_int64),
     ]
 
 

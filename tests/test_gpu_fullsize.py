@@ -6,6 +6,10 @@ oracle's synchronous sweep (OpenMP, 16 threads on the GPU box) from the same sta
   * C3: N = 1e6, D = 8, K = 64, the warm state, 5 eager sweeps then one 20-sweep graph replay (the sweep
     graph the bench times, with timing events on as in the bench), sorted layout, candidate pruning and the
     radius gathering; labels, counts, K, the max-likelihood snapshot bit-exact, total log-likelihood 1e-11.
+  * C3 from the reference's own initialisation (init_random(20), np_mcmc.cpp:49-92): 50 eager sweeps (the cold
+    start's new-cluster requests and partial acceptance, then the mixed regime: per-own-row list walks, waves of
+    several own rows, stale layouts re-sorted between replays) and one 20-sweep graph replay; labels, counts, K
+    and the snapshot bit-exact.
   * C5: N = 1e6, D = 64, K = 256, the NIW prior, fp32 items and the fp32 MFMA contraction: 2 frozen sweeps
     bit-exact (parameters too); 1 `niw_conjugate` sweep: labels and counts bit-exact, parameters within
     DESIGN.md 7's 1e-10 (statistics summed in another order).
@@ -71,6 +75,32 @@ def test_c3_full_size_warm_graph_bit_exact():
         np.testing.assert_allclose(g.total_loglik(), o.total_loglik(), rtol=1e-11)
         np.testing.assert_allclose(g.stats()["best_loglik"], o.best_loglik(), rtol=1e-11)
         print(f"C3 N=1e6 25 sweeps: K={st['K']} bit-exact")
+    finally:
+        O.set_threads(1)
+        g.close()
+
+
+@pytest.mark.timeout(900)
+def test_c3_full_size_mixed_regime_bit_exact():
+    args, (X, z, mu, sig, opts) = bench_workload("C3")
+    g = NealAlgorithm8(8, seed=args.seed, device=0, **opts)
+    o = O.Chain(8, seed=args.seed, kcap=g.kcap, chunk=0)
+    O.set_threads(THREADS)
+    try:
+        for c in (g, o):
+            c.set_data(X)
+            c.init_random(20)
+        for k in range(10):  # 50 eager sweeps (five at a time: below the 20-sweep graph)
+            g.sweep(5)
+            o.sweep(5)
+            st = same(g, o)
+        same(g, o, which=1)
+        g.sweep(20)  # one captured 20-sweep graph replay
+        o.sweep(20)
+        st = same(g, o)
+        same(g, o, which=1)
+        np.testing.assert_allclose(g.stats()["best_loglik"], o.best_loglik(), rtol=1e-11)
+        print(f"C3 N=1e6 init_random(20), 70 sweeps: K={st['K']} bit-exact")
     finally:
         O.set_threads(1)
         g.close()

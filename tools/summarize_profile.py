@@ -32,7 +32,11 @@ for (k, c), v in agg.items():
 out = {"source": src, "counters": per_kernel}
 # the assign step: np8_assign_fast + np8_assign_queue (C3, launched once each per step), np8_assign_wide (C5) or
 # np8_assign; counting instances (template flag true) run outside the timed sweeps and are left out
-assign = [k for k in per_kernel if "np8_assign" in k and ("true>" not in k or "assign_wide" in k) and "matrix" not in k]
+def counting(k):  # the executed-work counting instances (COUNT = true) run outside the timed sweeps
+    return "assign_wide" not in k and ((("true>" in k) and ("false, true>" not in k)) or (", true, false>" in k))
+
+
+assign = [k for k in per_kernel if "np8_assign" in k and not counting(k) and "matrix" not in k]
 assign.sort(key=lambda k: -per_kernel[k].get("SQ_WAVES", per_kernel[k].get("FETCH_SIZE", {})).get("launches", 0))
 if assign:
     a = per_kernel[assign[0]]
