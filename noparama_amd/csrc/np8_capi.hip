@@ -782,6 +782,12 @@ NiwArgs niw_args(np8_ctx *c) {
     A.slot_iso = c->slot_iso;
     A.cand = c->cand;
     A.r2 = c->r2;
+    if (c->wide) {  // the draw's own factor R becomes the slot's contraction rows (no np8_wide_rows factor)
+        A.wA = c->wA;
+        A.wfrag = c->wfrag;
+        A.wmu = c->wmu;
+        A.lam_lo = c->lam_lo;
+    }
     return A;
 }
 
@@ -1282,7 +1288,9 @@ int param_update(np8_ctx *c, int stats_mode = 0) {
     }
     else
         HIPC(c, np8_launch_mh_g0(A, c->stream));
-    int r = refresh_wide(c, true);  // every live slot's parameters changed
+    // every live slot's parameters changed; np8_niw_post wrote the contraction rows of the slots it drew (a slot it
+    // could not draw keeps its parameters and rows), np8_mh_g0 leaves them to np8_wide_rows
+    int r = refresh_wide(c, c->param_update != NP8_PARAM_NIW_CONJUGATE);
     if (r) return r;
     timer_end(c, t);
     return NP8_OK;
@@ -1780,7 +1788,7 @@ static int set_state_common(np8_ctx *c, const std::vector<SlotHost> &slots, cons
     if (r) return r;
     r = rebuild(c);
     if (r) return r;
-    r = refresh_wide(c, true);
+    r = refresh_wide(c, niw_init_map == nullptr);  // (the NIW G0 draws wrote their own contraction rows)
     if (r) return r;
     HIPC(c, hipStreamSynchronize(c->stream));
     c->have_state = true;

@@ -537,4 +537,31 @@ NP8_HD void pick_step(PickState &st, double lw, int32_t j) {
     st.S = S;
 }
 
+// The wide path's contraction rows of one slot from its fp64 factor R (upper, R^T R = P; element (a, b) at
+// R[a * LDR + b], any storage) and its fp64 mean: A = fp32(R) natural [D][D] (An) and in MFMA-fragment order
+// (Af: chunks (mt, s4), s4 >= mt, compact; in chunk c lane l's float4 element e (k-step ks = 4 s4 + e) holds
+// A[16 mt + (l & 15)][4 ks + (l >> 4)]; then muf transposed, [g][s] = muf[4 s + g]) and muf = fp32(mu) (wmu).
+// All threads of the block (np8_wide_rows, np8_niw_post).
+__device__ inline void wide_write_rows(int D, const double *R, int LDR, const double *mu, float *An, float *Af, float *wmu) {
+    for (int k = threadIdx.x; k < D * D; k += blockDim.x) {
+        const int a = k / D, b = k - a * D;
+        An[k] = (b >= a) ? (float)R[a * LDR + b] : 0.0f;
+    }
+    const int S = D / 4, S4 = D / 16, MT = D / 16, NCH = MT * (MT + 1) / 2;
+    for (int k = threadIdx.x; k < NCH * 256; k += blockDim.x) {
+        const int e = k & 3, l = (k >> 2) & 63, c = k >> 8;
+        int mt = 0;
+        while (c >= (mt + 1) * S4 - (mt * (mt + 1)) / 2) ++mt;  // chunk -> (mt, s4)
+        const int s4 = mt + (c - (mt * S4 - (mt * (mt - 1)) / 2));
+        const int ks = 4 * s4 + e;
+        const int ra = 16 * mt + (l & 15), rb = 4 * ks + (l >> 4);
+        Af[k] = (rb >= ra) ? (float)R[ra * LDR + rb] : 0.0f;
+    }
+    for (int k = threadIdx.x; k < D; k += blockDim.x) {
+        const int g = k / S, st = k - g * S;
+        Af[NCH * 256 + k] = (float)mu[4 * st + g];
+    }
+    for (int a = threadIdx.x; a < D; a += blockDim.x) wmu[a] = (float)mu[a];
+}
+
 }  // namespace np8

@@ -443,6 +443,10 @@ struct NiwArgs {
     const double *part = nullptr;
     const int32_t *part_slot = nullptr;
     int64_t n_rec = 0;
+    // np8_niw_post on the wide path (else null): the drawn slot's contraction rows from the draw's own factor R
+    // (WideArgs::wA / wfrag / wmu) and its precision eigenvalue bound (WideArgs::lam_lo)
+    float *wA = nullptr, *wfrag = nullptr, *wmu = nullptr;
+    double *lam_lo = nullptr;
 };
 
 // np8_step_tail (the end of a synchronous step in one launch): which parts run.

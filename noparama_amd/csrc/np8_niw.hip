@@ -111,7 +111,9 @@ __device__ void write_sigma(int D, int LD, const double *B, const double *Rhs, b
 
 // Sigma = T^T T in 2 x 2 blocks per thread (half the LDS reads), each element one k-ordered chain (write_sigma's
 // second half, for a T already formed).
-__device__ void sigma_from_t(int D, int LD, const double *T, double *Sigma) {
+// T lower triangular: the terms k < max(a, b) are products with a zero (fma(0, t, +0) = +0 keeps the chain's bits)
+// and are skipped.  Sl (or null): Sigma also into LDS (leading dimension LD).
+__device__ __forceinline__ void sigma_from_t(int D, int LD, const double *T, double *Sigma, double *Sl = nullptr) {
     const int H = (D + 1) / 2;
     for (int e = threadIdx.x; e < 16 * H; e += blockDim.x) {
       for (int bb = e & 15; bb < H; bb += 16) {
@@ -119,7 +121,7 @@ __device__ void sigma_from_t(int D, int LD, const double *T, double *Sigma) {
         const bool a1 = a + 1 < D, b1 = b + 1 < D;
         double s00 = 0.0, s01 = 0.0, s10 = 0.0, s11 = 0.0;
         #pragma unroll 4
-        for (int k = 0; k < D; ++k) {
+        for (int k = (a > b ? a : b); k < D; ++k) {
             const double ta0 = T[k * LD + a], ta1 = a1 ? T[k * LD + a + 1] : 0.0;
             const double tb0 = T[k * LD + b], tb1 = b1 ? T[k * LD + b + 1] : 0.0;
             s00 = fma(ta0, tb0, s00);
@@ -131,8 +133,77 @@ __device__ void sigma_from_t(int D, int LD, const double *T, double *Sigma) {
         if (b1) Sigma[a * D + b + 1] = s01;
         if (a1) Sigma[(a + 1) * D + b] = s10;
         if (a1 && b1) Sigma[(a + 1) * D + b + 1] = s11;
+        if (Sl) {
+            Sl[a * LD + b] = s00;
+            if (b1) Sl[a * LD + b + 1] = s01;
+            if (a1) Sl[(a + 1) * LD + b] = s10;
+            if (a1 && b1) Sl[(a + 1) * LD + b + 1] = s11;
+        }
       }
     }
+}
+
+// Y = X X (X symmetric, D a multiple of 4) in 4 x 4 register blocks per thread.
+__device__ __forceinline__ void sym_square(int D, int LD, const double *X, double *Y) {
+    const int nb = D / 4;
+    for (int e = threadIdx.x; e < nb * nb; e += blockDim.x) {
+        const int bi = e / nb, bj = e - bi * nb;
+        double acc[4][4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[i][j] = 0.0;
+#pragma unroll 4
+        for (int k = 0; k < D; ++k) {
+            double a[4], b[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                a[i] = X[(4 * bi + i) * LD + k];  // (row 4 bi + i = column, X symmetric)
+                b[i] = X[k * LD + 4 * bj + i];
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[i][j] = fma(a[i], b[j], acc[i][j]);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) Y[(4 * bi + i) * LD + 4 * bj + j] = acc[i][j];
+    }
+}
+
+// Largest |row sum| of X (one thread per row; rs: D doubles of scratch).  Block-uniform result.
+__device__ __forceinline__ double max_abs_row_sum(int D, int LD, const double *X, double *rs) {
+    for (int a = threadIdx.x; a < D; a += blockDim.x) {
+        double v = 0.0;
+        for (int b = 0; b < D; ++b) v += fabs(X[a * LD + b]);
+        rs[a] = v;
+    }
+    __syncthreads();
+    double m = 0.0;
+    for (int a = 0; a < D; ++a) m = fmax(m, rs[a]);
+    __syncthreads();
+    return m;
+}
+
+// P' = packed sym(R^T R) for R upper (element (a, b), a <= b: sum_{k <= a} R_ka R_kb, k ascending from 0), off-diagonals
+// doubled, into the slot table and its candidate row; returns the candidate table's isotropy value (write_pprime).
+__device__ __forceinline__ double write_pprime_r(int D, int LD, const double *R, double *slotP, double *candP) {
+    bool iso = true;
+    const double p00 = fma(R[0], R[0], 0.0);  // element (0, 0)
+    for (int e = threadIdx.x; e < D * D; e += blockDim.x) {
+        const int a = e / D, b = e - a * D;
+        if (b < a) continue;
+        double s = 0.0;
+        #pragma unroll 8
+        for (int k = 0; k <= a; ++k) s = fma(R[k * LD + a], R[k * LD + b], s);
+        const double v = (a == b) ? s : 2.0 * s;
+        slotP[pix(D, a, b)] = v;
+        if (candP) candP[pix(D, a, b)] = v;
+        iso = iso && ((a == b) ? v == p00 : v == 0.0);
+    }
+    return __syncthreads_and(iso ? 1 : 0) ? p00 : 0.0;
 }
 
 constexpr int kPanelN = 16;
@@ -209,11 +280,14 @@ __device__ __forceinline__ void forward_panel(double *X, const double *G, int LD
 
 // The panel's updates to rows r >= c0 + 16, fma(-G_rk, X_kj, .) for k = c0 .. c0 + 15 ascending (inv: k >= j only);
 // all threads.
-__device__ __forceinline__ void forward_trailing(double *X, const double *G, int LD, int D, int c0, bool inv) {
+// lower: X0 (hence X) lower triangular -- elements j > r stay 0 and are skipped.
+__device__ __forceinline__ void forward_trailing(double *X, const double *G, int LD, int D, int c0, bool inv,
+                                                 bool lower = false) {
     const int rows = D - (c0 + kPanelN);
     for (int e = threadIdx.x; e < rows * D; e += blockDim.x) {
         const int r = c0 + kPanelN + e / D, j = e - (e / D) * D;
         if (inv && j > c0 + kPanelN - 1) continue;  // (columns right of the panel get nothing from it)
+        if (lower && j > r) continue;
         double acc = X[r * LD + j];
 #pragma unroll
         for (int i = 0; i < kPanelN; ++i) {
@@ -229,9 +303,9 @@ __device__ __forceinline__ bool init_ok_records(const NiwArgs &A) { return A.ini
 // Slot s's statistics from np8_suffstats_wide's run records (ParamArgs::part): the matching records are listed in
 // record order (each thread scans a contiguous range of headers, an exclusive scan places its matches), then every
 // thread sums its raw accumulator elements over the list in that order -- a fixed order, no atomics -- and adds
-// them to what the atomic fallback left in acc.  S lands in L's lower triangle (element (b, a) = S_ab, a <= b), s1
-// in s1.  Scratch: an int list of cap entries (Li's storage, unused until the factor exists).
-__device__ void reduce_run_records(const NiwArgs &A, int s, const double *acc, double *L, int LD, double *s1, int *list,
+// them to what the atomic fallback left in acc.  S lands in L's lower triangle index-reversed (element
+// (D - 1 - a, D - 1 - b) = S_ab, a <= b: where np8_niw_post forms J Psin J), s1 in s1.  Scratch: an int list of cap entries (Li's storage, unused until the factor exists).
+__device__ __forceinline__ void reduce_run_records(const NiwArgs &A, int s, const double *acc, double *L, int LD, double *s1, int *list,
                                    int cap) {
     const int D = A.D, T = D / 16, NT = T * (T + 1) / 2, RS = NT * 4 * 64 + T * 16;
     const int tid = threadIdx.x, nt = blockDim.x, lane = tid & 63, wv = tid >> 6, nw = nt >> 6;
@@ -305,7 +379,7 @@ __device__ void reduce_run_records(const NiwArgs &A, int s, const double *acc, d
             }
             const int tj = ti + qq;
             const int a = 16 * ti + (ln >> 4) + 4 * r, b = 16 * tj + (ln & 15);
-            if (a <= b) L[b * LD + a] = acc[D + pix(D, a, b)] + vk;
+            if (a <= b) L[(D - 1 - a) * LD + (D - 1 - b)] = acc[D + pix(D, a, b)] + vk;
         } else {
             const int kk = e - NT * 256, dim = 16 * (kk >> 4) + (kk & 15);
             s1[dim] = acc[dim] + vk;
@@ -388,14 +462,16 @@ __global__ __launch_bounds__(kNiwThreads) void np8_niw_post(NiwArgs A) {
     }
     if (tid == 0) bad = 0;
     __syncthreads();
-    // Psin's lower triangle formed in LDS by all threads (the statistics and Psi0 come from HBM once); the
-    // Bartlett draws (they need nothing of Psin) in the same phase
+    // J Psin J (J the index reversal) formed in LDS's lower triangle by all threads: element (r, j), r >= j, is
+    // Psin[D-1-r][D-1-j] (the statistics and Psi0 come from HBM once); the Bartlett draws (they need nothing of
+    // Psin) in the same phase
     for (int e = tid; e < D * D; e += blockDim.x) {
         const int r = e / D, j = e - r * D;
         if (j > r) continue;
-        const double Srj = recs ? L[r * LD + j] : S[pix(D, j, r)];
-        const double sc = (n > 0) ? Srj - (s1[r] * s1[j]) / nd : 0.0;
-        L[r * LD + j] = fma(kf, dm[r] * dm[j], A.Psi0[r * D + j] + sc);
+        const int ri = D - 1 - r, ji = D - 1 - j;  // ri <= ji
+        const double Srj = recs ? L[r * LD + j] : S[pix(D, ri, ji)];
+        const double sc = (n > 0) ? Srj - (s1[ri] * s1[ji]) / nd : 0.0;
+        L[r * LD + j] = fma(kf, dm[ri] * dm[ji], A.Psi0[ri * D + ji] + sc);
     }
     for (int a = tid; a < D; a += blockDim.x) {  // Bartlett diagonal
         const double g = chi2_mt(A.seed, i, t, stream, kNiwGammaCalls * (uint32_t)a, nun - a);
@@ -411,13 +487,12 @@ __global__ __launch_bounds__(kNiwThreads) void np8_niw_post(NiwArgs A) {
         z[j] = normal_at(A.seed, i, t, stream, kNiwNormalCall0, (uint32_t)(D * (D - 1) / 2 + j));
     __syncthreads();
     NIW_T(1)
-    const int lane = tid & 63, wv = tid >> 6;
-    (void)lane;
-    // Cholesky of Psin, blocked right-looking (panels of 16 columns: the panel factored by wave 0 in registers, the
-    // rows below updated by every thread): element (r, c) receives fma(-L_rk, L_ck, .) for k = 0, 1, ... in order,
-    // then the division by its pivot -- the operations of the oracle's left-looking loop, in its order, with two
-    // barriers per panel (round 3: two per column).  Wave 1 meanwhile: y = B^{-T} z / sqrt(kn) (B, z drawn above).
-    __shared__ int skip_s, fail_s;
+    const int wv = tid >> 6;
+    // Lr = chol(J Psin J), blocked right-looking (panels of 16 columns: the panel factored by wave 0 in registers,
+    // the rows below updated by every thread): element (r, c) receives fma(-L_rk, L_ck, .) for k = 0, 1, ... in
+    // order, then the division by its pivot -- the operations of the oracle's left-looking loop, in its order, with
+    // two barriers per panel.  U = J Lr J is upper with Psin = U U^T.  Wave 1 meanwhile: y = B^{-T} z / sqrt(kn).
+    __shared__ int skip_s;
     for (int p = 0; p * kPanelN < D; ++p) {
         const int c0 = p * kPanelN;
         if (wv == 0) {
@@ -440,7 +515,6 @@ __global__ __launch_bounds__(kNiwThreads) void np8_niw_post(NiwArgs A) {
         lower_panel_trailing(L, LD, D, c0);
         __syncthreads();
     }
-    (void)fail_s;
     __syncthreads();
     NIW_T(2)
     if (bad) {  // block-uniform: not numerically positive definite, the slot keeps its parameters
@@ -448,15 +522,15 @@ __global__ __launch_bounds__(kNiwThreads) void np8_niw_post(NiwArgs A) {
             for (int w = tid; w < W; w += blockDim.x) A.acc[(int64_t)s * W + w] = 0.0;
         return;
     }
-    // Li = L^{-1} and T = B^{-1} L^T (into F's storage; F is formed after Sigma) as blocked forward substitutions:
+    // M = Lr^{-1} (U^{-1} = J M J) and T = B^{-1} U^T (lower; into F's storage) as blocked forward substitutions:
     // row k final once divided by its diagonal, then it updates every later row -- element (r, j) receives
-    // fma(-L_rk, Li_kj, .) for k = j, ..., r - 1 (T: fma(-B_ak, T_kj, .) for k = 0, ..., a - 1) in order, as the
+    // fma(-L_rk, M_kj, .) for k = j, ..., r - 1 (T: fma(-B_ak, T_kj, .) for k = 0, ..., a - 1) in order, as the
     // oracle's loops do; the two panels side by side (waves 0 and 1), the trailing rows by every thread.  Wave 2: the
-    // new mean mun + L y.
+    // new mean mun + U y.
     double *T = F;
     for (int e = tid; e < D * D; e += blockDim.x) {
         const int a = e / D, j = e - a * D;
-        T[a * LD + j] = L[j * LD + a];
+        T[a * LD + j] = (j <= a) ? L[(D - 1 - j) * LD + (D - 1 - a)] : 0.0;  // U^T_aj = U_ja = Lr[D-1-j][D-1-a]
     }
     __syncthreads();
     for (int p = 0; p * kPanelN < D; ++p) {
@@ -467,15 +541,15 @@ __global__ __launch_bounds__(kNiwThreads) void np8_niw_post(NiwArgs A) {
             forward_panel(T, B, LD, D, c0, false);
         } else if (wv == 2 && p == 0) {
             for (int a = tid - 128; a < D; a += 64) {
-                double v = 0.0;
+                double v = 0.0;  // (U y)_a = sum_{k >= a} Lr[D-1-a][D-1-k] y_k
 #pragma unroll 8
-                for (int k = 0; k <= a; ++k) v = fma(L[a * LD + k], y[k], v);
+                for (int k = a; k < D; ++k) v = fma(L[(D - 1 - a) * LD + (D - 1 - k)], y[k], v);
                 mun[a] = mun[a] + v;  // (mun no longer needed: the new mean in its place)
             }
         }
         __syncthreads();
         forward_trailing(Li, L, LD, D, c0, true);
-        forward_trailing(T, B, LD, D, c0, false);
+        forward_trailing(T, B, LD, D, c0, false, true);
         __syncthreads();
     }
     __syncthreads();
@@ -485,26 +559,68 @@ __global__ __launch_bounds__(kNiwThreads) void np8_niw_post(NiwArgs A) {
         A.slot_mu[(int64_t)s * D + a] = mun[a];
         if (row >= 0) A.cand[(int64_t)row * cand_stride(D) + a] = mun[a];
     }
+    // (L's diagonal leaves with its logarithms: L's storage takes Sigma next, for the eigenvalue bound)
+    double *lg = xb, *rs = anc + D;
+    for (int a = tid; a < D; a += blockDim.x) lg[a] = log_pos(L[a * LD + a]);
     if (tid == 0) {
         LogAcc la;
         for (int a = 0; a < D; ++a) la.add(gv[a], a, D - 1);
         sh[0] = la.sumlog;
     }
-    sigma_from_t(D, LD, F, A.slot_sigma + (int64_t)s * D * D);  // Sigma = T^T T (T in F's storage)
+    __syncthreads();
+    if (tid == 0) {
+        double sl = 0.0;
+        for (int a = 0; a < D; ++a) sl += lg[a];
+        sh[1] = sl;
+    }
+    const bool bound = A.lam_lo != nullptr;
+    sigma_from_t(D, LD, F, A.slot_sigma + (int64_t)s * D * D, bound ? L : nullptr);  // Sigma = T^T T
     __syncthreads();
     NIW_T(4)
-    for (int e = tid; e < D * D; e += blockDim.x) {  // F = Li^T B
+    // R = B^T U^{-1} (upper, into F's storage: T is dead): R_ab = sum_{k = a..b} B_ka M[D-1-k][D-1-b]
+    for (int e = tid; e < D * D; e += blockDim.x) {
         const int a = e / D, b = e - a * D;
         double v = 0.0;
-        #pragma unroll 8
-        for (int k = (a > b ? a : b); k < D; ++k) v = fma(Li[k * LD + a], B[k * LD + b], v);
+        if (b >= a) {
+#pragma unroll 8
+            for (int k = a; k <= b; ++k) v = fma(B[k * LD + a], Li[(D - 1 - k) * LD + (D - 1 - b)], v);
+        }
         F[a * LD + b] = v;
     }
     __syncthreads();
     NIW_T(5)
-    const double iso = write_pprime(D, LD, F, A.slot_P + (int64_t)s * (D * (D + 1) / 2),
-                                    row >= 0 ? A.cand + (int64_t)row * cand_stride(D) + D : nullptr);
+    const double iso = write_pprime_r(D, LD, F, A.slot_P + (int64_t)s * (D * (D + 1) / 2),
+                                      row >= 0 ? A.cand + (int64_t)row * cand_stride(D) + D : nullptr);
     NIW_T(6)
+    if (A.wA) {  // the wide path: the contraction rows from R itself, the eigenvalue bound from Sigma's row sums
+        const int NCH = (D / 16) * (D / 16 + 1) / 2;
+        wide_write_rows(D, F, LD, mun, A.wA + (int64_t)s * D * D, A.wfrag + (int64_t)s * (NCH * 256 + D),
+                        A.wmu + (int64_t)s * D);
+    }
+    if (bound) {
+        // lambda_min(P) = 1 / lambda_max(Sigma), lambda_max(Sigma) = rho(Sigma) <= ||Sigma^8||^(1/8) (any consistent
+        // norm; max |row sum| here) -- within a few % of lambda_max where the Gershgorin bound ||Sigma|| can be 40%
+        // above it.  Sigma is scaled by g = ||Sigma|| first (entries of (Sigma/g)^8 stay in [0, 1], no overflow,
+        // and ||(Sigma/g)^8|| >= D^-4: no underflow); 1% for the fp32 factor, the fp32 contraction and the rounding.
+        const double g = max_abs_row_sum(D, LD, L, rs);
+        const double rg = (g > 0.0) ? 1.0 / g : 0.0;
+        for (int e = tid; e < D * D; e += blockDim.x) {
+            const int a = e / D, b = e - a * D;
+            L[a * LD + b] *= rg;
+        }
+        __syncthreads();
+        sym_square(D, LD, L, B);   // (Sigma/g)^2  (B and Li are free once R exists)
+        __syncthreads();
+        sym_square(D, LD, B, Li);  // ^4
+        __syncthreads();
+        sym_square(D, LD, Li, L);  // ^8
+        __syncthreads();
+        const double m = max_abs_row_sum(D, LD, L, rs);
+        if (tid == 0) {
+            const double lmax = g * sqrt(sqrt(sqrt(m)));
+            A.lam_lo[s] = (lmax > 0.0 && lmax < 1e300) ? 0.99 / lmax : 0.0;
+        }
+    }
     NIW_T(7)
     NIW_T(8)
 #ifdef NP8_EXP_NIW_TIMING
@@ -513,11 +629,7 @@ __global__ __launch_bounds__(kNiwThreads) void np8_niw_post(NiwArgs A) {
                tph[2] - tph[1], tph[3] - tph[2], tph[4] - tph[3], tph[5] - tph[4], tph[6] - tph[5], tph[7] - tph[6],
                tph[8] - tph[7]);
 #endif
-    if (tid == 0) {
-        double sl = 0.0;
-        for (int a = 0; a < D; ++a) sl += log_pos(L[a * LD + a]);
-        write_row_scalars(A, s, row, fma(0.5, sh[0], fma(-0.5 * (double)D, kLog2Pi, -sl)), iso);
-    }
+    if (tid == 0) write_row_scalars(A, s, row, fma(0.5, sh[0], fma(-0.5 * (double)D, kLog2Pi, -sh[1])), iso);
     if (n > 0)
         for (int w = tid; w < W; w += blockDim.x) A.acc[(int64_t)s * W + w] = 0.0;  // zero for the next sweep
 }

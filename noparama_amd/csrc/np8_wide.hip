@@ -361,30 +361,9 @@ __global__ __launch_bounds__(256) void np8_wide_rows(WideArgs W) {
     }
     // 1% for the fp32 factor and the fp32 contraction, and the Cholesky's own rounding
     if (lam && tid == 0) W.lam_lo[s] = 0.99 * lo;
-    float *An = W.wA + (int64_t)s * D * D;
-    for (int k = threadIdx.x; k < D * D; k += blockDim.x) {
-        const int a = k / D, b = k - a * D;
-        An[k] = (b >= a) ? (float)Wk[a * LD + b] : 0.0f;
-    }
-    // fragment chunks (mt, s4), s4 >= mt, in compact order; in chunk c = chunk(mt, s4) lane l's float4
-    // element e (k-step ks = 4 s4 + e) holds A[16 mt + (l & 15)][4 ks + (l >> 4)]; then muf transposed:
-    // [g][s] = muf[4 s + g]
-    const int S = D / 4, S4 = D / 16, MT = D / 16, NCH = MT * (MT + 1) / 2;
-    float *Af = W.wfrag + (int64_t)s * (NCH * 256 + D);
-    for (int k = threadIdx.x; k < NCH * 256; k += blockDim.x) {
-        const int e = k & 3, l = (k >> 2) & 63, c = k >> 8;
-        int mt = 0;
-        while (c >= (mt + 1) * S4 - (mt * (mt + 1)) / 2) ++mt;  // chunk -> (mt, s4)
-        const int s4 = mt + (c - (mt * S4 - (mt * (mt - 1)) / 2));
-        const int ks = 4 * s4 + e;
-        const int ra = 16 * mt + (l & 15), rb = 4 * ks + (l >> 4);
-        Af[k] = (rb >= ra) ? (float)Wk[ra * LD + rb] : 0.0f;
-    }
-    for (int k = threadIdx.x; k < D; k += blockDim.x) {
-        const int g = k / S, st = k - g * S;
-        Af[NCH * 256 + k] = (float)W.slot_mu[(int64_t)s * D + 4 * st + g];
-    }
-    for (int a = threadIdx.x; a < D; a += blockDim.x) W.wmu[(int64_t)s * D + a] = (float)W.slot_mu[(int64_t)s * D + a];
+    const int NCH = (D / 16) * (D / 16 + 1) / 2;
+    wide_write_rows(D, Wk, LD, W.slot_mu + (int64_t)s * D, W.wA + (int64_t)s * D * D, W.wfrag + (int64_t)s * (NCH * 256 + D),
+                    W.wmu + (int64_t)s * D);
 #ifdef NP8_EXP_WIDE_TIMING
     WR_T(15)
     if (tid == 0 && s < 3)
@@ -551,11 +530,40 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NP8_WIDE_WA
     // with running maximum T >= lw_own(x): lw_j(x) <= c_j + log n_j - lam_j (|mu_j - mu_own| - |x - mu_own|)^2 / 2
     // (triangle inequality, lam_j <= the smallest eigenvalue of row j's precision); a row below T - 80 - 2
     // (and a relative margin) for every lane is one its pick_step would skip -- results unchanged.
-    // kMaskWords: up to 64 * 8 = 512 rows (kcap of the wide path).
-    constexpr int kMaskWords = 8;
+    // kMaskWords: up to 64 * 8 = 512 rows (kcap of the wide path).  The rows' scalars (slot, c + log n, lam / 2) are
+    // staged in LDS once per block, and the rows each stage keeps are compacted into a list (no bit scans per row).
+    constexpr int kMaskWords = 8, kRowsMax = 64 * kMaskWords;
     __shared__ unsigned long long rmask[kMaskWords], rmask2[kMaskWords];
-    const bool prune = A.wdist != nullptr && K <= 64 * kMaskWords;
+    __shared__ int32_t rslot[kRowsMax];
+    __shared__ double rbase[kRowsMax], rlamh[kRowsMax];
+    __shared__ int16_t rlist[2][kRowsMax];
+    __shared__ int rlist_n[2];
+    const bool prune = A.wdist != nullptr && K <= kRowsMax;
+    // the rows set in mask m, ascending, into list (all threads; a barrier before the list is read)
+    auto compact = [&](const unsigned long long *m, int16_t *list, int *cnt) {
+        for (int j = threadIdx.x; j < K; j += blockDim.x) {
+            const int w = j >> 6, bit = j & 63;
+            const unsigned long long mw = m[w];
+            if ((mw >> bit) & 1ull) {
+                int pos = __popcll(mw & ((1ull << bit) - 1ull));
+                for (int v = 0; v < w; ++v) pos += __popcll(m[v]);
+                list[pos] = (int16_t)j;
+            }
+        }
+        if (threadIdx.x == 0) {
+            int c = 0;
+            for (int v = 0; v < kMaskWords; ++v) c += __popcll(m[v]);
+            *cnt = c;
+        }
+    };
     if (prune) {
+        for (int j = threadIdx.x; j < K; j += blockDim.x) {
+            const double *e = cand + (int64_t)j * CS;
+            const int32_t sj = (int32_t)e[F + kFieldSlot];
+            rslot[j] = sj;
+            rbase[j] = e[F + kFieldC] + e[F + kFieldLogn];
+            rlamh[j] = 0.5 * A.lam_lo[sj];
+        }
         if (threadIdx.x < kMaskWords) rmask[threadIdx.x] = rmask2[threadIdx.x] = 0ull;
         __syncthreads();
         // per distinct own row of the wave (one in the label-sorted layout): the group's largest radius and
@@ -577,41 +585,32 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NP8_WIDE_WA
             for (int jb = 0; jb < K; jb += 64) {
                 const int j = jb + lane;
                 bool need = false;
-                if (j < K) {
-                    const double *e = cand + (int64_t)j * CS;
-                    const int32_t sj = (int32_t)e[F + kFieldSlot];
-                    if (sj != zg) {
-                        const double base = e[F + kFieldC] + e[F + kFieldLogn];
-                        const double gap = fmax(A.wdist[(int64_t)jg * A.kcap + j] - rmax, 0.0);
-                        const double far = 0.5 * A.lam_lo[sj] * gap * gap;
-                        const double U = base - far - tmin;
-                        need = !(U <= -kSkip - 2.0 - 1e-9 * (fabs(base) + fabs(tmin) + far));
-                    }
+                if (j < K && rslot[j] != zg) {
+                    const double base = rbase[j];
+                    const double gap = fmax(A.wdist[(int64_t)jg * A.kcap + j] - rmax, 0.0);
+                    const double far = rlamh[j] * gap * gap;
+                    const double U = base - far - tmin;
+                    need = !(U <= -kSkip - 2.0 - 1e-9 * (fabs(base) + fabs(tmin) + far));
                 }
                 const uint64_t b = __ballot(need);
                 if (b != 0ull && lane == 0) atomicOr(&rmask[jb >> 6], b);
             }
         }
         __syncthreads();
+        compact(rmask, rlist[0], &rlist_n[0]);
+        __syncthreads();
     }
-    // the next row at or after j in mask m (block-uniform)
-    auto next_in = [&](const unsigned long long *m, int j) -> int {
-        while (j < K) {
-            const unsigned long long w = m[j >> 6] >> (j & 63);
-            if (w) return j + __ffsll(w) - 1;
-            j = (j | 63) + 1;
-        }
-        return K;
-    };
     // The exact-distance screen of the rows the mask kept (DESIGN.md §5 "Wide-path pruning"): per item and row,
     // lw_j(x) <= c_j + log n_j - lam_j |x - muf_j|^2 / 2 with the distance itself, |x|^2 + |muf_j|^2 - 2 x.muf_j,
     // the dot products of 16 rows and the wave's 64 items on the matrix cores (D/4 MFMAs per item tile and 16
     // rows, against 2.5 D^2/16... for a contraction), lowered by a rigorous margin for their fp32 rounding
     // (|error| <= 64 u sum |x_a mu_a| <= 4e-6 (|x|^2 + |muf|^2)); the triangle inequality of the mask loses
     // most of it at D = 64 (x - mu_own is nearly orthogonal to mu_j - mu_own).  A row survives when a lane of
-    // the block may not skip it; results are unchanged.
+    // the block may not skip it; results are unchanged.  The next batch's means are loaded while this one's
+    // MFMAs run.
     if (prune) {
-        if (wave_live) {
+        const int n1 = rlist_n[0];
+        if (wave_live && n1 > 0) {
             using W2 = Wide<D>;
             const double Tl = valid ? st.T : 1e300;
             double Ti[4], x2i[4];
@@ -622,35 +621,33 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NP8_WIDE_WA
                 x2i[nt] = __shfl(x2, 16 * nt + col);
                 zit[nt] = __shfl(zi, 16 * nt + col);
             }
-            int j = next_in(rmask, 0);
-            while (j < K) {  // block-uniform: 16 kept rows at a time
-                int myrow = K, orow[4] = {K, K, K, K};
-                int jj = j;
-#pragma unroll 1
-                for (int c = 0; c < 16; ++c) {
-                    myrow = (col == c) ? jj : myrow;
+            // A operand: lane (g, col) holds muf[4 s + g] of row list[b0 + col] (the transposed mean of its row)
+            auto load_means = [&](int b0, float (&am)[W2::S]) {
+                if (b0 + col < n1) {
+                    const float *mt = A.wfrag + (int64_t)rslot[rlist[0][b0 + col]] * W2::ROW + W2::NCH * 256 + g * W2::S;
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) orow[r] = (4 * g + r == c) ? jj : orow[r];
-                    if (jj < K) jj = next_in(rmask, jj + 1);
-                }
-                j = jj;
-                // A operand: lane (g, col) holds muf[4 s + g] of row myrow (the transposed mean of its fragment row)
-                float am[W2::S];
-                double m2p = 0.0;
-                if (myrow < K) {
-                    const int sj = (int)cand[(int64_t)myrow * CS + F + kFieldSlot];
-                    const float *mt = A.wfrag + (int64_t)sj * W2::ROW + W2::NCH * 256 + g * W2::S;
-#pragma unroll
-                    for (int s = 0; s < W2::S; ++s) {
-                        am[s] = mt[s];
-                        m2p = fma((double)am[s], (double)am[s], m2p);
+                    for (int s4 = 0; s4 < W2::S / 4; ++s4) {
+                        const float4 v = *reinterpret_cast<const float4 *>(mt + 4 * s4);
+                        am[4 * s4] = v.x;
+                        am[4 * s4 + 1] = v.y;
+                        am[4 * s4 + 2] = v.z;
+                        am[4 * s4 + 3] = v.w;
                     }
                 } else {
 #pragma unroll
                     for (int s = 0; s < W2::S; ++s) am[s] = 0.0f;
                 }
+            };
+            float am[W2::S];
+            load_means(0, am);
+            for (int b0 = 0; b0 < n1; b0 += 16) {  // block-uniform: 16 kept rows at a time
+                float amn[W2::S];
+                if (b0 + 16 < n1) load_means(b0 + 16, amn);
+                double m2p = 0.0;
+#pragma unroll
+                for (int s = 0; s < W2::S; ++s) m2p = fma((double)am[s], (double)am[s], m2p);
                 double m2 = m2p + __shfl_xor(m2p, 16);
-                m2 += __shfl_xor(m2, 32);  // |muf|^2 of row myrow, on the four lanes of column col
+                m2 += __shfl_xor(m2, 32);  // |muf|^2 of row list[b0 + col], on the four lanes of column col
                 typedef float f32x4 __attribute__((ext_vector_type(4)));
                 f32x4 acc[4];
 #pragma unroll
@@ -659,23 +656,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NP8_WIDE_WA
                 for (int s = 0; s < W2::S; ++s)
 #pragma unroll
                     for (int nt = 0; nt < 4; ++nt) acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(am[s], xb[nt][s], acc[nt], 0, 0, 0);
-                // output (nt, r) of lane (g, col): row orow[r] (= 4 g + r of the 16), item 16 nt + col
+                // output (nt, r) of lane (g, col): row list[b0 + 4 g + r], item 16 nt + col
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    const int jr = orow[r];
+                    const int li = b0 + 4 * g + r;
+                    const int jr = (li < n1) ? (int)rlist[0][li] : K;
                     const double m2r = __shfl(m2, 4 * g + r);
                     bool nr = false;
                     if (jr < K) {
-                        const double *e = cand + (int64_t)jr * CS;
-                        const int32_t sjr = (int32_t)e[F + kFieldSlot];
-                        const double base = e[F + kFieldC] + e[F + kFieldLogn];
-                        const double lam = A.lam_lo[sjr];
+                        const int32_t sjr = rslot[jr];
+                        const double base = rbase[jr], lamh = rlamh[jr];
 #pragma unroll
                         for (int nt = 0; nt < 4; ++nt) {
                             if (sjr != zit[nt] && Ti[nt] < 1e299) {
                                 const double sq = x2i[nt] + m2r;
                                 const double d2 = fmax(fma(-2.0, (double)acc[nt][r], sq) - 1e-5 * sq, 0.0);
-                                const double far = 0.5 * lam * d2;
+                                const double far = lamh * d2;
                                 const double U = base - far - Ti[nt];
                                 nr = nr || !(U <= -kSkip - 2.0 - 1e-9 * (fabs(base) + fabs(Ti[nt]) + far));
                             }
@@ -690,30 +686,37 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NP8_WIDE_WA
                             atomicOr(&rmask2[row >> 6], 1ull << (row & 63));
                     }
                 }
+                if (b0 + 16 < n1) {
+#pragma unroll
+                    for (int s = 0; s < W2::S; ++s) am[s] = amn[s];
+                }
             }
         }
         __syncthreads();
+        compact(rmask2, rlist[1], &rlist_n[1]);
+        __syncthreads();
     }
-    // the next row to evaluate at or after j (block-uniform)
-    auto next_row = [&](int j) -> int { return prune ? next_in(rmask2, j) : j; };
+    // the rows to evaluate (block-uniform): the screen's list, or every row
+    const int nrows = prune ? rlist_n[1] : K;
+    auto row_at = [&](int i) -> int { return prune ? (int)rlist[1][i] : i; };
 
     // the evaluated candidates in ascending order, block-uniform: the next one is copied into the other
     // stage while the MFMAs of this one run; one barrier per row
-    int j = next_row(0), buf = 0, rows_done = 0;
-    if (j < K) row_glds<D>(A.wfrag, (int)cand[(int64_t)j * CS + F + kFieldSlot], stage);
+    int buf = 0, rows_done = 0;
+    if (nrows > 0) row_glds<D>(A.wfrag, (int)cand[(int64_t)row_at(0) * CS + F + kFieldSlot], stage);
     __syncthreads();
-    while (j < K) {
+    for (int i = 0; i < nrows; ++i) {
+        const int j = row_at(i);
         const double *e = cand + (int64_t)j * CS;  // block-uniform: scalar loads
         const int32_t sj = (int32_t)e[F + kFieldSlot];
-        const int jn = next_row(j + 1);
-        if (jn < K) row_glds<D>(A.wfrag, (int)cand[(int64_t)jn * CS + F + kFieldSlot], stage + (buf ^ 1) * W::ROW);
+        if (i + 1 < nrows)
+            row_glds<D>(A.wfrag, (int)cand[(int64_t)row_at(i + 1) * CS + F + kFieldSlot], stage + (buf ^ 1) * W::ROW);
         const float *row = stage + buf * W::ROW;
         if (wave_live) {
             const double q = wide_pass<D>(row, xb, lane);
             if (sj != zi) pick_step(st, fma(-0.5, q, e[F + kFieldC]) + e[F + kFieldLogn], j);
         }
         __syncthreads();  // the next row has landed (vmcnt(0)); this row's stage may be overwritten
-        j = jn;
         buf ^= 1;
         ++rows_done;
     }
@@ -890,21 +893,29 @@ hipError_t np8_launch_loglik_wide_mfma(const AssignArgs &A, int D, double *parti
 
 // ---- sufficient statistics on the fp64 matrix cores (niw_conjugate on the wide path) -------------------
 // Per slot: s1 = sum d, S = sum d d^T (packed upper) with d = x - mu_slot in fp64 (the layout of
-// np8_suffstats / np8o_suffstats).  One wave walks kSuffChunks chunks of 64 consecutive positions of
-// the (label-sorted) layout; each chunk is staged in LDS (coalesced row reads), then for the slot run
-// being accumulated S += D^T D on v_mfma_f64_16x16x4_f64 (items = the k dimension: 4 per MFMA, 16 steps
-// per chunk, the 16x16 tiles ti <= tj of S), items of other slots masked to 0.  Sums stay in registers
-// while the slot does not change and are committed with fp64 atomics when it does.
+// np8_suffstats / np8o_suffstats).  One wave walks 64 kSuffChunks consecutive positions of the (label-sorted)
+// layout in chunks of 32 items; each chunk is staged in LDS (coalesced row reads: one load instruction moves
+// 128 B of dim a and 128 B of dim a + D/2), then for the slot run being accumulated S += D^T D on
+// v_mfma_f64_16x16x4_f64 (items = the k dimension: 4 per MFMA, 8 steps per chunk, the 16x16 tiles ti <= tj of S),
+// items of other slots masked to 0.  Sums stay in registers while the slot does not change and are committed
+// as a run record (ParamArgs::part, reduced in record order by np8_niw_post) or with fp64 atomics.
+// Registers: the next chunk's 32 floats per lane in flight while this one is contracted, the accumulators in
+// AGPRs, one MFMA step's operands at a time -- two waves per SIMD (round 3: 472 registers, one wave).
 #ifndef NP8_SUFF_CHUNKS
 #define NP8_SUFF_CHUNKS 8
 #endif
-constexpr int kSuffChunks = NP8_SUFF_CHUNKS;
+constexpr int kSuffChunks = NP8_SUFF_CHUNKS;  // (64-item units per wave)
 
-template <int D>
-__global__ __launch_bounds__(256) void np8_suffstats_wide(ParamArgs P) {
-    constexpr int T = D / 16, NT = T * (T + 1) / 2, W = D + D * (D + 1) / 2;
+// BUF: item rows through a buffer descriptor (32-bit offsets: D n 4 < 2^31 bytes), two VGPRs of addressing instead
+// of one 64-bit address per row.
+template <int D, bool BUF>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void np8_suffstats_wide(ParamArgs P) {
+    constexpr int T = D / 16, NT = T * (T + 1) / 2, W = D + D * (D + 1) / 2, H = D / 2;
+    constexpr int CI = 32;           // items per chunk
+    constexpr int PS = 2 * CI + 2;   // floats per dim pair (a, a + H): conflict-free column reads
+    constexpr int NCH = 2 * kSuffChunks;
     typedef double f64x4 __attribute__((ext_vector_type(4)));
-    __shared__ float tile[4][D][65];  // per wave: [dim][item] (+1 pad: conflict-free column reads)
+    __shared__ float tile[4][H * PS];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, g = lane >> 4, col = lane & 15;
     const bool sorted = P.sorted != 0;
     constexpr int cur = 0;  // the label-sorted layout is always buffer 0 (buffer 1: the re-sort's scratch)
@@ -912,7 +923,7 @@ __global__ __launch_bounds__(256) void np8_suffstats_wide(ParamArgs P) {
     const int32_t *__restrict__ z = sorted ? (cur ? P.zs[1] : P.zs[0]) : P.z;
     const int64_t n = P.n_loc;
     const int64_t wid = (int64_t)blockIdx.x * 4 + wv;
-    const int64_t base = wid * (64 * kSuffChunks);
+    const int64_t base = wid * (int64_t)(CI * NCH);
     int nrun = 0;  // run records this wave wrote
     auto close_records = [&]() {  // the unused run records of this wave
         if (P.part && lane < kSuffRuns && lane >= nrun) P.part_slot[wid * kSuffRuns + lane] = -1;
@@ -921,7 +932,7 @@ __global__ __launch_bounds__(256) void np8_suffstats_wide(ParamArgs P) {
         close_records();
         return;
     }
-    float(*tl)[65] = tile[wv];
+    float *tl = tile[wv];
     f64x4 acc[NT];
     double s1[T];
     int32_t cs = -1;        // slot being accumulated
@@ -933,13 +944,18 @@ __global__ __launch_bounds__(256) void np8_suffstats_wide(ParamArgs P) {
         for (int t = 0; t < T; ++t) s1[t] = 0.0;
     };
     auto commit = [&]() {
+        // the lane's index made opaque here: its address arithmetic stays in this (rare) path instead of being
+        // hoisted out of the chunk loop and held in registers across it
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+        const int g = ln >> 4, col = ln & 15;
         if (P.part && nrun < kSuffRuns) {  // a run record: the raw accumulators, then s1 (dims 16 t + col)
             constexpr int RS = NT * 4 * 64 + T * 16;
             double *rec = P.part + (wid * kSuffRuns + nrun) * RS;
 #pragma unroll
             for (int q = 0; q < NT; ++q)
 #pragma unroll
-                for (int r = 0; r < 4; ++r) rec[(q * 4 + r) * 64 + lane] = acc[q][r];
+                for (int r = 0; r < 4; ++r) rec[(q * 4 + r) * 64 + ln] = acc[q][r];
 #pragma unroll
             for (int t = 0; t < T; ++t) {
                 double v = s1[t];
@@ -947,7 +963,7 @@ __global__ __launch_bounds__(256) void np8_suffstats_wide(ParamArgs P) {
                 v += __shfl_xor(v, 32);
                 if (g == 0) rec[NT * 4 * 64 + t * 16 + col] = v;
             }
-            if (lane == 0) P.part_slot[wid * kSuffRuns + nrun] = cs;
+            if (ln == 0) P.part_slot[wid * kSuffRuns + nrun] = cs;
             ++nrun;
             return;
         }
@@ -960,11 +976,7 @@ __global__ __launch_bounds__(256) void np8_suffstats_wide(ParamArgs P) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int a = 16 * ti + g + 4 * r, b = 16 * tj + col;  // f64 MFMA layout
-#ifdef NP8_EXP_SUFF_NOATOMIC  // experiment (wrong sums): plain stores instead of atomics
-                    if (a <= b) dst[D + a * D - (a * (a - 1)) / 2 + (b - a)] = acc[q][r];
-#else
                     if (a <= b) unsafeAtomicAdd(dst + D + a * D - (a * (a - 1)) / 2 + (b - a), acc[q][r]);
-#endif
                 }
 #pragma unroll
         for (int t = 0; t < T; ++t) {
@@ -975,29 +987,43 @@ __global__ __launch_bounds__(256) void np8_suffstats_wide(ParamArgs P) {
         }
     };
     reset();
-    // software-pipelined: chunk c + 1's item rows and labels are in flight (registers) while chunk c (LDS) is
-    // contracted -- one round of 64 loads per chunk instead of eight dependent rounds
-    float xn[D];
+    // LDS word of (dim, item): pair a = dim mod H, half dim / H
+    auto lds_at = [&](int dim, int it) { return (dim % H) * PS + (dim / H) * CI + it; };
+    // software-pipelined: chunk c + 1's item rows (lane: item lane & 31 of dims a + H (lane >> 5)) and labels are
+    // in flight while chunk c (LDS) is contracted
+    float xn[H];
     int32_t zn;
+    const uint64_t xa = reinterpret_cast<uint64_t>(X);
+    const uint32_t xlo = __builtin_amdgcn_readfirstlane((uint32_t)xa), xhi = __builtin_amdgcn_readfirstlane((uint32_t)(xa >> 32));
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<void *>(((uint64_t)xhi << 32) | xlo), 0, __builtin_amdgcn_readfirstlane((int)(BUF ? n * D * 4 : 0)),
+        0x00020000);
     auto fetch = [&](int c) {
-        const int64_t p = base + 64 * c + lane;
-        const bool valid = p < n && base + 64 * c < n;
+        const int64_t p = base + CI * c + (lane & 31);
+        const bool valid = p < n && lane < CI;
         zn = valid ? z[p] : -1;
+        const int64_t pr = (p < n) ? p : 0;  // (rows past the end: any in-bounds word, masked by its label)
+        if constexpr (BUF) {
+            const int vo = (int)(((int64_t)(lane >> 5) * H * n + pr) * 4);
+            const int n4 = (int)(n * 4);
 #pragma unroll
-        for (int a = 0; a < D; ++a) xn[a] = valid ? X[(int64_t)a * n + p] : 0.0f;
+            for (int a = 0; a < H; ++a) xn[a] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, vo, a * n4, 0));
+        } else {
+            const float *src = X + (int64_t)(lane >> 5) * H * n + pr;
+#pragma unroll
+            for (int a = 0; a < H; ++a) xn[a] = src[(int64_t)a * n];
+        }
     };
     fetch(0);
-    for (int c = 0; c < kSuffChunks; ++c) {
-        const int64_t p0 = base + 64 * c;
+    for (int c = 0; c < NCH; ++c) {
+        const int64_t p0 = base + CI * c;
         if (p0 >= n) break;
-        const int64_t p = p0 + lane;
-        const bool valid = p < n;
-        const int32_t zl = zn;
+        const int32_t zl = zn;  // labels of the chunk's items (lanes 0..31; -1 past the end)
 #pragma unroll
-        for (int a = 0; a < D; ++a) tl[a][lane] = xn[a];
+        for (int a = 0; a < H; ++a) tl[a * PS + lane] = xn[a];
         __builtin_amdgcn_wave_barrier();
-        if (c + 1 < kSuffChunks) fetch(c + 1);
-        uint64_t pend = __ballot(valid);
+        if (c + 1 < NCH) fetch(c + 1);
+        uint64_t pend = __ballot(zl >= 0);
         while (pend) {
             const int32_t sl = __shfl(zl, __ffsll((unsigned long long)pend) - 1);
             if (sl != cs) {
@@ -1008,13 +1034,13 @@ __global__ __launch_bounds__(256) void np8_suffstats_wide(ParamArgs P) {
                 for (int t = 0; t < T; ++t) anc[t] = P.slot_mu[(int64_t)cs * D + 16 * t + col];
             }
             pend &= ~__ballot(zl == sl);
-#pragma unroll
-            for (int st = 0; st < 16; ++st) {
+#pragma unroll 2
+            for (int st = 0; st < CI / 4; ++st) {
                 const int it = 4 * st + g;  // item of this k-step held by the lane
                 const bool in = __shfl(zl, it) == sl;
                 double dv[T];
 #pragma unroll
-                for (int t = 0; t < T; ++t) dv[t] = in ? (double)tl[16 * t + col][it] - anc[t] : 0.0;
+                for (int t = 0; t < T; ++t) dv[t] = in ? (double)tl[lds_at(16 * t + col, it)] - anc[t] : 0.0;
 #pragma unroll
                 for (int t = 0; t < T; ++t) s1[t] += dv[t];
                 int q = 0;
@@ -1032,7 +1058,7 @@ __global__ __launch_bounds__(256) void np8_suffstats_wide(ParamArgs P) {
 }
 
 // Waves of an np8_suffstats_wide launch over n items, and the doubles of one run record at D (ParamArgs::part).
-int64_t np8_suffstats_wide_waves(int64_t n) { return 4 * ((n + 4 * 64 * kSuffChunks - 1) / (4 * 64 * kSuffChunks)); }
+int64_t np8_suffstats_wide_waves(int64_t n) { return 4 * ((n + 4 * 64 * kSuffChunks - 1) / (4 * 64 * kSuffChunks)); }  // (64 kSuffChunks items per wave)
 int64_t np8_suffstats_wide_record(int D) {
     const int T = D / 16;
     return (int64_t)(T * (T + 1) / 2) * 4 * 64 + T * 16;
@@ -1042,15 +1068,20 @@ hipError_t np8_launch_suffstats_wide(const ParamArgs &P, hipStream_t s) {
     const int64_t per_block = 4 * 64 * kSuffChunks;
     const int64_t nb = (P.n_loc + per_block - 1) / per_block;
     if (nb <= 0) return hipSuccess;
-    if (P.D == 32)
-        hipLaunchKernelGGL((np8_suffstats_wide<32>), dim3((unsigned)nb), dim3(256), 0, s, P);
-    else if (P.D == 48)
-        hipLaunchKernelGGL((np8_suffstats_wide<48>), dim3((unsigned)nb), dim3(256), 0, s, P);
-    else if (P.D == 64)
-        hipLaunchKernelGGL((np8_suffstats_wide<64>), dim3((unsigned)nb), dim3(256), 0, s, P);
-    else
-        return hipErrorInvalidValue;
-    return hipGetLastError();
+    const bool buf = P.n_loc * P.D * 4 < ((int64_t)1 << 31);
+#define NP8_SUFF_LAUNCH(DD)                                                                                   \
+    if (P.D == DD) {                                                                                          \
+        if (buf)                                                                                              \
+            hipLaunchKernelGGL((np8_suffstats_wide<DD, true>), dim3((unsigned)nb), dim3(256), 0, s, P);       \
+        else                                                                                                  \
+            hipLaunchKernelGGL((np8_suffstats_wide<DD, false>), dim3((unsigned)nb), dim3(256), 0, s, P);      \
+        return hipGetLastError();                                                                             \
+    }
+    NP8_SUFF_LAUNCH(32)
+    NP8_SUFF_LAUNCH(48)
+    NP8_SUFF_LAUNCH(64)
+#undef NP8_SUFF_LAUNCH
+    return hipErrorInvalidValue;
 }
 
 // ---- dispatch ----------------------------------------------------------------------------------------

@@ -1071,17 +1071,23 @@ static void niw_aux_slot(const np8o_ctx *c, uint64_t i, uint32_t t, int m, const
  * upper) about the anchor a (d = x - a), then a draw (Sigma, mu) from it (n = 0: the prior):
  *   kn = kappa0 + n, nun = nu0 + n, xb = a + s1/n, mun = (kappa0 mu0 + n xb)/kn,
  *   Psin = Psi0 + (S - s1 s1^T/n) + (kappa0 n/kn)(xb - mu0)(xb - mu0)^T;
- *   Ln = chol(Psin); Sigma^{-1} = F F^T with F = Ln^{-T} B (B Bartlett-lower with nun), so Sigma ~ IW(Psin, nun);
- *   mu = mun + Ln B^{-T} z / sqrt(kn) ~ N(mun, Sigma/kn);  c = -D/2 log 2pi - sum log Ln_aa + 1/2 sum log B_aa^2.
+ *   Psin = U U^T with U upper triangular: Lr = chol(J Psin J) (J the index reversal), U = J Lr J;
+ *   R = B^T U^{-1} (upper; B Bartlett-lower with nun): Sigma^{-1} = R^T R = G B B^T G^T with G = U^{-T},
+ *   G G^T = Psin^{-1}, so Sigma ~ IW(Psin, nun) -- and R, upper with a positive diagonal, IS the Cholesky
+ *   factor of Sigma^{-1} that the fp32 contraction uses (no factorization of P afterwards);
+ *   mu = mun + U B^{-T} z / sqrt(kn) (= mun + R^{-1} z / sqrt(kn)) ~ N(mun, Sigma/kn);
+ *   Sigma = T^T T with T = B^{-1} U^T (lower);  c = -D/2 log 2pi - sum log U_aa + 1/2 sum log B_aa^2.
+ * Every output element is one k-ascending fma chain from 0 (the device's order, np8_niw.hip np8_niw_post).
  * Draws of (i, t, stream): chi^2(nun - a) from call 64 a, then normals from call NIW_NORMAL_CALL0:
  * B_ab (a > b) is normal a(a-1)/2 + b, z_j is normal D(D-1)/2 + j.  Returns -1 (nothing written) if
- * Psin is not numerically positive definite. */
+ * Psin is not numerically positive definite.  Rout (D x D row-major, or NULL): R. */
 static int niw_draw_impl(const np8o_ctx *c, uint64_t i, uint32_t t, uint32_t stream, int64_t n, const double *s1,
-                         const double *S, const double *anchor, double *mu, double *Ppk, double *Sigma, double *cc) {
+                         const double *S, const double *anchor, double *mu, double *Ppk, double *Sigma, double *cc,
+                         double *Rout) {
     const int D = c->D;
     const uint64_t seed = c->cfg.seed;
-    static _Thread_local double L[NP8O_DMAX * NP8O_DMAX], Li[NP8O_DMAX * NP8O_DMAX], B[NP8O_DMAX * NP8O_DMAX],
-        F[NP8O_DMAX * NP8O_DMAX], T[NP8O_DMAX * NP8O_DMAX], Lt[NP8O_DMAX * NP8O_DMAX];
+    static _Thread_local double L[NP8O_DMAX * NP8O_DMAX], M[NP8O_DMAX * NP8O_DMAX], B[NP8O_DMAX * NP8O_DMAX],
+        R[NP8O_DMAX * NP8O_DMAX], T[NP8O_DMAX * NP8O_DMAX], Ut[NP8O_DMAX * NP8O_DMAX];
     const double k0 = c->cfg.kappa, nd = (double)n;
     const double kn = k0 + nd, nun = c->cfg.nu + nd;
     const double kf = (k0 * nd) / kn;
@@ -1091,12 +1097,13 @@ static int niw_draw_impl(const np8o_ctx *c, uint64_t i, uint32_t t, uint32_t str
         dm[a] = xb[a] - c->cfg.mu0[a];
         mun[a] = fma(k0, c->cfg.mu0[a], nd * xb[a]) / kn;
     }
-    /* Cholesky of Psin (lower triangle of Psin formed on the fly) */
+    /* Cholesky Lr of J Psin J (element (r, j), r >= j, is Psin[D-1-r][D-1-j]; formed on the fly) */
     memset(L, 0, sizeof(double) * D * D);
     for (int j = 0; j < D; ++j) {
         for (int r = j; r < D; ++r) {
-            const double sc = (n > 0) ? S[packed_ix(D, j, r)] - (s1[r] * s1[j]) / nd : 0.0;
-            double v = fma(kf, dm[r] * dm[j], c->cfg.Lambda[r * D + j] + sc);
+            const int ri = D - 1 - r, ji = D - 1 - j; /* ri <= ji */
+            const double sc = (n > 0) ? S[packed_ix(D, ri, ji)] - (s1[ri] * s1[ji]) / nd : 0.0;
+            double v = fma(kf, dm[ri] * dm[ji], c->cfg.Lambda[ri * D + ji] + sc);
             for (int k = 0; k < j; ++k) v = fma(-L[r * D + k], L[j * D + k], v);
             if (r == j) {
                 if (!(v > 0.0)) return -1;
@@ -1106,14 +1113,14 @@ static int niw_draw_impl(const np8o_ctx *c, uint64_t i, uint32_t t, uint32_t str
             }
         }
     }
-    /* Li = Ln^{-1} (lower), forward substitution per column */
-    memset(Li, 0, sizeof(double) * D * D);
+    /* M = Lr^{-1} (lower), forward substitution per column; U^{-1} = J M J */
+    memset(M, 0, sizeof(double) * D * D);
     for (int j = 0; j < D; ++j) {
-        Li[j * D + j] = 1.0 / L[j * D + j];
+        M[j * D + j] = 1.0 / L[j * D + j];
         for (int r = j + 1; r < D; ++r) {
             double s = 0.0;
-            for (int k = j; k < r; ++k) s = fma(-L[r * D + k], Li[k * D + j], s);
-            Li[r * D + j] = s / L[r * D + r];
+            for (int k = j; k < r; ++k) s = fma(-L[r * D + k], M[k * D + j], s);
+            M[r * D + j] = s / L[r * D + r];
         }
     }
     memset(B, 0, sizeof(double) * D * D);
@@ -1128,18 +1135,24 @@ static int niw_draw_impl(const np8o_ctx *c, uint64_t i, uint32_t t, uint32_t str
             B[a * D + b] = normal_at(seed, i, t, stream, NIW_NORMAL_CALL0, (uint32_t)(a * (a - 1) / 2 + b));
     double z[NP8O_DMAX];
     for (int j = 0; j < D; ++j) z[j] = normal_at(seed, i, t, stream, NIW_NORMAL_CALL0, (uint32_t)(D * (D - 1) / 2 + j));
-    /* F = Li^T B */
+    /* R = B^T U^{-1}: R_ab = sum_{k = a..b} B_ka M[D-1-k][D-1-b] (a <= b) */
+    memset(R, 0, sizeof(double) * D * D);
     for (int a = 0; a < D; ++a)
-        for (int b = 0; b < D; ++b) {
+        for (int b = a; b < D; ++b) {
             double s = 0.0;
-            for (int k = (a > b ? a : b); k < D; ++k) s = fma(Li[k * D + a], B[k * D + b], s);
-            F[a * D + b] = s;
+            for (int k = a; k <= b; ++k) s = fma(B[k * D + a], M[(D - 1 - k) * D + (D - 1 - b)], s);
+            R[a * D + b] = s;
         }
-    niw_outputs_from_F(D, F, Ppk);
-    /* mu = mun + Ln B^{-T} z rskn */
+    /* P' = packed sym(R^T R), off-diagonals doubled: element (a, b), a <= b = sum_{k <= a} R_ka R_kb */
+    for (int a = 0; a < D; ++a)
+        for (int b = a; b < D; ++b) {
+            double s = 0.0;
+            for (int k = 0; k <= a; ++k) s = fma(R[k * D + a], R[k * D + b], s);
+            Ppk[packed_ix(D, a, b)] = (a == b) ? s : 2.0 * s;
+        }
+    /* mu = mun + U y, y = B^{-T} z / sqrt(kn): back substitution by columns, y_k = acc_k / B_kk for k = D-1, ..., 0,
+     * each leaving fma(-B_ka, y_k, acc_a) in the sums of a < k (the device runs it on one wave, np8_niw.hip) */
     const double rskn = 1.0 / sqrt(kn);
-    /* back substitution by columns: y_k = acc_k / B_kk for k = D-1, ..., 0, each leaving fma(-B_ka, y_k, acc_a)
-     * in the sums of a < k (acc_a from z_a rskn; the device runs it on one wave, np8_niw.hip) */
     double y[NP8O_DMAX], acc[NP8O_DMAX];
     for (int a = 0; a < D; ++a) acc[a] = z[a] * rskn;
     for (int k = D - 1; k >= 0; --k) {
@@ -1147,18 +1160,28 @@ static int niw_draw_impl(const np8o_ctx *c, uint64_t i, uint32_t t, uint32_t str
         for (int a = 0; a < k; ++a) acc[a] = fma(-B[k * D + a], y[k], acc[a]);
     }
     for (int a = 0; a < D; ++a) {
-        double s = 0.0;
-        for (int k = 0; k <= a; ++k) s = fma(L[a * D + k], y[k], s);
+        double s = 0.0; /* U_ak = Lr[D-1-a][D-1-k], k >= a */
+        for (int k = a; k < D; ++k) s = fma(L[(D - 1 - a) * D + (D - 1 - k)], y[k], s);
         mu[a] = mun[a] + s;
     }
-    /* Sigma = T^T T, T = B^{-1} Ln^T */
+    /* Sigma = T^T T, T = B^{-1} U^T (U^T_aj = Lr[D-1-j][D-1-a], lower) */
     for (int a = 0; a < D; ++a)
-        for (int b = 0; b < D; ++b) Lt[a * D + b] = L[b * D + a];
-    niw_sigma(D, B, Lt, T, Sigma);
+        for (int b = 0; b < D; ++b) Ut[a * D + b] = (b <= a) ? L[(D - 1 - b) * D + (D - 1 - a)] : 0.0;
+    niw_sigma(D, B, Ut, T, Sigma);
     double sl = 0.0;
     for (int a = 0; a < D; ++a) sl += np8o_log_pos(L[a * D + a]);
     *cc = fma(0.5, la.sumlog, fma(-0.5 * (double)D, LOG2PI, -sl));
+    if (Rout) memcpy(Rout, R, sizeof(double) * D * D);
     return 0;
+}
+
+/* The fp32 contraction rows of slot s from its factor R (R^T R = P): A = fp32(R) (transposed store), muf = fp32(mu). */
+static void wide_rows_from_r(np8o_ctx *c, int s, const double *R) {
+    const int D = c->D;
+    float *At = c->wA + (size_t)s * D * D; /* transposed: At[b][a] = fp32(R[a][b]) */
+    for (int a = 0; a < D; ++a)
+        for (int b = 0; b < D; ++b) At[b * D + a] = (b >= a) ? (float)R[a * D + b] : 0.0f;
+    for (int a = 0; a < D; ++a) c->wmu[(size_t)s * D + a] = (float)c->slot_mu[(size_t)s * D + a];
 }
 
 /* Candidate table: live slots in ascending order, log n_k, log(n_k - 1) (weight 0 as the finite
@@ -1195,10 +1218,7 @@ static void wide_factor(np8o_ctx *c, int s) {
             R[j * D + i] = w / R[j * D + j];
         }
     }
-    float *At = c->wA + (size_t)s * D * D; /* transposed: At[b][a] = fp32(R[a][b]) */
-    for (int a = 0; a < D; ++a)
-        for (int b = 0; b < D; ++b) At[b * D + a] = (float)R[a * D + b];
-    for (int a = 0; a < D; ++a) c->wmu[(size_t)s * D + a] = (float)c->slot_mu[(size_t)s * D + a];
+    wide_rows_from_r(c, s, R);
 }
 
 /* q of item x (fp32 values) for candidate slot sj (np8_oracle.h NP8O_CONTRACT_F32):
@@ -1302,11 +1322,15 @@ int np8o_init_random(np8o_ctx *c, int32_t K_init) {
         if (cntk[k] > 0) {
             remap[k] = s;
             if (c->wdirty) c->wdirty[s] = 1;
-            if (niw) /* G0 draw k: the NIW posterior of no items, stream INIT_THETA (i = k) */
-                niw_draw_impl(c, (uint64_t)k, 0xFFFFFFFFu, NP8O_STREAM_INIT_THETA, 0, NULL, NULL, NULL,
-                              c->slot_mu + (size_t)s * D, c->slot_P + (size_t)s * c->DP,
-                              c->slot_sigma + (size_t)s * D * D, c->slot_c + s);
-            else
+            if (niw) { /* G0 draw k: the NIW posterior of no items, stream INIT_THETA (i = k) */
+                static _Thread_local double Rk[NP8O_DMAX * NP8O_DMAX];
+                if (niw_draw_impl(c, (uint64_t)k, 0xFFFFFFFFu, NP8O_STREAM_INIT_THETA, 0, NULL, NULL, NULL,
+                                  c->slot_mu + (size_t)s * D, c->slot_P + (size_t)s * c->DP,
+                                  c->slot_sigma + (size_t)s * D * D, c->slot_c + s, Rk) == 0 && c->wdirty) {
+                    wide_rows_from_r(c, s, Rk); /* the draw's own factor */
+                    c->wdirty[s] = 0;
+                }
+            } else
                 slot_from_aux(c, s, vv[k], mu + (size_t)k * D);
             c->cnt[s] = cntk[k];
             ++s;
@@ -1686,10 +1710,14 @@ static int64_t niw_param_update(np8o_ctx *c, const double *stats) {
         if (n <= 0) continue;
         memcpy(anchor, c->slot_mu + (size_t)s * D, sizeof(double) * D);
         const double *s1 = stats + (size_t)s * W;
+        static _Thread_local double Rs[NP8O_DMAX * NP8O_DMAX];
         if (niw_draw_impl(c, (uint64_t)s, c->t, NP8O_STREAM_PARAM, n, s1, s1 + D, anchor, c->slot_mu + (size_t)s * D,
-                          c->slot_P + (size_t)s * c->DP, c->slot_sigma + (size_t)s * D * D, c->slot_c + s) == 0) {
+                          c->slot_P + (size_t)s * c->DP, c->slot_sigma + (size_t)s * D * D, c->slot_c + s, Rs) == 0) {
             ++updated;
-            if (c->wdirty) c->wdirty[s] = 1;
+            if (c->wdirty) {
+                wide_rows_from_r(c, s, Rs); /* the draw's own factor */
+                c->wdirty[s] = 0;
+            }
         }
     }
     rebuild_dense(c);
@@ -1701,7 +1729,7 @@ int np8o_niw_draw(np8o_ctx *c, uint64_t i, uint32_t t, uint32_t stream, int64_t 
     if (c->cfg.prior != NP8O_PRIOR_NIW) return -1;
     static double P[NP8O_DMAX * (NP8O_DMAX + 1) / 2];
     double cc;
-    return niw_draw_impl(c, i, t, stream, n, stats, stats ? stats + c->D : NULL, anchor, mu, P, Sigma, &cc);
+    return niw_draw_impl(c, i, t, stream, n, stats, stats ? stats + c->D : NULL, anchor, mu, P, Sigma, &cc, NULL);
 }
 
 int64_t np8o_param_update(np8o_ctx *c, const double *stats) {
