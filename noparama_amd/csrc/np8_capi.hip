@@ -861,6 +861,7 @@ int launch_prune(np8_ctx *c, bool last);
 
 SnapArgs snap_args(np8_ctx *c) {
     SnapArgs S;
+    S.ctl = c->ctl;
     S.L = &c->ctl->L;
     S.best = c->ctl->best;
     S.have_best = &c->ctl->have_best;
@@ -881,12 +882,20 @@ SnapArgs snap_args(np8_ctx *c) {
 
 // A snapshot the folded check may have left for the next np8_assign_fast: copied now, before anything else reads
 // or changes the labelling (every entry point but the data-parallel sweep's own continuation).
-int flush_snapshot(np8_ctx *c) {
-    if (!c->snap_lazy) return NP8_OK;
-    c->snap_lazy = false;
-    HIPC(c, np8_launch_snapshot_flush(snap_args(c), c->ctl, c->stream));
-    HIPC(c, hipMemsetAsync(&c->ctl->snap_pend, 0, sizeof(int32_t), c->stream));
+// z_best in item order (np8_assign_fast copies it in label-sorted position order; the layout's ids map it back)
+int best_item_order(np8_ctx *c) {
+    if (!c->z_best || !c->zs[1] || !c->ids[0] || c->n_loc <= 0) return NP8_OK;
+    HIPC(c, np8_launch_best_unsort(c->ctl, c->ids[0], c->z_best, c->zs[1], c->n_loc, c->stream));
     return NP8_OK;
+}
+
+int flush_snapshot(np8_ctx *c) {
+    if (c->snap_lazy) {
+        c->snap_lazy = false;
+        HIPC(c, np8_launch_snapshot_flush(snap_args(c), c->ctl, c->stream));
+        HIPC(c, hipMemsetAsync(&c->ctl->snap_pend, 0, sizeof(int32_t), c->stream));
+    }
+    return best_item_order(c);  // (every reader of z_best comes through here)
 }
 
 // prune: -1 none; 0 / 1 the candidate lists right after finalize, in the same launch (np8_step_tail), as
@@ -1066,6 +1075,8 @@ int launch_resort(np8_ctx *c, bool stale) {
     S.offset = c->offset;
     S.seed = c->seed;
     S.force = stale ? 1 : 0;  // otherwise the device re-sorts only if > n/32 items moved
+    int r = best_item_order(c);  // (a snapshot in position order needs the ids it was taken under)
+    if (r) return r;
     HIPC(c, np8_launch_resort(S, c->stream));
     c->sorted_valid = true;
     return NP8_OK;

@@ -403,6 +403,32 @@ NP8_HD void niw_aux_core(uint64_t seed, uint64_t i, uint32_t t, int m, int D, do
 NP8_HD double niw_aux_ll_screened(uint64_t seed, uint64_t i, uint32_t t, int m, int D, double nu0, double nd,
                                   double rsk, double caux, double smax, double thr);
 
+// Level 0 of the NIW auxiliary screen: true when niw_aux_ll_screened would return kZeroLogWeight for EVERY auxiliary
+// of an item at distance nd, whatever its draws -- its level-1 bound ub = caux + (log g0 + smax)/2 - e^2/2,
+// e = nd sqrt(g0) - z1 rsk, maximised over all draws the generators can return: |z1| <= zm = sqrt(-2 log 2^-33)
+// (Box-Muller over 32-bit uniforms) and g0 = 2 d v, v = (1 + cc x)^3 with |x| <= zm (Marsaglia-Tsang, d = nu0/2 - 1/3,
+// cc = 1/sqrt(9 d); the 4096-failure fallback 2 d lies inside).  With s = sqrt(g0), r = rsk zm:
+// log s - (nd s - r)_+^2 / 2 increases up to s* = (r + sqrt(r^2 + 4)) / (2 nd) and decreases after, so its maximum over
+// [sqrt(gmin), sqrt(gmax)] is at s* clamped.  The level-1 test's margins (1e-9 |magnitude| + 1e-6) are covered with
+// room: the quadratic is taken at (1 - 1e-9) and 1e-9 of every bounded magnitude is added.  Saves the 3 x (two
+// Philox calls, a Marsaglia-Tsang attempt, Box-Muller, a log) of items far from mu0 in the prior's metric.
+NP8_HD bool niw_aux_all_below(double nd, double nu0, double rsk, double caux, double smax, double thr) {
+    constexpr double zm = 6.7638;  // > sqrt(66 ln 2) = 6.76375...
+    const double d = 0.5 * nu0 - 1.0 / 3.0, cc = 1.0 / sqrt(9.0 * d);
+    const double vlo = fmax(fma(-cc, zm, 1.0), 0.0), vhi = fma(cc, zm, 1.0);
+    const double gmin = 2.0 * d * (vlo * vlo * vlo) * (1.0 - 1e-9), gmax = 2.0 * d * (vhi * vhi * vhi) * (1.0 + 1e-9);
+    const double s0 = sqrt(gmin), s1 = sqrt(gmax), r = rsk * zm * (1.0 + 1e-12);
+    const double ss = (nd > 0.0) ? (r + sqrt(fma(r, r, 4.0))) / (2.0 * nd) : s1;
+    const double sc = fmin(fmax(ss, s0), s1);
+    if (!(sc > 0.0)) return false;
+    const double e = fmax(fma(nd, sc, -r), 0.0);
+    const double h = fma(-0.5 * (1.0 - 1e-9), e * e, log_pos(sc) + 1e-12);
+    const double ub0 = fma(0.5, smax, caux) + h;
+    const double lmag = fmax(fabs(log_pos(fmax(gmin, 1e-300))), fabs(log_pos(gmax)));
+    const double margin = 1e-9 * (fabs(caux) + 0.5 * (lmag + fabs(smax)) + fabs(ub0) + fabs(thr)) + 2e-6;
+    return ub0 + margin <= thr;
+}
+
 // ll = caux + sumlog/2 - q/2, q = (|dt| b00 - z1/sqrt(kappa0))^2 + chi/kappa0 (nd = |dt|).
 NP8_HD double niw_aux_loglik(double nd, double sumlog, double b00, double chi, double z1, double rsk, double caux) {
     const double e = fma(-z1, rsk, nd * b00);

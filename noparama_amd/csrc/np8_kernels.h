@@ -20,7 +20,7 @@ struct Ctl {
     double L_local;     // this rank's part
     double best[2];     // best L, double-buffered by check parity
     int64_t moved;      // items that changed cluster since the last re-sort (local)
-    int32_t cur_unused; // (was: which label-sorted buffer is current; the layout is always buffer 0 now)
+    int32_t best_sorted; // z_best holds the snapshot in label-sorted position order (np8_assign_fast's lazy copy)
     int32_t do_sort;    // this re-sort pass runs (decided by np8_sort_scan)
     uint32_t done_blocks;
     uint32_t tail_done;   // np8_step_tail: workgroups finished (the last one runs the serial part, resets it)
@@ -506,6 +506,7 @@ struct ParamArgs {
 constexpr int kSuffRuns = 4;  // run records per wave of np8_suffstats_wide
 
 struct SnapArgs {
+    Ctl *ctl;  // best_sorted: cleared by the item-order copies
     const double *L;
     double *best;
     int32_t *have_best;
@@ -590,6 +591,10 @@ hipError_t np8_launch_step_tail(const np8::AssignArgs &A, const np8::FinArgs &F,
                                 const np8::TailArgs &T, int64_t n_waves, int D, int M, hipStream_t s);
 hipError_t np8_launch_req_select(const unsigned char *stage, int64_t stage_cap, unsigned char *rec, int64_t rec_cap,
                                  int kcap, int D, int req_max, const np8::Fx *llpart, int64_t ll_n, hipStream_t s);
+// z_best back to item order if np8_assign_fast left it in label-sorted position order (ctl->best_sorted): through
+// scratch (n ints) with the current layout's ids; a no-op otherwise.  Before every re-sort and every read of z_best.
+hipError_t np8_launch_best_unsort(np8::Ctl *ctl, const int32_t *ids, int32_t *z_best, int32_t *scratch, int64_t n,
+                                  hipStream_t s);
 // A snapshot the folded max-likelihood check left pending (ctl->snap_pend): copy it now and clear the flag.
 hipError_t np8_launch_snapshot_flush(const np8::SnapArgs &A, np8::Ctl *ctl, hipStream_t s);
 hipError_t np8_launch_loglik(const np8::LoglikArgs &A, int D, hipStream_t s);

@@ -694,8 +694,12 @@ __global__ __launch_bounds__(NP8_ASSIGN_BLOCK) __attribute__((amdgpu_waves_per_e
     const int K = A.ctl->K;
     const int lists_ok = A.ctl->lists_ok;  // (the same round of scalar loads)
     // a max-likelihood snapshot the last check left pending: the labelling before this step is the one it keeps
+    // (copied in position order -- coalesced; np8_best_unsort puts it in item order before a re-sort or a read)
     const int snap = (!LL && A.snap_on) ? A.ctl->snap_pend : 0;
-    if (snap) A.z_best[il] = zi;
+    if (snap) {
+        A.z_best[p] = zi;
+        if (p == A.p0) A.ctl->best_sorted = 1;
+    }
     NP8_CLK(1);
     bool defer = COUNT;  // counting runs: every lane takes np8_assign's counting instance
     PickState st;
@@ -2106,6 +2110,7 @@ __global__ __launch_bounds__(256) void np8_snapshot(SnapArgs A) {
         if (better) *A.have_best = 1;
     }
     if (!better) return;
+    if (blockIdx.x == 0 && threadIdx.x == 0) A.ctl->best_sorted = 0;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < A.n_loc; i += stride)
         A.z_best[i] = A.z[i];
@@ -2121,6 +2126,7 @@ __global__ __launch_bounds__(256) void np8_snapshot(SnapArgs A) {
 __global__ __launch_bounds__(256) void np8_snapshot_flush(SnapArgs A, const Ctl *__restrict__ ctl) {
     if (!ctl->snap_pend) return;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x, g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g == 0) A.ctl->best_sorted = 0;
     for (int64_t i = g; i < A.n_loc; i += stride) A.z_best[i] = A.z[i];
     for (int64_t k = g; k < A.kcap; k += stride) A.cnt_best[k] = A.cnt[k];
     const int64_t nm = (int64_t)A.kcap * A.D, ns = (int64_t)A.kcap * A.D * A.D;
@@ -2844,6 +2850,33 @@ hipError_t np8_launch_snapshot_flush(const SnapArgs &A, Ctl *ctl, hipStream_t s)
     if (nb < 1) nb = 1;
     hipLaunchKernelGGL(np8_snapshot_flush, dim3((unsigned)nb), dim3(256), 0, s, A, ctl);
     return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void np8_best_copy(const Ctl *__restrict__ ctl, const int32_t *__restrict__ src,
+                                                     int32_t *__restrict__ dst, int64_t n) {
+    if (!ctl->best_sorted) return;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        dst[i] = src[i];
+}
+
+__global__ __launch_bounds__(256) void np8_best_scatter(const Ctl *__restrict__ ctl, const int32_t *__restrict__ ids,
+                                                        const int32_t *__restrict__ src, int32_t *__restrict__ dst,
+                                                        int64_t n) {
+    if (!ctl->best_sorted) return;
+    for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (int64_t)gridDim.x * blockDim.x)
+        dst[ids[p]] = src[p];
+}
+
+hipError_t np8_launch_best_unsort(Ctl *ctl, const int32_t *ids, int32_t *z_best, int32_t *scratch, int64_t n,
+                                  hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    int64_t nb = (n + 255) / 256;
+    if (nb > 2048) nb = 2048;
+    hipLaunchKernelGGL(np8_best_copy, dim3((unsigned)nb), dim3(256), 0, s, ctl, z_best, scratch, n);
+    hipLaunchKernelGGL(np8_best_scatter, dim3((unsigned)nb), dim3(256), 0, s, ctl, ids, scratch, z_best, n);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    return hipMemsetAsync(&ctl->best_sorted, 0, sizeof(int32_t), s);
 }
 
 hipError_t np8_launch_snapshot(const SnapArgs &A, hipStream_t s) {

@@ -511,8 +511,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NP8_WIDE_WA
     double lwa[M];
     {
         const double logam = hyp[D + W::DP + 2];
+        bool all_below = false;  // (level 0: no auxiliary of this item can reach the skip threshold, whatever its draws)
+        if constexpr (PRIOR == kPriorNiw)
+            all_below = niw_aux_all_below(ny, hyp[D + W::DP + 3], hyp[D + W::DP + 1], hyp[D + W::DP],
+                                          hyp[D + W::DP + 4 + W::DP], st.T - kSkip - logam);
+#pragma unroll
+        for (int k = 0; k < M; ++k) lwa[k] = kZeroLogWeight + logam;
 #pragma unroll 1
-        for (int m = 0; m < M; ++m) {
+        for (int m = 0; m < (all_below ? 0 : M); ++m) {
             double v;
             if constexpr (PRIOR == kPriorNiw) {
                 const double caux = hyp[D + W::DP], rsk = hyp[D + W::DP + 1], nu = hyp[D + W::DP + 3];
