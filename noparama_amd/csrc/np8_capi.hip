@@ -121,6 +121,11 @@ struct np8_ctx {
     uint32_t fin_advance = 0;    // the next finalize advances ctl->t_base (a captured graph's last step)
     bool fin_advanced = false;
     bool capture_sort_outside = false;  // the graph being captured leaves the re-sort to np8_sweep (and mirrors moved)
+    // churn: many items move per sweep (the mixed regime after a cold start; the moved mirror, with hysteresis):
+    // sweeps keep the in-graph re-sort every resort_every-th sweep and the parallel np8_prune instead of the
+    // conditional one-workgroup lists -- both are the better choice only while few items move (round-4 A/B: mixed
+    // sweep 0.164 vs 0.176 ms with the conditional lists; warm sweep 39.8 vs 41.5 µs the other way round)
+    bool churn = false, graph_churn = false;
     bool graph_sort_outside = false;    // ... the graph in hand does
 
     // data-parallel sweep in `substeps` synchronous sub-steps (np8_config.substeps): sub-step s is the
@@ -722,7 +727,8 @@ FinArgs fin_args(np8_ctx *c, const unsigned char *recs, int world) {
     F.best = c->ctl->best;
     F.have_best = &c->ctl->have_best;
     F.lb = c->lb;
-    F.moved_mirror = (c->fin_advance && c->capture_sort_outside) ? c->moved_dev : nullptr;
+    // (np8_sweep's re-sort and churn decisions read it: a replay's last finalize, and eager steps)
+    F.moved_mirror = (c->fin_advance || !c->capturing) ? c->moved_dev : nullptr;
     F.advance = c->fin_advance;
     if (c->fin_advance) c->fin_advanced = true;
     c->fin_advance = 0;
@@ -911,8 +917,8 @@ int launch_finalize(np8_ctx *c, const unsigned char *recs, int world, int prune 
     // the conditional form (the default): the lists of the last build stay when finalize finds every count within
     // kListSlack of it -- the frozen reference-prior sweep's step with valid lists; a rebuild then costs the one
     // workgroup what np8_prune does in parallel, so steps after which the lists are stale anyway keep np8_prune
-    const bool cond = !c->tailcond_off && prune >= 0 && !c->gather && !c->wide && c->prior == NP8_PRIOR_REFERENCE &&
-                      c->param_update == NP8_PARAM_FROZEN && c->lists_valid;
+    const bool cond = !c->tailcond_off && !c->churn && prune >= 0 && !c->gather && !c->wide &&
+                      c->prior == NP8_PRIOR_REFERENCE && c->param_update == NP8_PARAM_FROZEN && c->lists_valid;
     const bool tail = cond || (!c->fuse_off && prune >= 0 && !c->gather && !c->wide && c->prior == NP8_PRIOR_REFERENCE);
     if (tail) {  // finalize (+ lists) in one launch
         TailArgs T;
@@ -1411,7 +1417,8 @@ int capture_graph(np8_ctx *c) {
                          c->prior == NP8_PRIOR_REFERENCE;
     c->fin_advanced = false;
     // the re-sort check leaves the graph when its last finalize mirrors ctl->moved for the host (np8_sweep)
-    c->capture_sort_outside = adv_fin && !c->sort_in_graph && c->moved_dev != nullptr;
+    c->capture_sort_outside = adv_fin && !c->sort_in_graph && !c->churn && c->moved_dev != nullptr;
+    c->graph_churn = c->churn;
     for (uint32_t i = 0; i < kGraphSweeps && !r; ++i) {
         if (adv_fin && i + 1 == kGraphSweeps) c->fin_advance = kGraphSweeps;
         r = population(c);
@@ -1454,7 +1461,7 @@ int capture_graph(np8_ctx *c) {
 // phase, check parity or timing setting).
 int ensure_graph(np8_ctx *c) {
     if (!c->graph || c->graph_par != (c->checks & 1) || c->graph_phase != (int)(c->epoch % kGraphSweeps) ||
-        c->graph_snap0 != c->snap_lazy ||
+        c->graph_snap0 != c->snap_lazy || c->graph_churn != c->churn ||
         c->graph_timing != ((c->timing ? 1 : 0) | (c->count_eval ? 2 : 0) | (c->time_all ? 4 : 0)))
         return capture_graph(c);
     return NP8_OK;
@@ -1902,6 +1909,10 @@ int np8_sweep(np8_ctx *c, int32_t n_sweeps) {
     const bool sync = chunk >= N;
     if (!sync && c->world > 1) return fail(c, NP8_ERR_ARG, "np8_sweep: chunk < N is single-rank only");
     for (int s = 0; s < n_sweeps; ++s) {
+        if (c->moved_host) {  // churn (moved since the last re-sort, as of the last finalize): enter > n/8, leave < n/64
+            const int64_t mv = *(volatile int64_t *)c->moved_host;
+            c->churn = c->churn ? (mv * 64 >= c->n_loc) : (mv * 8 > c->n_loc);
+        }
         if (graph_eligible(c, sync) && (uint32_t)(n_sweeps - s) >= kGraphSweeps) {
             int r = ensure_graph(c);
             if (r) return r;
