@@ -1001,13 +1001,17 @@ __global__ __launch_bounds__(NP8_ASSIGN_BLOCK) __attribute__((amdgpu_waves_per_e
     if (req) {  // np8_assign's request with its payload, the auxiliary's (v, mu)
         const int q = qreq;
         if (q < A.req_cap) {  // always: the area holds every item of the step
+            // the item key and epoch read again here (volatile: not kept live from the top of the kernel -- they
+            // were spilled to scratch on every lane, 16 MB of writes per C3 launch, for this rare path)
+            const uint64_t igr = (uint64_t)(A.offset + reinterpret_cast<const volatile int32_t *>(ids)[p]);
+            const uint32_t tr = reinterpret_cast<const volatile Ctl *>(A.ctl)->t_base + A.t;
             double *vm = A.vmu + (int64_t)q * (D + 1);
             double y0[D];
             whiten<D>(hyp, x, y0);
-            aux_params<D>(hyp, y0, ny, A.seed, ig, t, st.pick - K, vm);
+            aux_params<D>(hyp, y0, ny, A.seed, igr, tr, st.pick - K, vm);
             Request r;
-            r.pos = (int64_t)ig;  // synchronous sweep: scan position = item index
-            r.i = (int64_t)ig;
+            r.pos = (int64_t)igr;  // synchronous sweep: scan position = item index
+            r.i = (int64_t)igr;
             r.m = st.pick - K;
             r.zold = zi;
             r.lpos = (int32_t)p;
