@@ -284,10 +284,11 @@ __device__ __forceinline__ void forward_panel(double *X, const double *G, int LD
 __device__ __forceinline__ void forward_trailing(double *X, const double *G, int LD, int D, int c0, bool inv,
                                                  bool lower = false) {
     const int rows = D - (c0 + kPanelN);
-    for (int e = threadIdx.x; e < rows * D; e += blockDim.x) {
-        const int r = c0 + kPanelN + e / D, j = e - (e / D) * D;
-        if (inv && j > c0 + kPanelN - 1) continue;  // (columns right of the panel get nothing from it)
-        if (lower && j > r) continue;
+    // inv / lower: the columns right of the panel get nothing from it (X_kj = 0 for j > k, every panel row k < j), so
+    // only columns 0 .. c0 + 15 are visited -- a quarter of the row's elements at the first panel
+    const int W = (inv || lower) ? c0 + kPanelN : D;
+    for (int e = threadIdx.x; e < rows * W; e += blockDim.x) {
+        const int r = c0 + kPanelN + e / W, j = e - (e / W) * W;
         double acc = X[r * LD + j];
 #pragma unroll
         for (int i = 0; i < kPanelN; ++i) {
@@ -478,13 +479,26 @@ __global__ __launch_bounds__(kNiwThreads) void np8_niw_post(NiwArgs A) {
         gv[a] = g;
         B[a * LD + a] = sqrt(g);
     }
-    for (int e = tid; e < D * (D - 1) / 2; e += blockDim.x) {
-        int a, b;
-        lower_index(e, a, b);
-        B[a * LD + b] = normal_at(A.seed, i, t, stream, kNiwNormalCall0, (uint32_t)e);
+    // the normals by Philox call: one Box-Muller quad per call gives normals 4q .. 4q + 3 (normal_at's layout), so
+    // each call is made once, not once per normal -- B's off-diagonals first, then z
+    {
+        const int nb = D * (D - 1) / 2, nn = nb + D;
+        for (int qd = tid; 4 * qd < nn; qd += blockDim.x) {
+            double g[4];
+            normal_quad(A.seed, i, t, stream, kNiwNormalCall0 + (uint32_t)qd, g);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int e = 4 * qd + k;
+                if (e < nb) {
+                    int a, b;
+                    lower_index(e, a, b);
+                    B[a * LD + b] = g[k];
+                } else if (e < nn) {
+                    z[e - nb] = g[k];
+                }
+            }
+        }
     }
-    for (int j = tid; j < D; j += blockDim.x)
-        z[j] = normal_at(A.seed, i, t, stream, kNiwNormalCall0, (uint32_t)(D * (D - 1) / 2 + j));
     __syncthreads();
     NIW_T(1)
     const int wv = tid >> 6;
