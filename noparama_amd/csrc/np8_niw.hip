@@ -627,11 +627,25 @@ __global__ __launch_bounds__(kNiwThreads) void np8_niw_post(NiwArgs A) {
         __syncthreads();
         sym_square(D, LD, B, Li);  // ^4
         __syncthreads();
+#ifdef NP8_EXP_SIGMA4
+        const double m = max_abs_row_sum(D, LD, Li, rs);
+        if (tid == 0) {
+            const double lmax = g * sqrt(sqrt(m));
+#elif defined(NP8_EXP_SIGMA16)
+        sym_square(D, LD, Li, L);  // ^8
+        __syncthreads();
+        sym_square(D, LD, L, B);   // ^16
+        __syncthreads();
+        const double m = max_abs_row_sum(D, LD, B, rs);
+        if (tid == 0) {
+            const double lmax = g * sqrt(sqrt(sqrt(sqrt(m))));
+#else
         sym_square(D, LD, Li, L);  // ^8
         __syncthreads();
         const double m = max_abs_row_sum(D, LD, L, rs);
         if (tid == 0) {
             const double lmax = g * sqrt(sqrt(sqrt(m)));
+#endif
             A.lam_lo[s] = (lmax > 0.0 && lmax < 1e300) ? 0.99 / lmax : 0.0;
         }
     }
