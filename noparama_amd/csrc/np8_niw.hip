@@ -208,6 +208,14 @@ __device__ __forceinline__ double write_pprime_r(int D, int LD, const double *R,
 
 constexpr int kPanelN = 16;
 
+// Squarings of Sigma / ||Sigma|| behind the wide path's eigenvalue bound (np8_niw_post): lambda_max <= g ||.^(2^k)||^(2^-k).
+// A/B at C5 niw_conjugate, one box: k = 2: 1 157 sweeps/s, 3: 1 283, 4: 1 338 (each squaring ~10 us of np8_niw_post, a
+// tighter bound fewer screen batches in np8_assign_wide).
+#ifndef NP8_BOUND_SQUARINGS
+#define NP8_BOUND_SQUARINGS 4
+#endif
+constexpr int kBoundSquarings = NP8_BOUND_SQUARINGS;
+
 // Panel of 16 columns c0 .. c0 + 15 of the lower Cholesky factor of the symmetric matrix in L's lower triangle, on
 // one wave (lane = row r, its 16 panel entries in registers): per column j the pivot, the scaled column, and the
 // updates of the panel's later columns -- element (r, c) receives fma(-L_rj, L_cj, .) for j ascending, then the
@@ -612,10 +620,11 @@ __global__ __launch_bounds__(kNiwThreads) void np8_niw_post(NiwArgs A) {
                         A.wmu + (int64_t)s * D);
     }
     if (bound) {
-        // lambda_min(P) = 1 / lambda_max(Sigma), lambda_max(Sigma) = rho(Sigma) <= ||Sigma^8||^(1/8) (any consistent
-        // norm; max |row sum| here) -- within a few % of lambda_max where the Gershgorin bound ||Sigma|| can be 40%
-        // above it.  Sigma is scaled by g = ||Sigma|| first (entries of (Sigma/g)^8 stay in [0, 1], no overflow,
-        // and ||(Sigma/g)^8|| >= D^-4: no underflow); 1% for the fp32 factor, the fp32 contraction and the rounding.
+        // lambda_min(P) = 1 / lambda_max(Sigma), lambda_max(Sigma) = rho(Sigma) <= ||Sigma^n||^(1/n), n = 2^k (any
+        // consistent norm; max |row sum| here) -- within a few % of lambda_max where the Gershgorin bound ||Sigma||
+        // can be 40% above it.  Sigma is scaled by g = ||Sigma|| first (entries of (Sigma/g)^n stay in [0, 1], no
+        // overflow, and ||(Sigma/g)^n|| >= D^(-n/2) >= 8^-32 at D = 64, k <= 5: no underflow); 1% for the fp32
+        // factor, the fp32 contraction and the rounding.
         const double g = max_abs_row_sum(D, LD, L, rs);
         const double rg = (g > 0.0) ? 1.0 / g : 0.0;
         for (int e = tid; e < D * D; e += blockDim.x) {
@@ -623,29 +632,19 @@ __global__ __launch_bounds__(kNiwThreads) void np8_niw_post(NiwArgs A) {
             L[a * LD + b] *= rg;
         }
         __syncthreads();
-        sym_square(D, LD, L, B);   // (Sigma/g)^2  (B and Li are free once R exists)
-        __syncthreads();
-        sym_square(D, LD, B, Li);  // ^4
-        __syncthreads();
-#ifdef NP8_EXP_SIGMA4
-        const double m = max_abs_row_sum(D, LD, Li, rs);
+        // kBoundSquarings squarings, (Sigma/g)^(2^k), through L -> B -> Li -> L ... (B and Li are free once R exists)
+        double *buf[3] = {L, B, Li};
+        int cur = 0;
+        for (int q = 0; q < kBoundSquarings; ++q) {
+            sym_square(D, LD, buf[cur], buf[(cur + 1) % 3]);
+            cur = (cur + 1) % 3;
+            __syncthreads();
+        }
+        const double m = max_abs_row_sum(D, LD, buf[cur], rs);
         if (tid == 0) {
-            const double lmax = g * sqrt(sqrt(m));
-#elif defined(NP8_EXP_SIGMA16)
-        sym_square(D, LD, Li, L);  // ^8
-        __syncthreads();
-        sym_square(D, LD, L, B);   // ^16
-        __syncthreads();
-        const double m = max_abs_row_sum(D, LD, B, rs);
-        if (tid == 0) {
-            const double lmax = g * sqrt(sqrt(sqrt(sqrt(m))));
-#else
-        sym_square(D, LD, Li, L);  // ^8
-        __syncthreads();
-        const double m = max_abs_row_sum(D, LD, L, rs);
-        if (tid == 0) {
-            const double lmax = g * sqrt(sqrt(sqrt(m)));
-#endif
+            double root = m;
+            for (int q = 0; q < kBoundSquarings; ++q) root = sqrt(root);
+            const double lmax = g * root;
             A.lam_lo[s] = (lmax > 0.0 && lmax < 1e300) ? 0.99 / lmax : 0.0;
         }
     }

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 4: the C5 conjugate sweep with the Sigma^16 eigenvalue bound (four squarings, experiment s4.so) against Sigma^8 (three).
+# Round 4: the C5 conjugate sweep with the eigenvalue bound with one squaring more (experiment s4.so) against Sigma^8 (three).
 set -o pipefail
 export TMPDIR=/tmp
 OUT=${OUT:-gpurun_out/r4s4}
