@@ -251,10 +251,14 @@ __device__ __forceinline__ void lower_panel_factor(double *L, int LD, int D, int
 
 // The panel's 16 updates to element (r, c), r >= c >= c0 + 16, in ascending column order; all threads.
 __device__ __forceinline__ void lower_panel_trailing(double *L, int LD, int D, int c0) {
-    const int cols = D - (c0 + kPanelN);
-    for (int e = threadIdx.x; e < cols * D; e += blockDim.x) {
-        const int c = c0 + kPanelN + e / D, r = e - (e / D) * D;
-        if (r < c) continue;
+    const int rows = D - (c0 + kPanelN);
+    if (rows <= 0) return;  // (the last panel: nothing below it)
+    // only the trailing lower triangle (r >= c >= c0 + 16): e -> (r', c') row-major, r' = floor((sqrt(8e + 1) - 1) / 2)
+    for (int e = threadIdx.x; e < rows * (rows + 1) / 2; e += blockDim.x) {
+        int rr = (int)((sqrt(8.0 * (double)e + 1.0) - 1.0) * 0.5);
+        while (rr * (rr + 1) / 2 > e) --rr;
+        while ((rr + 1) * (rr + 2) / 2 <= e) ++rr;
+        const int r = c0 + kPanelN + rr, c = c0 + kPanelN + (e - rr * (rr + 1) / 2);
         double acc = L[r * LD + c];
 #pragma unroll
         for (int j = 0; j < kPanelN; ++j) acc = fma(-L[r * LD + c0 + j], L[c * LD + c0 + j], acc);  // (c0 + 16 <= c < D)
@@ -633,14 +637,15 @@ __global__ __launch_bounds__(kNiwThreads) void np8_niw_post(NiwArgs A) {
         }
         __syncthreads();
         // kBoundSquarings squarings, (Sigma/g)^(2^k), through L -> B -> Li -> L ... (B and Li are free once R exists)
-        double *buf[3] = {L, B, Li};
-        int cur = 0;
+        // (unrolled: each buffer is a known LDS array, so the loads stay ds_read -- a runtime-indexed pointer table
+        // made them flat loads, 2x slower)
+        auto buf = [&](int k) -> double * { return k == 0 ? L : (k == 1 ? B : Li); };
+#pragma unroll
         for (int q = 0; q < kBoundSquarings; ++q) {
-            sym_square(D, LD, buf[cur], buf[(cur + 1) % 3]);
-            cur = (cur + 1) % 3;
+            sym_square(D, LD, buf(q % 3), buf((q + 1) % 3));
             __syncthreads();
         }
-        const double m = max_abs_row_sum(D, LD, buf[cur], rs);
+        const double m = max_abs_row_sum(D, LD, buf(kBoundSquarings % 3), rs);
         if (tid == 0) {
             double root = m;
             for (int q = 0; q < kBoundSquarings; ++q) root = sqrt(root);
