@@ -478,13 +478,21 @@ __global__ __launch_bounds__(kNiwThreads) void np8_niw_post(NiwArgs A) {
     // J Psin J (J the index reversal) formed in LDS's lower triangle by all threads: element (r, j), r >= j, is
     // Psin[D-1-r][D-1-j] (the statistics and Psi0 come from HBM once); the Bartlett draws (they need nothing of
     // Psin) in the same phase
-    for (int e = tid; e < D * D; e += blockDim.x) {
-        const int r = e / D, j = e - r * D;
-        if (j > r) continue;
+    auto psin = [&](int r, int j, double Srj) {  // element (r, j), r >= j
         const int ri = D - 1 - r, ji = D - 1 - j;  // ri <= ji
-        const double Srj = recs ? L[r * LD + j] : S[pix(D, ri, ji)];
         const double sc = (n > 0) ? Srj - (s1[ri] * s1[ji]) / nd : 0.0;
         L[r * LD + j] = fma(kf, dm[ri] * dm[ji], A.Psi0[ri * D + ji] + sc);
+    };
+    if (recs) {  // (two loops: the statistics' source is LDS or HBM, and a select of the two pointers is a flat load)
+        for (int e = tid; e < D * D; e += blockDim.x) {
+            const int r = e / D, j = e - r * D;
+            if (j <= r) psin(r, j, L[r * LD + j]);
+        }
+    } else {
+        for (int e = tid; e < D * D; e += blockDim.x) {
+            const int r = e / D, j = e - r * D;
+            if (j <= r) psin(r, j, S[pix(D, D - 1 - r, D - 1 - j)]);
+        }
     }
     for (int a = tid; a < D; a += blockDim.x) {  // Bartlett diagonal
         const double g = chi2_mt(A.seed, i, t, stream, kNiwGammaCalls * (uint32_t)a, nun - a);
