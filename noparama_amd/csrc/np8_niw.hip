@@ -143,11 +143,18 @@ __device__ __forceinline__ void sigma_from_t(int D, int LD, const double *T, dou
     }
 }
 
-// Y = X X (X symmetric, D a multiple of 4) in 4 x 4 register blocks per thread.
+// Y = X X (X symmetric, D a multiple of 4) in 4 x 4 register blocks per thread.  Y is symmetric too (bit for bit:
+// element (j, i) is element (i, j)'s chain with the factors of each fma swapped), so only the blocks bi <= bj are
+// computed and each is stored twice.
 __device__ __forceinline__ void sym_square(int D, int LD, const double *X, double *Y) {
     const int nb = D / 4;
-    for (int e = threadIdx.x; e < nb * nb; e += blockDim.x) {
-        const int bi = e / nb, bj = e - bi * nb;
+    for (int e = threadIdx.x; e < nb * (nb + 1) / 2; e += blockDim.x) {
+        int bi = 0, rem = e;  // (bi, bj), bi <= bj: row-major over the upper block triangle
+        while (rem >= nb - bi) {
+            rem -= nb - bi;
+            ++bi;
+        }
+        const int bj = bi + rem;
         double acc[4][4];
 #pragma unroll
         for (int i = 0; i < 4; ++i)
@@ -169,7 +176,10 @@ __device__ __forceinline__ void sym_square(int D, int LD, const double *X, doubl
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-            for (int j = 0; j < 4; ++j) Y[(4 * bi + i) * LD + 4 * bj + j] = acc[i][j];
+            for (int j = 0; j < 4; ++j) {
+                Y[(4 * bi + i) * LD + 4 * bj + j] = acc[i][j];
+                Y[(4 * bj + j) * LD + 4 * bi + i] = acc[i][j];
+            }
     }
 }
 
