@@ -183,7 +183,7 @@ NealAlgorithm8Hip::NealAlgorithm8Hip(uint64_t seed, const np8_prior &prior, int6
     cfg.prior = prior.prior;
     cfg.contraction = prior.contraction;
     cfg.substeps = prior.substeps;
-    check(np8_create(&_ctx, &cfg), "np8_create");
+    check(NP8_CREATE(&_ctx, &cfg), "np8_create_sized");
 }
 
 namespace {
@@ -320,7 +320,7 @@ void NealAlgorithm8Hip::exportState(membertrix &trix, int which) {
 
 np8_stats_t NealAlgorithm8Hip::stats() {
     np8_stats_t s{};
-    check(np8_stats(_ctx, &s), "np8_stats");
+    check(NP8_STATS(_ctx, &s), "np8_stats_sized");
     return s;
 }
 

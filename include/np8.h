@@ -17,6 +17,7 @@
 #ifndef NP8_H
 #define NP8_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -70,6 +71,16 @@ typedef struct {
 } np8_config;
 
 #define NP8_SUBSTEPS_MAX 64
+
+/* ABI growth.  np8_config and np8_stats_t only ever grow at their end, and the entry points that take them have
+ * sized forms that honour the caller's size: np8_create_sized reads the first cfg_bytes of the configuration (the
+ * fields the caller does not have take their 0 = default values) and np8_stats_sized writes exactly
+ * min(out_bytes, sizeof(np8_stats_t)) bytes, so a caller built against an older or newer header never has its
+ * memory read or written past the struct it allocated.  Use NP8_CREATE / NP8_STATS, which pass sizeof of the
+ * caller's own struct.  The unsized forms: np8_create reads sizeof(np8_config) of this header (callers built
+ * against this header only); np8_stats writes the first NP8_STATS_MIN_BYTES (the first, smallest layout ever
+ * shipped: K .. last_loglik) and nothing beyond, whatever header the caller was built with. */
+#define NP8_CONFIG_MIN_BYTES offsetof(np8_config, param_update) /* D .. device: the first released layout */
 
 /* Cluster-likelihood arithmetic (DESIGN.md "Wide path").
  * F64:      fp64 table form (packed sym(Sigma^{-1})), any D from 1 to 16 with M = 3 (the reference's), and
@@ -146,8 +157,13 @@ typedef struct {
     int64_t pick_evals;
 } np8_stats_t;
 
+#define NP8_STATS_MIN_BYTES offsetof(np8_stats_t, ms_assign) /* K .. last_loglik: the first released layout */
+
 /* Create / destroy.  Replaces NealAlgorithm8::NealAlgorithm8 (np_neal_algorithm8.cpp:17-34). */
 int np8_create(np8_ctx **out, const np8_config *cfg);
+/* np8_create reading only the first cfg_bytes of *cfg (>= NP8_CONFIG_MIN_BYTES); see "ABI growth" above */
+int np8_create_sized(np8_ctx **out, const np8_config *cfg, size_t cfg_bytes);
+#define NP8_CREATE(out, cfg) np8_create_sized((out), (cfg), sizeof *(cfg))
 int np8_destroy(np8_ctx *ctx);
 const char *np8_last_error(const np8_ctx *ctx);
 
@@ -286,7 +302,11 @@ int np8_pick_batch(np8_ctx *ctx, const double *lw, int32_t n, const double *u, i
 /* Sum over items of log p(x_i | theta_{z_i}) for the current state (MCMC::considerMaxLikelihood). */
 int np8_total_loglik(np8_ctx *ctx, double *out);
 
+/* Writes exactly min(out_bytes, sizeof(np8_stats_t)) bytes of the statistics (out_bytes >= NP8_STATS_MIN_BYTES);
+ * np8_stats writes the first NP8_STATS_MIN_BYTES only (see "ABI growth"). */
+int np8_stats_sized(np8_ctx *ctx, np8_stats_t *out, size_t out_bytes);
 int np8_stats(np8_ctx *ctx, np8_stats_t *out);
+#define NP8_STATS(ctx, out) np8_stats_sized((ctx), (out), sizeof *(out))
 /* enable = NP8_TIMING_EVENTS: device-event timing of the kernels (event pairs around each launch, or
  * around one assign launch per replayed sweep graph); NP8_TIMING_COUNTERS: the assign kernel counts the
  * quadratic forms it executes (np8_stats_t.n_quad; a few scalar loads and two atomics per wave); 0 = off.

@@ -1497,9 +1497,16 @@ int run_graph(np8_ctx *c) {
 // =====================================================================================================
 extern "C" {
 
-int np8_create(np8_ctx **out, const np8_config *cfg) {
-    if (!out || !cfg) return NP8_ERR_ARG;
+int np8_create(np8_ctx **out, const np8_config *cfg) { return np8_create_sized(out, cfg, sizeof(np8_config)); }
+
+int np8_create_sized(np8_ctx **out, const np8_config *cfg_in, size_t cfg_bytes) {
+    if (!out || !cfg_in || cfg_bytes < NP8_CONFIG_MIN_BYTES) return NP8_ERR_ARG;
     *out = nullptr;
+    // the caller's prefix only: fields it does not have keep their zero ("default") values
+    np8_config cfg_copy;
+    std::memset(&cfg_copy, 0, sizeof(cfg_copy));
+    std::memcpy(&cfg_copy, cfg_in, cfg_bytes < sizeof(cfg_copy) ? cfg_bytes : sizeof(cfg_copy));
+    const np8_config *cfg = &cfg_copy;
     np8_ctx *c = new np8_ctx();
     c->D = cfg->D;
     c->M = cfg->M;
@@ -2382,8 +2389,9 @@ int np8_total_loglik(np8_ctx *c, double *out) {
     return NP8_OK;
 }
 
-int np8_stats(np8_ctx *c, np8_stats_t *out) {
-    if (!c || !out) return NP8_ERR_ARG;
+namespace {
+// The statistics as this build lays them out; np8_stats_sized copies the caller's prefix of it.
+int fill_stats(np8_ctx *c, np8_stats_t *out) {
     Ctl h;
     int r = read_ctl(c, &h);
     if (r) return r;
@@ -2430,6 +2438,18 @@ int np8_stats(np8_ctx *c, np8_stats_t *out) {
     }
     return NP8_OK;
 }
+}  // namespace
+
+int np8_stats_sized(np8_ctx *c, np8_stats_t *out, size_t out_bytes) {
+    if (!c || !out || out_bytes < NP8_STATS_MIN_BYTES) return NP8_ERR_ARG;
+    np8_stats_t full;
+    const int r = fill_stats(c, &full);
+    if (r) return r;
+    std::memcpy(out, &full, out_bytes < sizeof(full) ? out_bytes : sizeof(full));
+    return NP8_OK;
+}
+
+int np8_stats(np8_ctx *c, np8_stats_t *out) { return np8_stats_sized(c, out, NP8_STATS_MIN_BYTES); }
 
 int np8_set_timing(np8_ctx *c, int32_t enable) {
     if (!c) return NP8_ERR_ARG;

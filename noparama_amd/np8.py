@@ -138,6 +138,7 @@ def lib():
     P = C.POINTER
     sig = {
         "np8_create": ([P(vp), P(_Config)], i32),
+        "np8_create_sized": ([P(vp), P(_Config), C.c_size_t], i32),
         "np8_destroy": ([vp], i32),
         "np8_last_error": ([vp], C.c_char_p),
         "np8_set_data": ([vp, vp, i64, i32, i64, i64], i32),
@@ -161,6 +162,7 @@ def lib():
         "np8_total_loglik": ([vp, P(d)], i32),
         "np8_pick_batch": ([vp, vp, i32, vp, i64, vp], i32),
         "np8_stats": ([vp, P(Stats)], i32),
+        "np8_stats_sized": ([vp, P(Stats), C.c_size_t], i32),
         "np8_set_timing": ([vp, i32], i32),
         "np8_set_stream": ([vp, vp], i32),
         "np8_comm_unique_id": ([vp], i32),
@@ -242,7 +244,7 @@ class NealAlgorithm8:
         cfg.substeps = int(substeps)
         self.substeps = max(int(substeps), 1)
         h = C.c_void_p()
-        r = lib().np8_create(C.byref(h), C.byref(cfg))
+        r = lib().np8_create_sized(C.byref(h), C.byref(cfg), C.sizeof(cfg))
         if r:
             raise NP8Error(r, "np8_create failed (unsupported D/M, bad base measure or no HIP device)")
         self._h = h
@@ -338,7 +340,7 @@ class NealAlgorithm8:
 
     def stats(self):
         s = Stats()
-        self._check(lib().np8_stats(self._h, C.byref(s)))
+        self._check(lib().np8_stats_sized(self._h, C.byref(s), C.sizeof(s)))
         return {f: getattr(s, f) for f, _ in Stats._fields_}
 
     @property
