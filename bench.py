@@ -94,6 +94,12 @@ def parse():
     return a
 
 
+def n_label(n):
+    """1e6 for powers of ten (BASELINE.json's spelling), the plain count otherwise (125000, not '1e5')."""
+    e = len(str(n)) - 1
+    return f"1e{e}" if n == 10 ** e else str(n)
+
+
 def workload(args):
     """Data, warm state and sampler options of the configuration."""
     from noparama_amd import datasets
@@ -203,7 +209,7 @@ def main():
         if world == 1 and args.cpu_seconds > 0:
             cpu = cpu_baseline(X, z, mu, sig, D, args.seed, args.cpu_seconds, opts)
         out = {
-            "metric": f"Gibbs sweeps/sec (Neal-8, N={(n_rank if args.weak else N):.0e} D={D})".replace("+0", ""),
+            "metric": f"Gibbs sweeps/sec (Neal-8, N={n_label(n_rank if args.weak else N)} D={D})",
             "value": args.steps / m["dt"] * (N / n_rank if args.weak else 1.0),
             "unit": "sweeps/s",
             "n_gpus": world,
@@ -513,7 +519,7 @@ def main_sm(args):
     cpu = cpu_baseline_sm(X, z, mu, sig, D, args.seed, args.cpu_seconds, tri) if args.cpu_seconds > 0 else None
     name = "triadic" if tri else "Jain-Neal"
     out = {
-        "metric": f"split-merge sweeps/sec ({name}, N={N:.0e} attempts/sweep, D={D})".replace("+0", ""),
+        "metric": f"split-merge sweeps/sec ({name}, N={n_label(N)} attempts/sweep, D={D})",
         "value": args.steps / dt,
         "unit": "sweeps/s",
         "n_gpus": 1,

@@ -2,8 +2,10 @@
 device, so what runs here is the host-exchange transport -- the same per-step records moved over gloo
 (np8_step_local / np8_step_merge).  (The RCCL code path itself runs in tests/test_gpu_rccl_one_rank.py with
 a one-rank communicator; the driver's scaling runs use one GPU per rank.)  The sharded result must equal
-the single-rank sweep bit for bit -- at N = 8000 from a poor start, and at the C3 workload itself (N = 1e6, D = 8,
-K = 64, warm state; the contiguous shards of C4) as 2 and 4 ranks."""
+the single-rank sweep bit for bit -- at N = 8000 from a poor start, at the C3 workload itself (N = 1e6, D = 8,
+K = 64, warm state; the contiguous shards of C4) as 2, 4 and 8 ranks (8: the 125k-item shards of C4's 8-GPU point),
+and from the reference's own initialisation at full size (init_random(20), 20 sweeps: the cold start's 158k requests
+per step, partial acceptance by global scan position) as 2 ranks."""
 import os
 import socket
 
@@ -14,6 +16,7 @@ pytestmark = pytest.mark.gpu
 
 N, D, SWEEPS, SEED = 8000, 8, 6, 2024
 NC3, SWEEPS_C3 = 1_000_000, 12
+SWEEPS_COLD = 20
 
 
 def _port():
@@ -27,6 +30,9 @@ def _port():
 def _data(kind="small"):
     from noparama_amd import datasets
 
+    if kind == "cold":  # C3 data; the state comes from init_random(20) on every rank
+        X, z, mu, sig = datasets.config_c3(N=NC3)
+        return X, None, None, None
     if kind == "c3":  # the north-star workload: C3 data, its warm state (bench.py), 2% of the labels scrambled
         X, z, mu, sig = datasets.config_c3(N=NC3)
         z = z.astype(np.int32)
@@ -48,7 +54,7 @@ def _rank(rank, world, port, outdir, kind="small"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     X, zr, mu, sig = _data(kind)
-    n, sweeps = X.shape[0], (SWEEPS_C3 if kind == "c3" else SWEEPS)
+    n, sweeps = X.shape[0], {"c3": SWEEPS_C3, "cold": SWEEPS_COLD}.get(kind, SWEEPS)
     lo, hi = (n * rank) // world, (n * (rank + 1)) // world
     uid = [comm_unique_id() if rank == 0 else None]
     dist.broadcast_object_list(uid, src=0)
@@ -63,7 +69,10 @@ def _rank(rank, world, port, outdir, kind="small"):
     if all(flags):
         transport = "rccl"
         smp.set_data(X[lo:hi], offset=lo, n_global=n)
-        smp.set_state(zr[lo:hi], mu, sig)
+        if kind == "cold":
+            smp.init_random(20)
+        else:
+            smp.set_state(zr[lo:hi], mu, sig)
         smp.sweep(sweeps)
     else:
         transport = "gloo"
@@ -71,7 +80,10 @@ def _rank(rank, world, port, outdir, kind="small"):
         smp = NealAlgorithm8(D, seed=SEED, device=0)
         smp.comm_init(None, rank, world)
         smp.set_data(X[lo:hi], offset=lo, n_global=n)
-        smp.set_state(zr[lo:hi], mu, sig, counts=np.bincount(zr, minlength=mu.shape[0]))
+        if kind == "cold":  # (init_random counts over all items: the global counts without communication)
+            smp.init_random(20)
+        else:
+            smp.set_state(zr[lo:hi], mu, sig, counts=np.bincount(zr, minlength=mu.shape[0]))
         for _ in range(sweeps):
             rec = torch.from_numpy(smp.step_local())
             out = [torch.zeros_like(rec) for _ in range(world)]
@@ -81,6 +93,7 @@ def _rank(rank, world, port, outdir, kind="small"):
     st = smp.state()
     np.save(os.path.join(outdir, f"z{rank}.npy"), st["z"])
     np.save(os.path.join(outdir, f"c{rank}.npy"), st["counts"])
+    np.save(os.path.join(outdir, f"k{rank}.npy"), np.array([st["K"], smp.stats()["rejected_requests"]]))
     open(os.path.join(outdir, f"transport{rank}"), "w").write(transport)
     dist.barrier()
     dist.destroy_process_group()
@@ -106,10 +119,10 @@ def test_two_rank_processes_equal_single_rank(tmp_path):
     print("transport:", open(tmp_path / "transport0").read())
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_c3_workload_sharded_equals_single_rank(tmp_path, world):
     """C4's sharding of the C3 workload (N = 1e6, the warm state with 2% of the labels scrambled so that items move,
-    contiguous shards) on 2 and 4 ranks: labels and counts after 12 sweeps equal one rank's bit for bit."""
+    contiguous shards) on 2, 4 and 8 ranks: labels and counts after 12 sweeps equal one rank's bit for bit."""
     import torch.multiprocessing as mp
 
     from noparama_amd import NealAlgorithm8
@@ -126,3 +139,29 @@ def test_c3_workload_sharded_equals_single_rank(tmp_path, world):
     assert np.array_equal(zz, ref["z"])
     for r in range(world):
         assert np.array_equal(np.load(tmp_path / f"c{r}.npy"), ref["counts"])
+
+
+def test_cold_start_full_size_sharded_equals_single_rank(tmp_path):
+    """The reference's initialisation (np_mcmc.cpp:49-92: init_random(20)) at the full C3 size on 2 ranks, 20 sweeps:
+    the first steps carry far more new-cluster requests than req_max (partial acceptance by global scan position,
+    each rank sending its req_max lowest), later ones the mixed regime; labels, counts, K and the rejected-request
+    count equal one rank's bit for bit."""
+    import torch.multiprocessing as mp
+
+    from noparama_amd import NealAlgorithm8
+
+    X, _, _, _ = _data("cold")
+    one = NealAlgorithm8(D, seed=SEED, device=0)
+    one.set_data(X)
+    one.init_random(20)
+    one.sweep(SWEEPS_COLD)
+    ref = one.state()
+    rej = one.stats()["rejected_requests"]
+    one.close()
+    assert rej > 0  # the first step overflowed req_max
+    mp.spawn(_rank, args=(2, _port(), str(tmp_path), "cold"), nprocs=2, join=True)
+    zz = np.concatenate([np.load(tmp_path / f"z{r}.npy") for r in range(2)])
+    assert np.array_equal(zz, ref["z"])
+    for r in range(2):
+        assert np.array_equal(np.load(tmp_path / f"c{r}.npy"), ref["counts"])
+        assert list(np.load(tmp_path / f"k{r}.npy")) == [ref["K"], rej]
