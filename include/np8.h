@@ -155,6 +155,9 @@ typedef struct {
     /* NP8_TIMING_COUNTERS: walked candidate rows within kSkip (80 nats) of the running maximum, i.e. that pay the
      * pick's exp and division (cumulative) */
     int64_t pick_evals;
+    /* RCCL path: steps of a compact sweep graph whose requests did not fit the compact records; each
+     * halted its graph on every rank and was resumed by the host with the full records (cumulative) */
+    int64_t compact_halts;
 } np8_stats_t;
 
 #define NP8_STATS_MIN_BYTES offsetof(np8_stats_t, ms_assign) /* K .. last_loglik: the first released layout */

@@ -34,6 +34,18 @@ constexpr int kPruneMaxKcap = 4096;  // kcap x kcap int32 candidate lists (64 MB
 #endif
 constexpr uint32_t kGatherEvery = NP8_GATHER_EVERY;  // data-parallel sweeps per gathering of fresh pruning radii
 
+// Host state of one step of a captured compact sweep graph, taken right after its assign was captured: what the rest
+// of the step and end_sweep read.  A replay that halts at step i resumes from it (np8_sweep, recover_halt).
+struct HostSnap {
+    uint32_t di = 0;       // epoch offset from the graph's first sweep
+    int32_t dchecks = 0;   // max-likelihood checks before it, in the graph
+    int64_t dfolded = 0, dtail = 0;
+    int64_t assign_waves = 0;
+    bool step_ll = false, step_snap = false, sweep_ll = false, snap_lazy = false, collecting = false, gather = false,
+         lists_valid = false, r2_zero = false, gath_clear = false, pruned_last = false, use_sorted = false,
+         sorted_valid = false, churn = false;
+};
+
 struct Timer {
     hipEvent_t a = nullptr, b = nullptr;
     int phase = -1;  // -1: not timed
@@ -45,6 +57,8 @@ struct Timer {
 struct np8_ctx {
     // configuration
     int D = 0, M = 0, DP = 0, CS = 0, kcap = 0;
+    int DT = 0;  // the wide path's tile dimension: D rounded up to 16 (item rows and contraction tables, zero beyond D)
+    int64_t uw_off = 0;  // wide path: offset of AssignArgs::uw in hyp
     int64_t rec_cap = 0;  // requests the exchanged record holds (one rank: every item of a step)
     int req_max = NP8_REQ_DEFAULT;
     double alpha = 1.0, kappa = 1.0, nu = 1.0;
@@ -193,6 +207,27 @@ struct np8_ctx {
     // multi-GPU
     ncclComm_t comm = nullptr;
     int rank = 0, world = 1;
+    // compact exchange: the steps of a sharded sweep graph all-gather compact records -- the count deltas
+    // and at most c_cap requests per rank -- instead of the full ones (req_max requests); a step with more requests on
+    // some rank halts the graph on every rank, and the host runs that step's exchange with the full records
+    unsigned char *crec = nullptr, *cgath = nullptr;
+    int64_t c_bytes = 0;
+    int c_cap = 32;            // NP8_COMPACT_REQ (0: full records always)
+    bool compact_on = false;   // the next captured sharded graph exchanges compact records (policy, alike on all ranks)
+    bool compact_step = false; // the step being launched does
+    bool graph_compact = false;
+    int32_t *mirror_host = nullptr, *mirror_dev = nullptr;  // host-mapped [kMirrorInts] (np8::FinArgs::mirror)
+    std::vector<HostSnap> graph_snaps, cap_snaps;
+    uint32_t cap_sweep = 0;
+    int32_t cap_checks0 = 0;
+    // the last replay of a sharded graph, checked once the next one is queued (or by settle)
+    bool pend_on = false, pend_compact = false;
+    uint32_t pend_epoch = 0;
+    int32_t pend_checks = 0;
+    int64_t pend_folded = 0, pend_tail = 0;
+    hipEvent_t rev[2] = {nullptr, nullptr};
+    int rev_k = 0, pend_k = 0;
+    int64_t n_halts = 0;
     // timing: event pairs around launches; count_eval: the assign kernels' executed-work counters
     bool timing = false, count_eval = false, time_all = false;
     std::vector<Timer> timers;
@@ -484,9 +519,17 @@ void free_device(np8_ctx *c) {
                     c->sm_typ, c->sm_slist, c->sm_stheta, c->stage, c->evalc, c->z_base, c->cnt_base,
                     c->chg_slot, c->mu_base, c->sigma_base, c->chg_item, c->chg_count, c->chg_flags,
                     c->inv_hist, c->inv_out, c->queue, c->qcount, c->qlist, c->slot_logn1, c->plen_s,
-                    c->plr2_s, c->sm_mb, c->lb, c->llpart, c->part, c->part_slot};
+                    c->plr2_s, c->sm_mb, c->lb, c->llpart, c->part, c->part_slot, c->crec, c->cgath};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
+    c->crec = c->cgath = nullptr;
+    if (c->mirror_host) (void)hipHostFree(c->mirror_host);
+    c->mirror_host = c->mirror_dev = nullptr;
+    for (hipEvent_t &e : c->rev)
+        if (e) {
+            (void)hipEventDestroy(e);
+            e = nullptr;
+        }
     if (c->sm_first_host) (void)hipHostFree(c->sm_first_host);
     if (c->moved_host) (void)hipHostFree(c->moved_host);
     c->moved_host = c->moved_dev = nullptr;
@@ -570,6 +613,13 @@ int alloc_records(np8_ctx *c) {
     } else if (c->stage) {
         (void)hipFree(c->stage);
         c->stage = nullptr;
+    }
+    // compact records of the RCCL path's sweep graphs (the same layout with c_cap requests)
+    if (c->comm && c->c_cap > 0 && !c->wide) {
+        c->c_bytes = record_bytes(c->kcap, c->c_cap, c->D);
+        if ((r = dalloc(c, &c->crec, (size_t)c->c_bytes)) || (r = dalloc(c, &c->cgath, (size_t)c->c_bytes * c->world)))
+            return r;
+        c->compact_on = true;
     }
     return NP8_OK;
 }
@@ -729,6 +779,17 @@ FinArgs fin_args(np8_ctx *c, const unsigned char *recs, int world) {
     F.lb = c->lb;
     // (np8_sweep's re-sort and churn decisions read it: a replay's last finalize, and eager steps)
     F.moved_mirror = (c->fin_advance || !c->capturing) ? c->moved_dev : nullptr;
+    if (c->comm) {  // RCCL path: a halt as it happens; the requests' peak over a replay at its last step
+        F.mirror = c->mirror_dev;
+        F.peak_out = (c->capturing && c->fin_advance) ? 1 : 0;
+    }
+    if (c->compact_step) {  // the gathered compact records (np8_sweep)
+        F.recs = c->cgath;
+        F.rec_bytes = c->c_bytes;
+        F.rec_cap = c->c_cap;
+        F.local_rec = c->crec;
+        F.compact = 1;
+    }
     F.advance = c->fin_advance;
     if (c->fin_advance) c->fin_advanced = true;
     c->fin_advance = 0;
@@ -739,6 +800,7 @@ WideArgs wide_args(np8_ctx *c) {
     WideArgs W;
     W.D = c->D;
     W.kcap = c->kcap;
+    W.DT = c->DT;
     W.dirty = c->wdirty;
     W.cnt = c->cnt;
     W.slot_P = c->slot_P;
@@ -766,6 +828,7 @@ NiwArgs niw_args(np8_ctx *c) {
     std::memset(&A, 0, sizeof(A));
     A.D = c->D;
     A.kcap = c->kcap;
+    A.DT = c->DT;
     A.kappa0 = c->kappa;
     A.nu0 = c->nu;
     A.rsk = c->rsk;
@@ -843,6 +906,8 @@ AssignArgs assign_args(np8_ctx *c, int64_t p0, int64_t p1, const int64_t *order,
     A.wfrag = c->wfrag;
     A.wmu = c->wmu;
     A.lam_lo = c->lam_lo;
+    A.dim = c->D;
+    A.uw = c->wide ? c->hyp + c->uw_off : nullptr;
     A.wdist = nullptr;  // set by launch_assign on the wide path (after np8_wide_dist)
     A.queue = A.queue_out = A.qcount = A.qlist = nullptr;
     A.slot_mu = c->slot_mu;
@@ -899,7 +964,7 @@ int flush_snapshot(np8_ctx *c) {
     if (c->snap_lazy) {
         c->snap_lazy = false;
         HIPC(c, np8_launch_snapshot_flush(snap_args(c), c->ctl, c->stream));
-        HIPC(c, hipMemsetAsync(&c->ctl->snap_pend, 0, sizeof(int32_t), c->stream));
+        HIPC(c, np8_launch_ctl_clear(c->ctl, 1, c->stream));  // snap_pend (not while a compact graph is halted)
     }
     return best_item_order(c);  // (every reader of z_best comes through here)
 }
@@ -941,7 +1006,7 @@ int launch_finalize(np8_ctx *c, const unsigned char *recs, int world, int prune 
         return NP8_OK;
     }
     if (c->gather)  // the step's radius records (any order with finalize: both only raise the gathered radii)
-        HIPC(c, np8_launch_fold_r2(c->wr2, c->assign_waves, c->r2, c->kcap, c->stream));
+        HIPC(c, np8_launch_fold_r2(c->wr2, c->assign_waves, c->r2, c->kcap, c->ctl, c->stream));
     if (prune >= 0 && !c->fp_off && !c->wide && c->prior == NP8_PRIOR_REFERENCE) {
         // finalize and the lists in one launch, the lists still one per wave over several workgroups
         PruneArgs P = prune_args(c, prune == 1);
@@ -999,6 +1064,18 @@ int launch_assign(np8_ctx *c, int64_t p0, int64_t p1, const int64_t *order, bool
     c->snap_lazy = false;
     A.ll_on = c->step_ll ? 1 : 0;
     A.snap_on = c->step_snap ? 1 : 0;
+    // compact exchange: a whole frozen step of a captured sharded graph with the folded check (every kernel such a
+    // graph holds does nothing once a step halts it)
+    c->compact_step = whole && c->comm && c->capturing && c->compact_on && c->crec && c->fp_off &&
+                      c->param_update == NP8_PARAM_FROZEN && !c->llfold_off && c->gp_iso > 0.0 && c->llpart;
+    if (c->compact_step) {
+        A.compact = 1;
+        A.rec = c->crec;  // the count deltas; requests to the staging area and the first c_cap also to crec
+        A.nreq = &reinterpret_cast<RecHeader *>(c->crec)->nreq;
+        A.creq = reinterpret_cast<Request *>(c->crec + kRecHeaderBytes + 4ll * c->kcap);
+        A.cvmu = reinterpret_cast<double *>(c->crec + record_vmu_offset(c->kcap, c->c_cap));
+        A.ccap = c->c_cap;
+    }
     if (c->wide) {
         if (c->wdist && !c->wide_prune_off) {  // distances between the current rows' means (pruning)
             HIPC(c, np8_launch_wide_dist(wide_args(c), c->stream));
@@ -1076,6 +1153,7 @@ int launch_resort(np8_ctx *c, bool stale) {
     S.kcap = c->kcap;
     S.D = c->D;
     S.esz = c->wide ? 4 : 8;
+    if (c->wide) S.D = c->DT;  // (the wide path's item rows: DT, zero beyond D)
     S.nsub = c->substeps;
     S.pad = 0;
     S.offset = c->offset;
@@ -1103,6 +1181,8 @@ int prepare_sorted_now(np8_ctx *c) { return launch_resort(c, !c->sorted_valid); 
 // One synchronous step.  sub >= 0: sub-step `sub` of a data-parallel sweep (positions of the label-sorted
 // layout); otherwise local positions [p0,p1) of the chunked or explicit-order walk, and the whole
 // data-parallel sweep when [p0,p1) = [0,n) with no order (substeps == 1).
+int step_finish(np8_ctx *c, int sub);
+
 int step(np8_ctx *c, int64_t p0, int64_t p1, const int64_t *order, bool use_perm, int sub = -1) {
     if (sub >= 0) {
         p0 = c->sub_start[(size_t)sub];
@@ -1134,13 +1214,47 @@ int step(np8_ctx *c, int64_t p0, int64_t p1, const int64_t *order, bool use_perm
     int r = launch_assign(c, p0, p1, order, use_perm);
     if (r) return r;
     if (c->world > 1 && !c->comm) return fail(c, NP8_ERR_STATE, "host-exchange mode: use np8_step_local/np8_step_merge");
+    return step_finish(c, sub);
+}
+
+// The rest of a synchronous step after its assign: the exchange (RCCL: compact or full records) and finalize, the
+// candidate lists.  Also the resumption of a halted compact step (recover_halt), with the full records.
+int step_finish(np8_ctx *c, int sub) {
+    int r = 0;
     // the lists right after finalize (np8_step_tail) when nothing changes the table in between: the next sub-step's
     // (radii in use), or the sweep's when its parameters are frozen (end_sweep's prune)
     const bool mid = sub >= 0 && sub + 1 < c->substeps;
     const int fprune = (c->collecting && (!c->fuse_off || !c->fp_off || !c->tailcond_off) && !c->wide &&
                         c->prior == NP8_PRIOR_REFERENCE &&
                         (mid || c->param_update == NP8_PARAM_FROZEN)) ? (mid ? 0 : 1) : -1;
-    if (c->comm) {  // the exchange over RCCL (also with a one-rank communicator)
+    if (c->comm && c->compact_step) {  // a step of a compact sweep graph (np8_sweep)
+        if (c->capturing) {  // where a replay halted at this step resumes
+            HostSnap h;
+            h.di = c->cap_sweep;
+            h.dchecks = c->checks - c->cap_checks0;
+            h.dfolded = c->cap_folded;
+            h.dtail = c->cap_tail;
+            h.assign_waves = c->assign_waves;
+            h.step_ll = c->step_ll;
+            h.step_snap = c->step_snap;
+            h.sweep_ll = c->sweep_ll;
+            h.snap_lazy = c->snap_lazy;
+            h.collecting = c->collecting;
+            h.gather = c->gather;
+            h.lists_valid = c->lists_valid;
+            h.r2_zero = c->r2_zero;
+            h.gath_clear = c->gath_clear;
+            h.pruned_last = c->pruned_last;
+            h.use_sorted = c->use_sorted;
+            h.sorted_valid = c->sorted_valid;
+            h.churn = c->churn;
+            c->cap_snaps.push_back(h);
+        }
+        if (c->step_ll) HIPC(c, np8_launch_ll_header(c->ctl, c->llpart, c->assign_waves, c->crec, c->stream));
+        NCCLC(c, ncclAllGather(c->crec, c->cgath, (size_t)c->c_bytes, ncclUint8, c->comm, c->stream));
+        r = launch_finalize(c, c->cgath, c->world, fprune);
+        c->compact_step = false;
+    } else if (c->comm) {  // the exchange over RCCL (also with a one-rank communicator)
         HIPC(c, np8_launch_req_select(c->stage, c->stage_cap, c->rec, c->rec_cap, c->kcap, c->D, c->req_max,
                                       c->step_ll ? c->llpart : nullptr, c->assign_waves, c->stream));
         NCCLC(c, ncclAllGather(c->rec, c->gath, (size_t)c->rec_bytes, ncclUint8, c->comm, c->stream));
@@ -1250,6 +1364,7 @@ int param_update(np8_ctx *c, int stats_mode = 0) {
     A.n_loc = c->n_loc;
     A.kcap = c->kcap;
     A.D = c->D;
+    A.DT = c->DT;
     A.steps = c->mh_steps;
     A.acc = c->acc;
     A.cnt = c->cnt;
@@ -1385,6 +1500,9 @@ void drop_graph(np8_ctx *c) {
     c->graph_par = c->graph_phase = -1;
 }
 
+// The next sharded graph's records: compact (policy, alike on every rank) or full.
+bool want_compact(const np8_ctx *c) { return c->comm && c->crec && c->compact_on; }
+
 bool graph_eligible(np8_ctx *c, bool sync) {
     // sharded runs are captured with their RCCL collectives; the host-exchange path is not (host transport)
     return sync && !c->graphs_off && (c->world == 1 || c->comm) && c->n_loc > 0 && c->sorted_valid &&
@@ -1419,11 +1537,16 @@ int capture_graph(np8_ctx *c) {
     // the re-sort check leaves the graph when its last finalize mirrors ctl->moved for the host (np8_sweep)
     c->capture_sort_outside = adv_fin && !c->sort_in_graph && !c->churn && c->moved_dev != nullptr;
     c->graph_churn = c->churn;
+    c->cap_snaps.clear();
+    c->cap_checks0 = ch0;
+    const bool cmode = want_compact(c);
     for (uint32_t i = 0; i < kGraphSweeps && !r; ++i) {
         if (adv_fin && i + 1 == kGraphSweeps) c->fin_advance = kGraphSweeps;
+        c->cap_sweep = i;
         r = population(c);
         if (!r) r = end_sweep(c);
     }
+    c->compact_step = false;
     c->fin_advance = 0;
     const bool snap1 = c->snap_lazy;
     c->snap_lazy = snap0;
@@ -1447,6 +1570,8 @@ int capture_graph(np8_ctx *c) {
         c->graph_sort_outside = c->capture_sort_outside;
         c->graph_folded = c->cap_folded;
         c->graph_tail = c->cap_tail;
+        c->graph_compact = cmode;
+        c->graph_snaps = c->cap_snaps;
         c->graph_timing = (c->timing ? 1 : 0) | (c->count_eval ? 2 : 0) | (c->time_all ? 4 : 0);
     } else {
         c->graph_timers.clear();
@@ -1459,11 +1584,14 @@ int capture_graph(np8_ctx *c) {
 
 // The graph for the sweeps starting at the current epoch (captured when missing or captured at another
 // phase, check parity or timing setting).
+bool graph_current(const np8_ctx *c) {
+    return c->graph && c->graph_par == (c->checks & 1) && c->graph_phase == (int)(c->epoch % kGraphSweeps) &&
+           c->graph_snap0 == c->snap_lazy && c->graph_churn == c->churn && c->graph_compact == want_compact(c) &&
+           c->graph_timing == ((c->timing ? 1 : 0) | (c->count_eval ? 2 : 0) | (c->time_all ? 4 : 0));
+}
+
 int ensure_graph(np8_ctx *c) {
-    if (!c->graph || c->graph_par != (c->checks & 1) || c->graph_phase != (int)(c->epoch % kGraphSweeps) ||
-        c->graph_snap0 != c->snap_lazy || c->graph_churn != c->churn ||
-        c->graph_timing != ((c->timing ? 1 : 0) | (c->count_eval ? 2 : 0) | (c->time_all ? 4 : 0)))
-        return capture_graph(c);
+    if (!graph_current(c)) return capture_graph(c);
     return NP8_OK;
 }
 
@@ -1489,6 +1617,79 @@ int run_graph(np8_ctx *c) {
     c->epoch += kGraphSweeps;
     c->checks += (int32_t)(kGraphSweeps / 5);
     c->t_base += kGraphSweeps;
+    return NP8_OK;
+}
+
+// A compact replay halted at step i (every rank alike, np8_finalize): the host state of that step as its capture left
+// it after the assign, then the step's exchange with the full records -- the deltas the assign wrote into the compact
+// record and every request of the staging area -- and the rest of the sweep.  The halted replay's later kernels did
+// nothing, as did a replay queued behind it; the chain continues from the resumed step as if nothing had halted.
+// finish: then run the sweeps the host had already counted (up to the epoch it had reached) -- np8_sweep's own loop
+// does that itself (it continues to its target), every other entry point needs them done before it reads the state.
+int recover_halt(np8_ctx *c, bool finish) {
+    const uint32_t reached = c->epoch;
+    HIPC(c, hipStreamSynchronize(c->stream));
+    const uint32_t i = (uint32_t)*(volatile int32_t *)&c->mirror_host[1];
+    const HostSnap *hp = nullptr;
+    for (const HostSnap &h : c->graph_snaps)
+        if (h.di == i) hp = &h;
+    if (!hp) return fail(c, NP8_ERR_STATE, "a compact sweep graph halted at a step without its host state");
+    const HostSnap &h = *hp;
+    c->epoch = c->pend_epoch + h.di;
+    c->checks = c->pend_checks + h.dchecks;
+    c->n_folded = c->pend_folded + h.dfolded;
+    c->n_tail_cond = c->pend_tail + h.dtail;
+    c->t_base = c->pend_epoch;  // (the halted replay's last finalize did not advance the device's)
+    c->assign_waves = h.assign_waves;
+    c->step_ll = h.step_ll;
+    c->step_snap = h.step_snap;
+    c->sweep_ll = h.sweep_ll;
+    c->snap_lazy = h.snap_lazy;
+    c->collecting = h.collecting;
+    c->gather = h.gather;
+    c->lists_valid = h.lists_valid;
+    c->r2_zero = h.r2_zero;
+    c->gath_clear = h.gath_clear;
+    c->pruned_last = h.pruned_last;
+    c->use_sorted = h.use_sorted;
+    c->sorted_valid = h.sorted_valid;
+    c->churn = h.churn;
+    c->fin_advance = 0;
+    c->fin_advanced = false;
+    c->compact_step = false;
+    c->compact_on = false;  // full records until a replay's requests fit the compact ones again (np8_sweep)
+    c->n_halts += 1;
+    HIPC(c, hipMemsetD32Async(reinterpret_cast<int *>(&c->ctl->halt), 0, 1, c->stream));
+    HIPC(c, hipMemsetD32Async(reinterpret_cast<int *>(&c->ctl->t_base), (int)c->t_base, 1, c->stream));
+    c->mirror_host[0] = 0;
+    HIPC(c, hipMemcpyAsync(c->rec + kRecHeaderBytes, c->crec + kRecHeaderBytes, 4ull * c->kcap, hipMemcpyDeviceToDevice,
+                           c->stream));
+    HIPC(c, hipMemcpyAsync(&reinterpret_cast<RecHeader *>(c->stage)->nreq, &reinterpret_cast<RecHeader *>(c->crec)->nreq,
+                           sizeof(int32_t), hipMemcpyDeviceToDevice, c->stream));
+    HIPC(c, hipMemsetAsync(c->crec, 0, kRecHeaderBytes + 4ull * c->kcap, c->stream));
+    int r = step_finish(c, -1);
+    if (r) return r;
+    if ((r = end_sweep(c))) return r;
+    while (finish && (int32_t)(reached - c->epoch) > 0) {  // (full records: the policy switched them off)
+        if ((r = population(c)) || (r = end_sweep(c))) return r;
+    }
+    return NP8_OK;
+}
+
+// The last replay of a sharded graph, once it is done: resumed if it halted (recover_halt); otherwise its requests'
+// peak may bring compact records back (decided alike on every rank: the peak is a function of the gathered headers).
+// finish: see recover_halt (false only from np8_sweep's loop).
+int settle(np8_ctx *c, bool *recovered = nullptr, bool finish = true) {
+    if (recovered) *recovered = false;
+    if (!c->pend_on) return NP8_OK;
+    c->pend_on = false;
+    HIPC(c, hipEventSynchronize(c->rev[c->pend_k]));
+    if (*(volatile int32_t *)&c->mirror_host[0]) {
+        if (recovered) *recovered = true;
+        return recover_halt(c, finish);
+    }
+    if (!c->compact_on && c->crec && !c->pend_compact && *(volatile int32_t *)&c->mirror_host[2] * 2 <= c->c_cap)
+        c->compact_on = true;
     return NP8_OK;
 }
 
@@ -1520,6 +1721,7 @@ int np8_create_sized(np8_ctx **out, const np8_config *cfg_in, size_t cfg_bytes) 
         return NP8_ERR_ARG;
     }
     c->DP = packed_size(c->D);
+    c->DT = (cfg->contraction == NP8_CONTRACT_F32_MFMA) ? wide_dt(c->D) : c->D;
     c->CS = cand_stride(c->D);
     c->kcap = cfg->kcap > 0 ? cfg->kcap : (cfg->contraction == NP8_CONTRACT_F32_MFMA ? 512 : 2048);
 
@@ -1551,7 +1753,9 @@ int np8_create_sized(np8_ctx **out, const np8_config *cfg_in, size_t cfg_bytes) 
     // chi^2(nu0 - a), a < D, need nu0 >= D + 1 (Marsaglia-Tsang shape >= 1)
     const bool niw = cfg->prior == NP8_PRIOR_NIW;
     if ((niw && cfg->param_update == NP8_PARAM_MH_G0) || (!niw && cfg->param_update == NP8_PARAM_NIW_CONJUGATE) ||
-        (niw && !(cfg->nu >= cfg->D + 1.0 && cfg->nu < 1e12))) {
+        (niw && !(cfg->nu >= cfg->D + 1.0 && cfg->nu < 1e12)) ||
+        // np8_niw_post holds four D x (D + 1) double matrices in LDS: at most D = 64
+        (niw && cfg->contraction == NP8_CONTRACT_F32_MFMA && cfg->D > 64)) {
         delete c;
         return NP8_ERR_ARG;
     }
@@ -1612,6 +1816,15 @@ int np8_create_sized(np8_ctx **out, const np8_config *cfg_in, size_t cfg_bytes) 
         }
     }
     c->llfold_off = std::getenv("NP8_NO_LLFOLD") != nullptr;
+    if (const char *cr = std::getenv("NP8_COMPACT_REQ")) c->c_cap = std::max(0, std::min(atoi(cr), c->req_max));
+    if (hipHostMalloc((void **)&c->mirror_host, sizeof(int32_t) * kMirrorInts, hipHostMallocMapped) != hipSuccess ||
+        hipHostGetDevicePointer((void **)&c->mirror_dev, c->mirror_host, 0) != hipSuccess) {
+        if (c->mirror_host) (void)hipHostFree(c->mirror_host);
+        c->mirror_host = c->mirror_dev = nullptr;
+        c->c_cap = 0;  // (no mirror: no compact exchange)
+    } else {
+        for (int k = 0; k < kMirrorInts; ++k) c->mirror_host[k] = 0;
+    }
     c->rec_cap = c->req_max;  // grown to the item count by np8_set_data (one rank)
     c->rec_bytes = record_bytes(c->kcap, (int)c->rec_cap, c->D);
     int r = 0;
@@ -1665,6 +1878,12 @@ int np8_create_sized(np8_ctx **out, const np8_config *cfg_in, size_t cfg_bytes) 
         hyp.push_back(smax);
     }
     for (int a = 0; a < D; ++a) hyp.push_back(c->UinvT[a * D + a]);  // the whitening diagonal, contiguous (kUdiag)
+    if (c->wide) {  // the wide kernels' item frame at DT: mu0 and U^T packed, zero beyond D (AssignArgs::uw)
+        c->uw_off = (int64_t)hyp.size();
+        for (int a = 0; a < c->DT; ++a) hyp.push_back(a < D ? c->mu0[a] : 0.0);
+        for (int a = 0; a < c->DT; ++a)
+            for (int b = a; b < c->DT; ++b) hyp.push_back((a < D && b < D) ? c->UinvT[a * D + b] : 0.0);
+    }
     std::vector<double> gp;
     for (int a = 0; a < D; ++a)
         for (int b = a; b < D; ++b) gp.push_back(c->Gp[a * D + b]);
@@ -1675,9 +1894,9 @@ int np8_create_sized(np8_ctx **out, const np8_config *cfg_in, size_t cfg_bytes) 
          ((r = dalloc(c, &c->d_U, (size_t)D * D)) || (r = dalloc(c, &c->d_Uinv, (size_t)D * D)) ||
           (r = dalloc(c, &c->d_Psi0, (size_t)D * D)) || (r = dalloc(c, &c->pend, (size_t)4 * kReqMax)))) ||
         (c->wide && c->prior != NP8_PRIOR_NIW && (r = dalloc(c, &c->pend, (size_t)4 * kReqMax))) ||
-        (c->wide && ((r = dalloc(c, &c->wA, (size_t)kc * D * D)) ||
-                     (r = dalloc(c, &c->wfrag, (size_t)kc * (D * D + D))) ||  // >= the compact rows
-                     (r = dalloc(c, &c->wmu, (size_t)kc * D)) || (r = dalloc(c, &c->lam_lo, (size_t)kc)) ||
+        (c->wide && ((r = dalloc(c, &c->wA, (size_t)kc * c->DT * c->DT)) ||
+                     (r = dalloc(c, &c->wfrag, (size_t)kc * (c->DT * c->DT + c->DT))) ||  // >= the compact rows
+                     (r = dalloc(c, &c->wmu, (size_t)kc * c->DT)) || (r = dalloc(c, &c->lam_lo, (size_t)kc)) ||
                      (r = dalloc(c, &c->wdist, (size_t)kc * kc)) ||
                      (r = dalloc(c, &c->wdirty, (size_t)kc))))) {
         free_device(c);
@@ -1725,6 +1944,7 @@ const char *np8_last_error(const np8_ctx *c) { return c ? c->err.c_str() : "null
 
 int np8_set_data(np8_ctx *c, const double *X, int64_t n, int32_t D, int64_t offset, int64_t n_global) {
     if (!c) return NP8_ERR_ARG;
+    if (int r_ = settle(c)) return r_;  // a sharded replay still unchecked (np8_sweep)
     if (D != c->D) return fail(c, NP8_ERR_ARG, "np8_set_data: D does not match the configuration");
     if (n < 0 || (n > 0 && !X)) return fail(c, NP8_ERR_ARG, "np8_set_data: bad buffer");
     if (n_global <= 0) n_global = n;
@@ -1738,7 +1958,8 @@ int np8_set_data(np8_ctx *c, const double *X, int64_t n, int32_t D, int64_t offs
     c->n_glob = n_global;
     c->part_waves = c->wide ? np8_suffstats_wide_waves(n) : 0;
     int r = 0;
-    const size_t nx = c->wide ? ((size_t)n * D + 1) / 2 : (size_t)n * D;  // wide path: fp32 items
+    // wide path: fp32 items in DT rows (zero beyond D)
+    const size_t nx = c->wide ? ((size_t)n * c->DT + 1) / 2 : (size_t)n * D;
     if ((r = dalloc(c, &c->X, nx)) || (r = dalloc(c, &c->z, (size_t)n)) ||
         (r = dalloc(c, &c->z_best, (size_t)n)) || (r = dalloc(c, &c->wr2, (size_t)((n + 63) / 64))) ||
         (r = dalloc(c, &c->llpart, (size_t)((n + 63) / 64))) ||
@@ -1767,7 +1988,7 @@ int np8_set_data(np8_ctx *c, const double *X, int64_t n, int32_t D, int64_t offs
     c->vis_n.assign((size_t)n, 0u);
     c->sorted_valid = false;
     if (c->wide) {  // rounded to fp32 (round to nearest even), as oracle/np8_oracle.c set_data does
-        std::vector<float> soa((size_t)n * D);
+        std::vector<float> soa((size_t)n * c->DT, 0.0f);
         for (int64_t i = 0; i < n; ++i)
             for (int a = 0; a < D; ++a) soa[(size_t)a * n + i] = (float)X[(size_t)i * D + a];
         HIPC(c, hipMemcpyAsync(c->X, soa.data(), sizeof(float) * soa.size(), hipMemcpyHostToDevice, c->stream));
@@ -1827,6 +2048,7 @@ int np8_set_state(np8_ctx *c, const int32_t *z, int32_t K, const double *mu, con
 int np8_set_state_counts(np8_ctx *c, const int32_t *z, int32_t K, const double *mu, const double *Sigma,
                          const int64_t *counts) {
     if (!c) return NP8_ERR_ARG;
+    if (int r_ = settle(c)) return r_;  // a sharded replay still unchecked (np8_sweep)
     if (!c->have_data) return fail(c, NP8_ERR_STATE, "np8_set_state: no data");
     if (K < 1 || K > c->kcap || !mu || !Sigma || (c->n_loc > 0 && !z))
         return fail(c, NP8_ERR_ARG, "np8_set_state: K outside [1,kcap] or null buffer");
@@ -1865,6 +2087,7 @@ int np8_set_state_counts(np8_ctx *c, const int32_t *z, int32_t K, const double *
 
 int np8_init_random(np8_ctx *c, int32_t K_init) {
     if (!c) return NP8_ERR_ARG;
+    if (int r_ = settle(c)) return r_;  // a sharded replay still unchecked (np8_sweep)
     if (!c->have_data) return fail(c, NP8_ERR_STATE, "np8_init_random: no data");
     if (K_init < 1 || K_init > c->kcap) return fail(c, NP8_ERR_ARG, "np8_init_random: K_init outside [1,kcap]");
     const int D = c->D, Q = g0_calls(D);
@@ -1915,37 +2138,62 @@ int np8_sweep(np8_ctx *c, int32_t n_sweeps) {
     int64_t chunk = (c->chunk <= 0 || c->chunk >= c->n_glob) ? N : c->chunk;
     const bool sync = chunk >= N;
     if (!sync && c->world > 1) return fail(c, NP8_ERR_ARG, "np8_sweep: chunk < N is single-rank only");
-    for (int s = 0; s < n_sweeps; ++s) {
+    if (n_sweeps <= 0) return NP8_OK;
+    int r = settle(c);
+    if (r) return r;
+    const uint32_t target = c->epoch + (uint32_t)n_sweeps;
+    while ((int32_t)(target - c->epoch) > 0) {
         if (c->moved_host) {  // churn (moved since the last re-sort, as of the last finalize): enter > n/8, leave < n/64
             const int64_t mv = *(volatile int64_t *)c->moved_host;
             c->churn = c->churn ? (mv * 64 >= c->n_loc) : (mv * 8 > c->n_loc);
         }
-        if (graph_eligible(c, sync) && (uint32_t)(n_sweeps - s) >= kGraphSweeps) {
-            int r = ensure_graph(c);
-            if (r) return r;
+        const bool can_graph = graph_eligible(c, sync) && target - c->epoch >= kGraphSweeps;
+        // a sharded replay still unchecked: anything but the next replay of the same graph waits for it
+        if (c->pend_on && !(can_graph && graph_current(c))) {
+            if ((r = settle(c, nullptr, false))) return r;
+            continue;
+        }
+        if (can_graph) {
+            if ((r = ensure_graph(c))) return r;
             if (c->graph) {
                 if (c->graph_sort_outside && (*(volatile int64_t *)c->moved_host) * 32 > c->n_loc) {
                     // the layout went stale (as of a replay ago): re-sort before this one (the device re-checks)
-                    int r = prepare_sorted_now(c);
-                    if (r) return r;
+                    if ((r = prepare_sorted_now(c))) return r;
                     *(volatile int64_t *)c->moved_host = 0;  // (until a finalize reports again)
                 }
-                int r = run_graph(c);
-                if (r) return r;
-                s += (int)kGraphSweeps - 1;
+                const uint32_t e0 = c->epoch;
+                const int32_t ch0 = c->checks;
+                const int64_t f0 = c->n_folded, t0 = c->n_tail_cond;
+                if ((r = run_graph(c))) return r;
+                if (c->comm) {  // checked once the next replay is queued (the device stays busy meanwhile)
+                    const int k = c->rev_k;
+                    c->rev_k ^= 1;
+                    if (!c->rev[k]) HIPC(c, hipEventCreateWithFlags(&c->rev[k], hipEventDisableTiming));
+                    HIPC(c, hipEventRecord(c->rev[k], c->stream));
+                    bool rec = false;
+                    if ((r = settle(c, &rec, false))) return r;
+                    if (!rec) {  // (after a recovery this replay did nothing: the recovery rewound past it)
+                        c->pend_on = true;
+                        c->pend_k = k;
+                        c->pend_epoch = e0;
+                        c->pend_checks = ch0;
+                        c->pend_folded = f0;
+                        c->pend_tail = t0;
+                        c->pend_compact = c->graph_compact;
+                    }
+                }
                 continue;
             }
         }
-        int r = population(c);
-        if (r) return r;
-        r = end_sweep(c);
-        if (r) return r;
+        if ((r = population(c))) return r;
+        if ((r = end_sweep(c))) return r;
     }
     return NP8_OK;
 }
 
 int np8_check_invariants(np8_ctx *c, int64_t out[4]) {
     if (!c || !out) return NP8_ERR_ARG;
+    if (int r_ = settle(c)) return r_;  // a sharded replay still unchecked (np8_sweep)
     if (!c->have_state) return fail(c, NP8_ERR_STATE, "np8_check_invariants: no state");
     int r = launch_invariants(c);
     if (r) return r;
@@ -2021,6 +2269,7 @@ int64_t np8_checkpoint_bytes(np8_ctx *c) {
 
 int np8_checkpoint(np8_ctx *c, void *out, int64_t bytes) {
     if (!c || !out) return NP8_ERR_ARG;
+    if (int r_ = settle(c)) return r_;  // a sharded replay still unchecked (np8_sweep)
     if (!c->have_state) return fail(c, NP8_ERR_STATE, "np8_checkpoint: no state");
     if (bytes < np8_checkpoint_bytes(c)) return fail(c, NP8_ERR_ARG, "np8_checkpoint: buffer too small");
     int r = flush_snapshot(c);
@@ -2068,6 +2317,7 @@ int np8_checkpoint(np8_ctx *c, void *out, int64_t bytes) {
 
 int np8_restore(np8_ctx *c, const void *in, int64_t bytes) {
     if (!c || !in) return NP8_ERR_ARG;
+    if (int r_ = settle(c)) return r_;  // a sharded replay still unchecked (np8_sweep)
     if (!c->have_data) return fail(c, NP8_ERR_STATE, "np8_restore: no data (np8_set_data with the same items first)");
     if (bytes < (int64_t)sizeof(CkptHeader) || bytes != np8_checkpoint_bytes(c))
         return fail(c, NP8_ERR_ARG, "np8_restore: size differs from this context's checkpoint");
@@ -2117,12 +2367,14 @@ int np8_restore(np8_ctx *c, const void *in, int64_t bytes) {
 
 int np8_population_sweep(np8_ctx *c) {
     if (!c) return NP8_ERR_ARG;
+    if (int r_ = settle(c)) return r_;  // a sharded replay still unchecked (np8_sweep)
     if (!c->have_state) return fail(c, NP8_ERR_STATE, "np8_population_sweep: no state (np8_set_state/np8_init_random)");
     return population(c);
 }
 
 int np8_track_changes(np8_ctx *c, int32_t mode) {
     if (!c) return NP8_ERR_ARG;
+    if (int r_ = settle(c)) return r_;  // a sharded replay still unchecked (np8_sweep)
     if (mode < 0 || mode > NP8_CHANGES_FROM_EMPTY) return fail(c, NP8_ERR_ARG, "np8_track_changes: bad mode");
     c->track = mode ? 1 : 0;
     if (!mode) return NP8_OK;
@@ -2150,6 +2402,7 @@ int np8_changes(np8_ctx *c, int64_t item_cap, int64_t *item, int32_t *slot, int3
                 int32_t *updated, double *mu, double *Sigma, np8_changes_t *out) {
     if (!c || !out) return NP8_ERR_ARG;
     std::memset(out, 0, sizeof(*out));
+    if (int r_ = settle(c)) return r_;  // a sharded replay still unchecked (np8_sweep)
     if (!c->track) return fail(c, NP8_ERR_STATE, "np8_changes: change tracking is off (np8_track_changes)");
     if (!c->have_state) return fail(c, NP8_ERR_STATE, "np8_changes: no state");
     if (int r = flush_snapshot(c)) return r;
@@ -2220,6 +2473,7 @@ int np8_changes(np8_ctx *c, int64_t item_cap, int64_t *item, int32_t *slot, int3
 
 int np8_prepare_sweeps(np8_ctx *c, int32_t n_sweeps) {
     if (!c) return NP8_ERR_ARG;
+    if (int r_ = settle(c)) return r_;  // a sharded replay still unchecked (np8_sweep)
     if (!c->have_state) return fail(c, NP8_ERR_STATE, "np8_prepare_sweeps: no state");
     const int64_t chunk = (c->chunk <= 0 || c->chunk >= c->n_glob) ? c->n_loc : c->chunk;
     if (!graph_eligible(c, chunk >= c->n_loc) || (uint32_t)n_sweeps < kGraphSweeps) return NP8_OK;
@@ -2232,6 +2486,7 @@ int np8_prepare_sweeps(np8_ctx *c, int32_t n_sweeps) {
 
 int np8_update_points(np8_ctx *c, const int64_t *ids, int64_t n) {
     if (!c) return NP8_ERR_ARG;
+    if (int r_ = settle(c)) return r_;  // a sharded replay still unchecked (np8_sweep)
     if (!c->have_state) return fail(c, NP8_ERR_STATE, "np8_update_points: no state");
     if (c->world > 1) return fail(c, NP8_ERR_ARG, "np8_update_points: single-rank only");
     if (n <= 0) return NP8_OK;
@@ -2266,6 +2521,7 @@ int np8_update_points(np8_ctx *c, const int64_t *ids, int64_t n) {
 
 int np8_end_sweep(np8_ctx *c) {
     if (!c) return NP8_ERR_ARG;
+    if (int r_ = settle(c)) return r_;  // a sharded replay still unchecked (np8_sweep)
     if (!c->have_state) return fail(c, NP8_ERR_STATE, "np8_end_sweep: no state");
     if (c->sub_next != 0)
         return fail(c, NP8_ERR_STATE, "np8_end_sweep: the sweep's sub-steps are not all done (np8_step_local/np8_step_merge)");
@@ -2274,6 +2530,7 @@ int np8_end_sweep(np8_ctx *c) {
 
 int np8_sync(np8_ctx *c) {
     if (!c) return NP8_ERR_ARG;
+    if (int r_ = settle(c)) return r_;  // a sharded replay still unchecked (np8_sweep)
     Ctl h;
     int r = read_ctl(c, &h);
     if (r) return r;
@@ -2295,6 +2552,7 @@ int np8_sync(np8_ctx *c) {
 
 int np8_get_state(np8_ctx *c, int32_t which, int32_t *z, int32_t *K, double *mu, double *Sigma, int64_t *counts) {
     if (!c) return NP8_ERR_ARG;
+    if (int r_ = settle(c)) return r_;  // a sharded replay still unchecked (np8_sweep)
     if (!c->have_state) return fail(c, NP8_ERR_STATE, "np8_get_state: no state");
     int r = flush_snapshot(c);
     if (r) return r;
@@ -2331,6 +2589,7 @@ int np8_get_state(np8_ctx *c, int32_t which, int32_t *z, int32_t *K, double *mu,
 
 int np8_loglik_matrix(np8_ctx *c, const int64_t *idx, int64_t n, double *out) {
     if (!c) return NP8_ERR_ARG;
+    if (int r_ = settle(c)) return r_;  // a sharded replay still unchecked (np8_sweep)
     if (!c->have_state) return fail(c, NP8_ERR_STATE, "np8_loglik_matrix: no state");
     if (n <= 0) return NP8_OK;
     for (int64_t k = 0; k < n; ++k)
@@ -2379,6 +2638,7 @@ int np8_pick_batch(np8_ctx *c, const double *lw, int32_t n, const double *u, int
 
 int np8_total_loglik(np8_ctx *c, double *out) {
     if (!c || !out) return NP8_ERR_ARG;
+    if (int r_ = settle(c)) return r_;  // a sharded replay still unchecked (np8_sweep)
     if (!c->have_state) return fail(c, NP8_ERR_STATE, "np8_total_loglik: no state");
     int r = launch_total_loglik(c);
     if (r) return r;
@@ -2421,6 +2681,7 @@ int fill_stats(np8_ctx *c, np8_stats_t *out) {
     out->folded_checks = c->n_folded;
     out->tail_list_builds = (int64_t)h.list_builds;
     out->tail_steps = c->n_tail_cond;
+    out->compact_halts = c->n_halts;
     {
         std::vector<unsigned long long> ev((size_t)10 * kEvalSlots);
         HIPC(c, hipMemcpy(ev.data(), c->evalc, sizeof(unsigned long long) * ev.size(), hipMemcpyDeviceToHost));
@@ -2442,6 +2703,7 @@ int fill_stats(np8_ctx *c, np8_stats_t *out) {
 
 int np8_stats_sized(np8_ctx *c, np8_stats_t *out, size_t out_bytes) {
     if (!c || !out || out_bytes < NP8_STATS_MIN_BYTES) return NP8_ERR_ARG;
+    if (int r_ = settle(c)) return r_;  // a sharded replay still unchecked (np8_sweep)
     np8_stats_t full;
     const int r = fill_stats(c, &full);
     if (r) return r;
@@ -2489,6 +2751,7 @@ static int resize_records(np8_ctx *c, int world) {
 int np8_comm_init(np8_ctx *c, const uint8_t id[128], int32_t rank, int32_t world) {
     // np8_finalize walks at most 64 records (base[65] in LDS)
     if (!c || world < 1 || world > 64 || rank < 0 || rank >= world) return NP8_ERR_ARG;
+    if (int r_ = settle(c)) return r_;  // a sharded replay still unchecked (np8_sweep)
     if (!id) {  // host-exchange mode: the caller moves records (np8_step_local / np8_step_merge)
         c->rank = rank;
         return resize_records(c, world);
@@ -2505,6 +2768,7 @@ int64_t np8_record_bytes(np8_ctx *c) { return c ? c->rec_bytes : 0; }
 
 int np8_step_local(np8_ctx *c, void *record_out) {
     if (!c || !record_out) return NP8_ERR_ARG;
+    if (int r_ = settle(c)) return r_;  // a sharded replay still unchecked (np8_sweep)
     if (!c->have_state) return fail(c, NP8_ERR_STATE, "np8_step_local: no state");
     const int sub = c->sub_next;  // sub-step sub of the data-parallel sweep (0 with one step)
     const int64_t p0 = c->sub_start[(size_t)sub], p1 = c->sub_start[(size_t)sub + 1];
@@ -2533,6 +2797,7 @@ int64_t np8_param_stats_bytes(np8_ctx *c) {
 
 int np8_param_stats_local(np8_ctx *c, double *out) {
     if (!c || !out) return NP8_ERR_ARG;
+    if (int r_ = settle(c)) return r_;  // a sharded replay still unchecked (np8_sweep)
     if (!c->have_state) return fail(c, NP8_ERR_STATE, "np8_param_stats_local: no state");
     if (c->param_update == NP8_PARAM_FROZEN) return fail(c, NP8_ERR_STATE, "np8_param_stats_local: frozen parameters");
     const size_t nacc = (size_t)c->kcap * (c->D + c->DP);
@@ -2546,6 +2811,7 @@ int np8_param_stats_local(np8_ctx *c, double *out) {
 
 int np8_end_sweep_stats(np8_ctx *c, const double *summed) {
     if (!c || !summed) return NP8_ERR_ARG;
+    if (int r_ = settle(c)) return r_;  // a sharded replay still unchecked (np8_sweep)
     if (!c->have_state) return fail(c, NP8_ERR_STATE, "np8_end_sweep_stats: no state");
     if (c->param_update == NP8_PARAM_FROZEN) return fail(c, NP8_ERR_STATE, "np8_end_sweep_stats: frozen parameters");
     if (c->sub_next != 0)
@@ -2560,6 +2826,7 @@ int np8_end_sweep_stats(np8_ctx *c, const double *summed) {
 
 int np8_step_merge(np8_ctx *c, const void *records, int32_t world) {
     if (!c || !records || world < 1) return NP8_ERR_ARG;
+    if (int r_ = settle(c)) return r_;  // a sharded replay still unchecked (np8_sweep)
     if (world != c->world) return fail(c, NP8_ERR_ARG, "np8_step_merge: world differs from np8_comm_init");
     c->sub_next = (c->sub_next + 1) % c->substeps;
     if (world == 1) {
@@ -2675,6 +2942,7 @@ static int sm_rebuild(np8_ctx *c, bool triadic) {
 static int split_merge_sweeps(np8_ctx *c, int32_t n_sweeps, bool triadic) {
     const char *who = triadic ? "np8_tri_sweep" : "np8_sm_sweep";
     if (!c) return NP8_ERR_ARG;
+    if (int r_ = settle(c)) return r_;  // a sharded replay still unchecked (np8_sweep)
     if (!c->have_state) return fail(c, NP8_ERR_STATE, std::string(who) + ": no state (np8_set_state/np8_init_random)");
     if (c->world > 1) return fail(c, NP8_ERR_ARG, std::string(who) + ": split-merge runs on one rank");
     if (c->wide || c->prior != NP8_PRIOR_REFERENCE)

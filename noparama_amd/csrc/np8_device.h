@@ -13,7 +13,7 @@ namespace np8 {
 constexpr double kLog2Pi = 1.8378770664093454835606594728112;
 constexpr double kTwoPi = 6.283185307179586476925286766559;
 constexpr int kReqMax = 4096;     // new-cluster requests one finalize can accept
-constexpr int kMaxD = 64;
+constexpr int kMaxD = 80;
 constexpr int kMaxM = 8;
 
 enum Stream : uint32_t {
@@ -264,6 +264,57 @@ NP8_HD void aux_core_w(uint64_t seed, uint64_t i, uint32_t t, int m, double nu, 
             prod = 1.0;
             in_chunk = 0;
         }
+    }
+    if (odd) c2 = fma(godd, godd, c2);
+    chi2 = c2;
+}
+
+// aux_core_w's draws with D at run time (the wide path, D padded to a tile multiple): the same operations in the
+// same order; the words of each further call are consumed four at a time with static indices.
+NP8_HD void aux_core_rt(uint64_t seed, uint64_t i, uint32_t t, int m, int D, double nu, double &v, double &xpar,
+                        double &chi2) {
+    const int k = (D - 1) / 2;
+    const bool odd = ((D - 1) & 1) != 0;
+    const uint32_t base = (uint32_t)(m * aux_calls(D));
+    uint32_t w[4], w1[4] = {0u, 0u, 0u, 0u};
+    philox_call(seed, i, t, kStreamAux, base, w);
+    {
+        const double r = sqrt(-2.0 * log_pos(u32_01(w[0])));
+        double sn, cs;
+        sincos_2pi(u32_01(w[1]), sn, cs);
+        v = fma(nu, r * cs, (double)D);
+        xpar = r * sn;
+    }
+    double godd = 0.0;
+    if (odd || k > 2) {
+        philox_call(seed, i, t, kStreamAux, base + 1u, w1);
+        if (odd) {
+            const double r = sqrt(-2.0 * log_pos(u32_01(w1[0])));
+            double sn, cs;
+            sincos_2pi(u32_01(w1[1]), sn, cs);
+            godd = r * cs;
+        }
+    }
+    double c2 = 0.0, prod = 1.0;
+    int in_chunk = 0;
+    auto take = [&](uint32_t word, int j) {
+        prod *= u32_01(word);
+        if (++in_chunk == 16 || j == k - 1) {
+            c2 = fma(-2.0, log_pos(prod), c2);
+            prod = 1.0;
+            in_chunk = 0;
+        }
+    };
+    if (k > 0) take(w[2], 0);
+    if (k > 1) take(w[3], 1);
+    if (k > 2) take(w1[2], 2);
+    if (k > 3) take(w1[3], 3);
+    for (int c = 0; 4 + 4 * c < k; ++c) {
+        uint32_t wc[4];
+        philox_call(seed, i, t, kStreamAux, base + 2u + (uint32_t)c, wc);
+#pragma unroll
+        for (int h = 0; h < 4; ++h)
+            if (4 + 4 * c + h < k) take(wc[h], 4 + 4 * c + h);
     }
     if (odd) c2 = fma(godd, godd, c2);
     chi2 = c2;
@@ -568,12 +619,16 @@ NP8_HD void pick_step(PickState &st, double lw, int32_t j) {
 // (Af: chunks (mt, s4), s4 >= mt, compact; in chunk c lane l's float4 element e (k-step ks = 4 s4 + e) holds
 // A[16 mt + (l & 15)][4 ks + (l >> 4)]; then muf transposed, [g][s] = muf[4 s + g]) and muf = fp32(mu) (wmu).
 // All threads of the block (np8_wide_rows, np8_niw_post).
-__device__ inline void wide_write_rows(int D, const double *R, int LDR, const double *mu, float *An, float *Af, float *wmu) {
-    for (int k = threadIdx.x; k < D * D; k += blockDim.x) {
-        const int a = k / D, b = k - a * D;
-        An[k] = (b >= a) ? (float)R[a * LDR + b] : 0.0f;
+// D < DT (a dimension that is not a multiple of 16): every table is laid out for DT, rows and columns >= D zero, so
+// the contraction's extra terms are exact zeros -- fmaf(0, 0 - 0, y) = y and fmaf(0, 0, s) = s -- and q is the one
+// of the D x D factor (the padded items are zero in those dims too).
+__device__ inline void wide_write_rows(int D, int DT, const double *R, int LDR, const double *mu, float *An, float *Af,
+                                       float *wmu) {
+    for (int k = threadIdx.x; k < DT * DT; k += blockDim.x) {
+        const int a = k / DT, b = k - a * DT;
+        An[k] = (b >= a && b < D) ? (float)R[a * LDR + b] : 0.0f;
     }
-    const int S = D / 4, S4 = D / 16, MT = D / 16, NCH = MT * (MT + 1) / 2;
+    const int S = DT / 4, S4 = DT / 16, MT = DT / 16, NCH = MT * (MT + 1) / 2;
     for (int k = threadIdx.x; k < NCH * 256; k += blockDim.x) {
         const int e = k & 3, l = (k >> 2) & 63, c = k >> 8;
         int mt = 0;
@@ -581,13 +636,16 @@ __device__ inline void wide_write_rows(int D, const double *R, int LDR, const do
         const int s4 = mt + (c - (mt * S4 - (mt * (mt - 1)) / 2));
         const int ks = 4 * s4 + e;
         const int ra = 16 * mt + (l & 15), rb = 4 * ks + (l >> 4);
-        Af[k] = (rb >= ra) ? (float)R[ra * LDR + rb] : 0.0f;
+        Af[k] = (rb >= ra && rb < D) ? (float)R[ra * LDR + rb] : 0.0f;
     }
-    for (int k = threadIdx.x; k < D; k += blockDim.x) {
-        const int g = k / S, st = k - g * S;
-        Af[NCH * 256 + k] = (float)mu[4 * st + g];
+    for (int k = threadIdx.x; k < DT; k += blockDim.x) {
+        const int g = k / S, st = k - g * S, a = 4 * st + g;
+        Af[NCH * 256 + k] = (a < D) ? (float)mu[a] : 0.0f;
     }
-    for (int a = threadIdx.x; a < D; a += blockDim.x) wmu[a] = (float)mu[a];
+    for (int a = threadIdx.x; a < DT; a += blockDim.x) wmu[a] = (a < D) ? (float)mu[a] : 0.0f;
 }
+
+// The wide path's tile dimension: D rounded up to a multiple of 16.
+NP8_HD constexpr int wide_dt(int D) { return (D + 15) & ~15; }
 
 }  // namespace np8

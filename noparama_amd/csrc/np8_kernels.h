@@ -43,7 +43,19 @@ struct Ctl {
     // the next np8_assign_fast copies the labelling into the snapshot buffers (or np8_snapshot_flush does)
     int32_t snap_pend;
     uint32_t list_builds;  // candidate-list builds by the conditional step tail (diagnostics)
+    // compact exchange: a rank's requests of a step did not fit its compact record, which np8_finalize
+    // finds in the gathered headers alike on every rank: it sets halt (and the step's epoch offset) and applies
+    // nothing; every kernel of a sweep graph then does nothing until the host has run that step's exchange with the
+    // full records and cleared it
+    int32_t halt;
+    uint32_t halt_t;
+    int32_t req_peak;  // the largest request count of one rank in one step since the last replay's end (all ranks alike)
+    int32_t pad4;
 };
+
+// Host-mapped mirror the last finalize of a replayed sweep graph writes (np8_sweep reads it once the replay is done):
+// [0] halt, [1] the halted step's epoch offset, [2] req_peak over the replay's steps
+constexpr int kMirrorInts = 4;
 
 // Candidate lists are built with kListSlack nats of extra margin, so a list stays exact while no live slot's
 // log n or log(n - 1) moves by more than kListSlack / 2 from its value at the build (np8_step_tail's
@@ -122,7 +134,9 @@ enum : int32_t { kErrCapacity = 1, kErrSigma = 2, kErrInvariant = 4, kErrQueue =
 // can accept from it (DESIGN.md "Finalize").
 struct RecHeader {
     int32_t nreq;
-    int32_t pad[3];
+    int32_t nreq_all;  // the rank's requests before np8_req_select kept its req_max lowest (0: none were dropped, the
+                       // one-rank record); the rejected-request count is the same on any number of ranks
+    int32_t pad[2];
     Fx L_local;  // folded max-likelihood check: this rank's exact sum of log-likelihoods (np8_req_select)
 };
 constexpr int kRecHeaderBytes = 32;
@@ -198,6 +212,9 @@ struct AssignArgs {
     const float *wfrag;
     const float *wmu;          // natural fp32 means [kcap][D]
     const double *lam_lo;      // [kcap] precision eigenvalue lower bounds (np8_wide_rows)
+    int32_t dim = 0;           // wide path: the data's D (the kernels are instantiated for DT = D rounded up to 16; the
+                               // item rows, factors and means beyond D are zero)
+    const double *uw = nullptr;  // wide path: mu0 [DT] | U^T packed [DT (DT + 1) / 2], zero beyond D (the item frame)
     const double *wdist;       // [K][kcap] distances between row means (np8_wide_dist); null: no pruning
     // two-kernel step (np8_assign_fast + np8_assign): positions the fast kernel deferred; non-null makes
     // np8_assign run over them instead of [p0, p1)
@@ -214,6 +231,12 @@ struct AssignArgs {
     // np8_assign_fast: the host launches no np8_assign_queue after it (every live row isotropic, so no lane is
     // deferred; a deferred lane would set kErrQueue)
     int32_t no_queue, pad_nq;
+    // compact exchange (a sharded sweep graph's steps): the kernel does nothing once ctl->halt is set, and
+    // each request it appends to the staging area (nreq, req, vmu) is also copied into the compact record's first
+    // ccap entries (creq, cvmu) -- the record whose header holds the count (nreq) and whose deltas are at rec
+    int32_t compact = 0, ccap = 0;
+    Request *creq = nullptr;
+    double *cvmu = nullptr;
     // np8_assign_fast, folded max-likelihood check (frozen parameters): ll_on = this sweep is a check sweep: each
     // wave stores the sum of its items' log-likelihoods under their new label in llpart[wave] (a requester counts
     // under its old slot; its Request carries the difference); snap_on = a snapshot may be pending
@@ -230,6 +253,7 @@ struct AssignArgs {
 // Wide-path tables (np8_wide.hip), maintained for the slots flagged in dirty.
 struct WideArgs {
     int32_t D, kcap;
+    int32_t DT;  // D rounded up to a multiple of 16: the layout of wA [kcap][DT][DT], wfrag, wmu [kcap][DT] and the items
     int32_t *dirty;
     const int32_t *cnt;
     const double *slot_P, *slot_mu;
@@ -301,6 +325,10 @@ struct FinArgs {
     int32_t slack_test = 0;
     uint32_t advance = 0;               // ctl->t_base += advance at the end (a captured graph's last step)
     int64_t *moved_mirror = nullptr;    // host-mapped copy of ctl->moved (the host's re-sort decision), or null
+    // compact exchange: the records are compact (rec_cap of them per rank): a rank with more requests halts the graph
+    int32_t compact = 0;
+    int32_t peak_out = 0;               // (a replay's last step) mirror req_peak and start it anew
+    int32_t *mirror = nullptr;          // host-mapped [kMirrorInts]: halt as it happens, req_peak with peak_out
 };
 
 // Wave-aggregated atomics on a few hot addresses (count deltas, gathered radii): one atomic per distinct key
@@ -447,6 +475,7 @@ struct NiwArgs {
     // (WideArgs::wA / wfrag / wmu) and its precision eigenvalue bound (WideArgs::lam_lo)
     float *wA = nullptr, *wfrag = nullptr, *wmu = nullptr;
     double *lam_lo = nullptr;
+    int32_t DT = 0;  // wide path: the tables' tile dimension (WideArgs::DT)
 };
 
 // np8_step_tail (the end of a synchronous step in one launch): which parts run.
@@ -485,6 +514,7 @@ struct ParamArgs {
     int32_t sorted;
     int64_t n_loc;
     int32_t kcap, D, steps;
+    int32_t DT = 0;  // wide path: the items' row count (D rounded up to 16; rows >= D zero)
     double *acc;  // [kcap][D + DP]: sum d | packed sum d d^T, d = x - mu_slot
     const int32_t *cnt;
     const int32_t *dense_of;
@@ -564,7 +594,8 @@ hipError_t np8_launch_frame_slots(const np8::FinArgs &F, hipStream_t s);
 // np8_assign_queue: the lanes np8_assign_fast deferred (A.queue, A.qcount, A.qlist, ctl->qwaves)
 hipError_t np8_launch_assign_queue(const np8::AssignArgs &A, int D, int M, hipStream_t s);
 // Pruning radii: the step's per-wave records (AssignArgs::wr2) into the gathered radii (r2 + kcap).
-hipError_t np8_launch_fold_r2(const np8::WaveR2 *wr2, int64_t n, double *r2, int kcap, hipStream_t s);
+hipError_t np8_launch_fold_r2(const np8::WaveR2 *wr2, int64_t n, double *r2, int kcap, const np8::Ctl *ctl,
+                              hipStream_t s);
 // Debug invariants (np8_config / NP8_DEBUG_INVARIANTS): every label a live slot, the live slots' counts the
 // label histogram (one rank) and summing to n_global, K the live slots, the dense table live slots only.
 // Violations: bits in out[0] (1 label out of range or in an empty slot, 2 histogram != counts, 4 sum of
@@ -591,6 +622,10 @@ hipError_t np8_launch_step_tail(const np8::AssignArgs &A, const np8::FinArgs &F,
                                 const np8::TailArgs &T, int64_t n_waves, int D, int M, hipStream_t s);
 hipError_t np8_launch_req_select(const unsigned char *stage, int64_t stage_cap, unsigned char *rec, int64_t rec_cap,
                                  int kcap, int D, int req_max, const np8::Fx *llpart, int64_t ll_n, hipStream_t s);
+// compact exchange, check sweeps: this rank's exact sum of the step's per-wave log-likelihoods into the compact
+// record's header (nothing once ctl->halt is set)
+hipError_t np8_launch_ll_header(const np8::Ctl *ctl, const np8::Fx *llpart, int64_t ll_n, unsigned char *rec,
+                                hipStream_t s);
 // z_best back to item order if np8_assign_fast left it in label-sorted position order (ctl->best_sorted): through
 // scratch (n ints) with the current layout's ids; a no-op otherwise.  Before every re-sort and every read of z_best.
 hipError_t np8_launch_best_unsort(np8::Ctl *ctl, const int32_t *ids, int32_t *z_best, int32_t *scratch, int64_t n,
@@ -606,6 +641,8 @@ int64_t np8_suffstats_wide_waves(int64_t n);   // waves of one np8_suffstats_wid
 int64_t np8_suffstats_wide_record(int D);      // doubles of one run record
 hipError_t np8_launch_mh_g0(const np8::ParamArgs &A, hipStream_t s);
 hipError_t np8_launch_advance_epoch(np8::Ctl *ctl, uint32_t n, hipStream_t s);
+// ctl->best_sorted (which = 0) or ctl->snap_pend (1) = 0 in stream order, unless a compact sweep graph is halted
+hipError_t np8_launch_ctl_clear(np8::Ctl *ctl, int which, hipStream_t s);
 hipError_t np8_launch_prune(const np8::PruneArgs &A, int kcap, hipStream_t s);
 hipError_t np8_launch_fin_prune(const np8::FinArgs &F, const np8::PruneArgs &P, hipStream_t s);
 hipError_t np8_launch_sm_members(const np8::SmArgs &A, hipStream_t s);

@@ -693,6 +693,7 @@ __global__ __launch_bounds__(NP8_ASSIGN_BLOCK) __attribute__((amdgpu_waves_per_e
     for (int a = 0; a < D; ++a) x[a] = X[(int64_t)a * A.n_loc + p];
     const int K = A.ctl->K;
     const int lists_ok = A.ctl->lists_ok;  // (the same round of scalar loads)
+    if (A.compact && A.ctl->halt) return;  // a compact sweep graph halted at an earlier step: nothing until resolved
     // a max-likelihood snapshot the last check left pending: the labelling before this step is the one it keeps
     // (copied in position order -- coalesced; np8_best_unsort puts it in item order before a re-sort or a read)
     const int snap = (!LL && A.snap_on) ? A.ctl->snap_pend : 0;
@@ -1027,6 +1028,10 @@ __global__ __launch_bounds__(NP8_ASSIGN_BLOCK) __attribute__((amdgpu_waves_per_e
                 r.dll = fx_add(fx_of(fma(-0.5, s2 * iso_n, c_n)), fx_neg(fx_of(ll_own)));
             }
             A.req[q] = r;
+            if (q < A.ccap) {  // compact exchange: the record the ranks all-gather holds the first ccap requests too
+                A.creq[q] = r;
+                for (int a = 0; a <= D; ++a) A.cvmu[(int64_t)q * (D + 1) + a] = vm[a];
+            }
         }
     }
     if (snap) {  // the rest of the pending snapshot: counts and parameters as the check's finalize left them
@@ -1043,7 +1048,10 @@ __global__ __launch_bounds__(NP8_ASSIGN_BLOCK) __attribute__((amdgpu_waves_per_e
 // result: in the synchronous sweep every item's draw is a pure function of (state, item, epoch).
 constexpr int kSortThreads = 1024, kSortItems = 4;  // 4096 items per block
 
-__device__ __forceinline__ bool sort_needed(const SortArgs &S) { return S.force || S.ctl->moved * 32 > S.n; }
+// (never while a compact sweep graph is halted: the halted step's requests name positions of the current layout)
+__device__ __forceinline__ bool sort_needed(const SortArgs &S) {
+    return !S.ctl->halt && (S.force || S.ctl->moved * 32 > S.n);
+}
 
 // Sort key of position p: the slot, after the item's data-parallel sub-step (sub-steps are contiguous
 // ranges of the layout, clusters contiguous inside each).  ids = null: p is the local item itself.
@@ -1356,21 +1364,26 @@ __device__ const double *request_vmu(const FinArgs &F, const int *base, int q) {
 }
 
 // Wide path, reference prior: (v, mu) of auxiliary m of item i from the item frame (|y0|, y0) its
-// rank recorded (aux_params of the narrow path, with the frame read back instead of recomputed).
-template <int D>
-__device__ void frame_to_vmu_d(const FinArgs &F, const double *frame, int64_t i, int m, double *vmu) {
-    double y0[D];
-    for (int a = 0; a < D; ++a) y0[a] = frame[1 + a];
-    aux_params<D>(F.hyp, y0, frame[0], F.seed, (uint64_t)i, F.ctl->t_base + F.t, m, vmu);
-}
-
+// rank recorded -- aux_params of the narrow path with D at run time (any D of the wide path) and the frame read back
+// instead of recomputed: the same operations in the same order.
 __device__ void frame_to_vmu(const FinArgs &F, const double *frame, int64_t i, int m, double *vmu) {
-    if (F.D == 32)
-        frame_to_vmu_d<32>(F, frame, i, m, vmu);
-    else if (F.D == 48)
-        frame_to_vmu_d<48>(F, frame, i, m, vmu);
-    else
-        frame_to_vmu_d<64>(F, frame, i, m, vmu);
+    const int D = F.D, DP = D * (D + 1) / 2;
+    const double *hyp = F.hyp;  // mu0 | UinvT packed | caux | rsk | logam | nu | LT packed (HypView)
+    const uint32_t t = F.ctl->t_base + F.t;
+    double y0[kMaxD], xi[kMaxD];
+    for (int a = 0; a < D; ++a) y0[a] = frame[1 + a];
+    double v, xpar, chi2;
+    aux_core_rt(F.seed, (uint64_t)i, t, m, D, hyp[D + DP + 3], v, xpar, chi2);
+    aux_xi<kMaxD>(F.seed, (uint64_t)i, t, m, D, y0, frame[0], xpar, chi2, xi);
+    const double sc = fabs(v) * hyp[D + DP + 1];
+    const double *LT = hyp + D + DP + 4;
+    vmu[0] = v;
+    int k = 0;
+    for (int a = 0; a < D; ++a) {
+        double t0 = LT[k++] * xi[a];
+        for (int b = a + 1; b < D; ++b) t0 = fma(LT[k++], xi[b], t0);
+        vmu[1 + a] = fma(sc, t0, hyp[a]);
+    }
 }
 
 }  // namespace
@@ -1449,9 +1462,20 @@ __device__ void req_select_block(const unsigned char *__restrict__ stage, int64_
     __syncthreads();
     if (threadIdx.x == 0) {
         reinterpret_cast<RecHeader *>(rec)->nreq = k;
+        reinterpret_cast<RecHeader *>(rec)->nreq_all = n;
         if (llpart) reinterpret_cast<RecHeader *>(rec)->L_local = Lloc;
         sh_hdr->nreq = 0;
     }
+}
+
+// compact exchange, check sweeps: this rank's exact log-likelihood sum into the compact record's header (the full
+// records get it from np8_req_select)
+__global__ __launch_bounds__(kFinThreads) void np8_ll_header(const Ctl *__restrict__ ctl, const Fx *__restrict__ llpart,
+                                                             int64_t ll_n, unsigned char *__restrict__ rec) {
+    __shared__ Fx shfx[16];
+    if (ctl->halt) return;
+    const Fx L = partials_sum(llpart, ll_n, shfx);
+    if (threadIdx.x == 0) reinterpret_cast<RecHeader *>(rec)->L_local = L;
 }
 
 __global__ __launch_bounds__(kFinThreads) void np8_req_select(const unsigned char *__restrict__ stage, int64_t stage_cap,
@@ -1510,8 +1534,29 @@ __device__ int finalize_block(const FinArgs &F, unsigned char *smem) {
     }
     const int cand_fresh = F.ctl->cand_fresh;
     const int nreq0 = rec_header(F, 0)->nreq;  // (same round: every thread, one address)
+    if (F.compact && F.ctl->halt) return -1;   // (same round) a compact graph halted at an earlier step
     int nreq_all = min(nreq0, F.rec_cap);
-    for (int r = 1; r < F.world; ++r) nreq_all += min(rec_header(F, r)->nreq, F.rec_cap);
+    int peak = max(nreq0, rec_header(F, 0)->nreq_all), over = nreq0 > F.rec_cap;
+    for (int r = 1; r < F.world; ++r) {
+        const RecHeader *h = rec_header(F, r);
+        nreq_all += min(h->nreq, F.rec_cap);
+        peak = max(peak, max(h->nreq, h->nreq_all));
+        over |= h->nreq > F.rec_cap;
+    }
+    if (F.compact && over) {  // block-uniform (every thread read the same headers; so does every rank)
+        // some rank's requests did not fit its compact record: apply nothing, halt the graph (the host runs this step's
+        // exchange with the full records, from the records and staging area left as they are)
+        if (tid == 0) {
+            F.ctl->halt = 1;
+            F.ctl->halt_t = F.t;
+            if (F.mirror) {
+                F.mirror[1] = (int32_t)F.t;
+                F.mirror[0] = 1;
+            }
+        }
+        return -1;
+    }
+    if (tid == 0 && peak > F.ctl->req_peak) F.ctl->req_peak = peak;
     // the folded check's partials (one rank), eight independent loads per round
     Fx llv = {0ull, 0};
     if (F.ll_on && !F.ll_rec) {
@@ -1602,20 +1647,28 @@ __device__ int finalize_block(const FinArgs &F, unsigned char *smem) {
                 F.ctl->qwaves = 0;
                 if (F.prior == kPriorNiw) F.ctl->n_pend = 0;
                 if (F.moved_mirror) *F.moved_mirror = F.ctl->moved;
+                if (F.mirror && F.peak_out) {  // (a replay's last step) the requests' peak over the replay, then anew
+                    F.mirror[2] = max(F.ctl->req_peak, peak);
+                    F.ctl->req_peak = 0;
+                }
                 if (F.advance) F.ctl->t_base += F.advance;
             }
             return stale_f;
         }
     }
     if (tid == 0) {
-        int n = 0;
+        int n = 0, nall = 0;
         for (int r = 0; r < F.world; ++r) {
             base[r] = n;
-            n += min(r == 0 ? nreq0 : rec_header(F, r)->nreq, F.rec_cap);
+            const RecHeader *h = rec_header(F, r);
+            const int nr = min(r == 0 ? nreq0 : h->nreq, F.rec_cap);
+            n += nr;
+            nall += max(nr, h->nreq_all);
         }
         base[F.world] = n;
         s_flags[0] = n;
         s_flags[1] = 0;
+        s_flags[2] = nall;
     }
     // (slot s0 + q for q < kFinPre from the registers -- unrolled, static indices -- then any further ones)
 #pragma unroll
@@ -1642,7 +1695,7 @@ __device__ int finalize_block(const FinArgs &F, unsigned char *smem) {
     const int A = min(min(nreq, F.req_max), nfree);  // accepted this step (block-uniform)
     if (tid == 0) {
         F.ctl->n_new += A;
-        F.ctl->n_rejected += nreq - A;
+        F.ctl->n_rejected += s_flags[2] - A;  // (every rank's requests, also those its selection did not send)
     }
     if (A > 0) {  // block-uniform
         // the A requests of lowest scan position: all of them, or those up to the A-th smallest
@@ -1806,6 +1859,10 @@ __device__ int finalize_block(const FinArgs &F, unsigned char *smem) {
     }
     if (tid == 0) {
         if (F.moved_mirror) *F.moved_mirror = F.ctl->moved;  // (host-mapped: the host's lagged re-sort decision)
+        if (F.mirror && F.peak_out) {
+            F.mirror[2] = max(F.ctl->req_peak, peak);
+            F.ctl->req_peak = 0;
+        }
         if (F.advance) F.ctl->t_base += F.advance;  // nothing after this step reads t_base before the next replay
     }
     return stale;
@@ -1968,6 +2025,7 @@ __global__ __launch_bounds__(kFinThreads) void np8_step_tail(AssignArgs A, FinAr
                          reinterpret_cast<int *>(smem));
     int stale = 1;
     if (T.fin) stale = finalize_block(F, smem);
+    if (stale < 0) return;  // a halted compact graph: nothing applied, no lists
     if (T.prune == 1 || (T.prune == 2 && stale)) {
         prune_block<D>(P, smem, T.lds_bytes);
         if (T.prune == 2 && threadIdx.x == 0) P.ctl->list_builds += 1u;
@@ -2128,7 +2186,7 @@ __global__ __launch_bounds__(256) void np8_snapshot(SnapArgs A) {
 // A snapshot the folded check left pending (ctl->snap_pend, consumed otherwise by the next np8_assign_fast): the
 // labelling, counts and parameters as they stand; the host clears the flag behind this launch.
 __global__ __launch_bounds__(256) void np8_snapshot_flush(SnapArgs A, const Ctl *__restrict__ ctl) {
-    if (!ctl->snap_pend) return;
+    if (!ctl->snap_pend || ctl->halt) return;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x, g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (g == 0) A.ctl->best_sorted = 0;
     for (int64_t i = g; i < A.n_loc; i += stride) A.z_best[i] = A.z[i];
@@ -2484,7 +2542,9 @@ hipError_t np8_launch_assign(const AssignArgs &A, int D, int M, int prior, hipSt
 // one workgroup reading all records (250 KB at C3) took 14 us, latency bound.
 constexpr int kFoldPer = 1;
 
-__global__ __launch_bounds__(256) void np8_fold_r2(const WaveR2 *__restrict__ wr2, int64_t n, double *r2, int kcap) {
+__global__ __launch_bounds__(256) void np8_fold_r2(const WaveR2 *__restrict__ wr2, int64_t n, double *r2, int kcap,
+                                                   const Ctl *__restrict__ ctl) {
+    if (ctl->halt) return;
     const int64_t k0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * kFoldPer;
     unsigned long long *cur = reinterpret_cast<unsigned long long *>(r2 + kcap);
     int32_t sl = -1;
@@ -2517,10 +2577,10 @@ __global__ __launch_bounds__(256) void np8_fold_r2(const WaveR2 *__restrict__ wr
     }
 }
 
-hipError_t np8_launch_fold_r2(const WaveR2 *wr2, int64_t n, double *r2, int kcap, hipStream_t s) {
+hipError_t np8_launch_fold_r2(const WaveR2 *wr2, int64_t n, double *r2, int kcap, const Ctl *ctl, hipStream_t s) {
     if (n <= 0) return hipSuccess;
     const int64_t lanes = (n + kFoldPer - 1) / kFoldPer;
-    hipLaunchKernelGGL(np8_fold_r2, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, s, wr2, n, r2, kcap);
+    hipLaunchKernelGGL(np8_fold_r2, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, s, wr2, n, r2, kcap, ctl);
     return hipGetLastError();
 }
 
@@ -2745,6 +2805,11 @@ hipError_t np8_launch_fin_prune(const FinArgs &F, const PruneArgs &P, hipStream_
     return hipGetLastError();
 }
 
+hipError_t np8_launch_ll_header(const Ctl *ctl, const Fx *llpart, int64_t ll_n, unsigned char *rec, hipStream_t s) {
+    hipLaunchKernelGGL(np8_ll_header, dim3(1), dim3(kFinThreads), 0, s, ctl, llpart, ll_n, rec);
+    return hipGetLastError();
+}
+
 hipError_t np8_launch_req_select(const unsigned char *stage, int64_t stage_cap, unsigned char *rec, int64_t rec_cap,
                                  int kcap, int D, int req_max, const Fx *llpart, int64_t ll_n, hipStream_t s) {
     hipLaunchKernelGGL(np8_req_select, dim3(1), dim3(kFinThreads), sizeof(int) * 2048, s, stage, stage_cap, rec, rec_cap,
@@ -2812,6 +2877,7 @@ hipError_t np8_launch_mh_g0(const ParamArgs &A, hipStream_t s) {
 // lane checks its own distance against the radius its list was built for (np8_assign).
 template <int DT>
 __global__ __launch_bounds__(256) void np8_prune(PruneArgs A) {
+    if (A.ctl->halt) return;  // a halted compact sweep graph
     const int K = A.ctl->K;
     if (blockIdx.x == 0 && threadIdx.x == 0) A.ctl->lists_ok = 1;
     const double *src = A.r2 + (A.gathered ? A.kcap : 0);
@@ -2824,7 +2890,23 @@ __global__ __launch_bounds__(256) void np8_prune(PruneArgs A) {
         prune_row<DT>(A.cand, R2of, A.plist, A.plen, A.plr2, A.plen_s, A.plr2_s, A.ls, A.D, K, k0, A.lb, A.kcap);
 }
 
-__global__ void np8_advance_epoch(Ctl *ctl, uint32_t n) { ctl->t_base += n; }
+__global__ void np8_advance_epoch(Ctl *ctl, uint32_t n) {
+    if (!ctl->halt) ctl->t_base += n;
+}
+
+// a Ctl flag cleared in stream order, unless a compact sweep graph is halted (which = 0: best_sorted, 1: snap_pend)
+__global__ void np8_ctl_clear(Ctl *ctl, int which) {
+    if (ctl->halt) return;
+    if (which == 0)
+        ctl->best_sorted = 0;
+    else
+        ctl->snap_pend = 0;
+}
+
+hipError_t np8_launch_ctl_clear(Ctl *ctl, int which, hipStream_t s) {
+    hipLaunchKernelGGL(np8_ctl_clear, dim3(1), dim3(1), 0, s, ctl, which);
+    return hipGetLastError();
+}
 
 hipError_t np8_launch_prune(const PruneArgs &A, int kcap, hipStream_t s) {
     const int nb = (kcap + 3) / 4;
@@ -2858,7 +2940,7 @@ hipError_t np8_launch_snapshot_flush(const SnapArgs &A, Ctl *ctl, hipStream_t s)
 
 __global__ __launch_bounds__(256) void np8_best_copy(const Ctl *__restrict__ ctl, const int32_t *__restrict__ src,
                                                      int32_t *__restrict__ dst, int64_t n) {
-    if (!ctl->best_sorted) return;
+    if (!ctl->best_sorted || ctl->halt) return;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
         dst[i] = src[i];
 }
@@ -2866,7 +2948,7 @@ __global__ __launch_bounds__(256) void np8_best_copy(const Ctl *__restrict__ ctl
 __global__ __launch_bounds__(256) void np8_best_scatter(const Ctl *__restrict__ ctl, const int32_t *__restrict__ ids,
                                                         const int32_t *__restrict__ src, int32_t *__restrict__ dst,
                                                         int64_t n) {
-    if (!ctl->best_sorted) return;
+    if (!ctl->best_sorted || ctl->halt) return;
     for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (int64_t)gridDim.x * blockDim.x)
         dst[ids[p]] = src[p];
 }
@@ -2880,7 +2962,7 @@ hipError_t np8_launch_best_unsort(Ctl *ctl, const int32_t *ids, int32_t *z_best,
     hipLaunchKernelGGL(np8_best_scatter, dim3((unsigned)nb), dim3(256), 0, s, ctl, ids, scratch, z_best, n);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    return hipMemsetAsync(&ctl->best_sorted, 0, sizeof(int32_t), s);
+    return np8_launch_ctl_clear(ctl, 0, s);
 }
 
 hipError_t np8_launch_snapshot(const SnapArgs &A, hipStream_t s) {

@@ -330,7 +330,8 @@ __device__ __forceinline__ bool init_ok_records(const NiwArgs &A) { return A.ini
 // (D - 1 - a, D - 1 - b) = S_ab, a <= b: where np8_niw_post forms J Psin J), s1 in s1.  Scratch: an int list of cap entries (Li's storage, unused until the factor exists).
 __device__ __forceinline__ void reduce_run_records(const NiwArgs &A, int s, const double *acc, double *L, int LD, double *s1, int *list,
                                    int cap) {
-    const int D = A.D, T = D / 16, NT = T * (T + 1) / 2, RS = NT * 4 * 64 + T * 16;
+    // (the records' layout is np8_suffstats_wide's at DT: rows and columns >= D are the zero rows of the items)
+    const int D = A.D, T = A.DT / 16, NT = T * (T + 1) / 2, RS = NT * 4 * 64 + T * 16;
     const int tid = threadIdx.x, nt = blockDim.x, lane = tid & 63, wv = tid >> 6, nw = nt >> 6;
     __shared__ int woff[17];
     const int64_t per = (A.n_rec + nt - 1) / nt, h0 = (int64_t)tid * per, h1 = min(A.n_rec, h0 + per);
@@ -402,10 +403,10 @@ __device__ __forceinline__ void reduce_run_records(const NiwArgs &A, int s, cons
             }
             const int tj = ti + qq;
             const int a = 16 * ti + (ln >> 4) + 4 * r, b = 16 * tj + (ln & 15);
-            if (a <= b) L[(D - 1 - a) * LD + (D - 1 - b)] = acc[D + pix(D, a, b)] + vk;
+            if (a <= b && b < D) L[(D - 1 - a) * LD + (D - 1 - b)] = acc[D + pix(D, a, b)] + vk;
         } else {
             const int kk = e - NT * 256, dim = 16 * (kk >> 4) + (kk & 15);
-            s1[dim] = acc[dim] + vk;
+            if (dim < D) s1[dim] = acc[dim] + vk;
         }
     }
 }
@@ -637,9 +638,9 @@ __global__ __launch_bounds__(kNiwThreads) void np8_niw_post(NiwArgs A) {
                                       row >= 0 ? A.cand + (int64_t)row * cand_stride(D) + D : nullptr);
     NIW_T(6)
     if (A.wA) {  // the wide path: the contraction rows from R itself, the eigenvalue bound from Sigma's row sums
-        const int NCH = (D / 16) * (D / 16 + 1) / 2;
-        wide_write_rows(D, F, LD, mun, A.wA + (int64_t)s * D * D, A.wfrag + (int64_t)s * (NCH * 256 + D),
-                        A.wmu + (int64_t)s * D);
+        const int DT = A.DT, NCH = (DT / 16) * (DT / 16 + 1) / 2;
+        wide_write_rows(D, DT, F, LD, mun, A.wA + (int64_t)s * DT * DT, A.wfrag + (int64_t)s * (NCH * 256 + DT),
+                        A.wmu + (int64_t)s * DT);
     }
     if (bound) {
         // lambda_min(P) = 1 / lambda_max(Sigma), lambda_max(Sigma) = rho(Sigma) <= ||Sigma^n||^(1/n), n = 2^k (any

@@ -1,4 +1,5 @@
-// np8_wide.hip -- the wide path (DESIGN.md "Wide path"; BASELINE.json config C5): D in {32, 48, 64}, items
+// np8_wide.hip -- the wide path (DESIGN.md "Wide path"; BASELINE.json config C5): 16 < D <= 80 (kernels instantiated
+// for DT = D rounded up to 16 in {32, 48, 64, 80}; item rows, factors and means beyond D are zero), items
 // held in fp32, cluster likelihoods through fp32 MFMA (v_mfma_f32_16x16x4_f32, exact k-ordered fmaf
 // chains), everything else (auxiliary draws, the categorical pick, counts) in fp64 as on the narrow path.
 //
@@ -49,28 +50,29 @@ __device__ __forceinline__ int64_t wpos_to_local(const AssignArgs &A, int64_t p)
 
 // |U^T (x - mu0)| with U^T packed upper in hyp (the item frame of the auxiliary draws): the loop order
 // of whiten() + norm_of(); the whitened vector itself is never stored.
-template <int D>
-__device__ __forceinline__ double wide_whiten_norm(const double *__restrict__ hyp, const float (&xf)[D]) {
-    const double *U = hyp + D;
-    double dx[D];
+// uw: mu0 and U^T packed for DT (AssignArgs::uw; zero beyond D, as the item rows): the extra terms are exact zeros,
+// fma(0, 0, t) = t, so the norm is the one over the data's D dims.
+template <int DT>
+__device__ __forceinline__ double wide_whiten_norm(const double *__restrict__ uw, const float (&xf)[DT]) {
+    const double *U = uw + DT;
+    double dx[DT];
 #pragma unroll
-    for (int a = 0; a < D; ++a) dx[a] = (double)xf[a] - hyp[a];
+    for (int a = 0; a < DT; ++a) dx[a] = (double)xf[a] - uw[a];
     double n2 = 0.0;
     int k = 0;
 #pragma unroll
-    for (int a = 0; a < D; ++a) {  // fully unrolled: register operands, U through the scalar cache
+    for (int a = 0; a < DT; ++a) {  // fully unrolled: register operands, U through the scalar cache
         double t0 = U[k++] * dx[a];
 #pragma unroll
-        for (int b = a + 1; b < D; ++b) t0 = fma(U[k++], dx[b], t0);
+        for (int b = a + 1; b < DT; ++b) t0 = fma(U[k++], dx[b], t0);
         n2 = fma(t0, t0, n2);
     }
     return sqrt(n2);
 }
 
 // The request payload of the wide path: (|y0|, y0) with y0 = U^T (x - mu0), read from global memory.
-template <int D>
-__device__ void wide_frame_payload(const double *__restrict__ hyp, const float *__restrict__ X, int64_t n, int64_t xr,
-                                   double *vmu) {
+__device__ void wide_frame_payload(const double *__restrict__ hyp, int D, const float *__restrict__ X, int64_t n,
+                                   int64_t xr, double *vmu) {
     const double *U = hyp + D;
     double n2 = 0.0;
     int k = 0;
@@ -83,10 +85,10 @@ __device__ void wide_frame_payload(const double *__restrict__ hyp, const float *
     vmu[0] = sqrt(n2);
 }
 
-template <int D, int PRIOR>
-__device__ __forceinline__ double wide_aux_ll(const double *__restrict__ hyp, double ny, uint64_t seed, uint64_t ig,
-                                              uint32_t t, int m) {
-    constexpr int DP = D * (D + 1) / 2;
+template <int PRIOR>
+__device__ __forceinline__ double wide_aux_ll(const double *__restrict__ hyp, int D, double ny, uint64_t seed,
+                                              uint64_t ig, uint32_t t, int m) {
+    const int DP = D * (D + 1) / 2;
     const double caux = hyp[D + DP], rsk = hyp[D + DP + 1], nu = hyp[D + DP + 3];
     if constexpr (PRIOR == kPriorNiw) {
         double sumlog, b00, chi, z1;
@@ -94,7 +96,7 @@ __device__ __forceinline__ double wide_aux_ll(const double *__restrict__ hyp, do
         return niw_aux_loglik(ny, sumlog, b00, chi, z1, rsk, caux);
     } else {
         double v, xpar, chi2;
-        aux_core<D>(seed, ig, t, m, nu, v, xpar, chi2);
+        aux_core_rt(seed, ig, t, m, D, nu, v, xpar, chi2);
         return aux_loglik(ny, v, xpar, chi2, D, rsk, caux);
     }
 }
@@ -188,6 +190,8 @@ constexpr double kLamRelWidth = NP8_LAM_REL_WIDTH;  // ... or fewer, once the br
 // (wave 0) and P - beta_q I for the three betas of an eigenvalue round (waves 1-3).
 // LDS: four [D][D + 1] double matrices (133 KB at D = 64): the factor's work matrix (R in place), three tests.
 constexpr int kPanel = 16;
+// Cholesky tests np8_wide_rows runs beside the factor: three, or two when four D x (D + 1) doubles exceed the LDS.
+__host__ __device__ constexpr int wide_rows_tests(int D) { return D <= 64 ? 3 : 2; }
 
 // Panel p of matrix M (rows c0 .. c0 + 15, columns c0 .. D - 1) on one wave, lane = column.  Factor form (test =
 // false): row jj of R = row jj / sqrt(pivot); a non-positive pivot is replaced by 1e-300 and its column skips every
@@ -198,11 +202,12 @@ __device__ __forceinline__ void panel_factor(double *M, int LD, int D, int c0, b
     const int lane = threadIdx.x & 63;
     double w[kPanel];
 #pragma unroll
-    for (int i = 0; i < kPanel; ++i) w[i] = (lane < D) ? M[(c0 + i) * LD + lane] : 0.0;
+    for (int i = 0; i < kPanel; ++i) w[i] = (lane < D && c0 + i < D) ? M[(c0 + i) * LD + lane] : 0.0;
     int sk = 0, fl = 0;
 #pragma unroll
     for (int j = 0; j < kPanel; ++j) {
         const int jj = c0 + j;
+        if (jj >= D) break;  // (the last panel of a D that is not a multiple of 16)
         const double v = __shfl(w[j], jj);  // the pivot (row jj, column jj: lane jj)
         if (test) {
             if (!(v > 0.0) || fl) {
@@ -234,7 +239,7 @@ __device__ __forceinline__ void panel_factor(double *M, int LD, int D, int c0, b
     }
 #pragma unroll
     for (int i = 0; i < kPanel; ++i)
-        if (lane < D && lane >= c0 + i) M[(c0 + i) * LD + lane] = w[i];
+        if (lane < D && lane >= c0 + i && c0 + i < D) M[(c0 + i) * LD + lane] = w[i];
     if (lane == 0) {
         *skip = sk;
         *fail = fl;
@@ -276,6 +281,7 @@ __global__ __launch_bounds__(256) void np8_wide_rows(WideArgs W) {
     const int s = blockIdx.x;
     if (!W.dirty[s] || W.cnt[s] <= 0) return;  // block-uniform
     const int D = W.D, LD = D + 1, tid = threadIdx.x, wv = tid >> 6;
+    const int nq = wide_rows_tests(D);  // concurrent Cholesky tests: three, two above D = 64 (LDS)
     extern __shared__ __attribute__((aligned(16))) double smr[];
     double *Wk = smr, *C0 = Wk + D * LD;  // C0 + q * D * LD: test matrix q; R = the upper triangle of Wk at the end
     const double *Pp = W.slot_P + (int64_t)s * (D * (D + 1) / 2);
@@ -313,24 +319,25 @@ __global__ __launch_bounds__(256) void np8_wide_rows(WideArgs W) {
                 beta[0] = 0.93 * prev;
                 beta[1] = 0.98 * prev;
                 beta[2] = fmin(1.02 * prev, 0.5 * (prev + hi));
+                if (nq == 2) beta[1] = beta[2];
             } else {
 #pragma unroll
-                for (int q = 0; q < 3; ++q) beta[q] = lo + (hi - lo) * (0.25 * (q + 1));
+                for (int q = 0; q < 3; ++q) beta[q] = lo + (hi - lo) * ((double)(q + 1) / (nq + 1));
             }
-            for (int k = tid; k < 3 * D * D; k += blockDim.x) {
+            for (int k = tid; k < nq * D * D; k += blockDim.x) {
                 const int q = k / (D * D), kk = k - q * D * D, a = kk / D, b = kk - a * D;
                 if (b >= a) C0[q * D * LD + a * LD + b] = (a == b) ? pget(a, a) - beta[q] : pget(a, b);
             }
-            if (tid < 4) fail_s[tid] = 0;
+            if (tid < 4) fail_s[tid] = (tid < 3 && tid >= nq) ? 1 : 0;  // (a test not run: "not positive definite")
             __syncthreads();
         }
         if (!factor && !tests) break;
-        for (int p = 0; p < D / kPanel; ++p) {
+        for (int p = 0; p * kPanel < D; ++p) {
             const int c0 = p * kPanel;
             // panel steps: wave 0 the factor (first pass), wave q + 1 test q (a failed test stops)
             if (wv == 0 && factor) {
                 panel_factor(Wk, LD, D, c0, false, nullptr, &skip_s[0], &fail_s[3]);
-            } else if (wv > 0 && tests && !fail_s[wv - 1]) {
+            } else if (wv > 0 && wv <= nq && tests && !fail_s[wv - 1]) {
                 int dummy;
                 panel_factor(C0 + (wv - 1) * D * LD, LD, D, c0, true, rk_s[wv], &dummy, &fail_s[wv - 1]);
             }
@@ -340,7 +347,7 @@ __global__ __launch_bounds__(256) void np8_wide_rows(WideArgs W) {
                 panel_trailing(Wk, LD, D, c0, false, nullptr, skip_s[0]);
             }
             if (tests)
-                for (int q = 0; q < 3; ++q)
+                for (int q = 0; q < nq; ++q)
                     if (!fail_s[q]) panel_trailing(C0 + q * D * LD, LD, D, c0, true, rk_s[q + 1], 0);
             __syncthreads();
         }
@@ -355,15 +362,15 @@ __global__ __launch_bounds__(256) void np8_wide_rows(WideArgs W) {
         const int pd = (!fail_s[0]) | ((!fail_s[1]) << 1) | ((!fail_s[2]) << 2);
         const int top = (pd & 4) ? 3 : (pd & 2) ? 2 : (pd & 1) ? 1 : 0;
         if (top > 0) lo = beta[top - 1];
-        if (top < 3) hi = beta[top];
+        if (top < nq) hi = beta[top];
         __syncthreads();  // (fail_s read by every thread before the next round resets it)
         if (hi - lo <= kLamRelWidth * hi) break;  // block-uniform
     }
     // 1% for the fp32 factor and the fp32 contraction, and the Cholesky's own rounding
     if (lam && tid == 0) W.lam_lo[s] = 0.99 * lo;
-    const int NCH = (D / 16) * (D / 16 + 1) / 2;
-    wide_write_rows(D, Wk, LD, W.slot_mu + (int64_t)s * D, W.wA + (int64_t)s * D * D, W.wfrag + (int64_t)s * (NCH * 256 + D),
-                    W.wmu + (int64_t)s * D);
+    const int DT = W.DT, NCH = (DT / 16) * (DT / 16 + 1) / 2;
+    wide_write_rows(D, DT, Wk, LD, W.slot_mu + (int64_t)s * D, W.wA + (int64_t)s * DT * DT,
+                    W.wfrag + (int64_t)s * (NCH * 256 + DT), W.wmu + (int64_t)s * DT);
 #ifdef NP8_EXP_WIDE_TIMING
     WR_T(15)
     if (tid == 0 && s < 3)
@@ -380,10 +387,10 @@ __global__ __launch_bounds__(256) void np8_wide_dist(WideArgs W) {
     if (j0 >= K) return;
     const int D = W.D, DP = D * (D + 1) / 2, CS = cand_stride(D);
     const int s0 = (int)W.cand[(int64_t)j0 * CS + D + DP + kFieldSlot];
-    const float *m0 = W.wmu + (int64_t)s0 * D;
+    const float *m0 = W.wmu + (int64_t)s0 * W.DT;
     for (int j = threadIdx.x; j < K; j += blockDim.x) {
         const int sj = (int)W.cand[(int64_t)j * CS + D + DP + kFieldSlot];
-        const float *mj = W.wmu + (int64_t)sj * D;
+        const float *mj = W.wmu + (int64_t)sj * W.DT;
         double d2 = 0.0;
         for (int a = 0; a < D; ++a) {
             const double dd = (double)mj[a] - (double)m0[a];
@@ -402,13 +409,13 @@ __global__ void np8_wide_clean(WideArgs W) {
 // DIAGU: the base measure's whitening U^T is diagonal (Psi0 or Lambda diagonal, every configuration the
 // benchmarks run): |U^T (x - mu0)| streams over the item's dims, as wide_whiten_norm's operations with the
 // zero terms left out (fma(0, t, v) = v), instead of holding D doubles of x - mu0.
-template <int D, int M, int PRIOR, bool DIAGU>
+template <int DT, int M, int PRIOR, bool DIAGU>
 #ifndef NP8_WIDE_WAVES
 #define NP8_WIDE_WAVES 2
 #endif
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NP8_WIDE_WAVES, NP8_WIDE_WAVES))) void np8_assign_wide(AssignArgs A) {
-    using W = Wide<D>;
-    constexpr int CS = W::CS, F = W::F;
+    using W = Wide<DT>;
+    const int D = A.dim, DP = D * (D + 1) / 2, CS = cand_stride(D), F = D + DP;  // (the data's D: hyp, cand, records)
     extern __shared__ __attribute__((aligned(16))) float stage[];
     const int lane = threadIdx.x & 63, g = lane >> 4, col = lane & 15;
     const int64_t pw = A.p0 + (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63);
@@ -441,7 +448,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NP8_WIDE_WA
     double ny;
     if constexpr (DIAGU) {
         const double *U = hyp + D;
-        const float *mo = A.wmu + (int64_t)zi * D;
+        const float *mo = A.wmu + (int64_t)zi * DT;
         double n2 = 0.0, d2 = 0.0;
 #pragma unroll 16
         for (int a = 0; a < D; ++a) {
@@ -455,14 +462,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NP8_WIDE_WA
         ny = sqrt(n2);
         if (A.wdist) rown = sqrt(d2);
     } else {
-        float xf[D];
+        float xf[DT];
 #pragma unroll
-        for (int a = 0; a < D; ++a) xf[a] = X[(int64_t)a * n + xr];
-        ny = wide_whiten_norm<D>(hyp, xf);
+        for (int a = 0; a < DT; ++a) xf[a] = X[(int64_t)a * n + xr];  // (rows >= D: zeros)
+        ny = wide_whiten_norm<DT>(A.uw, xf);
 #pragma unroll
-        for (int a = 0; a < D; ++a) x2 = fma((double)xf[a], (double)xf[a], x2);
+        for (int a = 0; a < DT; ++a) x2 = fma((double)xf[a], (double)xf[a], x2);  // (rows >= D: + 0)
         if (A.wdist) {  // the item's distance to its own row's fp32 mean (candidate pruning)
-            const float *mo = A.wmu + (int64_t)zi * D;
+            const float *mo = A.wmu + (int64_t)zi * DT;
             double d2 = 0.0;
 #pragma unroll
             for (int a = 0; a < D; ++a) {
@@ -497,7 +504,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NP8_WIDE_WA
         ++own_passes;
         const int lead = __ffsll((unsigned long long)pend) - 1;
         const int32_t sj = __shfl(zi, lead);
-        const double q = wide_pass<D>(A.wfrag + (int64_t)sj * W::ROW, xb, lane);
+        const double q = wide_pass<DT>(A.wfrag + (int64_t)sj * W::ROW, xb, lane);
         const bool mine = valid && zi == sj;
         if (mine) {
             const double *e = cand + (int64_t)jo * CS;
@@ -510,22 +517,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NP8_WIDE_WA
     // T_own - kSkip (the pick's T only grows), so most of them skip their D chi^2 draws
     double lwa[M];
     {
-        const double logam = hyp[D + W::DP + 2];
+        const double logam = hyp[D + DP + 2];
         bool all_below = false;  // (level 0: no auxiliary of this item can reach the skip threshold, whatever its draws)
         if constexpr (PRIOR == kPriorNiw)
-            all_below = niw_aux_all_below(ny, hyp[D + W::DP + 3], hyp[D + W::DP + 1], hyp[D + W::DP],
-                                          hyp[D + W::DP + 4 + W::DP], st.T - kSkip - logam);
+            all_below = niw_aux_all_below(ny, hyp[D + DP + 3], hyp[D + DP + 1], hyp[D + DP],
+                                          hyp[D + DP + 4 + DP], st.T - kSkip - logam);
 #pragma unroll
         for (int k = 0; k < M; ++k) lwa[k] = kZeroLogWeight + logam;
 #pragma unroll 1
         for (int m = 0; m < (all_below ? 0 : M); ++m) {
             double v;
             if constexpr (PRIOR == kPriorNiw) {
-                const double caux = hyp[D + W::DP], rsk = hyp[D + W::DP + 1], nu = hyp[D + W::DP + 3];
-                const double smax = hyp[D + W::DP + 4 + W::DP];
+                const double caux = hyp[D + DP], rsk = hyp[D + DP + 1], nu = hyp[D + DP + 3];
+                const double smax = hyp[D + DP + 4 + DP];
                 v = niw_aux_ll_screened(A.seed, ig, t, m, D, nu, ny, rsk, caux, smax, st.T - kSkip - logam) + logam;
             } else {
-                v = wide_aux_ll<D, PRIOR>(hyp, ny, A.seed, ig, t, m) + logam;
+                v = wide_aux_ll<PRIOR>(hyp, D, ny, A.seed, ig, t, m) + logam;
             }
 #pragma unroll
             for (int k = 0; k < M; ++k) lwa[k] = (k == m) ? v : lwa[k];  // no dynamic register index
@@ -617,7 +624,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NP8_WIDE_WA
     if (prune) {
         const int n1 = rlist_n[0];
         if (wave_live && n1 > 0) {
-            using W2 = Wide<D>;
+            using W2 = Wide<DT>;
             const double Tl = valid ? st.T : 1e300;
             double Ti[4], x2i[4];
             int32_t zit[4];
@@ -709,17 +716,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NP8_WIDE_WA
     // the evaluated candidates in ascending order, block-uniform: the next one is copied into the other
     // stage while the MFMAs of this one run; one barrier per row
     int buf = 0, rows_done = 0;
-    if (nrows > 0) row_glds<D>(A.wfrag, (int)cand[(int64_t)row_at(0) * CS + F + kFieldSlot], stage);
+    if (nrows > 0) row_glds<DT>(A.wfrag, (int)cand[(int64_t)row_at(0) * CS + F + kFieldSlot], stage);
     __syncthreads();
     for (int i = 0; i < nrows; ++i) {
         const int j = row_at(i);
         const double *e = cand + (int64_t)j * CS;  // block-uniform: scalar loads
         const int32_t sj = (int32_t)e[F + kFieldSlot];
         if (i + 1 < nrows)
-            row_glds<D>(A.wfrag, (int)cand[(int64_t)row_at(i + 1) * CS + F + kFieldSlot], stage + (buf ^ 1) * W::ROW);
+            row_glds<DT>(A.wfrag, (int)cand[(int64_t)row_at(i + 1) * CS + F + kFieldSlot], stage + (buf ^ 1) * W::ROW);
         const float *row = stage + buf * W::ROW;
         if (wave_live) {
-            const double q = wide_pass<D>(row, xb, lane);
+            const double q = wide_pass<DT>(row, xb, lane);
             if (sj != zi) pick_step(st, fma(-0.5, q, e[F + kFieldC]) + e[F + kFieldLogn], j);
         }
         __syncthreads();  // the next row has landed (vmcnt(0)); this row's stage may be overwritten
@@ -765,7 +772,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NP8_WIDE_WA
             r.dll.hi = 0;
             A.req[q] = r;
             double *vmu = A.vmu + (int64_t)q * (D + 1);
-            wide_frame_payload<D>(hyp, X, n, xr, vmu);
+            wide_frame_payload(hyp, D, X, n, xr, vmu);
         }
     }
 }
@@ -773,38 +780,38 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NP8_WIDE_WA
 // ---- max likelihood and parity ---------------------------------------------------------------------
 // q of item x (fp32 values) against slot sj on the vector ALU: the same fmaf chains (zero terms of the
 // triangular A skipped) and the same fp64 summation order as wide_pass.
-template <int D>
+template <int DT>
 __device__ double wide_q_valu(const WideArgs &W, const float *__restrict__ X, int64_t n, int64_t xr, int sj) {
-    const float *Aj = W.wA + (int64_t)sj * D * D;
-    const float *mj = W.wmu + (int64_t)sj * D;
-    float xt[D];
+    const float *Aj = W.wA + (int64_t)sj * DT * DT;
+    const float *mj = W.wmu + (int64_t)sj * DT;
+    float xt[DT];
 #pragma unroll
-    for (int b = 0; b < D; ++b) xt[b] = X[(int64_t)b * n + xr] - mj[b];
+    for (int b = 0; b < DT; ++b) xt[b] = X[(int64_t)b * n + xr] - mj[b];
     float sg[4] = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-    for (int mt = 0; mt < D / 16; ++mt)
+    for (int mt = 0; mt < DT / 16; ++mt)
 #pragma unroll
         for (int r = 0; r < 4; ++r)
 #pragma unroll
             for (int gg = 0; gg < 4; ++gg) {
                 const int a = 16 * mt + 4 * gg + r;
                 float v = 0.0f;
-                for (int b = a; b < D; ++b) v = fmaf(Aj[(int64_t)a * D + b], xt[b], v);
+                for (int b = a; b < DT; ++b) v = fmaf(Aj[(int64_t)a * DT + b], xt[b], v);
                 sg[gg] = fmaf(v, v, sg[gg]);
             }
     return (double)((sg[0] + sg[1]) + (sg[2] + sg[3]));
 }
 
-template <int D>
+template <int DT>
 __global__ __launch_bounds__(256) void np8_loglik_wide(LoglikArgs L, WideArgs W) {
-    constexpr int CS = Wide<D>::CS, F = Wide<D>::F;
+    const int CS = cand_stride(W.D), F = W.D + W.D * (W.D + 1) / 2;
     __shared__ double red[256];
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     double ll = 0.0;
     if (i < L.n_loc) {
         const int32_t s = L.z[i];
         const double *e = L.cand + (int64_t)L.dense_of[s] * CS;
-        ll = fma(-0.5, wide_q_valu<D>(W, reinterpret_cast<const float *>(L.X), L.n_loc, i, s), e[F + kFieldC]);
+        ll = fma(-0.5, wide_q_valu<DT>(W, reinterpret_cast<const float *>(L.X), L.n_loc, i, s), e[F + kFieldC]);
     }
     red[threadIdx.x] = ll;
     __syncthreads();
@@ -815,10 +822,10 @@ __global__ __launch_bounds__(256) void np8_loglik_wide(LoglikArgs L, WideArgs W)
     if (threadIdx.x == 0) L.partial[blockIdx.x] = red[0];
 }
 
-template <int D, int M, int PRIOR>
+template <int DT, int M, int PRIOR>
 __global__ __launch_bounds__(64) void np8_loglik_matrix_wide(AssignArgs A, WideArgs W, const int64_t *__restrict__ idx,
                                                              int64_t n, double *__restrict__ out) {
-    constexpr int CS = Wide<D>::CS, F = Wide<D>::F;
+    const int D = W.D, CS = cand_stride(D), F = D + D * (D + 1) / 2;
     const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= n) return;
     const int64_t il = idx[r];
@@ -826,23 +833,25 @@ __global__ __launch_bounds__(64) void np8_loglik_matrix_wide(AssignArgs A, WideA
     const int K = A.ctl->K;
     for (int j = 0; j < K; ++j) {
         const double *e = A.cand + (int64_t)j * CS;
-        out[r * (K + M) + j] = fma(-0.5, wide_q_valu<D>(W, X, A.n_loc, il, (int)e[F + kFieldSlot]), e[F + kFieldC]);
+        out[r * (K + M) + j] = fma(-0.5, wide_q_valu<DT>(W, X, A.n_loc, il, (int)e[F + kFieldSlot]), e[F + kFieldC]);
     }
-    float xf[D];
-    for (int a = 0; a < D; ++a) xf[a] = X[(int64_t)a * A.n_loc + il];
-    const double ny = wide_whiten_norm<D>(A.hyp, xf);
+    float xf[DT];
+#pragma unroll
+    for (int a = 0; a < DT; ++a) xf[a] = X[(int64_t)a * A.n_loc + il];
+    const double ny = wide_whiten_norm<DT>(A.uw, xf);
     const uint32_t t = A.ctl->t_base + A.t;
-    for (int m = 0; m < M; ++m) out[r * (K + M) + K + m] = wide_aux_ll<D, PRIOR>(A.hyp, ny, A.seed, (uint64_t)(A.offset + il), t, m);
+    for (int m = 0; m < M; ++m)
+        out[r * (K + M) + K + m] = wide_aux_ll<PRIOR>(A.hyp, D, ny, A.seed, (uint64_t)(A.offset + il), t, m);
 }
 
 // ---- max likelihood on the matrix cores -------------------------------------------------------------
 // sum_i ll(x_i | theta_{z_i}) (MCMC::considerMaxLikelihood, np_mcmc.cpp:187-203): the own-cluster passes
 // of np8_assign_wide (one MFMA pass per distinct own slot of a wave; one on the label-sorted layout),
 // a fixed-order block reduction into partial[block] (reduced by np8_loglik_reduce).
-template <int D>
+template <int DT>
 __global__ __launch_bounds__(256) void np8_loglik_wide_mfma(AssignArgs A, double *__restrict__ partial) {
-    using W = Wide<D>;
-    constexpr int CS = W::CS, F = W::F;
+    using W = Wide<DT>;
+    const int CS = cand_stride(A.dim), F = A.dim + A.dim * (A.dim + 1) / 2;
     __shared__ double red[256];
     const int lane = threadIdx.x & 63, g = lane >> 4, col = lane & 15;
     const int64_t pw = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63);
@@ -868,7 +877,7 @@ __global__ __launch_bounds__(256) void np8_loglik_wide_mfma(AssignArgs A, double
         uint64_t pend = __ballot(valid);
         while (pend) {
             const int32_t sj = __shfl(zi, __ffsll((unsigned long long)pend) - 1);
-            const double q = wide_pass<D>(A.wfrag + (int64_t)sj * W::ROW, xb, lane);
+            const double q = wide_pass<DT>(A.wfrag + (int64_t)sj * W::ROW, xb, lane);
             const bool mine = valid && zi == sj;
             if (mine) ll = fma(-0.5, q, A.cand[(int64_t)A.dense_of[sj] * CS + F + kFieldC]);
             pend &= ~__ballot(mine);
@@ -886,12 +895,15 @@ __global__ __launch_bounds__(256) void np8_loglik_wide_mfma(AssignArgs A, double
 hipError_t np8_launch_loglik_wide_mfma(const AssignArgs &A, int D, double *partial, hipStream_t s) {
     const int64_t nb = (A.n_loc + 255) / 256;
     if (nb <= 0) return hipSuccess;
-    if (D == 32)
+    const int DT = wide_dt(D);
+    if (DT == 32)
         hipLaunchKernelGGL((np8_loglik_wide_mfma<32>), dim3((unsigned)nb), dim3(256), 0, s, A, partial);
-    else if (D == 48)
+    else if (DT == 48)
         hipLaunchKernelGGL((np8_loglik_wide_mfma<48>), dim3((unsigned)nb), dim3(256), 0, s, A, partial);
-    else if (D == 64)
+    else if (DT == 64)
         hipLaunchKernelGGL((np8_loglik_wide_mfma<64>), dim3((unsigned)nb), dim3(256), 0, s, A, partial);
+    else if (DT == 80)
+        hipLaunchKernelGGL((np8_loglik_wide_mfma<80>), dim3((unsigned)nb), dim3(256), 0, s, A, partial);
     else
         return hipErrorInvalidValue;
     return hipGetLastError();
@@ -914,9 +926,13 @@ constexpr int kSuffChunks = NP8_SUFF_CHUNKS;  // (64-item units per wave)
 
 // BUF: item rows through a buffer descriptor (32-bit offsets: D n 4 < 2^31 bytes), two VGPRs of addressing instead
 // of one 64-bit address per row.
-template <int D, bool BUF>
+// DT: the items' rows (D rounded up to 16, rows >= D zero); statistics and run records in the DT layout, acc in the
+// data's D layout (its packed upper triangle: entries with a row or column >= D are the zero rows, left out).
+template <int DT, bool BUF>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void np8_suffstats_wide(ParamArgs P) {
-    constexpr int T = D / 16, NT = T * (T + 1) / 2, W = D + D * (D + 1) / 2, H = D / 2;
+    constexpr int D = DT;  // (the tile structure; P.D is the data's)
+    constexpr int T = D / 16, NT = T * (T + 1) / 2, H = D / 2;
+    const int Dd = P.D, W = Dd + Dd * (Dd + 1) / 2;
     constexpr int CI = 32;           // items per chunk
     constexpr int PS = 2 * CI + 2;   // floats per dim pair (a, a + H): conflict-free column reads
     constexpr int NCH = 2 * kSuffChunks;
@@ -982,14 +998,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int a = 16 * ti + g + 4 * r, b = 16 * tj + col;  // f64 MFMA layout
-                    if (a <= b) unsafeAtomicAdd(dst + D + a * D - (a * (a - 1)) / 2 + (b - a), acc[q][r]);
+                    if (a <= b && b < Dd) unsafeAtomicAdd(dst + Dd + a * Dd - (a * (a - 1)) / 2 + (b - a), acc[q][r]);
                 }
 #pragma unroll
         for (int t = 0; t < T; ++t) {
             double v = s1[t];
             v += __shfl_xor(v, 16);
             v += __shfl_xor(v, 32);
-            if (g == 0) unsafeAtomicAdd(dst + 16 * t + col, v);
+            if (g == 0 && 16 * t + col < Dd) unsafeAtomicAdd(dst + 16 * t + col, v);
         }
     };
     reset();
@@ -1037,7 +1053,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
                 reset();
                 cs = sl;
 #pragma unroll
-                for (int t = 0; t < T; ++t) anc[t] = P.slot_mu[(int64_t)cs * D + 16 * t + col];
+                for (int t = 0; t < T; ++t) anc[t] = (16 * t + col < Dd) ? P.slot_mu[(int64_t)cs * Dd + 16 * t + col] : 0.0;
             }
             pend &= ~__ballot(zl == sl);
 #pragma unroll 2
@@ -1066,7 +1082,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 // Waves of an np8_suffstats_wide launch over n items, and the doubles of one run record at D (ParamArgs::part).
 int64_t np8_suffstats_wide_waves(int64_t n) { return 4 * ((n + 4 * 64 * kSuffChunks - 1) / (4 * 64 * kSuffChunks)); }  // (64 kSuffChunks items per wave)
 int64_t np8_suffstats_wide_record(int D) {
-    const int T = D / 16;
+    const int T = wide_dt(D) / 16;
     return (int64_t)(T * (T + 1) / 2) * 4 * 64 + T * 16;
 }
 
@@ -1074,9 +1090,9 @@ hipError_t np8_launch_suffstats_wide(const ParamArgs &P, hipStream_t s) {
     const int64_t per_block = 4 * 64 * kSuffChunks;
     const int64_t nb = (P.n_loc + per_block - 1) / per_block;
     if (nb <= 0) return hipSuccess;
-    const bool buf = P.n_loc * P.D * 4 < ((int64_t)1 << 31);
+    const bool buf = P.n_loc * P.DT * 4 < ((int64_t)1 << 31);
 #define NP8_SUFF_LAUNCH(DD)                                                                                   \
-    if (P.D == DD) {                                                                                          \
+    if (P.DT == DD) {                                                                                         \
         if (buf)                                                                                              \
             hipLaunchKernelGGL((np8_suffstats_wide<DD, true>), dim3((unsigned)nb), dim3(256), 0, s, P);       \
         else                                                                                                  \
@@ -1086,16 +1102,20 @@ hipError_t np8_launch_suffstats_wide(const ParamArgs &P, hipStream_t s) {
     NP8_SUFF_LAUNCH(32)
     NP8_SUFF_LAUNCH(48)
     NP8_SUFF_LAUNCH(64)
+    NP8_SUFF_LAUNCH(80)
 #undef NP8_SUFF_LAUNCH
     return hipErrorInvalidValue;
 }
 
 // ---- dispatch ----------------------------------------------------------------------------------------
-#define NP8_WIDE_FOR_EACH(X) X(32, 3) X(48, 3) X(64, 3)
+// tile dimensions DT (D rounded up to 16) the kernels are instantiated for, with M
+#define NP8_WIDE_FOR_EACH(X) X(32, 3) X(48, 3) X(64, 3) X(80, 3)
 
 bool np8_wide_supported(int D, int M) {
+    if (D <= 16) return false;  // (the fp64 path)
+    const int DT = wide_dt(D);
 #define X(d, m) \
-    if (D == d && M == m) return true;
+    if (DT == d && M == m) return true;
     NP8_WIDE_FOR_EACH(X)
 #undef X
     return false;
@@ -1105,8 +1125,9 @@ hipError_t np8_launch_assign_wide(const AssignArgs &A, int D, int M, int prior, 
     const int64_t n = A.p1 - A.p0;
     if (n <= 0) return hipSuccess;
     const dim3 grid((unsigned)((n + 255) / 256)), block(256);
+    const int DT = wide_dt(D);
 #define X(d, m)                                                                                       \
-    if (D == d && M == m) {                                                                           \
+    if (DT == d && M == m) {                                                                          \
         const size_t lds = 2 * sizeof(float) * Wide<d>::ROW;                                          \
         if (prior == kPriorNiw && diag_u)                                                             \
             hipLaunchKernelGGL((np8_assign_wide<d, m, kPriorNiw, true>), grid, block, lds, s, A);     \
@@ -1127,8 +1148,9 @@ hipError_t np8_launch_loglik_matrix_wide(const AssignArgs &A, const WideArgs &W,
                                          const int64_t *idx, int64_t n, double *out, hipStream_t s) {
     if (n <= 0) return hipSuccess;
     const dim3 grid((unsigned)((n + 63) / 64)), block(64);
+    const int DT = wide_dt(D);
 #define X(d, m)                                                                                                    \
-    if (D == d && M == m) {                                                                                        \
+    if (DT == d && M == m) {                                                                                       \
         if (prior == kPriorNiw)                                                                                    \
             hipLaunchKernelGGL((np8_loglik_matrix_wide<d, m, kPriorNiw>), grid, block, 0, s, A, W, idx, n, out);   \
         else                                                                                                       \
@@ -1144,12 +1166,15 @@ hipError_t np8_launch_loglik_matrix_wide(const AssignArgs &A, const WideArgs &W,
 hipError_t np8_launch_loglik_wide(const LoglikArgs &L, const WideArgs &W, int D, hipStream_t s) {
     const int64_t nb = (L.n_loc + 255) / 256;
     if (nb <= 0) return hipSuccess;
-    if (D == 32)
+    const int DT = wide_dt(D);
+    if (DT == 32)
         hipLaunchKernelGGL((np8_loglik_wide<32>), dim3((unsigned)nb), dim3(256), 0, s, L, W);
-    else if (D == 48)
+    else if (DT == 48)
         hipLaunchKernelGGL((np8_loglik_wide<48>), dim3((unsigned)nb), dim3(256), 0, s, L, W);
-    else if (D == 64)
+    else if (DT == 64)
         hipLaunchKernelGGL((np8_loglik_wide<64>), dim3((unsigned)nb), dim3(256), 0, s, L, W);
+    else if (DT == 80)
+        hipLaunchKernelGGL((np8_loglik_wide<80>), dim3((unsigned)nb), dim3(256), 0, s, L, W);
     else
         return hipErrorInvalidValue;
     return hipGetLastError();
@@ -1161,11 +1186,12 @@ hipError_t np8_launch_wide_dist(const WideArgs &W, hipStream_t s) {
 }
 
 hipError_t np8_launch_wide_refresh(const WideArgs &W, hipStream_t s) {
-    const size_t lds = 4 * sizeof(double) * W.D * (W.D + 1);  // 133 KB at D = 64
+    // the factor's matrix and the tests': 133 KB at D = 64, 156 KB at D = 80 (two tests)
+    const size_t lds = (1 + wide_rows_tests(W.D)) * sizeof(double) * W.D * (W.D + 1);
     static bool allowed = false;  // (set before the first launch, which is not inside a graph capture)
     if (!allowed) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&np8_wide_rows),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)(4 * sizeof(double) * 64 * 65));
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)(3 * sizeof(double) * 80 * 81));
         if (e != hipSuccess) return e;
         allowed = true;
     }

@@ -114,6 +114,7 @@ class Stats(C.Structure):
         ("tail_list_builds", C.c_int64),
         ("tail_steps", C.c_int64),
         ("pick_evals", C.c_int64),
+        ("compact_halts", C.c_int64),
     ]
 
 

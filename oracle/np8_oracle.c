@@ -496,7 +496,7 @@ np8o_ctx *np8o_create(const np8o_config *cfg) {
         return NULL;
     if (cfg->prior == NP8O_PRIOR_NIW && !(cfg->nu >= cfg->D + 1.0 && cfg->nu < 1e12)) return NULL;
     if (cfg->contraction != NP8O_CONTRACT_F64 &&
-        !(cfg->contraction == NP8O_CONTRACT_F32 && (cfg->D == 32 || cfg->D == 48 || cfg->D == 64) &&
+        !(cfg->contraction == NP8O_CONTRACT_F32 && cfg->D > 16 && cfg->D <= 80 &&
           cfg->param_update != NP8O_PARAM_MH_G0))
         return NULL;
     if (cfg->req_max < 0 || cfg->req_max > NP8O_REQMAX) return NULL;
@@ -1238,11 +1238,14 @@ static double wide_q(const np8o_ctx *c, const double *x, int sj) {
         const float *col = At + (size_t)b * D;
         for (int a = 0; a <= b; ++a) y[a] = fmaf(col[a], t, y[a]);
     }
+    /* any D: the device pads to DT = D rounded up to 16 with zero rows, whose squares are exact zeros */
     float s[4] = {0.0f, 0.0f, 0.0f, 0.0f};
     for (int g = 0; g < 4; ++g)
-        for (int mt = 0; mt < D / 16; ++mt)
+        for (int mt = 0; mt < (D + 15) / 16; ++mt)
             for (int r = 0; r < 4; ++r) {
-                const float v = y[16 * mt + 4 * g + r];
+                const int a = 16 * mt + 4 * g + r;
+                if (a >= D) continue;
+                const float v = y[a];
                 s[g] = fmaf(v, v, s[g]);
             }
     return (double)((s[0] + s[1]) + (s[2] + s[3]));

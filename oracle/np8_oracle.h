@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define NP8O_DMAX 64
+#define NP8O_DMAX 80
 #define NP8O_MMAX 8
 #define NP8O_KCAP_PICK 4096 /* kcap limit of NP8O_PICK_INVCDF (the weights of one update live on the stack) */
 #define NP8O_REQMAX 4096 /* upper bound of req_max (must match NP8_REQ_MAX) */
@@ -139,7 +139,7 @@ enum { NP8O_PICK_RESERVOIR = 0, NP8O_PICK_INVCDF = 1 };
 
 /* Cluster-likelihood arithmetic (DESIGN.md "Wide path").
  *   F64: fp64 table form, packed sym(Sigma^{-1}) (D <= 16 on the device).
- *   F32: D in {32, 48, 64}: items rounded to fp32 at set_data; per cluster A = fp32(chol_upper(sym Sigma^{-1}))
+ *   F32: 16 < D <= 80 (the device pads to D rounded up to 16): items rounded to fp32 at set_data; per cluster A = fp32(chol_upper(sym Sigma^{-1}))
  *        and muf = fp32(mu); for item x and candidate j:
  *          y_a = fmaf chain_b A_j[a][b] (x_b - muf_j[b]) from 0   (= the MFMA contraction, bit for bit),
  *          q = (s_0 + s_1) + (s_2 + s_3) in fp32, s_g = fp32 fmaf chain of y_a^2 over a = 16 mt + 4 g + r,

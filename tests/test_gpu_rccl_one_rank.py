@@ -37,3 +37,52 @@ def test_one_rank_rccl_sweeps_and_graph_bit_exact(param_update, substeps):
             assert g.stats()["mh_accepted"] == o.mh_accepted
     finally:
         g.close()
+
+
+@pytest.mark.parametrize("ccap", ["1", "4"])
+def test_compact_exchange_halts_resume_bit_exact(monkeypatch, ccap):
+    """Compact records too small for the cold start's requests: steps of the replayed graphs halt on the
+    device, the host resumes each from the step's captured host state with the full records -- and the chain is the
+    oracle's bit for bit, labels, counts, snapshot and best log-likelihood; later replays return to compact records
+    once a replay's requests fit them."""
+    monkeypatch.setenv("NP8_COMPACT_REQ", ccap)
+    X, z, mu, sig = datasets.mixture(20000, 8, 24, 0.8, 12.0, seed=3)
+    g = NealAlgorithm8(8, seed=72, kcap=1024, device=0)
+    o = O.Chain(8, seed=72, kcap=1024)
+    try:
+        g.comm_init(comm_unique_id(), 0, 1)
+        for c in (g, o):
+            c.set_data(X)
+            c.init_random(20)
+        for n in (20, 3, 40, 20, 60):
+            g.sweep(n)
+            o.sweep(n)
+            assert_same(g, o)
+            assert_same(g, o, which=1)
+        np.testing.assert_allclose(g.stats()["best_loglik"], o.best_loglik(), rtol=1e-11)
+        assert g.stats()["compact_halts"] > 0
+    finally:
+        g.close()
+
+
+def test_compact_exchange_warm_state_no_halt():
+    """The C3-like warm state (few requests per step) never halts the compact records at the default capacity."""
+    X, z, mu, sig = datasets.mixture(100000, 8, 64, 0.8, 20.0, seed=4)
+    z = z.astype(np.int32)
+    rng = np.random.default_rng(5)
+    idx = rng.choice(z.size, z.size // 50, replace=False)
+    z[idx] = rng.integers(0, mu.shape[0], size=idx.size)
+    g = NealAlgorithm8(8, seed=73, device=0)
+    o = O.Chain(8, seed=73)
+    try:
+        g.comm_init(comm_unique_id(), 0, 1)
+        for c in (g, o):
+            c.set_data(X)
+            c.set_state(z, mu, sig)
+        g.sweep(40)
+        o.sweep(40)
+        assert_same(g, o)
+        assert_same(g, o, which=1)
+        assert g.stats()["compact_halts"] == 0
+    finally:
+        g.close()

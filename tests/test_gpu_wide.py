@@ -1,4 +1,5 @@
-"""GPU parity of the wide path (DESIGN.md "Wide path"; config C5): D in {32, 48, 64}, fp32 items, the
+"""GPU parity of the wide path (DESIGN.md "Wide path"; config C5): any 16 < D <= 80 (D not a multiple of 16 is padded to
+the next one with zero rows -- 20, 40 and 80 here besides 32, 48, 64; the NIW prior up to D = 64), fp32 items, the
 cluster likelihoods contracted on the fp32 matrix cores (v_mfma_f32_16x16x4_f32, 16-row tiles of the triangular factor).
 
 The oracle restates the contraction (NP8O_CONTRACT_F32: fmaf chains in k order, the accumulator
@@ -46,8 +47,10 @@ def assert_state(a, b):
     assert np.array_equal(sa["sigma"], sb["sigma"])
 
 
-@pytest.mark.parametrize("D", [32, 48, 64])
-@pytest.mark.parametrize("prior", ["reference", "niw"])
+WIDE_CASES = [(D, p) for D in (20, 32, 40, 48, 64, 80) for p in ("reference", "niw") if not (p == "niw" and D > 64)]
+
+
+@pytest.mark.parametrize("D,prior", WIDE_CASES)
 def test_wide_loglik_matrix_bit_exact(D, prior):
     X, _, _ = mixture(D, 1500, 8, D)
     g, o = pair(D, prior, 3)
@@ -63,8 +66,7 @@ def test_wide_loglik_matrix_bit_exact(D, prior):
     np.testing.assert_allclose(lg[:, :K], ref[:, :K], rtol=F32_LL_RTOL)
 
 
-@pytest.mark.parametrize("D", [32, 48, 64])
-@pytest.mark.parametrize("prior", ["reference", "niw"])
+@pytest.mark.parametrize("D,prior", WIDE_CASES)
 def test_wide_sweeps_bit_exact(D, prior):
     """Warm start (the data's own clusters, unit covariances): the C5 benchmark's situation."""
     X, z, cent = mixture(D, 3000, 6, 100 + D)
@@ -138,7 +140,7 @@ def test_wide_graph_replay_bit_exact():
     assert_state(g, o)
 
 
-@pytest.mark.parametrize("D", [32, 48, 64])
+@pytest.mark.parametrize("D", [20, 32, 40, 48, 64])
 def test_wide_niw_conjugate_chain(D):
     """niw_conjugate on the wide path: statistics on the fp64 matrix cores (np8_suffstats_wide), summed
     in another order than the oracle's item loop, so posterior parameters agree to ~1e-13 relative and
@@ -160,3 +162,27 @@ def test_wide_niw_conjugate_chain(D):
         np.testing.assert_allclose(sa["mu"], sb["mu"], rtol=1e-10, atol=1e-10)
         np.testing.assert_allclose(sa["sigma"], sb["sigma"], rtol=1e-9, atol=1e-11)
     np.testing.assert_allclose(g.total_loglik(), o.total_loglik(), rtol=1e-10)
+
+
+@pytest.mark.parametrize("D", [20, 40, 80])
+def test_wide_padded_dims_init_random_and_graph_bit_exact(D):
+    """A D that is not a multiple of 16 from the reference initialisation (new clusters built from the item frame at
+    the data's D, np8_frame_slots) and through a replayed 20-sweep graph."""
+    X, _, _ = mixture(D, 2000, 4, 40 + D)
+    g, o = pair(D, "reference", 8, kcap=512)
+    for c in (g, o):
+        c.set_data(X)
+        c.init_random(10)
+    for n in (2, 20):
+        g.sweep(n)
+        o.sweep(n)
+        assert_state(g, o)
+    assert g.stats()["new_clusters"] > 0
+
+
+def test_wide_rejects_niw_above_64():
+    """np8_niw_post holds four D x (D + 1) double matrices in LDS: the NIW prior on the wide path stops at D = 64."""
+    from noparama_amd import NP8Error
+
+    with pytest.raises(NP8Error):
+        NealAlgorithm8(80, contraction="f32", kcap=256, device=0, **kw_for(80, "niw", 1))

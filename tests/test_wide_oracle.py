@@ -3,7 +3,7 @@
 The oracle restates the fp32 MFMA contraction (fmaf chains over 16-row tiles) that np8_assign_wide
 runs on the device; tests/test_gpu_wide.py pins device = oracle bit for bit.  Here the oracle's fp32
 likelihoods are checked against its fp64 formula with the general inverse
-(multivariatenormal.cpp:106-136) at every tiled D, within the tolerance the GPU tests use, and the
+(multivariatenormal.cpp:106-136) at tiled and padded D (20, 40, 80 are not multiples of 16), within the tolerance the GPU tests use, and the
 oracle's wide sweeps are checked to keep the membertrix invariants.
 """
 import numpy as np
@@ -29,7 +29,7 @@ def chain(D, prior, seed):
     return O.Chain(D, contraction="f32", kcap=256, seed=seed, **kw)
 
 
-@pytest.mark.parametrize("D", [32, 48, 64])
+@pytest.mark.parametrize("D", [20, 32, 40, 48, 64, 80])
 @pytest.mark.parametrize("prior", ["reference", "niw"])
 def test_wide_contraction_against_fp64_formula(D, prior):
     X, _, _ = mixture(D, 600, 6, D)
@@ -56,6 +56,9 @@ def test_wide_sweeps_keep_invariants(D):
         assert s["z"].min() >= 0 and s["z"].max() < s["K"]
 
 
-def test_wide_rejects_untiled_dimension():
+@pytest.mark.parametrize("D", [16, 81])
+def test_wide_rejects_dimension_outside_range(D):
+    """The wide path covers 16 < D <= 80 (any D: the device pads to the next multiple of 16); D <= 16 is the fp64
+    path's."""
     with pytest.raises(Exception):
-        O.Chain(40, contraction="f32", kcap=256, mu0=np.zeros(40), kappa=0.02, nu=4.0, Lambda=np.eye(40))
+        O.Chain(D, contraction="f32", kcap=256, mu0=np.zeros(D), kappa=0.02, nu=4.0, Lambda=np.eye(D))
