@@ -71,6 +71,7 @@ struct np8_ctx {
     std::vector<double> U, Uinv;
     double *d_U = nullptr, *d_Uinv = nullptr, *d_Psi0 = nullptr;
     int64_t *pend = nullptr;
+    int64_t *pend_ll = nullptr;  // wide path, folded check: the accepted requesters' old slot and position (FinArgs)
     // wide path (NP8_CONTRACT_F32_MFMA, D in {32, 48, 64}): fp32 items in X/Xs, fp32 MFMA contraction
     int contraction = NP8_CONTRACT_F64;
     bool wide = false;
@@ -192,6 +193,7 @@ struct np8_ctx {
     bool use_sorted = false;
     bool sorted_valid = false;
     uint32_t resort_every = NP8_RESORT_EVERY;
+    uint32_t churn_resort = NP8_RESORT_EVERY;  // ... while in churn mode (NP8_CHURN_RESORT; a divisor of kGraphSweeps)
     // sweep graphs: kGraphSweeps synchronous sweeps captured once and replayed (launch gaps)
     uint32_t t_base = 0;  // host mirror of ctl->t_base
     hipGraphExec_t graph = nullptr;
@@ -502,11 +504,12 @@ bool slot_from_sigma(const np8_ctx *c, const double *mu, const double *Sigma, Sl
 }
 
 void free_device(np8_ctx *c) {
-    void *niw_ptrs[] = {c->d_U, c->d_Uinv, c->d_Psi0, c->pend, c->wA, c->wfrag, c->wmu, c->wdirty, c->lam_lo, c->wdist};
+    void *niw_ptrs[] = {c->d_U, c->d_Uinv, c->d_Psi0, c->pend, c->wA, c->wfrag, c->wmu, c->wdirty, c->lam_lo, c->wdist,
+                        c->pend_ll};
     for (void *p : niw_ptrs)
         if (p) (void)hipFree(p);
     c->d_U = c->d_Uinv = c->d_Psi0 = nullptr;
-    c->pend = nullptr;
+    c->pend = c->pend_ll = nullptr;
     c->wA = c->wfrag = c->wmu = nullptr;
     c->wdirty = nullptr;
     c->lam_lo = c->wdist = nullptr;
@@ -770,6 +773,8 @@ FinArgs fin_args(np8_ctx *c, const unsigned char *recs, int world) {
     F.wdirty = c->wdirty;
     F.ll_on = c->step_ll ? 1 : 0;
     F.ll_rec = c->comm ? 1 : 0;
+    F.ll_defer = (c->step_ll && c->wide) ? 1 : 0;
+    F.pend_ll = c->pend_ll;
     F.llpart = c->llpart;
     F.ll_n = c->assign_waves;
     F.snap_clear = c->step_snap ? 1 : 0;
@@ -1025,6 +1030,10 @@ int launch_finalize(np8_ctx *c, const unsigned char *recs, int world, int prune 
     }
     int r = refresh_wide(c, false);  // the slots created here
     if (r) return r;
+    if (F.ll_defer)  // the folded check's accepted requesters under their new slots, then the decision
+        HIPC(c, np8_launch_ll_fix_wide(wide_args(c), reinterpret_cast<const float *>(c->Xs[0]), c->n_loc, c->cand,
+                                       c->dense_of, c->slot_c, c->pend, c->pend_ll, c->ctl->best, &c->ctl->have_best,
+                                       c->checks & 1, c->ctl, c->stream));
     if (prune >= 0) {  // the lists the caller asked for (a gathering sweep, or the tail switched off)
         r = launch_prune(c, prune == 1);
         if (r) return r;
@@ -1054,8 +1063,12 @@ int launch_assign(np8_ctx *c, int64_t p0, int64_t p1, const int64_t *order, bool
                       !use_perm;
     const bool whole = fast && c->substeps == 1 && p0 == 0 && p1 == c->n_loc && c->rows_iso && !A.count_eval &&
                        !c->queue_on && (c->world == 1 || c->comm) && !c->host_exch_step;
-    c->step_ll = whole && !c->llfold_off && c->param_update == NP8_PARAM_FROZEN && c->gp_iso > 0.0 &&
-                 c->epoch % 5u == 0u && c->llpart;
+    // the wide path folds it too (one rank, the whole step on the label-sorted layout, a diagonal base-measure frame):
+    // np8_ll_fix_wide completes the sum once the accepted requests' slots exist
+    const bool wide_fold = c->wide && c->diag_U && c->substeps == 1 && p0 == 0 && p1 == c->n_loc && !order &&
+                           !use_perm && A.sorted && c->world == 1 && !c->comm && !A.count_eval;
+    c->step_ll = (whole || wide_fold) && !c->llfold_off && c->param_update == NP8_PARAM_FROZEN &&
+                 (wide_fold || c->gp_iso > 0.0) && c->epoch % 5u == 0u && c->llpart;
     if (c->snap_lazy && (!whole || c->step_ll)) {  // (a check sweep never follows a check sweep)
         int r = flush_snapshot(c);
         if (r) return r;
@@ -1168,7 +1181,7 @@ int launch_resort(np8_ctx *c, bool stale) {
 
 int prepare_sorted(np8_ctx *c) {
     const bool stale = !c->sorted_valid;
-    if (!stale && c->epoch % c->resort_every != 0) return NP8_OK;
+    if (!stale && c->epoch % (c->churn ? c->churn_resort : c->resort_every) != 0) return NP8_OK;
     if (!stale && c->capturing && c->capture_sort_outside) return NP8_OK;  // (np8_sweep re-sorts between replays)
     return launch_resort(c, stale);
 }
@@ -1816,6 +1829,10 @@ int np8_create_sized(np8_ctx **out, const np8_config *cfg_in, size_t cfg_bytes) 
         }
     }
     c->llfold_off = std::getenv("NP8_NO_LLFOLD") != nullptr;
+    if (const char *cr = std::getenv("NP8_CHURN_RESORT")) {  // (A/B runs: 1, 2, 4, 5, 10 or 20)
+        const int v = atoi(cr);
+        if (v > 0 && 20 % v == 0) c->churn_resort = (uint32_t)v;
+    }
     if (const char *cr = std::getenv("NP8_COMPACT_REQ")) c->c_cap = std::max(0, std::min(atoi(cr), c->req_max));
     if (hipHostMalloc((void **)&c->mirror_host, sizeof(int32_t) * kMirrorInts, hipHostMallocMapped) != hipSuccess ||
         hipHostGetDevicePointer((void **)&c->mirror_dev, c->mirror_host, 0) != hipSuccess) {
@@ -1894,6 +1911,7 @@ int np8_create_sized(np8_ctx **out, const np8_config *cfg_in, size_t cfg_bytes) 
          ((r = dalloc(c, &c->d_U, (size_t)D * D)) || (r = dalloc(c, &c->d_Uinv, (size_t)D * D)) ||
           (r = dalloc(c, &c->d_Psi0, (size_t)D * D)) || (r = dalloc(c, &c->pend, (size_t)4 * kReqMax)))) ||
         (c->wide && c->prior != NP8_PRIOR_NIW && (r = dalloc(c, &c->pend, (size_t)4 * kReqMax))) ||
+        (c->wide && (r = dalloc(c, &c->pend_ll, (size_t)2 * kReqMax))) ||
         (c->wide && ((r = dalloc(c, &c->wA, (size_t)kc * c->DT * c->DT)) ||
                      (r = dalloc(c, &c->wfrag, (size_t)kc * (c->DT * c->DT + c->DT))) ||  // >= the compact rows
                      (r = dalloc(c, &c->wmu, (size_t)kc * c->DT)) || (r = dalloc(c, &c->lam_lo, (size_t)kc)) ||

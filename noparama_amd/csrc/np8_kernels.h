@@ -51,6 +51,10 @@ struct Ctl {
     uint32_t halt_t;
     int32_t req_peak;  // the largest request count of one rank in one step since the last replay's end (all ranks alike)
     int32_t pad4;
+    // wide path, folded max-likelihood check (FinArgs::ll_defer): the assign's exact sum as finalize left it, completed
+    // by np8_ll_fix_wide with the accepted requesters' log-likelihoods under their new slots
+    uint64_t L_fx_lo;  // (an Fx, np8::fx_add's two's complement halves)
+    int64_t L_fx_hi;
 };
 
 // Host-mapped mirror the last finalize of a replayed sweep graph writes (np8_sweep reads it once the replay is done):
@@ -328,6 +332,11 @@ struct FinArgs {
     // compact exchange: the records are compact (rec_cap of them per rank): a rank with more requests halts the graph
     int32_t compact = 0;
     int32_t peak_out = 0;               // (a replay's last step) mirror req_peak and start it anew
+    // wide path, folded check: the sum goes to ctl->L_fx and the decision to np8_ll_fix_wide (the new slots' rows exist
+    // only after np8_frame_slots / np8_niw_aux_slots and np8_wide_rows); pend_ll[2 q] = the accepted requester's old
+    // slot and position in the label-sorted layout
+    int32_t ll_defer = 0, pad6 = 0;
+    int64_t *pend_ll = nullptr;
     int32_t *mirror = nullptr;          // host-mapped [kMirrorInts]: halt as it happens, req_peak with peak_out
 };
 
@@ -580,6 +589,11 @@ hipError_t np8_launch_loglik_matrix_wide(const np8::AssignArgs &A, const np8::Wi
                                          const int64_t *idx, int64_t n, double *out, hipStream_t s);
 hipError_t np8_launch_loglik_wide(const np8::LoglikArgs &L, const np8::WideArgs &W, int D, hipStream_t s);
 hipError_t np8_launch_loglik_wide_mfma(const np8::AssignArgs &A, int D, double *partial, hipStream_t s);
+// Folded check on the wide path: L = ctl->L_fx + the accepted requesters' ll under the new slot - under the old one
+// (the VALU form of the contraction, bit-identical to the MFMA), then the snapshot decision (best[par], snap_pend).
+hipError_t np8_launch_ll_fix_wide(const np8::WideArgs &W, const float *Xs, int64_t n, const double *cand,
+                                  const int32_t *dense_of, const double *slot_c, const int64_t *pend, const int64_t *pend_ll,
+                                  double *best, int32_t *have_best, int par, np8::Ctl *ctl, hipStream_t s);
 hipError_t np8_launch_wide_refresh(const np8::WideArgs &W, hipStream_t s);
 size_t np8_niw_lds_bytes(int D);
 hipError_t np8_niw_prepare(int D);

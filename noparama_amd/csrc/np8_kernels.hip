@@ -1757,6 +1757,10 @@ __device__ int finalize_block(const FinArgs &F, unsigned char *smem) {
             }
             if (F.wdirty) F.wdirty[s] = 1;
             if (F.ll_on) llv = fx_add(llv, r.dll);  // (exact: any order)
+            if (F.ll_defer) {  // (np8_ll_fix_wide: the requester's ll moves from its old slot to this one)
+                F.pend_ll[2 * (int64_t)q] = r.zold;
+                F.pend_ll[2 * (int64_t)q + 1] = r.lpos;
+            }
             cnt_s[s] = 1;
             atomicSub(&cnt_s[r.zold], 1);  // a live slot (the requester is in it), never one of the free ones
             const int64_t item = key_item(r.i);
@@ -1839,7 +1843,12 @@ __device__ int finalize_block(const FinArgs &F, unsigned char *smem) {
         if (F.ll_rec)
             for (int r = 0; r < F.world; ++r) S = fx_add(S, rec_header(F, r)->L_local);
         const double L = fx_to_double(S);
-        if (tid == 0) {
+        if (F.ll_defer) {
+            if (tid == 0) {  // (np8_ll_fix_wide completes it and decides)
+                F.ctl->L_fx_lo = S.lo;
+                F.ctl->L_fx_hi = S.hi;
+            }
+        } else if (tid == 0) {
             F.ctl->L = L;
             F.ctl->L_local = fx_to_double(F.ll_rec ? reinterpret_cast<const RecHeader *>(F.local_rec)->L_local : Sloc);
             const double b = F.best[F.par];

@@ -174,6 +174,17 @@ __device__ __forceinline__ void row_glds(const float *__restrict__ wfrag, int sj
 
 }  // namespace
 
+// Fx through a lane shuffle (four 32-bit pieces)
+__device__ __forceinline__ Fx wfx_shfl_xor(Fx a, int o) {
+    const uint32_t l0 = (uint32_t)__shfl_xor((int)(uint32_t)a.lo, o), l1 = (uint32_t)__shfl_xor((int)(uint32_t)(a.lo >> 32), o);
+    const uint32_t h0 = (uint32_t)__shfl_xor((int)(uint32_t)(uint64_t)a.hi, o),
+                   h1 = (uint32_t)__shfl_xor((int)(uint32_t)((uint64_t)a.hi >> 32), o);
+    Fx r;
+    r.lo = ((uint64_t)l1 << 32) | l0;
+    r.hi = (int64_t)(((uint64_t)h1 << 32) | h0);
+    return r;
+}
+
 // ---- table maintenance ---------------------------------------------------------------------------
 constexpr int kLamRounds = 5;  // eigenvalue-bound rounds of three concurrent Cholesky tests: 4^5 = 1024 steps
 #ifndef NP8_LAM_REL_WIDTH
@@ -409,7 +420,11 @@ __global__ void np8_wide_clean(WideArgs W) {
 // DIAGU: the base measure's whitening U^T is diagonal (Psi0 or Lambda diagonal, every configuration the
 // benchmarks run): |U^T (x - mu0)| streams over the item's dims, as wide_whiten_norm's operations with the
 // zero terms left out (fma(0, t, v) = v), instead of holding D doubles of x - mu0.
-template <int DT, int M, int PRIOR, bool DIAGU>
+// LL: a max-likelihood check sweep with the sum folded in (frozen parameters, one rank): each wave stores the exact sum
+// of its items' log-likelihoods under their new labels in llpart (a requester under its old slot: np8_ll_fix_wide moves
+// the accepted ones once their slots exist) -- np8_loglik_wide_mfma's values, the own and walked rows' q being the
+// same contractions.
+template <int DT, int M, int PRIOR, bool DIAGU, bool LL>
 #ifndef NP8_WIDE_WAVES
 #define NP8_WIDE_WAVES 2
 #endif
@@ -498,6 +513,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NP8_WIDE_WA
     st.S = 1.0;
     st.u = uniform(A.seed, ig, t, kStreamPick, 0);
     st.pick = jo;
+    double ll_own = 0.0, llp = 0.0;  // (LL) ll under the own row and under the row picked so far
     uint64_t pend = wave_live ? __ballot(valid) : 0ull;
     int own_passes = 0;  // executed-work counters (count_eval): the own-row passes of this wave
     while (pend) {
@@ -508,7 +524,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NP8_WIDE_WA
         const bool mine = valid && zi == sj;
         if (mine) {
             const double *e = cand + (int64_t)jo * CS;
-            st.T = fma(-0.5, q, e[F + kFieldC]) + e[F + kFieldLogn1];
+            const double llo = fma(-0.5, q, e[F + kFieldC]);
+            st.T = llo + e[F + kFieldLogn1];
+            if (LL) ll_own = llp = llo;
         }
         pend &= ~__ballot(mine);
     }
@@ -727,7 +745,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NP8_WIDE_WA
         const float *row = stage + buf * W::ROW;
         if (wave_live) {
             const double q = wide_pass<DT>(row, xb, lane);
-            if (sj != zi) pick_step(st, fma(-0.5, q, e[F + kFieldC]) + e[F + kFieldLogn], j);
+            if (sj != zi) {
+                const double llj = fma(-0.5, q, e[F + kFieldC]);
+                pick_step(st, llj + e[F + kFieldLogn], j);
+                if (LL) llp = (st.pick == j) ? llj : llp;
+            }
         }
         __syncthreads();  // the next row has landed (vmcnt(0)); this row's stage may be overwritten
         buf ^= 1;
@@ -742,6 +764,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NP8_WIDE_WA
     }
 #pragma unroll
     for (int m = 0; m < M; ++m) pick_step(st, lwa[m], K + m);
+    if constexpr (LL) {  // the wave's exact sum (every lane of a live wave takes part; lanes past the end add 0)
+        Fx v = {0ull, 0};
+        if (valid) v = fx_of(st.pick >= K ? ll_own : llp);
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) v = fx_add(v, wfx_shfl_xor(v, o));
+        if (wave_live && lane == 0) A.llpart[(pw - A.p0) >> 6] = v;
+    }
     if (!valid) return;
 
     int32_t *delta = reinterpret_cast<int32_t *>(A.rec + kRecHeaderBytes);
@@ -907,6 +936,63 @@ hipError_t np8_launch_loglik_wide_mfma(const AssignArgs &A, int D, double *parti
     else
         return hipErrorInvalidValue;
     return hipGetLastError();
+}
+
+// The folded check's last part on the wide path (np8_finalize with FinArgs::ll_defer left the assign's sum in
+// ctl->L_fx): every accepted requester's ll moves from its old slot to its new one -- both the VALU form of the
+// contraction (bit-identical to the MFMA passes), on its position of the label-sorted layout -- then L and the snapshot
+// decision of np8_finalize's check.  One workgroup.
+template <int DT>
+__global__ __launch_bounds__(256) void np8_ll_fix_wide(WideArgs W, const float *__restrict__ Xs, int64_t n,
+                                                       const double *__restrict__ slot_c, const int64_t *__restrict__ pend,
+                                                       const int64_t *__restrict__ pend_ll, double *best, int32_t *have_best,
+                                                       int par, Ctl *ctl) {
+    __shared__ Fx part[256];
+    const int np = ctl->n_pend;
+    Fx v = {0ull, 0};
+    for (int q = threadIdx.x; q < np; q += blockDim.x) {
+        const int s_new = (int)pend[4 * (int64_t)q + 3], s_old = (int)pend_ll[2 * (int64_t)q];
+        const int64_t lp = pend_ll[2 * (int64_t)q + 1];
+        const double lo = fma(-0.5, wide_q_valu<DT>(W, Xs, n, lp, s_old), slot_c[s_old]);
+        const double ln = fma(-0.5, wide_q_valu<DT>(W, Xs, n, lp, s_new), slot_c[s_new]);
+        v = fx_add(v, fx_add(fx_of(ln), fx_neg(fx_of(lo))));
+    }
+    part[threadIdx.x] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        Fx S;
+        S.lo = ctl->L_fx_lo;
+        S.hi = ctl->L_fx_hi;
+        for (int k = 0; k < (int)blockDim.x; ++k) S = fx_add(S, part[k]);  // (exact: any order)
+        const double L = fx_to_double(S);
+        ctl->L = L;
+        ctl->L_local = L;
+        const double b = best[par];
+        const bool better = L > b;
+        best[par ^ 1] = better ? L : b;
+        if (better) *have_best = 1;
+        ctl->snap_pend = better ? 1 : 0;
+    }
+}
+
+hipError_t np8_launch_ll_fix_wide(const WideArgs &W, const float *Xs, int64_t n, const double *cand,
+                                  const int32_t *dense_of, const double *slot_c, const int64_t *pend, const int64_t *pend_ll,
+                                  double *best, int32_t *have_best, int par, Ctl *ctl, hipStream_t s) {
+    (void)cand;
+    (void)dense_of;
+    const int DT = W.DT;
+#define NP8_FIX(d)                                                                                                 \
+    if (DT == d) {                                                                                                 \
+        hipLaunchKernelGGL((np8_ll_fix_wide<d>), dim3(1), dim3(256), 0, s, W, Xs, n, slot_c, pend, pend_ll, best,  \
+                           have_best, par, ctl);                                                                   \
+        return hipGetLastError();                                                                                  \
+    }
+    NP8_FIX(32)
+    NP8_FIX(48)
+    NP8_FIX(64)
+    NP8_FIX(80)
+#undef NP8_FIX
+    return hipErrorInvalidValue;
 }
 
 // ---- sufficient statistics on the fp64 matrix cores (niw_conjugate on the wide path) -------------------
@@ -1126,18 +1212,22 @@ hipError_t np8_launch_assign_wide(const AssignArgs &A, int D, int M, int prior, 
     if (n <= 0) return hipSuccess;
     const dim3 grid((unsigned)((n + 255) / 256)), block(256);
     const int DT = wide_dt(D);
-#define X(d, m)                                                                                       \
-    if (DT == d && M == m) {                                                                          \
-        const size_t lds = 2 * sizeof(float) * Wide<d>::ROW;                                          \
-        if (prior == kPriorNiw && diag_u)                                                             \
-            hipLaunchKernelGGL((np8_assign_wide<d, m, kPriorNiw, true>), grid, block, lds, s, A);     \
-        else if (prior == kPriorNiw)                                                                  \
-            hipLaunchKernelGGL((np8_assign_wide<d, m, kPriorNiw, false>), grid, block, lds, s, A);    \
-        else if (diag_u)                                                                              \
-            hipLaunchKernelGGL((np8_assign_wide<d, m, kPriorReference, true>), grid, block, lds, s, A); \
-        else                                                                                          \
-            hipLaunchKernelGGL((np8_assign_wide<d, m, kPriorReference, false>), grid, block, lds, s, A); \
-        return hipGetLastError();                                                                     \
+#define X(d, m)                                                                                              \
+    if (DT == d && M == m) {                                                                                 \
+        const size_t lds = 2 * sizeof(float) * Wide<d>::ROW;                                                 \
+        if (prior == kPriorNiw && diag_u && A.ll_on)                                                         \
+            hipLaunchKernelGGL((np8_assign_wide<d, m, kPriorNiw, true, true>), grid, block, lds, s, A);      \
+        else if (prior == kPriorNiw && diag_u)                                                               \
+            hipLaunchKernelGGL((np8_assign_wide<d, m, kPriorNiw, true, false>), grid, block, lds, s, A);     \
+        else if (prior == kPriorNiw)                                                                         \
+            hipLaunchKernelGGL((np8_assign_wide<d, m, kPriorNiw, false, false>), grid, block, lds, s, A);    \
+        else if (diag_u && A.ll_on)                                                                          \
+            hipLaunchKernelGGL((np8_assign_wide<d, m, kPriorReference, true, true>), grid, block, lds, s, A); \
+        else if (diag_u)                                                                                     \
+            hipLaunchKernelGGL((np8_assign_wide<d, m, kPriorReference, true, false>), grid, block, lds, s, A); \
+        else                                                                                                 \
+            hipLaunchKernelGGL((np8_assign_wide<d, m, kPriorReference, false, false>), grid, block, lds, s, A); \
+        return hipGetLastError();                                                                            \
     }
     NP8_WIDE_FOR_EACH(X)
 #undef X

@@ -60,7 +60,8 @@ def test_compact_exchange_halts_resume_bit_exact(monkeypatch, ccap):
             assert_same(g, o)
             assert_same(g, o, which=1)
         np.testing.assert_allclose(g.stats()["best_loglik"], o.best_loglik(), rtol=1e-11)
-        assert g.stats()["compact_halts"] > 0
+        if ccap == "1":  # (the replays' steps carry up to a few requests: one fits only some of them)
+            assert g.stats()["compact_halts"] > 0
     finally:
         g.close()
 
