@@ -194,6 +194,7 @@ struct np8_ctx {
     bool sorted_valid = false;
     uint32_t resort_every = NP8_RESORT_EVERY;
     uint32_t churn_resort = NP8_RESORT_EVERY;  // ... while in churn mode (NP8_CHURN_RESORT; a divisor of kGraphSweeps)
+    bool niw_valu = false;  // NP8_NIW_VALU=1: np8_niw_post's dense products on the vector ALU (A/B runs)
     // sweep graphs: kGraphSweeps synchronous sweeps captured once and replayed (launch gaps)
     uint32_t t_base = 0;  // host mirror of ctl->t_base
     hipGraphExec_t graph = nullptr;
@@ -834,6 +835,7 @@ NiwArgs niw_args(np8_ctx *c) {
     A.D = c->D;
     A.kcap = c->kcap;
     A.DT = c->DT;
+    A.valu = c->niw_valu ? 1 : 0;
     A.kappa0 = c->kappa;
     A.nu0 = c->nu;
     A.rsk = c->rsk;
@@ -1829,6 +1831,7 @@ int np8_create_sized(np8_ctx **out, const np8_config *cfg_in, size_t cfg_bytes) 
         }
     }
     c->llfold_off = std::getenv("NP8_NO_LLFOLD") != nullptr;
+    c->niw_valu = std::getenv("NP8_NIW_VALU") != nullptr;
     if (const char *cr = std::getenv("NP8_CHURN_RESORT")) {  // (A/B runs: 1, 2, 4, 5, 10 or 20)
         const int v = atoi(cr);
         if (v > 0 && 20 % v == 0) c->churn_resort = (uint32_t)v;

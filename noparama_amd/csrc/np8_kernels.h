@@ -485,6 +485,7 @@ struct NiwArgs {
     float *wA = nullptr, *wfrag = nullptr, *wmu = nullptr;
     double *lam_lo = nullptr;
     int32_t DT = 0;  // wide path: the tables' tile dimension (WideArgs::DT)
+    int32_t valu = 0;  // np8_niw_post: the dense products on the vector ALU instead of the fp64 matrix cores (NP8_NIW_VALU=1)
 };
 
 // np8_step_tail (the end of a synchronous step in one launch): which parts run.

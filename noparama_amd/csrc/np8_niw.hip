@@ -218,6 +218,128 @@ __device__ __forceinline__ double write_pprime_r(int D, int LD, const double *R,
 
 constexpr int kPanelN = 16;
 
+// ---- dense products on the fp64 matrix cores (round 5) ---------------------------------------------------------
+// v_mfma_f64_16x16x4_f64 is a k-ordered fma chain (tools/mfma_f64_exact.hip measures it on the device): each output
+// element receives fma(a_k, b_k, .) for k = k0, k0 + 1, ... in order, one rounding per product -- the chains the VALU
+// loops above run.  Terms outside an element's own k range have a zero factor (the triangular operands), and
+// fma(0, t, +0) = +0 / fma(x, 0, v) = v leave the chain's bits alone, so a whole 16 x 16 tile takes one k range.
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+
+// One 16 x 16 tile (one wave): acc(i, j) = sum_k a_at(i, k) b_at(k, j) over k = k0 .. k1 - 1 (k1 - k0 a multiple of 4;
+// accessors return 0 outside the matrices); element r of lane l is (row (l >> 4) + 4 r, column l & 15).
+template <class FA, class FB>
+__device__ __forceinline__ f64x4 mfma_tile(FA a_at, FB b_at, int k0, int k1) {
+    const int lane = threadIdx.x & 63, il = lane & 15, kl = lane >> 4;
+    f64x4 acc = {0.0, 0.0, 0.0, 0.0};
+    for (int k = k0; k < k1; k += 4) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a_at(il, k + kl), b_at(k + kl, il), acc, 0, 0, 0);
+    return acc;
+}
+
+// Sigma = T^T T (T lower): tiles ti <= tj, element (a, b) = sum over k from 16 tj (below max(a, b) a factor is zero) of
+// T_ka T_kb, mirrored -- sigma_from_t's chains (its element (b, a) is the same chain with each fma's factors swapped).
+__device__ void sigma_from_t_mfma(int D, int LD, const double *T, double *Sigma, double *Sl) {
+    const int nt = (D + 15) / 16, wv = threadIdx.x >> 6, nw = blockDim.x >> 6, lane = threadIdx.x & 63;
+    const int k1 = (D + 3) & ~3;
+    for (int tt = wv; tt < nt * (nt + 1) / 2; tt += nw) {
+        int ti = 0, rem = tt;
+        while (rem >= nt - ti) {
+            rem -= nt - ti;
+            ++ti;
+        }
+        const int tj = ti + rem;
+        const f64x4 acc = mfma_tile([&](int i, int k) { return (k < D && 16 * ti + i < D) ? T[k * LD + 16 * ti + i] : 0.0; },
+                                    [&](int k, int j) { return (k < D && 16 * tj + j < D) ? T[k * LD + 16 * tj + j] : 0.0; },
+                                    16 * tj, k1);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int a = 16 * ti + (lane >> 4) + 4 * r, b = 16 * tj + (lane & 15);
+            if (a < D && b < D) {
+                Sigma[a * D + b] = acc[r];
+                Sigma[b * D + a] = acc[r];
+                if (Sl) {
+                    Sl[a * LD + b] = acc[r];
+                    Sl[b * LD + a] = acc[r];
+                }
+            }
+        }
+    }
+}
+
+// R = B^T U^{-1} (upper): R_ab = sum_{k = a..b} B_ka M[D-1-k][D-1-b] (M = Lr^{-1} lower, B lower), 0 below the diagonal.
+__device__ void r_from_b_mfma(int D, int LD, const double *B, const double *M, double *R) {
+    const int nt = (D + 15) / 16, wv = threadIdx.x >> 6, nw = blockDim.x >> 6, lane = threadIdx.x & 63;
+    for (int e = threadIdx.x; e < D * D; e += blockDim.x) {  // the lower triangle (tiles below the diagonal included)
+        const int a = e / D, b = e - a * D;
+        if (b < a) R[a * LD + b] = 0.0;
+    }
+    for (int tt = wv; tt < nt * (nt + 1) / 2; tt += nw) {
+        int ti = 0, rem = tt;
+        while (rem >= nt - ti) {
+            rem -= nt - ti;
+            ++ti;
+        }
+        const int tj = ti + rem;
+        const int k1 = min((D + 3) & ~3, 16 * tj + 16);
+        const f64x4 acc = mfma_tile(
+            [&](int i, int k) { return (k < D && 16 * ti + i < D) ? B[k * LD + 16 * ti + i] : 0.0; },
+            [&](int k, int j) { return (k < D && 16 * tj + j < D) ? M[(D - 1 - k) * LD + (D - 1 - (16 * tj + j))] : 0.0; },
+            16 * ti, k1);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int a = 16 * ti + (lane >> 4) + 4 * r, b = 16 * tj + (lane & 15);
+            if (a < D && b < D && b >= a) R[a * LD + b] = acc[r];
+        }
+    }
+}
+
+// P' = packed sym(R^T R) (R upper): element (a, b), a <= b, = sum_{k = 0..a} R_ka R_kb, off-diagonals doubled, into the
+// slot table and its candidate row; returns the isotropy value (write_pprime_r's).
+__device__ double write_pprime_r_mfma(int D, int LD, const double *R, double *slotP, double *candP) {
+    const int nt = (D + 15) / 16, wv = threadIdx.x >> 6, nw = blockDim.x >> 6, lane = threadIdx.x & 63;
+    const double p00 = fma(R[0], R[0], 0.0);
+    bool iso = true;
+    for (int tt = wv; tt < nt * (nt + 1) / 2; tt += nw) {
+        int ti = 0, rem = tt;
+        while (rem >= nt - ti) {
+            rem -= nt - ti;
+            ++ti;
+        }
+        const int tj = ti + rem;
+        const int k1 = min((D + 3) & ~3, 16 * ti + 16);
+        const f64x4 acc = mfma_tile([&](int i, int k) { return (k < D && 16 * ti + i < D) ? R[k * LD + 16 * ti + i] : 0.0; },
+                                    [&](int k, int j) { return (k < D && 16 * tj + j < D) ? R[k * LD + 16 * tj + j] : 0.0; },
+                                    0, k1);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int a = 16 * ti + (lane >> 4) + 4 * r, b = 16 * tj + (lane & 15);
+            if (a < D && b < D && b >= a) {
+                const double v = (a == b) ? acc[r] : 2.0 * acc[r];
+                slotP[pix(D, a, b)] = v;
+                if (candP) candP[pix(D, a, b)] = v;
+                iso = iso && ((a == b) ? v == p00 : v == 0.0);
+            }
+        }
+    }
+    return __syncthreads_and(iso ? 1 : 0) ? p00 : 0.0;
+}
+
+// Y = X X (X symmetric) for the eigenvalue bound (a bound, not a bit-exact quantity): every tile.
+__device__ void sym_square_mfma(int D, int LD, const double *X, double *Y) {
+    const int nt = (D + 15) / 16, wv = threadIdx.x >> 6, nw = blockDim.x >> 6, lane = threadIdx.x & 63;
+    const int k1 = (D + 3) & ~3;
+    for (int tt = wv; tt < nt * nt; tt += nw) {
+        const int ti = tt / nt, tj = tt - ti * nt;
+        const f64x4 acc = mfma_tile([&](int i, int k) { return (k < D && 16 * ti + i < D) ? X[(16 * ti + i) * LD + k] : 0.0; },
+                                    [&](int k, int j) { return (k < D && 16 * tj + j < D) ? X[k * LD + 16 * tj + j] : 0.0; },
+                                    0, k1);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int a = 16 * ti + (lane >> 4) + 4 * r, b = 16 * tj + (lane & 15);
+            if (a < D && b < D) Y[a * LD + b] = acc[r];
+        }
+    }
+}
+
 // Squarings of Sigma / ||Sigma|| behind the wide path's eigenvalue bound (np8_niw_post): lambda_max <= g ||.^(2^k)||^(2^-k).
 // A/B at C5 niw_conjugate, one box: k = 2: 1 157 sweeps/s, 3: 1 283, 4: 1 338 (each squaring ~10 us of np8_niw_post, a
 // tighter bound fewer screen batches in np8_assign_wide).
@@ -619,23 +741,33 @@ __global__ __launch_bounds__(kNiwThreads) void np8_niw_post(NiwArgs A) {
         sh[1] = sl;
     }
     const bool bound = A.lam_lo != nullptr;
-    sigma_from_t(D, LD, F, A.slot_sigma + (int64_t)s * D * D, bound ? L : nullptr);  // Sigma = T^T T
+    if (A.valu) {
+        sigma_from_t(D, LD, F, A.slot_sigma + (int64_t)s * D * D, bound ? L : nullptr);  // Sigma = T^T T
+    } else {
+        sigma_from_t_mfma(D, LD, F, A.slot_sigma + (int64_t)s * D * D, bound ? L : nullptr);
+    }
     __syncthreads();
     NIW_T(4)
     // R = B^T U^{-1} (upper, into F's storage: T is dead): R_ab = sum_{k = a..b} B_ka M[D-1-k][D-1-b]
-    for (int e = tid; e < D * D; e += blockDim.x) {
-        const int a = e / D, b = e - a * D;
-        double v = 0.0;
-        if (b >= a) {
+    if (A.valu) {
+        for (int e = tid; e < D * D; e += blockDim.x) {
+            const int a = e / D, b = e - a * D;
+            double v = 0.0;
+            if (b >= a) {
 #pragma unroll 8
-            for (int k = a; k <= b; ++k) v = fma(B[k * LD + a], Li[(D - 1 - k) * LD + (D - 1 - b)], v);
+                for (int k = a; k <= b; ++k) v = fma(B[k * LD + a], Li[(D - 1 - k) * LD + (D - 1 - b)], v);
+            }
+            F[a * LD + b] = v;
         }
-        F[a * LD + b] = v;
+    } else {
+        r_from_b_mfma(D, LD, B, Li, F);
     }
     __syncthreads();
     NIW_T(5)
-    const double iso = write_pprime_r(D, LD, F, A.slot_P + (int64_t)s * (D * (D + 1) / 2),
-                                      row >= 0 ? A.cand + (int64_t)row * cand_stride(D) + D : nullptr);
+    const double iso = A.valu ? write_pprime_r(D, LD, F, A.slot_P + (int64_t)s * (D * (D + 1) / 2),
+                                               row >= 0 ? A.cand + (int64_t)row * cand_stride(D) + D : nullptr)
+                              : write_pprime_r_mfma(D, LD, F, A.slot_P + (int64_t)s * (D * (D + 1) / 2),
+                                                    row >= 0 ? A.cand + (int64_t)row * cand_stride(D) + D : nullptr);
     NIW_T(6)
     if (A.wA) {  // the wide path: the contraction rows from R itself, the eigenvalue bound from Sigma's row sums
         const int DT = A.DT, NCH = (DT / 16) * (DT / 16 + 1) / 2;
@@ -661,7 +793,10 @@ __global__ __launch_bounds__(kNiwThreads) void np8_niw_post(NiwArgs A) {
         auto buf = [&](int k) -> double * { return k == 0 ? L : (k == 1 ? B : Li); };
 #pragma unroll
         for (int q = 0; q < kBoundSquarings; ++q) {
-            sym_square(D, LD, buf(q % 3), buf((q + 1) % 3));
+            if (A.valu)
+                sym_square(D, LD, buf(q % 3), buf((q + 1) % 3));
+            else
+                sym_square_mfma(D, LD, buf(q % 3), buf((q + 1) % 3));
             __syncthreads();
         }
         const double m = max_abs_row_sum(D, LD, buf(kBoundSquarings % 3), rs);

@@ -6,6 +6,7 @@
 #   smoke                           __graft_entry__.smoke()
 #   bench:<name>:<args>[:<env>]     python bench.py <args> > $OUT/<name>.json, one summary line
 #   py:<name>:<script args>[:<env>] python <script args> > $OUT/<name>.out
+#   cmd:<name>:<program args>       any program (a probe built in-tree) > $OUT/<name>.out
 #   trace:<name>:<script args>      rocprofv3 --kernel-trace --stats of python <script args> -> $OUT/<name>/
 #   pmc:<name>:<script args>        three rocprofv3 PMC passes (SQ issue/wait, FETCH_SIZE, WRITE_SIZE) -> $OUT/<name>/
 # Every step has its own time limit; the first failing step ends the recipe (no GPU step after a failure).
@@ -32,6 +33,9 @@ for job in "$@"; do
       python tools/bench_line.py "$OUT/$name.json" "$name" ;;
     py)
       env $E timeout -k 10 600 python -u $A > "$OUT/$name.out" 2> "$OUT/$name.err" || { tail -20 "$OUT/$name.err"; exit 1; }
+      tail -3 "$OUT/$name.out" ;;
+    cmd)
+      timeout -k 10 300 $A > "$OUT/$name.out" 2> "$OUT/$name.err" || { tail -20 "$OUT/$name.err"; exit 1; }
       tail -3 "$OUT/$name.out" ;;
     trace)
       mkdir -p "$OUT/$name"
