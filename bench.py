@@ -35,7 +35,7 @@ HBM_PEAK_GBS = 8000.0
 # committed rocprofv3 PMC summaries of the assign kernels (HBM bytes per launch, tools/prof*.sh)
 C3_TRAFFIC = "traffic_r04c.json"
 C5_TRAFFIC = "traffic_r04c_c5.json"
-MIXED_TRAFFIC = "traffic_r04_mixed.json"  # PMC pass of the mixed regime (tools/prof_mixed.sh, tools/summarize_profile.py)
+MIXED_TRAFFIC = "traffic_r05_mixed_head.json"  # PMC pass of the mixed regime (tools/prof_mixed.sh, tools/summarize_profile.py)
 
 
 def binding_roof(exec_flops, abytes, ms, peak_tflops, kname):

@@ -204,22 +204,29 @@ constexpr int kPanel = 16;
 // Cholesky tests np8_wide_rows runs beside the factor: three, or two when four D x (D + 1) doubles exceed the LDS.
 __host__ __device__ constexpr int wide_rows_tests(int D) { return D <= 64 ? 3 : 2; }
 
-// Panel p of matrix M (rows c0 .. c0 + 15, columns c0 .. D - 1) on one wave, lane = column.  Factor form (test =
-// false): row jj of R = row jj / sqrt(pivot); a non-positive pivot is replaced by 1e-300 and its column skips every
-// update (np8_wide_rows' error path), bit q of *skip.  Test form: the row is kept unscaled, rk[j] = 1 / sqrt(pivot)
-// scales both factors of each update; a non-positive pivot ends the test (*fail).
+// Panel p of matrix M (rows c0 .. c0 + 15, columns c0 .. D - 1) on one wave, lane = column (and lane + 64 above
+// D = 64: a second register set).  Factor form (test = false): row jj of R = row jj / sqrt(pivot); a non-positive pivot
+// is replaced by 1e-300 and its column skips every update (np8_wide_rows' error path), bit q of *skip.  Test form: the
+// row is kept unscaled, rk[j] = 1 / sqrt(pivot) scales both factors of each update; a non-positive pivot ends the test
+// (*fail).  Each column's chain is the same whichever register set holds it.
 __device__ __forceinline__ void panel_factor(double *M, int LD, int D, int c0, bool test, double *rk, int *skip,
                                              int *fail) {
-    const int lane = threadIdx.x & 63;
-    double w[kPanel];
+    const int lane = threadIdx.x & 63, l2 = lane + 64;
+    const bool two = D > 64;
+    double w[kPanel], u[kPanel];
 #pragma unroll
-    for (int i = 0; i < kPanel; ++i) w[i] = (lane < D && c0 + i < D) ? M[(c0 + i) * LD + lane] : 0.0;
+    for (int i = 0; i < kPanel; ++i) {
+        w[i] = (lane < D && c0 + i < D) ? M[(c0 + i) * LD + lane] : 0.0;
+        u[i] = (two && l2 < D && c0 + i < D) ? M[(c0 + i) * LD + l2] : 0.0;
+    }
+    // element (row j of the panel, column c), c wave-uniform
+    auto col = [&](double wj, double uj, int c) { return c < 64 ? __shfl(wj, c) : __shfl(uj, c - 64); };
     int sk = 0, fl = 0;
 #pragma unroll
     for (int j = 0; j < kPanel; ++j) {
         const int jj = c0 + j;
         if (jj >= D) break;  // (the last panel of a D that is not a multiple of 16)
-        const double v = __shfl(w[j], jj);  // the pivot (row jj, column jj: lane jj)
+        const double v = col(w[j], u[j], jj);  // the pivot (row jj, column jj)
         if (test) {
             if (!(v > 0.0) || fl) {
                 fl = 1;
@@ -227,11 +234,12 @@ __device__ __forceinline__ void panel_factor(double *M, int LD, int D, int c0, b
             }
             const double r = 1.0 / sqrt(v);
             if (lane == 0) rk[j] = r;
-            const double rowj = w[j] * r;  // C[jj][l] r
+            const double rowj = w[j] * r, rowj2 = u[j] * r;  // C[jj][l] r
 #pragma unroll
             for (int i = j + 1; i < kPanel; ++i) {
-                const double ci = __shfl(w[j], c0 + i) * r;  // C[jj][ii] r
+                const double ci = col(w[j], u[j], c0 + i) * r;  // C[jj][ii] r
                 if (lane >= c0 + i) w[i] = fma(-ci, rowj, w[i]);
+                if (two && l2 >= c0 + i) u[i] = fma(-ci, rowj2, u[i]);
             }
         } else {
             const bool ok = v > 0.0;
@@ -239,18 +247,25 @@ __device__ __forceinline__ void panel_factor(double *M, int LD, int D, int c0, b
             if (!ok) sk |= 1 << j;
             if (lane == jj) w[j] = dj;
             if (lane > jj) w[j] = ok ? w[j] / dj : 0.0;  // row jj of R (zero after a failed pivot)
+            if (two) {
+                if (l2 == jj) u[j] = dj;
+                if (l2 > jj) u[j] = ok ? u[j] / dj : 0.0;
+            }
             if (ok) {
 #pragma unroll
                 for (int i = j + 1; i < kPanel; ++i) {
-                    const double rji = __shfl(w[j], c0 + i);  // R[jj][ii]
+                    const double rji = col(w[j], u[j], c0 + i);  // R[jj][ii]
                     if (lane >= c0 + i) w[i] = fma(-rji, w[j], w[i]);
+                    if (two && l2 >= c0 + i) u[i] = fma(-rji, u[j], u[i]);
                 }
             }
         }
     }
 #pragma unroll
-    for (int i = 0; i < kPanel; ++i)
+    for (int i = 0; i < kPanel; ++i) {
         if (lane < D && lane >= c0 + i && c0 + i < D) M[(c0 + i) * LD + lane] = w[i];
+        if (two && l2 < D && l2 >= c0 + i && c0 + i < D) M[(c0 + i) * LD + l2] = u[i];
+    }
     if (lane == 0) {
         *skip = sk;
         *fail = fl;
