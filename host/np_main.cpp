@@ -30,7 +30,7 @@ static void usage(const char *p) {
               << " [-C chunk (0 = data-parallel sweep, 1 = sequential)] [-D dims=2] [-w workspace]"
               << " [-u frozen|mh_g0|niw_conjugate (cluster-parameter update)] [-p reference|niw (base measure)]"
               << " [-x f64|f32 (cluster likelihoods; f32 = fp32 matrix cores, D in {32, 64})]"
-              << " [-n subsample size=200, 0 = all items] [-S sub-steps of the data-parallel sweep=1] [-j per-sweep JSONL file] [-V (check the membertrix against the device after every update)]; data: 'x_1 .. x_D label' text or [N][D+1] .f64"
+              << " [-n subsample size=200, 0 = all items] [-S sub-steps of the data-parallel sweep, or auto (16 up to 8192 items, else 1)=auto] [-j per-sweep JSONL file] [-V (check the membertrix against the device after every update)]; data: 'x_1 .. x_D label' text or [N][D+1] .f64"
               << std::endl;
 }
 
@@ -87,7 +87,7 @@ static void subsample(dataset_t &ds, std::vector<int> &gt, int n, uint64_t seed)
 
 int main(int argc, char *argv[]) {
     std::string data, algo, mode = "clustering", ws, upd = "frozen", base = "reference", contr = "f64";
-    int T = 2000, D = 2, nsub = 200, substeps = 1;
+    int T = 2000, D = 2, nsub = 200, substeps = NP8_SUBSTEPS_AUTO;
     long long chunk = 0;
     unsigned long long seed = 0;
     bool seeded = false, verify = false;
@@ -109,7 +109,7 @@ int main(int argc, char *argv[]) {
             case 'x': contr = optarg; break;
             case 'j': jsonl = optarg; break;
             case 'V': verify = true; break;
-            case 'S': substeps = std::stoi(optarg); break;
+            case 'S': substeps = std::string(optarg) == "auto" ? NP8_SUBSTEPS_AUTO : std::stoi(optarg); break;
             default: usage(argv[0]); return 1;
         }
     }

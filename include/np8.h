@@ -67,10 +67,19 @@ typedef struct {
                              with a fixed hash of the item index equal to s, against the state the earlier
                              sub-steps left (DESIGN.md "Sub-steps").  One step updates every item against
                              the same state; more sub-steps bring the chain's statistics to the sequential
-                             sweep's (tests/test_gpu_chain_stats.py) at S launches of each step kernel. */
+                             sweep's (tests/test_gpu_chain_stats.py) at S launches of each step kernel.
+                             NP8_SUBSTEPS_AUTO: chosen by np8_set_data from n_global (see below). */
 } np8_config;
 
 #define NP8_SUBSTEPS_MAX 64
+/* np8_config.substeps = NP8_SUBSTEPS_AUTO: NP8_SUBSTEPS_AUTO_S sub-steps (or the most kcap allows) when the data set
+ * has at most NP8_SUBSTEPS_AUTO_N items, one step above.  One synchronous step over-splits small data (twogaussians,
+ * N = 200: K 15.6 vs the sequential sampler's 12.5) while 16 sub-steps hold SURVEY 8(d)'s tolerance; at N >= 1e5 one
+ * step scores like 16 (tests/test_gpu_chain_stats.py).  The choice depends on n_global only, so every rank of a
+ * sharded run makes the same one; np8_stats reports it (np8_stats_t.substeps). */
+#define NP8_SUBSTEPS_AUTO (-1)
+#define NP8_SUBSTEPS_AUTO_N 8192
+#define NP8_SUBSTEPS_AUTO_S 16
 
 /* ABI growth.  np8_config and np8_stats_t only ever grow at their end, and the entry points that take them have
  * sized forms that honour the caller's size: np8_create_sized reads the first cfg_bytes of the configuration (the
@@ -158,6 +167,9 @@ typedef struct {
     /* RCCL path: steps of a compact sweep graph whose requests did not fit the compact records; each
      * halted its graph on every rank and was resumed by the host with the full records (cumulative) */
     int64_t compact_halts;
+    /* the sub-steps of the data-parallel sweep in use (np8_config.substeps; NP8_SUBSTEPS_AUTO resolved by
+     * np8_set_data) */
+    int64_t substeps;
 } np8_stats_t;
 
 #define NP8_STATS_MIN_BYTES offsetof(np8_stats_t, ms_assign) /* K .. last_loglik: the first released layout */

@@ -87,6 +87,8 @@ struct np8_ctx {
     double *r2 = nullptr;
     WaveR2 *wr2 = nullptr;  // per-wave radius records of the sweep's assign (ceil(n_loc / 64))
     int32_t *plist = nullptr, *plen = nullptr;
+    float *pdist = nullptr;  // beside plist: the listed rows' distances to the list's own row (the walk's screen)
+    int32_t walk_screen = 1;  // NP8_WALK_SCREEN=0: np8_assign_fast evaluates every listed row
     unsigned long long *evalc = nullptr;  // [kEvalSlots][2] executed-work counters (timing mode)
     bool prune_on = false;     // kcap small enough for kcap x kcap lists
     bool wide_prune_off = false;  // NP8_NO_PRUNE=1: the wide path evaluates every row (A/B runs)
@@ -146,6 +148,7 @@ struct np8_ctx {
     // data-parallel sweep in `substeps` synchronous sub-steps (np8_config.substeps): sub-step s is the
     // contiguous range [sub_start[s], sub_start[s+1]) of the label-sorted layout (sorted by sub-step, slot)
     int substeps = 1;
+    bool substeps_auto = false;  // NP8_SUBSTEPS_AUTO: substeps chosen by np8_set_data
     std::vector<int64_t> sub_start;
     int sub_next = 0;  // host-exchange path: the sub-step np8_step_local runs next
     std::vector<double> mu0, Lambda;
@@ -518,7 +521,7 @@ void free_device(np8_ctx *c) {
                     c->cnt,    c->cnt_best, c->mu_best, c->sigma_best, c->cand, c->ctl,    c->hyp,
                     c->d_mu0,  c->d_LT,    c->d_Gp,   c->d_LTL,   c->rec,     c->gath,    c->order,
                     c->partial, c->dense_of, c->Xs[0], c->Xs[1], c->zs[0], c->zs[1], c->ids[0], c->ids[1],
-                    c->s_hist, c->s_cursor, c->s_off, c->slot_iso, c->acc, c->r2, c->wr2, c->plist, c->plen, c->plr2,
+                    c->s_hist, c->s_cursor, c->s_off, c->slot_iso, c->acc, c->r2, c->wr2, c->plist, c->pdist, c->plen, c->plr2,
                     c->sm_hist, c->sm_mem, c->sm_off, c->sm_live, c->sm_Xm, c->sm_ownm, c->sm_cross, c->sm_ctl,
                     c->sm_typ, c->sm_slist, c->sm_stheta, c->stage, c->evalc, c->z_base, c->cnt_base,
                     c->chg_slot, c->mu_base, c->sigma_base, c->chg_item, c->chg_count, c->chg_flags,
@@ -570,6 +573,7 @@ void free_device(np8_ctx *c) {
     c->chg_cap = 0;
     c->track = 0;
     c->plist = c->plen = nullptr;
+    c->pdist = nullptr;
     c->plr2 = nullptr;
     c->X = nullptr;
     c->z = c->z_best = nullptr;
@@ -901,6 +905,8 @@ AssignArgs assign_args(np8_ctx *c, int64_t p0, int64_t p1, const int64_t *order,
     A.t = c->epoch - c->t_base;
     A.kcap = c->kcap;
     A.plist = c->plist;
+    A.pdist = c->pdist;
+    A.walk_screen = c->walk_screen;
     A.plen = c->plen;
     A.plr2 = c->plr2;
     A.ls = c->kcap;
@@ -1125,6 +1131,7 @@ PruneArgs prune_args(np8_ctx *c, bool last) {
     P.ctl = c->ctl;
     P.r2 = c->r2;
     P.plist = c->plist;
+    P.pdist = c->pdist;
     P.plen = c->plen;
     P.plr2 = c->plr2;
     P.plen_s = c->plen_s;
@@ -1183,6 +1190,12 @@ int launch_resort(np8_ctx *c, bool stale) {
 
 int prepare_sorted(np8_ctx *c) {
     const bool stale = !c->sorted_valid;
+    // sweeps launched one by one (the cold start's): re-sort as soon as a quarter of the items moved since the last sort
+    // (the host-mapped count of the last finalize; the device re-checks) -- after init_random(20) the first sweeps move
+    // half the items each, and a layout sorted for 20 clusters sends every wave through several groups' walks
+    // (cold start 1 141 -> 1 358 sweeps/s measured with a re-sort every second sweep; graphs keep the cadence)
+    if (!stale && !c->capturing && c->moved_host && (*(volatile int64_t *)c->moved_host) * 4 > c->n_loc)
+        return launch_resort(c, false);
     if (!stale && c->epoch % (c->churn ? c->churn_resort : c->resort_every) != 0) return NP8_OK;
     if (!stale && c->capturing && c->capture_sort_outside) return NP8_OK;  // (np8_sweep re-sorts between replays)
     return launch_resort(c, stale);
@@ -1747,10 +1760,11 @@ int np8_create_sized(np8_ctx **out, const np8_config *cfg_in, size_t cfg_bytes) 
         return NP8_ERR_ARG;
     }
     c->req_max = cfg->req_max > 0 ? cfg->req_max : NP8_REQ_DEFAULT;
+    c->substeps_auto = cfg->substeps == NP8_SUBSTEPS_AUTO;
     c->substeps = cfg->substeps > 1 ? cfg->substeps : 1;
     c->debug_inv = std::getenv("NP8_DEBUG_INVARIANTS") != nullptr && std::getenv("NP8_DEBUG_INVARIANTS")[0] == '1';
     // the label-sorted layout is sorted by (sub-step, slot): substeps * kcap bins in the sort's LDS
-    if (cfg->substeps < 0 || cfg->substeps > NP8_SUBSTEPS_MAX || (int64_t)c->substeps * c->kcap > 16384) {
+    if ((cfg->substeps < 0 && !c->substeps_auto) || cfg->substeps > NP8_SUBSTEPS_MAX || (int64_t)c->substeps * c->kcap > 16384) {
         delete c;
         return NP8_ERR_ARG;
     }
@@ -1819,6 +1833,7 @@ int np8_create_sized(np8_ctx **out, const np8_config *cfg_in, size_t cfg_bytes) 
     c->fuse_off = std::getenv("NP8_FUSE") == nullptr;  // opt-in: measured slower than separate launches
     c->queue_on = std::getenv("NP8_QUEUE") != nullptr;
     c->tailcond_off = std::getenv("NP8_LISTS_ALWAYS") != nullptr;
+    c->walk_screen = !(std::getenv("NP8_WALK_SCREEN") && std::getenv("NP8_WALK_SCREEN")[0] == '0');
     c->sort_in_graph = std::getenv("NP8_SORT_IN_GRAPH") != nullptr;
     if (!c->sort_in_graph) {  // host-mapped mirror of ctl->moved (written by every finalize)
         if (hipHostMalloc((void **)&c->moved_host, sizeof(int64_t), hipHostMallocMapped) != hipSuccess ||
@@ -1862,7 +1877,7 @@ int np8_create_sized(np8_ctx **out, const np8_config *cfg_in, size_t cfg_bytes) 
         (kc <= kPruneMaxKcap && ((r = dalloc(c, &c->r2, 2 * (size_t)kc)) || (r = dalloc(c, &c->plen, (size_t)kc)) ||
                                  (r = dalloc(c, &c->lb, 2 * (size_t)kc)) ||
                                 (r = dalloc(c, &c->plr2, (size_t)kc)) ||
-                                 (r = dalloc(c, &c->plist, (size_t)kc * kc))))) {
+                                 (r = dalloc(c, &c->plist, (size_t)kc * kc)) || (r = dalloc(c, &c->pdist, (size_t)kc * kc))))) {
         free_device(c);
         delete c;
         return r;
@@ -1978,6 +1993,8 @@ int np8_set_data(np8_ctx *c, const double *X, int64_t n, int32_t D, int64_t offs
     c->offset = offset;
     c->n_glob = n_global;
     c->part_waves = c->wide ? np8_suffstats_wide_waves(n) : 0;
+    if (c->substeps_auto)  // (n_global only: the same choice on every rank)
+        c->substeps = n_global <= NP8_SUBSTEPS_AUTO_N ? std::max(1, std::min(NP8_SUBSTEPS_AUTO_S, 16384 / c->kcap)) : 1;
     int r = 0;
     // wide path: fp32 items in DT rows (zero beyond D)
     const size_t nx = c->wide ? ((size_t)n * c->DT + 1) / 2 : (size_t)n * D;
@@ -2703,6 +2720,7 @@ int fill_stats(np8_ctx *c, np8_stats_t *out) {
     out->tail_list_builds = (int64_t)h.list_builds;
     out->tail_steps = c->n_tail_cond;
     out->compact_halts = c->n_halts;
+    out->substeps = c->substeps;
     {
         std::vector<unsigned long long> ev((size_t)10 * kEvalSlots);
         HIPC(c, hipMemcpy(ev.data(), c->evalc, sizeof(unsigned long long) * ev.size(), hipMemcpyDeviceToHost));

@@ -206,8 +206,10 @@ struct AssignArgs {
     // plist[k0*ls .. +plen[k0]] instead of every row; r2 collects max |x - mu|^2 per slot for the
     // lists of the next sweep
     const int32_t *plist, *plen;
+    const float *pdist;  // beside plist: |mu_j - mu_k0| of each listed row, rounded down (0: not measured)
     const double *plr2;  // per dense row: the squared radius its list assumes (+inf: a full list)
     int32_t ls, use_lists, collect_r2, count_eval;
+    int32_t walk_screen;  // np8_assign_fast: screen each listed row for the wave before its quadratic forms
     double *r2;      // [2][kcap]: radii in use | gathered this sweep (collect_r2: mixed waves atomicMax here)
     WaveR2 *wr2;     // [ceil(n_loc / 64)]: a wave whose 64 items sit in one slot stores its maximum here
     unsigned long long *evalc;  // [kEvalSlots][2]: quadratic forms, isotropic ones
@@ -276,6 +278,7 @@ struct PruneArgs {
     Ctl *ctl;
     double *r2;         // [2][kcap]: radii in use | gathered this sweep
     int32_t *plist, *plen;
+    float *pdist;       // beside plist: |mu_j - mu_k0| rounded down (AssignArgs::pdist)
     double *plr2;       // per dense row: the squared radius the list was built for
     int32_t *plen_s;    // plen and plr2 again, indexed by the row's slot (np8_assign_fast)
     double *plr2_s;

@@ -802,22 +802,39 @@ __global__ __launch_bounds__(NP8_ASSIGN_BLOCK) __attribute__((amdgpu_waves_per_e
     static_assert(NP8_ASSIGN_BLOCK == 64, "the walk's LDS rows are per wave");
     __shared__ double s_row[D + 4][64];
     __shared__ int32_t s_j[64];
+    __shared__ float s_dist[64];
 #define NP8_ROWF(v, f, k) s_row[f][k]
 #define NP8_ROWJ(k) s_j[k]
+#define NP8_ROWD(v, k) s_dist[k]
 #else
 #define NP8_ROWF(v, f, k) readlane_d(v, k)
 #define NP8_ROWJ(k) __builtin_amdgcn_readlane(jq, k)
+#define NP8_ROWD(v, k) __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), k))
 #endif
-    auto walk = [&](auto row_of, int n, bool mine, bool own_skip) {
+    // The screen (AssignArgs::walk_screen): row j is left out for the wave when for every walking lane
+    //   lw_j(x) = c_j + log n_j - iso_j |x - mu_j|^2 / 2 <= c_j + log n_j - iso_j gap^2 / 2,
+    //   gap = max(|mu_j - mu_own| - |x - mu_own|, |x - mu_own| - |mu_j - mu_own|, 0)  (triangle inequality)
+    // lies below the lane's running maximum T by kSkip + 2 nats (plus 1e-9 of the terms): the row's pick_step would
+    // return at once and ensure_u draw nothing for every lane -- the row changes no result.  |mu_j - mu_own| comes
+    // from the lists' build (pdist, every pair of dense rows, rounded down; 2^-21 relative up for the upper side), for
+    // the lanes whose own row is the one staged (jg: the list's row, or the first walking lane's for the table);
+    // other lanes take gap = 0.  Valid while the lists are (the same table).  Cost per row: the bound instead of the
+    // quadratic form and the pick -- above all for the lanes beyond their list's radius, which walk the whole table.
+    const double d_own = sqrt(d2own);
+    const bool screen = A.walk_screen != 0 && A.pdist != nullptr && A.use_lists && lists_ok;
+    auto walk = [&](auto row_of, int32_t jg, int n, bool mine, bool own_skip) {
+        const bool known = jo == jg;
         const int nact = __popcll(__ballot(1));
         for (int qb = 0; qb < n; qb += nact) {
             const int q = qb + lane;
             int32_t jq = 0;
             double fm[D], fiso = 0.0, fc = 0.0, fl = 0.0, fsl = 0.0;
+            float fdist = 0.0f;
 #pragma unroll
             for (int a = 0; a < D; ++a) fm[a] = 0.0;
             if (q < n) {
                 jq = row_of(q);
+                if (screen) fdist = A.pdist[(int64_t)jg * A.ls + jq];
                 const double *e = cand + (int64_t)jq * CS;
 #pragma unroll
                 for (int a = 0; a < D; ++a) fm[a] = e[a];
@@ -835,11 +852,24 @@ __global__ __launch_bounds__(NP8_ASSIGN_BLOCK) __attribute__((amdgpu_waves_per_e
             s_row[D + 2][lane] = fl;
             s_row[D + 3][lane] = fsl;
             s_j[lane] = jq;
+            s_dist[lane] = fdist;
             __syncthreads();
 #endif
             const int nb = min(nact, n - qb);
             for (int k = 0; k < nb; ++k) {  // wave-uniform: the rows in order (ascending)
                 const double iso = NP8_ROWF(fiso, D, k);
+                if (screen) {  // (wave-uniform)
+                    bool need = mine && !defer;
+                    if (need && iso > 0.0) {
+                        const double base = NP8_ROWF(fc, D + 1, k) + NP8_ROWF(fl, D + 2, k);
+                        const double dl = (double)NP8_ROWD(fdist, k);
+                        const double gap = known ? fmax(fmax(dl - d_own, fma(-dl, 1.0 + 0x1p-21, d_own)), 0.0) : 0.0;
+                        const double far = 0.5 * iso * gap * gap;
+                        const double U = base - far - st.T;
+                        need = !(U <= -kSkip - 2.0 - 1e-9 * (fabs(base) + fabs(st.T) + far));
+                    }
+                    if (__ballot(need) == 0ull) continue;
+                }
                 if (mine && !defer) {
                     if (!(iso > 0.0)) {
                         defer = true;
@@ -880,13 +910,15 @@ __global__ __launch_bounds__(NP8_ASSIGN_BLOCK) __attribute__((amdgpu_waves_per_e
                 mine = !full;
             }
             if (__ballot(mine) == 0ull) continue;
-            walk([&](int q) { return A.plist[(int64_t)j0 * A.ls + q]; }, nl0, mine, false);
+            walk([&](int q) { return A.plist[(int64_t)j0 * A.ls + q]; }, j0, nl0, mine, false);
         }
     }
-    if (__ballot(full && !defer))  // wave-uniform row loop over the lanes that need it
-        walk([](int q) { return q; }, K, full && !defer, true);
+    if (const uint64_t fw = __ballot(full && !defer))  // wave-uniform row loop over the lanes that need it
+        walk([](int q) { return q; }, __builtin_amdgcn_readlane(jo, __ffsll((unsigned long long)fw) - 1), K,
+             full && !defer, true);
 #undef NP8_ROWF
 #undef NP8_ROWJ
+#undef NP8_ROWD
     NP8_CLK(3);
     // the auxiliaries: np8_assign's two-level screen, then the exact fp64 draw for the lanes it cannot clear;
     // a lane that picks an auxiliary makes a new-cluster request (appended below)
@@ -1260,6 +1292,12 @@ __device__ Fx partials_sum(const Fx *__restrict__ part, int64_t n, Fx *sh) {
 }  // namespace
 
 // ---- candidate pruning ------------------------------------------------------------------------------
+// v >= 0 as a float no larger than v (a distance the walk's screen may only underestimate)
+__device__ __forceinline__ float f32_down(double v) {
+    const float f = (float)v;
+    return ((double)f > v) ? __int_as_float(__float_as_int(f) - 1) : f;
+}
+
 // For dense row k0 (mean mu0, radius R = max |x - mu0| over its items, collected by the sweep), row j
 // can be left out of k0's list when no item of k0 can bring it within kSkip of its own log-weight:
 //   lw_j(x) - lw_own(x) <= (c_j + log n_j) - (c_0 + log(n_0 - 1)) - iso_j (|mu_j - mu0| - R)^2 / 2
@@ -1275,7 +1313,7 @@ constexpr int kPruneBlocks = 32;  // np8_prune grid: 128 rows per pass
 // R2of(slot): the squared radius of the slot's items that will walk the list.
 template <int DT = 0, typename R2of>
 __device__ void prune_row(const double *__restrict__ cand, R2of R2of_slot, int32_t *__restrict__ plist,
-                          int32_t *__restrict__ plen, double *__restrict__ plr2, int32_t *__restrict__ plen_s,
+                          float *__restrict__ pdist, int32_t *__restrict__ plen, double *__restrict__ plr2, int32_t *__restrict__ plen_s,
                           double *__restrict__ plr2_s, int ls, int Drt, int K, int k0, double *__restrict__ lb, int kcap) {
     const int D = DT > 0 ? DT : Drt;
     const int DP = D * (D + 1) / 2, CS = cand_stride(D), F = D + DP;
@@ -1291,20 +1329,21 @@ __device__ void prune_row(const double *__restrict__ cand, R2of R2of_slot, int32
     for (int jb = 0; jb < K; jb += 64) {
         const int j = jb + lane;
         bool keep = j < K && j != k0;
-        if (keep && prunable) {
+        if (j < K) {
             const double *ej = cand + (int64_t)j * CS;
-            const double isoj = ej[F + kFieldIso];
-            if (isoj > 0.0) {
-                double dist2 = 0.0;
+            double dist2 = 0.0;
 #pragma unroll
-                for (int a = 0; a < (DT > 0 ? DT : 1); ++a) {  // DT: fully unrolled
-                    const double dd = ej[a] - e0[a];
-                    dist2 = fma(dd, dd, dist2);
-                }
-                for (int a = (DT > 0 ? DT : 1); a < D; ++a) {  // runtime D (only when DT == 0)
-                    const double dd = ej[a] - e0[a];
-                    dist2 = fma(dd, dd, dist2);
-                }
+            for (int a = 0; a < (DT > 0 ? DT : 1); ++a) {  // DT: fully unrolled
+                const double dd = ej[a] - e0[a];
+                dist2 = fma(dd, dd, dist2);
+            }
+            for (int a = (DT > 0 ? DT : 1); a < D; ++a) {  // runtime D (only when DT == 0)
+                const double dd = ej[a] - e0[a];
+                dist2 = fma(dd, dd, dist2);
+            }
+            if (pdist) pdist[(int64_t)k0 * ls + j] = f32_down(sqrt(dist2));  // (every pair: the walk's screen)
+            const double isoj = ej[F + kFieldIso];
+            if (keep && prunable && isoj > 0.0) {
                 const double delta = sqrt(dist2) - R;
                 if (delta > 0.0) {
                     const double wj = ej[F + kFieldC] + ej[F + kFieldLogn];
@@ -1899,7 +1938,7 @@ __device__ void prune_block(const PruneArgs &A, unsigned char *smem, size_t lds_
     auto R2of = [&](int slot) { return src[slot]; };
     if ((size_t)K * RW * sizeof(double) > lds_bytes) {
         for (int k0 = wid; k0 < K; k0 += nwb)  // wave-uniform
-            prune_row<D>(A.cand, R2of, A.plist, A.plen, A.plr2, A.plen_s, A.plr2_s, A.ls, A.D, K, k0, A.lb, A.kcap);
+            prune_row<D>(A.cand, R2of, A.plist, A.pdist, A.plen, A.plr2, A.plen_s, A.plr2_s, A.ls, A.D, K, k0, A.lb, A.kcap);
     } else {
         double *st = reinterpret_cast<double *>(smem);
         for (int idx = tid; idx < K * RW; idx += kFinThreads) {
@@ -1936,15 +1975,16 @@ __device__ void prune_block(const PruneArgs &A, unsigned char *smem, size_t lds_
             for (int jb = 0; jb < K; jb += 64) {
                 const int j = jb + lane;
                 bool keep = j < K && j != k0;
-                if (keep && prunable) {
-                    const double isoj = st[(D + 2) * K + j];
-                    if (isoj > 0.0) {
-                        double dist2 = 0.0;
+                if (j < K) {
+                    double dist2 = 0.0;
 #pragma unroll
-                        for (int a = 0; a < D; ++a) {
-                            const double dd = st[a * K + j] - st[a * K + k0];
-                            dist2 = fma(dd, dd, dist2);
-                        }
+                    for (int a = 0; a < D; ++a) {
+                        const double dd = st[a * K + j] - st[a * K + k0];
+                        dist2 = fma(dd, dd, dist2);
+                    }
+                    if (A.pdist) A.pdist[(int64_t)k0 * A.ls + j] = f32_down(sqrt(dist2));
+                    const double isoj = st[(D + 2) * K + j];
+                    if (keep && prunable && isoj > 0.0) {
                         const double delta = sqrt(dist2) - R;
                         if (delta > 0.0) {
                             const double wj = st[D * K + j];
@@ -2093,7 +2133,7 @@ __global__ __launch_bounds__(kFinThreads) void np8_fin_prune(FinArgs F, PruneArg
         auto R2of = [&](int slot) { return src[slot]; };
         constexpr int kWaves = kFinThreads / 64;
         for (int k0 = ((int)blockIdx.x - 1) * kWaves + ((int)threadIdx.x >> 6); k0 < K; k0 += nP * kWaves)  // wave-uniform
-            prune_row<DT>(P.cand, R2of, P.plist, P.plen, P.plr2, P.plen_s, P.plr2_s, P.ls, P.D, K, k0, P.lb, P.kcap);
+            prune_row<DT>(P.cand, R2of, P.plist, P.pdist, P.plen, P.plr2, P.plen_s, P.plr2_s, P.ls, P.D, K, k0, P.lb, P.kcap);
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -2896,7 +2936,7 @@ __global__ __launch_bounds__(256) void np8_prune(PruneArgs A) {
         for (int s = threadIdx.x; s < A.kcap; s += blockDim.x) A.r2[A.kcap + s] = 0.0;
     auto R2of = [&](int slot) { return src[slot]; };
     for (int k0 = blockIdx.x * 4 + (threadIdx.x >> 6); k0 < K; k0 += gridDim.x * 4)  // wave-uniform
-        prune_row<DT>(A.cand, R2of, A.plist, A.plen, A.plr2, A.plen_s, A.plr2_s, A.ls, A.D, K, k0, A.lb, A.kcap);
+        prune_row<DT>(A.cand, R2of, A.plist, A.pdist, A.plen, A.plr2, A.plen_s, A.plr2_s, A.ls, A.D, K, k0, A.lb, A.kcap);
 }
 
 __global__ void np8_advance_epoch(Ctl *ctl, uint32_t n) {

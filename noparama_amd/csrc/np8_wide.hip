@@ -439,13 +439,15 @@ __global__ void np8_wide_clean(WideArgs W) {
 // of its items' log-likelihoods under their new labels in llpart (a requester under its old slot: np8_ll_fix_wide moves
 // the accepted ones once their slots exist) -- np8_loglik_wide_mfma's values, the own and walked rows' q being the
 // same contractions.
-template <int DT, int M, int PRIOR, bool DIAGU, bool LL>
+template <int DT, int M, int PRIOR, bool DIAGU, bool LL, bool EXACT>
 #ifndef NP8_WIDE_WAVES
 #define NP8_WIDE_WAVES 2
 #endif
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NP8_WIDE_WAVES, NP8_WIDE_WAVES))) void np8_assign_wide(AssignArgs A) {
     using W = Wide<DT>;
-    const int D = A.dim, DP = D * (D + 1) / 2, CS = cand_stride(D), F = D + DP;  // (the data's D: hyp, cand, records)
+    // the data's D (hyp, cand, records): EXACT = D is DT itself, a constant of the instance -- the DIAGU frame loop,
+    // the auxiliaries' D chi^2 draws and every table offset fold (a runtime D cost C5's assign 235 -> 338 us)
+    const int D = EXACT ? DT : A.dim, DP = D * (D + 1) / 2, CS = cand_stride(D), F = D + DP;
     extern __shared__ __attribute__((aligned(16))) float stage[];
     const int lane = threadIdx.x & 63, g = lane >> 4, col = lane & 15;
     const int64_t pw = A.p0 + (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63);
@@ -1227,25 +1229,28 @@ hipError_t np8_launch_assign_wide(const AssignArgs &A, int D, int M, int prior, 
     if (n <= 0) return hipSuccess;
     const dim3 grid((unsigned)((n + 255) / 256)), block(256);
     const int DT = wide_dt(D);
+    const bool exact = D == DT;  // (D a multiple of 16: the instances with a constant D)
+#define AW(d, m, prior_, diag_, ll_, ex_) hipLaunchKernelGGL((np8_assign_wide<d, m, prior_, diag_, ll_, ex_>), grid, block, lds, s, A)
 #define X(d, m)                                                                                              \
     if (DT == d && M == m) {                                                                                 \
         const size_t lds = 2 * sizeof(float) * Wide<d>::ROW;                                                 \
         if (prior == kPriorNiw && diag_u && A.ll_on)                                                         \
-            hipLaunchKernelGGL((np8_assign_wide<d, m, kPriorNiw, true, true>), grid, block, lds, s, A);      \
+            { if (exact) AW(d, m, kPriorNiw, true, true, true); else AW(d, m, kPriorNiw, true, true, false); }          \
         else if (prior == kPriorNiw && diag_u)                                                               \
-            hipLaunchKernelGGL((np8_assign_wide<d, m, kPriorNiw, true, false>), grid, block, lds, s, A);     \
+            { if (exact) AW(d, m, kPriorNiw, true, false, true); else AW(d, m, kPriorNiw, true, false, false); }        \
         else if (prior == kPriorNiw)                                                                         \
-            hipLaunchKernelGGL((np8_assign_wide<d, m, kPriorNiw, false, false>), grid, block, lds, s, A);    \
+            AW(d, m, kPriorNiw, false, false, false);                                                        \
         else if (diag_u && A.ll_on)                                                                          \
-            hipLaunchKernelGGL((np8_assign_wide<d, m, kPriorReference, true, true>), grid, block, lds, s, A); \
+            { if (exact) AW(d, m, kPriorReference, true, true, true); else AW(d, m, kPriorReference, true, true, false); } \
         else if (diag_u)                                                                                     \
-            hipLaunchKernelGGL((np8_assign_wide<d, m, kPriorReference, true, false>), grid, block, lds, s, A); \
+            { if (exact) AW(d, m, kPriorReference, true, false, true); else AW(d, m, kPriorReference, true, false, false); } \
         else                                                                                                 \
-            hipLaunchKernelGGL((np8_assign_wide<d, m, kPriorReference, false, false>), grid, block, lds, s, A); \
+            AW(d, m, kPriorReference, false, false, false);                                                  \
         return hipGetLastError();                                                                            \
     }
     NP8_WIDE_FOR_EACH(X)
 #undef X
+#undef AW
     return hipErrorInvalidValue;
 }
 

@@ -29,6 +29,7 @@ NP8_ERR_HIP = -6
 NP8_ERR_COMM = -7
 NP8_REQ_MAX = 4096
 NP8_REQ_DEFAULT = 1024
+NP8_SUBSTEPS_AUTO = -1  # np8_config.substeps: chosen by np8_set_data from n_global (include/np8.h)
 
 _ERRNAMES = {
     NP8_ERR_ARG: "NP8_ERR_ARG",
@@ -115,6 +116,7 @@ class Stats(C.Structure):
         ("tail_steps", C.c_int64),
         ("pick_evals", C.c_int64),
         ("compact_halts", C.c_int64),
+        ("substeps", C.c_int64),
     ]
 
 
@@ -211,10 +213,11 @@ class NealAlgorithm8:
     `req_max`: new clusters one synchronous step may create (0: NP8_REQ_DEFAULT); requests beyond it
     or beyond the free slots are deferred to the item's next update (lowest scan positions first).
     `prior`: "reference" (the reference's G0 as it draws) or "niw" (a proper Normal-Inverse-Wishart with
-    kappa0 = kappa, nu0 = nu >= D + 1, Psi0 = Lambda).  `contraction`: "f64" (D <= 16) or "f32" (D in
-    {32, 48, 64}: items in fp32, cluster likelihoods on the fp32 matrix cores; config C5).
+    kappa0 = kappa, nu0 = nu >= D + 1, Psi0 = Lambda).  `contraction`: "f64" (D <= 16) or "f32" (16 < D <= 80:
+    items in fp32, cluster likelihoods on the fp32 matrix cores; config C5).
     `substeps`: the data-parallel sweep (chunk 0) as S synchronous sub-steps over a fixed hash partition of
-    the items (DESIGN.md "Sub-steps"); 1 = one step against the sweep-start state.
+    the items (DESIGN.md "Sub-steps"); 1 = one step against the sweep-start state; "auto" = 16 sub-steps for
+    data sets of at most 8192 items (where one step over-splits), else one (resolved by set_data).
     """
 
     def __init__(self, D, M=3, alpha=1.0, mu0=None, kappa=1.0 / 500, nu=4.0, Lambda=None, seed=0, kcap=None,
@@ -242,8 +245,12 @@ class NealAlgorithm8:
         cfg.contraction = CONTRACTION[contraction]
         cfg.req_max = int(req_max)
         self.req_max = int(req_max) or NP8_REQ_DEFAULT
-        cfg.substeps = int(substeps)
-        self.substeps = max(int(substeps), 1)
+        auto = isinstance(substeps, str)
+        if auto and substeps != "auto":
+            raise ValueError('substeps must be an int or "auto"')
+        cfg.substeps = NP8_SUBSTEPS_AUTO if auto else int(substeps)
+        self.substeps = 1 if auto else max(int(substeps), 1)  # ("auto": set_data resolves it)
+        self._substeps_auto = auto
         h = C.c_void_p()
         r = lib().np8_create_sized(C.byref(h), C.byref(cfg), C.sizeof(cfg))
         if r:
@@ -279,6 +286,8 @@ class NealAlgorithm8:
         self._tracked, self._slot_id = None, {}
         self._check(lib().np8_set_data(self._h, _p(X), self.N, self.D, int(offset),
                                        int(self.N if n_global is None else n_global)))
+        if self._substeps_auto:
+            self.substeps = int(self.stats()["substeps"])
 
     def set_state(self, z, mu, sigma, counts=None):
         """Labels of this shard; counts = global cluster sizes (host-exchange runs), else derived."""

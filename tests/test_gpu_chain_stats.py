@@ -84,8 +84,9 @@ def test_sequential_gpu_chain_matches_reference_sampler():
 @pytest.mark.timeout(300)
 def test_data_parallel_gpu_chain_scores_like_reference_sampler():
     """The data-parallel sweep in 16 synchronous sub-steps (DESIGN.md "Sub-steps"; 12 items per sub-step on
-    twogaussians): within SURVEY's tolerances and 3.5 standard errors of the sequential sampler."""
-    runs = [gpu_run(30000 + s, chunk=0, substeps=16) for s in range(40)]
+    twogaussians): within SURVEY's tolerances and 3.5 standard errors of the sequential sampler.  Run as
+    substeps = "auto", the host driver's default (16 sub-steps up to 8192 items, include/np8.h)."""
+    runs = [gpu_run(30000 + s, chunk=0, substeps="auto") for s in range(40)]
     compare(runs, "maxlik")
     compare(runs, "last", tol=False)
 

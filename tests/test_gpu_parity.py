@@ -401,6 +401,29 @@ def test_substeps_twogaussians_bit_exact(S):
         assert_same_state(g, o, which=1)
 
 
+def test_substeps_auto_resolves_by_data_size():
+    """substeps = "auto" (NP8_SUBSTEPS_AUTO, include/np8.h): 16 sub-steps on twogaussians (N = 200, where one step
+    over-splits), the same chain as an explicit 16 and as the oracle's; one step above 8192 items."""
+    X, _ = datasets.twogaussians()
+    g, o = pair(2, 33, kcap=512, substeps=16)
+    from noparama_amd import NealAlgorithm8
+
+    a = NealAlgorithm8(2, seed=33, kcap=512, device=0, substeps="auto")
+    try:
+        for s in (g, o, a):
+            s.set_data(X)
+            s.init_random(20)
+        assert a.substeps == 16 and a.stats()["substeps"] == 16
+        for s in (g, o, a):
+            s.sweep(12)
+        assert_same_state(g, o)
+        assert np.array_equal(a.state()["z"], g.state()["z"])
+        a.set_data(datasets.mixture(8193, 2, 4, 0.5, 8.0, seed=1)[0])
+        assert a.substeps == 1 and a.stats()["substeps"] == 1
+    finally:
+        a.close()
+
+
 @pytest.mark.parametrize("S,param_update", [(4, "frozen"), (8, "frozen"), (8, "mh_g0")])
 def test_substeps_warm_c3_shape_bit_exact(S, param_update):
     """C3's shape (D = 8, K = 64) from the warm state with candidate pruning across sub-steps (lists
