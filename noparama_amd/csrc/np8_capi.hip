@@ -89,6 +89,7 @@ struct np8_ctx {
     int32_t *plist = nullptr, *plen = nullptr;
     float *pdist = nullptr;  // beside plist: the listed rows' distances to the list's own row (the walk's screen)
     int32_t walk_screen = 1;  // NP8_WALK_SCREEN=0: np8_assign_fast evaluates every listed row
+    int32_t max_groups = kMaxListGroups;  // NP8_MAX_LIST_GROUPS: own rows per wave walked list by list (more: the whole table)
     unsigned long long *evalc = nullptr;  // [kEvalSlots][2] executed-work counters (timing mode)
     bool prune_on = false;     // kcap small enough for kcap x kcap lists
     bool wide_prune_off = false;  // NP8_NO_PRUNE=1: the wide path evaluates every row (A/B runs)
@@ -907,6 +908,7 @@ AssignArgs assign_args(np8_ctx *c, int64_t p0, int64_t p1, const int64_t *order,
     A.plist = c->plist;
     A.pdist = c->pdist;
     A.walk_screen = c->walk_screen;
+    A.max_groups = c->max_groups;
     A.plen = c->plen;
     A.plr2 = c->plr2;
     A.ls = c->kcap;
@@ -1834,6 +1836,7 @@ int np8_create_sized(np8_ctx **out, const np8_config *cfg_in, size_t cfg_bytes) 
     c->queue_on = std::getenv("NP8_QUEUE") != nullptr;
     c->tailcond_off = std::getenv("NP8_LISTS_ALWAYS") != nullptr;
     c->walk_screen = !(std::getenv("NP8_WALK_SCREEN") && std::getenv("NP8_WALK_SCREEN")[0] == '0');
+    if (const char *g = std::getenv("NP8_MAX_LIST_GROUPS")) c->max_groups = std::max(1, std::min(64, std::atoi(g)));
     c->sort_in_graph = std::getenv("NP8_SORT_IN_GRAPH") != nullptr;
     if (!c->sort_in_graph) {  // host-mapped mirror of ctl->moved (written by every finalize)
         if (hipHostMalloc((void **)&c->moved_host, sizeof(int64_t), hipHostMallocMapped) != hipSuccess ||

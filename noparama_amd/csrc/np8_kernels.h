@@ -210,6 +210,7 @@ struct AssignArgs {
     const double *plr2;  // per dense row: the squared radius its list assumes (+inf: a full list)
     int32_t ls, use_lists, collect_r2, count_eval;
     int32_t walk_screen;  // np8_assign_fast: screen each listed row for the wave before its quadratic forms
+    int32_t max_groups;   // own rows per wave up to which the lanes walk their lists group by group (else the table)
     double *r2;      // [2][kcap]: radii in use | gathered this sweep (collect_r2: mixed waves atomicMax here)
     WaveR2 *wr2;     // [ceil(n_loc / 64)]: a wave whose 64 items sit in one slot stores its maximum here
     unsigned long long *evalc;  // [kEvalSlots][2]: quadratic forms, isotropic ones
@@ -546,6 +547,9 @@ struct ParamArgs {
     int32_t *part_slot = nullptr;  // [waves * kSuffRuns]: the run's slot, -1 unused
 };
 
+// Own rows per wave up to which np8_assign(_fast)'s lanes walk their rows' lists group by group (default of
+// AssignArgs::max_groups; NP8_MAX_LIST_GROUPS overrides it).
+constexpr int kMaxListGroups = 3;
 constexpr int kSuffRuns = 4;  // run records per wave of np8_suffstats_wide
 
 struct SnapArgs {

@@ -235,7 +235,9 @@ __device__ __forceinline__ void ensure_u(PickState &st, double lw, uint64_t seed
 }
 
 // Own rows per wave up to which the lanes walk their rows' pruned lists group by group (np8_assign).
-constexpr int kMaxListGroups = 3;
+// (own rows per wave walked list by list: AssignArgs::max_groups, kMaxListGroups in np8_kernels.h)
+// Own rows per wave whose row distances np8_assign_fast's walk screen stages (LDS: kScreenGroups x 64 floats).
+constexpr int kScreenGroups = 4;
 
 __device__ __forceinline__ int64_t position_to_local(const AssignArgs &A, int64_t p) {
     if (A.order) return A.order[p];
@@ -254,6 +256,9 @@ template <int D, int M, int PRIOR, bool COUNT>
 #endif
 #ifndef NP8_WALK_LDS
 #define NP8_WALK_LDS 1  // np8_assign_fast's candidate walk broadcasts rows through LDS (0: v_readlane)
+#endif
+#if !NP8_WALK_LDS
+#error "np8_assign_fast's walk screen stages its row distances beside the LDS rows"
 #endif
 #ifndef NP8_FAST_WAVES
 #define NP8_FAST_WAVES 4  // 127 VGPRs, 30 dwords spilled on the rare paths (62 KB written per C3 launch); 5: 2-6% slower
@@ -314,10 +319,10 @@ __device__ __forceinline__ void assign_item(const AssignArgs &A, const int64_t p
     int32_t pslot = zi;                  // slot of the picked row (no reload of the row at the end)
     // (a wave of many own rows -- a stale layout, a cold start -- walks the table once instead)
     int ngroups = 0;
-    for (uint64_t pend = __ballot(1); pend && ngroups <= kMaxListGroups; ++ngroups)
+    for (uint64_t pend = __ballot(1); pend && ngroups <= A.max_groups; ++ngroups)
         pend &= ~__ballot(jo == __builtin_amdgcn_readlane(jo, __ffsll((unsigned long long)pend) - 1));
     bool full = true;  // this lane walks the whole table
-    if (A.use_lists && A.ctl->lists_ok && ngroups <= kMaxListGroups) {
+    if (A.use_lists && A.ctl->lists_ok && ngroups <= A.max_groups) {
         uint64_t pend = __ballot(1);
         while (pend) {
             const int32_t j0 = __builtin_amdgcn_readlane(jo, __ffsll((unsigned long long)pend) - 1);
@@ -370,7 +375,7 @@ __device__ __forceinline__ void assign_item(const AssignArgs &A, const int64_t p
             unsigned long long *ec = A.evalc + 4 * kEvalSlots + 2 * w;
             atomicAdd(ec, (unsigned long long)__popcll(fb));
             atomicAdd(ec + 1, fb ? 1ull : 0ull);
-            atomicAdd(ec + 2 * kEvalSlots, (ngroups > kMaxListGroups) ? 1ull : 0ull);
+            atomicAdd(ec + 2 * kEvalSlots, (ngroups > A.max_groups) ? 1ull : 0ull);
             atomicAdd(ec + 2 * kEvalSlots + 1, (unsigned long long)nl_w);
         }
     }
@@ -618,6 +623,13 @@ __device__ unsigned long long g_np8_clk[kClkWaves * 8];
         if (!COUNT && (threadIdx.x & 63) == 0 && w_ < kClkWaves)                                       \
             g_np8_clk[w_ * 8 + (k)] = __builtin_amdgcn_s_memrealtime();                                \
     } while (0)
+// slot 7: the wave's walk shape (own-row passes | list groups << 8 | table walk << 16 | listed rows walked << 20)
+#define NP8_CLK_INFO(v)                                                                                \
+    do {                                                                                               \
+        const int64_t w_ = (p - A.p0) >> 6;                                                            \
+        if (!COUNT && (threadIdx.x & 63) == 0 && w_ < kClkWaves) g_np8_clk[w_ * 8 + 7] = (v);          \
+    } while (0)
+#define NP8_CLK_ON 1
 extern "C" int np8_exp_clocks(unsigned long long *out, int64_t n) {
     if (n > kClkWaves * 8) n = kClkWaves * 8;
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_np8_clk), sizeof(unsigned long long) * n, 0, hipMemcpyDeviceToHost) ==
@@ -625,6 +637,8 @@ extern "C" int np8_exp_clocks(unsigned long long *out, int64_t n) {
 }
 #else
 #define NP8_CLK(k)
+#define NP8_CLK_INFO(v)
+#define NP8_CLK_ON 0
 #endif
 
 // ---- the data-parallel sweep's fast path -------------------------------------------------------------
@@ -703,6 +717,7 @@ __global__ __launch_bounds__(NP8_ASSIGN_BLOCK) __attribute__((amdgpu_waves_per_e
     }
     NP8_CLK(1);
     bool defer = COUNT;  // counting runs: every lane takes np8_assign's counting instance
+    [[maybe_unused]] unsigned long long clk_own = 1, clk_rows = 0;  // (NP8_EXP_CLOCKS: the walk's shape)
     PickState st;
     st.S = 1.0;
     st.u = -1.0;
@@ -773,14 +788,17 @@ __global__ __launch_bounds__(NP8_ASSIGN_BLOCK) __attribute__((amdgpu_waves_per_e
             }
         };
         own(s_1, mo_1, iso_1, cs_1, l1_1, js_1, pl_1, pr_1);  // the first group, from the loads issued above
-        uint64_t pend = __ballot(zi != s_1);
-        while (pend) {  // (waves of several own slots: a stale layout, the range's edges)
-            const int32_t s = __builtin_amdgcn_readlane(zi, __ffsll((unsigned long long)pend) - 1);
-            double mo[D];
+        // waves of several own slots (a layout gone stale between re-sorts, the range's edges): the other lanes gather
+        // their rows' fields with vector loads, one round trip whatever the number of slots (a scalar round per slot
+        // cost a stale wave ~2 us each)
+        if (__ballot(zi != s_1)) {
+            if (NP8_CLK_ON) clk_own = 1 + __popcll(__ballot(zi != s_1));
+            if (zi != s_1) {
+                double mo[D];
 #pragma unroll
-            for (int a = 0; a < D; ++a) mo[a] = slot_mu[(int64_t)s * D + a];
-            own(s, mo, slot_iso[s], slot_c[s], slot_logn1[s], dense_of[s], plen_s[s], plr2_s[s]);
-            pend &= ~__ballot(zi == s);
+                for (int a = 0; a < D; ++a) mo[a] = slot_mu[(int64_t)zi * D + a];
+                own(zi, mo, slot_iso[zi], slot_c[zi], slot_logn1[zi], dense_of[zi], plen_s[zi], plr2_s[zi]);
+            }
         }
     }
     if (COUNT) defer = true;
@@ -789,52 +807,64 @@ __global__ __launch_bounds__(NP8_ASSIGN_BLOCK) __attribute__((amdgpu_waves_per_e
     NP8_CLK(2);
     const double zslot = (double)zi;
     int ngroups = 0;
-    for (uint64_t pend = __ballot(1); pend && ngroups <= kMaxListGroups; ++ngroups)
+    for (uint64_t pend = __ballot(1); pend && ngroups <= A.max_groups; ++ngroups)
         pend &= ~__ballot(jo == __builtin_amdgcn_readlane(jo, __ffsll((unsigned long long)pend) - 1));
     bool full = !defer;  // this lane walks the whole table
     // rows row_of(0 .. n-1) (wave-uniform), for the lanes with `mine`: a wave's worth of rows per round of loads
     // (lane q: row q's fields, the wave's active lanes are 0 .. nact - 1 -- the last wave of the range is
     // partial), then broadcast row by row: no dependent load per row (the mixed regime walks ~9 rows per item,
     // a stale wave the whole table).  A row that is not isotropic defers the lane (np8_assign takes it).
+    __shared__ float s_dist[kScreenGroups][64];  // the walk screen's row distances (below), per staged own row
 #if NP8_WALK_LDS
     // the round's rows staged in LDS ([field][row], one-wave workgroups) and read back at a wave-uniform address
     // (a broadcast on the LDS pipe) instead of 2 v_readlane per double on the VALU
     static_assert(NP8_ASSIGN_BLOCK == 64, "the walk's LDS rows are per wave");
     __shared__ double s_row[D + 4][64];
     __shared__ int32_t s_j[64];
-    __shared__ float s_dist[64];
 #define NP8_ROWF(v, f, k) s_row[f][k]
 #define NP8_ROWJ(k) s_j[k]
-#define NP8_ROWD(v, k) s_dist[k]
 #else
 #define NP8_ROWF(v, f, k) readlane_d(v, k)
 #define NP8_ROWJ(k) __builtin_amdgcn_readlane(jq, k)
-#define NP8_ROWD(v, k) __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), k))
 #endif
     // The screen (AssignArgs::walk_screen): row j is left out for the wave when for every walking lane
     //   lw_j(x) = c_j + log n_j - iso_j |x - mu_j|^2 / 2 <= c_j + log n_j - iso_j gap^2 / 2,
     //   gap = max(|mu_j - mu_own| - |x - mu_own|, |x - mu_own| - |mu_j - mu_own|, 0)  (triangle inequality)
     // lies below the lane's running maximum T by kSkip + 2 nats (plus 1e-9 of the terms): the row's pick_step would
     // return at once and ensure_u draw nothing for every lane -- the row changes no result.  |mu_j - mu_own| comes
-    // from the lists' build (pdist, every pair of dense rows, rounded down; 2^-21 relative up for the upper side), for
-    // the lanes whose own row is the one staged (jg: the list's row, or the first walking lane's for the table);
-    // other lanes take gap = 0.  Valid while the lists are (the same table).  Cost per row: the bound instead of the
-    // quadratic form and the pick -- above all for the lanes beyond their list's radius, which walk the whole table.
+    // from the lists' build (pdist, every pair of dense rows, rounded down; 2^-21 relative up for the upper side),
+    // staged per round for the first kScreenGroups own rows among the walking lanes (a list walk has one, a table walk
+    // of a wave with several labels several); lanes of further own rows take gap = 0.  Valid while the lists are (the
+    // same table).  Cost per row: the bound instead of the quadratic form and the pick.
     const double d_own = sqrt(d2own);
     const bool screen = A.walk_screen != 0 && A.pdist != nullptr && A.use_lists && lists_ok;
-    auto walk = [&](auto row_of, int32_t jg, int n, bool mine, bool own_skip) {
-        const bool known = jo == jg;
+    auto walk = [&](auto row_of, int n, bool mine, bool own_skip) {
+        // the walking lanes' own rows (wave-uniform, first kScreenGroups) and this lane's index among them
+        int32_t gid[kScreenGroups];
+        int ng = 0, gi = -1;
+        if (screen) {
+            uint64_t pg = __ballot(mine && !defer);
+            for (; pg && ng < kScreenGroups; ++ng) {
+                gid[ng] = __builtin_amdgcn_readlane(jo, __ffsll((unsigned long long)pg) - 1);
+                if (jo == gid[ng]) gi = ng;
+                pg &= ~__ballot(jo == gid[ng]);
+            }
+        }
         const int nact = __popcll(__ballot(1));
         for (int qb = 0; qb < n; qb += nact) {
             const int q = qb + lane;
             int32_t jq = 0;
             double fm[D], fiso = 0.0, fc = 0.0, fl = 0.0, fsl = 0.0;
-            float fdist = 0.0f;
+            float fdist[kScreenGroups];
+#pragma unroll
+            for (int g = 0; g < kScreenGroups; ++g) fdist[g] = 0.0f;
 #pragma unroll
             for (int a = 0; a < D; ++a) fm[a] = 0.0;
             if (q < n) {
                 jq = row_of(q);
-                if (screen) fdist = A.pdist[(int64_t)jg * A.ls + jq];
+#pragma unroll
+                for (int g = 0; g < kScreenGroups; ++g)
+                    if (g < ng) fdist[g] = A.pdist[(int64_t)gid[g] * A.ls + jq];
                 const double *e = cand + (int64_t)jq * CS;
 #pragma unroll
                 for (int a = 0; a < D; ++a) fm[a] = e[a];
@@ -852,7 +882,8 @@ __global__ __launch_bounds__(NP8_ASSIGN_BLOCK) __attribute__((amdgpu_waves_per_e
             s_row[D + 2][lane] = fl;
             s_row[D + 3][lane] = fsl;
             s_j[lane] = jq;
-            s_dist[lane] = fdist;
+#pragma unroll
+            for (int g = 0; g < kScreenGroups; ++g) s_dist[g][lane] = fdist[g];
             __syncthreads();
 #endif
             const int nb = min(nact, n - qb);
@@ -862,8 +893,8 @@ __global__ __launch_bounds__(NP8_ASSIGN_BLOCK) __attribute__((amdgpu_waves_per_e
                     bool need = mine && !defer;
                     if (need && iso > 0.0) {
                         const double base = NP8_ROWF(fc, D + 1, k) + NP8_ROWF(fl, D + 2, k);
-                        const double dl = (double)NP8_ROWD(fdist, k);
-                        const double gap = known ? fmax(fmax(dl - d_own, fma(-dl, 1.0 + 0x1p-21, d_own)), 0.0) : 0.0;
+                        const double dl = (gi >= 0) ? (double)s_dist[gi][k] : 0.0;
+                        const double gap = (gi >= 0) ? fmax(fmax(dl - d_own, fma(-dl, 1.0 + 0x1p-21, d_own)), 0.0) : 0.0;
                         const double far = 0.5 * iso * gap * gap;
                         const double U = base - far - st.T;
                         need = !(U <= -kSkip - 2.0 - 1e-9 * (fabs(base) + fabs(st.T) + far));
@@ -896,7 +927,7 @@ __global__ __launch_bounds__(NP8_ASSIGN_BLOCK) __attribute__((amdgpu_waves_per_e
             }
         }
     };
-    if (A.use_lists && lists_ok && ngroups <= kMaxListGroups) {  // wave-uniform
+    if (A.use_lists && lists_ok && ngroups <= A.max_groups) {  // wave-uniform
         uint64_t pend = __ballot(1);
         while (pend) {
             const int lead = __ffsll((unsigned long long)pend) - 1;
@@ -910,15 +941,16 @@ __global__ __launch_bounds__(NP8_ASSIGN_BLOCK) __attribute__((amdgpu_waves_per_e
                 mine = !full;
             }
             if (__ballot(mine) == 0ull) continue;
-            walk([&](int q) { return A.plist[(int64_t)j0 * A.ls + q]; }, j0, nl0, mine, false);
+            if (NP8_CLK_ON) clk_rows += (unsigned long long)nl0;
+            walk([&](int q) { return A.plist[(int64_t)j0 * A.ls + q]; }, nl0, mine, false);
         }
     }
-    if (const uint64_t fw = __ballot(full && !defer))  // wave-uniform row loop over the lanes that need it
-        walk([](int q) { return q; }, __builtin_amdgcn_readlane(jo, __ffsll((unsigned long long)fw) - 1), K,
-             full && !defer, true);
+    const bool table_walk = __ballot(full && !defer) != 0ull;
+    if (table_walk)  // wave-uniform row loop over the lanes that need it
+        walk([](int q) { return q; }, K, full && !defer, true);
+    NP8_CLK_INFO(clk_own | ((unsigned long long)ngroups << 8) | ((unsigned long long)table_walk << 16) | (clk_rows << 20));
 #undef NP8_ROWF
 #undef NP8_ROWJ
-#undef NP8_ROWD
     NP8_CLK(3);
     // the auxiliaries: np8_assign's two-level screen, then the exact fp64 draw for the lanes it cannot clear;
     // a lane that picks an auxiliary makes a new-cluster request (appended below)

@@ -183,18 +183,28 @@ __device__ __forceinline__ void sym_square(int D, int LD, const double *X, doubl
     }
 }
 
-// Largest |row sum| of X (one thread per row; rs: D doubles of scratch).  Block-uniform result.
+// Largest |row sum| of X (four threads per row, then the rows' sums in one wave; rs: D doubles of scratch).
+// Block-uniform result (a bound's norm: no bit-exact order needed).
 __device__ __forceinline__ double max_abs_row_sum(int D, int LD, const double *X, double *rs) {
-    for (int a = threadIdx.x; a < D; a += blockDim.x) {
+    for (int t = threadIdx.x; t < 4 * D; t += blockDim.x) {
+        const int a = t >> 2, part = t & 3;
         double v = 0.0;
-        for (int b = 0; b < D; ++b) v += fabs(X[a * LD + b]);
-        rs[a] = v;
+        for (int b = part; b < D; b += 4) v += fabs(X[a * LD + b]);
+        v += __shfl_xor(v, 1);
+        v += __shfl_xor(v, 2);
+        if (part == 0) rs[a] = v;
     }
     __syncthreads();
-    double m = 0.0;
-    for (int a = 0; a < D; ++a) m = fmax(m, rs[a]);
+    __shared__ double m_s;
+    if (threadIdx.x < 64) {
+        double m = 0.0;
+        for (int a = threadIdx.x; a < D; a += 64) m = fmax(m, rs[a]);
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) m = fmax(m, __shfl_xor(m, o));
+        if (threadIdx.x == 0) m_s = m;
+    }
     __syncthreads();
-    return m;
+    return m_s;
 }
 
 // P' = packed sym(R^T R) for R upper (element (a, b), a <= b: sum_{k <= a} R_ka R_kb, k ascending from 0), off-diagonals
@@ -225,19 +235,41 @@ constexpr int kPanelN = 16;
 // fma(0, t, +0) = +0 / fma(x, 0, v) = v leave the chain's bits alone, so a whole 16 x 16 tile takes one k range.
 typedef double f64x4 __attribute__((ext_vector_type(4)));
 
-// One 16 x 16 tile (one wave): acc(i, j) = sum_k a_at(i, k) b_at(k, j) over k = k0 .. k1 - 1 (k1 - k0 a multiple of 4;
-// accessors return 0 outside the matrices); element r of lane l is (row (l >> 4) + 4 r, column l & 15).
+// One 16 x 16 tile (one wave): acc(i, j) = acc0(i, j) + sum_k a_at(i, k) b_at(k, j) over k = k0 .. k1 - 1 (k1 - k0 a
+// multiple of 4; accessors return 0 outside the matrices); element r of lane l is (row (l >> 4) + 4 r, column l & 15).
+// Every operand of the tile is read from LDS first (at most kNiwMaxD / 4 k-steps, unrolled), then the MFMAs run back to
+// back: one LDS round trip per tile instead of one per k-step (the chain of dependent MFMAs waited on each load).
+constexpr int kNiwMaxD = 80;
+// M[o] when ok, else 0 -- the load made at offset 0 instead, so that it is unconditional (a guarded LDS load became a
+// branch around every operand of the tiles)
+__device__ __forceinline__ double lds_or0(const double *M, int o, bool ok) {
+    const double v = M[ok ? o : 0];
+    return ok ? v : 0.0;
+}
+template <class FA, class FB>
+__device__ __forceinline__ f64x4 mfma_tile_acc(f64x4 acc, FA a_at, FB b_at, int k0, int k1) {
+    const int lane = threadIdx.x & 63, il = lane & 15, kl = lane >> 4;
+    constexpr int KS = kNiwMaxD / 4;
+    double av[KS], bv[KS];
+#pragma unroll
+    for (int q = 0; q < KS; ++q) {  // (accessors are safe for any k: lds_or0)
+        const int k = k0 + 4 * q;
+        av[q] = a_at(il, k + kl);
+        bv[q] = b_at(k + kl, il);
+    }
+#pragma unroll
+    for (int q = 0; q < KS; ++q)
+        if (k0 + 4 * q < k1) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[q], bv[q], acc, 0, 0, 0);  // (wave-uniform)
+    return acc;
+}
 template <class FA, class FB>
 __device__ __forceinline__ f64x4 mfma_tile(FA a_at, FB b_at, int k0, int k1) {
-    const int lane = threadIdx.x & 63, il = lane & 15, kl = lane >> 4;
-    f64x4 acc = {0.0, 0.0, 0.0, 0.0};
-    for (int k = k0; k < k1; k += 4) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a_at(il, k + kl), b_at(k + kl, il), acc, 0, 0, 0);
-    return acc;
+    return mfma_tile_acc((f64x4){0.0, 0.0, 0.0, 0.0}, a_at, b_at, k0, k1);
 }
 
 // Sigma = T^T T (T lower): tiles ti <= tj, element (a, b) = sum over k from 16 tj (below max(a, b) a factor is zero) of
 // T_ka T_kb, mirrored -- sigma_from_t's chains (its element (b, a) is the same chain with each fma's factors swapped).
-__device__ void sigma_from_t_mfma(int D, int LD, const double *T, double *Sigma, double *Sl) {
+__device__ __forceinline__ void sigma_from_t_mfma(int D, int LD, const double *T, double *Sigma, double *Sl) {
     const int nt = (D + 15) / 16, wv = threadIdx.x >> 6, nw = blockDim.x >> 6, lane = threadIdx.x & 63;
     const int k1 = (D + 3) & ~3;
     for (int tt = wv; tt < nt * (nt + 1) / 2; tt += nw) {
@@ -247,8 +279,8 @@ __device__ void sigma_from_t_mfma(int D, int LD, const double *T, double *Sigma,
             ++ti;
         }
         const int tj = ti + rem;
-        const f64x4 acc = mfma_tile([&](int i, int k) { return (k < D && 16 * ti + i < D) ? T[k * LD + 16 * ti + i] : 0.0; },
-                                    [&](int k, int j) { return (k < D && 16 * tj + j < D) ? T[k * LD + 16 * tj + j] : 0.0; },
+        const f64x4 acc = mfma_tile([&](int i, int k) { return lds_or0(T, k * LD + 16 * ti + i, k < D && 16 * ti + i < D); },
+                                    [&](int k, int j) { return lds_or0(T, k * LD + 16 * tj + j, k < D && 16 * tj + j < D); },
                                     16 * tj, k1);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -266,7 +298,7 @@ __device__ void sigma_from_t_mfma(int D, int LD, const double *T, double *Sigma,
 }
 
 // R = B^T U^{-1} (upper): R_ab = sum_{k = a..b} B_ka M[D-1-k][D-1-b] (M = Lr^{-1} lower, B lower), 0 below the diagonal.
-__device__ void r_from_b_mfma(int D, int LD, const double *B, const double *M, double *R) {
+__device__ __forceinline__ void r_from_b_mfma(int D, int LD, const double *B, const double *M, double *R) {
     const int nt = (D + 15) / 16, wv = threadIdx.x >> 6, nw = blockDim.x >> 6, lane = threadIdx.x & 63;
     for (int e = threadIdx.x; e < D * D; e += blockDim.x) {  // the lower triangle (tiles below the diagonal included)
         const int a = e / D, b = e - a * D;
@@ -281,8 +313,8 @@ __device__ void r_from_b_mfma(int D, int LD, const double *B, const double *M, d
         const int tj = ti + rem;
         const int k1 = min((D + 3) & ~3, 16 * tj + 16);
         const f64x4 acc = mfma_tile(
-            [&](int i, int k) { return (k < D && 16 * ti + i < D) ? B[k * LD + 16 * ti + i] : 0.0; },
-            [&](int k, int j) { return (k < D && 16 * tj + j < D) ? M[(D - 1 - k) * LD + (D - 1 - (16 * tj + j))] : 0.0; },
+            [&](int i, int k) { return lds_or0(B, k * LD + 16 * ti + i, k < D && 16 * ti + i < D); },
+            [&](int k, int j) { return lds_or0(M, (D - 1 - k) * LD + (D - 1 - (16 * tj + j)), k < D && 16 * tj + j < D); },
             16 * ti, k1);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -294,7 +326,7 @@ __device__ void r_from_b_mfma(int D, int LD, const double *B, const double *M, d
 
 // P' = packed sym(R^T R) (R upper): element (a, b), a <= b, = sum_{k = 0..a} R_ka R_kb, off-diagonals doubled, into the
 // slot table and its candidate row; returns the isotropy value (write_pprime_r's).
-__device__ double write_pprime_r_mfma(int D, int LD, const double *R, double *slotP, double *candP) {
+__device__ __forceinline__ double write_pprime_r_mfma(int D, int LD, const double *R, double *slotP, double *candP) {
     const int nt = (D + 15) / 16, wv = threadIdx.x >> 6, nw = blockDim.x >> 6, lane = threadIdx.x & 63;
     const double p00 = fma(R[0], R[0], 0.0);
     bool iso = true;
@@ -306,8 +338,8 @@ __device__ double write_pprime_r_mfma(int D, int LD, const double *R, double *sl
         }
         const int tj = ti + rem;
         const int k1 = min((D + 3) & ~3, 16 * ti + 16);
-        const f64x4 acc = mfma_tile([&](int i, int k) { return (k < D && 16 * ti + i < D) ? R[k * LD + 16 * ti + i] : 0.0; },
-                                    [&](int k, int j) { return (k < D && 16 * tj + j < D) ? R[k * LD + 16 * tj + j] : 0.0; },
+        const f64x4 acc = mfma_tile([&](int i, int k) { return lds_or0(R, k * LD + 16 * ti + i, k < D && 16 * ti + i < D); },
+                                    [&](int k, int j) { return lds_or0(R, k * LD + 16 * tj + j, k < D && 16 * tj + j < D); },
                                     0, k1);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -324,13 +356,13 @@ __device__ double write_pprime_r_mfma(int D, int LD, const double *R, double *sl
 }
 
 // Y = X X (X symmetric) for the eigenvalue bound (a bound, not a bit-exact quantity): every tile.
-__device__ void sym_square_mfma(int D, int LD, const double *X, double *Y) {
+__device__ __forceinline__ void sym_square_mfma(int D, int LD, const double *X, double *Y) {
     const int nt = (D + 15) / 16, wv = threadIdx.x >> 6, nw = blockDim.x >> 6, lane = threadIdx.x & 63;
     const int k1 = (D + 3) & ~3;
     for (int tt = wv; tt < nt * nt; tt += nw) {
         const int ti = tt / nt, tj = tt - ti * nt;
-        const f64x4 acc = mfma_tile([&](int i, int k) { return (k < D && 16 * ti + i < D) ? X[(16 * ti + i) * LD + k] : 0.0; },
-                                    [&](int k, int j) { return (k < D && 16 * tj + j < D) ? X[k * LD + 16 * tj + j] : 0.0; },
+        const f64x4 acc = mfma_tile([&](int i, int k) { return lds_or0(X, (16 * ti + i) * LD + k, k < D && 16 * ti + i < D); },
+                                    [&](int k, int j) { return lds_or0(X, k * LD + 16 * tj + j, k < D && 16 * tj + j < D); },
                                     0, k1);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -352,27 +384,35 @@ constexpr int kBoundSquarings = NP8_BOUND_SQUARINGS;
 // one wave (lane = row r, its 16 panel entries in registers): per column j the pivot, the scaled column, and the
 // updates of the panel's later columns -- element (r, c) receives fma(-L_rj, L_cj, .) for j ascending, then the
 // division by its pivot.  *skip != 0 if a pivot is not positive.
+// Lane l's double (l wave-uniform) as two v_readlane: a scalar operand for the whole wave, no LDS round trip (the
+// ds_bpermute of __shfl, waited on one by one, made each column of the panel ~1 500 cycles).
+__device__ __forceinline__ double lane_d(double v, int l) {
+    const int64_t b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)(b & 0xFFFFFFFFll), l), hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+    return __longlong_as_double(((int64_t)hi << 32) | (uint32_t)lo);
+}
+
 __device__ __forceinline__ void lower_panel_factor(double *L, int LD, int D, int c0, int *skip) {
     const int lane = threadIdx.x & 63;
     double w[kPanelN];
 #pragma unroll
-    for (int i = 0; i < kPanelN; ++i) w[i] = (lane < D && c0 + i < D) ? L[lane * LD + c0 + i] : 0.0;
+    for (int i = 0; i < kPanelN; ++i) w[i] = lds_or0(L, lane * LD + c0 + i, lane < D && c0 + i < D);
     int sk = 0;
 #pragma unroll
     for (int j = 0; j < kPanelN; ++j) {
         const int jj = c0 + j;
-        if (jj >= D) break;  // (a last panel narrower than 16: D not a multiple of 16)
-        const double v = __shfl(w[j], jj);  // the pivot L[jj][jj]
-        const bool ok = v > 0.0;
-        if (!ok) sk = 1;
-        const double dj = ok ? sqrt(v) : 1e-300;
-        if (lane == jj) w[j] = dj;
-        if (lane > jj) w[j] = w[j] / dj;  // column jj of L
+        if (jj < D) {  // (wave-uniform: a last panel narrower than 16 when D is not a multiple of 16)
+            const double v = lane_d(w[j], jj);  // the pivot L[jj][jj]
+            const bool ok = v > 0.0;
+            if (!ok) sk = 1;
+            const double dj = ok ? sqrt(v) : 1e-300;
+            const double q = w[j] / dj;
+            w[j] = (lane == jj) ? dj : ((lane > jj) ? q : w[j]);  // column jj of L
 #pragma unroll
-        for (int i = j + 1; i < kPanelN; ++i) {
-            if (c0 + i >= D) break;
-            const double lcj = __shfl(w[j], c0 + i);  // L[c][jj], c = c0 + i
-            if (lane >= c0 + i) w[i] = fma(-w[j], lcj, w[i]);
+            for (int i = j + 1; i < kPanelN; ++i) {
+                const double lcj = lane_d(w[j], min(c0 + i, 63));  // L[c][jj], c = c0 + i
+                if (lane >= c0 + i && c0 + i < D) w[i] = fma(-w[j], lcj, w[i]);
+            }
         }
     }
 #pragma unroll
@@ -381,10 +421,39 @@ __device__ __forceinline__ void lower_panel_factor(double *L, int LD, int D, int
     if (lane == 0) *skip = sk;
 }
 
-// The panel's 16 updates to element (r, c), r >= c >= c0 + 16, in ascending column order; all threads.
-__device__ __forceinline__ void lower_panel_trailing(double *L, int LD, int D, int c0) {
+// The panel's 16 updates to element (r, c), r >= c >= c0 + 16, in ascending column order; all threads.  On the fp64
+// matrix cores: tile (ti, tj), tj <= ti, of the trailing lower triangle starts from L's elements and takes the 16 terms
+// fma(-L_rj, L_cj, .), j = c0 .. c0 + 15 ascending, as four k-ordered MFMA steps -- the VALU chain, bit for bit (the
+// negated factor is exact).  valu: the per-element VALU loop.
+__device__ __forceinline__ void lower_panel_trailing(double *L, int LD, int D, int c0, bool valu) {
     const int rows = D - (c0 + kPanelN);
     if (rows <= 0) return;  // (the last panel: nothing below it)
+    if (!valu) {
+        const int t0 = (c0 + kPanelN) / 16, nt = (D + 15) / 16, m = nt - t0;  // trailing tiles per side
+        const int wv = threadIdx.x >> 6, nw = blockDim.x >> 6, lane = threadIdx.x & 63;
+        for (int tt = wv; tt < m * (m + 1) / 2; tt += nw) {
+            int ti = 0, rem = tt;  // (ti, tj), tj <= ti, row-major over the lower tile triangle
+            while (rem > ti) {
+                rem -= ti + 1;
+                ++ti;
+            }
+            const int r0 = 16 * (t0 + ti), q0 = 16 * (t0 + rem);
+            f64x4 acc;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int a = r0 + (lane >> 4) + 4 * r, b = q0 + (lane & 15);
+                acc[r] = (a < D && b < D && b <= a) ? L[a * LD + b] : 0.0;
+            }
+            acc = mfma_tile_acc(acc, [&](int i, int k) { return -lds_or0(L, (r0 + i) * LD + c0 + k, r0 + i < D && k < kPanelN); },
+                                [&](int k, int j) { return lds_or0(L, (q0 + j) * LD + c0 + k, q0 + j < D && k < kPanelN); }, 0, kPanelN);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int a = r0 + (lane >> 4) + 4 * r, b = q0 + (lane & 15);
+                if (a < D && b < D && b <= a) L[a * LD + b] = acc[r];
+            }
+        }
+        return;
+    }
     // only the trailing lower triangle (r >= c >= c0 + 16): e -> (r', c') row-major, r' = floor((sqrt(8e + 1) - 1) / 2)
     for (int e = threadIdx.x; e < rows * (rows + 1) / 2; e += blockDim.x) {
         int rr = (int)((sqrt(8.0 * (double)e + 1.0) - 1.0) * 0.5);
@@ -405,17 +474,23 @@ __device__ __forceinline__ void forward_panel(double *X, const double *G, int LD
     const int lane = threadIdx.x & 63;
     double w[kPanelN];
 #pragma unroll
-    for (int i = 0; i < kPanelN; ++i) w[i] = (lane < D && c0 + i < D) ? X[(c0 + i) * LD + lane] : 0.0;
+    for (int i = 0; i < kPanelN; ++i) w[i] = lds_or0(X, (c0 + i) * LD + lane, lane < D && c0 + i < D);
 #pragma unroll
     for (int i = 0; i < kPanelN; ++i) {
         const int k = c0 + i;
-        if (k >= D) break;
-        const double gkk = G[k * LD + k];
-        const bool col = lane < D && (!inv || lane <= k);
-        if (col) w[i] = (inv && lane == k) ? 1.0 / gkk : w[i] / gkk;
+        if (k < D) {  // (wave-uniform)
+            // the row's divisor and its 15 multipliers in one round of (broadcast) LDS reads
+            double g[kPanelN];
 #pragma unroll
-        for (int i2 = i + 1; i2 < kPanelN; ++i2)
-            if (col && c0 + i2 < D) w[i2] = fma(-G[(c0 + i2) * LD + k], w[i], w[i2]);
+            for (int i2 = i; i2 < kPanelN; ++i2) g[i2] = lds_or0(G, (c0 + i2) * LD + k, c0 + i2 < D);
+            const double gkk = g[i];
+            const bool col = lane < D && (!inv || lane <= k);
+            const double q = ((inv && lane == k) ? 1.0 : w[i]) / gkk;
+            if (col) w[i] = q;
+#pragma unroll
+            for (int i2 = i + 1; i2 < kPanelN; ++i2)
+                if (col && c0 + i2 < D) w[i2] = fma(-g[i2], w[i], w[i2]);
+        }
     }
 #pragma unroll
     for (int i = 0; i < kPanelN; ++i)
@@ -425,12 +500,37 @@ __device__ __forceinline__ void forward_panel(double *X, const double *G, int LD
 // The panel's updates to rows r >= c0 + 16, fma(-G_rk, X_kj, .) for k = c0 .. c0 + 15 ascending (inv: k >= j only);
 // all threads.
 // lower: X0 (hence X) lower triangular -- elements j > r stay 0 and are skipped.
+// On the matrix cores (!valu): tile (rows r0.., columns q0..) from X's elements plus the 16 terms as four k-ordered MFMA
+// steps; the terms the VALU loop skips (inv: k < j; lower: X_kj = 0 for j > k) have X_kj = +0 and leave the chain alone
+// (fma(-g, +0, v) = v for v != -0, and the chains never hold -0: they start from +0 or nonzero values).
 __device__ __forceinline__ void forward_trailing(double *X, const double *G, int LD, int D, int c0, bool inv,
-                                                 bool lower = false) {
+                                                 bool lower, bool valu) {
     const int rows = D - (c0 + kPanelN);
     // inv / lower: the columns right of the panel get nothing from it (X_kj = 0 for j > k, every panel row k < j), so
     // only columns 0 .. c0 + 15 are visited -- a quarter of the row's elements at the first panel
     const int W = (inv || lower) ? c0 + kPanelN : D;
+    if (!valu) {
+        if (rows <= 0) return;
+        const int t0 = (c0 + kPanelN) / 16, nt = (D + 15) / 16, mr = nt - t0, mc = (W + 15) / 16;
+        const int wv = threadIdx.x >> 6, nw = blockDim.x >> 6, lane = threadIdx.x & 63;
+        for (int tt = wv; tt < mr * mc; tt += nw) {
+            const int r0 = 16 * (t0 + tt / mc), q0 = 16 * (tt % mc);
+            f64x4 acc;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int a = r0 + (lane >> 4) + 4 * r, b = q0 + (lane & 15);
+                acc[r] = (a < D && b < W) ? X[a * LD + b] : 0.0;
+            }
+            acc = mfma_tile_acc(acc, [&](int i, int k) { return -lds_or0(G, (r0 + i) * LD + c0 + k, r0 + i < D && k < kPanelN); },
+                                [&](int k, int j) { return lds_or0(X, (c0 + k) * LD + q0 + j, q0 + j < W && k < kPanelN); }, 0, kPanelN);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int a = r0 + (lane >> 4) + 4 * r, b = q0 + (lane & 15);
+                if (a < D && b < W) X[a * LD + b] = acc[r];
+            }
+        }
+        return;
+    }
     for (int e = threadIdx.x; e < rows * W; e += blockDim.x) {
         const int r = c0 + kPanelN + e / W, j = e - (e / W) * W;
         double acc = X[r * LD + j];
@@ -489,20 +589,24 @@ __device__ __forceinline__ void reduce_run_records(const NiwArgs &A, int s, cons
 #pragma unroll
     for (int k = 0; k < kRecE; ++k) v[k] = 0.0;
     if (nm <= cap) {
-        for (int m = 0; m < nm; m += 2) {
-            const int64_t r0 = (int64_t)list[m] * RS, r1 = (m + 1 < nm) ? (int64_t)list[m + 1] * RS : -1;
-            double a0[kRecE], a1[kRecE];
+        constexpr int kRecR = 4;  // records per round of loads (their sums still taken in record order)
+        for (int m = 0; m < nm; m += kRecR) {
+            int64_t rr[kRecR];
 #pragma unroll
-            for (int k = 0; k < kRecE; ++k) {
-                const int e = tid + k * nt;
-                a0[k] = (e < RS) ? A.part[r0 + e] : 0.0;
-                a1[k] = (e < RS && r1 >= 0) ? A.part[r1 + e] : 0.0;
-            }
+            for (int q = 0; q < kRecR; ++q) rr[q] = (m + q < nm) ? (int64_t)list[m + q] * RS : -1;
+            double a[kRecR][kRecE];
 #pragma unroll
-            for (int k = 0; k < kRecE; ++k) {
-                v[k] = v[k] + a0[k];
-                if (r1 >= 0) v[k] = v[k] + a1[k];
-            }
+            for (int q = 0; q < kRecR; ++q)
+#pragma unroll
+                for (int k = 0; k < kRecE; ++k) {
+                    const int e = tid + k * nt;
+                    a[q][k] = (e < RS && rr[q] >= 0) ? A.part[rr[q] + e] : 0.0;
+                }
+#pragma unroll
+            for (int k = 0; k < kRecE; ++k)
+#pragma unroll
+                for (int q = 0; q < kRecR; ++q)
+                    if (rr[q] >= 0) v[k] = v[k] + a[q][k];
         }
     } else {  // (more records than the scratch holds: every header in order)
         for (int64_t h = 0; h < A.n_rec; ++h)
@@ -589,15 +693,17 @@ __global__ __launch_bounds__(kNiwThreads) void np8_niw_post(NiwArgs A) {
     const double kn = k0 + nd, nun = A.nu0 + nd;
     const double kf = (k0 * nd) / kn;
 #ifdef NP8_EXP_NIW_TIMING
-    long long tph[12];
+    long long tph[40] = {0};
 #endif
     NIW_T(0)
     zero_block(L, 3 * D * LD);  // L, Li, B: upper triangles stay 0
+    NIW_T(10)
     const bool recs = A.part != nullptr && n > 0 && init_ok_records(A);
     if (recs) {  // the statistics from np8_suffstats_wide's run records: S into L's lower triangle, s1
         __syncthreads();
         reduce_run_records(A, s, acc, L, LD, s1, reinterpret_cast<int *>(Li), (int)(D * LD * 2));
         __syncthreads();
+        NIW_T(11)
     }
     for (int a = tid; a < D; a += blockDim.x) {
         anc[a] = (n > 0) ? A.slot_mu[(int64_t)s * D + a] : 0.0;
@@ -660,27 +766,33 @@ __global__ __launch_bounds__(kNiwThreads) void np8_niw_post(NiwArgs A) {
     // order, then the division by its pivot -- the operations of the oracle's left-looking loop, in its order, with
     // two barriers per panel.  U = J Lr J is upper with Psin = U U^T.  Wave 1 meanwhile: y = B^{-T} z / sqrt(kn).
     __shared__ int skip_s;
+    // (the solve for y is serial in its 64 rows: 16 of them beside each panel's factor keep it off the critical path)
+    double yv = 0.0;
+    if (wv == 1) {
+        const int ln = tid & 63;
+        yv = (ln < D) ? z[ln] * (1.0 / sqrt(kn)) : 0.0;
+    }
     for (int p = 0; p * kPanelN < D; ++p) {
         const int c0 = p * kPanelN;
         if (wv == 0) {
             lower_panel_factor(L, LD, D, c0, &skip_s);
-        } else if (wv == 1 && p == 0) {
+        } else if (wv == 1) {
             const int ln = tid & 63;
-            const double rskn = 1.0 / sqrt(kn);
-            double v = (ln < D) ? z[ln] * rskn : 0.0;
-            for (int k = D - 1; k >= 0; --k) {
-                const double yk = __shfl(v, k) / B[k * LD + k];
+            for (int k = D - 1 - c0; k >= 0 && k > D - 1 - c0 - kPanelN; --k) {
+                const double yk = lane_d(yv, k) / B[k * LD + k];
                 if (ln == k) y[k] = yk;
-                if (ln < k) v = fma(-B[k * LD + ln], yk, v);
+                if (ln < k) yv = fma(-B[k * LD + ln], yk, yv);
             }
         }
         __syncthreads();
+        NIW_T(14 + p)
         if (skip_s) {  // block-uniform: not numerically positive definite
             if (tid == 0) bad = 1;
             break;
         }
-        lower_panel_trailing(L, LD, D, c0);
+        lower_panel_trailing(L, LD, D, c0, A.valu);
         __syncthreads();
+        NIW_T(18 + p)
     }
     __syncthreads();
     NIW_T(2)
@@ -715,9 +827,11 @@ __global__ __launch_bounds__(kNiwThreads) void np8_niw_post(NiwArgs A) {
             }
         }
         __syncthreads();
-        forward_trailing(Li, L, LD, D, c0, true);
-        forward_trailing(T, B, LD, D, c0, false, true);
+        NIW_T(22 + p)
+        forward_trailing(Li, L, LD, D, c0, true, false, A.valu);
+        forward_trailing(T, B, LD, D, c0, false, true, A.valu);
         __syncthreads();
+        NIW_T(26 + p)
     }
     __syncthreads();
     NIW_T(3)
@@ -780,6 +894,7 @@ __global__ __launch_bounds__(kNiwThreads) void np8_niw_post(NiwArgs A) {
         // can be 40% above it.  Sigma is scaled by g = ||Sigma|| first (entries of (Sigma/g)^n stay in [0, 1], no
         // overflow, and ||(Sigma/g)^n|| >= D^(-n/2) >= 8^-32 at D = 64, k <= 5: no underflow); 1% for the fp32
         // factor, the fp32 contraction and the rounding.
+        NIW_T(30)
         const double g = max_abs_row_sum(D, LD, L, rs);
         const double rg = (g > 0.0) ? 1.0 / g : 0.0;
         for (int e = tid; e < D * D; e += blockDim.x) {
@@ -791,14 +906,27 @@ __global__ __launch_bounds__(kNiwThreads) void np8_niw_post(NiwArgs A) {
         // (unrolled: each buffer is a known LDS array, so the loads stay ds_read -- a runtime-indexed pointer table
         // made them flat loads, 2x slower)
         auto buf = [&](int k) -> double * { return k == 0 ? L : (k == 1 ? B : Li); };
-#pragma unroll
-        for (int q = 0; q < kBoundSquarings; ++q) {
+        // (written out: a loop the compiler failed to unroll left buf() runtime-indexed -- flat loads)
+        auto square = [&](const double *X, double *Y) {
             if (A.valu)
-                sym_square(D, LD, buf(q % 3), buf((q + 1) % 3));
+                sym_square(D, LD, X, Y);
             else
-                sym_square_mfma(D, LD, buf(q % 3), buf((q + 1) % 3));
+                sym_square_mfma(D, LD, X, Y);
             __syncthreads();
-        }
+        };
+        static_assert(kBoundSquarings >= 0 && kBoundSquarings <= 6, "squarings L -> B -> Li -> L ...");
+        NIW_T(32)
+        if (kBoundSquarings > 0) square(L, B);
+        NIW_T(33)
+        if (kBoundSquarings > 1) square(B, Li);
+        NIW_T(34)
+        if (kBoundSquarings > 2) square(Li, L);
+        NIW_T(35)
+        if (kBoundSquarings > 3) square(L, B);
+        NIW_T(36)
+        if (kBoundSquarings > 4) square(B, Li);
+        if (kBoundSquarings > 5) square(Li, L);
+        NIW_T(31)
         const double m = max_abs_row_sum(D, LD, buf(kBoundSquarings % 3), rs);
         if (tid == 0) {
             double root = m;
@@ -814,6 +942,11 @@ __global__ __launch_bounds__(kNiwThreads) void np8_niw_post(NiwArgs A) {
         printf("niw_post s=%d t=%u n=%ld phases %lld %lld %lld %lld %lld %lld %lld %lld\n", s, t, (long)n, tph[1] - tph[0],
                tph[2] - tph[1], tph[3] - tph[2], tph[4] - tph[3], tph[5] - tph[4], tph[6] - tph[5], tph[7] - tph[6],
                tph[8] - tph[7]);
+    if (tid == 0 && s < 1 && (t % 16) == 0) {
+        printf("niw_post detail t=%u:", t);
+        for (int k = 10; k < 37; ++k) printf(" %d:%lld", k, tph[k] ? tph[k] - tph[0] : -1ll);
+        printf("\n");
+    }
 #endif
     if (tid == 0) write_row_scalars(A, s, row, fma(0.5, sh[0], fma(-0.5 * (double)D, kLog2Pi, -sh[1])), iso);
     if (n > 0)
