@@ -355,19 +355,39 @@ __device__ __forceinline__ double write_pprime_r_mfma(int D, int LD, const doubl
     return __syncthreads_and(iso ? 1 : 0) ? p00 : 0.0;
 }
 
-// Y = X X (X symmetric) for the eigenvalue bound (a bound, not a bit-exact quantity): every tile.
+// Y = X X (X symmetric) for the eigenvalue bound (a bound, not a bit-exact quantity).  Y is symmetric: the tiles
+// ti <= tj are computed (nt (nt + 1) / 2 of nt^2) and each is stored twice; the k-steps past D are never loaded.  The f64
+// matrix core is the bound here (~64 cycles per 16x16x4 step on gfx950, the fp64 VALU rate), so fewer tiles is the lever.
 __device__ __forceinline__ void sym_square_mfma(int D, int LD, const double *X, double *Y) {
     const int nt = (D + 15) / 16, wv = threadIdx.x >> 6, nw = blockDim.x >> 6, lane = threadIdx.x & 63;
-    const int k1 = (D + 3) & ~3;
-    for (int tt = wv; tt < nt * nt; tt += nw) {
-        const int ti = tt / nt, tj = tt - ti * nt;
-        const f64x4 acc = mfma_tile([&](int i, int k) { return lds_or0(X, (16 * ti + i) * LD + k, k < D && 16 * ti + i < D); },
-                                    [&](int k, int j) { return lds_or0(X, k * LD + 16 * tj + j, k < D && 16 * tj + j < D); },
-                                    0, k1);
+    const int il = lane & 15, kl = lane >> 4, ks = (D + 3) / 4;
+    constexpr int KS = kNiwMaxD / 4;
+    for (int tt = wv; tt < nt * (nt + 1) / 2; tt += nw) {
+        int ti = 0, rem = tt;  // (ti, tj), ti <= tj, row-major over the upper tile triangle
+        while (rem >= nt - ti) {
+            rem -= nt - ti;
+            ++ti;
+        }
+        const int tj = ti + rem;
+        double av[KS], bv[KS];
+#pragma unroll
+        for (int q = 0; q < KS; ++q)
+            if (q < ks) {  // (wave-uniform)
+                const int k = 4 * q + kl;
+                av[q] = lds_or0(X, (16 * ti + il) * LD + k, 16 * ti + il < D && k < D);
+                bv[q] = lds_or0(X, k * LD + 16 * tj + il, k < D && 16 * tj + il < D);
+            }
+        f64x4 c = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int q = 0; q < KS; ++q)
+            if (q < ks) c = __builtin_amdgcn_mfma_f64_16x16x4f64(av[q], bv[q], c, 0, 0, 0);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int a = 16 * ti + (lane >> 4) + 4 * r, b = 16 * tj + (lane & 15);
-            if (a < D && b < D) Y[a * LD + b] = acc[r];
+            if (a < D && b < D) {
+                Y[a * LD + b] = c[r];
+                Y[b * LD + a] = c[r];
+            }
         }
     }
 }
@@ -557,8 +577,24 @@ __device__ __forceinline__ void reduce_run_records(const NiwArgs &A, int s, cons
     const int tid = threadIdx.x, nt = blockDim.x, lane = tid & 63, wv = tid >> 6, nw = nt >> 6;
     __shared__ int woff[17];
     const int64_t per = (A.n_rec + nt - 1) / nt, h0 = (int64_t)tid * per, h1 = min(A.n_rec, h0 + per);
+    // the thread's headers in batches of 8 independent loads, the matches as a bit mask (up to 64 headers per thread:
+    // one scan of dependent loads per header cost ~25 us at C5)
+    const bool fast = per <= 64;
+    uint64_t mb = 0ull;
     int c = 0;
-    for (int64_t h = h0; h < h1; ++h) c += (A.part_slot[h] == s);
+    if (fast) {
+        for (int64_t hb = h0; hb < h1; hb += 8) {
+            int32_t hv[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) hv[i] = (hb + i < h1) ? A.part_slot[hb + i] : -1;
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+                if (hv[i] == s) mb |= 1ull << (hb + i - h0);
+        }
+        c = __popcll(mb);
+    } else {
+        for (int64_t h = h0; h < h1; ++h) c += (A.part_slot[h] == s);
+    }
     int inc = c;  // block exclusive scan of the counts (thread order = record order)
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -579,9 +615,14 @@ __device__ __forceinline__ void reduce_run_records(const NiwArgs &A, int s, cons
     __syncthreads();
     int o = woff[wv] + inc - c;
     const int nm = woff[16];
-    if (nm <= cap)
-        for (int64_t h = h0; h < h1; ++h)
-            if (A.part_slot[h] == s) list[o++] = (int)h;
+    if (nm <= cap) {
+        if (fast) {
+            for (uint64_t m = mb; m; m &= m - 1ull) list[o++] = (int)(h0 + __ffsll((unsigned long long)m) - 1);
+        } else {
+            for (int64_t h = h0; h < h1; ++h)
+                if (A.part_slot[h] == s) list[o++] = (int)h;
+        }
+    }
     __syncthreads();
     // this thread's elements e = tid + k nt (RS <= kRecE nt for D <= 64), two records per round of loads
     constexpr int kRecE = 12;
