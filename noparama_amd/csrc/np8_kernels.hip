@@ -1964,7 +1964,7 @@ __device__ void prune_block(const PruneArgs &A, unsigned char *smem, size_t lds_
     constexpr int RW = D + 7;  // mu[D] | c + log n | c + log(n - 1) | iso | R^2 | slot | log n | log(n - 1)
     __syncthreads();
     const int K = A.ctl->K;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, nwb = kFinThreads / 64;
+    const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6), nwb = kFinThreads / 64;
     if (tid == 0) A.ctl->lists_ok = 1;
     const double *src = A.r2 + (A.gathered ? A.kcap : 0);
     auto R2of = [&](int slot) { return src[slot]; };
@@ -2164,7 +2164,8 @@ __global__ __launch_bounds__(kFinThreads) void np8_fin_prune(FinArgs F, PruneArg
         const double *src = P.r2 + (P.gathered ? P.kcap : 0);
         auto R2of = [&](int slot) { return src[slot]; };
         constexpr int kWaves = kFinThreads / 64;
-        for (int k0 = ((int)blockIdx.x - 1) * kWaves + ((int)threadIdx.x >> 6); k0 < K; k0 += nP * kWaves)  // wave-uniform
+        for (int k0 = ((int)blockIdx.x - 1) * kWaves + __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6); k0 < K;
+             k0 += nP * kWaves)  // wave-uniform (readfirstlane: SGPR loop)
             prune_row<DT>(P.cand, R2of, P.plist, P.pdist, P.plen, P.plr2, P.plen_s, P.plr2_s, P.ls, P.D, K, k0, P.lb, P.kcap);
     }
     __syncthreads();
@@ -2967,7 +2968,7 @@ __global__ __launch_bounds__(256) void np8_prune(PruneArgs A) {
     if (A.clear_next && blockIdx.x == 0)  // only the radii in use are read here (not gathered)
         for (int s = threadIdx.x; s < A.kcap; s += blockDim.x) A.r2[A.kcap + s] = 0.0;
     auto R2of = [&](int slot) { return src[slot]; };
-    for (int k0 = blockIdx.x * 4 + (threadIdx.x >> 6); k0 < K; k0 += gridDim.x * 4)  // wave-uniform
+    for (int k0 = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6); k0 < K; k0 += gridDim.x * 4)  // wave-uniform
         prune_row<DT>(A.cand, R2of, A.plist, A.pdist, A.plen, A.plr2, A.plen_s, A.plr2_s, A.ls, A.D, K, k0, A.lb, A.kcap);
 }
 

@@ -237,29 +237,81 @@ typedef double f64x4 __attribute__((ext_vector_type(4)));
 
 // One 16 x 16 tile (one wave): acc(i, j) = acc0(i, j) + sum_k a_at(i, k) b_at(k, j) over k = k0 .. k1 - 1 (k1 - k0 a
 // multiple of 4; accessors return 0 outside the matrices); element r of lane l is (row (l >> 4) + 4 r, column l & 15).
-// Every operand of the tile is read from LDS first (at most kNiwMaxD / 4 k-steps, unrolled), then the MFMAs run back to
-// back: one LDS round trip per tile instead of one per k-step (the chain of dependent MFMAs waited on each load).
-constexpr int kNiwMaxD = 80;
+// (chunked below: one LDS round trip per 16 k instead of one per k-step)
 // M[o] when ok, else 0 -- the load made at offset 0 instead, so that it is unconditional (a guarded LDS load became a
 // branch around every operand of the tiles)
 __device__ __forceinline__ double lds_or0(const double *M, int o, bool ok) {
     const double v = M[ok ? o : 0];
     return ok ? v : 0.0;
 }
-template <class FA, class FB>
-__device__ __forceinline__ f64x4 mfma_tile_acc(f64x4 acc, FA a_at, FB b_at, int k0, int k1) {
+// EX: D a multiple of 16, every index the tiles form is inside the matrix -- a plain load, nothing to mask (the select
+// after a masked load pins its wait next to it)
+template <bool EX>
+__device__ __forceinline__ double lds_at(const double *M, int o, bool ok) {
+    if constexpr (EX) {
+        (void)ok;
+        return M[o];
+    } else {
+        return lds_or0(M, o, ok);
+    }
+}
+// NC chunks of 16 k with every operand read before the first MFMA (one LDS wait per tile)
+template <int NC, class FA, class FB>
+__device__ __forceinline__ f64x4 mfma_run(f64x4 acc, FA a_at, FB b_at, int k0) {
     const int lane = threadIdx.x & 63, il = lane & 15, kl = lane >> 4;
-    constexpr int KS = kNiwMaxD / 4;
-    double av[KS], bv[KS];
+    double a[4 * NC], b[4 * NC];
 #pragma unroll
-    for (int q = 0; q < KS; ++q) {  // (accessors are safe for any k: lds_or0)
-        const int k = k0 + 4 * q;
-        av[q] = a_at(il, k + kl);
-        bv[q] = b_at(k + kl, il);
+    for (int q = 0; q < 4 * NC; ++q) {
+        a[q] = a_at(il, k0 + 4 * q + kl);
+        b[q] = b_at(k0 + 4 * q + kl, il);
     }
 #pragma unroll
-    for (int q = 0; q < KS; ++q)
-        if (k0 + 4 * q < k1) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[q], bv[q], acc, 0, 0, 0);  // (wave-uniform)
+    for (int q = 0; q < 4 * NC; ++q) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[q], b[q], acc, 0, 0, 0);
+    return acc;
+}
+
+template <class FA, class FB>
+__device__ __forceinline__ f64x4 mfma_tile_acc(f64x4 acc, FA a_at, FB b_at, int k0, int k1) {
+    switch ((k1 - k0 + 15) >> 4) {  // (wave-uniform) up to D = 80: the whole range's operands first
+        case 1: return mfma_run<1>(acc, a_at, b_at, k0);
+        case 2: return mfma_run<2>(acc, a_at, b_at, k0);
+        case 3: return mfma_run<3>(acc, a_at, b_at, k0);
+        case 4: return mfma_run<4>(acc, a_at, b_at, k0);
+        case 5: return mfma_run<5>(acc, a_at, b_at, k0);
+        default: break;
+    }
+    // chunks of 16 k (4 steps): the next chunk's operands are read while this chunk's MFMAs run (one wait per chunk,
+    // not per step: per-step waits made a 64 x 64 product ~15k cycles, the loads-first form ~6k).  A chunk that runs
+    // past k1 takes terms the accessors return as exact zeros (triangular operands, or masked past D), which leave the
+    // chain's bits alone.
+    const int lane = threadIdx.x & 63, il = lane & 15, kl = lane >> 4;
+    const int nch = (k1 - k0 + 15) >> 4;  // (wave-uniform)
+    double a[4], b[4];
+    if (nch > 0) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            a[q] = a_at(il, k0 + 4 * q + kl);
+            b[q] = b_at(k0 + 4 * q + kl, il);
+        }
+    }
+    for (int c = 0; c < nch; ++c) {
+        double an[4], bn[4];
+        if (c + 1 < nch) {
+            const int kb = k0 + 16 * (c + 1);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                an[q] = a_at(il, kb + 4 * q + kl);
+                bn[q] = b_at(kb + 4 * q + kl, il);
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[q], b[q], acc, 0, 0, 0);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            a[q] = an[q];
+            b[q] = bn[q];
+        }
+    }
     return acc;
 }
 template <class FA, class FB>
@@ -269,8 +321,9 @@ __device__ __forceinline__ f64x4 mfma_tile(FA a_at, FB b_at, int k0, int k1) {
 
 // Sigma = T^T T (T lower): tiles ti <= tj, element (a, b) = sum over k from 16 tj (below max(a, b) a factor is zero) of
 // T_ka T_kb, mirrored -- sigma_from_t's chains (its element (b, a) is the same chain with each fma's factors swapped).
+template <bool EX>
 __device__ __forceinline__ void sigma_from_t_mfma(int D, int LD, const double *T, double *Sigma, double *Sl) {
-    const int nt = (D + 15) / 16, wv = threadIdx.x >> 6, nw = blockDim.x >> 6, lane = threadIdx.x & 63;
+    const int nt = (D + 15) / 16, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), nw = __builtin_amdgcn_readfirstlane(blockDim.x >> 6), lane = threadIdx.x & 63;
     const int k1 = (D + 3) & ~3;
     for (int tt = wv; tt < nt * (nt + 1) / 2; tt += nw) {
         int ti = 0, rem = tt;
@@ -279,8 +332,8 @@ __device__ __forceinline__ void sigma_from_t_mfma(int D, int LD, const double *T
             ++ti;
         }
         const int tj = ti + rem;
-        const f64x4 acc = mfma_tile([&](int i, int k) { return lds_or0(T, k * LD + 16 * ti + i, k < D && 16 * ti + i < D); },
-                                    [&](int k, int j) { return lds_or0(T, k * LD + 16 * tj + j, k < D && 16 * tj + j < D); },
+        const f64x4 acc = mfma_tile([&](int i, int k) { return lds_at<EX>(T, k * LD + 16 * ti + i, k < D && 16 * ti + i < D); },
+                                    [&](int k, int j) { return lds_at<EX>(T, k * LD + 16 * tj + j, k < D && 16 * tj + j < D); },
                                     16 * tj, k1);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -298,8 +351,9 @@ __device__ __forceinline__ void sigma_from_t_mfma(int D, int LD, const double *T
 }
 
 // R = B^T U^{-1} (upper): R_ab = sum_{k = a..b} B_ka M[D-1-k][D-1-b] (M = Lr^{-1} lower, B lower), 0 below the diagonal.
+template <bool EX>
 __device__ __forceinline__ void r_from_b_mfma(int D, int LD, const double *B, const double *M, double *R) {
-    const int nt = (D + 15) / 16, wv = threadIdx.x >> 6, nw = blockDim.x >> 6, lane = threadIdx.x & 63;
+    const int nt = (D + 15) / 16, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), nw = __builtin_amdgcn_readfirstlane(blockDim.x >> 6), lane = threadIdx.x & 63;
     for (int e = threadIdx.x; e < D * D; e += blockDim.x) {  // the lower triangle (tiles below the diagonal included)
         const int a = e / D, b = e - a * D;
         if (b < a) R[a * LD + b] = 0.0;
@@ -313,8 +367,8 @@ __device__ __forceinline__ void r_from_b_mfma(int D, int LD, const double *B, co
         const int tj = ti + rem;
         const int k1 = min((D + 3) & ~3, 16 * tj + 16);
         const f64x4 acc = mfma_tile(
-            [&](int i, int k) { return lds_or0(B, k * LD + 16 * ti + i, k < D && 16 * ti + i < D); },
-            [&](int k, int j) { return lds_or0(M, (D - 1 - k) * LD + (D - 1 - (16 * tj + j)), k < D && 16 * tj + j < D); },
+            [&](int i, int k) { return lds_at<EX>(B, k * LD + 16 * ti + i, k < D && 16 * ti + i < D); },
+            [&](int k, int j) { return lds_at<EX>(M, (D - 1 - k) * LD + (D - 1 - (16 * tj + j)), k < D && 16 * tj + j < D); },
             16 * ti, k1);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -326,8 +380,9 @@ __device__ __forceinline__ void r_from_b_mfma(int D, int LD, const double *B, co
 
 // P' = packed sym(R^T R) (R upper): element (a, b), a <= b, = sum_{k = 0..a} R_ka R_kb, off-diagonals doubled, into the
 // slot table and its candidate row; returns the isotropy value (write_pprime_r's).
+template <bool EX>
 __device__ __forceinline__ double write_pprime_r_mfma(int D, int LD, const double *R, double *slotP, double *candP) {
-    const int nt = (D + 15) / 16, wv = threadIdx.x >> 6, nw = blockDim.x >> 6, lane = threadIdx.x & 63;
+    const int nt = (D + 15) / 16, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), nw = __builtin_amdgcn_readfirstlane(blockDim.x >> 6), lane = threadIdx.x & 63;
     const double p00 = fma(R[0], R[0], 0.0);
     bool iso = true;
     for (int tt = wv; tt < nt * (nt + 1) / 2; tt += nw) {
@@ -338,8 +393,8 @@ __device__ __forceinline__ double write_pprime_r_mfma(int D, int LD, const doubl
         }
         const int tj = ti + rem;
         const int k1 = min((D + 3) & ~3, 16 * ti + 16);
-        const f64x4 acc = mfma_tile([&](int i, int k) { return lds_or0(R, k * LD + 16 * ti + i, k < D && 16 * ti + i < D); },
-                                    [&](int k, int j) { return lds_or0(R, k * LD + 16 * tj + j, k < D && 16 * tj + j < D); },
+        const f64x4 acc = mfma_tile([&](int i, int k) { return lds_at<EX>(R, k * LD + 16 * ti + i, k < D && 16 * ti + i < D); },
+                                    [&](int k, int j) { return lds_at<EX>(R, k * LD + 16 * tj + j, k < D && 16 * tj + j < D); },
                                     0, k1);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -358,10 +413,10 @@ __device__ __forceinline__ double write_pprime_r_mfma(int D, int LD, const doubl
 // Y = X X (X symmetric) for the eigenvalue bound (a bound, not a bit-exact quantity).  Y is symmetric: the tiles
 // ti <= tj are computed (nt (nt + 1) / 2 of nt^2) and each is stored twice; the k-steps past D are never loaded.  The f64
 // matrix core is the bound here (~64 cycles per 16x16x4 step on gfx950, the fp64 VALU rate), so fewer tiles is the lever.
+template <bool EX>
 __device__ __forceinline__ void sym_square_mfma(int D, int LD, const double *X, double *Y) {
-    const int nt = (D + 15) / 16, wv = threadIdx.x >> 6, nw = blockDim.x >> 6, lane = threadIdx.x & 63;
-    const int il = lane & 15, kl = lane >> 4, ks = (D + 3) / 4;
-    constexpr int KS = kNiwMaxD / 4;
+    const int nt = (D + 15) / 16, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int nw = __builtin_amdgcn_readfirstlane(blockDim.x >> 6);
     for (int tt = wv; tt < nt * (nt + 1) / 2; tt += nw) {
         int ti = 0, rem = tt;  // (ti, tj), ti <= tj, row-major over the upper tile triangle
         while (rem >= nt - ti) {
@@ -369,18 +424,11 @@ __device__ __forceinline__ void sym_square_mfma(int D, int LD, const double *X, 
             ++ti;
         }
         const int tj = ti + rem;
-        double av[KS], bv[KS];
-#pragma unroll
-        for (int q = 0; q < KS; ++q)
-            if (q < ks) {  // (wave-uniform)
-                const int k = 4 * q + kl;
-                av[q] = lds_or0(X, (16 * ti + il) * LD + k, 16 * ti + il < D && k < D);
-                bv[q] = lds_or0(X, k * LD + 16 * tj + il, k < D && 16 * tj + il < D);
-            }
-        f64x4 c = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-        for (int q = 0; q < KS; ++q)
-            if (q < ks) c = __builtin_amdgcn_mfma_f64_16x16x4f64(av[q], bv[q], c, 0, 0, 0);
+        // A(i, k) = X[16 ti + i][k] read as X[k][16 ti + i] (X symmetric): consecutive lanes, consecutive words -- the
+        // row-wise read put four lanes on each bank pair
+        const f64x4 c = mfma_tile([&](int i, int k) { return lds_at<EX>(X, k * LD + 16 * ti + i, k < D && 16 * ti + i < D); },
+                                  [&](int k, int j) { return lds_at<EX>(X, k * LD + 16 * tj + j, k < D && 16 * tj + j < D); },
+                                  0, D);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int a = 16 * ti + (lane >> 4) + 4 * r, b = 16 * tj + (lane & 15);
@@ -445,12 +493,13 @@ __device__ __forceinline__ void lower_panel_factor(double *L, int LD, int D, int
 // matrix cores: tile (ti, tj), tj <= ti, of the trailing lower triangle starts from L's elements and takes the 16 terms
 // fma(-L_rj, L_cj, .), j = c0 .. c0 + 15 ascending, as four k-ordered MFMA steps -- the VALU chain, bit for bit (the
 // negated factor is exact).  valu: the per-element VALU loop.
+template <bool EX>
 __device__ __forceinline__ void lower_panel_trailing(double *L, int LD, int D, int c0, bool valu) {
     const int rows = D - (c0 + kPanelN);
     if (rows <= 0) return;  // (the last panel: nothing below it)
     if (!valu) {
         const int t0 = (c0 + kPanelN) / 16, nt = (D + 15) / 16, m = nt - t0;  // trailing tiles per side
-        const int wv = threadIdx.x >> 6, nw = blockDim.x >> 6, lane = threadIdx.x & 63;
+        const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), nw = __builtin_amdgcn_readfirstlane(blockDim.x >> 6), lane = threadIdx.x & 63;
         for (int tt = wv; tt < m * (m + 1) / 2; tt += nw) {
             int ti = 0, rem = tt;  // (ti, tj), tj <= ti, row-major over the lower tile triangle
             while (rem > ti) {
@@ -464,8 +513,8 @@ __device__ __forceinline__ void lower_panel_trailing(double *L, int LD, int D, i
                 const int a = r0 + (lane >> 4) + 4 * r, b = q0 + (lane & 15);
                 acc[r] = (a < D && b < D && b <= a) ? L[a * LD + b] : 0.0;
             }
-            acc = mfma_tile_acc(acc, [&](int i, int k) { return -lds_or0(L, (r0 + i) * LD + c0 + k, r0 + i < D && k < kPanelN); },
-                                [&](int k, int j) { return lds_or0(L, (q0 + j) * LD + c0 + k, q0 + j < D && k < kPanelN); }, 0, kPanelN);
+            acc = mfma_tile_acc(acc, [&](int i, int k) { return -lds_at<EX>(L, (r0 + i) * LD + c0 + k, r0 + i < D && k < kPanelN); },
+                                [&](int k, int j) { return lds_at<EX>(L, (q0 + j) * LD + c0 + k, q0 + j < D && k < kPanelN); }, 0, kPanelN);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int a = r0 + (lane >> 4) + 4 * r, b = q0 + (lane & 15);
@@ -523,6 +572,7 @@ __device__ __forceinline__ void forward_panel(double *X, const double *G, int LD
 // On the matrix cores (!valu): tile (rows r0.., columns q0..) from X's elements plus the 16 terms as four k-ordered MFMA
 // steps; the terms the VALU loop skips (inv: k < j; lower: X_kj = 0 for j > k) have X_kj = +0 and leave the chain alone
 // (fma(-g, +0, v) = v for v != -0, and the chains never hold -0: they start from +0 or nonzero values).
+template <bool EX>
 __device__ __forceinline__ void forward_trailing(double *X, const double *G, int LD, int D, int c0, bool inv,
                                                  bool lower, bool valu) {
     const int rows = D - (c0 + kPanelN);
@@ -532,7 +582,7 @@ __device__ __forceinline__ void forward_trailing(double *X, const double *G, int
     if (!valu) {
         if (rows <= 0) return;
         const int t0 = (c0 + kPanelN) / 16, nt = (D + 15) / 16, mr = nt - t0, mc = (W + 15) / 16;
-        const int wv = threadIdx.x >> 6, nw = blockDim.x >> 6, lane = threadIdx.x & 63;
+        const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), nw = __builtin_amdgcn_readfirstlane(blockDim.x >> 6), lane = threadIdx.x & 63;
         for (int tt = wv; tt < mr * mc; tt += nw) {
             const int r0 = 16 * (t0 + tt / mc), q0 = 16 * (tt % mc);
             f64x4 acc;
@@ -541,8 +591,8 @@ __device__ __forceinline__ void forward_trailing(double *X, const double *G, int
                 const int a = r0 + (lane >> 4) + 4 * r, b = q0 + (lane & 15);
                 acc[r] = (a < D && b < W) ? X[a * LD + b] : 0.0;
             }
-            acc = mfma_tile_acc(acc, [&](int i, int k) { return -lds_or0(G, (r0 + i) * LD + c0 + k, r0 + i < D && k < kPanelN); },
-                                [&](int k, int j) { return lds_or0(X, (c0 + k) * LD + q0 + j, q0 + j < W && k < kPanelN); }, 0, kPanelN);
+            acc = mfma_tile_acc(acc, [&](int i, int k) { return -lds_at<EX>(G, (r0 + i) * LD + c0 + k, r0 + i < D && k < kPanelN); },
+                                [&](int k, int j) { return lds_at<EX>(X, (c0 + k) * LD + q0 + j, q0 + j < W && k < kPanelN); }, 0, kPanelN);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int a = r0 + (lane >> 4) + 4 * r, b = q0 + (lane & 15);
@@ -574,7 +624,7 @@ __device__ __forceinline__ void reduce_run_records(const NiwArgs &A, int s, cons
                                    int cap) {
     // (the records' layout is np8_suffstats_wide's at DT: rows and columns >= D are the zero rows of the items)
     const int D = A.D, T = A.DT / 16, NT = T * (T + 1) / 2, RS = NT * 4 * 64 + T * 16;
-    const int tid = threadIdx.x, nt = blockDim.x, lane = tid & 63, wv = tid >> 6, nw = nt >> 6;
+    const int tid = threadIdx.x, nt = blockDim.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6), nw = nt >> 6;
     __shared__ int woff[17];
     const int64_t per = (A.n_rec + nt - 1) / nt, h0 = (int64_t)tid * per, h1 = min(A.n_rec, h0 + per);
     // the thread's headers in batches of 8 independent loads, the matches as a bit mask (up to 64 headers per thread:
@@ -701,6 +751,7 @@ size_t np8_niw_lds_bytes(int D) { return sizeof(double) * (4 * (size_t)D * (D + 
 // otherwise slot b's posterior on stream PARAM at the current epoch (oracle niw_draw_impl).
 __global__ __launch_bounds__(kNiwThreads) void np8_niw_post(NiwArgs A) {
     const int D = A.D, W = D + D * (D + 1) / 2, LD = D + 1;
+    const bool ex16 = D % 16 == 0;  // the MFMA tiles' instances without masking (lds_at)
     int s;
     int64_t n;
     uint64_t i;
@@ -801,7 +852,7 @@ __global__ __launch_bounds__(kNiwThreads) void np8_niw_post(NiwArgs A) {
     }
     __syncthreads();
     NIW_T(1)
-    const int wv = tid >> 6;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);  // (wave-uniform: SGPR loops and branches)
     // Lr = chol(J Psin J), blocked right-looking (panels of 16 columns: the panel factored by wave 0 in registers,
     // the rows below updated by every thread): element (r, c) receives fma(-L_rk, L_ck, .) for k = 0, 1, ... in
     // order, then the division by its pivot -- the operations of the oracle's left-looking loop, in its order, with
@@ -831,7 +882,10 @@ __global__ __launch_bounds__(kNiwThreads) void np8_niw_post(NiwArgs A) {
             if (tid == 0) bad = 1;
             break;
         }
-        lower_panel_trailing(L, LD, D, c0, A.valu);
+        if (ex16)
+            lower_panel_trailing<true>(L, LD, D, c0, A.valu);
+        else
+            lower_panel_trailing<false>(L, LD, D, c0, A.valu);
         __syncthreads();
         NIW_T(18 + p)
     }
@@ -869,8 +923,13 @@ __global__ __launch_bounds__(kNiwThreads) void np8_niw_post(NiwArgs A) {
         }
         __syncthreads();
         NIW_T(22 + p)
-        forward_trailing(Li, L, LD, D, c0, true, false, A.valu);
-        forward_trailing(T, B, LD, D, c0, false, true, A.valu);
+        if (ex16) {
+            forward_trailing<true>(Li, L, LD, D, c0, true, false, A.valu);
+            forward_trailing<true>(T, B, LD, D, c0, false, true, A.valu);
+        } else {
+            forward_trailing<false>(Li, L, LD, D, c0, true, false, A.valu);
+            forward_trailing<false>(T, B, LD, D, c0, false, true, A.valu);
+        }
         __syncthreads();
         NIW_T(26 + p)
     }
@@ -899,7 +958,10 @@ __global__ __launch_bounds__(kNiwThreads) void np8_niw_post(NiwArgs A) {
     if (A.valu) {
         sigma_from_t(D, LD, F, A.slot_sigma + (int64_t)s * D * D, bound ? L : nullptr);  // Sigma = T^T T
     } else {
-        sigma_from_t_mfma(D, LD, F, A.slot_sigma + (int64_t)s * D * D, bound ? L : nullptr);
+        if (ex16)
+            sigma_from_t_mfma<true>(D, LD, F, A.slot_sigma + (int64_t)s * D * D, bound ? L : nullptr);
+        else
+            sigma_from_t_mfma<false>(D, LD, F, A.slot_sigma + (int64_t)s * D * D, bound ? L : nullptr);
     }
     __syncthreads();
     NIW_T(4)
@@ -915,13 +977,18 @@ __global__ __launch_bounds__(kNiwThreads) void np8_niw_post(NiwArgs A) {
             F[a * LD + b] = v;
         }
     } else {
-        r_from_b_mfma(D, LD, B, Li, F);
+        if (ex16)
+            r_from_b_mfma<true>(D, LD, B, Li, F);
+        else
+            r_from_b_mfma<false>(D, LD, B, Li, F);
     }
     __syncthreads();
     NIW_T(5)
     const double iso = A.valu ? write_pprime_r(D, LD, F, A.slot_P + (int64_t)s * (D * (D + 1) / 2),
                                                row >= 0 ? A.cand + (int64_t)row * cand_stride(D) + D : nullptr)
-                              : write_pprime_r_mfma(D, LD, F, A.slot_P + (int64_t)s * (D * (D + 1) / 2),
+                       : ex16 ? write_pprime_r_mfma<true>(D, LD, F, A.slot_P + (int64_t)s * (D * (D + 1) / 2),
+                                                          row >= 0 ? A.cand + (int64_t)row * cand_stride(D) + D : nullptr)
+                              : write_pprime_r_mfma<false>(D, LD, F, A.slot_P + (int64_t)s * (D * (D + 1) / 2),
                                                     row >= 0 ? A.cand + (int64_t)row * cand_stride(D) + D : nullptr);
     NIW_T(6)
     if (A.wA) {  // the wide path: the contraction rows from R itself, the eigenvalue bound from Sigma's row sums
@@ -951,8 +1018,10 @@ __global__ __launch_bounds__(kNiwThreads) void np8_niw_post(NiwArgs A) {
         auto square = [&](const double *X, double *Y) {
             if (A.valu)
                 sym_square(D, LD, X, Y);
+            else if (ex16)
+                sym_square_mfma<true>(D, LD, X, Y);
             else
-                sym_square_mfma(D, LD, X, Y);
+                sym_square_mfma<false>(D, LD, X, Y);
             __syncthreads();
         };
         static_assert(kBoundSquarings >= 0 && kBoundSquarings <= 6, "squarings L -> B -> Li -> L ...");

@@ -306,7 +306,7 @@ __global__ __launch_bounds__(256) void np8_wide_rows(WideArgs W) {
     WR_T(0)
     const int s = blockIdx.x;
     if (!W.dirty[s] || W.cnt[s] <= 0) return;  // block-uniform
-    const int D = W.D, LD = D + 1, tid = threadIdx.x, wv = tid >> 6;
+    const int D = W.D, LD = D + 1, tid = threadIdx.x, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int nq = wide_rows_tests(D);  // concurrent Cholesky tests: three, two above D = 64 (LDS)
     extern __shared__ __attribute__((aligned(16))) double smr[];
     double *Wk = smr, *C0 = Wk + D * LD;  // C0 + q * D * LD: test matrix q; R = the upper triangle of Wk at the end
@@ -1041,7 +1041,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     constexpr int NCH = 2 * kSuffChunks;
     typedef double f64x4 __attribute__((ext_vector_type(4)));
     __shared__ float tile[4][H * PS];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, g = lane >> 4, col = lane & 15;
+    const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), g = lane >> 4, col = lane & 15;
     const bool sorted = P.sorted != 0;
     constexpr int cur = 0;  // the label-sorted layout is always buffer 0 (buffer 1: the re-sort's scratch)
     const float *__restrict__ X = reinterpret_cast<const float *>(sorted ? (cur ? P.Xs[1] : P.Xs[0]) : P.X);
