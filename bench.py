@@ -35,6 +35,7 @@ HBM_PEAK_GBS = 8000.0
 # committed rocprofv3 PMC summaries of the assign kernels (HBM bytes per launch, tools/prof*.sh)
 C3_TRAFFIC = "traffic_r04c.json"
 C5_TRAFFIC = "traffic_r04c_c5.json"
+C5_CONJ_TRAFFIC = None  # PMC pass of the niw_conjugate C5 sweep (its assign reads more candidate rows than the frozen one)
 MIXED_TRAFFIC = "traffic_r05_mixed_head.json"  # PMC pass of the mixed regime (tools/prof_mixed.sh, tools/summarize_profile.py)
 
 
@@ -90,7 +91,8 @@ def parse():
     a.d = a.d if a.d is not None else (64 if c5 else 8)
     a.k = a.k if a.k is not None else (256 if c5 else 64)
     if a.traffic_json is None:
-        a.traffic_json = os.path.join(ROOT, "profiles", C5_TRAFFIC if c5 else C3_TRAFFIC)
+        name = (C5_CONJ_TRAFFIC if a.param_update == "niw_conjugate" else C5_TRAFFIC) if c5 else C3_TRAFFIC
+        a.traffic_json = os.path.join(ROOT, "profiles", name) if name else None
     return a
 
 
@@ -454,6 +456,12 @@ def chain_quality(smp, labels):
     return res
 
 
+def c5_traffic(pu):
+    """The PMC traffic file of the C5 sweep with cluster-parameter update pu (None: not profiled)."""
+    name = C5_TRAFFIC if pu == "frozen" else C5_CONJ_TRAFFIC
+    return os.path.join(ROOT, "profiles", name) if name else None
+
+
 def c5_record(args, device, torch):
     """Config C5 (N = 1e6, D = 64, K = 256, NIW prior, fp32 MFMA contraction) timed inside the default run
     (VERDICT r2 #7): frozen and niw_conjugate sweeps/s with the roofline of np8_assign_wide."""
@@ -470,7 +478,7 @@ def c5_record(args, device, torch):
         smp.set_data(X)
         smp.set_state(z, mu, sig)
         m = measure(smp, lambda n, sync=True: smp.sweep(n, sync=sync), steps, 5, True, None, torch, X.shape[0],
-                    64, True, 1, os.path.join(ROOT, "profiles", C5_TRAFFIC) if pu == "frozen" else None)
+                    64, True, 1, c5_traffic(pu))
         out[pu] = {"value": steps / m["dt"], "unit": "sweeps/s", "steps": steps, "ms_per_step": m["dt"] / steps * 1e3,
                    "K_final": m["K_final"], "params_ms_per_timed_sweep": m["params_ms"], "roofline": m["roofline"]}
         smp.close()

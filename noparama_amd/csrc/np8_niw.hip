@@ -460,29 +460,36 @@ __device__ __forceinline__ double lane_d(double v, int l) {
     return __longlong_as_double(((int64_t)hi << 32) | (uint32_t)lo);
 }
 
+// Column J of the panel and then the later ones, by template recursion: the indices into w[] are constants (a `#pragma
+// unroll` the compiler declined left w[j] runtime-indexed -- v_cndmask selection trees, ~700 cycles per column)
+template <int J>
+__device__ __forceinline__ void panel_cols(double (&w)[kPanelN], int lane, int c0, int D, int &sk) {
+    if constexpr (J < kPanelN) {
+        const int jj = c0 + J;
+        if (jj < D) {  // (wave-uniform: a last panel narrower than 16 when D is not a multiple of 16)
+            const double v = lane_d(w[J], jj);  // the pivot L[jj][jj]
+            const bool ok = v > 0.0;
+            if (!ok) sk = 1;
+            const double dj = ok ? sqrt(v) : 1e-300;
+            const double q = w[J] / dj;
+            w[J] = (lane == jj) ? dj : ((lane > jj) ? q : w[J]);  // column jj of L
+#pragma unroll
+            for (int i = J + 1; i < kPanelN; ++i) {
+                const double lcj = lane_d(w[J], min(c0 + i, 63));  // L[c][jj], c = c0 + i
+                if (lane >= c0 + i && c0 + i < D) w[i] = fma(-w[J], lcj, w[i]);
+            }
+        }
+        panel_cols<J + 1>(w, lane, c0, D, sk);
+    }
+}
+
 __device__ __forceinline__ void lower_panel_factor(double *L, int LD, int D, int c0, int *skip) {
     const int lane = threadIdx.x & 63;
     double w[kPanelN];
 #pragma unroll
     for (int i = 0; i < kPanelN; ++i) w[i] = lds_or0(L, lane * LD + c0 + i, lane < D && c0 + i < D);
     int sk = 0;
-#pragma unroll
-    for (int j = 0; j < kPanelN; ++j) {
-        const int jj = c0 + j;
-        if (jj < D) {  // (wave-uniform: a last panel narrower than 16 when D is not a multiple of 16)
-            const double v = lane_d(w[j], jj);  // the pivot L[jj][jj]
-            const bool ok = v > 0.0;
-            if (!ok) sk = 1;
-            const double dj = ok ? sqrt(v) : 1e-300;
-            const double q = w[j] / dj;
-            w[j] = (lane == jj) ? dj : ((lane > jj) ? q : w[j]);  // column jj of L
-#pragma unroll
-            for (int i = j + 1; i < kPanelN; ++i) {
-                const double lcj = lane_d(w[j], min(c0 + i, 63));  // L[c][jj], c = c0 + i
-                if (lane >= c0 + i && c0 + i < D) w[i] = fma(-w[j], lcj, w[i]);
-            }
-        }
-    }
+    panel_cols<0>(w, lane, c0, D, sk);
 #pragma unroll
     for (int i = 0; i < kPanelN; ++i)
         if (lane < D && c0 + i < D && lane >= c0 + i) L[lane * LD + c0 + i] = w[i];
@@ -539,28 +546,35 @@ __device__ __forceinline__ void lower_panel_trailing(double *L, int LD, int D, i
 // Forward substitution panel (rows c0 .. c0 + 15) of X = G^{-1} X0 (G lower) on one wave (lane = column j, the 16
 // rows in registers): row k divided by G_kk (inv: the lower inverse, columns j <= k only and 1 / G_kk on the
 // diagonal), then the panel's later rows updated, fma(-G_rk, X_kj, .).
+// Row I of a forward-substitution panel and then the later ones (template recursion, as panel_cols)
+template <int I>
+__device__ __forceinline__ void forward_rows(double (&w)[kPanelN], const double *G, int LD, int D, int c0, bool inv,
+                                             int lane) {
+    if constexpr (I < kPanelN) {
+        const int k = c0 + I;
+        if (k < D) {  // (wave-uniform)
+            // the row's divisor and its multipliers in one round of (broadcast) LDS reads
+            double g[kPanelN];
+#pragma unroll
+            for (int i2 = I; i2 < kPanelN; ++i2) g[i2] = lds_or0(G, (c0 + i2) * LD + k, c0 + i2 < D);
+            const double gkk = g[I];
+            const bool col = lane < D && (!inv || lane <= k);
+            const double q = ((inv && lane == k) ? 1.0 : w[I]) / gkk;
+            if (col) w[I] = q;
+#pragma unroll
+            for (int i2 = I + 1; i2 < kPanelN; ++i2)
+                if (col && c0 + i2 < D) w[i2] = fma(-g[i2], w[I], w[i2]);
+        }
+        forward_rows<I + 1>(w, G, LD, D, c0, inv, lane);
+    }
+}
+
 __device__ __forceinline__ void forward_panel(double *X, const double *G, int LD, int D, int c0, bool inv) {
     const int lane = threadIdx.x & 63;
     double w[kPanelN];
 #pragma unroll
     for (int i = 0; i < kPanelN; ++i) w[i] = lds_or0(X, (c0 + i) * LD + lane, lane < D && c0 + i < D);
-#pragma unroll
-    for (int i = 0; i < kPanelN; ++i) {
-        const int k = c0 + i;
-        if (k < D) {  // (wave-uniform)
-            // the row's divisor and its 15 multipliers in one round of (broadcast) LDS reads
-            double g[kPanelN];
-#pragma unroll
-            for (int i2 = i; i2 < kPanelN; ++i2) g[i2] = lds_or0(G, (c0 + i2) * LD + k, c0 + i2 < D);
-            const double gkk = g[i];
-            const bool col = lane < D && (!inv || lane <= k);
-            const double q = ((inv && lane == k) ? 1.0 : w[i]) / gkk;
-            if (col) w[i] = q;
-#pragma unroll
-            for (int i2 = i + 1; i2 < kPanelN; ++i2)
-                if (col && c0 + i2 < D) w[i2] = fma(-g[i2], w[i], w[i2]);
-        }
-    }
+    forward_rows<0>(w, G, LD, D, c0, inv, lane);
 #pragma unroll
     for (int i = 0; i < kPanelN; ++i)
         if (lane < D && c0 + i < D && (!inv || lane <= c0 + i)) X[(c0 + i) * LD + lane] = w[i];
@@ -680,7 +694,7 @@ __device__ __forceinline__ void reduce_run_records(const NiwArgs &A, int s, cons
 #pragma unroll
     for (int k = 0; k < kRecE; ++k) v[k] = 0.0;
     if (nm <= cap) {
-        constexpr int kRecR = 4;  // records per round of loads (their sums still taken in record order)
+        constexpr int kRecR = 4;  // records per round of loads (their sums still taken in record order; 8: no faster)
         for (int m = 0; m < nm; m += kRecR) {
             int64_t rr[kRecR];
 #pragma unroll

@@ -58,11 +58,28 @@ __global__ __launch_bounds__(256) void probe(double *out, long long *cyc, int D)
         __syncthreads();
     }
     long long t4 = __builtin_amdgcn_s_memtime();
+    // one panel factor (wave 0) and one forward-substitution panel (wave 1) on a diagonally dominant matrix
+    for (int e = threadIdx.x; e < D * LD; e += blockDim.x) {
+        const int r = e / LD, c = e - r * LD;
+        X[e] = (r == c) ? 100.0 + r : 1.0 / (1.0 + r + c);
+        Y[e] = 0.0;
+    }
+    __shared__ int skip;
+    __syncthreads();
+    long long t5 = __builtin_amdgcn_s_memtime();
+    if ((threadIdx.x >> 6) == 0) lower_panel_factor(X, LD, D, 0, &skip);
+    __syncthreads();
+    long long t6 = __builtin_amdgcn_s_memtime();
+    if ((threadIdx.x >> 6) == 1) forward_panel(Y, X, LD, D, 16, true);
+    __syncthreads();
+    long long t7 = __builtin_amdgcn_s_memtime();
     if (threadIdx.x == 0) {
         cyc[0] = t1 - t0;
         cyc[1] = t2 - t1;
         cyc[2] = t3 - t2;
         cyc[3] = t4 - t3;
+        cyc[4] = t6 - t5;
+        cyc[5] = t7 - t6;
     }
     out[threadIdx.x] = Z[threadIdx.x];
 }
@@ -71,7 +88,7 @@ int main() {
     double *out;
     long long *cyc;
     (void)hipMallocManaged(&out, sizeof(double) * 256);
-    (void)hipMallocManaged(&cyc, sizeof(long long) * 4);
+    (void)hipMallocManaged(&cyc, sizeof(long long) * 8);
     const int D = 64;
     const size_t lds = sizeof(double) * 3 * D * (D + 1);
     for (int it = 0; it < 2; ++it) {
@@ -80,5 +97,6 @@ int main() {
     }
     printf("sym_square_mfma: %.0f cycles per call; sym_square (VALU): %.0f; barrier alone: %.0f; straight-line: %.0f\n",
            cyc[0] / 8.0, cyc[1] / 8.0, cyc[2] / 8.0, cyc[3] / 8.0);
+    printf("lower_panel_factor: %lld cycles per 16-column panel; forward_panel: %lld\n", cyc[4], cyc[5]);
     return 0;
 }
