@@ -263,6 +263,9 @@ template <int D, int M, int PRIOR, bool COUNT>
 #ifndef NP8_FAST_WAVES
 #define NP8_FAST_WAVES 4  // 127 VGPRs, 30 dwords spilled on the rare paths (62 KB written per C3 launch); 5: 2-6% slower
 #endif
+#ifndef NP8_FAST_WAVES_LL
+#define NP8_FAST_WAVES_LL NP8_FAST_WAVES  // the max-likelihood instance (every 5th sweep)
+#endif
 __device__ __forceinline__ void assign_item(const AssignArgs &A, const int64_t p, const int64_t qslot) {
     constexpr int DP = D * (D + 1) / 2;
     constexpr int CS = (D + DP + 5 + 1) & ~1;
@@ -683,7 +686,7 @@ __device__ __forceinline__ Fx fx_readlane(Fx a, int l) {
 // operation (the walk's quadratic forms are the table form's isotropic one) -- in a separate instance, so that the
 // other sweeps carry none of its registers.
 template <int D, int M, int PRIOR, bool COUNT, bool LL>
-__global__ __launch_bounds__(NP8_ASSIGN_BLOCK) __attribute__((amdgpu_waves_per_eu(NP8_FAST_WAVES))) void np8_assign_fast(AssignArgs A) {
+__global__ __launch_bounds__(NP8_ASSIGN_BLOCK) __attribute__((amdgpu_waves_per_eu(LL ? NP8_FAST_WAVES_LL : NP8_FAST_WAVES))) void np8_assign_fast(AssignArgs A) {
     using H = HypView<D>;
     constexpr int DP = D * (D + 1) / 2;
     constexpr int CS = (D + DP + 5 + 1) & ~1;
@@ -836,12 +839,13 @@ __global__ __launch_bounds__(NP8_ASSIGN_BLOCK) __attribute__((amdgpu_waves_per_e
     // staged per round for the first kScreenGroups own rows among the walking lanes (a list walk has one, a table walk
     // of a wave with several labels several); lanes of further own rows take gap = 0.  Valid while the lists are (the
     // same table).  Cost per row: the bound instead of the quadratic form and the pick.
-    const double d_own = sqrt(d2own);
     const bool screen = A.walk_screen != 0 && A.pdist != nullptr && A.use_lists && lists_ok;
     auto walk = [&](auto row_of, int n, bool mine, bool own_skip) {
+        if (n <= 0) return;  // (wave-uniform: the warm state's lists are empty -- none of the set-up below)
         // the walking lanes' own rows (wave-uniform, first kScreenGroups) and this lane's index among them
         int32_t gid[kScreenGroups];
         int ng = 0, gi = -1;
+        const double d_own = screen ? sqrt(d2own) : 0.0;
         if (screen) {
             uint64_t pg = __ballot(mine && !defer);
             for (; pg && ng < kScreenGroups; ++ng) {
