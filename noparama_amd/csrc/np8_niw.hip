@@ -442,9 +442,10 @@ __device__ __forceinline__ void sym_square_mfma(int D, int LD, const double *X, 
 
 // Squarings of Sigma / ||Sigma|| behind the wide path's eigenvalue bound (np8_niw_post): lambda_max <= g ||.^(2^k)||^(2^-k).
 // A/B at C5 niw_conjugate, one box: k = 2: 1 157 sweeps/s, 3: 1 283, 4: 1 338 (each squaring ~10 us of np8_niw_post, a
-// tighter bound fewer screen batches in np8_assign_wide).
+// tighter bound fewer screen batches in np8_assign_wide).  Round 5 (a squaring ~5 us on the matrix cores): k = 4: 1 496,
+// 5: 1 525, 6: 1 512.
 #ifndef NP8_BOUND_SQUARINGS
-#define NP8_BOUND_SQUARINGS 4
+#define NP8_BOUND_SQUARINGS 5
 #endif
 constexpr int kBoundSquarings = NP8_BOUND_SQUARINGS;
 
@@ -634,8 +635,11 @@ __device__ __forceinline__ bool init_ok_records(const NiwArgs &A) { return A.ini
 // thread sums its raw accumulator elements over the list in that order -- a fixed order, no atomics -- and adds
 // them to what the atomic fallback left in acc.  S lands in L's lower triangle index-reversed (element
 // (D - 1 - a, D - 1 - b) = S_ab, a <= b: where np8_niw_post forms J Psin J), s1 in s1.  Scratch: an int list of cap entries (Li's storage, unused until the factor exists).
+// overlap(): block-wide work that needs none of the statistics (the NIW draws), run once while the first round of
+// record loads is in flight (every thread calls it exactly once, no barrier inside).
+template <class Overlap>
 __device__ __forceinline__ void reduce_run_records(const NiwArgs &A, int s, const double *acc, double *L, int LD, double *s1, int *list,
-                                   int cap) {
+                                   int cap, Overlap overlap) {
     // (the records' layout is np8_suffstats_wide's at DT: rows and columns >= D are the zero rows of the items)
     const int D = A.D, T = A.DT / 16, NT = T * (T + 1) / 2, RS = NT * 4 * 64 + T * 16;
     const int tid = threadIdx.x, nt = blockDim.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6), nw = nt >> 6;
@@ -707,13 +711,16 @@ __device__ __forceinline__ void reduce_run_records(const NiwArgs &A, int s, cons
                     const int e = tid + k * nt;
                     a[q][k] = (e < RS && rr[q] >= 0) ? A.part[rr[q] + e] : 0.0;
                 }
+            if (m == 0) overlap();  // (the first round's loads are in flight)
 #pragma unroll
             for (int k = 0; k < kRecE; ++k)
 #pragma unroll
                 for (int q = 0; q < kRecR; ++q)
                     if (rr[q] >= 0) v[k] = v[k] + a[q][k];
         }
+        if (nm == 0) overlap();
     } else {  // (more records than the scratch holds: every header in order)
+        overlap();
         for (int64_t h = 0; h < A.n_rec; ++h)
             if (A.part_slot[h] == s)
 #pragma unroll
@@ -804,12 +811,42 @@ __global__ __launch_bounds__(kNiwThreads) void np8_niw_post(NiwArgs A) {
     NIW_T(0)
     zero_block(L, 3 * D * LD);  // L, Li, B: upper triangles stay 0
     NIW_T(10)
+    // the Bartlett draws and the normals (nothing of the statistics): with run records they run while the records'
+    // first round of loads is in flight
+    auto draws = [&]() {
+        for (int a = tid; a < D; a += blockDim.x) {  // Bartlett diagonal
+            const double g = chi2_mt(A.seed, i, t, stream, kNiwGammaCalls * (uint32_t)a, nun - a);
+            gv[a] = g;
+            B[a * LD + a] = sqrt(g);
+        }
+        // the normals by Philox call: one Box-Muller quad per call gives normals 4q .. 4q + 3 (normal_at's layout), so
+        // each call is made once, not once per normal -- B's off-diagonals first, then z
+        const int nb = D * (D - 1) / 2, nn = nb + D;
+        for (int qd = tid; 4 * qd < nn; qd += blockDim.x) {
+            double g[4];
+            normal_quad(A.seed, i, t, stream, kNiwNormalCall0 + (uint32_t)qd, g);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int e = 4 * qd + k;
+                if (e < nb) {
+                    int a, b;
+                    lower_index(e, a, b);
+                    B[a * LD + b] = g[k];
+                } else if (e < nn) {
+                    z[e - nb] = g[k];
+                }
+            }
+        }
+    };
     const bool recs = A.part != nullptr && n > 0 && init_ok_records(A);
     if (recs) {  // the statistics from np8_suffstats_wide's run records: S into L's lower triangle, s1
         __syncthreads();
-        reduce_run_records(A, s, acc, L, LD, s1, reinterpret_cast<int *>(Li), (int)(D * LD * 2));
+        reduce_run_records(A, s, acc, L, LD, s1, reinterpret_cast<int *>(Li), (int)(D * LD * 2), draws);
         __syncthreads();
         NIW_T(11)
+    } else {
+        __syncthreads();  // (zero_block's writes to B land first)
+        draws();
     }
     for (int a = tid; a < D; a += blockDim.x) {
         anc[a] = (n > 0) ? A.slot_mu[(int64_t)s * D + a] : 0.0;
@@ -837,31 +874,6 @@ __global__ __launch_bounds__(kNiwThreads) void np8_niw_post(NiwArgs A) {
         for (int e = tid; e < D * D; e += blockDim.x) {
             const int r = e / D, j = e - r * D;
             if (j <= r) psin(r, j, S[pix(D, D - 1 - r, D - 1 - j)]);
-        }
-    }
-    for (int a = tid; a < D; a += blockDim.x) {  // Bartlett diagonal
-        const double g = chi2_mt(A.seed, i, t, stream, kNiwGammaCalls * (uint32_t)a, nun - a);
-        gv[a] = g;
-        B[a * LD + a] = sqrt(g);
-    }
-    // the normals by Philox call: one Box-Muller quad per call gives normals 4q .. 4q + 3 (normal_at's layout), so
-    // each call is made once, not once per normal -- B's off-diagonals first, then z
-    {
-        const int nb = D * (D - 1) / 2, nn = nb + D;
-        for (int qd = tid; 4 * qd < nn; qd += blockDim.x) {
-            double g[4];
-            normal_quad(A.seed, i, t, stream, kNiwNormalCall0 + (uint32_t)qd, g);
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const int e = 4 * qd + k;
-                if (e < nb) {
-                    int a, b;
-                    lower_index(e, a, b);
-                    B[a * LD + b] = g[k];
-                } else if (e < nn) {
-                    z[e - nb] = g[k];
-                }
-            }
         }
     }
     __syncthreads();
