@@ -245,6 +245,7 @@ def main():
         if world == 1 and not wide and args.cold_sweeps > 0:
             smp.close()
             out["cold_start"] = cold_start(args, X, z, D, opts, local_rank, torch)
+            out["survey_state"] = survey_state(args, X, z, D, opts, local_rank, torch)
         if world == 1 and not wide and args.c5_sub:
             smp.close()
             del X, z, mu, sig
@@ -441,6 +442,35 @@ def cold_start(args, X, labels, D, opts, device, torch):
     out["quality"]["note"] = ("S = 16 runs with kcap 1024 (the sub-step sort holds substeps x kcap <= 16384 bins); "
                               "tolerance SURVEY.md 8(d): |d purity| <= 0.02, |d ARI| <= 0.05")
     s16.close()
+    return out
+
+
+def survey_state(args, X, labels, D, opts, device, torch):
+    """SURVEY.md 8(d)'s C3 start: z = the generator's labels, theta_k = G0 draws (64 of them, np8_init_random's),
+    frozen parameters; sweeps 0 .. 9 one by one, then sweeps 10 .. 109 timed as the warm leg is (graph replays), with
+    K per sweep over the eager ones and at the end.  Unlike the headline's warm state (theta = the generating
+    parameters, a fixed point of the chain) the items leave their badly placed clusters: the regime of the mixed leg."""
+    from noparama_amd import NealAlgorithm8
+
+    smp = NealAlgorithm8(D, seed=args.seed + 2, device=device, param_update=args.param_update, **opts)
+    smp.set_data(X)
+    smp.init_random(int(labels.max()) + 1)  # (the G0 draws; its uniform labels are replaced next)
+    st = smp.state(params=True)
+    smp.set_state(labels.astype(np.int32), st["mu"], st["sigma"])
+    Ks, per = [], []
+    for _ in range(10):
+        t0 = time.perf_counter()
+        smp.sweep(1)
+        per.append((time.perf_counter() - t0) * 1e3)
+        Ks.append(smp.K)
+    m = measure(smp, lambda n, sync=True: smp.sweep(n, sync=sync), 100, 0, True, None, torch, X.shape[0], D,
+                False, 1, os.path.join(ROOT, "profiles", MIXED_TRAFFIC))
+    out = {"start": "z = generator labels, theta_k = 64 G0 draws (SURVEY.md 8(d) C3 input)",
+           "eager_ms_per_sweep_0_9": [round(v, 3) for v in per], "K_per_sweep_0_9": Ks,
+           "sweeps": "10..109 (graph replays)", "value": 100 / m["dt"], "unit": "sweeps/s",
+           "ms_per_sweep": m["dt"] / 100 * 1e3, "K_final": m["K_final"],
+           "assign_ms_per_launch": m["roofline"].get("assign_ms_per_launch")}
+    smp.close()
     return out
 
 

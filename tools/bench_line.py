@@ -14,6 +14,9 @@ if isinstance(c, dict) and "value" in c:
     out.append(f"cold {c['value']:.0f}")
     if isinstance(c.get("mixed"), dict):
         out.append(f"mixed {c['mixed']['ms_per_sweep'] * 1e3:.1f} us")
+sv = d.get("survey_state")
+if isinstance(sv, dict) and "ms_per_sweep" in sv:
+    out.append(f"survey {sv['ms_per_sweep'] * 1e3:.1f} us K {sv['K_final']}")
 c5 = d.get("c5")
 if isinstance(c5, dict):
     out.append("c5 " + " ".join(f"{k}={v['value']:.0f}" for k, v in c5.items() if isinstance(v, dict) and "value" in v))
