@@ -777,6 +777,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NP8_WIDE_WA
         if (lane == 0) {
             unsigned long long *ec = A.evalc + 2 * ((blockIdx.x * 4 + (threadIdx.x >> 6)) % kEvalSlots);
             atomicAdd(ec, items * (unsigned long long)(rows_done + own_passes));
+#ifdef NP8_EXP_WIDE_ROWS  // experiment: per wave, the rows the triangle mask kept and the rows the exact screen kept
+            if (prune) {
+                atomicAdd(ec + 6 * kEvalSlots, (unsigned long long)rlist_n[0]);
+                atomicAdd(ec + 4 * kEvalSlots + 1, (unsigned long long)rlist_n[1]);
+            }
+#endif
         }
     }
 #pragma unroll
