@@ -94,7 +94,8 @@ typedef struct {
 /* Cluster-likelihood arithmetic (DESIGN.md "Wide path").
  * F64:      fp64 table form (packed sym(Sigma^{-1})), any D from 1 to 16 with M = 3 (the reference's), and
  *           M in {1, 2, 3, 4} for D in {1, 2, 3, 4, 8, 16}.
- * F32_MFMA: D in {32, 48, 64} (config C5): items held in fp32, (x-mu)^T Sigma^{-1} (x-mu) = |A (x-mu)|^2 with
+ * F32_MFMA: 16 < D <= 80 (config C5: D = 64; tables padded with zero rows to D rounded up to 16; the NIW prior up to
+ *           D = 64): items held in fp32, (x-mu)^T Sigma^{-1} (x-mu) = |A (x-mu)|^2 with
  *           A = fp32(chol(sym Sigma^{-1})) contracted on the matrix cores (v_mfma_f32_16x16x4_f32),
  *           |.|^2 in fp32, the draws and the pick in fp64; bit-exact against oracle/ (NP8O_CONTRACT_F32)
  *           and within 1e-5 relative of the fp64 formula.  param_update FROZEN or NIW_CONJUGATE. */
