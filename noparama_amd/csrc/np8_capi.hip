@@ -33,6 +33,10 @@ constexpr int kPruneMaxKcap = 4096;  // kcap x kcap int32 candidate lists (64 MB
 #define NP8_RESORT_EVERY 10
 #endif
 constexpr uint32_t kGatherEvery = NP8_GATHER_EVERY;  // data-parallel sweeps per gathering of fresh pruning radii
+#ifndef NP8_GATHER_PHASE
+#define NP8_GATHER_PHASE 1  // (0 put every gathering sweep on a max-likelihood sweep: 0.4% slower at C3)
+#endif
+constexpr uint32_t kGatherPhase = NP8_GATHER_PHASE;  // the epoch (mod kGatherEvery) of the gathering sweeps
 
 // Host state of one step of a captured compact sweep graph, taken right after its assign was captured: what the rest
 // of the step and end_sweep read.  A replay that halts at step i resumes from it (np8_sweep, recover_halt).
@@ -1149,7 +1153,7 @@ PruneArgs prune_args(np8_ctx *c, bool last) {
     P.gathered = (last && c->gather) ? 1 : 0;
     // the next sweep gathers: clear its buffer here instead of with a memset node at its start (a stale
     // buffer would only raise radii: pruning stays exact)
-    P.clear_next = (last && !P.gathered && c->r2_zero && (c->epoch + 1) % kGatherEvery == 0) ? 1 : 0;
+    P.clear_next = (last && !P.gathered && c->r2_zero && (c->epoch + 1) % kGatherEvery == kGatherPhase) ? 1 : 0;
     c->gath_clear = P.clear_next != 0;
     return P;
 }
@@ -1236,7 +1240,7 @@ int step(np8_ctx *c, int64_t p0, int64_t p1, const int64_t *order, bool use_perm
     c->collecting = c->prune_on && c->use_sorted;
     if (!c->use_sorted) c->lists_valid = c->r2_zero = false;
     if (c->collecting && sub <= 0) {  // the start of a data-parallel sweep: gather radii on this one?
-        c->gather = !c->r2_zero || c->epoch % kGatherEvery == 0;
+        c->gather = !c->r2_zero || c->epoch % kGatherEvery == kGatherPhase;
         const bool cleared = c->gath_clear && c->r2_zero;  // by the previous sweep's prune
         c->gath_clear = false;
         if (!c->r2_zero) {  // no radii yet: every lane walks the table until the first gathered sweep ends
