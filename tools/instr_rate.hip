@@ -73,6 +73,30 @@ __global__ void k_sqrt(double *out, double a) {
     out[blockIdx.x * blockDim.x + threadIdx.x] = s;
 }
 
+__global__ void k_fma32(float *out, float a) {
+    float x[8];
+    for (int i = 0; i < 8; ++i) x[i] = threadIdx.x + i;
+    for (int it = 0; it < kIters; ++it)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) x[i] = fmaf(x[i], a, 0.5f);
+    float s = 0;
+    for (int i = 0; i < 8; ++i) s += x[i];
+    out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__global__ void k_pkfma(float *out, float a) {  // v_pk_fma_f32: two fp32 fmas per lane per instruction
+    f32x2 x[8];
+    for (int i = 0; i < 8; ++i) x[i] = (f32x2){(float)threadIdx.x + i, (float)threadIdx.x - i};
+    const f32x2 av = {a, a}, h = {0.5f, 0.25f};
+    for (int it = 0; it < kIters; ++it)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) x[i] = __builtin_elementwise_fma(x[i], av, h);
+    float s = 0;
+    for (int i = 0; i < 8; ++i) s += x[i].x + x[i].y;
+    out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+
 #define RUN(name, kern, T, arg, ops)                                                                  \
     {                                                                                               \
         T *out;                                                                                     \
@@ -97,6 +121,8 @@ int main() {
     hipEventCreate(&a);
     hipEventCreate(&b);
     RUN("fma_f64", k_fma, double, 1.0000001, 8.0 * kIters);
+    RUN("fma_f32", k_fma32, float, 1.0000001f, 8.0 * kIters);
+    RUN("pkfma_f32", k_pkfma, float, 1.0000001f, 8.0 * kIters);
     RUN("mad_u64", k_mad64, uint64_t, 0xD2511F53u, 8.0 * kIters);
     RUN("mul_lo", k_mullo, uint32_t, 0xD2511F53u, 8.0 * kIters);
     RUN("xor+add", k_xor, uint32_t, 0xD2511F53u, 16.0 * kIters);
