@@ -82,6 +82,7 @@ struct np8_ctx {
     float *wA = nullptr, *wfrag = nullptr, *wmu = nullptr;
     int32_t *wdirty = nullptr;
     double *lam_lo = nullptr, *wdist = nullptr;  // wide-path candidate pruning (np8_wide_dist)
+    double *wnx = nullptr;  // wide path: per local item (|U^T (x - mu0)|, |x|^2), np8_wide_frame at np8_set_data
     double *acc = nullptr;  // [kcap][D + DP] parameter-update statistics
     // wide path, one rank, niw_conjugate: np8_suffstats_wide's run records (reduced by np8_niw_post, no atomics)
     double *part = nullptr;
@@ -515,14 +516,14 @@ bool slot_from_sigma(const np8_ctx *c, const double *mu, const double *Sigma, Sl
 
 void free_device(np8_ctx *c) {
     void *niw_ptrs[] = {c->d_U, c->d_Uinv, c->d_Psi0, c->pend, c->wA, c->wfrag, c->wmu, c->wdirty, c->lam_lo, c->wdist,
-                        c->pend_ll};
+                        c->pend_ll, c->wnx};
     for (void *p : niw_ptrs)
         if (p) (void)hipFree(p);
     c->d_U = c->d_Uinv = c->d_Psi0 = nullptr;
     c->pend = c->pend_ll = nullptr;
     c->wA = c->wfrag = c->wmu = nullptr;
     c->wdirty = nullptr;
-    c->lam_lo = c->wdist = nullptr;
+    c->lam_lo = c->wdist = c->wnx = nullptr;
     void *ptrs[] = {c->X,      c->z,       c->z_best, c->slot_mu, c->slot_P,  c->slot_c,  c->slot_sigma,
                     c->cnt,    c->cnt_best, c->mu_best, c->sigma_best, c->cand, c->ctl,    c->hyp,
                     c->d_mu0,  c->d_LT,    c->d_Gp,   c->d_LTL,   c->rec,     c->gath,    c->order,
@@ -928,6 +929,7 @@ AssignArgs assign_args(np8_ctx *c, int64_t p0, int64_t p1, const int64_t *order,
     A.lam_lo = c->lam_lo;
     A.dim = c->D;
     A.uw = c->wide ? c->hyp + c->uw_off : nullptr;
+    A.wnx = c->wnx;
     A.wdist = nullptr;  // set by launch_assign on the wide path (after np8_wide_dist)
     A.queue = A.queue_out = A.qcount = A.qlist = nullptr;
     A.slot_mu = c->slot_mu;
@@ -1112,7 +1114,7 @@ int launch_assign(np8_ctx *c, int64_t p0, int64_t p1, const int64_t *order, bool
             HIPC(c, np8_launch_wide_dist(wide_args(c), c->stream));
             A.wdist = c->wdist;
         }
-        HIPC(c, np8_launch_assign_wide(A, c->D, c->M, c->prior, c->diag_U, c->stream));
+        HIPC(c, np8_launch_assign_wide(A, c->D, c->M, c->prior, c->stream));
     }
     else if (c->diag_U && !c->fast_off && c->prior == NP8_PRIOR_REFERENCE && A.sorted && !order && !use_perm) {
         // the lean kernel for every lane, then the full one over the lanes it deferred (ctl->qn)
@@ -2016,6 +2018,7 @@ int np8_set_data(np8_ctx *c, const double *X, int64_t n, int32_t D, int64_t offs
         (c->wide && c->param_update == NP8_PARAM_NIW_CONJUGATE &&
          ((r = dalloc(c, &c->part, (size_t)(np8_suffstats_wide_waves(n) * kSuffRuns * np8_suffstats_wide_record(D)))) ||
           (r = dalloc(c, &c->part_slot, (size_t)(np8_suffstats_wide_waves(n) * kSuffRuns))))) ||
+        (c->wide && (r = dalloc(c, &c->wnx, (size_t)2 * n))) ||
         (r = dalloc(c, &c->queue, (size_t)(64 * ((n + 63) / 64) + 64))) ||
         (r = dalloc(c, &c->qcount, (size_t)((n + 63) / 64 + 1))) ||
         (r = dalloc(c, &c->qlist, (size_t)((n + 63) / 64 + 1))))
@@ -2042,6 +2045,8 @@ int np8_set_data(np8_ctx *c, const double *X, int64_t n, int32_t D, int64_t offs
         for (int64_t i = 0; i < n; ++i)
             for (int a = 0; a < D; ++a) soa[(size_t)a * n + i] = (float)X[(size_t)i * D + a];
         HIPC(c, hipMemcpyAsync(c->X, soa.data(), sizeof(float) * soa.size(), hipMemcpyHostToDevice, c->stream));
+        HIPC(c, np8_launch_wide_frame(reinterpret_cast<const float *>(c->X), n, c->hyp + c->uw_off, c->DT, c->wnx,
+                                      c->stream));
         HIPC(c, hipStreamSynchronize(c->stream));
     } else {
         std::vector<double> soa((size_t)n * D);

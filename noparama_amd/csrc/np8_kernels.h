@@ -222,6 +222,7 @@ struct AssignArgs {
     int32_t dim = 0;           // wide path: the data's D (the kernels are instantiated for DT = D rounded up to 16; the
                                // item rows, factors and means beyond D are zero)
     const double *uw = nullptr;  // wide path: mu0 [DT] | U^T packed [DT (DT + 1) / 2], zero beyond D (the item frame)
+    const double *wnx = nullptr; // wide path: per local item, (|U^T (x - mu0)|, |x|^2) (np8_wide_frame, once per data set)
     const double *wdist;       // [K][kcap] distances between row means (np8_wide_dist); null: no pruning
     // two-kernel step (np8_assign_fast + np8_assign): positions the fast kernel deferred; non-null makes
     // np8_assign run over them instead of [p0, p1)
@@ -590,7 +591,9 @@ struct SortArgs {
 
 bool np8_supported(int D, int M);
 bool np8_wide_supported(int D, int M);
-hipError_t np8_launch_assign_wide(const np8::AssignArgs &A, int D, int M, int prior, bool diag_u, hipStream_t s);
+hipError_t np8_launch_assign_wide(const np8::AssignArgs &A, int D, int M, int prior, hipStream_t s);
+// the wide path's per-item frame (AssignArgs::wnx) over the fp32 items X [DT][n] and uw (AssignArgs::uw)
+hipError_t np8_launch_wide_frame(const float *X, int64_t n, const double *uw, int DT, double *wnx, hipStream_t s);
 // Wide-path pruning: the distance table of the current dense rows (after every table change).
 hipError_t np8_launch_wide_dist(const np8::WideArgs &W, hipStream_t s);
 hipError_t np8_launch_loglik_matrix_wide(const np8::AssignArgs &A, const np8::WideArgs &W, int D, int M, int prior,

@@ -432,20 +432,17 @@ __global__ void np8_wide_clean(WideArgs W) {
 
 // ---- the sweep kernel -----------------------------------------------------------------------------
 // Dynamic LDS: two candidate-row stages of Wide<D>::ROW floats (33 KB at D = 64).
-// DIAGU: the base measure's whitening U^T is diagonal (Psi0 or Lambda diagonal, every configuration the
-// benchmarks run): |U^T (x - mu0)| streams over the item's dims, as wide_whiten_norm's operations with the
-// zero terms left out (fma(0, t, v) = v), instead of holding D doubles of x - mu0.
 // LL: a max-likelihood check sweep with the sum folded in (frozen parameters, one rank): each wave stores the exact sum
 // of its items' log-likelihoods under their new labels in llpart (a requester under its old slot: np8_ll_fix_wide moves
 // the accepted ones once their slots exist) -- np8_loglik_wide_mfma's values, the own and walked rows' q being the
 // same contractions.
-template <int DT, int M, int PRIOR, bool DIAGU, bool LL, bool EXACT>
+template <int DT, int M, int PRIOR, bool LL, bool EXACT>
 #ifndef NP8_WIDE_WAVES
 #define NP8_WIDE_WAVES 2
 #endif
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NP8_WIDE_WAVES, NP8_WIDE_WAVES))) void np8_assign_wide(AssignArgs A) {
     using W = Wide<DT>;
-    // the data's D (hyp, cand, records): EXACT = D is DT itself, a constant of the instance -- the DIAGU frame loop,
+    // the data's D (hyp, cand, records): EXACT = D is DT itself, a constant of the instance -- the pruning distance,
     // the auxiliaries' D chi^2 draws and every table offset fold (a runtime D cost C5's assign 235 -> 338 us)
     const int D = EXACT ? DT : A.dim, DP = D * (D + 1) / 2, CS = cand_stride(D), F = D + DP;
     extern __shared__ __attribute__((aligned(16))) float stage[];
@@ -474,42 +471,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NP8_WIDE_WA
     const int32_t zi = sorted ? zs[pc] : A.z[il];
     const int32_t jo = A.dense_of[zi];
 
-    // the item's frame for the auxiliaries: only |U^T (x - mu0)| is needed
-    double rown = 0.0;  // |x - muf_own|
-    double x2 = 0.0;    // |x|^2 (the exact distance screen)
-    double ny;
-    if constexpr (DIAGU) {
-        const double *U = hyp + D;
+    // the item's frame for the auxiliaries (|U^T (x - mu0)|) and |x|^2 (the exact distance screen): per item, once
+    // per data set (np8_wide_frame) -- a general U^T's D (D + 1) / 2 products per lane stay out of the sweep
+    const double ny = A.wnx[2 * il], x2 = A.wnx[2 * il + 1];
+    double rown = 0.0;  // |x - muf_own| (candidate pruning)
+    if (A.wdist) {
         const float *mo = A.wmu + (int64_t)zi * DT;
-        double n2 = 0.0, d2 = 0.0;
+        double d2 = 0.0;
 #pragma unroll 16
         for (int a = 0; a < D; ++a) {
-            const float xa = X[(int64_t)a * n + xr];
-            const double y = U[a * D - (a * (a - 1)) / 2] * ((double)xa - hyp[a]);
-            n2 = fma(y, y, n2);
-            const double dd = (double)xa - (double)mo[a];
+            const double dd = (double)X[(int64_t)a * n + xr] - (double)mo[a];
             d2 = fma(dd, dd, d2);
-            x2 = fma((double)xa, (double)xa, x2);
         }
-        ny = sqrt(n2);
-        if (A.wdist) rown = sqrt(d2);
-    } else {
-        float xf[DT];
-#pragma unroll
-        for (int a = 0; a < DT; ++a) xf[a] = X[(int64_t)a * n + xr];  // (rows >= D: zeros)
-        ny = wide_whiten_norm<DT>(A.uw, xf);
-#pragma unroll
-        for (int a = 0; a < DT; ++a) x2 = fma((double)xf[a], (double)xf[a], x2);  // (rows >= D: + 0)
-        if (A.wdist) {  // the item's distance to its own row's fp32 mean (candidate pruning)
-            const float *mo = A.wmu + (int64_t)zi * DT;
-            double d2 = 0.0;
-#pragma unroll
-            for (int a = 0; a < D; ++a) {
-                const double dd = (double)xf[a] - (double)mo[a];
-                d2 = fma(dd, dd, d2);
-            }
-            rown = sqrt(d2);
-        }
+        rown = sqrt(d2);
     }
 
     // MFMA operand B: raw items 16 nt + col of the wave, dims 4 s + g
@@ -1230,33 +1204,61 @@ bool np8_wide_supported(int D, int M) {
     return false;
 }
 
-hipError_t np8_launch_assign_wide(const AssignArgs &A, int D, int M, int prior, bool diag_u, hipStream_t s) {
+hipError_t np8_launch_assign_wide(const AssignArgs &A, int D, int M, int prior, hipStream_t s) {
     const int64_t n = A.p1 - A.p0;
     if (n <= 0) return hipSuccess;
     const dim3 grid((unsigned)((n + 255) / 256)), block(256);
     const int DT = wide_dt(D);
     const bool exact = D == DT;  // (D a multiple of 16: the instances with a constant D)
-#define AW(d, m, prior_, diag_, ll_, ex_) hipLaunchKernelGGL((np8_assign_wide<d, m, prior_, diag_, ll_, ex_>), grid, block, lds, s, A)
+#define AW(d, m, prior_, ll_, ex_) hipLaunchKernelGGL((np8_assign_wide<d, m, prior_, ll_, ex_>), grid, block, lds, s, A)
+#define AWP(d, m, prior_)                                                                                    \
+    {                                                                                                        \
+        if (A.ll_on)                                                                                         \
+            { if (exact) AW(d, m, prior_, true, true); else AW(d, m, prior_, true, false); }                 \
+        else                                                                                                 \
+            { if (exact) AW(d, m, prior_, false, true); else AW(d, m, prior_, false, false); }               \
+    }
 #define X(d, m)                                                                                              \
     if (DT == d && M == m) {                                                                                 \
         const size_t lds = 2 * sizeof(float) * Wide<d>::ROW;                                                 \
-        if (prior == kPriorNiw && diag_u && A.ll_on)                                                         \
-            { if (exact) AW(d, m, kPriorNiw, true, true, true); else AW(d, m, kPriorNiw, true, true, false); }          \
-        else if (prior == kPriorNiw && diag_u)                                                               \
-            { if (exact) AW(d, m, kPriorNiw, true, false, true); else AW(d, m, kPriorNiw, true, false, false); }        \
-        else if (prior == kPriorNiw)                                                                         \
-            AW(d, m, kPriorNiw, false, false, false);                                                        \
-        else if (diag_u && A.ll_on)                                                                          \
-            { if (exact) AW(d, m, kPriorReference, true, true, true); else AW(d, m, kPriorReference, true, true, false); } \
-        else if (diag_u)                                                                                     \
-            { if (exact) AW(d, m, kPriorReference, true, false, true); else AW(d, m, kPriorReference, true, false, false); } \
-        else                                                                                                 \
-            AW(d, m, kPriorReference, false, false, false);                                                  \
+        if (prior == kPriorNiw) AWP(d, m, kPriorNiw) else AWP(d, m, kPriorReference)                         \
         return hipGetLastError();                                                                            \
     }
     NP8_WIDE_FOR_EACH(X)
 #undef X
+#undef AWP
 #undef AW
+    return hipErrorInvalidValue;
+}
+
+// The per-item frame of the wide assign (AssignArgs::wnx): |U^T (x - mu0)| (wide_whiten_norm, the fully unrolled
+// triangular product) and |x|^2, one thread per item, once per data set.
+template <int DT>
+__global__ __launch_bounds__(256) void np8_wide_frame(const float *__restrict__ X, int64_t n,
+                                                      const double *__restrict__ uw, double *__restrict__ wnx) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    float xf[DT];
+#pragma unroll
+    for (int a = 0; a < DT; ++a) xf[a] = X[(int64_t)a * n + i];  // (rows >= D: zeros)
+    const double ny = wide_whiten_norm<DT>(uw, xf);
+    double x2 = 0.0;
+#pragma unroll
+    for (int a = 0; a < DT; ++a) x2 = fma((double)xf[a], (double)xf[a], x2);  // (rows >= D: + 0)
+    wnx[2 * i] = ny;
+    wnx[2 * i + 1] = x2;
+}
+
+hipError_t np8_launch_wide_frame(const float *X, int64_t n, const double *uw, int DT, double *wnx, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    const dim3 grid((unsigned)((n + 255) / 256)), block(256);
+#define X(d, m)                                                                                     \
+    if (DT == d) {                                                                                  \
+        hipLaunchKernelGGL((np8_wide_frame<d>), grid, block, 0, s, X, n, uw, wnx);                  \
+        return hipGetLastError();                                                                   \
+    }
+    NP8_WIDE_FOR_EACH(X)
+#undef X
     return hipErrorInvalidValue;
 }
 

@@ -186,3 +186,35 @@ def test_wide_rejects_niw_above_64():
 
     with pytest.raises(NP8Error):
         NealAlgorithm8(80, contraction="f32", kcap=256, device=0, **kw_for(80, "niw", 1))
+
+
+def spd(D, seed):
+    rng = np.random.default_rng(seed)
+    A = rng.normal(size=(D, D)) / np.sqrt(D)
+    return A @ A.T + 0.5 * np.eye(D)
+
+
+@pytest.mark.parametrize("D,prior", [(20, "niw"), (40, "reference"), (64, "niw"), (80, "reference")])
+def test_wide_full_prior_scale_bit_exact(D, prior):
+    """A prior scale with off-diagonal terms (Lambda / Psi0 not diagonal): the general whitening U^T of the item frame
+    (np8_wide_frame, once per data set), warm sweeps and the reference initialisation's new clusters."""
+    kw = kw_for(D, prior, 31)
+    kw["Lambda"] = kw["Lambda"][0, 0] * spd(D, D)
+    X, z, cent = mixture(D, 2500, 5, 500 + D)
+    sig = np.repeat(np.eye(D)[None], 5, axis=0)
+    g = NealAlgorithm8(D, contraction="f32", kcap=512, device=0, **kw)
+    o = O.Chain(D, contraction="f32", kcap=512, **kw)
+    for c in (g, o):
+        c.set_data(X)
+        c.set_state(z.astype(np.int32), cent, sig)
+    for _ in range(2):
+        g.sweep(2)
+        o.sweep(2)
+        assert_state(g, o)
+    for c in (g, o):
+        c.init_random(10)
+    for n in (1, 3):
+        g.sweep(n)
+        o.sweep(n)
+        assert_state(g, o)
+    assert g.stats()["new_clusters"] > 0
