@@ -5,8 +5,7 @@
 //
 //   np8_wide_rows     per slot whose parameters changed: R = chol_upper(sym Sigma^{-1}) (fp64, in LDS),
 //                     A = fp32(R) in natural and MFMA-fragment order, muf = fp32(mu) (natural and
-//                     fragment order)
-//   np8_wide_clean    clears the change flags
+//                     fragment order); clears the change flags
 //   np8_assign_wide   4 waves x 64 items per block (one lane per item for the fp64 parts): per candidate
 //                     row the 64 x D x D contraction y = A_j (x - muf_j) on the matrix cores, q = |y|^2 in
 //                     fp64, then the single-uniform reservoir pick of np8_assign (src/np_neal_algorithm8.cpp:
@@ -297,15 +296,14 @@ __device__ __forceinline__ void panel_trailing(double *M, int LD, int D, int c0,
 #else
 #define WR_T(k)
 #endif
-__global__ __launch_bounds__(256) void np8_wide_rows(WideArgs W) {
+__device__ void wide_rows_slot(const WideArgs &W, const int s) {
 #ifdef NP8_EXP_WIDE_TIMING
     long long tph[16];
     for (int k = 0; k < 16; ++k) tph[k] = 0;
     int nrd = 0;
 #endif
     WR_T(0)
-    const int s = blockIdx.x;
-    if (!W.dirty[s] || W.cnt[s] <= 0) return;  // block-uniform
+    if (W.cnt[s] <= 0) return;  // block-uniform
     const int D = W.D, LD = D + 1, tid = threadIdx.x, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int nq = wide_rows_tests(D);  // concurrent Cholesky tests: three, two above D = 64 (LDS)
     extern __shared__ __attribute__((aligned(16))) double smr[];
@@ -406,28 +404,51 @@ __global__ __launch_bounds__(256) void np8_wide_rows(WideArgs W) {
 #endif
 }
 
-// Candidate pruning (DESIGN.md "Wide path"): distances between the fp32 means of the dense rows, in fp64,
-// wdist[j0 * kcap + j].  One block per row j0 (a grid of kcap; rows >= K exit).
-__global__ __launch_bounds__(256) void np8_wide_dist(WideArgs W) {
-    const int K = W.ctl->K, j0 = blockIdx.x;
-    if (j0 >= K) return;
-    const int D = W.D, DP = D * (D + 1) / 2, CS = cand_stride(D);
-    const int s0 = (int)W.cand[(int64_t)j0 * CS + D + DP + kFieldSlot];
-    const float *m0 = W.wmu + (int64_t)s0 * W.DT;
-    for (int j = threadIdx.x; j < K; j += blockDim.x) {
-        const int sj = (int)W.cand[(int64_t)j * CS + D + DP + kFieldSlot];
-        const float *mj = W.wmu + (int64_t)sj * W.DT;
-        double d2 = 0.0;
-        for (int a = 0; a < D; ++a) {
-            const double dd = (double)mj[a] - (double)m0[a];
-            d2 = fma(dd, dd, d2);
-        }
-        W.wdist[(int64_t)j0 * W.kcap + j] = sqrt(d2);  // the distance itself: no square root per lane and row
+// The slots flagged in wdirty, each by one block in turn (a grid of at most one block per CU: the factor's LDS
+// allows one per CU anyway, and a sweep that changed no slot costs one round of blocks instead of kcap / 256); the
+// flags are cleared as they are taken.
+constexpr int kWideRowsBlocks = 256;
+__global__ __launch_bounds__(256) void np8_wide_rows(WideArgs W) {
+    for (int s = blockIdx.x; s < W.kcap; s += gridDim.x) {
+        if (!W.dirty[s]) continue;  // block-uniform
+        __syncthreads();            // every thread has read the flag; the previous slot's LDS reads are done
+        if (threadIdx.x == 0) W.dirty[s] = 0;
+        wide_rows_slot(W, s);
     }
 }
 
-__global__ void np8_wide_clean(WideArgs W) {
-    for (int s = blockIdx.x * blockDim.x + threadIdx.x; s < W.kcap; s += gridDim.x * blockDim.x) W.dirty[s] = 0;
+// Candidate pruning (DESIGN.md "Wide path"): distances between the fp32 means of the dense rows, in fp64,
+// wdist[j0 * kcap + j].  One block per row j0 (a grid of kcap; rows >= K exit).  The means are read four at a
+// time over all DT dims (zero beyond D: fma(0, 0, d2) = d2), every load of a row before the chain.
+__global__ __launch_bounds__(256) void np8_wide_dist(WideArgs W) {
+    const int K = W.ctl->K, j0 = blockIdx.x;
+    if (j0 >= K) return;
+    const int D = W.D, DP = D * (D + 1) / 2, CS = cand_stride(D), DT = W.DT;
+    const int s0 = (int)W.cand[(int64_t)j0 * CS + D + DP + kFieldSlot];
+    const float4 *m0 = reinterpret_cast<const float4 *>(W.wmu + (int64_t)s0 * DT);
+    for (int j = threadIdx.x; j < K; j += blockDim.x) {
+        const int sj = (int)W.cand[(int64_t)j * CS + D + DP + kFieldSlot];
+        const float4 *mj = reinterpret_cast<const float4 *>(W.wmu + (int64_t)sj * DT);
+        double d2 = 0.0;
+        for (int a0 = 0; a0 < DT / 4; a0 += 4) {  // (DT / 4 is a multiple of 4)
+            float4 v[4], u[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                v[q] = mj[a0 + q];
+                u[q] = m0[a0 + q];
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const double d0 = (double)v[q].x - (double)u[q].x, d1 = (double)v[q].y - (double)u[q].y;
+                const double e0 = (double)v[q].z - (double)u[q].z, e1 = (double)v[q].w - (double)u[q].w;
+                d2 = fma(d0, d0, d2);
+                d2 = fma(d1, d1, d2);
+                d2 = fma(e0, e0, d2);
+                d2 = fma(e1, e1, d2);
+            }
+        }
+        W.wdist[(int64_t)j0 * W.kcap + j] = sqrt(d2);  // the distance itself: no square root per lane and row
+    }
 }
 
 // ---- the sweep kernel -----------------------------------------------------------------------------
@@ -1313,7 +1334,6 @@ hipError_t np8_launch_wide_refresh(const WideArgs &W, hipStream_t s) {
         if (e != hipSuccess) return e;
         allowed = true;
     }
-    hipLaunchKernelGGL(np8_wide_rows, dim3((unsigned)W.kcap), dim3(256), lds, s, W);
-    hipLaunchKernelGGL(np8_wide_clean, dim3((unsigned)((W.kcap + 255) / 256)), dim3(256), 0, s, W);
+    hipLaunchKernelGGL(np8_wide_rows, dim3((unsigned)std::min(W.kcap, kWideRowsBlocks)), dim3(256), lds, s, W);
     return hipGetLastError();
 }
