@@ -83,6 +83,7 @@ struct np8_ctx {
     int32_t *wdirty = nullptr;
     double *lam_lo = nullptr, *wdist = nullptr;  // wide-path candidate pruning (np8_wide_dist)
     double *wnx = nullptr;  // wide path: per local item (|U^T (x - mu0)|, |x|^2), np8_wide_frame at np8_set_data
+    bool screen16 = false;  // wide path: every item's |x|^2 <= kScreen16X2 (the fp16 exact-distance screen, AssignArgs)
     double *acc = nullptr;  // [kcap][D + DP] parameter-update statistics
     // wide path, one rank, niw_conjugate: np8_suffstats_wide's run records (reduced by np8_niw_post, no atomics)
     double *part = nullptr;
@@ -930,6 +931,7 @@ AssignArgs assign_args(np8_ctx *c, int64_t p0, int64_t p1, const int64_t *order,
     A.dim = c->D;
     A.uw = c->wide ? c->hyp + c->uw_off : nullptr;
     A.wnx = c->wnx;
+    A.screen16 = c->screen16 ? 1 : 0;
     A.wdist = nullptr;  // set by launch_assign on the wide path (after np8_wide_dist)
     A.queue = A.queue_out = A.qcount = A.qlist = nullptr;
     A.slot_mu = c->slot_mu;
@@ -2042,8 +2044,17 @@ int np8_set_data(np8_ctx *c, const double *X, int64_t n, int32_t D, int64_t offs
     c->sorted_valid = false;
     if (c->wide) {  // rounded to fp32 (round to nearest even), as oracle/np8_oracle.c set_data does
         std::vector<float> soa((size_t)n * c->DT, 0.0f);
-        for (int64_t i = 0; i < n; ++i)
-            for (int a = 0; a < D; ++a) soa[(size_t)a * n + i] = (float)X[(size_t)i * D + a];
+        double x2max = 0.0;
+        for (int64_t i = 0; i < n; ++i) {
+            double x2 = 0.0;
+            for (int a = 0; a < D; ++a) {
+                const float v = (float)X[(size_t)i * D + a];
+                soa[(size_t)a * n + i] = v;
+                x2 += (double)v * v;
+            }
+            x2max = std::max(x2max, x2);
+        }
+        c->screen16 = x2max <= kScreen16X2 && std::getenv("NP8_SCREEN_F32") == nullptr;  // (NaN: false; env: A/B switch)
         HIPC(c, hipMemcpyAsync(c->X, soa.data(), sizeof(float) * soa.size(), hipMemcpyHostToDevice, c->stream));
         HIPC(c, np8_launch_wide_frame(reinterpret_cast<const float *>(c->X), n, c->hyp + c->uw_off, c->DT, c->wnx,
                                       c->stream));

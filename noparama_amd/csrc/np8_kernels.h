@@ -223,6 +223,8 @@ struct AssignArgs {
                                // item rows, factors and means beyond D are zero)
     const double *uw = nullptr;  // wide path: mu0 [DT] | U^T packed [DT (DT + 1) / 2], zero beyond D (the item frame)
     const double *wnx = nullptr; // wide path: per local item, (|U^T (x - mu0)|, |x|^2) (np8_wide_frame, once per data set)
+    int32_t screen16 = 0;        // wide path: the exact-distance screen's dot products in fp16 (every |x|^2 <= kScreen16X2)
+    int32_t pad_s16 = 0;
     const double *wdist;       // [K][kcap] distances between row means (np8_wide_dist); null: no pruning
     // two-kernel step (np8_assign_fast + np8_assign): positions the fast kernel deferred; non-null makes
     // np8_assign run over them instead of [p0, p1)
@@ -551,6 +553,9 @@ struct ParamArgs {
 // Own rows per wave up to which np8_assign(_fast)'s lanes walk their rows' lists group by group (default of
 // AssignArgs::max_groups; NP8_MAX_LIST_GROUPS overrides it).
 constexpr int kMaxListGroups = 3;
+// the wide path's fp16 exact-distance screen: for data with every |x|^2 at most this (its margin, 2e-3 (|x|^2 + |muf|^2),
+// stays small against the distances between clusters; larger data keep the fp32 screen, margin 1e-5 (...))
+constexpr double kScreen16X2 = 4096.0;
 constexpr int kSuffRuns = 4;  // run records per wave of np8_suffstats_wide
 
 struct SnapArgs {

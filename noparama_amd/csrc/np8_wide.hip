@@ -651,8 +651,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NP8_WIDE_WA
     // most of it at D = 64 (x - mu_own is nearly orthogonal to mu_j - mu_own).  A row survives when a lane of
     // the block may not skip it; results are unchanged.  The next batch's means are loaded while this one's
     // MFMAs run.
+    // h16 (DT <= 64, items with |x|^2 <= kScreen16X2, np8_set_data): the dot products in fp16, v_mfma_f32_16x16x32_f16, S / 8
+    // MFMAs per item tile and 16 rows instead of S.  Rigorous margin: rounding x and muf to fp16 (relative 2^-11,
+    // absolute 2^-14 with subnormals flushed) and summing the exact products in fp32 errs by <= 2^-10 sum |x_a muf_a| +
+    // 2^-14 (sum |x_a| + sum |muf_a|) + 2^-17 sq <= 9.8e-4 sq + 2.5e-4 (D <= 64, sq = |x|^2 + |muf|^2), so
+    // d^2 >= sq - 2 x.muf - (2e-3 sq + 1e-3); a pair with sq > 1e8 (fp16 overflow possible) is not screened.
     if (prune) {
         const int n1 = rlist_n[0];
+        const bool h16 = DT <= 64 && A.screen16;
         if (wave_live && n1 > 0) {
             using W2 = Wide<DT>;
             const double Tl = valid ? st.T : 1e300;
@@ -695,10 +701,29 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NP8_WIDE_WA
                 f32x4 acc[4];
 #pragma unroll
                 for (int nt = 0; nt < 4; ++nt) acc[nt] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+                if (h16) {  // fp16 operands, 32 dims per MFMA (the same dims of a lane in A and B: any k order will do)
+                    typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+                    constexpr int HC = (W2::S + 7) / 8;
 #pragma unroll
-                for (int s = 0; s < W2::S; ++s)
+                    for (int hc = 0; hc < HC; ++hc) {
+                        h8 ah;
 #pragma unroll
-                    for (int nt = 0; nt < 4; ++nt) acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(am[s], xb[nt][s], acc[nt], 0, 0, 0);
+                        for (int e = 0; e < 8; ++e) ah[e] = (8 * hc + e < W2::S) ? (_Float16)am[(8 * hc + e) % W2::S] : (_Float16)0.0f;
+#pragma unroll
+                        for (int nt = 0; nt < 4; ++nt) {
+                            h8 bh;
+#pragma unroll
+                            for (int e = 0; e < 8; ++e)
+                                bh[e] = (8 * hc + e < W2::S) ? (_Float16)xb[nt][(8 * hc + e) % W2::S] : (_Float16)0.0f;
+                            acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh, acc[nt], 0, 0, 0);
+                        }
+                    }
+                } else {
+#pragma unroll
+                    for (int s = 0; s < W2::S; ++s)
+#pragma unroll
+                        for (int nt = 0; nt < 4; ++nt) acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(am[s], xb[nt][s], acc[nt], 0, 0, 0);
+                }
                 // output (nt, r) of lane (g, col): row list[b0 + 4 g + r], item 16 nt + col
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
@@ -713,10 +738,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NP8_WIDE_WA
                         for (int nt = 0; nt < 4; ++nt) {
                             if (sjr != zit[nt] && Ti[nt] < 1e299) {
                                 const double sq = x2i[nt] + m2r;
-                                const double d2 = fmax(fma(-2.0, (double)acc[nt][r], sq) - 1e-5 * sq, 0.0);
+                                const double d2 = fmax(fma(-2.0, (double)acc[nt][r], sq) - (h16 ? 2e-3 * sq + 1e-3 : 1e-5 * sq), 0.0);
                                 const double far = lamh * d2;
                                 const double U = base - far - Ti[nt];
-                                nr = nr || !(U <= -kSkip - 2.0 - 1e-9 * (fabs(base) + fabs(Ti[nt]) + far));
+                                nr = nr || (h16 && !(sq <= 1e8)) || !(U <= -kSkip - 2.0 - 1e-9 * (fabs(base) + fabs(Ti[nt]) + far));
                             }
                         }
                     }

@@ -218,3 +218,29 @@ def test_wide_full_prior_scale_bit_exact(D, prior):
         o.sweep(n)
         assert_state(g, o)
     assert g.stats()["new_clusters"] > 0
+
+
+@pytest.mark.parametrize("offset", [0.0, 25.0])
+def test_wide_screen_fp16_and_fp32_bit_exact(offset):
+    """The exact-distance screen in fp16 (every |x|^2 <= 4096: centred data) and in fp32 (offset data): many clusters
+    at D = 64, scrambled labels (mixed waves, several screened rows per wave), then sweeps from the reference
+    initialisation; the screen only drops rows its rigorous margin excludes, so labels stay bit-exact."""
+    D = 64
+    X, z, cent = mixture(D, 4096, 48, 77, spread=2.5)
+    X, cent = X + offset, cent + offset
+    sig = np.repeat(np.eye(D)[None], 48, axis=0)
+    zr = np.random.default_rng(3).integers(0, 48, 4096).astype(np.int32)
+    kw = kw_for(D, "reference", 23)
+    kw["mu0"] = np.full(D, offset)
+    g = NealAlgorithm8(D, contraction="f32", kcap=512, device=0, **kw)
+    o = O.Chain(D, contraction="f32", kcap=512, **kw)
+    for c in (g, o):
+        c.set_data(X)
+        c.set_state(zr, cent, sig)
+    for _ in range(3):
+        g.sweep(1)
+        o.sweep(1)
+        assert_state(g, o)
+    g.sweep(5)
+    o.sweep(5)
+    assert_state(g, o)
