@@ -34,8 +34,8 @@ FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X FP32 matrix peak (MI355X_MICROARCH.md: 1
 HBM_PEAK_GBS = 8000.0
 # committed rocprofv3 PMC summaries of the assign kernels (HBM bytes per launch, tools/prof*.sh)
 C3_TRAFFIC = "traffic_r05_c3.json"
-C5_TRAFFIC = "traffic_r05_c5.json"
-C5_CONJ_TRAFFIC = "traffic_r05_c5conj.json"  # PMC pass of the niw_conjugate C5 sweep (its assign reads more candidate rows than the frozen one)
+C5_TRAFFIC = "traffic_r05g_c5.json"
+C5_CONJ_TRAFFIC = "traffic_r05g_c5conj.json"  # PMC pass of the niw_conjugate C5 sweep (its assign reads more candidate rows than the frozen one)
 MIXED_TRAFFIC = "traffic_r05_mixed_head.json"  # PMC pass of the mixed regime (tools/prof_mixed.sh, tools/summarize_profile.py)
 
 

@@ -82,7 +82,6 @@ struct np8_ctx {
     float *wA = nullptr, *wfrag = nullptr, *wmu = nullptr;
     int32_t *wdirty = nullptr;
     double *lam_lo = nullptr, *wdist = nullptr;  // wide-path candidate pruning (np8_wide_dist)
-    double *wnx = nullptr;  // wide path: per local item (|U^T (x - mu0)|, |x|^2), np8_wide_frame at np8_set_data
     bool screen16 = false;  // wide path: every item's |x|^2 <= kScreen16X2 (the fp16 exact-distance screen, AssignArgs)
     double *acc = nullptr;  // [kcap][D + DP] parameter-update statistics
     // wide path, one rank, niw_conjugate: np8_suffstats_wide's run records (reduced by np8_niw_post, no atomics)
@@ -517,14 +516,14 @@ bool slot_from_sigma(const np8_ctx *c, const double *mu, const double *Sigma, Sl
 
 void free_device(np8_ctx *c) {
     void *niw_ptrs[] = {c->d_U, c->d_Uinv, c->d_Psi0, c->pend, c->wA, c->wfrag, c->wmu, c->wdirty, c->lam_lo, c->wdist,
-                        c->pend_ll, c->wnx};
+                        c->pend_ll};
     for (void *p : niw_ptrs)
         if (p) (void)hipFree(p);
     c->d_U = c->d_Uinv = c->d_Psi0 = nullptr;
     c->pend = c->pend_ll = nullptr;
     c->wA = c->wfrag = c->wmu = nullptr;
     c->wdirty = nullptr;
-    c->lam_lo = c->wdist = c->wnx = nullptr;
+    c->lam_lo = c->wdist = nullptr;
     void *ptrs[] = {c->X,      c->z,       c->z_best, c->slot_mu, c->slot_P,  c->slot_c,  c->slot_sigma,
                     c->cnt,    c->cnt_best, c->mu_best, c->sigma_best, c->cand, c->ctl,    c->hyp,
                     c->d_mu0,  c->d_LT,    c->d_Gp,   c->d_LTL,   c->rec,     c->gath,    c->order,
@@ -930,7 +929,6 @@ AssignArgs assign_args(np8_ctx *c, int64_t p0, int64_t p1, const int64_t *order,
     A.lam_lo = c->lam_lo;
     A.dim = c->D;
     A.uw = c->wide ? c->hyp + c->uw_off : nullptr;
-    A.wnx = c->wnx;
     A.screen16 = c->screen16 ? 1 : 0;
     A.wdist = nullptr;  // set by launch_assign on the wide path (after np8_wide_dist)
     A.queue = A.queue_out = A.qcount = A.qlist = nullptr;
@@ -1189,7 +1187,7 @@ int launch_resort(np8_ctx *c, bool stale) {
     S.kcap = c->kcap;
     S.D = c->D;
     S.esz = c->wide ? 4 : 8;
-    if (c->wide) S.D = c->DT;  // (the wide path's item rows: DT, zero beyond D)
+    if (c->wide) S.D = c->DT + kFrameRows;  // (the wide path's item rows: DT, zero beyond D, then the item's frame)
     S.nsub = c->substeps;
     S.pad = 0;
     S.offset = c->offset;
@@ -2012,15 +2010,14 @@ int np8_set_data(np8_ctx *c, const double *X, int64_t n, int32_t D, int64_t offs
     if (c->substeps_auto)  // (n_global only: the same choice on every rank)
         c->substeps = n_global <= NP8_SUBSTEPS_AUTO_N ? std::max(1, std::min(NP8_SUBSTEPS_AUTO_S, 16384 / c->kcap)) : 1;
     int r = 0;
-    // wide path: fp32 items in DT rows (zero beyond D)
-    const size_t nx = c->wide ? ((size_t)n * c->DT + 1) / 2 : (size_t)n * D;
+    // wide path: fp32 items in DT rows (zero beyond D), then kFrameRows rows of the item's frame (np8_wide_frame)
+    const size_t nx = c->wide ? ((size_t)n * (c->DT + kFrameRows) + 1) / 2 : (size_t)n * D;
     if ((r = dalloc(c, &c->X, nx)) || (r = dalloc(c, &c->z, (size_t)n)) ||
         (r = dalloc(c, &c->z_best, (size_t)n)) || (r = dalloc(c, &c->wr2, (size_t)((n + 63) / 64))) ||
         (r = dalloc(c, &c->llpart, (size_t)((n + 63) / 64))) ||
         (c->wide && c->param_update == NP8_PARAM_NIW_CONJUGATE &&
          ((r = dalloc(c, &c->part, (size_t)(np8_suffstats_wide_waves(n) * kSuffRuns * np8_suffstats_wide_record(D)))) ||
           (r = dalloc(c, &c->part_slot, (size_t)(np8_suffstats_wide_waves(n) * kSuffRuns))))) ||
-        (c->wide && (r = dalloc(c, &c->wnx, (size_t)2 * n))) ||
         (r = dalloc(c, &c->queue, (size_t)(64 * ((n + 63) / 64) + 64))) ||
         (r = dalloc(c, &c->qcount, (size_t)((n + 63) / 64 + 1))) ||
         (r = dalloc(c, &c->qlist, (size_t)((n + 63) / 64 + 1))))
@@ -2056,7 +2053,7 @@ int np8_set_data(np8_ctx *c, const double *X, int64_t n, int32_t D, int64_t offs
         }
         c->screen16 = x2max <= kScreen16X2 && std::getenv("NP8_SCREEN_F32") == nullptr;  // (NaN: false; env: A/B switch)
         HIPC(c, hipMemcpyAsync(c->X, soa.data(), sizeof(float) * soa.size(), hipMemcpyHostToDevice, c->stream));
-        HIPC(c, np8_launch_wide_frame(reinterpret_cast<const float *>(c->X), n, c->hyp + c->uw_off, c->DT, c->wnx,
+        HIPC(c, np8_launch_wide_frame(reinterpret_cast<float *>(c->X), n, c->hyp + c->uw_off, c->DT,
                                       c->stream));
         HIPC(c, hipStreamSynchronize(c->stream));
     } else {

@@ -222,7 +222,6 @@ struct AssignArgs {
     int32_t dim = 0;           // wide path: the data's D (the kernels are instantiated for DT = D rounded up to 16; the
                                // item rows, factors and means beyond D are zero)
     const double *uw = nullptr;  // wide path: mu0 [DT] | U^T packed [DT (DT + 1) / 2], zero beyond D (the item frame)
-    const double *wnx = nullptr; // wide path: per local item, (|U^T (x - mu0)|, |x|^2) (np8_wide_frame, once per data set)
     int32_t screen16 = 0;        // wide path: the exact-distance screen's dot products in fp16 (every |x|^2 <= kScreen16X2)
     int32_t pad_s16 = 0;
     const double *wdist;       // [K][kcap] distances between row means (np8_wide_dist); null: no pruning
@@ -556,6 +555,10 @@ constexpr int kMaxListGroups = 3;
 // the wide path's fp16 exact-distance screen: for data with every |x|^2 at most this (its margin, 2e-3 (|x|^2 + |muf|^2),
 // stays small against the distances between clusters; larger data keep the fp32 screen, margin 1e-5 (...))
 constexpr double kScreen16X2 = 4096.0;
+// the wide path's item rows carry, after the DT fp32 rows, the item's frame (|U^T (x - mu0)|, |x|^2) as two doubles in
+// four 32-bit rows (low, high word each): computed once per data set (np8_wide_frame) and moved with the item by the
+// layout's sort, so the assign reads it coalesced at the item's position
+constexpr int kFrameRows = 4;
 constexpr int kSuffRuns = 4;  // run records per wave of np8_suffstats_wide
 
 struct SnapArgs {
@@ -597,8 +600,8 @@ struct SortArgs {
 bool np8_supported(int D, int M);
 bool np8_wide_supported(int D, int M);
 hipError_t np8_launch_assign_wide(const np8::AssignArgs &A, int D, int M, int prior, hipStream_t s);
-// the wide path's per-item frame (AssignArgs::wnx) over the fp32 items X [DT][n] and uw (AssignArgs::uw)
-hipError_t np8_launch_wide_frame(const float *X, int64_t n, const double *uw, int DT, double *wnx, hipStream_t s);
+// the wide path's per-item frame over the fp32 items X [DT][n] and uw (AssignArgs::uw), into X's kFrameRows rows
+hipError_t np8_launch_wide_frame(float *X, int64_t n, const double *uw, int DT, hipStream_t s);
 // Wide-path pruning: the distance table of the current dense rows (after every table change).
 hipError_t np8_launch_wide_dist(const np8::WideArgs &W, hipStream_t s);
 hipError_t np8_launch_loglik_matrix_wide(const np8::AssignArgs &A, const np8::WideArgs &W, int D, int M, int prior,

@@ -1182,9 +1182,9 @@ __global__ __launch_bounds__(kSortThreads) void np8_sort_scatter(SortArgs S) {
         const int64_t q = (int64_t)S.off[zp[k]] + lbase[zp[k]] + rk[k];
         zo[q] = z[p];
         ido[q] = ids ? ids[p] : (int32_t)p;
-        if (S.esz == 4) {  // wide path: fp32 items
-            const float *Xf = reinterpret_cast<const float *>(X);
-            float *Xfo = reinterpret_cast<float *>(Xo);
+        if (S.esz == 4) {  // wide path: fp32 items and the frame's words, copied as bits
+            const uint32_t *Xf = reinterpret_cast<const uint32_t *>(X);
+            uint32_t *Xfo = reinterpret_cast<uint32_t *>(Xo);
             for (int a = 0; a < S.D; ++a) Xfo[(int64_t)a * S.n + q] = Xf[(int64_t)a * S.n + p];
         } else {
             for (int a = 0; a < S.D; ++a) Xo[(int64_t)a * S.n + q] = X[(int64_t)a * S.n + p];

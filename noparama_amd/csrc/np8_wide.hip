@@ -493,8 +493,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NP8_WIDE_WA
     const int32_t jo = A.dense_of[zi];
 
     // the item's frame for the auxiliaries (|U^T (x - mu0)|) and |x|^2 (the exact distance screen): per item, once
-    // per data set (np8_wide_frame) -- a general U^T's D (D + 1) / 2 products per lane stay out of the sweep
-    const double ny = A.wnx[2 * il], x2 = A.wnx[2 * il + 1];
+    // per data set (np8_wide_frame, the kFrameRows rows after the item's DT rows) -- a general U^T's D (D + 1) / 2
+    // products per lane stay out of the sweep
+    const uint32_t *fr = reinterpret_cast<const uint32_t *>(X) + (int64_t)DT * n + xr;
+    const double ny = __hiloint2double((int)fr[n], (int)fr[0]), x2 = __hiloint2double((int)fr[3 * n], (int)fr[2 * n]);
     double rown = 0.0;  // |x - muf_own| (candidate pruning)
     if (A.wdist) {
         const float *mo = A.wmu + (int64_t)zi * DT;
@@ -1277,11 +1279,10 @@ hipError_t np8_launch_assign_wide(const AssignArgs &A, int D, int M, int prior, 
     return hipErrorInvalidValue;
 }
 
-// The per-item frame of the wide assign (AssignArgs::wnx): |U^T (x - mu0)| (wide_whiten_norm, the fully unrolled
-// triangular product) and |x|^2, one thread per item, once per data set.
+// The per-item frame of the wide assign (kFrameRows): |U^T (x - mu0)| (wide_whiten_norm, the fully unrolled triangular
+// product) and |x|^2, one thread per item, once per data set, into the four 32-bit rows after the item's DT rows.
 template <int DT>
-__global__ __launch_bounds__(256) void np8_wide_frame(const float *__restrict__ X, int64_t n,
-                                                      const double *__restrict__ uw, double *__restrict__ wnx) {
+__global__ __launch_bounds__(256) void np8_wide_frame(float *__restrict__ X, int64_t n, const double *__restrict__ uw) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     float xf[DT];
@@ -1291,16 +1292,19 @@ __global__ __launch_bounds__(256) void np8_wide_frame(const float *__restrict__ 
     double x2 = 0.0;
 #pragma unroll
     for (int a = 0; a < DT; ++a) x2 = fma((double)xf[a], (double)xf[a], x2);  // (rows >= D: + 0)
-    wnx[2 * i] = ny;
-    wnx[2 * i + 1] = x2;
+    uint32_t *fr = reinterpret_cast<uint32_t *>(X) + (int64_t)DT * n + i;
+    fr[0] = (uint32_t)__double2loint(ny);
+    fr[n] = (uint32_t)__double2hiint(ny);
+    fr[2 * n] = (uint32_t)__double2loint(x2);
+    fr[3 * n] = (uint32_t)__double2hiint(x2);
 }
 
-hipError_t np8_launch_wide_frame(const float *X, int64_t n, const double *uw, int DT, double *wnx, hipStream_t s) {
+hipError_t np8_launch_wide_frame(float *X, int64_t n, const double *uw, int DT, hipStream_t s) {
     if (n <= 0) return hipSuccess;
     const dim3 grid((unsigned)((n + 255) / 256)), block(256);
 #define X(d, m)                                                                                     \
     if (DT == d) {                                                                                  \
-        hipLaunchKernelGGL((np8_wide_frame<d>), grid, block, 0, s, X, n, uw, wnx);                  \
+        hipLaunchKernelGGL((np8_wide_frame<d>), grid, block, 0, s, X, n, uw);                       \
         return hipGetLastError();                                                                   \
     }
     NP8_WIDE_FOR_EACH(X)
