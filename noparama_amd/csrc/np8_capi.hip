@@ -130,7 +130,7 @@ struct np8_ctx {
     Fx *llpart = nullptr;        // [waves]
     bool llfold_off = false;
     bool step_ll = false;        // the running step folds the check in
-    bool wide_llfold = false;    // NP8_WIDE_LLFOLD=1: the wide path folds it too (slower at C5, see launch_assign)
+    bool wide_llfold = true;     // the wide path folds it too (NP8_WIDE_LLFOLD=0: the separate pass, see launch_assign)
     bool step_snap = false;      // the running step's assign consumes a pending snapshot
     bool sweep_ll = false;       // this sweep's check was folded into its step
     bool snap_lazy = false;
@@ -1082,9 +1082,10 @@ int launch_assign(np8_ctx *c, int64_t p0, int64_t p1, const int64_t *order, bool
                        !c->queue_on && (c->world == 1 || c->comm) && !c->host_exch_step;
     // the wide path folds it too (one rank, the whole step on the label-sorted layout, a diagonal base-measure frame):
     // np8_ll_fix_wide completes the sum once the accepted requests' slots exist
-    // Off by default: measured at C5 (one box, 40 sweeps) the folded instance takes 0.33 ms against 0.22 for the plain
-    // one, more than the separate np8_loglik_wide_mfma pass it replaces (0.09 ms): 3 543 vs 3 649 sweeps/s.
-    // NP8_WIDE_LLFOLD=1 turns it on (it stays bit-exact: tests/test_gpu_wide.py runs it).
+    // On by default since the per-item frame and the fp16 screen (late round 5): C5 frozen 4 312-4 323 sweeps/s folded
+    // vs 4 091-4 122 with the separate np8_loglik_wide_mfma pass (0.09 ms every 5th sweep), A/B on one box; before them
+    // the folded instance lost (3 543 vs 3 649).  NP8_WIDE_LLFOLD=0 keeps the separate pass (tests/test_gpu_fold.py
+    // compares the two).
     const bool wide_fold = c->wide_llfold && c->wide && c->diag_U && c->substeps == 1 && p0 == 0 && p1 == c->n_loc &&
                            !order && !use_perm && A.sorted && c->world == 1 && !c->comm && !A.count_eval;
     c->step_ll = (whole || wide_fold) && !c->llfold_off && c->param_update == NP8_PARAM_FROZEN &&
@@ -1859,7 +1860,7 @@ int np8_create_sized(np8_ctx **out, const np8_config *cfg_in, size_t cfg_bytes) 
         }
     }
     c->llfold_off = std::getenv("NP8_NO_LLFOLD") != nullptr;
-    c->wide_llfold = std::getenv("NP8_WIDE_LLFOLD") != nullptr && std::getenv("NP8_WIDE_LLFOLD")[0] == '1';
+    c->wide_llfold = !(std::getenv("NP8_WIDE_LLFOLD") != nullptr && std::getenv("NP8_WIDE_LLFOLD")[0] == '0');
     c->niw_valu = std::getenv("NP8_NIW_VALU") != nullptr;
     if (const char *cr = std::getenv("NP8_CHURN_RESORT")) {  // (A/B runs: 1, 2, 4, 5, 10 or 20)
         const int v = atoi(cr);

@@ -92,14 +92,14 @@ def test_fold_against_oracle_cold_start():
 
 
 @pytest.mark.parametrize("D", [40, 64])
-def test_wide_fold_opt_in_transparent(D):
-    """The wide path's folded check (NP8_WIDE_LLFOLD=1: np8_assign_wide sums the items' log-likelihoods per wave,
-    np8_ll_fix_wide moves the accepted requesters) against the default separate np8_loglik_wide_mfma pass: labels,
+def test_wide_fold_transparent(D):
+    """The wide path's folded check (the default: np8_assign_wide sums the items' log-likelihoods per wave,
+    np8_ll_fix_wide moves the accepted requesters) against the separate np8_loglik_wide_mfma pass (NP8_WIDE_LLFOLD=0): labels,
     counts and the snapshot bit-exact, the best log-likelihood within 1e-11 relative, through eager sweeps and a
     graph replay from init_random (new clusters every early sweep)."""
     X, _, _, _ = datasets.mixture(12_000, D, 12, 1.0, 5.0, seed=9)
     kw = dict(prior="niw", contraction="f32", mu0=np.full(D, 6.0), kappa=0.01, nu=D + 2.0, Lambda=np.eye(D))
-    runs = [make({"NP8_WIDE_LLFOLD": "1"}, D, 13, **kw), make({}, D, 13, **kw)]
+    runs = [make({}, D, 13, **kw), make({"NP8_WIDE_LLFOLD": "0"}, D, 13, **kw)]
     for s in runs:
         s.set_data(X)
         s.init_random(20)
