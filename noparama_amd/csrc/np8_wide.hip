@@ -664,12 +664,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NP8_WIDE_WA
         if (wave_live && n1 > 0) {
             using W2 = Wide<DT>;
             const double Tl = valid ? st.T : 1e300;
-            double Ti[4], x2i[4];
+            // a pair (row j, item i) stays skippable when U = base_j - lam_j/2 d^2 - T_i <= -kSkip - 2 - 1e-9 (|base_j| +
+            // |T_i| + lam_j/2 d^2), d^2 = max(sq - 2 x.muf - (mA sq + mB), 0), evaluated as
+            // fma(lam_j/2 (1 - 1e-9), d^2, Tm_i) >= base_j + 1e-9 |base_j| with Tm_i = T_i - kSkip - 2 - 1e-9 |T_i| and
+            // sq (1 - mA) - mB = x2m_i + m2m_j: the same inequality, its per-item and per-row terms formed once (the
+            // rounding of the regrouping is far inside the 1e-9 slack); lanes past the end (T = 1e300) never keep a row
+            const double mA = h16 ? 2e-3 : 1e-5, mB = h16 ? 1e-3 : 0.0;
+            double Tm[4], x2m[4];
             int32_t zit[4];
 #pragma unroll
             for (int nt = 0; nt < 4; ++nt) {
-                Ti[nt] = __shfl(Tl, 16 * nt + col);
-                x2i[nt] = __shfl(x2, 16 * nt + col);
+                const double Ti = __shfl(Tl, 16 * nt + col);
+                Tm[nt] = Ti - kSkip - 2.0 - 1e-9 * fabs(Ti);
+                x2m[nt] = __shfl(x2, 16 * nt + col) * (1.0 - mA);
                 zit[nt] = __shfl(zi, 16 * nt + col);
             }
             // A operand: lane (g, col) holds muf[4 s + g] of row list[b0 + col] (the transposed mean of its row)
@@ -735,15 +742,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NP8_WIDE_WA
                     bool nr = false;
                     if (jr < K) {
                         const int32_t sjr = rslot[jr];
-                        const double base = rbase[jr], lamh = rlamh[jr];
+                        const double base = rbase[jr];
+                        const double Bp = base + 1e-9 * fabs(base), lamp = rlamh[jr] * (1.0 - 1e-9);
+                        const double m2m = fma(m2r, 1.0 - mA, -mB);
+                        // fp16: |x|^2 <= 4096, so sq > 1e8 (overflow possible) implies |muf|^2 > 5e7: not screened
+                        const bool rowbig = h16 && !(m2r <= 5e7);
 #pragma unroll
                         for (int nt = 0; nt < 4; ++nt) {
-                            if (sjr != zit[nt] && Ti[nt] < 1e299) {
-                                const double sq = x2i[nt] + m2r;
-                                const double d2 = fmax(fma(-2.0, (double)acc[nt][r], sq) - (h16 ? 2e-3 * sq + 1e-3 : 1e-5 * sq), 0.0);
-                                const double far = lamh * d2;
-                                const double U = base - far - Ti[nt];
-                                nr = nr || (h16 && !(sq <= 1e8)) || !(U <= -kSkip - 2.0 - 1e-9 * (fabs(base) + fabs(Ti[nt]) + far));
+                            if (sjr != zit[nt]) {
+                                const double d2 = fmax(fma(-2.0, (double)acc[nt][r], x2m[nt] + m2m), 0.0);
+                                nr = nr || rowbig || !(fma(lamp, d2, Tm[nt]) >= Bp);
                             }
                         }
                     }
