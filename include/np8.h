@@ -88,7 +88,11 @@ typedef struct {
  * memory read or written past the struct it allocated.  Use NP8_CREATE / NP8_STATS, which pass sizeof of the
  * caller's own struct.  The unsized forms: np8_create reads sizeof(np8_config) of this header (callers built
  * against this header only); np8_stats writes the first NP8_STATS_MIN_BYTES (the first, smallest layout ever
- * shipped: K .. last_loglik) and nothing beyond, whatever header the caller was built with. */
+ * shipped: K .. last_loglik) and nothing beyond, whatever header the caller was built with.
+ * BEHAVIOUR CHANGE (round 5): a binary built against the round-4 header that calls the unsized np8_stats and reads
+ * ms_assign .. pick_evals now finds those fields untouched (the library cannot tell a round-3 struct from a
+ * round-4 one, and writing the round-4 layout overran round-3 callers).  Such callers must zero their struct
+ * before the call or move to NP8_STATS; INTEGRATION.md "ABI growth" says the same. */
 #define NP8_CONFIG_MIN_BYTES offsetof(np8_config, param_update) /* D .. device: the first released layout */
 
 /* Cluster-likelihood arithmetic (DESIGN.md "Wide path").
@@ -203,7 +207,11 @@ int np8_init_random(np8_ctx *ctx, int32_t K_init);
 
 /* n full sweeps (np_mcmc.cpp:109-175 with the population update of np_neal_algorithm8.cpp:49-167),
  * including the max-likelihood check every 5th sweep (np_mcmc.cpp:172-174).  Asynchronous on the
- * context's stream; errors raised on the device are reported by the next np8_sync(). */
+ * context's stream; errors raised on the device are reported by the next np8_sync().
+ * With an RCCL communicator (np8_comm_init) np8_sweep is collective -- every rank calls it with the same n --
+ * and returns once its last sweep graph is settled (a replay that halted on a compact record is resumed inside
+ * the call), so the other entry points never run collectives: one rank may alone ask for statistics, the state
+ * or a checkpoint.  Every rank of a communicator needs at least one item. */
 int np8_sweep(np8_ctx *ctx, int32_t n_sweeps);
 /* Prepares the next np8_sweep(ctx, n_sweeps) without running anything: captures and uploads the
  * 20-sweep graph it would replay (whole synchronous sweeps on one rank), so that capture and
@@ -350,6 +358,21 @@ int np8_comm_init(np8_ctx *ctx, const uint8_t id[128], int32_t rank, int32_t wor
 int64_t np8_record_bytes(np8_ctx *ctx);
 int np8_step_local(np8_ctx *ctx, void *record_out);
 int np8_step_merge(np8_ctx *ctx, const void *records, int32_t world);
+
+/* Compact records over the caller's transport: the exchange an RCCL sweep graph runs, step by step.
+ * np8_step_local_compact writes this rank's compact record (np8_compact_record_bytes() bytes: the count deltas and
+ * the first NP8_COMPACT_REQ requests, its header counting all of them); the caller all-gathers them in rank order;
+ * np8_step_merge_compact applies them, or -- when some rank's requests did not fit its compact record, which every
+ * rank sees alike in the gathered headers -- applies nothing and sets *halted = 1.  After a halt every rank calls
+ * np8_step_resume (this rank's full record of the same step, np8_record_bytes() bytes), the caller all-gathers those
+ * and calls np8_step_merge as after np8_step_local.  The chain is the full records' chain bit for bit.
+ * np8_compact_record_bytes() is 0 where the step cannot use them (the wide path, the NIW prior, rows that are not
+ * isotropic, NP8_COMPACT_REQ=0, or a context without the host transport): use np8_step_local there.
+ * Replaces, for the sharded sweep, the per-point exchange-free loop of np_mcmc.cpp:146-164. */
+int64_t np8_compact_record_bytes(np8_ctx *ctx);
+int np8_step_local_compact(np8_ctx *ctx, void *record_out);
+int np8_step_merge_compact(np8_ctx *ctx, const void *records, int32_t world, int32_t *halted);
+int np8_step_resume(np8_ctx *ctx, void *record_out);
 
 /* Host-exchange form of the cluster-parameter update (param_update != FROZEN): after the sweep's
  * np8_step_merge, np8_param_stats_local writes this rank's per-cluster statistics (np8_param_stats_bytes()

@@ -228,6 +228,9 @@ struct np8_ctx {
     int c_cap = 32;            // NP8_COMPACT_REQ (0: full records always)
     bool compact_on = false;   // the next captured sharded graph exchanges compact records (policy, alike on all ranks)
     bool compact_step = false; // the step being launched does
+    bool host_compact = false; // np8_step_local_compact's assign (the host transport's compact step)
+    bool host_cstep = false;   // ... its record awaits np8_step_merge_compact
+    bool host_halted = false;  // ... which halted: np8_step_resume writes the step's full record
     bool graph_compact = false;
     int32_t *mirror_host = nullptr, *mirror_dev = nullptr;  // host-mapped [kMirrorInts] (np8::FinArgs::mirror)
     std::vector<HostSnap> graph_snaps, cap_snaps;
@@ -629,12 +632,13 @@ int alloc_records(np8_ctx *c) {
         (void)hipFree(c->stage);
         c->stage = nullptr;
     }
-    // compact records of the RCCL path's sweep graphs (the same layout with c_cap requests)
-    if (c->comm && c->c_cap > 0 && !c->wide) {
+    // compact records of the RCCL path's sweep graphs (the same layout with c_cap requests), and of the host
+    // transport's compact steps (np8_step_local_compact)
+    if (exch && c->c_cap > 0 && !c->wide) {
         c->c_bytes = record_bytes(c->kcap, c->c_cap, c->D);
         if ((r = dalloc(c, &c->crec, (size_t)c->c_bytes)) || (r = dalloc(c, &c->cgath, (size_t)c->c_bytes * c->world)))
             return r;
-        c->compact_on = true;
+        c->compact_on = c->comm != nullptr;
     }
     return NP8_OK;
 }
@@ -1100,8 +1104,9 @@ int launch_assign(np8_ctx *c, int64_t p0, int64_t p1, const int64_t *order, bool
     A.snap_on = c->step_snap ? 1 : 0;
     // compact exchange: a whole frozen step of a captured sharded graph with the folded check (every kernel such a
     // graph holds does nothing once a step halts it)
-    c->compact_step = whole && c->comm && c->capturing && c->compact_on && c->crec && c->fp_off &&
-                      c->param_update == NP8_PARAM_FROZEN && !c->llfold_off && c->gp_iso > 0.0 && c->llpart;
+    c->compact_step = (whole && c->comm && c->capturing && c->compact_on && c->crec && c->fp_off &&
+                       c->param_update == NP8_PARAM_FROZEN && !c->llfold_off && c->gp_iso > 0.0 && c->llpart) ||
+                      c->host_compact;  // (np8_step_local_compact checked that the lean kernel takes every lane)
     if (c->compact_step) {
         A.compact = 1;
         A.rec = c->crec;  // the count deltas; requests to the staging area and the first c_cap also to crec
@@ -1250,7 +1255,12 @@ int step(np8_ctx *c, int64_t p0, int64_t p1, const int64_t *order, bool use_perm
             HIPC(c, hipMemsetAsync(c->r2, 0, sizeof(double) * c->kcap, c->stream));
             c->r2_zero = true;
         }
-        if (c->gather && !cleared) HIPC(c, hipMemsetAsync(c->r2 + c->kcap, 0, sizeof(double) * c->kcap, c->stream));
+        if (c->gather && !cleared) {
+            if (c->capturing && c->comm)  // a sharded graph: a later sweep of a halted replay must not clear them
+                HIPC(c, np8_launch_clear_unless_halted(c->r2 + c->kcap, c->kcap, c->ctl, c->stream));
+            else
+                HIPC(c, hipMemsetAsync(c->r2 + c->kcap, 0, sizeof(double) * c->kcap, c->stream));
+        }
     }
     int r = launch_assign(c, p0, p1, order, use_perm);
     if (r) return r;
@@ -2202,12 +2212,18 @@ int np8_sweep(np8_ctx *c, int32_t n_sweeps) {
     int64_t chunk = (c->chunk <= 0 || c->chunk >= c->n_glob) ? N : c->chunk;
     const bool sync = chunk >= N;
     if (!sync && c->world > 1) return fail(c, NP8_ERR_ARG, "np8_sweep: chunk < N is single-rank only");
+    if (c->comm && c->world > 1 && N == 0)  // (its peers would replay graphs it cannot capture)
+        return fail(c, NP8_ERR_ARG, "np8_sweep: every rank of a communicator needs at least one item");
     if (n_sweeps <= 0) return NP8_OK;
     int r = settle(c);
     if (r) return r;
     const uint32_t target = c->epoch + (uint32_t)n_sweeps;
     while ((int32_t)(target - c->epoch) > 0) {
-        if (c->moved_host) {  // churn (moved since the last re-sort, as of the last finalize): enter > n/8, leave < n/64
+        // churn (moved since the last re-sort, as of the last finalize): enter > n/8, leave < n/64.  Not under a
+        // communicator: the mirror is this rank's own count, read while a replay runs, and churn selects the graph --
+        // whether the pending replay is settled before or after the next one is queued must be alike on every rank
+        // (the settle of a halted replay runs collectives), so a sharded context decides from rank-uniform state only
+        if (c->moved_host && !c->comm) {
             const int64_t mv = *(volatile int64_t *)c->moved_host;
             c->churn = c->churn ? (mv * 64 >= c->n_loc) : (mv * 8 > c->n_loc);
         }
@@ -2219,6 +2235,8 @@ int np8_sweep(np8_ctx *c, int32_t n_sweeps) {
         }
         if (can_graph) {
             if ((r = ensure_graph(c))) return r;
+            if (!c->graph && c->comm)  // (a capture failed on this rank only: its peers replay graphs)
+                return fail(c, NP8_ERR_HIP, "np8_sweep: a sharded sweep graph could not be captured");
             if (c->graph) {
                 if (c->graph_sort_outside && (*(volatile int64_t *)c->moved_host) * 32 > c->n_loc) {
                     // the layout went stale (as of a replay ago): re-sort before this one (the device re-checks)
@@ -2252,6 +2270,10 @@ int np8_sweep(np8_ctx *c, int32_t n_sweeps) {
         if ((r = population(c))) return r;
         if ((r = end_sweep(c))) return r;
     }
+    // a sharded context returns with its last replay settled (a halted one resumed here, where every rank is), so
+    // that no other entry point has collectives to run: a rank that alone asks for statistics or a checkpoint must
+    // not block in an all-gather its peers never join
+    if (c->comm && c->pend_on && (r = settle(c))) return r;
     return NP8_OK;
 }
 
@@ -2903,6 +2925,90 @@ int np8_step_merge(np8_ctx *c, const void *records, int32_t world) {
     if (r) return r;
     HIPC(c, hipStreamSynchronize(c->stream));
     return NP8_OK;
+}
+
+// ---- compact records over the caller's transport ---------------------------------------
+// The exchange an RCCL sweep graph runs, step by step over MPI / gloo: the compact record (count deltas and the
+// first c_cap requests, its header counting all of them), the halt decision np8_finalize takes from the gathered
+// headers (alike on every rank), and the resumption of a halted step with the full records.
+namespace {
+// the lean kernel takes every lane of the step (no deferred lane, no queue launch) and writes the compact record
+bool host_compact_ok(const np8_ctx *c) {
+    return c->crec && !c->comm && c->world > 1 && !c->wide && c->diag_U && !c->fast_off &&
+           c->prior == NP8_PRIOR_REFERENCE && c->rows_iso && !c->count_eval && !c->queue_on && c->n_loc > 0;
+}
+}  // namespace
+
+int64_t np8_compact_record_bytes(np8_ctx *c) { return (c && host_compact_ok(c)) ? c->c_bytes : 0; }
+
+int np8_step_local_compact(np8_ctx *c, void *record_out) {
+    if (!c || !record_out) return NP8_ERR_ARG;
+    if (!c->have_state) return fail(c, NP8_ERR_STATE, "np8_step_local_compact: no state");
+    if (!host_compact_ok(c))
+        return fail(c, NP8_ERR_STATE, "np8_step_local_compact: no compact records here (np8_compact_record_bytes() == 0)");
+    if (c->host_halted) return fail(c, NP8_ERR_STATE, "np8_step_local_compact: a halted step awaits np8_step_resume");
+    const int sub = c->sub_next;
+    const int64_t p0 = c->sub_start[(size_t)sub], p1 = c->sub_start[(size_t)sub + 1];
+    c->use_sorted = true;
+    if (sub == 0) {
+        int r0 = prepare_sorted(c);
+        if (r0) return r0;
+    }
+    c->collecting = false;  // no pruning on the host-exchange path
+    c->lists_valid = c->r2_zero = false;
+    c->host_exch_step = true;
+    c->host_compact = true;
+    int r = launch_assign(c, p0, p1, nullptr, false);
+    c->host_exch_step = c->host_compact = false;
+    c->compact_step = false;
+    if (r) return r;
+    HIPC(c, hipMemcpyAsync(record_out, c->crec, (size_t)c->c_bytes, hipMemcpyDeviceToHost, c->stream));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    c->host_cstep = true;
+    return NP8_OK;
+}
+
+int np8_step_merge_compact(np8_ctx *c, const void *records, int32_t world, int32_t *halted) {
+    if (!c || !records || !halted || world < 1) return NP8_ERR_ARG;
+    if (world != c->world) return fail(c, NP8_ERR_ARG, "np8_step_merge_compact: world differs from np8_comm_init");
+    if (!c->host_cstep) return fail(c, NP8_ERR_STATE, "np8_step_merge_compact: no np8_step_local_compact step pending");
+    c->host_cstep = false;
+    HIPC(c, hipMemcpyAsync(c->cgath, records, (size_t)c->c_bytes * world, hipMemcpyHostToDevice, c->stream));
+    c->compact_step = true;  // (fin_args: the gathered compact records, their capacity, the local compact record)
+    int r = launch_finalize(c, c->cgath, world);
+    c->compact_step = false;
+    if (r) return r;
+    Ctl h;
+    if ((r = read_ctl(c, &h))) return r;
+    *halted = h.halt ? 1 : 0;
+    if (!h.halt) {
+        c->sub_next = (c->sub_next + 1) % c->substeps;
+        return NP8_OK;
+    }
+    // some rank's requests did not fit its compact record: np8_finalize applied nothing; this step's full record
+    // comes from the deltas the assign wrote into the compact record and every request of the staging area
+    // (as recover_halt prepares it for the RCCL path)
+    HIPC(c, hipMemsetD32Async(reinterpret_cast<int *>(&c->ctl->halt), 0, 1, c->stream));
+    HIPC(c, hipMemcpyAsync(c->rec + kRecHeaderBytes, c->crec + kRecHeaderBytes, 4ull * c->kcap, hipMemcpyDeviceToDevice,
+                           c->stream));
+    HIPC(c, hipMemcpyAsync(&reinterpret_cast<RecHeader *>(c->stage)->nreq, &reinterpret_cast<RecHeader *>(c->crec)->nreq,
+                           sizeof(int32_t), hipMemcpyDeviceToDevice, c->stream));
+    HIPC(c, hipMemsetAsync(c->crec, 0, kRecHeaderBytes + 4ull * c->kcap, c->stream));
+    c->n_halts += 1;
+    c->host_halted = true;
+    HIPC(c, hipStreamSynchronize(c->stream));
+    return NP8_OK;
+}
+
+int np8_step_resume(np8_ctx *c, void *record_out) {
+    if (!c || !record_out) return NP8_ERR_ARG;
+    if (!c->host_halted) return fail(c, NP8_ERR_STATE, "np8_step_resume: no halted compact step");
+    c->host_halted = false;
+    HIPC(c, np8_launch_req_select(c->stage, c->stage_cap, c->rec, c->rec_cap, c->kcap, c->D, c->req_max, nullptr, 0,
+                                  c->stream));
+    HIPC(c, hipMemcpyAsync(record_out, c->rec, (size_t)c->rec_bytes, hipMemcpyDeviceToHost, c->stream));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    return NP8_OK;  // then the full records' all-gather and np8_step_merge, as after np8_step_local
 }
 
 // ---- Jain-Neal split-merge (np8_sm.hip; DESIGN.md "Split-merge") ------------------------------------

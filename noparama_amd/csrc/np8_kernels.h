@@ -676,6 +676,8 @@ hipError_t np8_launch_mh_g0(const np8::ParamArgs &A, hipStream_t s);
 hipError_t np8_launch_advance_epoch(np8::Ctl *ctl, uint32_t n, hipStream_t s);
 // ctl->best_sorted (which = 0) or ctl->snap_pend (1) = 0 in stream order, unless a compact sweep graph is halted
 hipError_t np8_launch_ctl_clear(np8::Ctl *ctl, int which, hipStream_t s);
+// p[0..n) = 0 in stream order, unless a compact sweep graph is halted (the captured form of a memset)
+hipError_t np8_launch_clear_unless_halted(double *p, int n, const np8::Ctl *ctl, hipStream_t s);
 hipError_t np8_launch_prune(const np8::PruneArgs &A, int kcap, hipStream_t s);
 hipError_t np8_launch_fin_prune(const np8::FinArgs &F, const np8::PruneArgs &P, hipStream_t s);
 hipError_t np8_launch_sm_members(const np8::SmArgs &A, hipStream_t s);

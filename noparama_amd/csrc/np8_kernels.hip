@@ -2550,10 +2550,14 @@ __global__ __launch_bounds__(256) void np8_loglik_matrix_kernel(AssignArgs A, co
 }
 
 // ---- dispatch ----------------------------------------------------------------------------------------
+#ifdef NP8_EXP_ONLY_D8  // (A/B experiment builds, tools/ab_build.sh: the C3 instances only, a fast compile)
+#define NP8_FOR_EACH_DM(X) X(8, 3)
+#else
 #define NP8_FOR_EACH_DM(X) \
     X(1, 1) X(1, 2) X(1, 3) X(1, 4) X(2, 1) X(2, 2) X(2, 3) X(2, 4) X(3, 1) X(3, 2) X(3, 3) X(3, 4) X(4, 1) \
     X(4, 2) X(4, 3) X(4, 4) X(8, 1) X(8, 2) X(8, 3) X(8, 4) X(16, 1) X(16, 2) X(16, 3) X(16, 4)         \
     X(5, 3) X(6, 3) X(7, 3) X(9, 3) X(10, 3) X(11, 3) X(12, 3) X(13, 3) X(14, 3) X(15, 3)
+#endif
 
 bool np8_supported(int D, int M) {
 #define X(d, m) \
@@ -2991,6 +2995,18 @@ __global__ void np8_ctl_clear(Ctl *ctl, int which) {
 
 hipError_t np8_launch_ctl_clear(Ctl *ctl, int which, hipStream_t s) {
     hipLaunchKernelGGL(np8_ctl_clear, dim3(1), dim3(1), 0, s, ctl, which);
+    return hipGetLastError();
+}
+
+// p[0..n) = 0 in stream order, unless a compact sweep graph is halted: the memset a captured sweep would otherwise
+// hold ignores ctl->halt and could clear the halted step's gathered radii before the host resumes that step
+__global__ void np8_clear_unless_halted(double *p, int n, const Ctl *ctl) {
+    if (ctl->halt) return;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) p[i] = 0.0;
+}
+
+hipError_t np8_launch_clear_unless_halted(double *p, int n, const Ctl *ctl, hipStream_t s) {
+    hipLaunchKernelGGL(np8_clear_unless_halted, dim3(1), dim3(256), 0, s, p, n, ctl);
     return hipGetLastError();
 }
 

@@ -173,6 +173,10 @@ def lib():
         "np8_record_bytes": ([vp], i64),
         "np8_step_local": ([vp, vp], i32),
         "np8_step_merge": ([vp, vp, i32], i32),
+        "np8_compact_record_bytes": ([vp], i64),
+        "np8_step_local_compact": ([vp, vp], i32),
+        "np8_step_merge_compact": ([vp, vp, i32, P(i32)], i32),
+        "np8_step_resume": ([vp, vp], i32),
         "np8_param_stats_bytes": ([vp], i64),
         "np8_param_stats_local": ([vp, vp], i32),
         "np8_end_sweep_stats": ([vp, vp], i32),
@@ -402,6 +406,40 @@ class NealAlgorithm8:
     def step_merge(self, records, world):
         records = np.ascontiguousarray(records, dtype=np.uint8)
         self._check(lib().np8_step_merge(self._h, _p(records), int(world)))
+
+    def compact_record_bytes(self):
+        """Bytes of this rank's compact record (0: the step cannot use compact records; use step_local)."""
+        return int(lib().np8_compact_record_bytes(self._h))
+
+    def step_local_compact(self):
+        rec = np.zeros(self.compact_record_bytes(), dtype=np.uint8)
+        self._check(lib().np8_step_local_compact(self._h, _p(rec)))
+        return rec
+
+    def step_merge_compact(self, records, world):
+        """Applies the gathered compact records; True when the step halted (some rank's requests did not fit):
+        every rank then calls step_resume and exchanges the full records (step_merge)."""
+        records = np.ascontiguousarray(records, dtype=np.uint8)
+        halted = C.c_int32(0)
+        self._check(lib().np8_step_merge_compact(self._h, _p(records), int(world), C.byref(halted)))
+        return bool(halted.value)
+
+    def step_resume(self):
+        rec = np.zeros(self.record_bytes(), dtype=np.uint8)
+        self._check(lib().np8_step_resume(self._h, _p(rec)))
+        return rec
+
+    def exchange_step(self, all_gather, world, compact=True):
+        """One synchronous step over the caller's transport: all_gather(np.uint8 array) -> the ranks' arrays
+        concatenated in rank order.  compact: the compact records with the halt-and-resume rule (DESIGN.md §6);
+        returns True when this step halted and was resumed with the full records."""
+        if compact and self.compact_record_bytes() > 0:
+            if not self.step_merge_compact(all_gather(self.step_local_compact()), world):
+                return False
+            self.step_merge(all_gather(self.step_resume()), world)
+            return True
+        self.step_merge(all_gather(self.step_local()), world)
+        return False
 
     def param_stats_local(self):
         """This rank's per-cluster statistics (host exchange of the parameter update)."""

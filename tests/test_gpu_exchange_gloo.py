@@ -99,6 +99,88 @@ def _rank(rank, world, port, outdir, kind="small"):
     dist.destroy_process_group()
 
 
+def _rank_compact(rank, world, port, outdir, cap):
+    """The compact records of a sharded sweep graph over gloo: each step exchanges this rank's
+    compact record (count deltas + the first `cap` requests); a step where some rank's requests do not fit halts
+    alike on every rank and is resumed with the full records."""
+    os.environ["NP8_COMPACT_REQ"] = str(cap)
+    import torch
+    import torch.distributed as dist
+
+    from noparama_amd import NealAlgorithm8
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    X, _, _, _ = _data("cold")
+    n = X.shape[0]
+    lo, hi = (n * rank) // world, (n * (rank + 1)) // world
+    smp = NealAlgorithm8(D, seed=SEED, device=0)
+    smp.comm_init(None, rank, world)
+    smp.set_data(X[lo:hi], offset=lo, n_global=n)
+    smp.init_random(20)
+    cb = smp.compact_record_bytes()
+    assert cb > 0
+    per_step = []  # (requests of every rank, halted)
+
+    def all_gather(a):
+        t = torch.from_numpy(a)
+        out = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(out, t)
+        g = np.concatenate([o.numpy() for o in out])
+        if a.size == cb:  # a compact record: its header's request count, per rank
+            per_step.append([int(g[r * cb:r * cb + 4].view(np.int32)[0]) for r in range(world)])
+        return g
+
+    halts = 0
+    for _ in range(SWEEPS_COLD):
+        halts += smp.exchange_step(all_gather, world, compact=True)
+        smp.end_sweep()
+    st = smp.state()
+    nreq = np.array(per_step)
+    over = nreq > cap
+    partial = int(np.sum(over.any(axis=1) & ~over.all(axis=1)))  # steps where only some ranks overflowed
+    assert halts == int(np.sum(over.any(axis=1))) == smp.stats()["compact_halts"]
+    np.save(os.path.join(outdir, f"z{rank}.npy"), st["z"])
+    np.save(os.path.join(outdir, f"c{rank}.npy"), st["counts"])
+    np.save(os.path.join(outdir, f"k{rank}.npy"),
+            np.array([st["K"], smp.stats()["rejected_requests"], halts, partial]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,cap", [(2, 1), (8, 1), (2, 32), (8, 32)])
+def test_compact_records_gloo_cold_start_equals_single_rank(tmp_path, world, cap):
+    """Compact records over the host transport from the reference's initialisation (init_random(20), C3 data,
+    N = 1e6, 20 sweeps) at 2 and 8 ranks, capacity 1 and 32: the first steps overflow on every rank (halt, full
+    records), the mixed regime's steps overflow on some ranks only; labels, counts, K and the rejected-request count
+    equal one rank's (the full-record chain) bit for bit."""
+    import torch.multiprocessing as mp
+
+    from noparama_amd import NealAlgorithm8
+
+    X, _, _, _ = _data("cold")
+    one = NealAlgorithm8(D, seed=SEED, device=0)
+    one.set_data(X)
+    one.init_random(20)
+    one.sweep(SWEEPS_COLD)
+    ref = one.state()
+    rej = one.stats()["rejected_requests"]
+    one.close()
+    mp.spawn(_rank_compact, args=(world, _port(), str(tmp_path), cap), nprocs=world, join=True)
+    zz = np.concatenate([np.load(tmp_path / f"z{r}.npy") for r in range(world)])
+    assert np.array_equal(zz, ref["z"])
+    ks = [np.load(tmp_path / f"k{r}.npy") for r in range(world)]
+    for r in range(world):
+        assert np.array_equal(np.load(tmp_path / f"c{r}.npy"), ref["counts"])
+        assert list(ks[r][:2]) == [ref["K"], rej]
+        assert list(ks[r][2:]) == list(ks[0][2:])  # halts and their kind alike on every rank
+    halts, partial = int(ks[0][2]), int(ks[0][3])
+    print(f"world {world} cap {cap}: {halts} halted steps of {SWEEPS_COLD}, {partial} with only some ranks over")
+    assert 0 < halts < SWEEPS_COLD  # the first steps halt, the warm ones fit
+    if cap == 1:
+        assert partial > 0
+
+
 def test_two_rank_processes_equal_single_rank(tmp_path):
     import torch.multiprocessing as mp
 

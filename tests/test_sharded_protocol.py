@@ -74,3 +74,58 @@ def test_two_rank_gloo_sweeps_equal_single_process(tmp_path):
         k = np.load(tmp_path / f"k{r}.npy")
         assert int(k[0]) == ref["K"] and list(k[1:1 + SWEEPS]) == deferred
         assert list(k[1 + SWEEPS:]) == list(one.request_stats)
+
+
+CAP = 2  # compact records: room for this many requests per rank (NP8_COMPACT_REQ)
+
+
+def _rank_compact(rank, world, port, X, outdir):
+    """The compact-record form of the exchange:
+    each rank gathers its count deltas and at most CAP requests with its request count; when some rank's count
+    exceeds CAP -- seen alike by every rank in the gathered headers -- nothing is applied and the step is exchanged
+    again with the full records."""
+    import oracle as O
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    lo, hi = (N * rank) // world, (N * (rank + 1)) // world
+    c = O.Chain(D, seed=SEED, kcap=KCAP, req_max=REQ_MAX)
+    c.set_data(X)
+    c.init_random(20)
+    halts, partial = 0, 0
+    for _ in range(SWEEPS):
+        delta, rp, ri, rm, rz, n = c.assign_range(lo, hi)
+        heads = [None] * world
+        dist.all_gather_object(heads, [delta, rp[:CAP], ri[:CAP], rm[:CAP], rz[:CAP], n])
+        over = [h[5] > CAP for h in heads]
+        if any(over):  # halt: the full records of the same step
+            halts += 1
+            partial += not all(over)
+            heads = [None] * world
+            dist.all_gather_object(heads, [delta, rp, ri, rm, rz, n])
+        dsum = np.sum([h[0] for h in heads], axis=0).astype(np.int32)
+        cat = [np.concatenate([h[k] for h in heads]) for k in (1, 2, 3, 4)]
+        c.finalize(dsum, *cat, n_req=int(sum(h[5] for h in heads)), owner_lo=lo, owner_hi=hi)
+        c.end_sweep()
+    np.save(os.path.join(outdir, f"z{rank}.npy"), c.state()["z"][lo:hi])
+    np.save(os.path.join(outdir, f"k{rank}.npy"), np.array([c.K, halts, partial] + list(c.request_stats)))
+    dist.destroy_process_group()
+
+
+def test_two_rank_gloo_compact_records_equal_single_process(tmp_path):
+    import oracle as O
+
+    X, _, _, _ = datasets.mixture(N, D, 8, 0.6, 4.0, seed=3)
+    one = O.Chain(D, seed=SEED, kcap=KCAP, req_max=REQ_MAX)
+    one.set_data(X)
+    one.init_random(20)
+    for _ in range(SWEEPS):
+        assert one.sweep(1) == 0
+    ref = one.state()
+    mp.spawn(_rank_compact, args=(2, _free_port(), X, str(tmp_path)), nprocs=2, join=True)
+    z = np.concatenate([np.load(tmp_path / f"z{r}.npy") for r in range(2)])
+    assert np.array_equal(z, ref["z"])
+    k0 = np.load(tmp_path / "k0.npy")
+    assert np.array_equal(k0, np.load(tmp_path / "k1.npy"))
+    assert int(k0[0]) == ref["K"] and list(k0[3:]) == list(one.request_stats)
+    assert 0 < int(k0[1]) <= SWEEPS  # the first steps from init_random(20) overflow the compact records
