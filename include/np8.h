@@ -323,6 +323,13 @@ int np8_loglik_matrix(np8_ctx *ctx, const int64_t *idx, int64_t n, double *out);
  * against the reference function itself. */
 int np8_pick_batch(np8_ctx *ctx, const double *lw, int32_t n, const double *u, int64_t n_draws, int32_t *out);
 
+/* Debug: the level-0 auxiliary screen's upper bound (DESIGN.md "Auxiliary screen": from the item's prefix call alone,
+ * the supremum over the auxiliary's other draws in closed form, without the threshold's own margin term) of each
+ * listed item's M auxiliary log-likelihoods at the current epoch, out[n][M]; the reference prior's fp64 path only.
+ * np8_assign_fast skips auxiliary m of an item when this bound lies below its running maximum by kSkip;
+ * tests/test_gpu_screen.py holds it above the exact values np8_loglik_matrix returns. */
+int np8_aux_bounds(np8_ctx *ctx, const int64_t *idx, int64_t n, double *out);
+
 /* Sum over items of log p(x_i | theta_{z_i}) for the current state (MCMC::considerMaxLikelihood). */
 int np8_total_loglik(np8_ctx *ctx, double *out);
 

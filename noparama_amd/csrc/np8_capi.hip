@@ -1938,6 +1938,14 @@ int np8_create_sized(np8_ctx **out, const np8_config *cfg_in, size_t cfg_bytes) 
         hyp.push_back(smax);
     }
     for (int a = 0; a < D; ++a) hyp.push_back(c->UinvT[a * D + a]);  // the whitening diagonal, contiguous (kUdiag)
+    {  // level 0 of the auxiliary screen (kPre, aux_screen0_ub): 1/gamma, the |v| interval, c = rsk xmax; xmax = 6.77
+       // bounds |r cos|, |r sin| of every Box-Muller pair of u32_01 uniforms (r <= sqrt(-2 log 2^-33) = 6.7638)
+        const double xmax = 6.77, cc = c->rsk * xmax, an = std::fabs(c->nu);
+        hyp.push_back(2.0 / (std::sqrt(cc * cc + 4.0 * D) + cc));
+        hyp.push_back(std::max((double)D - an * xmax, 0.0));
+        hyp.push_back((double)D + an * xmax);
+        hyp.push_back(cc);
+    }
     if (c->wide) {  // the wide kernels' item frame at DT: mu0 and U^T packed, zero beyond D (AssignArgs::uw)
         c->uw_off = (int64_t)hyp.size();
         for (int a = 0; a < c->DT; ++a) hyp.push_back(a < D ? c->mu0[a] : 0.0);
@@ -2670,6 +2678,27 @@ int np8_get_state(np8_ctx *c, int32_t which, int32_t *z, int32_t *K, double *mu,
             if (counts) counts[lab[s]] = cn[s];
         }
     }
+    return NP8_OK;
+}
+
+int np8_aux_bounds(np8_ctx *c, const int64_t *idx, int64_t n, double *out) {
+    if (!c) return NP8_ERR_ARG;
+    if (!c->have_state) return fail(c, NP8_ERR_STATE, "np8_aux_bounds: no state");
+    if (c->wide || c->prior != NP8_PRIOR_REFERENCE)
+        return fail(c, NP8_ERR_STATE, "np8_aux_bounds: the reference prior's fp64 path only");
+    if (n <= 0) return NP8_OK;
+    for (int64_t k = 0; k < n; ++k)
+        if (idx[k] < 0 || idx[k] >= c->n_loc) return fail(c, NP8_ERR_RANGE, "np8_aux_bounds: index out of range");
+    int64_t *d_idx = nullptr;
+    double *d_out = nullptr;
+    HIPC(c, hipMalloc(&d_idx, sizeof(int64_t) * n));
+    HIPC(c, hipMalloc(&d_out, sizeof(double) * n * c->M));
+    HIPC(c, hipMemcpy(d_idx, idx, sizeof(int64_t) * n, hipMemcpyHostToDevice));
+    HIPC(c, np8_launch_aux_bounds(assign_args(c, 0, 0, nullptr, false), c->D, c->M, d_idx, n, d_out, c->stream));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    HIPC(c, hipMemcpy(out, d_out, sizeof(double) * n * c->M, hipMemcpyDeviceToHost));
+    (void)hipFree(d_idx);
+    (void)hipFree(d_out);
     return NP8_OK;
 }
 

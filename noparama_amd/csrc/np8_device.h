@@ -25,7 +25,9 @@ enum Stream : uint32_t {
     kStreamParamU = 6,  // MH acceptance uniforms (i = slot)
     kStreamAuxDir = 7,  // direction of a picked auxiliary's xi orthogonal to the item (i = item);
                         // NIW: Bartlett off-diagonals and the z_perp direction of a picked auxiliary
-    kStreamAuxNiw = 8   // NIW prior: an auxiliary's Bartlett chi^2 draws, chi^2_{D-1} and z_1 (i = item)
+    kStreamAuxNiw = 8,  // NIW prior: an auxiliary's Bartlett chi^2 draws, chi^2_{D-1} and z_1 (i = item)
+    // (9 .. 11: split-merge, np8_sm.hip)
+    kStreamAuxPre = 12  // reference prior: the auxiliaries' chi^2 prefixes (i = item, call 0; aux_pre_bits)
 };
 
 // Base measures (include/np8.h NP8_PRIOR_*).
@@ -212,13 +214,55 @@ NP8_HD int aux_calls(int D) {
 }
 NP8_HD int dir_calls(int D) { return (D + 3) / 4; }
 
+// The screen prefixes (round 6, DESIGN.md "Auxiliary screen"), for D <= kPreMaxD (the fast kernel's level-0 screen; above
+// it the draws are the round-5 ones and the kernels screen from each auxiliary's call 0, as before: their register
+// budget has no room for the prefix words).  One Philox call per item and epoch -- stream AUX_PRE,
+// call 0 -- holds the leading b bits of the first P = min(k, 3) chi^2 uniforms of all M auxiliaries, b = min(16,
+// floor(128 / (M P))): field f = m P + j is bits [b f, b f + b) of the call's output (word 0 = bits 0 .. 31).  The
+// 32-bit word that feeds chi^2 uniform j < P of auxiliary m is (field << (32 - b)) | (the word the calls above give it
+// & (2^(32 - b) - 1)).  The chi^2 uniforms stay uniform and independent of everything else drawn; what the prefixes buy
+// is a lower bound of every auxiliary's chi^2 -- so an upper bound of its log-likelihood, with the supremum over
+// (v, xi_par) taken in closed form -- from one call per item instead of call 0 of every auxiliary.
+constexpr int kPreMaxD = 8;
+NP8_HD int aux_pre_n(int D) {
+    const int k = (D - 1) / 2;
+    return D > kPreMaxD ? 0 : (k < 3 ? k : 3);
+}
+NP8_HD int aux_pre_bits(int D, int M) {
+    const int P = aux_pre_n(D);
+    if (P <= 0 || M <= 0) return 0;
+    const int b = 128 / (M * P);
+    return b > 16 ? 16 : b;
+}
+// field f of width b (1..16) of the 128-bit prefix call (word selects instead of a run-time register index)
+NP8_HD uint32_t aux_pre_field(const uint32_t (&W)[4], int f, int b) {
+    const int lo = b * f, wi = lo >> 5, sh = lo & 31;
+    const uint32_t a = wi == 0 ? W[0] : (wi == 1 ? W[1] : (wi == 2 ? W[2] : W[3]));
+    const uint32_t n = wi == 0 ? W[1] : (wi == 1 ? W[2] : (wi == 2 ? W[3] : 0u));
+    const uint64_t v = ((uint64_t)n << 32 | a) >> sh;
+    return (uint32_t)v & ((1u << b) - 1u);
+}
+NP8_HD uint32_t aux_pre_word(uint32_t w, uint32_t field, int b) {
+    return b > 0 ? ((field << (32 - b)) | (w & ((1u << (32 - b)) - 1u))) : w;
+}
+// chi^2 uniform j's word of auxiliary m (the word its own calls give, combined with its prefix when j < P)
+NP8_HD uint32_t aux_chi_word(const uint32_t (&pre)[4], uint32_t w, int m, int j, int D, int M) {
+    const int P = aux_pre_n(D), b = aux_pre_bits(D, M);
+    return (j < P && b > 0) ? aux_pre_word(w, aux_pre_field(pre, m * P + j, b), b) : w;
+}
+NP8_HD void aux_pre_call(uint64_t seed, uint64_t i, uint32_t t, uint32_t out[4]) {
+    philox_call(seed, i, t, kStreamAuxPre, 0u, out);
+}
+
 // w: the words of call m*Qa; w1g the words of call m*Qa + 1 when have_w1 (else drawn here).  Arrays by
 // reference, never through a pointer: a pointer to a register array would move it to scratch memory.
 // D is a template constant: the chi^2 loop unrolls and every word index is static (a run-time index
 // into a register array would move the array to scratch memory).
+// pre: the item's prefix call (aux_pre_call), M the auxiliaries per item (the prefixes' layout).
 template <int D>
 NP8_HD void aux_core_w(uint64_t seed, uint64_t i, uint32_t t, int m, double nu, double &v, double &xpar,
-                       double &chi2, const uint32_t (&w)[4], bool have_w1, const uint32_t (&w1g)[4]) {
+                       double &chi2, const uint32_t (&w)[4], bool have_w1, const uint32_t (&w1g)[4],
+                       const uint32_t (&pre)[4], int M) {
     constexpr int k = (D - 1) / 2;
     constexpr bool odd = ((D - 1) & 1) != 0;
     const int Qa = aux_calls(D);
@@ -251,9 +295,9 @@ NP8_HD void aux_core_w(uint64_t seed, uint64_t i, uint32_t t, int m, double nu, 
     for (int j = 0; j < k; ++j) {
         uint32_t word;
         if (j < 2) {
-            word = w[2 + j];
+            word = aux_chi_word(pre, w[2 + j], m, j, D, M);
         } else if (j < 4) {
-            word = w1[j];
+            word = aux_chi_word(pre, w1[j], m, j, D, M);
         } else {
             if (((j - 4) & 3) == 0) philox_call(seed, i, t, kStreamAux, base + 2u + (uint32_t)((j - 4) >> 2), wc);
             word = wc[(j - 4) & 3];
@@ -269,13 +313,15 @@ NP8_HD void aux_core_w(uint64_t seed, uint64_t i, uint32_t t, int m, double nu, 
     chi2 = c2;
 }
 
-// aux_core_w's draws with D at run time (the wide path, D padded to a tile multiple): the same operations in the
+// aux_core_w's draws with D at run time (the wide path, D > kPreMaxD: no prefixes; D padded to a tile multiple): the
+// same operations in the
 // same order; the words of each further call are consumed four at a time with static indices.
-NP8_HD void aux_core_rt(uint64_t seed, uint64_t i, uint32_t t, int m, int D, double nu, double &v, double &xpar,
-                        double &chi2) {
+NP8_HD void aux_core_rt(uint64_t seed, uint64_t i, uint32_t t, int m, int M, int D, double nu, double &v,
+                        double &xpar, double &chi2) {
     const int k = (D - 1) / 2;
     const bool odd = ((D - 1) & 1) != 0;
     const uint32_t base = (uint32_t)(m * aux_calls(D));
+    (void)M;  // (the wide path's D > kPreMaxD: no prefixes)
     uint32_t w[4], w1[4] = {0u, 0u, 0u, 0u};
     philox_call(seed, i, t, kStreamAux, base, w);
     {
@@ -321,11 +367,13 @@ NP8_HD void aux_core_rt(uint64_t seed, uint64_t i, uint32_t t, int m, int D, dou
 }
 
 template <int D>
-NP8_HD void aux_core(uint64_t seed, uint64_t i, uint32_t t, int m, double nu, double &v, double &xpar, double &chi2) {
-    uint32_t w[4];
+NP8_HD void aux_core(uint64_t seed, uint64_t i, uint32_t t, int m, int M, double nu, double &v, double &xpar,
+                     double &chi2) {
+    uint32_t w[4], pre[4] = {0u, 0u, 0u, 0u};
     const uint32_t none[4] = {0u, 0u, 0u, 0u};
+    if (aux_pre_n(D) > 0) aux_pre_call(seed, i, t, pre);
     philox_call(seed, i, t, kStreamAux, (uint32_t)(m * aux_calls(D)), w);
-    aux_core_w<D>(seed, i, t, m, nu, v, xpar, chi2, w, false, none);
+    aux_core_w<D>(seed, i, t, m, nu, v, xpar, chi2, w, false, none, pre, M);
 }
 
 // Log-likelihood of the item under auxiliary (v, xi_par, chi2); ny = |y0|.

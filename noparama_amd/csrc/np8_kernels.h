@@ -645,6 +645,8 @@ hipError_t np8_launch_changes(const int32_t *z, const int32_t *z_base, int64_t n
 // Parity/debug: the sweep's categorical draw (pick_step) on given log-weights, one lane per draw.
 hipError_t np8_launch_pick_batch(const double *lw, int32_t n, const double *u, int64_t n_draws, int32_t *out,
                                  hipStream_t s);
+hipError_t np8_launch_aux_bounds(const np8::AssignArgs &A, int D, int M, const int64_t *idx, int64_t n, double *out,
+                                 hipStream_t s);
 hipError_t np8_launch_loglik_matrix(const np8::AssignArgs &A, int D, int M, int prior, const int64_t *idx, int64_t n,
                                     double *out, hipStream_t s);
 size_t np8_finalize_lds_bytes(int kcap);

@@ -18,6 +18,30 @@
 
 using namespace np8;
 
+// Checked indices (debug builds only, -DNP8_CHECKED, tools/ab_build.sh): an index outside [lo, hi) is printed with its
+// source line and replaced by lo, so that a bad state is named instead of faulting the GPU.
+#ifdef NP8_CHECKED
+__device__ int g_np8_chk[8];  // the first failed check: line, value, lo, hi (read by np8_exp_checks)
+__device__ __noinline__ int64_t np8_chk(int64_t v, int64_t lo, int64_t hi, int line) {
+    if (v < lo || v >= hi) {
+        if (atomicCAS(&g_np8_chk[0], 0, line) == 0) {
+            g_np8_chk[1] = (int)v;
+            g_np8_chk[2] = (int)lo;
+            g_np8_chk[3] = (int)hi;
+        }
+        atomicAdd(&g_np8_chk[4], 1);
+        return lo;
+    }
+    return v;
+}
+extern "C" int np8_exp_checks(int *out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_np8_chk), sizeof(int) * 8, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#define NP8_CHK(v, lo, hi) np8_chk((int64_t)(v), (int64_t)(lo), (int64_t)(hi), __LINE__)
+#else
+#define NP8_CHK(v, lo, hi) (v)
+#endif
+
 namespace {
 
 template <int D>
@@ -33,6 +57,8 @@ struct HypView {
     static constexpr int kLT = kCaux + 4;
     static constexpr int kSmax = kLT + DP;  // NIW screen: bound of the D-1 further log chi^2 draws
     static constexpr int kUdiag = kSmax + 1;  // the diagonal of UinvT again, contiguous (one scalar load round)
+    // level 0 of the auxiliary screen (aux_screen0): 1/gamma, the |v| interval [v_lo, v_hi], c = rsk xmax
+    static constexpr int kPre = kUdiag + D;
 };
 
 // ll = c - q/2 with q = d' P d.  Isotropic entries (iso > 0, a wave-uniform branch): q = iso * |d|^2;
@@ -88,10 +114,10 @@ __device__ __forceinline__ void whiten(const double *__restrict__ hyp, const dou
 // multivariatenormal.cpp:124-135; DESIGN.md "G0").
 template <int D>
 __device__ __forceinline__ double aux_ll(const double *__restrict__ hyp, double ny, uint64_t seed, uint64_t ig,
-                                         uint32_t t, int m) {
+                                         uint32_t t, int m, int M) {
     using H = HypView<D>;
     double v, xpar, chi2;
-    aux_core<D>(seed, ig, t, m, hyp[H::kNu], v, xpar, chi2);
+    aux_core<D>(seed, ig, t, m, M, hyp[H::kNu], v, xpar, chi2);
     return aux_loglik(ny, v, xpar, chi2, D, hyp[H::kRsk], hyp[H::kCaux]);
 }
 
@@ -153,6 +179,48 @@ __device__ __forceinline__ float aux_screen_ub(const uint32_t (&w)[4], float chi
     return (av_lo >= 0.02f) ? ub_ll + err : __builtin_inff();
 }
 
+// Level 0 of the screen (round 6): an upper bound of auxiliary m's log-likelihood from the item's prefix call alone
+// (aux_pre_call: the leading b bits of its first P chi^2 uniforms), the supremum over the draws of call 0 taken in
+// closed form:
+//   ll = caux - D log|v| - q/2,  q = (ny/|v| - rsk xi_par)^2 + rsk^2 chi2  <=  caux + S(ny) - rsk^2 chi2_lb / 2,
+//   S(ny) = max over |v| in [v_lo, v_hi] of h(|v|),  h(a) = -D log a - (ny/a - c)_+^2 / 2,  c = rsk xmax,
+// since |xi_par| <= r <= xmax = 6.77 for every Box-Muller pair of u32_01 uniforms (r <= sqrt(-2 log 2^-33) = 6.7638)
+// and |v| = |D + nu g0| lies in [max(D - |nu| xmax, 0), D + |nu| xmax].  h rises up to a* = ny / gamma, gamma =
+// (sqrt(c^2 + 4D) + c) / 2, and falls after it (a^3 h'(a) = -D a^2 - c ny a + ny^2 below ny/c, -D a^2 above), so
+// S = h(clamp(a*, v_lo, v_hi)).  chi2 >= chi2_lb = -2 log prod_j (field_j + 1) 2^-b over the prefixed uniforms (each
+// u32_01 word with that prefix is below (field + 1) 2^-b; the other uniforms are <= 1 and g_odd^2 >= 0).  In fp32 with
+// the level-1 screen's margin (1 nat + 1e-4 of every term); S = +inf (no screen) when the interval reaches |v| = 0 at
+// ny = 0.  Returns the bound without the threshold's own margin term, which the caller adds (as for level 1).
+// s0: S(ny) (aux_screen0_s, once per item); k2 = rsk^2 / 2.
+template <int D, int M>
+__device__ __forceinline__ float aux_screen0_ub(const uint32_t (&pre)[4], int m, float s0, float s0_abs, float caux,
+                                                float k2) {
+    constexpr int P = D > kPreMaxD ? 0 : ((D - 1) / 2 < 3 ? (D - 1) / 2 : 3);  // (aux_pre_n)
+    constexpr int b0 = P > 0 ? 128 / (M * P) : 0;
+    constexpr int b = b0 > 16 ? 16 : b0;
+    if constexpr (P == 0) {
+        return __builtin_inff();
+    } else {
+        float prod = 1.0f;
+#pragma unroll
+        for (int j = 0; j < P; ++j) prod *= (float)(aux_pre_field(pre, m * P + j, b) + 1u);
+        // chi2_lb = 2 ln2 (P b - log2 prod) >= 0 (each factor <= 2^b)
+        const float chi = 2.0f * 0.693147180559945f * fmaxf((float)(P * b) - __builtin_amdgcn_logf(prod), 0.0f);
+        const float ub = fmaf(-k2, chi, caux + s0);
+        return ub + 1.0f + 1e-4f * (fabsf(caux) + s0_abs + k2 * chi);
+    }
+}
+
+// S(ny) of aux_screen0_ub and the size of its terms (for the margin); +inf when no bound applies.
+__device__ __forceinline__ float aux_screen0_s(float ny, float inv_gamma, float v_lo, float v_hi, float c, int D,
+                                               float &s_abs) {
+    const float a = fminf(fmaxf(ny * inv_gamma, v_lo), v_hi);
+    const float tt = fmaxf(ny * __builtin_amdgcn_rcpf(a) - c, 0.0f);
+    const float dl = (float)D * 0.693147180559945f * __builtin_amdgcn_logf(a);
+    s_abs = fabsf(dl) + 0.5f * tt * tt;
+    return (a > 0.0f) ? fmaf(-0.5f * tt, tt, -dl) : __builtin_inff();
+}
+
 // Level 2 of the screen from the words w1 of call 1: the further chi^2 terms it holds (uniforms 2, 3 and
 // g_odd^2 for odd D - 1; exact chi2 for D <= 9) and their fp32 error.
 template <int D>
@@ -179,22 +247,36 @@ __device__ __forceinline__ float aux_screen_chi1(const uint32_t (&w1)[4], float 
     return chi;
 }
 
+// call 0 / call 1 words of auxiliary m with its chi^2 prefixes in place (aux_chi_word): what the level-1 / level-2
+// screens read; aux_core_w takes them as they are (combining a combined word again changes nothing)
+template <int D, int M>
+__device__ __forceinline__ void aux_words0(const uint32_t (&pre)[4], int m, uint32_t (&w)[4]) {
+    if constexpr (D <= kPreMaxD) {
+        w[2] = aux_chi_word(pre, w[2], m, 0, D, M);
+        w[3] = aux_chi_word(pre, w[3], m, 1, D, M);
+    }
+}
+template <int D, int M>
+__device__ __forceinline__ void aux_words1(const uint32_t (&pre)[4], int m, uint32_t (&w1)[4]) {
+    if constexpr (D <= kPreMaxD) w1[2] = aux_chi_word(pre, w1[2], m, 2, D, M);
+}
+
 template <int D, int PRIOR>
 __device__ __forceinline__ double prior_aux_ll(const double *__restrict__ hyp, double ny, uint64_t seed, uint64_t ig,
-                                               uint32_t t, int m) {
+                                               uint32_t t, int m, int M) {
     if constexpr (PRIOR == kPriorNiw)
         return niw_aux_ll<D>(hyp, ny, seed, ig, t, m);
     else
-        return aux_ll<D>(hyp, ny, seed, ig, t, m);
+        return aux_ll<D>(hyp, ny, seed, ig, t, m, M);
 }
 
 // (v, mu) of a picked auxiliary: mu = mu0 + (|v|/sqrt kappa) L^T xi with xi from aux_xi.
 template <int D>
 __device__ __forceinline__ void aux_params(const double *__restrict__ hyp, const double (&y0)[D], double ny,
-                                           uint64_t seed, uint64_t ig, uint32_t t, int m, double *vmu) {
+                                           uint64_t seed, uint64_t ig, uint32_t t, int m, int M, double *vmu) {
     using H = HypView<D>;
     double v, xpar, chi2, xi[D];
-    aux_core<D>(seed, ig, t, m, hyp[H::kNu], v, xpar, chi2);
+    aux_core<D>(seed, ig, t, m, M, hyp[H::kNu], v, xpar, chi2);
     aux_xi<D>(seed, ig, t, m, D, y0, ny, xpar, chi2, xi);
     const double sc = fabs(v) * hyp[H::kRsk];
     const double *LT = hyp + H::kLT;
@@ -446,6 +528,8 @@ __device__ __forceinline__ void assign_item(const AssignArgs &A, const int64_t p
             // level 1 for every auxiliary at once (M independent Philox chains): a bit per auxiliary the
             // screen cannot rule out
             uint32_t need = 0u;
+            uint32_t pre[4] = {0u, 0u, 0u, 0u};
+            if constexpr (D <= kPreMaxD && (D - 1) / 2 >= 1) aux_pre_call(A.seed, ig, t, pre);
 #ifdef NP8_EXP_UNROLL
 #pragma unroll
 #else
@@ -457,6 +541,7 @@ __device__ __forceinline__ void assign_item(const AssignArgs &A, const int64_t p
 #endif
                 uint32_t w[4];
                 philox_call(A.seed, ig, t, kStreamAux, (uint32_t)(m * Qa), w);
+                aux_words0<D, M>(pre, m, w);
                 if (!(aux_screen_ub<D>(w, 0.0f, 0.0f, nyf, nuf, rskf, cauxf, thr) <= thr)) need |= 1u << m;
             }
             int64_t n_viol = 0, n_ex_lane = 0, n_ex_wave = 0;
@@ -469,9 +554,11 @@ __device__ __forceinline__ void assign_item(const AssignArgs &A, const int64_t p
 #endif
                 uint32_t w0[4], w1[4] = {0u, 0u, 0u, 0u};
                 philox_call(A.seed, ig, t, kStreamAux, (uint32_t)(m * Qa), w0);
+                aux_words0<D, M>(pre, m, w0);
                 const bool l2 = has_call1 && !skip;
                 if (l2) {  // level 2: the chi^2 terms of call 1
                     philox_call(A.seed, ig, t, kStreamAux, (uint32_t)(m * Qa + 1), w1);
+                    aux_words1<D, M>(pre, m, w1);
                     float e1;
                     const float c1 = aux_screen_chi1<D>(w1, e1);
                     skip = aux_screen_ub<D>(w0, c1, e1, nyf, nuf, rskf, cauxf, thr) <= thr;
@@ -483,7 +570,7 @@ __device__ __forceinline__ void assign_item(const AssignArgs &A, const int64_t p
                 }
                 if (!skip || COUNT) {
                     double v, xpar, chi2;
-                    aux_core_w<D>(A.seed, ig, t, m, nu, v, xpar, chi2, w0, l2, w1);
+                    aux_core_w<D>(A.seed, ig, t, m, nu, v, xpar, chi2, w0, l2, w1, pre, M);
                     const double lw = aux_loglik(ny, v, xpar, chi2, D, rsk, caux) + logam;
                     if (!skip) {
                         ensure_u(st, lw, A.seed, ig, t);
@@ -586,7 +673,7 @@ __device__ __forceinline__ void assign_item(const AssignArgs &A, const int64_t p
 #pragma unroll
                 for (int a = 0; a < D; ++a) vmu[1 + a] = y0[a];
             } else {
-                aux_params<D>(hyp, y0, ny, A.seed, ig, t, st.pick - K, vmu);
+                aux_params<D>(hyp, y0, ny, A.seed, ig, t, st.pick - K, M, vmu);
             }
         }
     }
@@ -701,8 +788,8 @@ __global__ __launch_bounds__(NP8_ASSIGN_BLOCK) __attribute__((amdgpu_waves_per_e
     const double *__restrict__ X = A.Xs[0];
     const double *__restrict__ cand = A.cand;
     const double *__restrict__ hyp = A.hyp;
-    const int32_t zi = zs[p];
-    const int32_t il = ids[p];
+    const int32_t zi = (int32_t)NP8_CHK(zs[p], 0, A.kcap);
+    const int32_t il = (int32_t)NP8_CHK(ids[p], 0, A.n_loc);
     const uint64_t ig = (uint64_t)(A.offset + il);
     const uint32_t t = A.ctl->t_base + A.t;
     double x[D];
@@ -743,29 +830,55 @@ __global__ __launch_bounds__(NP8_ASSIGN_BLOCK) __attribute__((amdgpu_waves_per_e
     const double iso_1 = slot_iso[s_1], cs_1 = slot_c[s_1], l1_1 = slot_logn1[s_1];
     const int32_t js_1 = dense_of[s_1], pl_1 = plen_s[s_1];
     const double pr_1 = plr2_s[s_1];
-    // level 1 of the auxiliary screen while the own row's loads are in flight: each auxiliary's bound from its
-    // Philox call 0, without the threshold (the running maximum), which is compared below
-    double ny = 0.0;
+    // level 0 of the auxiliary screen while the own row's loads are in flight: every auxiliary's bound from the item's
+    // prefix call (aux_screen0_ub), without the threshold (the running maximum), which is compared below.  |y0|^2 in
+    // fp64 (its root in fp64 only where an auxiliary is drawn exactly, fp32 for the bounds)
+    // (D > kPreMaxD: no prefixes; every auxiliary's bound from its call 0 up front, the round-5 form of the screen)
+    constexpr bool kL0 = D <= kPreMaxD && (D - 1) / 2 >= 1;
+    double n2 = 0.0;
     {
         const double *U = hyp + H::kUdiag;  // diagonal (launch condition): whiten() + norm_of() with zeros left out
-        double n2 = 0.0;
 #pragma unroll
         for (int a = 0; a < D; ++a) {
             const double y = U[a] * (x[a] - hyp[H::kMu0 + a]);
             n2 = fma(y, y, n2);
         }
-        ny = sqrt(n2);
     }
+    [[maybe_unused]] double ny = 0.0;
+    [[maybe_unused]] float nyf = 0.0f;
+    if constexpr (kL0)
+        nyf = __builtin_amdgcn_sqrtf((float)n2);
+    else
+        ny = sqrt(n2);
     constexpr int Qa = (1 + ((((D - 1) & 1) || (D - 1) / 2 > 2) ? 1 : 0) + ((D - 1) / 2 > 4 ? ((D - 1) / 2 - 1) / 4 : 0));
-    float ub1[M];
+    [[maybe_unused]] uint32_t pre[4];
+    float ub0[M];
     if (!COUNT) {
-        const float nyf = (float)ny, nuf = (float)hyp[H::kNu], rskf = (float)hyp[H::kRsk], cauxf = (float)hyp[H::kCaux];
+        if constexpr (kL0) {
+            aux_pre_call(A.seed, ig, t, pre);
+            float s_abs;
+            const float s0 = aux_screen0_s(nyf, (float)hyp[H::kPre], (float)hyp[H::kPre + 1], (float)hyp[H::kPre + 2],
+                                           (float)hyp[H::kPre + 3], D, s_abs);
+            const float rskf = (float)hyp[H::kRsk], cauxf = (float)hyp[H::kCaux];
 #pragma unroll
-        for (int m = 0; m < M; ++m) {
-            uint32_t w[4];
-            philox_call(A.seed, ig, t, kStreamAux, (uint32_t)(m * Qa), w);
-            ub1[m] = aux_screen_ub<D>(w, 0.0f, 0.0f, nyf, nuf, rskf, cauxf, 0.0f, false);
-            asm volatile("" ::"v"(ub1[m]));  // computed here, while the own row's loads are in flight (not sunk)
+            for (int m = 0; m < M; ++m) {
+#ifdef NP8_EXP_NOAUXSCREEN  // (ablation timing only: no auxiliary is ever evaluated -- not the chain)
+                ub0[m] = -__builtin_inff() + 0.0f * nyf;
+#else
+                ub0[m] = aux_screen0_ub<D, M>(pre, m, s0, s_abs, cauxf, 0.5f * rskf * rskf);
+#endif
+                asm volatile("" ::"v"(ub0[m]));  // computed here, while the own row's loads are in flight (not sunk)
+            }
+        } else {
+            const float nyf1 = (float)ny, nuf = (float)hyp[H::kNu], rskf = (float)hyp[H::kRsk],
+                        cauxf = (float)hyp[H::kCaux];
+#pragma unroll
+            for (int m = 0; m < M; ++m) {
+                uint32_t w[4];
+                philox_call(A.seed, ig, t, kStreamAux, (uint32_t)(m * Qa), w);
+                ub0[m] = aux_screen_ub<D>(w, 0.0f, 0.0f, nyf1, nuf, rskf, cauxf, 0.0f, false);
+                asm volatile("" ::"v"(ub0[m]));  // computed here, while the own row's loads are in flight (not sunk)
+            }
         }
     }
     {
@@ -800,7 +913,8 @@ __global__ __launch_bounds__(NP8_ASSIGN_BLOCK) __attribute__((amdgpu_waves_per_e
                 double mo[D];
 #pragma unroll
                 for (int a = 0; a < D; ++a) mo[a] = slot_mu[(int64_t)zi * D + a];
-                own(zi, mo, slot_iso[zi], slot_c[zi], slot_logn1[zi], dense_of[zi], plen_s[zi], plr2_s[zi]);
+                own(zi, mo, slot_iso[zi], slot_c[zi], slot_logn1[zi], (int32_t)NP8_CHK(dense_of[zi], 0, A.ctl->K),
+                    plen_s[zi], plr2_s[zi]);
             }
         }
     }
@@ -868,8 +982,8 @@ __global__ __launch_bounds__(NP8_ASSIGN_BLOCK) __attribute__((amdgpu_waves_per_e
                 jq = row_of(q);
 #pragma unroll
                 for (int g = 0; g < kScreenGroups; ++g)
-                    if (g < ng) fdist[g] = A.pdist[(int64_t)gid[g] * A.ls + jq];
-                const double *e = cand + (int64_t)jq * CS;
+                    if (g < ng) fdist[g] = A.pdist[NP8_CHK((int64_t)gid[g] * A.ls + jq, 0, (int64_t)A.kcap * A.ls)];
+                const double *e = cand + (int64_t)NP8_CHK(jq, 0, K) * CS;
 #pragma unroll
                 for (int a = 0; a < D; ++a) fm[a] = e[a];
                 fiso = e[F + kFieldIso];
@@ -946,7 +1060,8 @@ __global__ __launch_bounds__(NP8_ASSIGN_BLOCK) __attribute__((amdgpu_waves_per_e
             }
             if (__ballot(mine) == 0ull) continue;
             if (NP8_CLK_ON) clk_rows += (unsigned long long)nl0;
-            walk([&](int q) { return A.plist[(int64_t)j0 * A.ls + q]; }, nl0, mine, false);
+            walk([&](int q) { return A.plist[NP8_CHK((int64_t)j0 * A.ls + q, 0, (int64_t)A.kcap * A.ls)]; }, nl0, mine,
+                 false);
         }
     }
     const bool table_walk = __ballot(full && !defer) != 0ull;
@@ -956,39 +1071,70 @@ __global__ __launch_bounds__(NP8_ASSIGN_BLOCK) __attribute__((amdgpu_waves_per_e
 #undef NP8_ROWF
 #undef NP8_ROWJ
     NP8_CLK(3);
-    // the auxiliaries: np8_assign's two-level screen, then the exact fp64 draw for the lanes it cannot clear;
-    // a lane that picks an auxiliary makes a new-cluster request (appended below)
+    // the auxiliaries: the screen's three levels (0: the prefix call, above; 1: the auxiliary's call 0; 2: its call 1),
+    // then the exact fp64 draw for the lanes none of them clears; a lane that picks an auxiliary makes a new-cluster
+    // request (appended below)
     bool req = false;
     if (!defer) {
         const double logam = hyp[H::kLogam];
         const float thr = (float)(st.T - kSkip - logam);  // T only grows: conservative for every m
-        const float nyf = (float)ny, nuf = (float)hyp[H::kNu], rskf = (float)hyp[H::kRsk], cauxf = (float)hyp[H::kCaux];
+        const float nuf = (float)hyp[H::kNu], rskf = (float)hyp[H::kRsk], cauxf = (float)hyp[H::kCaux];
         constexpr bool has_call1 = Qa > 1;
         uint32_t need = 0u;
         const float thr_err = 1e-4f * fabsf(thr);
 #pragma unroll
         for (int m = 0; m < M; ++m)
-            if (!(ub1[m] + thr_err <= thr)) need |= 1u << m;
+            if (!(ub0[m] + thr_err <= thr)) need |= 1u << m;
         NP8_CLK(4);
+        if constexpr (kL0) {
 #pragma unroll 1
-        for (int m = 0; m < M; ++m) {
-            bool skip = ((need >> m) & 1u) == 0u;
-            if (__ballot(!skip) == 0ull) continue;  // wave-uniform: the common case
-            uint32_t w0[4], w1[4] = {0u, 0u, 0u, 0u};
-            philox_call(A.seed, ig, t, kStreamAux, (uint32_t)(m * Qa), w0);
-            const bool l2 = has_call1 && !skip;
-            if (l2) {  // level 2: the chi^2 terms of call 1
-                philox_call(A.seed, ig, t, kStreamAux, (uint32_t)(m * Qa + 1), w1);
-                float e1;
-                const float c1 = aux_screen_chi1<D>(w1, e1);
-                skip = aux_screen_ub<D>(w0, c1, e1, nyf, nuf, rskf, cauxf, thr) <= thr;
+            for (int m = 0; m < M; ++m) {
+                bool skip = ((need >> m) & 1u) == 0u;
+                if (__ballot(!skip) == 0ull) continue;  // wave-uniform: the common case
+                uint32_t w0[4], w1[4] = {0u, 0u, 0u, 0u};
+                philox_call(A.seed, ig, t, kStreamAux, (uint32_t)(m * Qa), w0);
+                aux_words0<D, M>(pre, m, w0);
+                if (!skip) skip = aux_screen_ub<D>(w0, 0.0f, 0.0f, nyf, nuf, rskf, cauxf, thr) <= thr;  // level 1
+                if (__ballot(!skip) == 0ull) continue;
+                const bool l2 = has_call1 && !skip;
+                if (l2) {  // level 2: the chi^2 terms of call 1
+                    philox_call(A.seed, ig, t, kStreamAux, (uint32_t)(m * Qa + 1), w1);
+                    aux_words1<D, M>(pre, m, w1);
+                    float e1;
+                    const float c1 = aux_screen_chi1<D>(w1, e1);
+                    skip = aux_screen_ub<D>(w0, c1, e1, nyf, nuf, rskf, cauxf, thr) <= thr;
+                }
+                if (!skip) {
+                    double v, xpar, chi2;
+                    aux_core_w<D>(A.seed, ig, t, m, hyp[H::kNu], v, xpar, chi2, w0, l2, w1, pre, M);
+                    const double lw = aux_loglik(sqrt(n2), v, xpar, chi2, D, hyp[H::kRsk], hyp[H::kCaux]) + logam;
+                    ensure_u(st, lw, A.seed, ig, t);
+                    pick_step(st, lw, K + m);
+                }
             }
-            if (!skip) {
-                double v, xpar, chi2;
-                aux_core_w<D>(A.seed, ig, t, m, hyp[H::kNu], v, xpar, chi2, w0, l2, w1);
-                const double lw = aux_loglik(ny, v, xpar, chi2, D, hyp[H::kRsk], hyp[H::kCaux]) + logam;
-                ensure_u(st, lw, A.seed, ig, t);
-                pick_step(st, lw, K + m);
+        } else {  // (the round-5 loop: level 1 was computed up front for every lane)
+            const uint32_t none[4] = {0u, 0u, 0u, 0u};
+            const float nyf1 = (float)ny;
+#pragma unroll 1
+            for (int m = 0; m < M; ++m) {
+                bool skip = ((need >> m) & 1u) == 0u;
+                if (__ballot(!skip) == 0ull) continue;  // wave-uniform: the common case
+                uint32_t w0[4], w1[4] = {0u, 0u, 0u, 0u};
+                philox_call(A.seed, ig, t, kStreamAux, (uint32_t)(m * Qa), w0);
+                const bool l2 = has_call1 && !skip;
+                if (l2) {  // level 2: the chi^2 terms of call 1
+                    philox_call(A.seed, ig, t, kStreamAux, (uint32_t)(m * Qa + 1), w1);
+                    float e1;
+                    const float c1 = aux_screen_chi1<D>(w1, e1);
+                    skip = aux_screen_ub<D>(w0, c1, e1, nyf1, nuf, rskf, cauxf, thr) <= thr;
+                }
+                if (!skip) {
+                    double v, xpar, chi2;
+                    aux_core_w<D>(A.seed, ig, t, m, hyp[H::kNu], v, xpar, chi2, w0, l2, w1, none, M);
+                    const double lw = aux_loglik(ny, v, xpar, chi2, D, hyp[H::kRsk], hyp[H::kCaux]) + logam;
+                    ensure_u(st, lw, A.seed, ig, t);
+                    pick_step(st, lw, K + m);
+                }
             }
         }
         req = st.pick >= K;
@@ -1013,7 +1159,7 @@ __global__ __launch_bounds__(NP8_ASSIGN_BLOCK) __attribute__((amdgpu_waves_per_e
     if (A.collect_r2) {  // np8_assign's radius collection, over the lanes not deferred
         // (a requester counts for its old cluster, in case the request is rejected: np8_assign's rule)
         const int32_t tr = (defer || req) ? jo : st.pick;
-        const double *e = cand + (int64_t)tr * CS;
+        const double *e = cand + (int64_t)NP8_CHK(tr, 0, K) * CS;
         double d2 = 0.0;
 #pragma unroll
         for (int a = 0; a < D; ++a) {
@@ -1030,12 +1176,13 @@ __global__ __launch_bounds__(NP8_ASSIGN_BLOCK) __attribute__((amdgpu_waves_per_e
 #pragma unroll
             for (int o = 32; o > 0; o >>= 1) d2 = fmax(d2, __shfl_xor(d2, o));
         } else {
-            wave_max_by_key(reinterpret_cast<unsigned long long *>(A.r2 + A.kcap), snew, d2, !defer);
+            wave_max_by_key(reinterpret_cast<unsigned long long *>(A.r2 + A.kcap), (int32_t)NP8_CHK(snew, 0, A.kcap), d2,
+                            !defer);
         }
         if (lane == (__ffsll((unsigned long long)__ballot(1)) - 1)) {  // the wave's record
             WaveR2 wr;
             wr.d2 = one ? d2 : 0.0;
-            wr.slot = one ? t0 : -1;
+            wr.slot = one ? (int32_t)NP8_CHK(t0, 0, A.kcap) : -1;
             wr.pad = 0;
             A.wr2[(p - A.p0) >> 6] = wr;
         }
@@ -1047,7 +1194,7 @@ __global__ __launch_bounds__(NP8_ASSIGN_BLOCK) __attribute__((amdgpu_waves_per_e
         int32_t *delta = reinterpret_cast<int32_t *>(A.rec + kRecHeaderBytes);
         const bool mover = !defer && snew != zi;
         wave_add_by_key(delta, zi, -1, mover);
-        wave_add_by_key(delta, snew, 1, mover);
+        wave_add_by_key(delta, (int32_t)NP8_CHK(snew, 0, A.kcap), 1, mover);
     }
     if (!defer && snew != zi) {
         A.z[il] = snew;
@@ -1068,7 +1215,7 @@ __global__ __launch_bounds__(NP8_ASSIGN_BLOCK) __attribute__((amdgpu_waves_per_e
     }
     const int qreq = wave_append(A.nreq, req);  // (requests are accepted by scan position, not arrival)
     if (req) {  // np8_assign's request with its payload, the auxiliary's (v, mu)
-        const int q = qreq;
+        const int q = (int)NP8_CHK(qreq, 0, A.req_cap);
         if (q < A.req_cap) {  // always: the area holds every item of the step
             // the item key and epoch read again here (volatile: not kept live from the top of the kernel -- they
             // were spilled to scratch on every lane, 16 MB of writes per C3 launch, for this rare path)
@@ -1077,7 +1224,7 @@ __global__ __launch_bounds__(NP8_ASSIGN_BLOCK) __attribute__((amdgpu_waves_per_e
             double *vm = A.vmu + (int64_t)q * (D + 1);
             double y0[D];
             whiten<D>(hyp, x, y0);
-            aux_params<D>(hyp, y0, ny, A.seed, igr, tr, st.pick - K, vm);
+            aux_params<D>(hyp, y0, kL0 ? norm_of<D>(y0) : ny, A.seed, igr, tr, st.pick - K, M, vm);
             Request r;
             r.pos = (int64_t)igr;  // synchronous sweep: scan position = item index
             r.i = (int64_t)igr;
@@ -1125,7 +1272,7 @@ __device__ __forceinline__ bool sort_needed(const SortArgs &S) {
 // ranges of the layout, clusters contiguous inside each).  ids = null: p is the local item itself.
 __device__ __forceinline__ int sort_key(const SortArgs &S, const int32_t *__restrict__ z, const int32_t *__restrict__ ids,
                                         int64_t p) {
-    const int32_t slot = z[p];
+    const int32_t slot = (int32_t)NP8_CHK(z[p], 0, S.kcap);
     if (S.nsub <= 1) return slot;
     const int64_t item = S.offset + (ids ? (int64_t)ids[p] : p);
     return (int)substep_of(S.seed, item, (uint32_t)S.nsub) * S.kcap + slot;
@@ -1355,7 +1502,7 @@ __device__ void prune_row(const double *__restrict__ cand, R2of R2of_slot, int32
     const int DP = D * (D + 1) / 2, CS = cand_stride(D), F = D + DP;
     const int lane = threadIdx.x & 63;
     const double *e0 = cand + (int64_t)k0 * CS;
-    const int slot0 = (int)e0[F + kFieldSlot];
+    const int slot0 = (int)NP8_CHK((int)e0[F + kFieldSlot], 0, kcap);
     const double R2 = R2of_slot(slot0);
     const double iso0 = e0[F + kFieldIso];
     const double base0 = e0[F + kFieldC] + e0[F + kFieldLogn1];
@@ -1448,7 +1595,7 @@ __device__ void frame_to_vmu(const FinArgs &F, const double *frame, int64_t i, i
     double y0[kMaxD], xi[kMaxD];
     for (int a = 0; a < D; ++a) y0[a] = frame[1 + a];
     double v, xpar, chi2;
-    aux_core_rt(F.seed, (uint64_t)i, t, m, D, hyp[D + DP + 3], v, xpar, chi2);
+    aux_core_rt(F.seed, (uint64_t)i, t, m, F.M, D, hyp[D + DP + 3], v, xpar, chi2);
     aux_xi<kMaxD>(F.seed, (uint64_t)i, t, m, D, y0, frame[0], xpar, chi2, xi);
     const double sc = fabs(v) * hyp[D + DP + 1];
     const double *LT = hyp + D + DP + 4;
@@ -1817,8 +1964,8 @@ __device__ int finalize_block(const FinArgs &F, unsigned char *smem) {
             }
         }
         for (int q = tid; q < A; q += kFinThreads) {
-            const Request r = *request_at(F, base, kidx[q]);
-            const int s = freeslot[q];
+            const Request r = *request_at(F, base, (int)NP8_CHK(kidx[q], 0, kReqMax * 64));
+            const int s = (int)NP8_CHK(freeslot[q], 0, kcap);
             if (F.prior == kPriorNiw || F.frame_payload) {
                 // built by np8_niw_aux_slots (NIW: O(D^3) per slot) or np8_frame_slots (the wide path's (v, mu)
                 // from the item frame): registers this one workgroup cannot spare
@@ -1837,11 +1984,11 @@ __device__ int finalize_block(const FinArgs &F, unsigned char *smem) {
                 F.pend_ll[2 * (int64_t)q + 1] = r.lpos;
             }
             cnt_s[s] = 1;
-            atomicSub(&cnt_s[r.zold], 1);  // a live slot (the requester is in it), never one of the free ones
+            atomicSub(&cnt_s[NP8_CHK(r.zold, 0, kcap)], 1);  // a live slot (the requester is in it), never a free one
             const int64_t item = key_item(r.i);
             if (item >= F.offset && item < F.offset + F.n_loc) {
                 F.z[item - F.offset] = s;
-                if (F.zs[0] && r.lpos >= 0) F.zs[0][r.lpos] = s;
+                if (F.zs[0] && r.lpos >= 0) F.zs[0][NP8_CHK(r.lpos, 0, F.n_loc)] = s;
             }
         }
     }
@@ -2546,11 +2693,43 @@ __global__ __launch_bounds__(256) void np8_loglik_matrix_kernel(AssignArgs A, co
     whiten<D>(A.hyp, x, y0);
     const double ny = norm_of<D>(y0);
     const uint32_t t = A.ctl->t_base + A.t;
-    for (int m = 0; m < M; ++m) out[r * (K + M) + K + m] = prior_aux_ll<D, PRIOR>(A.hyp, ny, A.seed, ig, t, m);
+    for (int m = 0; m < M; ++m) out[r * (K + M) + K + m] = prior_aux_ll<D, PRIOR>(A.hyp, ny, A.seed, ig, t, m, M);
+}
+
+// debug: the level-0 auxiliary bound np8_assign_fast screens with (aux_screen0_ub, without the threshold's own
+// margin term) for chosen items, out[r M + m]; tests/test_gpu_screen.py holds it above the exact log-likelihood
+template <int D, int M>
+__global__ __launch_bounds__(256) void np8_aux_bounds_kernel(AssignArgs A, const int64_t *__restrict__ idx, int64_t n,
+                                                             double *__restrict__ out) {
+    using H = HypView<D>;
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    const int64_t il = idx[r];
+    const uint64_t ig = (uint64_t)(A.offset + il);
+    const double *hyp = A.hyp;
+    double x[D], y0[D];
+#pragma unroll
+    for (int a = 0; a < D; ++a) x[a] = A.X[(int64_t)a * A.n_loc + il];
+    whiten<D>(hyp, x, y0);
+    double n2 = 0.0;
+#pragma unroll
+    for (int a = 0; a < D; ++a) n2 = fma(y0[a], y0[a], n2);
+    const float nyf = __builtin_amdgcn_sqrtf((float)n2);
+    const uint32_t t = A.ctl->t_base + A.t;
+    uint32_t pre[4];
+    aux_pre_call(A.seed, ig, t, pre);
+    float s_abs;
+    const float s0 = aux_screen0_s(nyf, (float)hyp[H::kPre], (float)hyp[H::kPre + 1], (float)hyp[H::kPre + 2],
+                                   (float)hyp[H::kPre + 3], D, s_abs);
+    const float rskf = (float)hyp[H::kRsk], cauxf = (float)hyp[H::kCaux];
+    for (int m = 0; m < M; ++m)
+        out[r * M + m] = (double)aux_screen0_ub<D, M>(pre, m, s0, s_abs, cauxf, 0.5f * rskf * rskf);
 }
 
 // ---- dispatch ----------------------------------------------------------------------------------------
-#ifdef NP8_EXP_ONLY_D8  // (A/B experiment builds, tools/ab_build.sh: the C3 instances only, a fast compile)
+#if defined(NP8_EXP_ONLY_D9)  // (debug builds: the D = 9 instances only)
+#define NP8_FOR_EACH_DM(X) X(9, 3)
+#elif defined(NP8_EXP_ONLY_D8)  // (A/B experiment builds, tools/ab_build.sh: the C3 instances only, a fast compile)
 #define NP8_FOR_EACH_DM(X) X(8, 3)
 #else
 #define NP8_FOR_EACH_DM(X) \
@@ -2643,8 +2822,9 @@ __global__ __launch_bounds__(256) void np8_fold_r2(const WaveR2 *__restrict__ wr
 #pragma unroll
     for (int u = 0; u < kFoldPer; ++u) {
         if (k0 + u >= n) break;
-        const WaveR2 r = wr2[k0 + u];
+        WaveR2 r = wr2[k0 + u];
         if (r.slot < 0) continue;
+        r.slot = (int32_t)NP8_CHK(r.slot, 0, kcap);
         const unsigned long long b = (unsigned long long)__double_as_longlong(r.d2);
         if (sl < 0 || sl == r.slot) {
             sl = r.slot;
@@ -2827,6 +3007,20 @@ hipError_t np8_launch_loglik_matrix(const AssignArgs &A, int D, int M, int prior
             hipLaunchKernelGGL((np8_loglik_matrix_kernel<d, m, kPriorReference>), grid, block, 0, s, A, idx, n, \
                                out);                                                                            \
         return hipGetLastError();                                                                               \
+    }
+    NP8_FOR_EACH_DM(X)
+#undef X
+    return hipErrorInvalidValue;
+}
+
+hipError_t np8_launch_aux_bounds(const AssignArgs &A, int D, int M, const int64_t *idx, int64_t n, double *out,
+                                 hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    const dim3 grid((unsigned)((n + 255) / 256)), block(256);
+#define X(d, m)                                                                                       \
+    if (D == d && M == m) {                                                                           \
+        hipLaunchKernelGGL((np8_aux_bounds_kernel<d, m>), grid, block, 0, s, A, idx, n, out);         \
+        return hipGetLastError();                                                                     \
     }
     NP8_FOR_EACH_DM(X)
 #undef X

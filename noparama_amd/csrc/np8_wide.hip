@@ -86,7 +86,7 @@ __device__ void wide_frame_payload(const double *__restrict__ hyp, int D, const 
 
 template <int PRIOR>
 __device__ __forceinline__ double wide_aux_ll(const double *__restrict__ hyp, int D, double ny, uint64_t seed,
-                                              uint64_t ig, uint32_t t, int m) {
+                                              uint64_t ig, uint32_t t, int m, int M) {
     const int DP = D * (D + 1) / 2;
     const double caux = hyp[D + DP], rsk = hyp[D + DP + 1], nu = hyp[D + DP + 3];
     if constexpr (PRIOR == kPriorNiw) {
@@ -95,7 +95,7 @@ __device__ __forceinline__ double wide_aux_ll(const double *__restrict__ hyp, in
         return niw_aux_loglik(ny, sumlog, b00, chi, z1, rsk, caux);
     } else {
         double v, xpar, chi2;
-        aux_core_rt(seed, ig, t, m, D, nu, v, xpar, chi2);
+        aux_core_rt(seed, ig, t, m, M, D, nu, v, xpar, chi2);
         return aux_loglik(ny, v, xpar, chi2, D, rsk, caux);
     }
 }
@@ -564,7 +564,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NP8_WIDE_WA
                 const double smax = hyp[D + DP + 4 + DP];
                 v = niw_aux_ll_screened(A.seed, ig, t, m, D, nu, ny, rsk, caux, smax, st.T - kSkip - logam) + logam;
             } else {
-                v = wide_aux_ll<PRIOR>(hyp, D, ny, A.seed, ig, t, m) + logam;
+                v = wide_aux_ll<PRIOR>(hyp, D, ny, A.seed, ig, t, m, M) + logam;
             }
 #pragma unroll
             for (int k = 0; k < M; ++k) lwa[k] = (k == m) ? v : lwa[k];  // no dynamic register index
@@ -923,7 +923,7 @@ __global__ __launch_bounds__(64) void np8_loglik_matrix_wide(AssignArgs A, WideA
     const double ny = wide_whiten_norm<DT>(A.uw, xf);
     const uint32_t t = A.ctl->t_base + A.t;
     for (int m = 0; m < M; ++m)
-        out[r * (K + M) + K + m] = wide_aux_ll<PRIOR>(A.hyp, D, ny, A.seed, (uint64_t)(A.offset + il), t, m);
+        out[r * (K + M) + K + m] = wide_aux_ll<PRIOR>(A.hyp, D, ny, A.seed, (uint64_t)(A.offset + il), t, m, M);
 }
 
 // ---- max likelihood on the matrix cores -------------------------------------------------------------

@@ -162,6 +162,7 @@ def lib():
         "np8_sync": ([vp], i32),
         "np8_get_state": ([vp, i32, vp, vp, vp, vp, vp], i32),
         "np8_loglik_matrix": ([vp, vp, i64, vp], i32),
+        "np8_aux_bounds": ([vp, vp, i64, vp], i32),
         "np8_total_loglik": ([vp, P(d)], i32),
         "np8_pick_batch": ([vp, vp, i32, vp, i64, vp], i32),
         "np8_stats": ([vp, P(Stats)], i32),
@@ -360,6 +361,13 @@ class NealAlgorithm8:
     @property
     def K(self):
         return self.stats()["K"]
+
+    def aux_bounds(self, idx):
+        """Debug: the level-0 screen's upper bound of each listed item's M auxiliary log-likelihoods (n x M)."""
+        idx = np.ascontiguousarray(idx, dtype=np.int64)
+        out = np.zeros((idx.size, self.M))
+        self._check(lib().np8_aux_bounds(self._h, _p(idx), idx.size, _p(out)))
+        return out
 
     def loglik_matrix(self, idx):
         idx = np.ascontiguousarray(idx, dtype=np.int64)

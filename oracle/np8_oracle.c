@@ -731,10 +731,37 @@ static inline int aux_calls(int D) {
 }
 static inline int dir_calls(int D) { return (D + 3) / 4; }
 
+/* The screen prefixes (round 6; noparama_amd/csrc/np8_device.h aux_pre_bits, DESIGN.md "Auxiliary screen"), D <= 8: call 0
+ * of stream AUX_PRE (i = item key) holds the leading b bits of the first P = min(k, 3) chi^2 uniforms of every
+ * auxiliary, b = min(16, floor(128 / (M P))); field f = m P + j is bits [b f, b f + b) of the call's four words
+ * (word 0 = bits 0..31).  Chi^2 uniform j < P of auxiliary m takes the word (field << (32 - b)) | (its own word &
+ * (2^(32 - b) - 1)).  (A restatement of the specification; the reference draws from an unseeded engine, so only
+ * the distribution is the reference's: uniform 32-bit words, independent of the rest.) */
+#define NP8O_PRE_MAX_D 8 /* prefixes for D <= 8 only (the device's kPreMaxD) */
+static inline int aux_pre_n(int D) {
+    const int k = (D - 1) / 2;
+    return D > NP8O_PRE_MAX_D ? 0 : (k < 3 ? k : 3);
+}
+static inline int aux_pre_bits(int D, int M) {
+    const int P = aux_pre_n(D);
+    if (P <= 0 || M <= 0) return 0;
+    const int b = 128 / (M * P);
+    return b > 16 ? 16 : b;
+}
+static uint32_t aux_chi_word(const uint32_t pre[4], uint32_t w, int m, int j, int D, int M) {
+    const int P = aux_pre_n(D), b = aux_pre_bits(D, M);
+    if (j >= P || b <= 0) return w;
+    const int lo = b * (m * P + j), wi = lo >> 5, sh = lo & 31;
+    const uint64_t v = (((uint64_t)(wi < 3 ? pre[wi + 1] : 0u)) << 32 | pre[wi]) >> sh;
+    const uint32_t field = (uint32_t)v & ((1u << b) - 1u);
+    return (field << (32 - b)) | (w & ((1u << (32 - b)) - 1u));
+}
+
 static void aux_core(const np8o_ctx *c, uint64_t i, uint32_t t, int m, double *v, double *xpar, double *chi2) {
     const int D = c->D, Qa = aux_calls(D), k = (D - 1) / 2, odd = (D - 1) & 1;
     const uint32_t base = (uint32_t)(m * Qa);
-    uint32_t w[4], w1[4] = {0u, 0u, 0u, 0u}, wc[4] = {0u, 0u, 0u, 0u};
+    uint32_t w[4], w1[4] = {0u, 0u, 0u, 0u}, wc[4] = {0u, 0u, 0u, 0u}, pre[4] = {0u, 0u, 0u, 0u};
+    if (aux_pre_n(D) > 0) philox_call(c->cfg.seed, i, t, NP8O_STREAM_AUX_PRE, 0u, pre);
     philox_call(c->cfg.seed, i, t, NP8O_STREAM_AUX, base, w);
     {
         const double r = sqrt(-2.0 * np8o_log_pos(u32_01(w[0])));
@@ -758,9 +785,9 @@ static void aux_core(const np8o_ctx *c, uint64_t i, uint32_t t, int m, double *v
     for (int j = 0; j < k; ++j) {
         uint32_t word;
         if (j < 2) {
-            word = w[2 + j];
+            word = aux_chi_word(pre, w[2 + j], m, j, D, c->M);
         } else if (j < 4) {
-            word = w1[j];
+            word = aux_chi_word(pre, w1[j], m, j, D, c->M);
         } else {
             if (((j - 4) & 3) == 0)
                 philox_call(c->cfg.seed, i, t, NP8O_STREAM_AUX, base + 2u + (uint32_t)((j - 4) >> 2), wc);

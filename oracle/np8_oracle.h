@@ -56,7 +56,8 @@ enum {
     NP8O_STREAM_AUX_NIW = 8, /* NIW prior: the auxiliary's Bartlett chi^2 draws, chi^2_{D-1}, z_1 */
     NP8O_STREAM_SM_THETA = 9,  /* split-merge: G0 draw of a split's new cluster (i = attempt) */
     NP8O_STREAM_SM_ALLOC = 10, /* split-merge: SAMS allocation uniforms (i = attempt, call = member rank) */
-    NP8O_STREAM_SM_ACCEPT = 11 /* split-merge: acceptance uniform (i = attempt) */
+    NP8O_STREAM_SM_ACCEPT = 11, /* split-merge: acceptance uniform (i = attempt) */
+    NP8O_STREAM_AUX_PRE = 12   /* reference prior: the auxiliaries' chi^2 prefixes (i = item, call 0) */
 };
 
 /* Base measure G0 (DESIGN.md "Priors").

@@ -52,3 +52,39 @@ def test_screen_has_no_violations_near_v_zero(D, nu):
     finally:
         O.set_threads(1)
         g.close()
+
+
+@pytest.mark.parametrize("D,M,nu", [(3, 3, 4.0), (5, 3, 4.0), (8, 1, 4.0), (8, 3, 4.0), (8, 4, 16.0), (16, 3, 4.0),
+                                    (16, 2, 40.0)])
+def test_level0_bound_holds(D, M, nu):
+    """Level 0 of the auxiliary screen (round 6, np8_kernels.hip aux_screen0_ub): from the item's prefix call alone,
+    an upper bound of every auxiliary's exact log-likelihood -- for items near mu0 (where it must give way: +inf or a
+    large bound), at the C3 scale of distances and far beyond, and for nu large against D (|v| reaching 0).  Each bound
+    (without the caller's 1e-4 |threshold| term) lies above the exact value np8_loglik_matrix computes; at the C3
+    distances it clears most auxiliaries by far more than the skip threshold."""
+    rng = np.random.default_rng(100 + D + M)
+    n = 6000
+    mu0 = np.full(D, 6.0)
+    scale = np.concatenate([np.full(n // 6, 0.01), np.full(n // 6, 0.3), np.full(n // 6, 3.0), np.full(n // 6, 12.0),
+                            np.full(n // 6, 40.0), np.full(n - 5 * (n // 6), 400.0)])
+    X = mu0 + scale[:, None] * rng.normal(size=(n, D))
+    z = np.zeros(n, np.int32)
+    g = NealAlgorithm8(D, M=M, seed=5 + D, device=0, kappa=1.0 / 500, nu=nu, mu0=mu0, Lambda=0.01 * np.eye(D))
+    try:
+        g.set_data(X)
+        g.set_state(z, mu0[None] + 1.0, np.eye(D)[None])
+        idx = np.arange(n)
+        for _ in range(2):  # two epochs: fresh draws
+            ll = g.loglik_matrix(idx)[:, -M:]
+            ub = g.aux_bounds(idx)
+            assert np.all(np.isfinite(ll))
+            bad = ll > ub
+            assert not bad.any(), (ll[bad][:5], ub[bad][:5])
+            g.sweep(1)
+        if D > 8:  # no prefixes above D = 8 (np8_device.h kPreMaxD): no level-0 bound, the round-5 screen instead
+            assert np.all(np.isinf(ub))
+        elif D == 8 and nu == 4.0:  # the C3-like regime (|x - mu0| ~ 12-40): the bound sits far below the own cluster
+            far = (scale >= 12.0) & (scale <= 40.0)
+            assert np.mean(ub[far] < -200.0) > 0.9
+    finally:
+        g.close()
