@@ -634,11 +634,12 @@ int alloc_records(np8_ctx *c) {
     }
     // compact records of the RCCL path's sweep graphs (the same layout with c_cap requests), and of the host
     // transport's compact steps (np8_step_local_compact)
-    if (exch && c->c_cap > 0 && !c->wide) {
+    // (the wide path: the host transport's compact steps only -- its sweep graphs exchange the full records)
+    if (exch && c->c_cap > 0) {
         c->c_bytes = record_bytes(c->kcap, c->c_cap, c->D);
         if ((r = dalloc(c, &c->crec, (size_t)c->c_bytes)) || (r = dalloc(c, &c->cgath, (size_t)c->c_bytes * c->world)))
             return r;
-        c->compact_on = c->comm != nullptr;
+        c->compact_on = c->comm != nullptr && !c->wide;
     }
     return NP8_OK;
 }
@@ -2961,10 +2962,11 @@ int np8_step_merge(np8_ctx *c, const void *records, int32_t world) {
 // first c_cap requests, its header counting all of them), the halt decision np8_finalize takes from the gathered
 // headers (alike on every rank), and the resumption of a halted step with the full records.
 namespace {
-// the lean kernel takes every lane of the step (no deferred lane, no queue launch) and writes the compact record
+// the step's assign writes the compact record for every lane: the lean narrow kernel when it takes every lane (no
+// deferred lane, no queue launch), or np8_assign_wide (any prior, any parameter update)
 bool host_compact_ok(const np8_ctx *c) {
-    return c->crec && !c->comm && c->world > 1 && !c->wide && c->diag_U && !c->fast_off &&
-           c->prior == NP8_PRIOR_REFERENCE && c->rows_iso && !c->count_eval && !c->queue_on && c->n_loc > 0;
+    if (!c->crec || c->comm || c->world <= 1 || c->count_eval || c->n_loc <= 0) return false;
+    return c->wide || (c->diag_U && !c->fast_off && c->prior == NP8_PRIOR_REFERENCE && c->rows_iso && !c->queue_on);
 }
 }  // namespace
 

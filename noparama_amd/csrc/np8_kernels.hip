@@ -434,14 +434,26 @@ __device__ __forceinline__ void assign_item(const AssignArgs &A, const int64_t p
                         const int j = lst[q];  // uniform across the group: scalar loads
                         const double *e = cand + (int64_t)j * CS;
                         const double lw = cand_ll<D>(e, x) + e[F + kFieldLogn];
+#ifdef NP8_EXP_SKIPCOUNT  // (experiment: pick_evals counts the listed rows no walking lane of the group needs,
+                          //  iso counts the group's listed rows, once per group)
+                        if constexpr (COUNT) {
+                            const uint64_t bn = __ballot(lw - st.T > -kSkip - 2.0);
+                            const bool lead = (threadIdx.x & 63) == (__ffsll((unsigned long long)__ballot(1)) - 1);
+                            npick_lane += (lead && bn == 0ull) ? 1 : 0;
+                            niso_lane += lead ? 1 : 0;
+                        }
+#else
                         if constexpr (COUNT) npick_lane += (lw - st.T > -kSkip) ? 1 : 0;
+#endif
                         ensure_u(st, lw, A.seed, ig, t);
                         pick_step(st, lw, j);
                         pslot = (st.pick == j) ? (int32_t)e[F + kFieldSlot] : pslot;
                         if constexpr (COUNT) {
                             nq_lane += 1;
                             nlist_lane += 1;
+#ifndef NP8_EXP_SKIPCOUNT
                             niso_lane += (e[F + kFieldIso] > 0.0) ? 1 : 0;
+#endif
                         }
                     }
                 }
@@ -1771,6 +1783,7 @@ __device__ int finalize_block(const FinArgs &F, unsigned char *smem) {
         if (tid == 0) {
             F.ctl->halt = 1;
             F.ctl->halt_t = F.t;
+            F.ctl->n_pend = 0;  // (the NIW / wide slot kernels after this finalize: no accepted request to build)
             if (F.mirror) {
                 F.mirror[1] = (int32_t)F.t;
                 F.mirror[0] = 1;

@@ -855,6 +855,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NP8_WIDE_WA
             A.req[q] = r;
             double *vmu = A.vmu + (int64_t)q * (D + 1);
             wide_frame_payload(hyp, D, X, n, xr, vmu);
+            if (q < A.ccap) {  // compact exchange (np8_step_local_compact): the first ccap requests in the compact record
+                A.creq[q] = r;
+                for (int a = 0; a <= D; ++a) A.cvmu[(int64_t)q * (D + 1) + a] = vmu[a];
+            }
         }
     }
 }
