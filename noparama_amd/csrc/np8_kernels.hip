@@ -784,6 +784,22 @@ __device__ __forceinline__ Fx fx_readlane(Fx a, int l) {
 // items' log-likelihoods under their new labels -- the values np8_loglik would compute after the step, operation for
 // operation (the walk's quadratic forms are the table form's isotropic one) -- in a separate instance, so that the
 // other sweeps carry none of its registers.
+// A field of np8_assign_fast's argument (the kernel's only explicit argument: offset 0 of the kernarg segment) read where
+// it is used: a scalar load behind an empty asm barrier on the segment pointer, so that it is neither hoisted into the
+// entry block nor held (and spilled to VGPR lanes, a v_writelane/v_readlane pair each) across the kernel
+#ifdef NP8_EXP_EARLY_ARGS  // (A/B: the compiler's own placement)
+#define NP8_LATE(f) (A.f)
+#else
+template <class T>
+__device__ __forceinline__ T late_arg(size_t off) {
+    typedef const __attribute__((address_space(4))) char *KP;
+    KP kp = (KP)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(kp));
+    return *(const __attribute__((address_space(4))) T *)(kp + off);
+}
+#define NP8_LATE(f) late_arg<decltype(AssignArgs::f)>(offsetof(AssignArgs, f))
+#endif
+
 template <int D, int M, int PRIOR, bool COUNT, bool LL>
 __global__ __launch_bounds__(NP8_ASSIGN_BLOCK) __attribute__((amdgpu_waves_per_eu(LL ? NP8_FAST_WAVES_LL : NP8_FAST_WAVES))) void np8_assign_fast(AssignArgs A) {
     using H = HypView<D>;
@@ -1156,19 +1172,19 @@ __global__ __launch_bounds__(NP8_ASSIGN_BLOCK) __attribute__((amdgpu_waves_per_e
     // for np8_assign's queue mode; nothing else is written for them
     const uint64_t db = __ballot(defer);
     if (db) {  // rare (rows that are not isotropic): the wave lists itself for np8_assign's queue mode
-        if (A.no_queue) {  // the host left the queue kernel out (every row isotropic): must not happen
-            if (lane == (__ffsll((unsigned long long)db) - 1)) atomicOr(&A.ctl->err, kErrQueue);
+        if (NP8_LATE(no_queue)) {  // the host left the queue kernel out (every row isotropic): must not happen
+            if (lane == (__ffsll((unsigned long long)db) - 1)) atomicOr(&NP8_LATE(ctl)->err, kErrQueue);
             return;
         }
-        const int64_t wv = (p - A.p0) >> 6;
-        if (defer) A.queue_out[wv * 64 + __popcll(db & ((1ull << lane) - 1ull))] = (int32_t)p;
+        const int64_t wv = (p - NP8_LATE(p0)) >> 6;
+        if (defer) NP8_LATE(queue_out)[wv * 64 + __popcll(db & ((1ull << lane) - 1ull))] = (int32_t)p;
         if (lane == (__ffsll((unsigned long long)db) - 1)) {
-            A.qcount[wv] = __popcll(db);
-            A.qlist[atomicAdd(&A.ctl->qwaves, 1u)] = (int32_t)wv;
+            NP8_LATE(qcount)[wv] = __popcll(db);
+            NP8_LATE(qlist)[atomicAdd(&NP8_LATE(ctl)->qwaves, 1u)] = (int32_t)wv;
         }
     }
     const int32_t snew = req ? zi : pslot;  // a lane not deferred picked an existing row or stays (request)
-    if (A.collect_r2) {  // np8_assign's radius collection, over the lanes not deferred
+    if (NP8_LATE(collect_r2)) {  // np8_assign's radius collection, over the lanes not deferred
         // (a requester counts for its old cluster, in case the request is rejected: np8_assign's rule)
         const int32_t tr = (defer || req) ? jo : st.pick;
         const double *e = cand + (int64_t)NP8_CHK(tr, 0, K) * CS;
@@ -1188,28 +1204,28 @@ __global__ __launch_bounds__(NP8_ASSIGN_BLOCK) __attribute__((amdgpu_waves_per_e
 #pragma unroll
             for (int o = 32; o > 0; o >>= 1) d2 = fmax(d2, __shfl_xor(d2, o));
         } else {
-            wave_max_by_key(reinterpret_cast<unsigned long long *>(A.r2 + A.kcap), (int32_t)NP8_CHK(snew, 0, A.kcap), d2,
+            wave_max_by_key(reinterpret_cast<unsigned long long *>(NP8_LATE(r2) + NP8_LATE(kcap)), (int32_t)NP8_CHK(snew, 0, NP8_LATE(kcap)), d2,
                             !defer);
         }
         if (lane == (__ffsll((unsigned long long)__ballot(1)) - 1)) {  // the wave's record
             WaveR2 wr;
             wr.d2 = one ? d2 : 0.0;
-            wr.slot = one ? (int32_t)NP8_CHK(t0, 0, A.kcap) : -1;
+            wr.slot = one ? (int32_t)NP8_CHK(t0, 0, NP8_LATE(kcap)) : -1;
             wr.pad = 0;
-            A.wr2[(p - A.p0) >> 6] = wr;
+            NP8_LATE(wr2)[(p - NP8_LATE(p0)) >> 6] = wr;
         }
     }
     const uint64_t mv = __ballot(!defer && snew != zi);
     if (mv && lane == (__ffsll((unsigned long long)__ballot(1)) - 1))
-        atomicAdd(reinterpret_cast<unsigned long long *>(&A.ctl->moved), (unsigned long long)__popcll(mv));
+        atomicAdd(reinterpret_cast<unsigned long long *>(&NP8_LATE(ctl)->moved), (unsigned long long)__popcll(mv));
     {
-        int32_t *delta = reinterpret_cast<int32_t *>(A.rec + kRecHeaderBytes);
+        int32_t *delta = reinterpret_cast<int32_t *>(NP8_LATE(rec) + kRecHeaderBytes);
         const bool mover = !defer && snew != zi;
         wave_add_by_key(delta, zi, -1, mover);
-        wave_add_by_key(delta, (int32_t)NP8_CHK(snew, 0, A.kcap), 1, mover);
+        wave_add_by_key(delta, (int32_t)NP8_CHK(snew, 0, NP8_LATE(kcap)), 1, mover);
     }
     if (!defer && snew != zi) {
-        A.z[il] = snew;
+        NP8_LATE(z)[il] = snew;
         zs[p] = snew;
     }
     if constexpr (LL) {  // the wave's exact sum (a requester counts under its old slot)
@@ -1223,20 +1239,20 @@ __global__ __launch_bounds__(NP8_ASSIGN_BLOCK) __attribute__((amdgpu_waves_per_e
             for (uint64_t m = act; m; m &= m - 1ull) s = fx_add(s, fx_readlane(v, __ffsll((unsigned long long)m) - 1));
             v = s;
         }
-        if (lane == __ffsll((unsigned long long)act) - 1) A.llpart[(p - A.p0) >> 6] = v;
+        if (lane == __ffsll((unsigned long long)act) - 1) NP8_LATE(llpart)[(p - NP8_LATE(p0)) >> 6] = v;
     }
-    const int qreq = wave_append(A.nreq, req);  // (requests are accepted by scan position, not arrival)
+    const int qreq = wave_append(NP8_LATE(nreq), req);  // (requests are accepted by scan position, not arrival)
     if (req) {  // np8_assign's request with its payload, the auxiliary's (v, mu)
-        const int q = (int)NP8_CHK(qreq, 0, A.req_cap);
-        if (q < A.req_cap) {  // always: the area holds every item of the step
+        const int q = (int)NP8_CHK(qreq, 0, NP8_LATE(req_cap));
+        if (q < NP8_LATE(req_cap)) {  // always: the area holds every item of the step
             // the item key and epoch read again here (volatile: not kept live from the top of the kernel -- they
             // were spilled to scratch on every lane, 16 MB of writes per C3 launch, for this rare path)
-            const uint64_t igr = (uint64_t)(A.offset + reinterpret_cast<const volatile int32_t *>(ids)[p]);
-            const uint32_t tr = reinterpret_cast<const volatile Ctl *>(A.ctl)->t_base + A.t;
-            double *vm = A.vmu + (int64_t)q * (D + 1);
+            const uint64_t igr = (uint64_t)(NP8_LATE(offset) + reinterpret_cast<const volatile int32_t *>(ids)[p]);
+            const uint32_t tr = reinterpret_cast<const volatile Ctl *>(NP8_LATE(ctl))->t_base + NP8_LATE(t);
+            double *vm = NP8_LATE(vmu) + (int64_t)q * (D + 1);
             double y0[D];
             whiten<D>(hyp, x, y0);
-            aux_params<D>(hyp, y0, kL0 ? norm_of<D>(y0) : ny, A.seed, igr, tr, st.pick - K, M, vm);
+            aux_params<D>(hyp, y0, kL0 ? norm_of<D>(y0) : ny, NP8_LATE(seed), igr, tr, st.pick - K, M, vm);
             Request r;
             r.pos = (int64_t)igr;  // synchronous sweep: scan position = item index
             r.i = (int64_t)igr;
@@ -1248,24 +1264,24 @@ __global__ __launch_bounds__(NP8_ASSIGN_BLOCK) __attribute__((amdgpu_waves_per_e
             r.dll.hi = 0;
             if (LL) {  // ll under the slot np8_finalize would build from (v, mu) (write_new_slot), as np8_loglik evaluates it
                 const double v = vm[0], v2 = v * v;
-                const double iso_n = A.gp0 / v2, c_n = fma(-(double)D, log_pos(fabs(v)), hyp[H::kCaux]);
+                const double iso_n = NP8_LATE(gp0) / v2, c_n = fma(-(double)D, log_pos(fabs(v)), hyp[H::kCaux]);
                 double s2 = (x[0] - vm[1]) * (x[0] - vm[1]);
 #pragma unroll
                 for (int a = 1; a < D; ++a) s2 = fma(x[a] - vm[1 + a], x[a] - vm[1 + a], s2);
                 r.dll = fx_add(fx_of(fma(-0.5, s2 * iso_n, c_n)), fx_neg(fx_of(ll_own)));
             }
-            A.req[q] = r;
-            if (q < A.ccap) {  // compact exchange: the record the ranks all-gather holds the first ccap requests too
-                A.creq[q] = r;
-                for (int a = 0; a <= D; ++a) A.cvmu[(int64_t)q * (D + 1) + a] = vm[a];
+            NP8_LATE(req)[q] = r;
+            if (q < NP8_LATE(ccap)) {  // compact exchange: the record the ranks all-gather holds the first ccap requests too
+                NP8_LATE(creq)[q] = r;
+                for (int a = 0; a <= D; ++a) NP8_LATE(cvmu)[(int64_t)q * (D + 1) + a] = vm[a];
             }
         }
     }
     if (snap) {  // the rest of the pending snapshot: counts and parameters as the check's finalize left them
-        const int64_t g = p - A.p0, ng = A.p1 - A.p0;
-        for (int64_t k = g; k < A.kcap; k += ng) A.cnt_best[k] = A.cnt[k];
-        for (int64_t k = g; k < (int64_t)A.kcap * D; k += ng) A.mu_best[k] = A.slot_mu[k];
-        for (int64_t k = g; k < (int64_t)A.kcap * D * D; k += ng) A.sigma_best[k] = A.slot_sigma[k];
+        const int64_t g = p - NP8_LATE(p0), ng = NP8_LATE(p1) - NP8_LATE(p0);
+        for (int64_t k = g; k < NP8_LATE(kcap); k += ng) NP8_LATE(cnt_best)[k] = NP8_LATE(cnt)[k];
+        for (int64_t k = g; k < (int64_t)NP8_LATE(kcap) * D; k += ng) NP8_LATE(mu_best)[k] = NP8_LATE(slot_mu)[k];
+        for (int64_t k = g; k < (int64_t)NP8_LATE(kcap) * D * D; k += ng) NP8_LATE(sigma_best)[k] = NP8_LATE(slot_sigma)[k];
     }
     NP8_CLK(6);
 }
