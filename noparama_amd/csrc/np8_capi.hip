@@ -79,6 +79,7 @@ struct np8_ctx {
     // wide path (NP8_CONTRACT_F32_MFMA, D in {32, 48, 64}): fp32 items in X/Xs, fp32 MFMA contraction
     int contraction = NP8_CONTRACT_F64;
     bool wide = false;
+    bool rt = false;  // the fp64 kernels with D and M at run time (np8_rt.hip): a (D, M) without a templated instance
     float *wA = nullptr, *wfrag = nullptr, *wmu = nullptr;
     int32_t *wdirty = nullptr;
     double *lam_lo = nullptr, *wdist = nullptr;  // wide-path candidate pruning (np8_wide_dist)
@@ -1009,9 +1010,9 @@ int launch_finalize(np8_ctx *c, const unsigned char *recs, int world, int prune 
     // the conditional form (the default): the lists of the last build stay when finalize finds every count within
     // kListSlack of it -- the frozen reference-prior sweep's step with valid lists; a rebuild then costs the one
     // workgroup what np8_prune does in parallel, so steps after which the lists are stale anyway keep np8_prune
-    const bool cond = !c->tailcond_off && !c->churn && prune >= 0 && !c->gather && !c->wide &&
+    const bool cond = !c->tailcond_off && !c->churn && prune >= 0 && !c->gather && !c->wide && !c->rt &&
                       c->prior == NP8_PRIOR_REFERENCE && c->param_update == NP8_PARAM_FROZEN && c->lists_valid;
-    const bool tail = cond || (!c->fuse_off && prune >= 0 && !c->gather && !c->wide && c->prior == NP8_PRIOR_REFERENCE);
+    const bool tail = cond || (!c->fuse_off && prune >= 0 && !c->gather && !c->wide && !c->rt && c->prior == NP8_PRIOR_REFERENCE);
     if (tail) {  // finalize (+ lists) in one launch
         TailArgs T;
         std::memset(&T, 0, sizeof(T));
@@ -1034,7 +1035,7 @@ int launch_finalize(np8_ctx *c, const unsigned char *recs, int world, int prune 
     }
     if (c->gather)  // the step's radius records (any order with finalize: both only raise the gathered radii)
         HIPC(c, np8_launch_fold_r2(c->wr2, c->assign_waves, c->r2, c->kcap, c->ctl, c->stream));
-    if (prune >= 0 && !c->fp_off && !c->wide && c->prior == NP8_PRIOR_REFERENCE) {
+    if (prune >= 0 && !c->fp_off && !c->wide && !c->rt && c->prior == NP8_PRIOR_REFERENCE) {
         // finalize and the lists in one launch, the lists still one per wave over several workgroups
         PruneArgs P = prune_args(c, prune == 1);
         HIPC(c, np8_launch_fin_prune(F, P, c->stream));
@@ -1081,7 +1082,7 @@ int launch_assign(np8_ctx *c, int64_t p0, int64_t p1, const int64_t *order, bool
     c->assign_waves = (p1 - p0 + 63) / 64;
     // the fast kernel over the whole sweep, every row isotropic: it can fold the max-likelihood check in (frozen
     // parameters: the labels after the step are what the check scores) and take a pending snapshot along
-    const bool fast = !c->wide && c->diag_U && !c->fast_off && c->prior == NP8_PRIOR_REFERENCE && A.sorted && !order &&
+    const bool fast = !c->wide && !c->rt && c->diag_U && !c->fast_off && c->prior == NP8_PRIOR_REFERENCE && A.sorted && !order &&
                       !use_perm;
     const bool whole = fast && c->substeps == 1 && p0 == 0 && p1 == c->n_loc && c->rows_iso && !A.count_eval &&
                        !c->queue_on && (c->world == 1 || c->comm) && !c->host_exch_step;
@@ -1123,7 +1124,7 @@ int launch_assign(np8_ctx *c, int64_t p0, int64_t p1, const int64_t *order, bool
         }
         HIPC(c, np8_launch_assign_wide(A, c->D, c->M, c->prior, c->stream));
     }
-    else if (c->diag_U && !c->fast_off && c->prior == NP8_PRIOR_REFERENCE && A.sorted && !order && !use_perm) {
+    else if (!c->rt && c->diag_U && !c->fast_off && c->prior == NP8_PRIOR_REFERENCE && A.sorted && !order && !use_perm) {
         // the lean kernel for every lane, then the full one over the lanes it deferred (ctl->qn)
         A.queue_out = c->queue;
         A.qcount = c->qcount;
@@ -1768,10 +1769,17 @@ int np8_create_sized(np8_ctx **out, const np8_config *cfg_in, size_t cfg_bytes) 
         delete c;
         return NP8_ERR_ARG;
     }
-    if (!np8_supported(c->D, c->M) && !(cfg->contraction == NP8_CONTRACT_F32_MFMA && np8_wide_supported(c->D, c->M))) {
+    // F64 at a (D, M) without a templated instance (16 < D <= kMaxD, or a rarer M): the run-time-D kernels, reference
+    // prior, frozen parameters
+    const bool rt = cfg->contraction == NP8_CONTRACT_F64 && !np8_supported(c->D, c->M) &&
+                    np8_rt_supported(c->D, c->M, kPriorReference) && cfg->prior == NP8_PRIOR_REFERENCE &&
+                    cfg->param_update == NP8_PARAM_FROZEN;
+    if (!np8_supported(c->D, c->M) && !rt &&
+        !(cfg->contraction == NP8_CONTRACT_F32_MFMA && np8_wide_supported(c->D, c->M))) {
         delete c;
         return NP8_ERR_ARG;
     }
+    c->rt = rt;
     c->DP = packed_size(c->D);
     c->DT = (cfg->contraction == NP8_CONTRACT_F32_MFMA) ? wide_dt(c->D) : c->D;
     c->CS = cand_stride(c->D);
@@ -3147,8 +3155,8 @@ static int split_merge_sweeps(np8_ctx *c, int32_t n_sweeps, bool triadic) {
     if (int r_ = settle(c)) return r_;  // a sharded replay still unchecked (np8_sweep)
     if (!c->have_state) return fail(c, NP8_ERR_STATE, std::string(who) + ": no state (np8_set_state/np8_init_random)");
     if (c->world > 1) return fail(c, NP8_ERR_ARG, std::string(who) + ": split-merge runs on one rank");
-    if (c->wide || c->prior != NP8_PRIOR_REFERENCE)
-        return fail(c, NP8_ERR_ARG, std::string(who) + ": needs the reference prior and the fp64 contraction");
+    if (c->wide || c->rt || c->prior != NP8_PRIOR_REFERENCE)
+        return fail(c, NP8_ERR_ARG, std::string(who) + ": needs the reference prior and the fp64 contraction at D <= 16");
     if (c->n_loc > INT32_MAX) return fail(c, NP8_ERR_ARG, std::string(who) + ": at most 2^31-1 items");
     int r = flush_snapshot(c);
     if (r) return r;

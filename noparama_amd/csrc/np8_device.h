@@ -13,7 +13,7 @@ namespace np8 {
 constexpr double kLog2Pi = 1.8378770664093454835606594728112;
 constexpr double kTwoPi = 6.283185307179586476925286766559;
 constexpr int kReqMax = 4096;     // new-cluster requests one finalize can accept
-constexpr int kMaxD = 80;
+constexpr int kMaxD = 128;  // (the fp64 path with D at run time, np8_rt.hip; the fp32 wide path stops at 80)
 constexpr int kMaxM = 8;
 
 enum Stream : uint32_t {

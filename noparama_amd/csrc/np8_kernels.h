@@ -257,6 +257,7 @@ struct AssignArgs {
     double *mu_best = nullptr, *sigma_best = nullptr;
     const int32_t *cnt = nullptr;
     const double *slot_sigma = nullptr;
+    int32_t naux = 0, pad_rt = 0;  // np8_assign_rt (np8_rt.hip): M at run time (D in dim)
 };
 
 // Wide-path tables (np8_wide.hip), maintained for the slots flagged in dirty.
@@ -668,6 +669,13 @@ hipError_t np8_launch_best_unsort(np8::Ctl *ctl, const int32_t *ids, int32_t *z_
 // A snapshot the folded max-likelihood check left pending (ctl->snap_pend): copy it now and clear the flag.
 hipError_t np8_launch_snapshot_flush(const np8::SnapArgs &A, np8::Ctl *ctl, hipStream_t s);
 hipError_t np8_launch_loglik(const np8::LoglikArgs &A, int D, hipStream_t s);
+// np8_rt.hip: the fp64 kernels with D and M at run time, for the (D, M) np8_supported() has no instance of (the
+// dispatchers above fall back to them): 8 < D <= kMaxD, reference prior
+hipError_t np8_launch_assign_rt(const np8::AssignArgs &A, int D, int M, hipStream_t s);
+hipError_t np8_launch_loglik_rt(const np8::LoglikArgs &A, int D, hipStream_t s);
+hipError_t np8_launch_loglik_matrix_rt(const np8::AssignArgs &A, int D, int M, const int64_t *idx, int64_t n,
+                                       double *out, hipStream_t s);
+bool np8_rt_supported(int D, int M, int prior);
 hipError_t np8_launch_loglik_reduce(const double *partial, int64_t nb, double *out, double *out2, hipStream_t s);
 hipError_t np8_launch_snapshot(const np8::SnapArgs &A, hipStream_t s);
 hipError_t np8_launch_suffstats(const np8::ParamArgs &A, hipStream_t s);

@@ -2831,7 +2831,12 @@ hipError_t np8_launch_assign(const AssignArgs &A, int D, int M, int prior, hipSt
     }
     NP8_FOR_EACH_DM(X)
 #undef X
+    if (prior == kPriorReference && np8_rt_supported(D, M, prior)) return np8_launch_assign_rt(A, D, M, s);
     return hipErrorInvalidValue;
+}
+
+bool np8_rt_supported(int D, int M, int prior) {
+    return prior == kPriorReference && D > kPreMaxD && D <= kMaxD && M >= 1 && M <= kMaxM && !np8_supported(D, M);
 }
 
 // ---- pruning radii: the step's wave records into this sweep's buffer (DESIGN.md "Candidate pruning") ----
@@ -3039,6 +3044,7 @@ hipError_t np8_launch_loglik_matrix(const AssignArgs &A, int D, int M, int prior
     }
     NP8_FOR_EACH_DM(X)
 #undef X
+    if (np8_rt_supported(D, M, prior)) return np8_launch_loglik_matrix_rt(A, D, M, idx, n, out, s);
     return hipErrorInvalidValue;
 }
 
@@ -3141,7 +3147,7 @@ hipError_t np8_launch_loglik(const LoglikArgs &A, int D, hipStream_t s) {
         Y(1) Y(2) Y(3) Y(4) Y(5) Y(6) Y(7) Y(8) Y(9) Y(10) Y(11) Y(12) Y(13) Y(14) Y(15) Y(16)
 #undef Y
         default:
-            return hipErrorInvalidValue;
+            return np8_launch_loglik_rt(A, D, s);
     }
     return hipGetLastError();
 }

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define NP8O_DMAX 80
+#define NP8O_DMAX 128
 #define NP8O_MMAX 8
 #define NP8O_KCAP_PICK 4096 /* kcap limit of NP8O_PICK_INVCDF (the weights of one update live on the stack) */
 #define NP8O_REQMAX 4096 /* upper bound of req_max (must match NP8_REQ_MAX) */

@@ -16,7 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB = os.path.join(_HERE, "_build", "libnp8oracle.so")
 _REF = os.path.join(_HERE, "_ref", "libnp8ref.so")
 
-NP8O_DMAX = 80
+NP8O_DMAX = 128
 
 
 class _Config(C.Structure):

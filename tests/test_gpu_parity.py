@@ -165,10 +165,13 @@ def test_errors_are_reported():
         g.set_state(np.array([0, 0, 0, 5], np.int32), np.zeros((1, 2)), np.eye(2)[None])
     with pytest.raises(NP8Error):
         g.set_state(np.zeros(4, np.int32), np.zeros((1, 2)), np.zeros((1, 2, 2)))  # det = 0
+    NealAlgorithm8(17, seed=0, device=0).close()  # fp64 above D = 16: the run-time-D kernels (np8_rt.hip)
     with pytest.raises(NP8Error):
-        NealAlgorithm8(17, seed=0, device=0)  # the fp64 path covers D <= 16 (D 32 / 64: the wide path)
+        NealAlgorithm8(129, seed=0, device=0)  # at most kMaxD = 128
+    with pytest.raises(NP8Error):  # the run-time-D path: reference prior, frozen parameters
+        NealAlgorithm8(17, seed=0, device=0, prior="niw", nu=20.0)
     with pytest.raises(NP8Error):
-        NealAlgorithm8(5, M=2, seed=0, device=0)  # D outside {1, 2, 3, 4, 8, 16} runs M = 3 (the reference's)
+        NealAlgorithm8(5, M=2, seed=0, device=0)  # D <= 8 outside {1, 2, 3, 4, 8} runs M = 3 (the reference's)
 
 
 def test_partial_accept_at_kcap_matches_oracle():

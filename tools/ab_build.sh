@@ -13,5 +13,5 @@ mkdir -p "$OUT"
 FLAGS="--offload-arch=gfx950 -O3 -ffp-contract=off -std=c++17 -fPIC -Wall"
 /opt/rocm/bin/hipcc $FLAGS "$@" -c "$SRC/np8_kernels.hip" -o "$OUT/np8_kernels.o"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o "$OUT/libnp8.so" "$OUT/np8_kernels.o" "$LIB/np8_niw.o" \
-    "$LIB/np8_wide.o" "$LIB/np8_sm.o" "$LIB/np8_capi.o" -lrccl
+    "$LIB/np8_wide.o" "$LIB/np8_sm.o" "$LIB/np8_rt.o" "$LIB/np8_capi.o" -lrccl
 echo "$OUT/libnp8.so"
