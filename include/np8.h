@@ -95,9 +95,11 @@ typedef struct {
  * before the call or move to NP8_STATS; INTEGRATION.md "ABI growth" says the same. */
 #define NP8_CONFIG_MIN_BYTES offsetof(np8_config, param_update) /* D .. device: the first released layout */
 
-/* Cluster-likelihood arithmetic (DESIGN.md "Wide path").
- * F64:      fp64 table form (packed sym(Sigma^{-1})), any D from 1 to 16 with M = 3 (the reference's), and
- *           M in {1, 2, 3, 4} for D in {1, 2, 3, 4, 8, 16}.
+/* Cluster-likelihood arithmetic (DESIGN.md "Wide path", "Run-time D").
+ * F64:      fp64 table form (packed sym(Sigma^{-1})), the reference's arithmetic: any D from 1 to 16 with M = 3 (the
+ *           reference's), and M in {1, 2, 3, 4} for D in {1, 2, 3, 4, 8, 16} (templated kernels); any D from 9 to
+ *           128 with any M <= 8 otherwise (np8_rt.hip: D and M at run time; reference prior, param_update FROZEN;
+ *           bit-exact against oracle/'s F64 path, tests/test_gpu_rt.py).
  * F32_MFMA: 16 < D <= 80 (config C5: D = 64; tables padded with zero rows to D rounded up to 16; the NIW prior up to
  *           D = 64): items held in fp32, (x-mu)^T Sigma^{-1} (x-mu) = |A (x-mu)|^2 with
  *           A = fp32(chol(sym Sigma^{-1})) contracted on the matrix cores (v_mfma_f32_16x16x4_f32),

@@ -218,8 +218,9 @@ class NealAlgorithm8:
     `req_max`: new clusters one synchronous step may create (0: NP8_REQ_DEFAULT); requests beyond it
     or beyond the free slots are deferred to the item's next update (lowest scan positions first).
     `prior`: "reference" (the reference's G0 as it draws) or "niw" (a proper Normal-Inverse-Wishart with
-    kappa0 = kappa, nu0 = nu >= D + 1, Psi0 = Lambda).  `contraction`: "f64" (D <= 16) or "f32" (16 < D <= 80:
-    items in fp32, cluster likelihoods on the fp32 matrix cores; config C5).
+    kappa0 = kappa, nu0 = nu >= D + 1, Psi0 = Lambda).  `contraction`: "f64" (any D <= 128; above 16 the
+    run-time-D kernels of np8_rt.hip: reference prior, frozen parameters) or "f32" (16 < D <= 80: items in fp32,
+    cluster likelihoods on the fp32 matrix cores; config C5).
     `substeps`: the data-parallel sweep (chunk 0) as S synchronous sub-steps over a fixed hash partition of
     the items (DESIGN.md "Sub-steps"); 1 = one step against the sweep-start state; "auto" = 16 sub-steps for
     data sets of at most 8192 items (where one step over-splits), else one (resolved by set_data).
