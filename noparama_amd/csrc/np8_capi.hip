@@ -1865,7 +1865,9 @@ int np8_create_sized(np8_ctx **out, const np8_config *cfg_in, size_t cfg_bytes) 
     c->fuse_off = std::getenv("NP8_FUSE") == nullptr;  // opt-in: measured slower than separate launches
     c->queue_on = std::getenv("NP8_QUEUE") != nullptr;
     c->tailcond_off = std::getenv("NP8_LISTS_ALWAYS") != nullptr;
-    c->walk_screen = !(std::getenv("NP8_WALK_SCREEN") && std::getenv("NP8_WALK_SCREEN")[0] == '0');
+    // the walk screen (np8_assign_fast): opt-in since the buffered pick of round 6 (mixed 137.6 vs 145.0 us per sweep
+    // without it, profiles/r06/mixed_env_ab)
+    c->walk_screen = std::getenv("NP8_WALK_SCREEN") && std::getenv("NP8_WALK_SCREEN")[0] == '1';
     if (const char *g = std::getenv("NP8_MAX_LIST_GROUPS")) c->max_groups = std::max(1, std::min(64, std::atoi(g)));
     c->sort_in_graph = std::getenv("NP8_SORT_IN_GRAPH") != nullptr;
     if (!c->sort_in_graph) {  // host-mapped mirror of ctl->moved (written by every finalize)

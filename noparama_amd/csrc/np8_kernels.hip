@@ -1033,6 +1033,79 @@ __global__ __launch_bounds__(NP8_ASSIGN_BLOCK) __attribute__((amdgpu_waves_per_e
             __syncthreads();
 #endif
             const int nb = min(nact, n - qb);
+#if NP8_WALK_LDS && !defined(NP8_EXP_INLINE_PICK)
+            // Two passes over the round's rows.  Pass 1 (every row): the quadratic form, and the rows the lane's
+            // pick_step would not skip -- lw - T > -kSkip with T the running maximum, which only such rows raise --
+            // appended to a per-lane buffer (ll, row index in the round).  Pass 2 (flush: a full buffer, the round's
+            // end): pick_step over each lane's buffered rows in order.  The same steps on the same values as one
+            // pass, but the wave runs the pick's exp and division for max-over-lanes of the buffered rows instead of
+            // for every row that some lane needs (the mixed regime: ~19 listed rows per wave, ~1.35 picked per item).
+            constexpr int kBuf = 4;
+            double bl[kBuf];
+            int bk[kBuf];
+            int nbuf = 0;
+            double Tc = st.T;  // the running maximum pick_step will have reached at this row
+            auto flush = [&]() {
+#pragma unroll
+                for (int e = 0; e < kBuf; ++e) {
+                    if (__ballot(e < nbuf) == 0ull) break;  // (wave-uniform)
+                    if (e < nbuf) {
+                        const double llj = bl[e];
+                        const int kk = bk[e];
+                        const double lw = llj + s_row[D + 2][kk];
+                        const int j = s_j[kk];
+                        ensure_u(st, lw, A.seed, ig, t);
+                        pick_step(st, lw, j);
+                        pslot = (st.pick == j) ? (int32_t)s_row[D + 3][kk] : pslot;
+                        if (LL) llp = (st.pick == j) ? llj : llp;
+                    }
+                }
+                nbuf = 0;
+            };
+            for (int k = 0; k < nb; ++k) {  // wave-uniform: the rows in order (ascending)
+                const double iso = s_row[D][k];
+                if (screen) {  // (wave-uniform)
+                    bool need = mine && !defer;
+                    if (need && iso > 0.0) {
+                        const double base = s_row[D + 1][k] + s_row[D + 2][k];
+                        const double dl = (gi >= 0) ? (double)s_dist[gi][k] : 0.0;
+                        const double gap = (gi >= 0) ? fmax(fmax(dl - d_own, fma(-dl, 1.0 + 0x1p-21, d_own)), 0.0) : 0.0;
+                        const double far = 0.5 * iso * gap * gap;
+                        const double U = base - far - Tc;
+                        need = !(U <= -kSkip - 2.0 - 1e-9 * (fabs(base) + fabs(Tc) + far));
+                    }
+                    if (__ballot(need) == 0ull) continue;
+                }
+                if (mine && !defer) {
+                    if (!(iso > 0.0)) {
+                        defer = true;
+                    } else {
+                        const double m0 = s_row[0][k];
+                        double s2 = (x[0] - m0) * (x[0] - m0);
+#pragma unroll
+                        for (int a = 1; a < D; ++a) {
+                            const double ma = s_row[a][k];
+                            s2 = fma(x[a] - ma, x[a] - ma, s2);
+                        }
+                        const double llj = fma(-0.5, s2 * iso, s_row[D + 1][k]);
+                        const double lw = llj + s_row[D + 2][k];
+                        const double sl = s_row[D + 3][k];
+                        if (!(own_skip && sl == zslot) && lw - Tc > -kSkip) {
+#pragma unroll
+                            for (int e = 0; e < kBuf; ++e)
+                                if (nbuf == e) {
+                                    bl[e] = llj;
+                                    bk[e] = k;
+                                }
+                            ++nbuf;
+                            Tc = fmax(Tc, lw);
+                        }
+                    }
+                }
+                if (__ballot(nbuf == kBuf)) flush();  // (wave-uniform)
+            }
+            flush();  // (the round's rows are still in LDS)
+#else
             for (int k = 0; k < nb; ++k) {  // wave-uniform: the rows in order (ascending)
                 const double iso = NP8_ROWF(fiso, D, k);
                 if (screen) {  // (wave-uniform)
@@ -1071,6 +1144,7 @@ __global__ __launch_bounds__(NP8_ASSIGN_BLOCK) __attribute__((amdgpu_waves_per_e
                     }
                 }
             }
+#endif
         }
     };
     if (A.use_lists && lists_ok && ngroups <= A.max_groups) {  // wave-uniform
