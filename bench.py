@@ -33,7 +33,7 @@ FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector (= FP64 matrix) peak, vendor spec 
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X FP32 matrix peak (MI355X_MICROARCH.md: 155 measured)
 HBM_PEAK_GBS = 8000.0
 # committed rocprofv3 PMC summaries of the assign kernels (HBM bytes per launch, tools/prof*.sh)
-C3_TRAFFIC = "traffic_r06_c3.json"
+C3_TRAFFIC = "traffic_r06_final_c3.json"
 C5_TRAFFIC = "traffic_r05g_c5.json"
 C5_CONJ_TRAFFIC = "traffic_r05g_c5conj.json"  # PMC pass of the niw_conjugate C5 sweep (its assign reads more candidate rows than the frozen one)
 MIXED_TRAFFIC = "traffic_r06_mixed.json"  # PMC pass of the mixed regime (tools/prof_mixed.sh, tools/summarize_profile.py)
