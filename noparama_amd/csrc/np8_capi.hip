@@ -175,6 +175,10 @@ struct np8_ctx {
     double *X = nullptr;
     int32_t *z = nullptr, *z_best = nullptr;
     double *slot_mu = nullptr, *slot_P = nullptr, *slot_c = nullptr, *slot_sigma = nullptr, *slot_iso = nullptr;
+    // [2][kcap] precision eigenvalue bounds lo | hi per slot (0: unknown -- the row is never left out of a list), for the
+    // candidate lists of rows that are not isotropic; Gp's (G0 draws: P = Gp / v^2)
+    double *slot_lam = nullptr;
+    double gp_lamlo = 0.0, gp_lamhi = 0.0;
     double gp_iso = 0.0;
     // every row np8_assign_fast can meet is isotropic (the uploaded live slots, and every G0 draw: gp_iso > 0), so
     // it defers no lane and np8_assign_queue is left out of the step (a restored checkpoint: unknown, false)
@@ -426,6 +430,59 @@ bool prepare_niw(np8_ctx *c) {
     return true;
 }
 
+// Bounds lo <= eig(S) <= hi of a symmetric n x n matrix S (row-major, overwritten): cyclic Jacobi rotations to an
+// off-diagonal mass below 1e-30 of the total, then the diagonal's range widened by 1e-9 of the largest magnitude (the
+// rotations' rounding is ~n eps of it).  For the candidate lists' bound (prune_row), which keeps 2 nats of margin.
+void sym_eig_bounds(std::vector<double> &S, int n, double &lo, double &hi) {
+    double tot = 0.0;
+    for (double v : S) tot += v * v;
+    for (int sweep = 0; sweep < 64; ++sweep) {
+        double off = 0.0;
+        for (int p = 0; p < n; ++p)
+            for (int q = p + 1; q < n; ++q) off += S[p * n + q] * S[p * n + q];
+        if (off <= 1e-30 * tot) break;
+        for (int p = 0; p < n; ++p)
+            for (int q = p + 1; q < n; ++q) {
+                const double apq = S[p * n + q];
+                if (apq == 0.0) continue;
+                const double th = (S[q * n + q] - S[p * n + p]) / (2.0 * apq);
+                const double t = (th >= 0.0 ? 1.0 : -1.0) / (std::fabs(th) + std::sqrt(th * th + 1.0));
+                const double cs = 1.0 / std::sqrt(t * t + 1.0), sn = t * cs;
+                for (int k = 0; k < n; ++k) {  // columns p, q
+                    const double skp = S[k * n + p], skq = S[k * n + q];
+                    S[k * n + p] = cs * skp - sn * skq;
+                    S[k * n + q] = sn * skp + cs * skq;
+                }
+                for (int k = 0; k < n; ++k) {  // rows p, q
+                    const double spk = S[p * n + k], sqk = S[q * n + k];
+                    S[p * n + k] = cs * spk - sn * sqk;
+                    S[q * n + k] = sn * spk + cs * sqk;
+                }
+            }
+    }
+    lo = hi = S[0];
+    double mag = 0.0;
+    for (int a = 0; a < n; ++a) {
+        lo = std::min(lo, S[a * n + a]);
+        hi = std::max(hi, S[a * n + a]);
+        mag = std::max(mag, std::fabs(S[a * n + a]));
+    }
+    lo -= 1e-9 * mag;
+    hi += 1e-9 * mag;
+    if (!(lo > 0.0)) lo = 0.0;  // (no bound: never left out)
+}
+
+// the bounds of a packed precision (upper triangle, off-diagonals doubled)
+void packed_eig_bounds(const double *P, int D, double &lo, double &hi) {
+    std::vector<double> S((size_t)D * D);
+    for (int a = 0, q = 0; a < D; ++a)
+        for (int b = a; b < D; ++b, ++q) {
+            const double v = (a == b) ? P[q] : 0.5 * P[q];
+            S[(size_t)a * D + b] = S[(size_t)b * D + a] = v;
+        }
+    sym_eig_bounds(S, D, lo, hi);
+}
+
 // Base-measure precomputes: L = chol(Lambda) (invwishart.h:40), (L^T)^{-1}, (L^T L)^{-1}, L^T L.
 bool prepare_base(np8_ctx *c) {
     if (c->prior == NP8_PRIOR_NIW) return prepare_niw(c);
@@ -474,6 +531,16 @@ bool prepare_base(np8_ctx *c) {
     for (int a = 0; a < D; ++a)
         for (int b = 0; b < D; ++b) iso = iso && ((a == b) ? c->Gp[a * D + b] == c->Gp[0] : c->Gp[a * D + b] == 0.0);
     c->gp_iso = iso ? c->Gp[0] : 0.0;
+    {  // Gp's eigenvalue bounds (a G0 draw's precision is Gp / v^2)
+        std::vector<double> S((size_t)D * D);
+        for (int a = 0; a < D; ++a)
+            for (int b = a; b < D; ++b) {
+                const double v = (a == b) ? c->Gp[a * D + b] : 0.5 * c->Gp[a * D + b];
+                S[(size_t)a * D + b] = S[(size_t)b * D + a] = v;
+            }
+        sym_eig_bounds(S, D, c->gp_lamlo, c->gp_lamhi);
+        if (c->gp_lamlo <= 0.0) c->gp_lamhi = 0.0;
+    }
     return true;
 }
 
@@ -537,7 +604,7 @@ void free_device(np8_ctx *c) {
                     c->sm_typ, c->sm_slist, c->sm_stheta, c->stage, c->evalc, c->z_base, c->cnt_base,
                     c->chg_slot, c->mu_base, c->sigma_base, c->chg_item, c->chg_count, c->chg_flags,
                     c->inv_hist, c->inv_out, c->queue, c->qcount, c->qlist, c->slot_logn1, c->plen_s,
-                    c->plr2_s, c->sm_mb, c->lb, c->llpart, c->part, c->part_slot, c->crec, c->cgath};
+                    c->plr2_s, c->sm_mb, c->lb, c->llpart, c->part, c->part_slot, c->crec, c->cgath, c->slot_lam};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     c->crec = c->cgath = nullptr;
@@ -567,6 +634,7 @@ void free_device(np8_ctx *c) {
     }
     c->s_hist = c->s_cursor = c->s_off = nullptr;
     c->slot_iso = nullptr;
+    c->slot_lam = nullptr;
     c->lb = nullptr;
     c->llpart = nullptr;
     c->part = nullptr;
@@ -664,6 +732,18 @@ int upload_slots(np8_ctx *c, const std::vector<SlotHost> &slots, const std::vect
     c->rows_iso = c->gp_iso > 0.0;
     for (int s = 0; s < K; ++s) c->rows_iso = c->rows_iso && (cnt[s] == 0 || iso[s] > 0.0);
     HIPC(c, hipMemcpyAsync(c->slot_iso, iso.data(), sizeof(double) * iso.size(), hipMemcpyHostToDevice, c->stream));
+    if (c->slot_lam) {  // eigenvalue bounds of the live slots that are not isotropic (the candidate lists' bound)
+        std::vector<double> lam(2 * (size_t)c->kcap, 0.0);
+        for (int s = 0; s < K; ++s) {
+            if (iso[s] > 0.0) {
+                lam[s] = lam[c->kcap + s] = iso[s];
+            } else if (cnt[s] > 0) {
+                packed_eig_bounds(slots[s].P.data(), D, lam[s], lam[c->kcap + s]);
+                if (lam[s] <= 0.0) lam[c->kcap + s] = 0.0;
+            }
+        }
+        HIPC(c, hipMemcpyAsync(c->slot_lam, lam.data(), sizeof(double) * lam.size(), hipMemcpyHostToDevice, c->stream));
+    }
     std::vector<int32_t> cn(c->kcap, 0);
     for (int s = 0; s < K; ++s) cn[s] = cnt[s];
     HIPC(c, hipMemcpyAsync(c->slot_mu, mu.data(), sizeof(double) * mu.size(), hipMemcpyHostToDevice, c->stream));
@@ -769,6 +849,9 @@ FinArgs fin_args(np8_ctx *c, const unsigned char *recs, int world) {
     F.slot_iso = c->slot_iso;
     F.slot_logn1 = c->slot_logn1;
     F.gp_iso = c->gp_iso;
+    F.slot_lam = c->slot_lam;
+    F.gp_lamlo = c->gp_lamlo;
+    F.gp_lamhi = c->gp_lamhi;
     F.cand = c->cand;
     F.dense_of = c->dense_of;
     F.ctl = c->ctl;
@@ -1160,6 +1243,9 @@ PruneArgs prune_args(np8_ctx *c, bool last) {
     P.D = c->D;
     P.kcap = c->kcap;
     P.lb = c->lb;
+    // eigenvalue bounds for rows that are not isotropic: kept exact only while every slot's parameters come from an
+    // upload or a G0 draw (reference prior, frozen parameters)
+    P.lam = (c->prior == NP8_PRIOR_REFERENCE && c->param_update == NP8_PARAM_FROZEN) ? c->slot_lam : nullptr;
     P.gathered = (last && c->gather) ? 1 : 0;
     // the next sweep gathers: clear its buffer here instead of with a memset node at its start (a stale
     // buffer would only raise radii: pruning stays exact)
@@ -1906,6 +1992,7 @@ int np8_create_sized(np8_ctx **out, const np8_config *cfg_in, size_t cfg_bytes) 
         (r = dalloc(c, &c->mu_best, (size_t)kc * D)) || (r = dalloc(c, &c->sigma_best, (size_t)kc * D * D)) ||
         (r = dalloc(c, &c->cand, (size_t)kc * c->CS)) || (r = dalloc(c, &c->ctl, 1)) ||
         (r = dalloc(c, &c->dense_of, (size_t)kc)) || (r = dalloc(c, &c->slot_iso, (size_t)kc)) ||
+        (r = dalloc(c, &c->slot_lam, 2 * (size_t)kc)) ||
         (r = dalloc(c, &c->slot_logn1, (size_t)kc)) || (r = dalloc(c, &c->plen_s, (size_t)kc)) ||
         (r = dalloc(c, &c->plr2_s, (size_t)kc)) ||
         (r = dalloc(c, &c->rec, (size_t)c->rec_bytes)) || (r = dalloc(c, &c->evalc, (size_t)10 * kEvalSlots)) ||
@@ -2443,6 +2530,8 @@ int np8_restore(np8_ctx *c, const void *in, int64_t bytes) {
         p += q.bytes;
     }
     c->rows_iso = false;  // raw slot tables: isotropy unknown (np8_assign_queue stays in)
+    // eigenvalue bounds unknown for the restored slots (0: a row that is not isotropic stays in every list)
+    if (c->slot_lam) HIPC(c, hipMemsetAsync(c->slot_lam, 0, sizeof(double) * 2 * c->kcap, c->stream));
     c->snap_lazy = false;  // the snapshot buffers are the checkpoint's
     c->sorted_valid = false;
     c->use_sorted = false;

@@ -291,6 +291,9 @@ struct PruneArgs {
                         // then become the radii in use
     int32_t clear_next; // (not gathered) zero the gathered buffer for the next sweep, which gathers
     double *lb = nullptr;  // [2][kcap]: log n | log(n - 1) of each listed row's slot at the build (kListSlack test)
+    // [2][kcap] bounds lo <= eig(P) <= hi of each slot's precision (FinArgs::slot_lam), or null: a row that is not
+    // isotropic is then never left out of a list (and a non-isotropic own row lists every row)
+    const double *lam = nullptr;
 };
 
 struct FinArgs {
@@ -313,6 +316,10 @@ struct FinArgs {
     uint64_t seed;
     uint32_t t;  // epoch offset: epoch = ctl->t_base + t
     double *r2;  // pruning radii [2][kcap]: +inf for every slot created here (unknown radius)
+    // precision eigenvalue bounds [2][kcap] (lo | hi) of every slot, for the candidate lists of rows that are not
+    // isotropic (PruneArgs::lam); a slot created here gets those of Gp / v^2.  Null: not kept.
+    double *slot_lam = nullptr;
+    double gp_lamlo = 0.0, gp_lamhi = 0.0;
     // NIW prior: accepted requests are listed in pend[4 q] = (byte offset of the request's record
     // payload in recs, item, m, slot) for np8_niw_aux_slots instead of being written here
     int32_t prior, req_max;  // req_max: new clusters one step may create
@@ -413,6 +420,10 @@ __device__ __forceinline__ void write_new_slot(const FinArgs &F, const double *v
     for (int k = 0; k < D * D; ++k) F.slot_sigma[(int64_t)s * D * D + k] = v2 * F.LTL[k];
     F.slot_iso[s] = (F.gp_iso > 0.0) ? F.Gp[0] / v2 : 0.0;
     r2_unknown(F.r2, F.kcap, s);  // radius unknown until a sweep measures it
+    if (F.slot_lam) {  // P = Gp / v^2: its eigenvalues are Gp's over v^2 (the bounds carry a 1e-9 relative margin)
+        F.slot_lam[s] = F.gp_lamlo / v2;
+        F.slot_lam[F.kcap + s] = F.gp_lamhi / v2;
+    }
 }
 
 // Jain-Neal split-merge (np8_sm.hip, DESIGN.md "Split-merge").

@@ -1599,7 +1599,8 @@ constexpr int kPruneBlocks = 32;  // np8_prune grid: 128 rows per pass
 template <int DT = 0, typename R2of>
 __device__ void prune_row(const double *__restrict__ cand, R2of R2of_slot, int32_t *__restrict__ plist,
                           float *__restrict__ pdist, int32_t *__restrict__ plen, double *__restrict__ plr2, int32_t *__restrict__ plen_s,
-                          double *__restrict__ plr2_s, int ls, int Drt, int K, int k0, double *__restrict__ lb, int kcap) {
+                          double *__restrict__ plr2_s, int ls, int Drt, int K, int k0, double *__restrict__ lb, int kcap,
+                          const double *__restrict__ lam) {
     const int D = DT > 0 ? DT : Drt;
     const int DP = D * (D + 1) / 2, CS = cand_stride(D), F = D + DP;
     const int lane = threadIdx.x & 63;
@@ -1607,8 +1608,11 @@ __device__ void prune_row(const double *__restrict__ cand, R2of R2of_slot, int32
     const int slot0 = (int)NP8_CHK((int)e0[F + kFieldSlot], 0, kcap);
     const double R2 = R2of_slot(slot0);
     const double iso0 = e0[F + kFieldIso];
+    // (rows that are not isotropic, round 6: q_0(x) <= hi_0 |x - mu0|^2 and q_j(x) >= lo_j |x - mu_j|^2 with the slots'
+    // precision eigenvalue bounds -- the same bound with iso replaced; isotropic rows exactly as before)
+    const double hi0 = iso0 > 0.0 ? iso0 : (lam ? lam[kcap + slot0] : 0.0);
     const double base0 = e0[F + kFieldC] + e0[F + kFieldLogn1];
-    const bool prunable = iso0 > 0.0 && R2 < 1e300 && base0 > -1e299;
+    const bool prunable = hi0 > 0.0 && R2 < 1e300 && base0 > -1e299;
     const double R = sqrt(R2);
     int count = 0;
     for (int jb = 0; jb < K; jb += 64) {
@@ -1628,11 +1632,12 @@ __device__ void prune_row(const double *__restrict__ cand, R2of R2of_slot, int32
             }
             if (pdist) pdist[(int64_t)k0 * ls + j] = f32_down(sqrt(dist2));  // (every pair: the walk's screen)
             const double isoj = ej[F + kFieldIso];
-            if (keep && prunable && isoj > 0.0) {
+            const double loj = isoj > 0.0 ? isoj : (lam ? lam[(int)NP8_CHK((int)ej[F + kFieldSlot], 0, kcap)] : 0.0);
+            if (keep && prunable && loj > 0.0) {
                 const double delta = sqrt(dist2) - R;
                 if (delta > 0.0) {
                     const double wj = ej[F + kFieldC] + ej[F + kFieldLogn];
-                    const double far = 0.5 * isoj * delta * delta, near = 0.5 * iso0 * R2;
+                    const double far = 0.5 * loj * delta * delta, near = 0.5 * hi0 * R2;
                     const double U = (wj - base0) - far + near;
                     const double mag = fabs(wj) + fabs(base0) + far + near;
                     keep = !(U <= -kSkip - 2.0 - kListSlack - 1e-9 * mag);
@@ -2224,7 +2229,7 @@ __device__ void prune_block(const PruneArgs &A, unsigned char *smem, size_t lds_
     auto R2of = [&](int slot) { return src[slot]; };
     if ((size_t)K * RW * sizeof(double) > lds_bytes) {
         for (int k0 = wid; k0 < K; k0 += nwb)  // wave-uniform
-            prune_row<D>(A.cand, R2of, A.plist, A.pdist, A.plen, A.plr2, A.plen_s, A.plr2_s, A.ls, A.D, K, k0, A.lb, A.kcap);
+            prune_row<D>(A.cand, R2of, A.plist, A.pdist, A.plen, A.plr2, A.plen_s, A.plr2_s, A.ls, A.D, K, k0, A.lb, A.kcap, A.lam);
     } else {
         double *st = reinterpret_cast<double *>(smem);
         for (int idx = tid; idx < K * RW; idx += kFinThreads) {
@@ -2420,7 +2425,7 @@ __global__ __launch_bounds__(kFinThreads) void np8_fin_prune(FinArgs F, PruneArg
         constexpr int kWaves = kFinThreads / 64;
         for (int k0 = ((int)blockIdx.x - 1) * kWaves + __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6); k0 < K;
              k0 += nP * kWaves)  // wave-uniform (readfirstlane: SGPR loop)
-            prune_row<DT>(P.cand, R2of, P.plist, P.pdist, P.plen, P.plr2, P.plen_s, P.plr2_s, P.ls, P.D, K, k0, P.lb, P.kcap);
+            prune_row<DT>(P.cand, R2of, P.plist, P.pdist, P.plen, P.plr2, P.plen_s, P.plr2_s, P.ls, P.D, K, k0, P.lb, P.kcap, P.lam);
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -3280,7 +3285,7 @@ __global__ __launch_bounds__(256) void np8_prune(PruneArgs A) {
         for (int s = threadIdx.x; s < A.kcap; s += blockDim.x) A.r2[A.kcap + s] = 0.0;
     auto R2of = [&](int slot) { return src[slot]; };
     for (int k0 = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6); k0 < K; k0 += gridDim.x * 4)  // wave-uniform
-        prune_row<DT>(A.cand, R2of, A.plist, A.pdist, A.plen, A.plr2, A.plen_s, A.plr2_s, A.ls, A.D, K, k0, A.lb, A.kcap);
+        prune_row<DT>(A.cand, R2of, A.plist, A.pdist, A.plen, A.plr2, A.plen_s, A.plr2_s, A.ls, A.D, K, k0, A.lb, A.kcap, A.lam);
 }
 
 __global__ void np8_advance_epoch(Ctl *ctl, uint32_t n) {

@@ -109,3 +109,28 @@ def test_fp64_rt_max_likelihood_check():
     np.testing.assert_allclose(g.stats()["best_loglik"], o.best_loglik(), rtol=1e-11)
     bg, bo = g.state(which=1), o.state(which=1)
     assert np.array_equal(bg["z"], bo["z"])
+
+
+@pytest.mark.parametrize("D", [8, 12, 24])
+def test_non_isotropic_rows_pruned_bit_exact(D):
+    """Rows that are not isotropic (full covariances; a non-isotropic Lambda, so every G0 draw too) are left out of
+    the candidate lists by the slots' precision eigenvalue bounds (prune_row, round 6) -- on the templated path's
+    general kernel (D = 8, 12) and on the run-time-D one (D = 24): labels, counts and K bit-exact against the oracle,
+    which walks every row."""
+    N = 12000
+    X, z, mu, _ = datasets.mixture(N, D, 8, 0.6, 8.0, seed=100 + D)
+    sig = spd(D, 8, 7 + D)
+    rng = np.random.default_rng(5)
+    B = rng.normal(size=(D, D)) / D
+    g, o = pair(D, 800 + D, Lambda=0.01 * (np.eye(D) + B @ B.T))
+    for c in (g, o):
+        c.set_data(X)
+        c.set_state(z, mu, sig)
+    g.sweep(12)
+    o.sweep(12)
+    same_state(g, o)
+    for c in (g, o):
+        c.init_random(20)
+    g.sweep(12)
+    o.sweep(12)
+    same_state(g, o)
