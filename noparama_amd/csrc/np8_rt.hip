@@ -46,7 +46,18 @@ __device__ __forceinline__ double cand_ll_rt(const double *__restrict__ e, int D
         for (int a = 0; a < D; ++a) {
             const double da = xa(a) - e[a];
             double t = P[k++] * da;
-            for (int b = a + 1; b < D; ++b) t = fma(P[k++], xa(b) - e[b], t);
+            int b = a + 1;
+            for (; b + 8 <= D; b += 8, k += 8) {  // eight terms' operands loaded together, then their fmas in order
+                double pv[8], dv[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    pv[u] = P[k + u];
+                    dv[u] = xa(b + u) - e[b + u];
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u) t = fma(pv[u], dv[u], t);
+            }
+            for (; b < D; ++b) t = fma(P[k++], xa(b) - e[b], t);
             q = fma(t, da, q);
         }
     }
