@@ -34,9 +34,9 @@ FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X FP32 matrix peak (MI355X_MICROARCH.md: 1
 HBM_PEAK_GBS = 8000.0
 # committed rocprofv3 PMC summaries of the assign kernels (HBM bytes per launch, tools/prof*.sh)
 C3_TRAFFIC = "traffic_r06_final_c3.json"
-C5_TRAFFIC = "traffic_r05g_c5.json"
-C5_CONJ_TRAFFIC = "traffic_r05g_c5conj.json"  # PMC pass of the niw_conjugate C5 sweep (its assign reads more candidate rows than the frozen one)
-MIXED_TRAFFIC = "traffic_r06_mixed.json"  # PMC pass of the mixed regime (tools/prof_mixed.sh, tools/summarize_profile.py)
+C5_TRAFFIC = "traffic_r06_final_c5.json"
+C5_CONJ_TRAFFIC = "traffic_r06_final_c5conj.json"  # PMC pass of the niw_conjugate C5 sweep (its assign reads more candidate rows than the frozen one)
+MIXED_TRAFFIC = "traffic_r06_final_mixed.json"  # PMC pass of the mixed regime (tools/prof_mixed.sh, tools/summarize_profile.py)
 
 
 def binding_roof(exec_flops, abytes, ms, peak_tflops, kname):
