@@ -354,6 +354,17 @@ struct FinArgs {
     int32_t *mirror = nullptr;          // host-mapped [kMirrorInts]: halt as it happens, req_peak with peak_out
 };
 
+// A field of a kernel's argument struct (the kernel's only explicit argument: offset 0 of the kernarg segment) read
+// where it is used: a scalar load behind an empty asm barrier on the segment pointer, so that the compiler neither loads
+// it in the entry block nor holds it (spilled to VGPR lanes: a v_writelane / v_readlane pair each) across the kernel.
+template <class T>
+__device__ __forceinline__ T np8_late_arg(size_t off) {
+    typedef const __attribute__((address_space(4))) char *KP;
+    KP kp = (KP)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(kp));
+    return *(const __attribute__((address_space(4))) T *)(kp + off);
+}
+
 // Wave-aggregated atomics on a few hot addresses (count deltas, gathered radii): one atomic per distinct key
 // among the wave's `on` lanes instead of one per lane.  Same-address device-scope atomics serialise at the
 // memory side across the XCDs; in the regime the reference's start reaches (duplicate clusters, ~30% of the

@@ -790,14 +790,7 @@ __device__ __forceinline__ Fx fx_readlane(Fx a, int l) {
 #ifdef NP8_EXP_EARLY_ARGS  // (A/B: the compiler's own placement)
 #define NP8_LATE(f) (A.f)
 #else
-template <class T>
-__device__ __forceinline__ T late_arg(size_t off) {
-    typedef const __attribute__((address_space(4))) char *KP;
-    KP kp = (KP)__builtin_amdgcn_kernarg_segment_ptr();
-    asm volatile("" : "+s"(kp));
-    return *(const __attribute__((address_space(4))) T *)(kp + off);
-}
-#define NP8_LATE(f) late_arg<decltype(AssignArgs::f)>(offsetof(AssignArgs, f))
+#define NP8_LATE(f) np8_late_arg<decltype(AssignArgs::f)>(offsetof(AssignArgs, f))
 #endif
 
 template <int D, int M, int PRIOR, bool COUNT, bool LL>

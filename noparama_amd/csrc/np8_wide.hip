@@ -457,6 +457,12 @@ __global__ __launch_bounds__(256) void np8_wide_dist(WideArgs W) {
 // of its items' log-likelihoods under their new labels in llpart (a requester under its old slot: np8_ll_fix_wide moves
 // the accepted ones once their slots exist) -- np8_loglik_wide_mfma's values, the own and walked rows' q being the
 // same contractions.
+// (the assign's late-used arguments: np8_late_arg, as np8_assign_fast's NP8_LATE)
+#ifdef NP8_EXP_EARLY_ARGS
+#define NP8_WLATE(f) (A.f)
+#else
+#define NP8_WLATE(f) np8_late_arg<decltype(AssignArgs::f)>(offsetof(AssignArgs, f))
+#endif
 template <int DT, int M, int PRIOR, bool LL, bool EXACT>
 #ifndef NP8_WIDE_WAVES
 #define NP8_WIDE_WAVES 2
@@ -802,10 +808,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NP8_WIDE_WA
         buf ^= 1;
         ++rows_done;
     }
-    if (A.count_eval && wave_live) {  // item-row contractions this wave executed (own passes + evaluated rows)
+    if (NP8_WLATE(count_eval) && wave_live) {  // item-row contractions this wave executed (own passes + evaluated rows)
         const unsigned long long items = (unsigned long long)__popcll(__ballot(valid));
         if (lane == 0) {
-            unsigned long long *ec = A.evalc + 2 * ((blockIdx.x * 4 + (threadIdx.x >> 6)) % kEvalSlots);
+            unsigned long long *ec = NP8_WLATE(evalc) + 2 * ((blockIdx.x * 4 + (threadIdx.x >> 6)) % kEvalSlots);
             atomicAdd(ec, items * (unsigned long long)(rows_done + own_passes));
 #ifdef NP8_EXP_WIDE_ROWS  // experiment: per wave, the rows the triangle mask kept and the rows the exact screen kept
             if (prune) {
@@ -822,29 +828,29 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NP8_WIDE_WA
         if (valid) v = fx_of(st.pick >= K ? ll_own : llp);
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) v = fx_add(v, wfx_shfl_xor(v, o));
-        if (wave_live && lane == 0) A.llpart[(pw - A.p0) >> 6] = v;
+        if (wave_live && lane == 0) NP8_WLATE(llpart)[(pw - NP8_WLATE(p0)) >> 6] = v;
     }
     if (!valid) return;
 
-    int32_t *delta = reinterpret_cast<int32_t *>(A.rec + kRecHeaderBytes);
+    int32_t *delta = reinterpret_cast<int32_t *>(NP8_WLATE(rec) + kRecHeaderBytes);
     const int32_t snew = (st.pick < K) ? (int32_t)cand[(int64_t)st.pick * CS + F + kFieldSlot] : -1;
     const uint64_t mv = __ballot(snew != zi);
     if (mv && lane == (__ffsll((unsigned long long)__ballot(1)) - 1))
-        atomicAdd(reinterpret_cast<unsigned long long *>(&A.ctl->moved), (unsigned long long)__popcll(mv));
+        atomicAdd(reinterpret_cast<unsigned long long *>(&NP8_WLATE(ctl)->moved), (unsigned long long)__popcll(mv));
     const bool mover = st.pick < K && snew != zi;
     wave_add_by_key(delta, zi, -1, mover);
     wave_add_by_key(delta, snew, 1, mover);
-    const int qreq = wave_append(A.nreq, st.pick >= K);  // (requests are accepted by scan position, not arrival)
+    const int qreq = wave_append(NP8_WLATE(nreq), st.pick >= K);  // (requests are accepted by scan position, not arrival)
     if (st.pick < K) {
         if (snew != zi) {
-            A.z[il] = snew;
+            NP8_WLATE(z)[il] = snew;
             if (sorted) zs[pc] = snew;
         }
     } else {
         const int q = qreq;
-        if (q < A.req_cap) {  // always: the area holds every item of the step
+        if (q < NP8_WLATE(req_cap)) {  // always: the area holds every item of the step
             Request r;
-            r.pos = sorted ? (int64_t)ig : A.offset + p;
+            r.pos = sorted ? (int64_t)ig : NP8_WLATE(offset) + p;
             r.i = (int64_t)ig;
             r.m = st.pick - K;
             r.zold = zi;
@@ -852,12 +858,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NP8_WIDE_WA
             r.pad = 0;
             r.dll.lo = 0ull;
             r.dll.hi = 0;
-            A.req[q] = r;
-            double *vmu = A.vmu + (int64_t)q * (D + 1);
+            NP8_WLATE(req)[q] = r;
+            double *vmu = NP8_WLATE(vmu) + (int64_t)q * (D + 1);
             wide_frame_payload(hyp, D, X, n, xr, vmu);
-            if (q < A.ccap) {  // compact exchange (np8_step_local_compact): the first ccap requests in the compact record
-                A.creq[q] = r;
-                for (int a = 0; a <= D; ++a) A.cvmu[(int64_t)q * (D + 1) + a] = vmu[a];
+            if (q < NP8_WLATE(ccap)) {  // compact exchange (np8_step_local_compact): the first ccap requests in the compact record
+                NP8_WLATE(creq)[q] = r;
+                for (int a = 0; a <= D; ++a) NP8_WLATE(cvmu)[(int64_t)q * (D + 1) + a] = vmu[a];
             }
         }
     }
