@@ -375,8 +375,9 @@ int np8_step_merge(np8_ctx *ctx, const void *records, int32_t world);
  * rank sees alike in the gathered headers -- applies nothing and sets *halted = 1.  After a halt every rank calls
  * np8_step_resume (this rank's full record of the same step, np8_record_bytes() bytes), the caller all-gathers those
  * and calls np8_step_merge as after np8_step_local.  The chain is the full records' chain bit for bit.
- * np8_compact_record_bytes() is 0 where the step cannot use them (the wide path, the NIW prior, rows that are not
- * isotropic, NP8_COMPACT_REQ=0, or a context without the host transport): use np8_step_local there.
+ * np8_compact_record_bytes() is 0 where the step cannot use them (on the fp64 path: the NIW prior, rows that are not
+ * isotropic, D and M without a templated instance; NP8_COMPACT_REQ=0, or a context without the host transport): use
+ * np8_step_local there.  The wide path (NP8_CONTRACT_F32_MFMA, any prior and parameter update) has them.
  * Replaces, for the sharded sweep, the per-point exchange-free loop of np_mcmc.cpp:146-164. */
 int64_t np8_compact_record_bytes(np8_ctx *ctx);
 int np8_step_local_compact(np8_ctx *ctx, void *record_out);
