@@ -421,20 +421,37 @@ __device__ __forceinline__ void r2_unknown(double *r2, int kcap, int s) {
     r2[kcap + s] = __longlong_as_double(0x7FF0000000000000ll);
 }
 
-__device__ __forceinline__ void write_new_slot(const FinArgs &F, const double *vmu, int s) {
+// Slot s from an accepted request's (v, mu): element f of new_slot_elems(D) = D means, DP precision entries, D^2
+// covariance entries and the scalars -- one thread per element (np8_finalize spreads a step's new slots over its
+// workgroup: one thread writing all of a slot waited on ~100 dependent loads of Gp / LTL, 40k cycles a step), or all of
+// them in order (write_new_slot).
+__device__ __forceinline__ int new_slot_elems(int D) { return D + D * (D + 1) / 2 + D * D + 1; }
+
+__device__ __forceinline__ void write_new_slot_elem(const FinArgs &F, const double *vmu, int s, int f) {
     const int D = F.D, DP = D * (D + 1) / 2;
-    const double v = vmu[0];
-    for (int a = 0; a < D; ++a) F.slot_mu[(int64_t)s * D + a] = vmu[1 + a];
-    const double v2 = v * v;
-    for (int k = 0; k < DP; ++k) F.slot_P[(int64_t)s * DP + k] = F.Gp[k] / v2;
-    F.slot_c[s] = fma(-(double)D, log_pos(fabs(v)), F.caux);
-    for (int k = 0; k < D * D; ++k) F.slot_sigma[(int64_t)s * D * D + k] = v2 * F.LTL[k];
-    F.slot_iso[s] = (F.gp_iso > 0.0) ? F.Gp[0] / v2 : 0.0;
-    r2_unknown(F.r2, F.kcap, s);  // radius unknown until a sweep measures it
-    if (F.slot_lam) {  // P = Gp / v^2: its eigenvalues are Gp's over v^2 (the bounds carry a 1e-9 relative margin)
-        F.slot_lam[s] = F.gp_lamlo / v2;
-        F.slot_lam[F.kcap + s] = F.gp_lamhi / v2;
+    const double v = vmu[0], v2 = v * v;
+    if (f < D) {
+        F.slot_mu[(int64_t)s * D + f] = vmu[1 + f];
+    } else if (f < D + DP) {
+        const int k = f - D;
+        F.slot_P[(int64_t)s * DP + k] = F.Gp[k] / v2;
+    } else if (f < D + DP + D * D) {
+        const int k = f - D - DP;
+        F.slot_sigma[(int64_t)s * D * D + k] = v2 * F.LTL[k];
+    } else {
+        F.slot_c[s] = fma(-(double)D, log_pos(fabs(v)), F.caux);
+        F.slot_iso[s] = (F.gp_iso > 0.0) ? F.Gp[0] / v2 : 0.0;
+        r2_unknown(F.r2, F.kcap, s);  // radius unknown until a sweep measures it
+        if (F.slot_lam) {  // P = Gp / v^2: its eigenvalues are Gp's over v^2 (the bounds carry a 1e-9 relative margin)
+            F.slot_lam[s] = F.gp_lamlo / v2;
+            F.slot_lam[F.kcap + s] = F.gp_lamhi / v2;
+        }
     }
+}
+
+__device__ __forceinline__ void write_new_slot(const FinArgs &F, const double *vmu, int s) {
+    const int ne = new_slot_elems(F.D);
+    for (int f = 0; f < ne; ++f) write_new_slot_elem(F, vmu, s, f);
 }
 
 // Jain-Neal split-merge (np8_sm.hip, DESIGN.md "Split-merge").

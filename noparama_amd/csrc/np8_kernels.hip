@@ -1818,6 +1818,12 @@ __device__ int64_t request_pos(const FinArgs &F, const int *base, int q) { retur
 // with every requester still in its old slot; the A = min(req_max, free, requests) requests of lowest
 // scan position are accepted, in position order, into the lowest free slots in ascending order; each
 // accepted requester leaves its old slot; the others keep their cluster (deferred to their next update).
+#ifdef NP8_EXP_FIN_TIMING  // experiment: finalize_block phase clocks (thread 0), printed per call
+#define FIN_T(k) \
+    if (threadIdx.x == 0) ftm[k] = (long long)__builtin_amdgcn_s_memtime();
+#else
+#define FIN_T(k)
+#endif
 // (the body of np8_finalize, also run as the serial tail of np8_step_tail; smem: np8_finalize_lds_bytes)
 // Returns (block-uniform) whether the candidate lists of the last build may be stale after this step: a slot changed
 // liveness, requests were accepted, the rows were re-copied, or (slack_test) a live slot's log n or log(n - 1) moved
@@ -1833,6 +1839,10 @@ __device__ int finalize_block(const FinArgs &F, unsigned char *smem) {
     __shared__ int s_flags[4];  // nreq, gathered
     const int tid = threadIdx.x;
     const int kcap = F.kcap;
+#ifdef NP8_EXP_FIN_TIMING
+    long long ftm[12] = {0};
+#endif
+    FIN_T(0)
     const int D = F.D, DP = D * (D + 1) / 2, CS = cand_stride(D);
     const int per = (kcap + kFinThreads - 1) / kFinThreads;
     const int s0 = min(kcap, tid * per), s1 = min(kcap, s0 + per);
@@ -1902,6 +1912,7 @@ __device__ int finalize_block(const FinArgs &F, unsigned char *smem) {
             }
         }
     }
+    FIN_T(1)
 
     // The steady step (no request, no slot changing liveness, rows current): the dense table keeps its rows, so only
     // the slots whose count moved get their count and logs rewritten (rows from the prefetched dense_of) -- no scan,
@@ -1918,6 +1929,7 @@ __device__ int finalize_block(const FinArgs &F, unsigned char *smem) {
             lch |= (s < s1) && ((c > 0) != (cold[q] > 0));
         }
         const int any_lch = __syncthreads_or(lch);
+        FIN_T(2)
         if (!any_lch && nreq_all == 0 && cand_fresh && per <= kFinPre && !F.frame_payload) {  // block-uniform
             int viol = 0;
 #pragma unroll
@@ -2009,6 +2021,7 @@ __device__ int finalize_block(const FinArgs &F, unsigned char *smem) {
         cnt_s[s] = c;
     }
     __syncthreads();
+    FIN_T(3)
     const int nreq = s_flags[0];
     int nf = 0, nfree = 0, frank = 0;
     if (nreq > 0) {  // block-uniform: the free slots are only needed when there are requests
@@ -2016,6 +2029,7 @@ __device__ int finalize_block(const FinArgs &F, unsigned char *smem) {
         frank = block_excl_scan(nf, sh, &nfree);
     }
     const int A = min(min(nreq, F.req_max), nfree);  // accepted this step (block-uniform)
+    FIN_T(4)
     if (tid == 0) {
         F.ctl->n_new += A;
         F.ctl->n_rejected += s_flags[2] - A;  // (every rank's requests, also those its selection did not send)
@@ -2064,6 +2078,7 @@ __device__ int finalize_block(const FinArgs &F, unsigned char *smem) {
                 __syncthreads();
             }
         }
+        FIN_T(5)
         for (int q = tid; q < A; q += kFinThreads) {
             const Request r = *request_at(F, base, (int)NP8_CHK(kidx[q], 0, kReqMax * 64));
             const int s = (int)NP8_CHK(freeslot[q], 0, kcap);
@@ -2075,9 +2090,7 @@ __device__ int finalize_block(const FinArgs &F, unsigned char *smem) {
                 pe[1] = r.i;
                 pe[2] = r.m;
                 pe[3] = s;
-            } else {
-                write_new_slot(F, request_vmu(F, base, kidx[q]), s);
-            }
+            }  // (else: the slot's parameters below, spread over the workgroup)
             if (F.wdirty) F.wdirty[s] = 1;
             if (F.ll_on) llv = fx_add(llv, r.dll);  // (exact: any order)
             if (F.ll_defer) {  // (np8_ll_fix_wide: the requester's ll moves from its old slot to this one)
@@ -2092,9 +2105,17 @@ __device__ int finalize_block(const FinArgs &F, unsigned char *smem) {
                 if (F.zs[0] && r.lpos >= 0) F.zs[0][NP8_CHK(r.lpos, 0, F.n_loc)] = s;
             }
         }
+        if (!(F.prior == kPriorNiw || F.frame_payload)) {  // block-uniform; kidx / freeslot final since the sort
+            const int ne = new_slot_elems(D);
+            for (int e = tid; e < A * ne; e += kFinThreads) {
+                const int q = e / ne;
+                write_new_slot_elem(F, request_vmu(F, base, kidx[q]), freeslot[q], e - q * ne);
+            }
+        }
     }
     __syncthreads();
     // write counts back and rebuild the dense candidate table in ascending slot order
+    FIN_T(6)
     int nl = 0, lchange = 0;
 #pragma unroll
     for (int q = 0; q < kFinPre; ++q) {
@@ -2143,6 +2164,7 @@ __device__ int finalize_block(const FinArgs &F, unsigned char *smem) {
     for (int s = s0 + kFinPre; s < s1; ++s)
         write_slot(s, F.slot_c[s], F.slot_iso[s], F.slack_test ? F.lb[s] : 0.0, F.slack_test ? F.lb[kcap + s] : 0.0);
     const int stale = __syncthreads_or(viol) != 0 || copy_rows;
+    FIN_T(7)
     // mu and P' of every live row, all threads (not on the wide path: its kernels read the fp32 factor
     // rows of np8_wide_rows, and 4 MB of P' at D = 64 would keep this one workgroup busy for 0.3 ms)
     const int W = D + DP;
@@ -2150,6 +2172,7 @@ __device__ int finalize_block(const FinArgs &F, unsigned char *smem) {
         const int r = idx / W, f = idx - r * W, s = live_s[r];
         F.cand[(int64_t)r * CS + f] = (f < D) ? F.slot_mu[(int64_t)s * D + f] : F.slot_P[(int64_t)s * DP + (f - D)];
     }
+    FIN_T(8)
     if (tid == 0) {
         F.ctl->K = nlive;
         F.ctl->qwaves = 0;  // np8_assign_fast's deferred waves of this step are done
@@ -2197,6 +2220,14 @@ __device__ int finalize_block(const FinArgs &F, unsigned char *smem) {
         }
         if (F.advance) F.ctl->t_base += F.advance;  // nothing after this step reads t_base before the next replay
     }
+#ifdef NP8_EXP_FIN_TIMING
+    FIN_T(9)
+    if (tid == 0)
+        printf("fin nreq %d A %d nlive %d copy %d ph %lld %lld %lld %lld %lld %lld %lld %lld %lld\n", nreq, A, nlive,
+               (int)copy_rows, ftm[1] - ftm[0], ftm[2] - ftm[1], ftm[3] - ftm[2], ftm[4] - ftm[3],
+               ftm[5] ? ftm[5] - ftm[4] : 0ll, ftm[6] - (ftm[5] ? ftm[5] : ftm[4]), ftm[7] - ftm[6], ftm[8] - ftm[7],
+               ftm[9] - ftm[8]);
+#endif
     return stale;
 }
 

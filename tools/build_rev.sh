@@ -8,7 +8,7 @@ tmp=$(mktemp -d)
 git -C "$root" archive "$rev" noparama_amd/csrc include | tar -x -C "$tmp"
 cd "$tmp/noparama_amd/csrc"
 F="--offload-arch=gfx950 -O3 -ffp-contract=off -std=c++17 -fPIC -Wall $*"
-for f in np8_kernels np8_niw np8_wide np8_sm np8_capi; do /opt/rocm/bin/hipcc $F -c $f.hip -o $f.o & done
+for f in $(ls *.hip | sed "s/\.hip$//"); do /opt/rocm/bin/hipcc $F -c $f.hip -o $f.o & done
 wait
 mkdir -p "$root/noparama_amd/lib/exp"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o "$root/noparama_amd/lib/exp/$name.so" *.o -lrccl
