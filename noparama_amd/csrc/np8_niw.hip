@@ -23,6 +23,13 @@ using namespace np8;
 namespace {
 
 constexpr int kNiwThreads = 256;
+// np8_niw_post's workgroup: its MFMA tiles, trailing updates and record sums spread over blockDim.x / 64 waves, the
+// serial panels stay on waves 0-2.  512 (two waves per SIMD, 251 VGPRs): C5 niw_conjugate 1 706 -> 1 745 sweeps/s
+// against 256, A/B on one box (profiles/r06/ab_niw512); 1 024 would leave 128 registers per lane.
+#ifndef NP8_NIW_POST_THREADS
+#define NP8_NIW_POST_THREADS 512
+#endif
+constexpr int kNiwPostThreads = NP8_NIW_POST_THREADS;
 
 #ifdef NP8_EXP_NIW_TIMING  // experiment: phase cycle counts of np8_niw_post, block 0, printed
 #define NIW_T(k) \
@@ -770,7 +777,7 @@ size_t np8_niw_lds_bytes(int D) { return sizeof(double) * (4 * (size_t)D * (D + 
 // ---- posterior (and prior) draw -------------------------------------------------------------------
 // Block b: init mode (A.init_k > 0) draws G0 sample b into slot init_map[b] on stream INIT_THETA;
 // otherwise slot b's posterior on stream PARAM at the current epoch (oracle niw_draw_impl).
-__global__ __launch_bounds__(kNiwThreads) void np8_niw_post(NiwArgs A) {
+__global__ __launch_bounds__(kNiwPostThreads) void np8_niw_post(NiwArgs A) {
     const int D = A.D, W = D + D * (D + 1) / 2, LD = D + 1;
     const bool ex16 = D % 16 == 0;  // the MFMA tiles' instances without masking (lds_at)
     int s;
@@ -1232,7 +1239,7 @@ hipError_t np8_niw_prepare(int D) {
 hipError_t np8_launch_niw_post(const NiwArgs &A, int nblocks, hipStream_t s) {
     if (nblocks <= 0) return hipSuccess;
     const size_t lds = np8_niw_lds_bytes(A.D);
-    hipLaunchKernelGGL(np8_niw_post, dim3((unsigned)nblocks), dim3(kNiwThreads), lds, s, A);
+    hipLaunchKernelGGL(np8_niw_post, dim3((unsigned)nblocks), dim3(kNiwPostThreads), lds, s, A);
     return hipGetLastError();
 }
 
