@@ -941,7 +941,13 @@ __global__ __launch_bounds__(64) void np8_loglik_matrix_wide(AssignArgs A, WideA
 // of np8_assign_wide (one MFMA pass per distinct own slot of a wave; one on the label-sorted layout),
 // a fixed-order block reduction into partial[block] (reduced by np8_loglik_reduce).
 template <int DT>
-__global__ __launch_bounds__(256) void np8_loglik_wide_mfma(AssignArgs A, double *__restrict__ partial) {
+// Three waves per SIMD (159 VGPRs, no spills; 180 and two waves without the attribute, four spill): C5 niw_conjugate
+// 1 753-1 755 -> 1 759-1 765 sweeps/s, A/B on one box (profiles/r06/ab_llw3).
+#ifndef NP8_LLW_WAVES
+#define NP8_LLW_WAVES 3
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NP8_LLW_WAVES))) void np8_loglik_wide_mfma(
+    AssignArgs A, double *__restrict__ partial) {
     using W = Wide<DT>;
     const int CS = cand_stride(A.dim), F = A.dim + A.dim * (A.dim + 1) / 2;
     __shared__ double red[256];
